@@ -1,0 +1,717 @@
+// Python bindings for the native autoscaler runtime (`kube_sqs_autoscaler_amd.ops._ksa_native`).
+//
+// Python owns configuration and bootstrap (Go-compatible flag parsing, the AWS credential
+// chain, kubeconfig / in-cluster discovery); everything on the poll -> patch path runs here in
+// C++ with the GIL released. The injectable seams of the reference -- the `SQS` interface
+// (/root/reference/sqs/sqs.go:14-18) and typedappv1.DeploymentInterface
+// (/root/reference/scale/scale.go:22) -- are exposed as subclassable base classes
+// (SqsApi, DeploymentApi), so Python fakes plug into the native loop exactly like the
+// reference's Go mocks plug into Run().
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <unistd.h>
+
+#include "../core/clock.h"
+#include "../core/fakes.h"
+#include "../core/goutil.h"
+#include "../core/http.h"
+#include "../core/json.h"
+#include "../core/kube.h"
+#include "../core/log.h"
+#include "../core/runner.h"
+#include "../core/sigv4.h"
+#include "../core/sqs.h"
+#include "../core/xml.h"
+
+namespace py = pybind11;
+using namespace ksa;
+
+namespace {
+
+py::object g_native_error;  // kube_sqs_autoscaler_amd.ops._ksa_native.NativeError
+
+[[noreturn]] void raise_status(const Status& s) {
+  PyErr_SetString(g_native_error.ptr(), s.message().c_str());
+  throw py::error_already_set();
+}
+
+template <class T>
+T unwrap(Result<T> r) {
+  if (!r.ok()) raise_status(r.status);
+  return std::move(r.value);
+}
+
+std::string py_error_text(py::error_already_set& e) {
+  py::gil_scoped_acquire g;
+  std::string msg = py::str(e.value());
+  return msg;
+}
+
+// ---- trampolines ------------------------------------------------------------------------
+
+class PySqsApi : public SqsApi, public py::trampoline_self_life_support {
+ public:
+  Result<AttrMap> get_queue_attributes(const std::string& queue_url,
+                                       const std::vector<std::string>& names) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(static_cast<const SqsApi*>(this), "get_queue_attributes");
+    if (!f) return Result<AttrMap>::Err(Status::Err("SqsApi.get_queue_attributes not implemented"));
+    try {
+      py::object r = f(queue_url, names);
+      AttrMap out;
+      for (auto item : r.cast<py::dict>())
+        out[py::str(item.first)] = py::str(item.second);
+      return Result<AttrMap>::Ok(std::move(out));
+    } catch (py::error_already_set& e) {
+      return Result<AttrMap>::Err(Status::Err(py_error_text(e)));
+    }
+  }
+};
+
+class PyDeploymentApi : public DeploymentApi, public py::trampoline_self_life_support {
+ public:
+  Result<ScaleObject> get(const std::string& name) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(static_cast<const DeploymentApi*>(this), "get");
+    if (!f) return Result<ScaleObject>::Err(Status::Err("DeploymentApi.get not implemented"));
+    try {
+      return Result<ScaleObject>::Ok(f(name).cast<ScaleObject>());
+    } catch (py::error_already_set& e) {
+      return Result<ScaleObject>::Err(Status::Err(py_error_text(e)));
+    }
+  }
+  Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(static_cast<const DeploymentApi*>(this), "update");
+    if (!f) return Status::Err("DeploymentApi.update not implemented");
+    try {
+      f(name, fetched, replicas);
+      return Status::OK();
+    } catch (py::error_already_set& e) {
+      return Status::Err(py_error_text(e));
+    }
+  }
+};
+
+class PyCredentialsProvider : public CredentialsProvider, public py::trampoline_self_life_support {
+ public:
+  Result<Credentials> retrieve() override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(static_cast<const CredentialsProvider*>(this), "retrieve");
+    if (!f) return Result<Credentials>::Err(Status::Err("CredentialsProvider.retrieve not implemented"));
+    try {
+      return Result<Credentials>::Ok(f().cast<Credentials>());
+    } catch (py::error_already_set& e) {
+      return Result<Credentials>::Err(Status::Err(py_error_text(e)));
+    }
+  }
+};
+
+class PyTokenProvider : public TokenProvider, public py::trampoline_self_life_support {
+ public:
+  Result<std::string> token() override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(static_cast<const TokenProvider*>(this), "token");
+    if (!f) return Result<std::string>::Err(Status::Err("TokenProvider.token not implemented"));
+    try {
+      return Result<std::string>::Ok(f().cast<std::string>());
+    } catch (py::error_already_set& e) {
+      return Result<std::string>::Err(Status::Err(py_error_text(e)));
+    }
+  }
+};
+
+Level level_from(const std::string& s) {
+  Level l;
+  if (!parse_level(s, &l)) throw py::value_error("not a valid logrus Level: " + s);
+  return l;
+}
+
+py::dict record_dict(const IterationRecord& r) {
+  py::dict d;
+  d["index"] = r.index;
+  d["stopped"] = r.stopped;
+  d["t_poll"] = r.t_poll;
+  d["depth_ok"] = r.depth_ok;
+  d["depth"] = r.depth;
+  d["up"] = action_name(r.up);
+  d["down"] = action_name(r.down);
+  d["replicas_before"] = r.replicas_before;
+  d["replicas_after"] = r.replicas_after;
+  d["depth_ns"] = r.depth_ns;
+  d["get_ns"] = r.get_ns;
+  d["update_ns"] = r.update_ns;
+  d["total_ns"] = r.total_ns;
+  d["patch_latency_ns"] = r.patch_latency_ns;
+  d["error"] = r.error;
+  return d;
+}
+
+py::dict http_stats_dict(const HttpClientStats& s) {
+  py::dict d;
+  d["requests"] = s.requests;
+  d["connects"] = s.connects;
+  d["reconnect_retries"] = s.reconnect_retries;
+  d["bytes_out"] = s.bytes_out;
+  d["bytes_in"] = s.bytes_in;
+  return d;
+}
+
+Headers headers_from(const py::object& o) {
+  Headers h;
+  if (o.is_none()) return h;
+  if (py::isinstance<py::dict>(o)) {
+    for (auto item : o.cast<py::dict>()) h.emplace_back(py::str(item.first), py::str(item.second));
+    return h;
+  }
+  for (auto item : o) {
+    auto t = item.cast<py::tuple>();
+    h.emplace_back(t[0].cast<std::string>(), t[1].cast<std::string>());
+  }
+  return h;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_ksa_native, m) {
+  m.doc() = "Native runtime of the MI355X SQS autoscaler (control loop, SigV4, HTTP, fakes).";
+  g_native_error = py::reinterpret_borrow<py::object>(
+      PyErr_NewException("kube_sqs_autoscaler_amd.ops._ksa_native.NativeError", PyExc_RuntimeError, nullptr));
+  m.attr("NativeError") = g_native_error;
+
+  // ---- Go stdlib helpers ----
+  m.def("go_atoi", [](const std::string& s) { return unwrap(go_atoi(s)); });
+  m.def("go_quote", &go_quote);
+  m.def("rfc3339_utc", &rfc3339_utc);
+  m.def("amz_date", &amz_date);
+  m.def("go_int32", &go_int32);
+
+  // ---- JSON / XML ----
+  m.def("set_spec_replicas", [](const std::string& raw, int32_t r) { return unwrap(set_spec_replicas(raw, r)); });
+  m.def("json_roundtrip", [](const std::string& t) { return json_serialize(unwrap(json_parse(t))); });
+  m.def("xml_sqs_attributes", &xml_sqs_attributes);
+  m.def("xml_first_text", [](const std::string& doc, const std::string& tag) {
+    bool found = false;
+    std::string v = xml_first_text(doc, tag, &found);
+    return found ? py::object(py::str(v)) : py::object(py::none());
+  });
+
+  // ---- crypto / SigV4 ----
+  m.def("sha256_hex", [](py::bytes b) { return sha256_hex(std::string(b)); });
+  m.def("hmac_sha256_hex", [](py::bytes k, py::bytes d) { return hex_encode(hmac_sha256(std::string(k), std::string(d))); });
+  m.def("aws_uri_encode", &aws_uri_encode, py::arg("s"), py::arg("keep_slash") = false);
+
+  py::class_<Credentials>(m, "Credentials")
+      .def(py::init([](std::string akid, std::string secret, std::string token, int64_t exp, std::string name) {
+             Credentials c;
+             c.access_key_id = std::move(akid);
+             c.secret_access_key = std::move(secret);
+             c.session_token = std::move(token);
+             c.expires_unix_ns = exp;
+             c.provider_name = std::move(name);
+             return c;
+           }),
+           py::arg("access_key_id"), py::arg("secret_access_key"), py::arg("session_token") = "",
+           py::arg("expires_unix_ns") = 0, py::arg("provider_name") = "")
+      .def_readwrite("access_key_id", &Credentials::access_key_id)
+      .def_readwrite("secret_access_key", &Credentials::secret_access_key)
+      .def_readwrite("session_token", &Credentials::session_token)
+      .def_readwrite("expires_unix_ns", &Credentials::expires_unix_ns)
+      .def_readwrite("provider_name", &Credentials::provider_name)
+      .def("valid", &Credentials::valid)
+      .def("__repr__", [](const Credentials& c) {
+        return "Credentials(access_key_id=" + c.access_key_id + ", provider=" + c.provider_name + ")";
+      });
+
+  py::class_<CredentialsProvider, PyCredentialsProvider, py::smart_holder>(m, "CredentialsProvider")
+      .def(py::init<>())
+      .def("retrieve", [](CredentialsProvider& p) {
+        Result<Credentials> r;
+        {
+          py::gil_scoped_release rel;
+          r = p.retrieve();
+        }
+        return unwrap(r);
+      });
+  py::class_<StaticCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "StaticCredentialsProvider")
+      .def(py::init<Credentials>());
+
+  py::class_<SigV4Signer, std::shared_ptr<SigV4Signer>>(m, "SigV4Signer")
+      .def(py::init<std::string, std::string>(), py::arg("region"), py::arg("service"))
+      .def("sign",
+           [](SigV4Signer& s, const Credentials& c, int64_t unix_ns, const std::string& method,
+              const std::string& path, const std::string& query, py::object headers, py::bytes body) {
+             Headers h = headers_from(headers);
+             SignDebug dbg;
+             s.sign(c, unix_ns, method, path, query, &h, std::string(body), &dbg);
+             py::dict d;
+             d["canonical_request"] = dbg.canonical_request;
+             d["string_to_sign"] = dbg.string_to_sign;
+             d["signed_headers"] = dbg.signed_headers;
+             d["signature"] = dbg.signature;
+             d["scope"] = dbg.scope;
+             return py::make_tuple(h, d);
+           })
+      .def("signing_key_hex", [](SigV4Signer& s, const std::string& secret, const std::string& date) {
+        return hex_encode(s.signing_key(secret, date));
+      });
+  m.def("sigv4_verify",
+        [](const std::string& method, const std::string& path, const std::string& query, py::object headers,
+           py::bytes body, const std::string& akid, const std::string& secret, const std::string& region,
+           const std::string& service) {
+          Status s = sigv4_verify(method, path, query, headers_from(headers), std::string(body), akid, secret,
+                                  region, service);
+          if (!s.ok()) raise_status(s);
+        });
+
+  // ---- logging ----
+  py::class_<Logger, std::shared_ptr<Logger>>(m, "Logger")
+      .def(py::init<>())
+      .def_static("default", &Logger::default_logger)
+      .def("set_level", [](Logger& l, const std::string& s) { l.set_level(level_from(s)); })
+      .def("level", [](Logger& l) { return std::string(level_name(l.level())); })
+      .def("set_format", [](Logger& l, const std::string& f) {
+        if (f == "text") l.set_format(LogFormat::Text);
+        else if (f == "json") l.set_format(LogFormat::Json);
+        else throw py::value_error("log format must be text or json");
+      })
+      .def("set_sink",
+           [](Logger& l, py::object cb) {
+             if (cb.is_none()) {
+               l.set_sink([](const std::string& line) {
+                 std::string s = line + "\n";
+                 ssize_t r = ::write(2, s.data(), s.size());
+                 (void)r;
+               });
+               return;
+             }
+             auto holder = std::make_shared<py::object>(cb);
+             l.set_sink([holder](const std::string& line) {
+               py::gil_scoped_acquire g;
+               try {
+                 (*holder)(line);
+               } catch (py::error_already_set& e) {
+                 e.discard_as_unraisable(__func__);
+               }
+             });
+           })
+      .def("set_time_source",
+           [](Logger& l, std::shared_ptr<Clock> c) {
+             l.set_time_source([c] { return c->unix_nanos(); });
+           })
+      .def("set_base_fields", &Logger::set_base_fields)
+      .def("with_fields", &Logger::with_fields)
+      .def("log",
+           [](Logger& l, const std::string& level, const std::string& msg, const Fields& f) {
+             l.log(level_from(level), msg, f);
+           },
+           py::arg("level"), py::arg("msg"), py::arg("fields") = Fields{},
+           py::call_guard<py::gil_scoped_release>())
+      .def("format", [](Logger& l, const std::string& level, const std::string& msg, const Fields& f,
+                        int64_t ts) { return l.format(level_from(level), msg, f, ts); });
+  m.def("logrus_needs_quoting", &logrus_needs_quoting);
+
+  // ---- clocks ----
+  py::class_<Clock, std::shared_ptr<Clock>>(m, "Clock")
+      .def("now", &Clock::now)
+      .def("unix_nanos", &Clock::unix_nanos)
+      .def("sleep", [](Clock& c, Nanos d) { return c.sleep(d, nullptr); }, py::call_guard<py::gil_scoped_release>());
+  py::class_<RealClock, Clock, std::shared_ptr<RealClock>>(m, "RealClock").def(py::init<>());
+  py::class_<VirtualClock, Clock, std::shared_ptr<VirtualClock>>(m, "VirtualClock")
+      .def(py::init<Nanos, int64_t>(), py::arg("start") = 0, py::arg("unix_epoch_ns") = 1700000000LL * kSecond)
+      .def("advance", &VirtualClock::advance)
+      .def("set", &VirtualClock::set);
+
+  // ---- HTTP ----
+  py::class_<TlsOptions>(m, "TlsOptions")
+      .def(py::init<>())
+      .def_readwrite("insecure_skip_verify", &TlsOptions::insecure_skip_verify)
+      .def_readwrite("ca_file", &TlsOptions::ca_file)
+      .def_readwrite("ca_pem", &TlsOptions::ca_pem)
+      .def_readwrite("cert_pem", &TlsOptions::cert_pem)
+      .def_readwrite("key_pem", &TlsOptions::key_pem)
+      .def_readwrite("server_name", &TlsOptions::server_name);
+
+  py::class_<HttpClient, std::shared_ptr<HttpClient>>(m, "HttpClient")
+      .def(py::init([](const std::string& url, const TlsOptions& tls, Nanos timeout) {
+             return std::make_shared<HttpClient>(unwrap(parse_url(url)), tls, timeout);
+           }),
+           py::arg("origin"), py::arg("tls") = TlsOptions(), py::arg("timeout_ns") = 30 * kSecond)
+      .def("request",
+           [](HttpClient& c, const std::string& method, const std::string& target, py::object headers,
+              py::bytes body) {
+             HttpRequest req;
+             req.method = method;
+             req.target = target;
+             req.headers = headers_from(headers);
+             req.body = std::string(body);
+             HttpResponse resp;
+             Status s;
+             {
+               py::gil_scoped_release rel;
+               s = c.round_trip(req, &resp);
+             }
+             if (!s.ok()) raise_status(s);
+             return py::make_tuple(resp.status, resp.headers, py::bytes(resp.body));
+           },
+           py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""))
+      .def("close", &HttpClient::close)
+      .def("stats", [](HttpClient& c) { return http_stats_dict(c.stats()); });
+  m.def("parse_url", [](const std::string& s) {
+    Url u = unwrap(parse_url(s));
+    return py::make_tuple(u.scheme, u.host, u.port, u.path);
+  });
+  m.def("generate_self_signed", [](const std::string& host) {
+    std::string c, k;
+    Status s = generate_self_signed(host, &c, &k);
+    if (!s.ok()) raise_status(s);
+    return py::make_tuple(c, k);
+  });
+
+  // ---- SQS ----
+  m.def("default_attribute_names", &default_attribute_names);
+  py::enum_<SqsProtocol>(m, "SqsProtocol").value("Query", SqsProtocol::Query).value("Json", SqsProtocol::Json);
+  py::class_<SqsHttpOptions>(m, "SqsHttpOptions")
+      .def(py::init<>())
+      .def_readwrite("region", &SqsHttpOptions::region)
+      .def_readwrite("endpoint", &SqsHttpOptions::endpoint)
+      .def_readwrite("protocol", &SqsHttpOptions::protocol)
+      .def_readwrite("timeout_ns", &SqsHttpOptions::timeout)
+      .def_readwrite("max_retries", &SqsHttpOptions::max_retries)
+      .def_readwrite("min_retry_delay_ns", &SqsHttpOptions::min_retry_delay)
+      .def_readwrite("min_throttle_delay_ns", &SqsHttpOptions::min_throttle_delay)
+      .def_readwrite("max_retry_delay_ns", &SqsHttpOptions::max_retry_delay)
+      .def_readwrite("tls", &SqsHttpOptions::tls);
+
+  py::class_<SqsApi, PySqsApi, py::smart_holder>(m, "SqsApi")
+      .def(py::init<>())
+      .def("get_queue_attributes", [](SqsApi& a, const std::string& url, const std::vector<std::string>& names) {
+        Result<AttrMap> r;
+        {
+          py::gil_scoped_release rel;
+          r = a.get_queue_attributes(url, names);
+        }
+        return unwrap(r);
+      });
+  py::class_<HttpSqsApi, SqsApi, py::smart_holder>(m, "HttpSqsApi")
+      .def(py::init<SqsHttpOptions, std::shared_ptr<CredentialsProvider>, std::shared_ptr<Clock>>(),
+           py::arg("options"), py::arg("credentials"), py::arg("clock"))
+      .def_static("endpoint_for_region", &HttpSqsApi::endpoint_for_region)
+      .def("endpoint", &HttpSqsApi::endpoint)
+      .def("stats", [](HttpSqsApi& a) {
+        auto s = a.stats();
+        py::dict d;
+        d["calls"] = s.calls;
+        d["retries"] = s.retries;
+        d["errors"] = s.errors;
+        d["http"] = http_stats_dict(s.http);
+        return d;
+      });
+  py::class_<MockSqsApi, SqsApi, py::smart_holder>(m, "MockSqsApi")
+      .def(py::init<AttrMap>(), py::arg("attributes") = AttrMap{})
+      .def("set_attributes", &MockSqsApi::set_attributes)
+      .def("set_latency", &MockSqsApi::set_latency)
+      .def("fail_next", &MockSqsApi::fail_next)
+      .def("calls", &MockSqsApi::calls);
+  py::class_<TraceSqsApi, SqsApi, py::smart_holder>(m, "TraceSqsApi")
+      .def(py::init<std::shared_ptr<Clock>, std::vector<std::pair<Nanos, AttrMap>>, Nanos>(),
+           py::arg("clock"), py::arg("segments"), py::arg("per_call_latency_ns") = 0);
+  py::class_<SqsClient, std::shared_ptr<SqsClient>>(m, "SqsClient")
+      .def(py::init<std::shared_ptr<SqsApi>, std::string, std::vector<std::string>>(), py::arg("api"),
+           py::arg("queue_url"), py::arg("attribute_names"))
+      .def("num_messages", [](SqsClient& c) {
+        Result<int64_t> r;
+        {
+          py::gil_scoped_release rel;
+          r = c.num_messages();
+        }
+        return unwrap(r);
+      })
+      .def_property_readonly("queue_url", &SqsClient::queue_url)
+      .def_property_readonly("attribute_names", &SqsClient::attribute_names)
+      .def_property_readonly("api", &SqsClient::api);
+
+  // ---- Kubernetes ----
+  py::class_<ScaleObject>(m, "ScaleObject")
+      .def(py::init([](int32_t replicas, bool has_replicas, std::string rv, std::string raw) {
+             ScaleObject o;
+             o.replicas = replicas;
+             o.has_replicas = has_replicas;
+             o.resource_version = std::move(rv);
+             o.raw = std::move(raw);
+             return o;
+           }),
+           py::arg("replicas") = 0, py::arg("has_replicas") = true, py::arg("resource_version") = "",
+           py::arg("raw") = "")
+      .def_readwrite("replicas", &ScaleObject::replicas)
+      .def_readwrite("has_replicas", &ScaleObject::has_replicas)
+      .def_readwrite("resource_version", &ScaleObject::resource_version)
+      .def_readwrite("raw", &ScaleObject::raw);
+  m.def("parse_scale_object", [](const std::string& j, bool absent_is_zero) {
+    return unwrap(parse_scale_object(j, absent_is_zero));
+  });
+
+  py::class_<TokenProvider, PyTokenProvider, py::smart_holder>(m, "TokenProvider")
+      .def(py::init<>())
+      .def("token", [](TokenProvider& t) {
+        Result<std::string> r;
+        {
+          py::gil_scoped_release rel;
+          r = t.token();
+        }
+        return unwrap(r);
+      });
+  py::class_<StaticTokenProvider, TokenProvider, py::smart_holder>(m, "StaticTokenProvider")
+      .def(py::init<std::string>());
+  py::class_<FileTokenProvider, TokenProvider, py::smart_holder>(m, "FileTokenProvider")
+      .def(py::init<std::string, std::shared_ptr<Clock>, Nanos>(), py::arg("path"), py::arg("clock"),
+           py::arg("refresh_ns") = 60 * kSecond);
+
+  py::enum_<ScaleMode>(m, "ScaleMode")
+      .value("Deployment", ScaleMode::Deployment)
+      .value("Scale", ScaleMode::Scale)
+      .value("Patch", ScaleMode::Patch);
+  py::class_<KubeOptions>(m, "KubeOptions")
+      .def(py::init<>())
+      .def_readwrite("server", &KubeOptions::server)
+      .def_readwrite("namespace", &KubeOptions::namespace_)
+      .def_readwrite("mode", &KubeOptions::mode)
+      .def_readwrite("tls", &KubeOptions::tls)
+      .def_readwrite("token", &KubeOptions::token)
+      .def_readwrite("basic_user", &KubeOptions::basic_user)
+      .def_readwrite("basic_password", &KubeOptions::basic_password)
+      .def_readwrite("timeout_ns", &KubeOptions::timeout);
+
+  py::class_<DeploymentApi, PyDeploymentApi, py::smart_holder>(m, "DeploymentApi")
+      .def(py::init<>())
+      .def("get", [](DeploymentApi& a, const std::string& name) {
+        Result<ScaleObject> r;
+        {
+          py::gil_scoped_release rel;
+          r = a.get(name);
+        }
+        return unwrap(r);
+      })
+      .def("update", [](DeploymentApi& a, const std::string& name, const ScaleObject& o, int32_t n) {
+        Status s;
+        {
+          py::gil_scoped_release rel;
+          s = a.update(name, o, n);
+        }
+        if (!s.ok()) raise_status(s);
+      });
+  py::class_<KubeRestDeployments, DeploymentApi, py::smart_holder>(m, "KubeRestDeployments")
+      .def(py::init<KubeOptions>())
+      .def("path_for", &KubeRestDeployments::path_for)
+      .def("stats", [](KubeRestDeployments& k) {
+        auto s = k.stats();
+        py::dict d;
+        d["gets"] = s.gets;
+        d["updates"] = s.updates;
+        d["errors"] = s.errors;
+        d["conflicts"] = s.conflicts;
+        d["http"] = http_stats_dict(s.http);
+        return d;
+      });
+  py::class_<FakeDeployments, DeploymentApi, py::smart_holder>(m, "FakeDeployments")
+      .def(py::init<std::string>(), py::arg("namespace") = "namespace")
+      .def("add", &FakeDeployments::add)
+      .def("add_without_replicas", &FakeDeployments::add_without_replicas)
+      .def("replicas", &FakeDeployments::replicas)
+      .def("set_replicas", &FakeDeployments::set_replicas)
+      .def("set_latency", &FakeDeployments::set_latency)
+      .def("fail_next_get", &FakeDeployments::fail_next_get)
+      .def("fail_next_update", &FakeDeployments::fail_next_update)
+      .def("conflict_next", &FakeDeployments::conflict_next)
+      .def("gets", &FakeDeployments::gets)
+      .def("updates", &FakeDeployments::updates);
+
+  py::class_<ScaleSpan>(m, "ScaleSpan")
+      .def_readonly("get_ns", &ScaleSpan::get_ns)
+      .def_readonly("update_ns", &ScaleSpan::update_ns)
+      .def_readonly("read", &ScaleSpan::read)
+      .def_readonly("wrote", &ScaleSpan::wrote)
+      .def_readonly("before", &ScaleSpan::before)
+      .def_readonly("after", &ScaleSpan::after);
+
+  py::class_<PodAutoScaler, std::shared_ptr<PodAutoScaler>>(m, "PodAutoScaler")
+      .def(py::init<std::shared_ptr<DeploymentApi>, std::string, std::string, int64_t, int64_t, int64_t,
+                    int64_t, std::shared_ptr<Logger>, std::shared_ptr<Clock>>(),
+           py::arg("api"), py::arg("deployment"), py::arg("namespace"), py::arg("max"), py::arg("min"),
+           py::arg("scale_up_pods"), py::arg("scale_down_pods"), py::arg("logger"), py::arg("clock"))
+      .def("scale_up", [](PodAutoScaler& p) {
+        ScaleSpan span;
+        Status s;
+        {
+          py::gil_scoped_release rel;
+          s = p.scale_up(&span);
+        }
+        if (!s.ok()) raise_status(s);
+        return span;
+      })
+      .def("scale_down", [](PodAutoScaler& p) {
+        ScaleSpan span;
+        Status s;
+        {
+          py::gil_scoped_release rel;
+          s = p.scale_down(&span);
+        }
+        if (!s.ok()) raise_status(s);
+        return span;
+      })
+      .def_property_readonly("api", &PodAutoScaler::api)
+      .def_property_readonly("deployment", &PodAutoScaler::deployment)
+      .def_property_readonly("namespace", &PodAutoScaler::namespace_)
+      .def_property("max", &PodAutoScaler::max, &PodAutoScaler::set_max)
+      .def_property_readonly("min", &PodAutoScaler::min)
+      .def_property_readonly("scale_up_pods", &PodAutoScaler::scale_up_pods)
+      .def_property_readonly("scale_down_pods", &PodAutoScaler::scale_down_pods);
+
+  // ---- control loop ----
+  py::class_<LoopConfig>(m, "LoopConfig")
+      .def(py::init<>())
+      .def_readwrite("poll_period_ns", &LoopConfig::poll_period)
+      .def_readwrite("scale_down_cool_down_ns", &LoopConfig::scale_down_cool_down)
+      .def_readwrite("scale_up_cool_down_ns", &LoopConfig::scale_up_cool_down)
+      .def_readwrite("scale_up_messages", &LoopConfig::scale_up_messages)
+      .def_readwrite("scale_down_messages", &LoopConfig::scale_down_messages);
+
+  py::class_<Runner, std::shared_ptr<Runner>>(m, "Runner")
+      .def(py::init<LoopConfig, std::shared_ptr<SqsClient>, std::shared_ptr<PodAutoScaler>, std::shared_ptr<Clock>,
+                    std::shared_ptr<Logger>>(),
+           py::arg("config"), py::arg("sqs"), py::arg("scaler"), py::arg("clock"), py::arg("logger"))
+      .def("arm", &Runner::arm)
+      .def("step", [](Runner& r) {
+        IterationRecord rec;
+        {
+          py::gil_scoped_release rel;
+          rec = r.step(nullptr);
+        }
+        return record_dict(rec);
+      })
+      .def("run_iterations", [](Runner& r, int64_t n) {
+        py::gil_scoped_release rel;
+        r.run(nullptr, n);
+      })
+      .def("steps", [](Runner& r, int64_t n) {
+        std::vector<IterationRecord> recs;
+        {
+          py::gil_scoped_release rel;
+          recs.reserve(static_cast<size_t>(n));
+          for (int64_t i = 0; i < n; ++i) recs.push_back(r.step(nullptr));
+        }
+        py::list out;
+        for (auto& rec : recs) out.append(record_dict(rec));
+        return out;
+      })
+      .def("stats", [](Runner& r) {
+        auto s = r.stats();
+        py::dict d;
+        d["polls"] = s.polls;
+        d["depth_errors"] = s.depth_errors;
+        d["scale_ups"] = s.scale_ups;
+        d["scale_downs"] = s.scale_downs;
+        d["noop_ups"] = s.noop_ups;
+        d["noop_downs"] = s.noop_downs;
+        d["cooldown_skips_up"] = s.cooldown_skips_up;
+        d["cooldown_skips_down"] = s.cooldown_skips_down;
+        d["failed_ups"] = s.failed_ups;
+        d["failed_downs"] = s.failed_downs;
+        d["last_depth"] = s.last_depth;
+        d["last_replicas"] = s.last_replicas;
+        d["latency_samples"] = s.latency_samples;
+        return d;
+      })
+      .def("latencies", &Runner::latencies)
+      .def("clear_latencies", &Runner::clear_latencies)
+      .def_property_readonly("sqs", &Runner::sqs)
+      .def_property_readonly("scaler", &Runner::scaler)
+      .def_property_readonly("last_scale_up", &Runner::last_scale_up)
+      .def_property_readonly("last_scale_down", &Runner::last_scale_down);
+
+  py::class_<Supervisor, std::shared_ptr<Supervisor>>(m, "Supervisor")
+      .def(py::init<>())
+      .def("add", &Supervisor::add)
+      .def("start", &Supervisor::start, py::arg("max_iterations") = -1)
+      .def("stop", &Supervisor::stop)
+      .def("stopped", &Supervisor::stopped)
+      .def("wait", &Supervisor::wait, py::arg("timeout_ns"), py::call_guard<py::gil_scoped_release>())
+      .def("join", &Supervisor::join, py::call_guard<py::gil_scoped_release>())
+      .def("__len__", &Supervisor::size)
+      .def("runner", &Supervisor::runner);
+
+  m.def("percentile", &percentile);
+
+  // ---- fakes ----
+  py::class_<InjectedFault>(m, "InjectedFault")
+      .def(py::init([](int status, std::string body, std::string ct, bool drop) {
+             InjectedFault f;
+             f.status = status;
+             f.body = std::move(body);
+             f.content_type = std::move(ct);
+             f.drop_connection = drop;
+             return f;
+           }),
+           py::arg("status") = 500, py::arg("body") = "", py::arg("content_type") = "text/plain",
+           py::arg("drop_connection") = false);
+
+  py::class_<FakeSqsServer, std::shared_ptr<FakeSqsServer>>(m, "FakeSqsServer")
+      .def(py::init<>())
+      .def("require_signature", &FakeSqsServer::require_signature)
+      .def("start",
+           [](FakeSqsServer& s, const std::string& host, int port, bool tls) {
+             Status st = s.start(host, port, tls);
+             if (!st.ok()) raise_status(st);
+           },
+           py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("tls") = false)
+      .def("stop", &FakeSqsServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &FakeSqsServer::port)
+      .def_property_readonly("url", &FakeSqsServer::url)
+      .def_property_readonly("cert_pem", &FakeSqsServer::cert_pem)
+      .def("set_attributes", &FakeSqsServer::set_attributes)
+      .def("set_default_attributes", &FakeSqsServer::set_default_attributes)
+      .def("inject", &FakeSqsServer::inject)
+      .def("set_latency", &FakeSqsServer::set_latency)
+      .def("drop_connections", &FakeSqsServer::drop_connections)
+      .def("requests", &FakeSqsServer::requests)
+      .def("signature_failures", &FakeSqsServer::signature_failures)
+      .def("connections", &FakeSqsServer::connections)
+      .def("last_body", &FakeSqsServer::last_body)
+      .def("last_headers", &FakeSqsServer::last_headers);
+
+  py::class_<FakeKubeServer, std::shared_ptr<FakeKubeServer>>(m, "FakeKubeServer")
+      .def(py::init<>())
+      .def("require_token", &FakeKubeServer::require_token)
+      .def("start",
+           [](FakeKubeServer& s, const std::string& host, int port, bool tls) {
+             Status st = s.start(host, port, tls);
+             if (!st.ok()) raise_status(st);
+           },
+           py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("tls") = false)
+      .def("stop", &FakeKubeServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &FakeKubeServer::port)
+      .def_property_readonly("url", &FakeKubeServer::url)
+      .def_property_readonly("cert_pem", &FakeKubeServer::cert_pem)
+      .def("add_deployment", &FakeKubeServer::add_deployment)
+      .def("replicas", &FakeKubeServer::replicas)
+      .def("set_replicas", &FakeKubeServer::set_replicas)
+      .def("deployment_json", &FakeKubeServer::deployment_json)
+      .def("inject", &FakeKubeServer::inject)
+      .def("conflict_next", &FakeKubeServer::conflict_next)
+      .def("set_latency", &FakeKubeServer::set_latency)
+      .def("drop_connections", &FakeKubeServer::drop_connections)
+      .def("requests", &FakeKubeServer::requests)
+      .def("gets", &FakeKubeServer::gets)
+      .def("writes", &FakeKubeServer::writes)
+      .def("conflicts", &FakeKubeServer::conflicts)
+      .def("auth_failures", &FakeKubeServer::auth_failures)
+      .def("connections", &FakeKubeServer::connections)
+      .def("last_method", &FakeKubeServer::last_method)
+      .def("last_body", &FakeKubeServer::last_body)
+      .def("last_path", &FakeKubeServer::last_path);
+
+  m.attr("SECOND") = kSecond;
+  m.attr("MILLISECOND") = kMillisecond;
+  m.attr("MICROSECOND") = kMicrosecond;
+}

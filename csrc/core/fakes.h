@@ -1,0 +1,133 @@
+// Localhost fake endpoints for end-to-end tests and the latency benchmark.
+//
+// The reference's tests never leave the process (MockSQS, client-go's fake clientset;
+// /root/reference/main_test.go:241-304). To exercise the real wire path -- SigV4, the Query
+// and JSON protocols, keep-alive, TLS, resourceVersion conflicts, 5xx handling -- these
+// servers speak the actual HTTP APIs:
+//   * FakeSqsServer  -- POST / GetQueueAttributes (Query form or AWS JSON 1.0), verifies the
+//                       SigV4 signature by recomputation when credentials are configured.
+//   * FakeKubeServer -- apps/v1 Deployment GET/PUT and the autoscaling/v1 /scale subresource
+//                       GET/PUT/PATCH, bearer-token auth, resourceVersion optimistic
+//                       concurrency, realistic (~3 KB) Deployment bodies.
+// Both support injected failures and per-request latency.
+#pragma once
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "http.h"
+#include "sqs.h"
+
+namespace ksa {
+
+struct InjectedFault {
+  int status = 500;
+  std::string body;
+  std::string content_type = "text/plain";
+  bool drop_connection = false;  // close the socket without responding
+};
+
+class FakeSqsServer {
+ public:
+  FakeSqsServer();
+  ~FakeSqsServer();
+  // Requires valid SigV4 signatures for (access_key, secret, region).
+  void require_signature(std::string access_key, std::string secret, std::string region);
+  Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
+  void stop();
+  int port() const;
+  std::string url() const;
+  std::string cert_pem() const { return cert_pem_; }
+
+  void set_attributes(const std::string& queue_url, AttrMap attrs);
+  void set_default_attributes(AttrMap attrs);  // for queues not set explicitly
+  void inject(int count, InjectedFault fault);
+  void set_latency(Nanos per_request);
+  void drop_connections();
+
+  uint64_t requests() const { return requests_.load(); }
+  uint64_t signature_failures() const { return sig_failures_.load(); }
+  uint64_t connections() const;
+  std::string last_body() const;
+  Headers last_headers() const;
+
+ private:
+  void handle(const HttpRequest& req, HttpResponse* resp);
+
+  std::unique_ptr<HttpServer> server_;
+  bool tls_ = false;
+  std::string cert_pem_, key_pem_;
+  mutable std::mutex mu_;
+  std::map<std::string, AttrMap> queues_;
+  AttrMap default_attrs_;
+  bool verify_ = false;
+  std::string akid_, secret_, region_;
+  std::vector<InjectedFault> faults_;
+  Nanos latency_ = 0;
+  std::string last_body_;
+  Headers last_headers_;
+  std::atomic<uint64_t> requests_{0};
+  std::atomic<uint64_t> sig_failures_{0};
+};
+
+class FakeKubeServer {
+ public:
+  FakeKubeServer();
+  ~FakeKubeServer();
+  void require_token(std::string token);
+  Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
+  void stop();
+  int port() const;
+  std::string url() const;
+  std::string cert_pem() const { return cert_pem_; }
+
+  void add_deployment(const std::string& ns, const std::string& name, int32_t replicas);
+  int32_t replicas(const std::string& ns, const std::string& name) const;  // -1 if absent
+  void set_replicas(const std::string& ns, const std::string& name, int32_t replicas);
+  std::string deployment_json(const std::string& ns, const std::string& name) const;
+  void inject(int count, InjectedFault fault);
+  // The next n GETs are followed by a concurrent write (resourceVersion bump) -> next PUT 409s.
+  void conflict_next(int n);
+  void set_latency(Nanos per_request);
+  void drop_connections();
+
+  uint64_t requests() const { return requests_.load(); }
+  uint64_t gets() const { return gets_.load(); }
+  uint64_t writes() const { return writes_.load(); }
+  uint64_t conflicts() const { return conflicts_.load(); }
+  uint64_t auth_failures() const { return auth_failures_.load(); }
+  uint64_t connections() const;
+  std::string last_method() const;
+  std::string last_body() const;
+  std::string last_path() const;
+
+ private:
+  struct Obj {
+    int32_t replicas = 1;
+    uint64_t rv = 1;
+    int64_t generation = 1;
+  };
+  void handle(const HttpRequest& req, HttpResponse* resp);
+  std::string render_deployment(const std::string& ns, const std::string& name, const Obj& o) const;
+  std::string render_scale(const std::string& ns, const std::string& name, const Obj& o) const;
+  static std::string status_json(int code, const std::string& reason, const std::string& message);
+
+  std::unique_ptr<HttpServer> server_;
+  bool tls_ = false;
+  std::string cert_pem_, key_pem_;
+  mutable std::mutex mu_;
+  std::map<std::string, Obj> objs_;  // key: ns + "/" + name
+  std::string token_;
+  std::vector<InjectedFault> faults_;
+  int conflict_ = 0;
+  Nanos latency_ = 0;
+  uint64_t rv_counter_ = 5000;
+  std::string last_method_, last_body_, last_path_;
+  std::atomic<uint64_t> requests_{0}, gets_{0}, writes_{0}, conflicts_{0}, auth_failures_{0};
+};
+
+}  // namespace ksa

@@ -1,0 +1,896 @@
+#include "http.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstring>
+
+namespace ksa {
+
+namespace {
+
+int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+bool iequals(const std::string& a, const std::string& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i])))
+      return false;
+  return true;
+}
+
+std::string trim(const std::string& s) {
+  size_t b = 0, e = s.size();
+  while (b < e && (s[b] == ' ' || s[b] == '\t')) ++b;
+  while (e > b && (s[e - 1] == ' ' || s[e - 1] == '\t' || s[e - 1] == '\r')) --e;
+  return s.substr(b, e - b);
+}
+
+std::string header_of(const Headers& hs, const std::string& name) {
+  for (auto& [k, v] : hs)
+    if (iequals(k, name)) return v;
+  return "";
+}
+
+bool has_header(const Headers& hs, const std::string& name) {
+  for (auto& kv : hs)
+    if (iequals(kv.first, name)) return true;
+  return false;
+}
+
+std::string ssl_error_string() {
+  unsigned long e = ERR_get_error();
+  if (!e) return "unknown TLS error";
+  char buf[256];
+  ERR_error_string_n(e, buf, sizeof buf);
+  ERR_clear_error();
+  return buf;
+}
+
+// Waits for `events` on fd until the absolute deadline (0 = forever).
+Status wait_fd(int fd, short events, int64_t deadline_ns) {
+  while (true) {
+    int timeout_ms = -1;
+    if (deadline_ns) {
+      int64_t left = deadline_ns - mono_ns();
+      if (left <= 0) return Status::Err("i/o timeout");
+      timeout_ms = static_cast<int>((left + 999999) / 1000000);
+    }
+    struct pollfd p{fd, events, 0};
+    int r = ::poll(&p, 1, timeout_ms);
+    if (r > 0) return Status::OK();
+    if (r == 0) {
+      if (deadline_ns && mono_ns() >= deadline_ns) return Status::Err("i/o timeout");
+      continue;
+    }
+    if (errno == EINTR) continue;
+    return Status::Err(std::string("poll: ") + std::strerror(errno));
+  }
+}
+
+// A non-blocking socket, optionally wrapped in TLS, with deadline-bounded I/O.
+class Stream {
+ public:
+  Stream(int fd, SSL* ssl) : fd_(fd), ssl_(ssl) {}
+  ~Stream() {
+    if (ssl_) {
+      SSL_shutdown(ssl_);
+      SSL_free(ssl_);
+    }
+    if (fd_ >= 0) ::close(fd_);
+  }
+  int fd() const { return fd_; }
+
+  // Drives an SSL_* call that may want read/write readiness.
+  template <class F>
+  Status ssl_op(F op, int64_t deadline_ns, int* out, const char* what) {
+    while (true) {
+      ERR_clear_error();
+      int r = op();
+      if (r > 0) {
+        *out = r;
+        return Status::OK();
+      }
+      int e = SSL_get_error(ssl_, r);
+      if (e == SSL_ERROR_WANT_READ) {
+        Status s = wait_fd(fd_, POLLIN, deadline_ns);
+        if (!s.ok()) return s;
+      } else if (e == SSL_ERROR_WANT_WRITE) {
+        Status s = wait_fd(fd_, POLLOUT, deadline_ns);
+        if (!s.ok()) return s;
+      } else if (e == SSL_ERROR_ZERO_RETURN) {
+        *out = 0;
+        return Status::OK();
+      } else if (e == SSL_ERROR_SYSCALL && ERR_peek_error() == 0) {
+        *out = 0;  // unexpected EOF: treat as connection closed
+        return Status::OK();
+      } else {
+        return Status::Err(std::string(what) + ": " + ssl_error_string());
+      }
+    }
+  }
+
+  Status handshake(bool server, int64_t deadline_ns) {
+    int out = 0;
+    if (server) return ssl_op([&] { return SSL_accept(ssl_); }, deadline_ns, &out, "tls accept");
+    Status s = ssl_op([&] { return SSL_connect(ssl_); }, deadline_ns, &out, "tls handshake");
+    if (s.ok() && out == 0) return Status::Err("tls handshake: connection closed");
+    return s;
+  }
+
+  // Appends what is available (at least one byte) to buf. *eof on orderly close.
+  Status read_some(std::string* buf, int64_t deadline_ns, bool* eof) {
+    char tmp[16384];
+    *eof = false;
+    if (ssl_) {
+      int n = 0;
+      Status s = ssl_op([&] { return SSL_read(ssl_, tmp, sizeof tmp); }, deadline_ns, &n, "tls read");
+      if (!s.ok()) return s;
+      if (n == 0) *eof = true;
+      else buf->append(tmp, static_cast<size_t>(n));
+      return Status::OK();
+    }
+    while (true) {
+      ssize_t n = ::recv(fd_, tmp, sizeof tmp, 0);
+      if (n > 0) {
+        buf->append(tmp, static_cast<size_t>(n));
+        return Status::OK();
+      }
+      if (n == 0) {
+        *eof = true;
+        return Status::OK();
+      }
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        Status s = wait_fd(fd_, POLLIN, deadline_ns);
+        if (!s.ok()) return s;
+        continue;
+      }
+      if (errno == ECONNRESET) {
+        *eof = true;
+        return Status::Err("connection reset by peer");
+      }
+      return Status::Err(std::string("read: ") + std::strerror(errno));
+    }
+  }
+
+  Status write_all(const std::string& data, int64_t deadline_ns) {
+    size_t off = 0;
+    while (off < data.size()) {
+      if (ssl_) {
+        int n = 0;
+        Status s = ssl_op(
+            [&] { return SSL_write(ssl_, data.data() + off, static_cast<int>(data.size() - off)); },
+            deadline_ns, &n, "tls write");
+        if (!s.ok()) return s;
+        if (n == 0) return Status::Err("write: connection closed");
+        off += static_cast<size_t>(n);
+        continue;
+      }
+      ssize_t n = ::send(fd_, data.data() + off, data.size() - off, MSG_NOSIGNAL);
+      if (n > 0) {
+        off += static_cast<size_t>(n);
+        continue;
+      }
+      if (n < 0 && errno == EINTR) continue;
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        Status s = wait_fd(fd_, POLLOUT, deadline_ns);
+        if (!s.ok()) return s;
+        continue;
+      }
+      return Status::Err(std::string("write: ") + std::strerror(errno));
+    }
+    return Status::OK();
+  }
+
+ private:
+  int fd_;
+  SSL* ssl_;
+};
+
+// Incremental HTTP/1.1 message framing over a Stream with a carry-over buffer.
+class Reader {
+ public:
+  Reader(Stream* s, std::string* buf) : s_(s), buf_(buf) {}
+
+  // Reads through the blank line; returns the head (without the terminator).
+  Status read_head(std::string* head, int64_t deadline_ns, bool* got_any) {
+    *got_any = !buf_->empty();
+    while (true) {
+      size_t p = buf_->find("\r\n\r\n");
+      if (p != std::string::npos) {
+        head->assign(*buf_, 0, p);
+        buf_->erase(0, p + 4);
+        return Status::OK();
+      }
+      if (buf_->size() > 1 << 20) return Status::Err("header too large");
+      bool eof = false;
+      Status s = s_->read_some(buf_, deadline_ns, &eof);
+      if (!s.ok()) return s;
+      if (eof) return Status::Err(buf_->empty() ? "EOF" : "unexpected EOF");
+      *got_any = true;
+    }
+  }
+
+  Status read_exact(size_t n, std::string* out, int64_t deadline_ns) {
+    while (buf_->size() < n) {
+      bool eof = false;
+      Status s = s_->read_some(buf_, deadline_ns, &eof);
+      if (!s.ok()) return s;
+      if (eof) return Status::Err("unexpected EOF");
+    }
+    out->append(*buf_, 0, n);
+    buf_->erase(0, n);
+    return Status::OK();
+  }
+
+  Status read_line(std::string* line, int64_t deadline_ns) {
+    while (true) {
+      size_t p = buf_->find("\r\n");
+      if (p != std::string::npos) {
+        line->assign(*buf_, 0, p);
+        buf_->erase(0, p + 2);
+        return Status::OK();
+      }
+      bool eof = false;
+      Status s = s_->read_some(buf_, deadline_ns, &eof);
+      if (!s.ok()) return s;
+      if (eof) return Status::Err("unexpected EOF");
+    }
+  }
+
+  Status read_chunked(std::string* out, int64_t deadline_ns) {
+    while (true) {
+      std::string line;
+      Status s = read_line(&line, deadline_ns);
+      if (!s.ok()) return s;
+      size_t semi = line.find(';');
+      std::string hex = trim(semi == std::string::npos ? line : line.substr(0, semi));
+      if (hex.empty()) return Status::Err("malformed chunk size");
+      char* end = nullptr;
+      unsigned long long n = std::strtoull(hex.c_str(), &end, 16);
+      if (*end != '\0') return Status::Err("malformed chunk size");
+      if (n == 0) {
+        // trailers until blank line
+        while (true) {
+          std::string t;
+          s = read_line(&t, deadline_ns);
+          if (!s.ok()) return s;
+          if (t.empty()) return Status::OK();
+        }
+      }
+      s = read_exact(static_cast<size_t>(n), out, deadline_ns);
+      if (!s.ok()) return s;
+      std::string crlf;
+      s = read_line(&crlf, deadline_ns);
+      if (!s.ok()) return s;
+    }
+  }
+
+  Status read_to_eof(std::string* out, int64_t deadline_ns) {
+    out->append(*buf_);
+    buf_->clear();
+    while (true) {
+      bool eof = false;
+      std::string tmp;
+      Status s = s_->read_some(&tmp, deadline_ns, &eof);
+      if (!s.ok()) return s;
+      if (eof) return Status::OK();
+      out->append(tmp);
+    }
+  }
+
+ private:
+  Stream* s_;
+  std::string* buf_;
+};
+
+void parse_header_lines(const std::string& head, size_t from, Headers* out) {
+  size_t pos = from;
+  while (pos < head.size()) {
+    size_t e = head.find("\r\n", pos);
+    if (e == std::string::npos) e = head.size();
+    std::string line = head.substr(pos, e - pos);
+    size_t colon = line.find(':');
+    if (colon != std::string::npos) out->emplace_back(trim(line.substr(0, colon)), trim(line.substr(colon + 1)));
+    pos = e + 2;
+  }
+}
+
+bool wants_close(const Headers& hs, bool http10) {
+  std::string c = lower(header_of(hs, "Connection"));
+  if (c.find("close") != std::string::npos) return true;
+  if (http10 && c.find("keep-alive") == std::string::npos) return true;
+  return false;
+}
+
+bool is_chunked(const Headers& hs) {
+  return lower(header_of(hs, "Transfer-Encoding")).find("chunked") != std::string::npos;
+}
+
+struct SslInit {
+  SslInit() { OPENSSL_init_ssl(0, nullptr); }
+};
+void ensure_ssl() { static SslInit once; }
+
+Status load_ca_pem(SSL_CTX* ctx, const std::string& pem) {
+  BIO* bio = BIO_new_mem_buf(pem.data(), static_cast<int>(pem.size()));
+  X509_STORE* store = SSL_CTX_get_cert_store(ctx);
+  int added = 0;
+  while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
+    X509_STORE_add_cert(store, x);
+    X509_free(x);
+    ++added;
+  }
+  ERR_clear_error();
+  BIO_free(bio);
+  if (!added) return Status::Err("no certificates found in CA data");
+  return Status::OK();
+}
+
+Status use_cert_key(SSL_CTX* ctx, const std::string& cert_pem, const std::string& key_pem) {
+  BIO* cb = BIO_new_mem_buf(cert_pem.data(), static_cast<int>(cert_pem.size()));
+  X509* cert = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr);
+  if (!cert) {
+    BIO_free(cb);
+    return Status::Err("invalid certificate PEM: " + ssl_error_string());
+  }
+  int ok = SSL_CTX_use_certificate(ctx, cert);
+  X509_free(cert);
+  // Remaining certificates form the chain.
+  while (X509* extra = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr)) {
+    SSL_CTX_add_extra_chain_cert(ctx, extra);  // takes ownership
+  }
+  ERR_clear_error();
+  BIO_free(cb);
+  if (ok != 1) return Status::Err("SSL_CTX_use_certificate: " + ssl_error_string());
+  BIO* kb = BIO_new_mem_buf(key_pem.data(), static_cast<int>(key_pem.size()));
+  EVP_PKEY* key = PEM_read_bio_PrivateKey(kb, nullptr, nullptr, nullptr);
+  BIO_free(kb);
+  if (!key) return Status::Err("invalid private key PEM: " + ssl_error_string());
+  ok = SSL_CTX_use_PrivateKey(ctx, key);
+  EVP_PKEY_free(key);
+  if (ok != 1) return Status::Err("SSL_CTX_use_PrivateKey: " + ssl_error_string());
+  return Status::OK();
+}
+
+bool is_ip_literal(const std::string& h) {
+  unsigned char buf[16];
+  return inet_pton(AF_INET, h.c_str(), buf) == 1 || inet_pton(AF_INET6, h.c_str(), buf) == 1;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// URL
+
+std::string Url::host_header() const {
+  std::string h = host.find(':') != std::string::npos ? "[" + host + "]" : host;
+  bool dflt = (tls() && port == 443) || (!tls() && port == 80);
+  return dflt ? h : h + ":" + std::to_string(port);
+}
+
+std::string Url::origin() const { return scheme + "://" + host_header(); }
+
+Result<Url> parse_url(const std::string& s) {
+  Url u;
+  size_t p = s.find("://");
+  if (p == std::string::npos) return Result<Url>::Err(Status::Err("invalid URL " + s + ": missing scheme"));
+  u.scheme = lower(s.substr(0, p));
+  if (u.scheme != "http" && u.scheme != "https")
+    return Result<Url>::Err(Status::Err("unsupported protocol scheme \"" + u.scheme + "\""));
+  size_t host_start = p + 3;
+  size_t path_start = s.find_first_of("/?#", host_start);
+  std::string authority = s.substr(host_start, path_start == std::string::npos ? std::string::npos : path_start - host_start);
+  size_t at = authority.rfind('@');
+  if (at != std::string::npos) authority = authority.substr(at + 1);
+  std::string port_str;
+  if (!authority.empty() && authority[0] == '[') {
+    size_t rb = authority.find(']');
+    if (rb == std::string::npos) return Result<Url>::Err(Status::Err("invalid URL " + s + ": bad IPv6 host"));
+    u.host = authority.substr(1, rb - 1);
+    if (rb + 1 < authority.size() && authority[rb + 1] == ':') port_str = authority.substr(rb + 2);
+  } else {
+    size_t colon = authority.rfind(':');
+    if (colon != std::string::npos) {
+      u.host = authority.substr(0, colon);
+      port_str = authority.substr(colon + 1);
+    } else {
+      u.host = authority;
+    }
+  }
+  if (u.host.empty()) return Result<Url>::Err(Status::Err("invalid URL " + s + ": empty host"));
+  if (!port_str.empty()) {
+    for (char c : port_str)
+      if (c < '0' || c > '9') return Result<Url>::Err(Status::Err("invalid URL " + s + ": bad port"));
+    u.port = std::atoi(port_str.c_str());
+    if (u.port <= 0 || u.port > 65535) return Result<Url>::Err(Status::Err("invalid URL " + s + ": bad port"));
+  } else {
+    u.port = u.tls() ? 443 : 80;
+  }
+  if (path_start == std::string::npos) {
+    u.path = "/";
+  } else {
+    u.path = s.substr(path_start);
+    size_t hash = u.path.find('#');
+    if (hash != std::string::npos) u.path = u.path.substr(0, hash);
+    if (u.path.empty() || u.path[0] != '/') u.path = "/" + u.path;
+  }
+  return Result<Url>::Ok(u);
+}
+
+std::string HttpRequest::header(const std::string& name) const { return header_of(headers, name); }
+std::string HttpResponse::header(const std::string& name) const { return header_of(headers, name); }
+
+const char* http_reason(int status) {
+  switch (status) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 403: return "Forbidden";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 415: return "Unsupported Media Type";
+    case 422: return "Unprocessable Entity";
+    case 429: return "Too Many Requests";
+    case 500: return "Internal Server Error";
+    case 502: return "Bad Gateway";
+    case 503: return "Service Unavailable";
+    case 504: return "Gateway Timeout";
+  }
+  return "Status";
+}
+
+// ---------------------------------------------------------------------------------------
+// Client
+
+struct HttpClient::Conn {
+  std::unique_ptr<Stream> stream;
+  std::string rbuf;
+  uint64_t uses = 0;
+};
+
+HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
+    : origin_(origin), tls_(std::move(tls)), timeout_(timeout) {
+  if (!origin_.tls()) return;
+  ensure_ssl();
+  ctx_ = SSL_CTX_new(TLS_client_method());
+  if (!ctx_) {
+    ctx_status_ = Status::Err("SSL_CTX_new: " + ssl_error_string());
+    return;
+  }
+  SSL_CTX_set_min_proto_version(ctx_, TLS1_2_VERSION);
+  if (tls_.insecure_skip_verify) {
+    SSL_CTX_set_verify(ctx_, SSL_VERIFY_NONE, nullptr);
+  } else {
+    SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
+    if (!tls_.ca_pem.empty()) {
+      ctx_status_ = load_ca_pem(ctx_, tls_.ca_pem);
+    } else if (!tls_.ca_file.empty()) {
+      if (SSL_CTX_load_verify_locations(ctx_, tls_.ca_file.c_str(), nullptr) != 1)
+        ctx_status_ = Status::Err("unable to load CA file " + tls_.ca_file + ": " + ssl_error_string());
+    } else {
+      SSL_CTX_set_default_verify_paths(ctx_);
+    }
+  }
+  if (ctx_status_.ok() && !tls_.cert_pem.empty())
+    ctx_status_ = use_cert_key(ctx_, tls_.cert_pem, tls_.key_pem);
+  // Session resumption makes reconnects after an idle close cheap.
+  SSL_CTX_set_session_cache_mode(ctx_, SSL_SESS_CACHE_CLIENT);
+}
+
+HttpClient::~HttpClient() {
+  conn_.reset();
+  if (ctx_) SSL_CTX_free(ctx_);
+}
+
+void HttpClient::close() {
+  std::lock_guard<std::mutex> lk(mu_);
+  conn_.reset();
+}
+
+HttpClientStats HttpClient::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+Status HttpClient::connect_locked(int64_t deadline_ns) {
+  if (!ctx_status_.ok()) return ctx_status_;
+  struct addrinfo hints;
+  std::memset(&hints, 0, sizeof hints);
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  struct addrinfo* res = nullptr;
+  std::string port = std::to_string(origin_.port);
+  int gai = getaddrinfo(origin_.host.c_str(), port.c_str(), &hints, &res);
+  if (gai != 0)
+    return Status::Err("dial tcp: lookup " + origin_.host + ": " + gai_strerror(gai));
+  Status last = Status::Err("dial tcp " + origin_.host_header() + ": no addresses");
+  int fd = -1;
+  for (auto* ai = res; ai; ai = ai->ai_next) {
+    fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, ai->ai_protocol);
+    if (fd < 0) continue;
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    int r = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    if (r != 0 && errno == EINPROGRESS) {
+      Status w = wait_fd(fd, POLLOUT, deadline_ns);
+      int err = 0;
+      socklen_t len = sizeof err;
+      getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
+      if (w.ok() && err == 0) r = 0;
+      else {
+        last = Status::Err("dial tcp " + origin_.host_header() + ": " +
+                           (w.ok() ? std::strerror(err) : w.message()));
+      }
+    } else if (r != 0) {
+      last = Status::Err("dial tcp " + origin_.host_header() + ": " + std::strerror(errno));
+    }
+    if (r == 0) break;
+    ::close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(res);
+  if (fd < 0) return last;
+
+  SSL* ssl = nullptr;
+  if (origin_.tls()) {
+    ssl = SSL_new(ctx_);
+    SSL_set_fd(ssl, fd);
+    const std::string& name = tls_.server_name.empty() ? origin_.host : tls_.server_name;
+    if (!is_ip_literal(name)) SSL_set_tlsext_host_name(ssl, name.c_str());
+    if (!tls_.insecure_skip_verify) {
+      X509_VERIFY_PARAM* param = SSL_get0_param(ssl);
+      if (is_ip_literal(name)) X509_VERIFY_PARAM_set1_ip_asc(param, name.c_str());
+      else X509_VERIFY_PARAM_set1_host(param, name.c_str(), 0);
+    }
+  }
+  auto stream = std::make_unique<Stream>(fd, ssl);
+  if (ssl) {
+    Status h = stream->handshake(false, deadline_ns);
+    if (!h.ok()) {
+      long vr = SSL_get_verify_result(ssl);
+      if (vr != X509_V_OK)
+        return Status::Err("x509: certificate verification failed: " +
+                           std::string(X509_verify_cert_error_string(vr)));
+      return h;
+    }
+  }
+  conn_ = std::make_unique<Conn>();
+  conn_->stream = std::move(stream);
+  stats_.connects++;
+  return Status::OK();
+}
+
+Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
+                           bool* retryable) {
+  *retryable = false;
+  if (!conn_) {
+    Status s = connect_locked(deadline_ns);
+    if (!s.ok()) return s;
+  }
+  const bool reused = conn_->uses > 0;
+  conn_->uses++;
+
+  std::string wire;
+  wire.reserve(256 + req.body.size());
+  wire += req.method;
+  wire.push_back(' ');
+  wire += req.target.empty() ? "/" : req.target;
+  wire += " HTTP/1.1\r\n";
+  if (!has_header(req.headers, "Host")) wire += "Host: " + origin_.host_header() + "\r\n";
+  if (!has_header(req.headers, "User-Agent")) wire += "User-Agent: kube-sqs-autoscaler-amd/1.0\r\n";
+  for (auto& [k, v] : req.headers) wire += k + ": " + v + "\r\n";
+  if (!req.body.empty() || req.method == "POST" || req.method == "PUT" || req.method == "PATCH") {
+    if (!has_header(req.headers, "Content-Length"))
+      wire += "Content-Length: " + std::to_string(req.body.size()) + "\r\n";
+  }
+  wire += "\r\n";
+  wire += req.body;
+
+  Status s = conn_->stream->write_all(wire, deadline_ns);
+  if (!s.ok()) {
+    *retryable = reused && s.message() != "i/o timeout";
+    conn_.reset();
+    return s;
+  }
+  stats_.bytes_out += wire.size();
+
+  Reader rd(conn_->stream.get(), &conn_->rbuf);
+  std::string head;
+  bool got_any = false;
+  while (true) {
+    s = rd.read_head(&head, deadline_ns, &got_any);
+    if (!s.ok()) {
+      *retryable = reused && !got_any && s.message() != "i/o timeout";
+      conn_.reset();
+      return s;
+    }
+    // Status line
+    size_t eol = head.find("\r\n");
+    std::string status_line = head.substr(0, eol);
+    if (status_line.compare(0, 5, "HTTP/") != 0) {
+      conn_.reset();
+      return Status::Err("malformed HTTP response " + status_line);
+    }
+    size_t sp1 = status_line.find(' ');
+    if (sp1 == std::string::npos) {
+      conn_.reset();
+      return Status::Err("malformed HTTP status line");
+    }
+    resp->status = std::atoi(status_line.c_str() + sp1 + 1);
+    size_t sp2 = status_line.find(' ', sp1 + 1);
+    resp->reason = sp2 == std::string::npos ? "" : status_line.substr(sp2 + 1);
+    resp->headers.clear();
+    if (eol != std::string::npos) parse_header_lines(head, eol + 2, &resp->headers);
+    if (resp->status >= 100 && resp->status < 200 && resp->status != 101) continue;  // interim
+    break;
+  }
+  const bool http10 = head.compare(0, 8, "HTTP/1.0") == 0;
+  bool close_after = wants_close(resp->headers, http10);
+  resp->body.clear();
+  if (req.method == "HEAD" || resp->status == 204 || resp->status == 304) {
+    // no body
+  } else if (is_chunked(resp->headers)) {
+    s = rd.read_chunked(&resp->body, deadline_ns);
+  } else if (!resp->header("Content-Length").empty()) {
+    long long n = std::atoll(resp->header("Content-Length").c_str());
+    if (n < 0) s = Status::Err("bad Content-Length");
+    else s = rd.read_exact(static_cast<size_t>(n), &resp->body, deadline_ns);
+  } else {
+    s = rd.read_to_eof(&resp->body, deadline_ns);
+    close_after = true;
+  }
+  if (!s.ok()) {
+    conn_.reset();
+    return s;
+  }
+  stats_.bytes_in += head.size() + resp->body.size();
+  if (close_after) conn_.reset();
+  return Status::OK();
+}
+
+Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
+  stats_.requests++;
+  bool retryable = false;
+  Status s = attempt(req, resp, deadline, &retryable);
+  if (!s.ok() && retryable) {
+    stats_.reconnect_retries++;
+    s = attempt(req, resp, deadline, &retryable);
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// Server
+
+HttpServer::HttpServer(Handler h) : handler_(std::move(h)) {}
+
+HttpServer::~HttpServer() {
+  stop();
+  if (ctx_) SSL_CTX_free(ctx_);
+}
+
+Status HttpServer::enable_tls(const std::string& cert_pem, const std::string& key_pem) {
+  ensure_ssl();
+  ctx_ = SSL_CTX_new(TLS_server_method());
+  if (!ctx_) return Status::Err("SSL_CTX_new: " + ssl_error_string());
+  return use_cert_key(ctx_, cert_pem, key_pem);
+}
+
+Status HttpServer::listen(const std::string& host, int port) {
+  struct addrinfo hints;
+  std::memset(&hints, 0, sizeof hints);
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_flags = AI_PASSIVE;
+  struct addrinfo* res = nullptr;
+  std::string p = std::to_string(port);
+  if (getaddrinfo(host.c_str(), p.c_str(), &hints, &res) != 0) return Status::Err("bad listen address " + host);
+  int fd = ::socket(res->ai_family, res->ai_socktype | SOCK_CLOEXEC, res->ai_protocol);
+  if (fd < 0) {
+    freeaddrinfo(res);
+    return Status::Err(std::string("socket: ") + std::strerror(errno));
+  }
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (::bind(fd, res->ai_addr, res->ai_addrlen) != 0 || ::listen(fd, 128) != 0) {
+    std::string e = std::strerror(errno);
+    ::close(fd);
+    freeaddrinfo(res);
+    return Status::Err("listen " + host + ":" + p + ": " + e);
+  }
+  freeaddrinfo(res);
+  struct sockaddr_storage ss;
+  socklen_t len = sizeof ss;
+  getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len);
+  port_ = ss.ss_family == AF_INET6 ? ntohs(reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port)
+                                   : ntohs(reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+  listen_fd_ = fd;
+  acceptor_ = std::thread([this] { accept_loop(); });
+  return Status::OK();
+}
+
+void HttpServer::accept_loop() {
+  while (!stopping_.load()) {
+    int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+    if (fd < 0) {
+      if (errno == EINTR || errno == ECONNABORTED) continue;
+      break;  // listener shut down
+    }
+    if (stopping_.load()) {
+      ::close(fd);
+      break;
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    accepted_++;
+    std::lock_guard<std::mutex> lk(mu_);
+    open_fds_.push_back(fd);
+    workers_.emplace_back([this, fd] { serve(fd); });
+  }
+}
+
+void HttpServer::serve(int fd) {
+  SSL* ssl = nullptr;
+  if (ctx_) {
+    ssl = SSL_new(ctx_);
+    SSL_set_fd(ssl, fd);
+  }
+  int fl = fcntl(fd, F_GETFL, 0);
+  fcntl(fd, F_SETFL, fl | O_NONBLOCK);
+  {
+    Stream stream(fd, ssl);
+    bool ok = true;
+    if (ssl) ok = stream.handshake(true, mono_ns() + 10 * kSecond).ok();
+    std::string rbuf;
+    Reader rd(&stream, &rbuf);
+    while (ok && !stopping_.load()) {
+      std::string head;
+      bool got_any = false;
+      if (!rd.read_head(&head, 0, &got_any).ok()) break;
+      HttpRequest req;
+      size_t eol = head.find("\r\n");
+      std::string line = head.substr(0, eol);
+      size_t a = line.find(' '), b = line.rfind(' ');
+      if (a == std::string::npos || b == a) break;
+      req.method = line.substr(0, a);
+      req.target = line.substr(a + 1, b - a - 1);
+      const bool http10 = line.compare(b + 1, 8, "HTTP/1.0") == 0;
+      if (eol != std::string::npos) parse_header_lines(head, eol + 2, &req.headers);
+      Status s;
+      if (is_chunked(req.headers)) {
+        s = rd.read_chunked(&req.body, 0);
+      } else if (!req.header("Content-Length").empty()) {
+        long long n = std::atoll(req.header("Content-Length").c_str());
+        if (n < 0 || n > (64LL << 20)) break;
+        s = rd.read_exact(static_cast<size_t>(n), &req.body, 0);
+      }
+      if (!s.ok()) break;
+      HttpResponse resp;
+      resp.status = 200;
+      handler_(req, &resp);
+      bool close_after = wants_close(req.headers, http10) || resp.status < 0;
+      if (resp.status < 0) break;  // handler asked to drop the connection without replying
+      std::string wire = "HTTP/1.1 " + std::to_string(resp.status) + " " +
+                         (resp.reason.empty() ? http_reason(resp.status) : resp.reason) + "\r\n";
+      for (auto& [k, v] : resp.headers) wire += k + ": " + v + "\r\n";
+      if (!has_header(resp.headers, "Content-Length"))
+        wire += "Content-Length: " + std::to_string(resp.body.size()) + "\r\n";
+      if (close_after) wire += "Connection: close\r\n";
+      wire += "\r\n";
+      wire += resp.body;
+      if (!stream.write_all(wire, mono_ns() + 10 * kSecond).ok()) break;
+      served_++;
+      if (close_after) break;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    open_fds_.erase(std::remove(open_fds_.begin(), open_fds_.end(), fd), open_fds_.end());
+  }  // Stream dtor closes fd (after removal from open_fds_, so no fd-reuse race)
+}
+
+void HttpServer::drop_connections() {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int fd : open_fds_) ::shutdown(fd, SHUT_RDWR);
+}
+
+void HttpServer::stop() {
+  if (stopping_.exchange(true)) return;
+  if (listen_fd_ >= 0) {
+    ::shutdown(listen_fd_, SHUT_RDWR);
+  }
+  if (acceptor_.joinable()) acceptor_.join();
+  if (listen_fd_ >= 0) {
+    ::close(listen_fd_);
+    listen_fd_ = -1;
+  }
+  std::vector<std::thread> ws;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int fd : open_fds_) ::shutdown(fd, SHUT_RDWR);
+    ws.swap(workers_);
+  }
+  for (auto& t : ws)
+    if (t.joinable()) t.join();
+}
+
+// ---------------------------------------------------------------------------------------
+// Self-signed certificates for TLS fakes
+
+Status generate_self_signed(const std::string& host, std::string* cert_pem, std::string* key_pem) {
+  ensure_ssl();
+  EVP_PKEY* pkey = EVP_EC_gen("P-256");
+  if (!pkey) return Status::Err("EVP_EC_gen: " + ssl_error_string());
+  X509* x = X509_new();
+  X509_set_version(x, 2);
+  ASN1_INTEGER_set(X509_get_serialNumber(x), 1);
+  X509_gmtime_adj(X509_getm_notBefore(x), -3600);
+  X509_gmtime_adj(X509_getm_notAfter(x), 3600L * 24 * 365);
+  X509_set_pubkey(x, pkey);
+  X509_NAME* name = X509_get_subject_name(x);
+  X509_NAME_add_entry_by_txt(name, "CN", MBSTRING_ASC,
+                             reinterpret_cast<const unsigned char*>(host.c_str()), -1, -1, 0);
+  X509_set_issuer_name(x, name);
+  std::string san = (is_ip_literal(host) ? "IP:" : "DNS:") + host;
+  X509V3_CTX v3;
+  X509V3_set_ctx_nodb(&v3);
+  X509V3_set_ctx(&v3, x, x, nullptr, nullptr, 0);
+  X509_EXTENSION* ext = X509V3_EXT_conf_nid(nullptr, &v3, NID_subject_alt_name, san.c_str());
+  if (ext) {
+    X509_add_ext(x, ext, -1);
+    X509_EXTENSION_free(ext);
+  }
+  X509_EXTENSION* bc = X509V3_EXT_conf_nid(nullptr, &v3, NID_basic_constraints, "critical,CA:TRUE");
+  if (bc) {
+    X509_add_ext(x, bc, -1);
+    X509_EXTENSION_free(bc);
+  }
+  if (!X509_sign(x, pkey, EVP_sha256())) {
+    X509_free(x);
+    EVP_PKEY_free(pkey);
+    return Status::Err("X509_sign: " + ssl_error_string());
+  }
+  BIO* cb = BIO_new(BIO_s_mem());
+  PEM_write_bio_X509(cb, x);
+  BIO* kb = BIO_new(BIO_s_mem());
+  PEM_write_bio_PrivateKey(kb, pkey, nullptr, nullptr, 0, nullptr, nullptr);
+  char* data = nullptr;
+  long n = BIO_get_mem_data(cb, &data);
+  cert_pem->assign(data, static_cast<size_t>(n));
+  n = BIO_get_mem_data(kb, &data);
+  key_pem->assign(data, static_cast<size_t>(n));
+  BIO_free(cb);
+  BIO_free(kb);
+  X509_free(x);
+  EVP_PKEY_free(pkey);
+  return Status::OK();
+}
+
+}  // namespace ksa

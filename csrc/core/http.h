@@ -1,0 +1,151 @@
+// HTTP/1.1 transport: keep-alive client (plain TCP or TLS) and a small threaded server.
+//
+// The reference's only "communication backend" is two HTTPS request/response APIs: SQS
+// GetQueueAttributes (/root/reference/sqs/sqs.go:51) and the kube-apiserver Deployment GET/PUT
+// (/root/reference/scale/scale.go:55,72,82,100), made through the AWS SDK's and client-go's
+// pooled net/http transports. Poll->patch latency is three sequential round trips, so what
+// matters is (a) never paying a TCP/TLS handshake on the hot path (persistent connection per
+// endpoint, transparent reconnect when the peer closed an idle socket), (b) TCP_NODELAY so
+// small request/response pairs are not held back by Nagle, and (c) no per-request
+// allocation churn beyond the body strings. Per-call deadlines are enforced with poll(2);
+// the reference has none.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "clock.h"
+#include "sigv4.h"  // Headers
+#include "status.h"
+
+typedef struct ssl_ctx_st SSL_CTX;
+
+namespace ksa {
+
+struct Url {
+  std::string scheme;  // "http" | "https"
+  std::string host;    // without brackets for IPv6
+  int port = 0;
+  std::string path;    // path + query as it appears on the wire ("/" when empty)
+  bool tls() const { return scheme == "https"; }
+  std::string host_header() const;  // host[:port], port omitted when default
+  std::string origin() const;       // scheme://host[:port]
+};
+Result<Url> parse_url(const std::string& s);
+
+struct TlsOptions {
+  bool insecure_skip_verify = false;
+  std::string ca_file;
+  std::string ca_pem;
+  std::string cert_pem;  // client certificate (mutual TLS, kubeconfig client-certificate-data)
+  std::string key_pem;
+  std::string server_name;  // SNI / verification name override (kubeconfig tls-server-name)
+};
+
+struct HttpRequest {
+  std::string method = "GET";
+  std::string target = "/";  // origin-form request target (path + query)
+  Headers headers;
+  std::string body;
+  std::string header(const std::string& name) const;  // case-insensitive, first match
+};
+
+struct HttpResponse {
+  int status = 0;
+  std::string reason;
+  Headers headers;
+  std::string body;
+  std::string header(const std::string& name) const;
+};
+
+struct HttpClientStats {
+  uint64_t requests = 0;
+  uint64_t connects = 0;
+  uint64_t reconnect_retries = 0;
+  uint64_t bytes_out = 0;
+  uint64_t bytes_in = 0;
+};
+
+// One persistent connection to one origin. Thread-safe (requests are serialised), but each
+// control-loop worker owns its clients, so there is no contention in practice.
+class HttpClient {
+ public:
+  HttpClient(const Url& origin, TlsOptions tls, Nanos timeout);
+  ~HttpClient();
+  HttpClient(const HttpClient&) = delete;
+  HttpClient& operator=(const HttpClient&) = delete;
+
+  // Sends `req` (Host / Content-Length / User-Agent added when absent) and reads the full
+  // response. Reuses the connection; if a reused connection turns out to be dead before any
+  // response byte arrived, reconnects and retries once (what Go's transport does for
+  // requests that are safe to replay).
+  Status round_trip(const HttpRequest& req, HttpResponse* resp);
+  void close();
+  HttpClientStats stats() const;
+  const Url& origin() const { return origin_; }
+  void set_timeout(Nanos t) { timeout_ = t; }
+
+ private:
+  struct Conn;
+  Status connect_locked(int64_t deadline_ns);
+  Status attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
+                 bool* retryable);
+
+  Url origin_;
+  TlsOptions tls_;
+  Nanos timeout_;
+  SSL_CTX* ctx_ = nullptr;
+  Status ctx_status_;
+  mutable std::mutex mu_;
+  std::unique_ptr<Conn> conn_;
+  HttpClientStats stats_;
+};
+
+// Threaded HTTP/1.1 server (accept thread + one thread per connection). Used by the fake
+// SQS / kube-apiserver endpoints in tests and benchmarks; blocking reads give the lowest
+// wake-up latency for a handful of persistent connections.
+class HttpServer {
+ public:
+  using Handler = std::function<void(const HttpRequest&, HttpResponse*)>;
+  explicit HttpServer(Handler h);
+  ~HttpServer();
+  // TLS: PEM certificate chain + key; call before listen().
+  Status enable_tls(const std::string& cert_pem, const std::string& key_pem);
+  Status listen(const std::string& host, int port);
+  int port() const { return port_; }
+  void stop();
+  uint64_t requests_served() const { return served_.load(); }
+  uint64_t connections_accepted() const { return accepted_.load(); }
+  // Close every open client connection after its in-flight response (idle-close test).
+  void drop_connections();
+
+ private:
+  void accept_loop();
+  void serve(int fd);
+
+  Handler handler_;
+  SSL_CTX* ctx_ = nullptr;
+  int listen_fd_ = -1;
+  int port_ = 0;
+  std::atomic<bool> stopping_{false};
+  std::thread acceptor_;
+  std::mutex mu_;
+  std::vector<int> open_fds_;
+  std::vector<std::thread> workers_;
+  std::atomic<uint64_t> served_{0};
+  std::atomic<uint64_t> accepted_{0};
+};
+
+// Self-signed certificate for `host` (DNS name or IP literal) -- fakes only.
+Status generate_self_signed(const std::string& host, std::string* cert_pem,
+                            std::string* key_pem);
+
+const char* http_reason(int status);
+
+}  // namespace ksa

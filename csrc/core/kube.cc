@@ -1,0 +1,443 @@
+#include "kube.h"
+
+#include <cctype>
+#include <fstream>
+#include <sstream>
+
+#include "goutil.h"
+#include "json.h"
+#include "sigv4.h"  // aws_uri_encode for path segments
+
+namespace ksa {
+
+// ---------------------------------------------------------------------------------------
+// Token providers
+
+FileTokenProvider::FileTokenProvider(std::string path, std::shared_ptr<Clock> clock, Nanos refresh)
+    : path_(std::move(path)), clock_(std::move(clock)), refresh_(refresh) {}
+
+Result<std::string> FileTokenProvider::token() {
+  std::lock_guard<std::mutex> lk(mu_);
+  Nanos now = clock_->now();
+  if (have_ && now - read_at_ < refresh_) return Result<std::string>::Ok(cached_);
+  std::ifstream f(path_);
+  if (!f) {
+    if (have_) return Result<std::string>::Ok(cached_);  // keep the last good token
+    return Result<std::string>::Err(Status::Err("open " + path_ + ": no such file or directory"));
+  }
+  std::stringstream ss;
+  ss << f.rdbuf();
+  std::string t = ss.str();
+  while (!t.empty() && (t.back() == '\n' || t.back() == '\r' || t.back() == ' ')) t.pop_back();
+  cached_ = t;
+  have_ = true;
+  read_at_ = now;
+  return Result<std::string>::Ok(cached_);
+}
+
+// ---------------------------------------------------------------------------------------
+// Object helpers
+
+Result<ScaleObject> parse_scale_object(const std::string& json, bool absent_is_zero) {
+  auto j = json_parse(json);
+  if (!j.ok()) return Result<ScaleObject>::Err(j.status);
+  ScaleObject o;
+  o.raw = json;
+  const JsonValue* rv = j.value.path({"metadata", "resourceVersion"});
+  if (rv && rv->is_string()) o.resource_version = rv->str;
+  const JsonValue* r = j.value.path({"spec", "replicas"});
+  if (r && r->type != JsonValue::Type::Null) {
+    int64_t v;
+    if (!r->as_int64(&v)) return Result<ScaleObject>::Err(Status::Err("spec.replicas is not an integer"));
+    o.has_replicas = true;
+    o.replicas = go_int32(v);
+  } else if (absent_is_zero) {
+    o.has_replicas = true;
+    o.replicas = 0;
+  }
+  return Result<ScaleObject>::Ok(std::move(o));
+}
+
+Result<std::string> set_spec_replicas(const std::string& raw, int32_t replicas) {
+  auto j = json_parse(raw);
+  if (!j.ok()) return Result<std::string>::Err(j.status);
+  if (!j.value.is_object()) return Result<std::string>::Err(Status::Err("object is not a JSON object"));
+  const std::string num = std::to_string(replicas);
+  const JsonValue* spec = j.value.get("spec");
+  if (spec && spec->is_object()) {
+    const JsonValue* r = spec->get("replicas");
+    if (r) return Result<std::string>::Ok(json_splice(raw, *r, num));
+    // insert as the first member of spec
+    std::string out = raw.substr(0, spec->begin + 1) + "\"replicas\":" + num +
+                      (spec->obj.empty() ? "" : ",") + raw.substr(spec->begin + 1);
+    return Result<std::string>::Ok(out);
+  }
+  std::string ins = "\"spec\":{\"replicas\":" + num + "}";
+  const JsonValue& root = j.value;
+  std::string out = raw.substr(0, root.begin + 1) + ins + (root.obj.empty() ? "" : ",") +
+                    raw.substr(root.begin + 1);
+  return Result<std::string>::Ok(out);
+}
+
+// ---------------------------------------------------------------------------------------
+// REST client
+
+KubeRestDeployments::KubeRestDeployments(KubeOptions opts) : opts_(std::move(opts)) {
+  auto u = parse_url(opts_.server);
+  if (!u.ok()) {
+    init_status_ = u.status;
+    return;
+  }
+  url_ = u.value;
+  http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
+}
+
+KubeStats KubeRestDeployments::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  KubeStats s = stats_;
+  if (http_) s.http = http_->stats();
+  return s;
+}
+
+std::string KubeRestDeployments::path_for(const std::string& name) const {
+  std::string base = url_.path;
+  while (!base.empty() && base.back() == '/') base.pop_back();
+  std::string p = base + "/apis/apps/v1/namespaces/" + aws_uri_encode(opts_.namespace_, false) +
+                  "/deployments/" + aws_uri_encode(name, false);
+  if (opts_.mode != ScaleMode::Deployment) p += "/scale";
+  return p;
+}
+
+namespace {
+
+// client-go's error text for a non-2xx response.
+std::string kube_error_message(const HttpResponse& resp, const std::string& verb,
+                               const std::string& name, const std::string& resource) {
+  auto j = json_parse(resp.body);
+  if (j.ok() && j.value.is_object()) {
+    const JsonValue* kind = j.value.get("kind");
+    const JsonValue* msg = j.value.get("message");
+    if (kind && kind->string_or("") == "Status" && msg && msg->is_string() && !msg->str.empty())
+      return msg->str;
+  }
+  std::string what = "(" + verb + " " + resource + " " + name + ")";
+  switch (resp.status) {
+    case 401: return "Unauthorized";
+    case 403: return "forbidden: User cannot " + verb + " resource " + what;
+    case 404: return "the server could not find the requested resource " + what;
+    case 409: return "the server reported a conflict " + what;
+    case 429: return "the server has received too many requests and has asked us to try again later " + what;
+    default: break;
+  }
+  if (resp.status >= 500) {
+    std::string body = resp.body.size() > 200 ? resp.body.substr(0, 200) : resp.body;
+    return "an error on the server (" + go_quote(body) +
+           ") has prevented the request from succeeding " + what;
+  }
+  return "the server responded with the status code " + std::to_string(resp.status) +
+         " but did not return more information " + what;
+}
+
+std::string base64(const std::string& in) {
+  static const char* tbl = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string out;
+  size_t i = 0;
+  while (i + 2 < in.size()) {
+    uint32_t v = (uint8_t(in[i]) << 16) | (uint8_t(in[i + 1]) << 8) | uint8_t(in[i + 2]);
+    out.push_back(tbl[v >> 18]);
+    out.push_back(tbl[(v >> 12) & 63]);
+    out.push_back(tbl[(v >> 6) & 63]);
+    out.push_back(tbl[v & 63]);
+    i += 3;
+  }
+  if (i + 1 == in.size()) {
+    uint32_t v = uint8_t(in[i]) << 16;
+    out.push_back(tbl[v >> 18]);
+    out.push_back(tbl[(v >> 12) & 63]);
+    out += "==";
+  } else if (i + 2 == in.size()) {
+    uint32_t v = (uint8_t(in[i]) << 16) | (uint8_t(in[i + 1]) << 8);
+    out.push_back(tbl[v >> 18]);
+    out.push_back(tbl[(v >> 12) & 63]);
+    out.push_back(tbl[(v >> 6) & 63]);
+    out.push_back('=');
+  }
+  return out;
+}
+
+}  // namespace
+
+Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest* req,
+                                       HttpResponse* resp, const std::string& name) {
+  req->headers.emplace_back("Accept", "application/json, */*");
+  if (opts_.token) {
+    auto t = opts_.token->token();
+    if (!t.ok()) return t.status;
+    if (!t.value.empty()) req->headers.emplace_back("Authorization", "Bearer " + t.value);
+  } else if (!opts_.basic_user.empty()) {
+    req->headers.emplace_back("Authorization",
+                              "Basic " + base64(opts_.basic_user + ":" + opts_.basic_password));
+  }
+  Status s = http_->round_trip(*req, resp);
+  if (!s.ok()) {
+    std::string m = req->method;
+    std::string verb = m.substr(0, 1) + std::string(m.begin() + 1, m.end());
+    for (size_t i = 1; i < verb.size(); ++i) verb[i] = static_cast<char>(std::tolower(verb[i]));
+    return Status::Err(verb + " \"" + url_.origin() + req->target + "\": " + s.message());
+  }
+  if (resp->status < 200 || resp->status >= 300) {
+    const std::string resource = "deployments.apps";
+    std::lock_guard<std::mutex> lk(mu_);
+    if (resp->status == 409) stats_.conflicts++;
+    return Status::Err(kube_error_message(*resp, verb_desc, name, resource), resp->status);
+  }
+  return Status::OK();
+}
+
+Result<ScaleObject> KubeRestDeployments::get(const std::string& name) {
+  if (!init_status_.ok()) return Result<ScaleObject>::Err(init_status_);
+  if (name.empty()) return Result<ScaleObject>::Err(Status::Err("resource name may not be empty"));
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.gets++;
+  }
+  HttpRequest req;
+  req.method = "GET";
+  req.target = path_for(name);
+  HttpResponse resp;
+  Status s = do_request("get", &req, &resp, name);
+  if (!s.ok()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.errors++;
+    return Result<ScaleObject>::Err(s);
+  }
+  auto o = parse_scale_object(resp.body, opts_.mode != ScaleMode::Deployment);
+  if (!o.ok()) return Result<ScaleObject>::Err(o.status);
+  return o;
+}
+
+Status KubeRestDeployments::update(const std::string& name, const ScaleObject& fetched,
+                                   int32_t replicas) {
+  if (!init_status_.ok()) return init_status_;
+  if (name.empty()) return Status::Err("resource name may not be empty");
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.updates++;
+  }
+  HttpRequest req;
+  req.target = path_for(name);
+  if (opts_.mode == ScaleMode::Patch) {
+    req.method = "PATCH";
+    req.headers.emplace_back("Content-Type", "application/merge-patch+json");
+    req.body = "{\"metadata\":{\"resourceVersion\":" + json_quote(fetched.resource_version) +
+               "},\"spec\":{\"replicas\":" + std::to_string(replicas) + "}}";
+  } else {
+    req.method = "PUT";
+    req.headers.emplace_back("Content-Type", "application/json");
+    auto body = set_spec_replicas(fetched.raw, replicas);
+    if (!body.ok()) return body.status;
+    req.body = std::move(body.value);
+  }
+  HttpResponse resp;
+  Status s = do_request("update", &req, &resp, name);
+  if (!s.ok()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.errors++;
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------
+// FakeDeployments
+
+FakeDeployments::FakeDeployments(std::string namespace_) : ns_(std::move(namespace_)) {}
+
+void FakeDeployments::add(const std::string& name, int32_t replicas) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Obj o;
+  o.replicas = replicas;
+  o.rv = ++rv_counter_;
+  objs_[name] = o;
+}
+
+void FakeDeployments::add_without_replicas(const std::string& name) {
+  std::lock_guard<std::mutex> lk(mu_);
+  Obj o;
+  o.has_replicas = false;
+  o.rv = ++rv_counter_;
+  objs_[name] = o;
+}
+
+Result<ScaleObject> FakeDeployments::get(const std::string& name) {
+  std::lock_guard<std::mutex> lk(mu_);
+  gets_++;
+  if (clock_) clock_->advance(latency_);
+  if (fail_get_ > 0) {
+    fail_get_--;
+    return Result<ScaleObject>::Err(Status::Err(fail_get_msg_, 500));
+  }
+  auto it = objs_.find(name);
+  if (it == objs_.end())
+    return Result<ScaleObject>::Err(Status::Err("deployments.apps \"" + name + "\" not found", 404));
+  ScaleObject o;
+  o.has_replicas = it->second.has_replicas;
+  o.replicas = it->second.replicas;
+  o.resource_version = std::to_string(it->second.rv);
+  if (conflict_ > 0) {
+    conflict_--;
+    it->second.rv = ++rv_counter_;  // a concurrent writer (e.g. the deployment controller)
+  }
+  return Result<ScaleObject>::Ok(o);
+}
+
+Status FakeDeployments::update(const std::string& name, const ScaleObject& fetched,
+                               int32_t replicas) {
+  std::lock_guard<std::mutex> lk(mu_);
+  updates_++;
+  if (clock_) clock_->advance(latency_);
+  if (fail_update_ > 0) {
+    fail_update_--;
+    return Status::Err(fail_update_msg_, 500);
+  }
+  auto it = objs_.find(name);
+  if (it == objs_.end()) return Status::Err("deployments.apps \"" + name + "\" not found", 404);
+  if (!fetched.resource_version.empty() && fetched.resource_version != std::to_string(it->second.rv))
+    return Status::Err("Operation cannot be fulfilled on deployments.apps \"" + name +
+                           "\": the object has been modified; please apply your changes to the "
+                           "latest version and try again",
+                       409);
+  it->second.has_replicas = true;
+  it->second.replicas = replicas;
+  it->second.rv = ++rv_counter_;
+  return Status::OK();
+}
+
+int32_t FakeDeployments::replicas(const std::string& name) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = objs_.find(name);
+  return it == objs_.end() ? -1 : it->second.replicas;
+}
+
+void FakeDeployments::set_replicas(const std::string& name, int32_t r) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& o = objs_[name];
+  o.has_replicas = true;
+  o.replicas = r;
+  o.rv = ++rv_counter_;
+}
+
+void FakeDeployments::set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call) {
+  std::lock_guard<std::mutex> lk(mu_);
+  clock_ = std::move(clock);
+  latency_ = per_call;
+}
+
+void FakeDeployments::fail_next_get(int n, std::string message) {
+  std::lock_guard<std::mutex> lk(mu_);
+  fail_get_ = n;
+  fail_get_msg_ = std::move(message);
+}
+
+void FakeDeployments::fail_next_update(int n, std::string message) {
+  std::lock_guard<std::mutex> lk(mu_);
+  fail_update_ = n;
+  fail_update_msg_ = std::move(message);
+}
+
+void FakeDeployments::conflict_next(int n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  conflict_ = n;
+}
+
+uint64_t FakeDeployments::gets() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return gets_;
+}
+
+uint64_t FakeDeployments::updates() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return updates_;
+}
+
+// ---------------------------------------------------------------------------------------
+// PodAutoScaler
+
+PodAutoScaler::PodAutoScaler(std::shared_ptr<DeploymentApi> api, std::string deployment,
+                             std::string ns, int64_t max, int64_t min, int64_t scale_up_pods,
+                             int64_t scale_down_pods, std::shared_ptr<Logger> log,
+                             std::shared_ptr<Clock> clock)
+    : api_(std::move(api)),
+      deployment_(std::move(deployment)),
+      ns_(std::move(ns)),
+      max_(max),
+      min_(min),
+      up_(scale_up_pods),
+      down_(scale_down_pods),
+      log_(std::move(log)),
+      clock_(std::move(clock)) {}
+
+Status PodAutoScaler::scale_up(ScaleSpan* span) {
+  Nanos t0 = clock_->now();
+  auto d = api_->get(deployment_);
+  Nanos t1 = clock_->now();
+  if (span) span->get_ns = t1 - t0;
+  if (!d.ok()) return d.status.wrap("Failed to get deployment from kube server, no scale up occurred");
+  if (!d.value.has_replicas)  // the reference dereferences a nil pointer here (scale.go:60)
+    return Status::Err("deployment has no spec.replicas")
+        .wrap("Failed to get deployment from kube server, no scale up occurred");
+  const int32_t cur = d.value.replicas;
+  if (span) {
+    span->read = true;
+    span->before = span->after = cur;
+  }
+  const int32_t max32 = go_int32(max_);
+  if (cur >= max32) {
+    log_->info("More than max pods running. No scale up. Replicas: " + std::to_string(cur));
+    return Status::OK();
+  }
+  int32_t next = wrap_add32(cur, go_int32(up_));
+  if (next > max32) next = max32;
+  Status s = api_->update(deployment_, d.value, next);
+  if (span) {
+    span->update_ns = clock_->now() - t1;
+    span->wrote = s.ok();
+    if (s.ok()) span->after = next;
+  }
+  if (!s.ok()) return s.wrap("Failed to scale up");
+  log_->info("Scale up successful. Replicas: " + std::to_string(next));
+  return Status::OK();
+}
+
+Status PodAutoScaler::scale_down(ScaleSpan* span) {
+  Nanos t0 = clock_->now();
+  auto d = api_->get(deployment_);
+  Nanos t1 = clock_->now();
+  if (span) span->get_ns = t1 - t0;
+  if (!d.ok()) return d.status.wrap("Failed to get deployment from kube server, no scale down occurred");
+  if (!d.value.has_replicas)
+    return Status::Err("deployment has no spec.replicas")
+        .wrap("Failed to get deployment from kube server, no scale down occurred");
+  const int32_t cur = d.value.replicas;
+  if (span) {
+    span->read = true;
+    span->before = span->after = cur;
+  }
+  const int32_t min32 = go_int32(min_);
+  if (cur <= min32) {
+    log_->info("Less than min pods running. No scale down. Replicas: " + std::to_string(cur));
+    return Status::OK();
+  }
+  int32_t next = wrap_sub32(cur, go_int32(down_));
+  if (next < min32) next = min32;
+  Status s = api_->update(deployment_, d.value, next);
+  if (span) {
+    span->update_ns = clock_->now() - t1;
+    span->wrote = s.ok();
+    if (s.ok()) span->after = next;
+  }
+  if (!s.ok()) return s.wrap("Failed to scale down");
+  log_->info("Scale down successful. Replicas: " + std::to_string(next));
+  return Status::OK();
+}
+
+}  // namespace ksa

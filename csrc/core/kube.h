@@ -1,0 +1,199 @@
+// Replica actuator: Kubernetes Deployment scaling.
+//
+// Reference: /root/reference/scale/scale.go. PodAutoScaler reads the Deployment, computes the
+// clamped next replica count and writes it back (full-object GET + PUT through client-go,
+// scale.go:54-107). Here:
+//   * DeploymentApi       -- the injectable seam (the reference's typedappv1.DeploymentInterface,
+//                            scale.go:22); `get` returns the replica count plus the opaque object
+//                            that `update` writes back (optimistic concurrency via
+//                            metadata.resourceVersion, exactly like client-go's Update).
+//   * KubeRestDeployments -- REST client: ScaleMode::Deployment reproduces the reference's
+//                            GET/PUT of the whole apps/v1 Deployment; ScaleMode::Scale (the
+//                            default, per BASELINE.json) uses the autoscaling/v1 /scale
+//                            subresource (smaller payloads, narrower RBAC); ScaleMode::Patch
+//                            sends a JSON merge patch with a resourceVersion precondition.
+//   * FakeDeployments     -- in-memory object tracker (the fake clientset the reference tests
+//                            use, scale_test.go:85-115) with latency and fault injection.
+//   * PodAutoScaler       -- ScaleUp/ScaleDown with the reference's int32 clamp arithmetic and
+//                            log messages; a no-op at a bound returns OK (scale.go:62-65,89-92).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "clock.h"
+#include "http.h"
+#include "log.h"
+#include "status.h"
+
+namespace ksa {
+
+struct ScaleObject {
+  bool has_replicas = false;
+  int32_t replicas = 0;
+  std::string resource_version;
+  std::string raw;  // object as fetched (JSON); empty for in-memory fakes
+};
+
+class DeploymentApi {
+ public:
+  virtual ~DeploymentApi() = default;
+  virtual Result<ScaleObject> get(const std::string& name) = 0;
+  // Writes `fetched` back with spec.replicas = replicas.
+  virtual Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) = 0;
+};
+
+class TokenProvider {
+ public:
+  virtual ~TokenProvider() = default;
+  virtual Result<std::string> token() = 0;
+};
+
+class StaticTokenProvider final : public TokenProvider {
+ public:
+  explicit StaticTokenProvider(std::string t) : t_(std::move(t)) {}
+  Result<std::string> token() override { return Result<std::string>::Ok(t_); }
+
+ private:
+  std::string t_;
+};
+
+// Bound service-account tokens rotate (~1 h lifetime); client-go re-reads the projected
+// token file periodically. Re-read every `refresh` (default 60 s) using `clock`.
+class FileTokenProvider final : public TokenProvider {
+ public:
+  FileTokenProvider(std::string path, std::shared_ptr<Clock> clock, Nanos refresh = 60 * kSecond);
+  Result<std::string> token() override;
+
+ private:
+  std::string path_;
+  std::shared_ptr<Clock> clock_;
+  Nanos refresh_;
+  std::mutex mu_;
+  bool have_ = false;
+  Nanos read_at_ = 0;
+  std::string cached_;
+};
+
+enum class ScaleMode { Deployment, Scale, Patch };
+
+struct KubeOptions {
+  std::string server;  // https://host:port
+  std::string namespace_ = "default";
+  ScaleMode mode = ScaleMode::Scale;
+  TlsOptions tls;
+  std::shared_ptr<TokenProvider> token;  // bearer token (may be null)
+  std::string basic_user, basic_password;  // legacy kubeconfig basic auth
+  Nanos timeout = 30 * kSecond;
+};
+
+struct KubeStats {
+  uint64_t gets = 0;
+  uint64_t updates = 0;
+  uint64_t errors = 0;
+  uint64_t conflicts = 0;
+  HttpClientStats http;
+};
+
+class KubeRestDeployments final : public DeploymentApi {
+ public:
+  explicit KubeRestDeployments(KubeOptions opts);
+  Result<ScaleObject> get(const std::string& name) override;
+  Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override;
+  KubeStats stats() const;
+  std::string path_for(const std::string& name) const;
+
+ private:
+  Status do_request(const std::string& verb_desc, HttpRequest* req, HttpResponse* resp,
+                    const std::string& name);
+
+  KubeOptions opts_;
+  Status init_status_;
+  Url url_;
+  std::unique_ptr<HttpClient> http_;
+  mutable std::mutex mu_;
+  KubeStats stats_;
+};
+
+// Parses a Deployment or Scale object (JSON) into a ScaleObject. `absent_is_zero` is true for
+// autoscaling/v1 Scale, whose spec.replicas is omitempty (absent means 0).
+Result<ScaleObject> parse_scale_object(const std::string& json, bool absent_is_zero);
+// Returns `raw` with spec.replicas set to `replicas` (inserted when absent).
+Result<std::string> set_spec_replicas(const std::string& raw, int32_t replicas);
+
+// In-memory object tracker (client-go fake clientset equivalent).
+class FakeDeployments final : public DeploymentApi {
+ public:
+  explicit FakeDeployments(std::string namespace_ = "namespace");
+  void add(const std::string& name, int32_t replicas);
+  void add_without_replicas(const std::string& name);
+  Result<ScaleObject> get(const std::string& name) override;
+  Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override;
+
+  int32_t replicas(const std::string& name) const;  // -1 if absent
+  void set_replicas(const std::string& name, int32_t r);  // out-of-band edit (kubectl scale)
+  void set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call);
+  void fail_next_get(int n, std::string message);
+  void fail_next_update(int n, std::string message);
+  // Simulates a concurrent writer: bump resourceVersion right after each of the next n GETs,
+  // so the following update conflicts (409).
+  void conflict_next(int n);
+  uint64_t gets() const;
+  uint64_t updates() const;
+
+ private:
+  struct Obj {
+    bool has_replicas = true;
+    int32_t replicas = 0;
+    uint64_t rv = 1;
+  };
+  mutable std::mutex mu_;
+  std::string ns_;
+  std::map<std::string, Obj> objs_;
+  std::shared_ptr<VirtualClock> clock_;
+  Nanos latency_ = 0;
+  int fail_get_ = 0, fail_update_ = 0, conflict_ = 0;
+  std::string fail_get_msg_, fail_update_msg_;
+  uint64_t gets_ = 0, updates_ = 0;
+  uint64_t rv_counter_ = 1000;
+};
+
+// Per-call timing of one ScaleUp/ScaleDown (for poll->patch latency spans).
+struct ScaleSpan {
+  Nanos get_ns = 0;
+  Nanos update_ns = 0;
+  bool read = false;   // the GET succeeded and carried a replica count
+  bool wrote = false;
+  int32_t before = 0;
+  int32_t after = 0;
+};
+
+class PodAutoScaler {
+ public:
+  PodAutoScaler(std::shared_ptr<DeploymentApi> api, std::string deployment, std::string ns,
+                int64_t max, int64_t min, int64_t scale_up_pods, int64_t scale_down_pods,
+                std::shared_ptr<Logger> log, std::shared_ptr<Clock> clock);
+  Status scale_up(ScaleSpan* span = nullptr);    // scale.go:54-79
+  Status scale_down(ScaleSpan* span = nullptr);  // scale.go:81-107
+
+  std::shared_ptr<DeploymentApi> api() const { return api_; }
+  const std::string& deployment() const { return deployment_; }
+  const std::string& namespace_() const { return ns_; }
+  int64_t max() const { return max_; }
+  int64_t min() const { return min_; }
+  int64_t scale_up_pods() const { return up_; }
+  int64_t scale_down_pods() const { return down_; }
+  void set_max(int64_t m) { max_ = m; }
+
+ private:
+  std::shared_ptr<DeploymentApi> api_;
+  std::string deployment_, ns_;
+  int64_t max_, min_, up_, down_;
+  std::shared_ptr<Logger> log_;
+  std::shared_ptr<Clock> clock_;
+};
+
+}  // namespace ksa

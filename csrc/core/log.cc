@@ -1,0 +1,141 @@
+#include "log.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <unistd.h>
+
+#include "goutil.h"
+#include "json.h"
+
+namespace ksa {
+
+const char* level_name(Level l) {
+  switch (l) {
+    case Level::Panic: return "panic";
+    case Level::Fatal: return "fatal";
+    case Level::Error: return "error";
+    case Level::Warn: return "warning";
+    case Level::Info: return "info";
+    case Level::Debug: return "debug";
+    case Level::Trace: return "trace";
+  }
+  return "unknown";
+}
+
+bool parse_level(const std::string& s, Level* out) {
+  std::string l = s;
+  std::transform(l.begin(), l.end(), l.begin(), ::tolower);
+  static const std::pair<const char*, Level> table[] = {
+      {"panic", Level::Panic}, {"fatal", Level::Fatal}, {"error", Level::Error},
+      {"warn", Level::Warn},   {"warning", Level::Warn}, {"info", Level::Info},
+      {"debug", Level::Debug}, {"trace", Level::Trace}};
+  for (auto& [name, lvl] : table) {
+    if (l == name) {
+      *out = lvl;
+      return true;
+    }
+  }
+  return false;
+}
+
+bool logrus_needs_quoting(const std::string& s) {
+  for (unsigned char ch : s) {
+    bool ok = (ch >= 'a' && ch <= 'z') || (ch >= 'A' && ch <= 'Z') || (ch >= '0' && ch <= '9') ||
+              ch == '-' || ch == '.' || ch == '_' || ch == '/' || ch == '@' || ch == '^' ||
+              ch == '+';
+    if (!ok) return true;
+  }
+  return false;
+}
+
+Logger::Logger() : shared_(std::make_shared<Shared>()) {
+  shared_->sink = [](const std::string& line) {
+    std::string l = line;
+    l.push_back('\n');
+    ssize_t r = ::write(2, l.data(), l.size());
+    (void)r;
+  };
+  shared_->time = [] {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+  };
+}
+
+std::shared_ptr<Logger> Logger::default_logger() {
+  static std::shared_ptr<Logger> l = std::make_shared<Logger>();
+  return l;
+}
+
+void Logger::set_sink(Sink s) {
+  std::lock_guard<std::mutex> lk(shared_->mu);
+  shared_->sink = std::move(s);
+}
+
+void Logger::set_time_source(TimeSource t) {
+  std::lock_guard<std::mutex> lk(shared_->mu);
+  shared_->time = std::move(t);
+}
+
+std::shared_ptr<Logger> Logger::with_fields(const Fields& extra) const {
+  auto l = std::make_shared<Logger>(*this);  // shares sink/time (shared_ptr copy)
+  for (auto& kv : extra) l->base_.push_back(kv);
+  return l;
+}
+
+std::string Logger::format(Level l, const std::string& msg, const Fields& fields,
+                           int64_t unix_ns) const {
+  Fields data = base_;
+  data.insert(data.end(), fields.begin(), fields.end());
+  std::stable_sort(data.begin(), data.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::string out;
+  if (format_ == LogFormat::Json) {
+    // encoding/json marshals the map with sorted keys; time/level/msg sort among them.
+    Fields all = data;
+    all.emplace_back("level", level_name(l));
+    all.emplace_back("msg", msg);
+    all.emplace_back("time", rfc3339_utc(unix_ns));
+    std::stable_sort(all.begin(), all.end(),
+                     [](const auto& a, const auto& b) { return a.first < b.first; });
+    out.push_back('{');
+    bool first = true;
+    for (auto& kv : all) {
+      if (!first) out.push_back(',');
+      first = false;
+      out += json_quote(kv.first);
+      out.push_back(':');
+      out += json_quote(kv.second);
+    }
+    out.push_back('}');
+    return out;
+  }
+  auto append = [&](const std::string& k, const std::string& v) {
+    if (!out.empty()) out.push_back(' ');
+    out += k;
+    out.push_back('=');
+    out += logrus_needs_quoting(v) ? go_quote(v) : v;
+  };
+  append("time", rfc3339_utc(unix_ns));
+  append("level", level_name(l));
+  append("msg", msg);
+  for (auto& kv : data) append(kv.first, kv.second);
+  return out;
+}
+
+void Logger::log(Level l, const std::string& msg, const Fields& fields) {
+  if (!enabled(l)) return;
+  Sink sink;
+  int64_t ts;
+  {
+    std::lock_guard<std::mutex> lk(shared_->mu);
+    ts = shared_->time();
+    sink = shared_->sink;
+  }
+  std::string line = format(l, msg, fields, ts);
+  std::lock_guard<std::mutex> lk(shared_->mu);  // one line at a time across threads
+  sink(line);
+}
+
+}  // namespace ksa

@@ -1,0 +1,74 @@
+// logrus-compatible structured logger.
+//
+// The reference logs through the logrus package-level logger with default settings
+// (text formatter, stderr, Info level; /root/reference/main.go:13, scale/scale.go:9). Off a
+// TTY each line is
+//   time="2024-01-01T00:00:00Z" level=info msg="Found 3 messages in the queue"
+// This formatter reproduces that layout (fixed keys time/level/msg, then the remaining
+// fields sorted by key, values quoted with Go %q only when they contain characters outside
+// [A-Za-z0-9-._/@^+]) so log-based parity diffs against the reference work. A JSON
+// formatter (logrus.JSONFormatter layout) is offered as an extension.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace ksa {
+
+enum class Level : int { Panic = 0, Fatal = 1, Error = 2, Warn = 3, Info = 4, Debug = 5, Trace = 6 };
+
+const char* level_name(Level l);  // "panic", ..., "warning", "info", ...
+bool parse_level(const std::string& s, Level* out);
+
+using Fields = std::vector<std::pair<std::string, std::string>>;
+
+enum class LogFormat { Text, Json };
+
+class Logger {
+ public:
+  using Sink = std::function<void(const std::string& line)>;
+  using TimeSource = std::function<int64_t()>;  // unix nanos
+
+  Logger();
+  static std::shared_ptr<Logger> default_logger();
+
+  void set_level(Level l) { level_ = l; }
+  Level level() const { return level_; }
+  void set_format(LogFormat f) { format_ = f; }
+  // Replaces the output (default: stderr). The sink receives the line without '\n'.
+  void set_sink(Sink s);
+  void set_time_source(TimeSource t);
+  // Fields appended to every entry of this logger (e.g. queue=... in multi-queue mode).
+  void set_base_fields(Fields f) { base_ = std::move(f); }
+  std::shared_ptr<Logger> with_fields(const Fields& extra) const;
+
+  bool enabled(Level l) const { return static_cast<int>(l) <= static_cast<int>(level_); }
+  void log(Level l, const std::string& msg, const Fields& fields = {});
+  void info(const std::string& msg) { log(Level::Info, msg); }
+  void error(const std::string& msg) { log(Level::Error, msg); }
+  void warn(const std::string& msg) { log(Level::Warn, msg); }
+  void debug(const std::string& msg) { log(Level::Debug, msg); }
+
+  // Exposed for tests.
+  std::string format(Level l, const std::string& msg, const Fields& fields, int64_t unix_ns) const;
+
+ private:
+  struct Shared {
+    std::mutex mu;
+    Sink sink;
+    TimeSource time;
+  };
+  Level level_ = Level::Info;
+  LogFormat format_ = LogFormat::Text;
+  Fields base_;
+  std::shared_ptr<Shared> shared_;
+};
+
+// logrus TextFormatter.needsQuoting
+bool logrus_needs_quoting(const std::string& s);
+
+}  // namespace ksa

@@ -1,0 +1,244 @@
+#include "runner.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+
+namespace ksa {
+
+const char* action_name(Action a) {
+  switch (a) {
+    case Action::None: return "none";
+    case Action::CoolDown: return "cooldown";
+    case Action::Scaled: return "scaled";
+    case Action::NoopAtBound: return "noop";
+    case Action::Failed: return "failed";
+  }
+  return "?";
+}
+
+namespace {
+
+// last + cool with saturation (Go's Time.Add drops the monotonic reading on overflow; a
+// saturated sum preserves the comparison outcome).
+Nanos sat_add(Nanos a, Nanos b) {
+  if (b > 0 && a > std::numeric_limits<Nanos>::max() - b) return std::numeric_limits<Nanos>::max();
+  if (b < 0 && a < std::numeric_limits<Nanos>::min() - b) return std::numeric_limits<Nanos>::min();
+  return a + b;
+}
+
+}  // namespace
+
+Runner::Runner(LoopConfig cfg, std::shared_ptr<SqsClient> sqs, std::shared_ptr<PodAutoScaler> scaler,
+               std::shared_ptr<Clock> clock, std::shared_ptr<Logger> log)
+    : cfg_(cfg),
+      sqs_(std::move(sqs)),
+      scaler_(std::move(scaler)),
+      clock_(std::move(clock)),
+      log_(std::move(log)) {
+  lat_ring_.reserve(1024);
+}
+
+void Runner::arm() {
+  last_up_ = clock_->now();
+  last_down_ = clock_->now();
+}
+
+IterationRecord Runner::step(StopFlag* stop) {
+  IterationRecord rec;
+  // main.go:41 -- sleep BEFORE the poll.
+  if (!clock_->sleep(cfg_.poll_period, stop)) {
+    rec.stopped = true;
+    return rec;
+  }
+  rec.index = ++index_;
+  const Nanos t0 = clock_->now();
+  rec.t_poll = t0;
+
+  // main.go:43-47
+  auto depth = sqs_->num_messages();
+  Nanos t1 = clock_->now();
+  rec.depth_ns = t1 - t0;
+  if (!depth.ok()) {
+    rec.error = depth.status.message();
+    log_->error("Failed to get SQS messages: " + depth.status.message());
+    rec.total_ns = clock_->now() - t0;
+    record(rec);
+    return rec;
+  }
+  const int64_t n = depth.value;
+  rec.depth_ok = true;
+  rec.depth = n;
+  log_->info("Found " + std::to_string(n) + " messages in the queue");  // main.go:49
+
+  auto finish = [&]() -> IterationRecord& {
+    rec.total_ns = clock_->now() - t0;
+    record(rec);
+    return rec;
+  };
+
+  // main.go:51-63
+  if (n >= cfg_.scale_up_messages) {
+    if (sat_add(last_up_, cfg_.scale_up_cool_down) > clock_->now()) {
+      log_->info("Waiting for cool down, skipping scale up ");  // trailing space: main.go:53
+      rec.up = Action::CoolDown;
+      return finish();
+    }
+    ScaleSpan span;
+    Status s = scaler_->scale_up(&span);
+    rec.get_ns += span.get_ns;
+    rec.update_ns += span.update_ns;
+    if (span.read) {
+      rec.replicas_before = span.before;
+      rec.replicas_after = span.after;
+    }
+    if (!s.ok()) {
+      rec.error = s.message();
+      log_->error("Failed scaling up: " + s.message());
+      rec.up = Action::Failed;
+      return finish();
+    }
+    last_up_ = clock_->now();  // main.go:62 -- also after a no-op at max
+    rec.up = span.wrote ? Action::Scaled : Action::NoopAtBound;
+    if (span.wrote) rec.patch_latency_ns = clock_->now() - t0;
+  }
+
+  // main.go:65-77
+  if (n <= cfg_.scale_down_messages) {
+    if (sat_add(last_down_, cfg_.scale_down_cool_down) > clock_->now()) {
+      log_->info("Waiting for cool down, skipping scale down");
+      rec.down = Action::CoolDown;
+      return finish();
+    }
+    ScaleSpan span;
+    Status s = scaler_->scale_down(&span);
+    rec.get_ns += span.get_ns;
+    rec.update_ns += span.update_ns;
+    if (span.read) {
+      if (rec.replicas_before < 0) rec.replicas_before = span.before;
+      rec.replicas_after = span.after;
+    }
+    if (!s.ok()) {
+      rec.error = s.message();
+      log_->error("Failed scaling down: " + s.message());
+      rec.down = Action::Failed;
+      return finish();
+    }
+    last_down_ = clock_->now();  // main.go:76
+    rec.down = span.wrote ? Action::Scaled : Action::NoopAtBound;
+    if (span.wrote) rec.patch_latency_ns = clock_->now() - t0;
+  }
+  return finish();
+}
+
+void Runner::record(const IterationRecord& r) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.polls++;
+    if (!r.depth_ok) stats_.depth_errors++;
+    else stats_.last_depth = r.depth;
+    switch (r.up) {
+      case Action::Scaled: stats_.scale_ups++; break;
+      case Action::NoopAtBound: stats_.noop_ups++; break;
+      case Action::CoolDown: stats_.cooldown_skips_up++; break;
+      case Action::Failed: stats_.failed_ups++; break;
+      default: break;
+    }
+    switch (r.down) {
+      case Action::Scaled: stats_.scale_downs++; break;
+      case Action::NoopAtBound: stats_.noop_downs++; break;
+      case Action::CoolDown: stats_.cooldown_skips_down++; break;
+      case Action::Failed: stats_.failed_downs++; break;
+      default: break;
+    }
+    if (r.replicas_after >= 0) stats_.last_replicas = r.replicas_after;
+    if (r.patch_latency_ns >= 0) {
+      stats_.latency_samples++;
+      if (lat_ring_.size() < kLatRing) {
+        lat_ring_.push_back(r.patch_latency_ns);
+      } else {
+        lat_ring_[lat_pos_] = r.patch_latency_ns;
+        lat_pos_ = (lat_pos_ + 1) % kLatRing;
+      }
+    }
+  }
+  if (observer_) observer_(r);
+}
+
+void Runner::run(StopFlag* stop, int64_t max_iterations) {
+  arm();
+  int64_t done = 0;
+  while (!(stop && stop->stopped())) {
+    if (max_iterations > 0 && done >= max_iterations) break;
+    IterationRecord r = step(stop);
+    if (r.stopped) break;
+    ++done;
+  }
+}
+
+RunnerStats Runner::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+std::vector<Nanos> Runner::latencies() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (lat_ring_.size() < kLatRing) return lat_ring_;
+  std::vector<Nanos> out;
+  out.reserve(kLatRing);
+  out.insert(out.end(), lat_ring_.begin() + static_cast<long>(lat_pos_), lat_ring_.end());
+  out.insert(out.end(), lat_ring_.begin(), lat_ring_.begin() + static_cast<long>(lat_pos_));
+  return out;
+}
+
+void Runner::clear_latencies() {
+  std::lock_guard<std::mutex> lk(mu_);
+  lat_ring_.clear();
+  lat_pos_ = 0;
+}
+
+// ---------------------------------------------------------------------------------------
+
+void Supervisor::start(int64_t max_iterations) {
+  std::lock_guard<std::mutex> lk(mu_);
+  running_ = runners_.size();
+  for (auto& r : runners_) {
+    threads_.emplace_back([this, r, max_iterations] {
+      r->run(&stop_, max_iterations);
+      std::lock_guard<std::mutex> g(mu_);
+      --running_;
+      cv_.notify_all();
+    });
+  }
+}
+
+bool Supervisor::wait(Nanos timeout) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (timeout <= 0) {
+    cv_.wait(lk, [&] { return running_ == 0; });
+    return true;
+  }
+  return cv_.wait_for(lk, std::chrono::nanoseconds(timeout), [&] { return running_ == 0; });
+}
+
+void Supervisor::join() {
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+Supervisor::~Supervisor() {
+  stop();
+  join();
+}
+
+Nanos percentile(std::vector<Nanos> v, double p) {
+  if (v.empty()) return -1;
+  std::sort(v.begin(), v.end());
+  double rank = std::ceil(p / 100.0 * static_cast<double>(v.size()));
+  size_t idx = rank < 1 ? 0 : static_cast<size_t>(rank) - 1;
+  if (idx >= v.size()) idx = v.size() - 1;
+  return v[idx];
+}
+
+}  // namespace ksa

@@ -1,0 +1,153 @@
+// The control loop and its multi-queue supervisor.
+//
+// Runner::step() is one iteration of the reference's `Run` loop (/root/reference/main.go:40-78):
+//   sleep(poll) -> depth := NumMessages() -> scale-up gate -> scale-down gate
+// with the exact decision semantics catalogued in SURVEY.md §3.3:
+//   * timers armed at Run() entry (main.go:37-38) -- Runner::arm();
+//   * inclusive thresholds (main.go:51,65);
+//   * proceed iff now >= last + cool-down (`After` is strict, main.go:52,66), `now` re-read at
+//     every comparison and again when the timer is refreshed (main.go:62,76);
+//   * a cool-down skip or a failed scale-up `continue`s, so the scale-down check is skipped in
+//     that iteration (main.go:54,59);
+//   * the timer is refreshed after a successful call even when it was a no-op at a bound,
+//     and NOT refreshed after a failure (main.go:57-62,71-76).
+// Each step returns an IterationRecord, which is what the decision-parity harness compares
+// against the reference-semantics oracle, and carries the poll->patch latency span (the
+// BASELINE.json metric), measured from the end of the sleep to the end of the last write.
+//
+// Supervisor runs one Runner per tracked queue on its own thread (the reference tracks a
+// single queue per process); runners share nothing, so there is no cross-queue locking.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "clock.h"
+#include "kube.h"
+#include "log.h"
+#include "sqs.h"
+
+namespace ksa {
+
+struct LoopConfig {
+  Nanos poll_period = 5 * kSecond;            // --poll-period           main.go:83
+  Nanos scale_down_cool_down = 30 * kSecond;  // --scale-down-cool-down  main.go:84
+  Nanos scale_up_cool_down = 10 * kSecond;    // --scale-up-cool-down    main.go:85
+  int64_t scale_up_messages = 100;            // --scale-up-messages     main.go:86
+  int64_t scale_down_messages = 10;           // --scale-down-messages   main.go:87
+};
+
+enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };
+const char* action_name(Action a);
+
+struct IterationRecord {
+  uint64_t index = 0;     // 1-based poll number
+  bool stopped = false;   // the sleep was interrupted by a stop request
+  Nanos t_poll = 0;       // clock time at the end of the sleep
+  bool depth_ok = false;
+  int64_t depth = 0;
+  Action up = Action::None;
+  Action down = Action::None;
+  int32_t replicas_before = -1;  // as read by the last GET of the iteration (-1: not read)
+  int32_t replicas_after = -1;
+  Nanos depth_ns = 0;          // SQS GetQueueAttributes round trip
+  Nanos get_ns = 0;            // Deployment GET(s)
+  Nanos update_ns = 0;         // Deployment PUT/PATCH(es)
+  Nanos total_ns = 0;          // end of sleep -> end of iteration
+  Nanos patch_latency_ns = -1; // end of sleep -> end of last successful write (-1: no write)
+  std::string error;
+};
+
+struct RunnerStats {
+  uint64_t polls = 0;
+  uint64_t depth_errors = 0;
+  uint64_t scale_ups = 0;
+  uint64_t scale_downs = 0;
+  uint64_t noop_ups = 0;
+  uint64_t noop_downs = 0;
+  uint64_t cooldown_skips_up = 0;
+  uint64_t cooldown_skips_down = 0;
+  uint64_t failed_ups = 0;
+  uint64_t failed_downs = 0;
+  int64_t last_depth = 0;
+  int32_t last_replicas = -1;
+  uint64_t latency_samples = 0;
+};
+
+class Runner {
+ public:
+  Runner(LoopConfig cfg, std::shared_ptr<SqsClient> sqs, std::shared_ptr<PodAutoScaler> scaler,
+         std::shared_ptr<Clock> clock, std::shared_ptr<Logger> log);
+
+  // main.go:37-38: lastScaleUpTime = lastScaleDownTime = time.Now().
+  void arm();
+  // One loop iteration; `stop` may interrupt the sleep.
+  IterationRecord step(StopFlag* stop = nullptr);
+  // The reference's Run(): arm(), then step() until stopped (or max_iterations > 0 reached).
+  void run(StopFlag* stop, int64_t max_iterations = -1);
+
+  RunnerStats stats() const;
+  // Recent poll->patch latencies (ns), oldest first; bounded ring.
+  std::vector<Nanos> latencies() const;
+  void clear_latencies();
+  // Optional per-iteration observer (metrics export, tests). Called on the runner thread.
+  void set_observer(std::function<void(const IterationRecord&)> f) { observer_ = std::move(f); }
+  const LoopConfig& config() const { return cfg_; }
+  std::shared_ptr<SqsClient> sqs() const { return sqs_; }
+  std::shared_ptr<PodAutoScaler> scaler() const { return scaler_; }
+  Nanos last_scale_up() const { return last_up_; }
+  Nanos last_scale_down() const { return last_down_; }
+
+ private:
+  void record(const IterationRecord& r);
+
+  LoopConfig cfg_;
+  std::shared_ptr<SqsClient> sqs_;
+  std::shared_ptr<PodAutoScaler> scaler_;
+  std::shared_ptr<Clock> clock_;
+  std::shared_ptr<Logger> log_;
+  Nanos last_up_ = 0, last_down_ = 0;
+  uint64_t index_ = 0;
+  std::function<void(const IterationRecord&)> observer_;
+
+  mutable std::mutex mu_;
+  RunnerStats stats_;
+  std::vector<Nanos> lat_ring_;
+  size_t lat_pos_ = 0;
+  static constexpr size_t kLatRing = 1 << 16;
+};
+
+class Supervisor {
+ public:
+  void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
+  // Starts one thread per runner; each arms its timers then loops.
+  void start(int64_t max_iterations = -1);
+  void stop() { stop_.request_stop(); }
+  bool stopped() const { return stop_.stopped(); }
+  // Waits up to `timeout` (<= 0: forever); true when every runner thread has exited.
+  bool wait(Nanos timeout);
+  void join();
+  size_t size() const { return runners_.size(); }
+  std::shared_ptr<Runner> runner(size_t i) const { return runners_.at(i); }
+  StopFlag* stop_flag() { return &stop_; }
+  ~Supervisor();
+
+ private:
+  std::vector<std::shared_ptr<Runner>> runners_;
+  std::vector<std::thread> threads_;
+  StopFlag stop_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  size_t running_ = 0;
+};
+
+// Percentile (nearest-rank on a sorted copy), p in [0, 100].
+Nanos percentile(std::vector<Nanos> v, double p);
+
+}  // namespace ksa

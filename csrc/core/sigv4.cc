@@ -1,0 +1,311 @@
+#include "sigv4.h"
+
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
+
+#include <algorithm>
+#include <cctype>
+
+#include "goutil.h"
+
+namespace ksa {
+
+std::string hex_encode(const std::string& raw) {
+  static const char* hex = "0123456789abcdef";
+  std::string out;
+  out.reserve(raw.size() * 2);
+  for (unsigned char c : raw) {
+    out.push_back(hex[c >> 4]);
+    out.push_back(hex[c & 0xF]);
+  }
+  return out;
+}
+
+std::string sha256_hex(const std::string& data) {
+  unsigned char md[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  EVP_Digest(data.data(), data.size(), md, &len, EVP_sha256(), nullptr);
+  return hex_encode(std::string(reinterpret_cast<char*>(md), len));
+}
+
+std::string hmac_sha256(const std::string& key, const std::string& data) {
+  unsigned char md[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  HMAC(EVP_sha256(), key.data(), static_cast<int>(key.size()),
+       reinterpret_cast<const unsigned char*>(data.data()), data.size(), md, &len);
+  return std::string(reinterpret_cast<char*>(md), len);
+}
+
+std::string aws_uri_encode(const std::string& s, bool keep_slash) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string out;
+  out.reserve(s.size() * 3 / 2);
+  for (unsigned char c : s) {
+    if ((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '-' ||
+        c == '_' || c == '.' || c == '~' || (keep_slash && c == '/')) {
+      out.push_back(static_cast<char>(c));
+    } else {
+      out.push_back('%');
+      out.push_back(hex[c >> 4]);
+      out.push_back(hex[c & 0xF]);
+    }
+  }
+  return out;
+}
+
+std::string url_decode(const std::string& s, bool plus_is_space) {
+  auto hv = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  std::string out;
+  out.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    char c = s[i];
+    if (c == '%') {
+      int a = (i + 1 < s.size()) ? hv(s[i + 1]) : -1;
+      int b = (i + 2 < s.size()) ? hv(s[i + 2]) : -1;
+      if (a >= 0 && b >= 0) {
+        out.push_back(static_cast<char>((a << 4) | b));
+        i += 2;
+        continue;
+      }
+      out.push_back(c);
+    } else if (c == '+' && plus_is_space) {
+      out.push_back(' ');
+    } else {
+      out.push_back(c);
+    }
+  }
+  return out;
+}
+
+std::vector<std::pair<std::string, std::string>> parse_query(const std::string& q) {
+  std::vector<std::pair<std::string, std::string>> out;
+  size_t i = 0;
+  while (i <= q.size()) {
+    size_t amp = q.find('&', i);
+    if (amp == std::string::npos) amp = q.size();
+    std::string part = q.substr(i, amp - i);
+    if (!part.empty()) {
+      size_t eq = part.find('=');
+      if (eq == std::string::npos) {
+        out.emplace_back(url_decode(part, true), "");
+      } else {
+        out.emplace_back(url_decode(part.substr(0, eq), true),
+                         url_decode(part.substr(eq + 1), true));
+      }
+    }
+    i = amp + 1;
+  }
+  return out;
+}
+
+Result<Credentials> CachedCredentials::get(int64_t unix_now_ns) {
+  std::lock_guard<std::mutex> lk(mu_);
+  bool fresh = have_ && (cached_.expires_unix_ns == 0 ||
+                         unix_now_ns + window_ < cached_.expires_unix_ns);
+  if (fresh) return Result<Credentials>::Ok(cached_);
+  auto r = provider_->retrieve();
+  if (!r.ok()) {
+    have_ = false;
+    return r;
+  }
+  if (!r.value.valid()) {
+    have_ = false;
+    return Result<Credentials>::Err(Status::Err(
+        "NoCredentialProviders: no valid providers in chain"));
+  }
+  cached_ = r.value;
+  have_ = true;
+  return r;
+}
+
+void CachedCredentials::invalidate() {
+  std::lock_guard<std::mutex> lk(mu_);
+  have_ = false;
+}
+
+namespace {
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+// Trim and collapse runs of spaces (SigV4 "Trimall").
+std::string trimall(const std::string& v) {
+  std::string out;
+  bool space = false;
+  for (char c : v) {
+    if (c == ' ' || c == '\t') {
+      space = true;
+      continue;
+    }
+    if (space && !out.empty()) out.push_back(' ');
+    space = false;
+    out.push_back(c);
+  }
+  return out;
+}
+
+bool ignored_header(const std::string& lname) {
+  return lname == "authorization" || lname == "user-agent" || lname == "x-amzn-trace-id" ||
+         lname == "content-length" || lname == "connection" || lname == "expect";
+}
+
+}  // namespace
+
+CanonicalParts sigv4_canonical(const std::string& method, const std::string& path,
+                               const std::string& raw_query, const Headers& headers,
+                               const std::vector<std::string>* only_headers,
+                               const std::string& payload_hash) {
+  // Canonical URI: the on-the-wire path, encoded once more (non-S3 services).
+  std::string uri = path.empty() ? "/" : aws_uri_encode(path, true);
+
+  // Canonical query: decode, sort by key then value, re-encode strictly.
+  auto params = parse_query(raw_query);
+  std::sort(params.begin(), params.end());
+  std::string cq;
+  for (size_t i = 0; i < params.size(); ++i) {
+    if (i) cq.push_back('&');
+    cq += aws_uri_encode(params[i].first, false);
+    cq.push_back('=');
+    cq += aws_uri_encode(params[i].second, false);
+  }
+
+  // Canonical headers: lowercase names; repeated headers joined with ','.
+  std::vector<std::pair<std::string, std::string>> hs;
+  for (auto& [k, v] : headers) {
+    std::string lk = lower(k);
+    if (only_headers) {
+      if (std::find(only_headers->begin(), only_headers->end(), lk) == only_headers->end())
+        continue;
+    } else if (ignored_header(lk)) {
+      continue;
+    }
+    bool merged = false;
+    for (auto& h : hs) {
+      if (h.first == lk) {
+        h.second += "," + trimall(v);
+        merged = true;
+        break;
+      }
+    }
+    if (!merged) hs.emplace_back(lk, trimall(v));
+  }
+  std::sort(hs.begin(), hs.end(),
+            [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::string ch, sh;
+  for (size_t i = 0; i < hs.size(); ++i) {
+    ch += hs[i].first + ":" + hs[i].second + "\n";
+    if (i) sh.push_back(';');
+    sh += hs[i].first;
+  }
+  CanonicalParts parts;
+  parts.signed_headers = sh;
+  parts.canonical_request =
+      method + "\n" + uri + "\n" + cq + "\n" + ch + "\n" + sh + "\n" + payload_hash;
+  return parts;
+}
+
+std::string SigV4Signer::signing_key(const std::string& secret, const std::string& date) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!key_.empty() && key_secret_ == secret && key_date_ == date) return key_;
+  std::string k = hmac_sha256("AWS4" + secret, date);
+  k = hmac_sha256(k, region_);
+  k = hmac_sha256(k, service_);
+  k = hmac_sha256(k, "aws4_request");
+  key_secret_ = secret;
+  key_date_ = date;
+  key_ = k;
+  return k;
+}
+
+void SigV4Signer::sign(const Credentials& creds, int64_t unix_ns, const std::string& method,
+                       const std::string& path, const std::string& raw_query, Headers* headers,
+                       const std::string& body, SignDebug* debug) {
+  const std::string amzdate = amz_date(unix_ns);
+  const std::string date = amzdate.substr(0, 8);
+  headers->emplace_back("X-Amz-Date", amzdate);
+  if (!creds.session_token.empty()) headers->emplace_back("X-Amz-Security-Token", creds.session_token);
+
+  CanonicalParts parts =
+      sigv4_canonical(method, path, raw_query, *headers, nullptr, sha256_hex(body));
+  const std::string scope = date + "/" + region_ + "/" + service_ + "/aws4_request";
+  const std::string sts =
+      "AWS4-HMAC-SHA256\n" + amzdate + "\n" + scope + "\n" + sha256_hex(parts.canonical_request);
+  const std::string sig = hex_encode(hmac_sha256(signing_key(creds.secret_access_key, date), sts));
+  headers->emplace_back("Authorization", "AWS4-HMAC-SHA256 Credential=" + creds.access_key_id +
+                                             "/" + scope + ", SignedHeaders=" +
+                                             parts.signed_headers + ", Signature=" + sig);
+  if (debug) {
+    debug->canonical_request = parts.canonical_request;
+    debug->string_to_sign = sts;
+    debug->signed_headers = parts.signed_headers;
+    debug->signature = sig;
+    debug->scope = scope;
+  }
+}
+
+Status sigv4_verify(const std::string& method, const std::string& path,
+                    const std::string& raw_query, const Headers& headers,
+                    const std::string& body, const std::string& expected_access_key,
+                    const std::string& secret, const std::string& region,
+                    const std::string& service) {
+  std::string auth, amzdate;
+  for (auto& [k, v] : headers) {
+    std::string lk = lower(k);
+    if (lk == "authorization") auth = v;
+    if (lk == "x-amz-date") amzdate = v;
+  }
+  if (auth.empty()) return Status::Err("MissingAuthenticationToken", 403);
+  const std::string prefix = "AWS4-HMAC-SHA256 ";
+  if (auth.compare(0, prefix.size(), prefix) != 0)
+    return Status::Err("IncompleteSignature: unsupported algorithm", 403);
+  auto field = [&](const std::string& name) -> std::string {
+    size_t p = auth.find(name + "=");
+    if (p == std::string::npos) return "";
+    p += name.size() + 1;
+    size_t e = auth.find(',', p);
+    std::string v = auth.substr(p, e == std::string::npos ? std::string::npos : e - p);
+    while (!v.empty() && v.back() == ' ') v.pop_back();
+    return v;
+  };
+  std::string cred = field("Credential"), sh = field("SignedHeaders"), sig = field("Signature");
+  if (cred.empty() || sh.empty() || sig.empty() || amzdate.size() != 16)
+    return Status::Err("IncompleteSignature", 403);
+  size_t slash = cred.find('/');
+  std::string akid = cred.substr(0, slash);
+  std::string scope = slash == std::string::npos ? "" : cred.substr(slash + 1);
+  if (akid != expected_access_key) return Status::Err("InvalidClientTokenId", 403);
+  const std::string date = amzdate.substr(0, 8);
+  const std::string want_scope = date + "/" + region + "/" + service + "/aws4_request";
+  if (scope != want_scope)
+    return Status::Err("SignatureDoesNotMatch: credential scope " + scope + " != " + want_scope,
+                       403);
+  std::vector<std::string> only;
+  size_t i = 0;
+  while (i <= sh.size()) {
+    size_t semi = sh.find(';', i);
+    if (semi == std::string::npos) semi = sh.size();
+    only.push_back(sh.substr(i, semi - i));
+    i = semi + 1;
+  }
+  if (std::find(only.begin(), only.end(), "host") == only.end())
+    return Status::Err("SignatureDoesNotMatch: host not signed", 403);
+  CanonicalParts parts = sigv4_canonical(method, path, raw_query, headers, &only, sha256_hex(body));
+  std::string k = hmac_sha256("AWS4" + secret, date);
+  k = hmac_sha256(k, region);
+  k = hmac_sha256(k, service);
+  k = hmac_sha256(k, "aws4_request");
+  const std::string sts = "AWS4-HMAC-SHA256\n" + amzdate + "\n" + want_scope + "\n" +
+                          sha256_hex(parts.canonical_request);
+  const std::string want = hex_encode(hmac_sha256(k, sts));
+  if (want != sig) return Status::Err("SignatureDoesNotMatch", 403);
+  return Status::OK();
+}
+
+}  // namespace ksa

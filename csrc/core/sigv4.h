@@ -1,0 +1,127 @@
+// AWS Signature Version 4 and credential caching.
+//
+// The reference delegates request signing and the credential chain to aws-sdk-go v1.35.35
+// (session.NewSession + sqs.New, /root/reference/sqs/sqs.go:36; go.mod:6). Without the SDK
+// this module implements the published SigV4 algorithm directly:
+//   canonical request -> string to sign -> HMAC-SHA256 chain -> Authorization header.
+// The derived signing key only changes once per UTC day (and per secret), so it is cached;
+// steady-state signing costs two SHA-256 digests and one HMAC.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "status.h"
+
+namespace ksa {
+
+using Headers = std::vector<std::pair<std::string, std::string>>;
+
+std::string sha256_hex(const std::string& data);
+std::string hmac_sha256(const std::string& key, const std::string& data);  // raw bytes
+std::string hex_encode(const std::string& raw);
+
+// RFC 3986 percent-encoding of everything outside [A-Za-z0-9-_.~]; '/' kept when
+// `keep_slash` (canonical URI) -- this equals Go's url.QueryEscape with '+' -> "%20".
+std::string aws_uri_encode(const std::string& s, bool keep_slash);
+std::string url_decode(const std::string& s, bool plus_is_space);
+// Form/query parsing of "a=1&b=2" into decoded pairs (order preserved).
+std::vector<std::pair<std::string, std::string>> parse_query(const std::string& q);
+
+struct Credentials {
+  std::string access_key_id;
+  std::string secret_access_key;
+  std::string session_token;
+  int64_t expires_unix_ns = 0;  // 0 = does not expire
+  std::string provider_name;
+  bool valid() const { return !access_key_id.empty() && !secret_access_key.empty(); }
+};
+
+// Credential source (env, shared file, web identity, ECS, IMDS ... live in Python; see
+// kube_sqs_autoscaler_amd/sqs/credentials.py). Native code only needs retrieve().
+class CredentialsProvider {
+ public:
+  virtual ~CredentialsProvider() = default;
+  virtual Result<Credentials> retrieve() = 0;
+};
+
+class StaticCredentialsProvider final : public CredentialsProvider {
+ public:
+  explicit StaticCredentialsProvider(Credentials c) : c_(std::move(c)) {}
+  Result<Credentials> retrieve() override { return Result<Credentials>::Ok(c_); }
+
+ private:
+  Credentials c_;
+};
+
+// aws.Credentials-style cache: retrieve() again only when the cached value is within
+// `expiry_window_ns` of its expiry (or was invalidated after a 403).
+class CachedCredentials {
+ public:
+  CachedCredentials(std::shared_ptr<CredentialsProvider> p, int64_t expiry_window_ns)
+      : provider_(std::move(p)), window_(expiry_window_ns) {}
+  Result<Credentials> get(int64_t unix_now_ns);
+  void invalidate();
+
+ private:
+  std::shared_ptr<CredentialsProvider> provider_;
+  int64_t window_;
+  std::mutex mu_;
+  bool have_ = false;
+  Credentials cached_;
+};
+
+struct SignDebug {
+  std::string canonical_request;
+  std::string string_to_sign;
+  std::string signed_headers;
+  std::string signature;
+  std::string scope;
+};
+
+class SigV4Signer {
+ public:
+  SigV4Signer(std::string region, std::string service)
+      : region_(std::move(region)), service_(std::move(service)) {}
+
+  // Signs in place: appends X-Amz-Date, X-Amz-Security-Token (session credentials) and
+  // Authorization to `headers`. `headers` must already contain Host. `raw_query` is the
+  // query string as sent (percent-encoded), `path` the path as sent.
+  void sign(const Credentials& creds, int64_t unix_ns, const std::string& method,
+            const std::string& path, const std::string& raw_query, Headers* headers,
+            const std::string& body, SignDebug* debug = nullptr);
+
+  // Derived key for (secret, yyyymmdd); cached per day.
+  std::string signing_key(const std::string& secret, const std::string& date);
+
+  const std::string& region() const { return region_; }
+  const std::string& service() const { return service_; }
+
+ private:
+  std::string region_, service_;
+  std::mutex mu_;
+  std::string key_secret_, key_date_, key_;
+};
+
+// Builds the canonical request pieces; shared with the fake server's verifier.
+struct CanonicalParts {
+  std::string canonical_request;
+  std::string signed_headers;
+};
+CanonicalParts sigv4_canonical(const std::string& method, const std::string& path,
+                               const std::string& raw_query, const Headers& headers,
+                               const std::vector<std::string>* only_headers,
+                               const std::string& payload_hash);
+
+// Server-side verification of an incoming request's Authorization header.
+Status sigv4_verify(const std::string& method, const std::string& path,
+                    const std::string& raw_query, const Headers& headers,
+                    const std::string& body, const std::string& expected_access_key,
+                    const std::string& secret, const std::string& region,
+                    const std::string& service);
+
+}  // namespace ksa

@@ -1,0 +1,308 @@
+#include "sqs.h"
+
+#include <algorithm>
+
+#include "goutil.h"
+#include "json.h"
+#include "xml.h"
+
+namespace ksa {
+
+const std::vector<std::string>& default_attribute_names() {
+  static const std::vector<std::string> names = {
+      "ApproximateNumberOfMessages",
+      "ApproximateNumberOfMessagesDelayed",
+      "ApproximateNumberOfMessagesNotVisible",
+  };
+  return names;
+}
+
+std::string aws_request_failure(const std::string& code, const std::string& message, int status,
+                                const std::string& request_id) {
+  return code + ": " + message + "\n\tstatus code: " + std::to_string(status) +
+         ", request id: " + request_id;
+}
+
+// ---------------------------------------------------------------------------------------
+// HttpSqsApi
+
+std::string HttpSqsApi::endpoint_for_region(const std::string& region) {
+  if (region.empty()) return "";
+  std::string suffix = "amazonaws.com";
+  if (region.rfind("cn-", 0) == 0) suffix = "amazonaws.com.cn";
+  return "https://sqs." + region + "." + suffix;
+}
+
+HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider> creds,
+                       std::shared_ptr<Clock> clock)
+    : opts_(std::move(opts)),
+      clock_(std::move(clock)),
+      creds_(std::move(creds), 5LL * 60 * kSecond),
+      signer_(opts_.region, "sqs") {
+  endpoint_ = opts_.endpoint.empty() ? endpoint_for_region(opts_.region) : opts_.endpoint;
+  if (opts_.region.empty()) {
+    // aws-sdk-go v1 validates the region before sending (request.ValidateEndpointHandler).
+    endpoint_status_ = Status::Err("MissingRegion: could not find region configuration");
+    return;
+  }
+  auto u = parse_url(endpoint_);
+  if (!u.ok()) {
+    endpoint_status_ = u.status;
+    return;
+  }
+  url_ = u.value;
+  http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
+}
+
+SqsApiStats HttpSqsApi::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  SqsApiStats s = stats_;
+  if (http_) s.http = http_->stats();
+  return s;
+}
+
+Nanos HttpSqsApi::retry_delay(int retry_count, bool throttle) {
+  // DefaultRetryer.RetryRules: 2^retryCount * jitter(minDelay), jitter(d) in [d, 2d),
+  // capped at jitter(maxDelay/2).
+  Nanos min_delay = throttle ? opts_.min_throttle_delay : opts_.min_retry_delay;
+  Nanos max_delay = opts_.max_retry_delay;
+  auto jitter = [&](Nanos d) -> Nanos {
+    if (d <= 0) return 0;
+    rng_ ^= rng_ << 13;
+    rng_ ^= rng_ >> 7;
+    rng_ ^= rng_ << 17;
+    return d + static_cast<Nanos>(rng_ % static_cast<uint64_t>(d));
+  };
+  if (retry_count >= 62) return jitter(max_delay / 2);
+  Nanos base = jitter(min_delay);
+  if (base > (max_delay >> retry_count)) return jitter(max_delay / 2);
+  Nanos d = base << retry_count;
+  return d > max_delay ? jitter(max_delay / 2) : d;
+}
+
+Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
+                                      const std::vector<std::string>& names, bool* retryable,
+                                      bool* throttle, bool* expired) {
+  *retryable = *throttle = *expired = false;
+  auto cr = creds_.get(clock_->unix_nanos());
+  if (!cr.ok()) return Result<AttrMap>::Err(cr.status);
+
+  HttpRequest req;
+  req.method = "POST";
+  req.target = url_.path.empty() ? "/" : url_.path;
+  req.headers.emplace_back("Host", url_.host_header());
+  if (opts_.protocol == SqsProtocol::Query) {
+    // url.Values.Encode(): keys sorted, QueryEscape'd.
+    std::vector<std::pair<std::string, std::string>> params;
+    params.emplace_back("Action", "GetQueueAttributes");
+    for (size_t i = 0; i < names.size(); ++i)
+      params.emplace_back("AttributeName." + std::to_string(i + 1), names[i]);
+    params.emplace_back("QueueUrl", queue_url);
+    params.emplace_back("Version", "2012-11-05");
+    std::stable_sort(params.begin(), params.end(),
+                     [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (size_t i = 0; i < params.size(); ++i) {
+      if (i) req.body.push_back('&');
+      req.body += aws_uri_encode(params[i].first, false) + "=" + aws_uri_encode(params[i].second, false);
+    }
+    req.headers.emplace_back("Content-Type", "application/x-www-form-urlencoded; charset=utf-8");
+  } else {
+    JsonValue body = JsonValue::make_object();
+    JsonValue arr;
+    arr.type = JsonValue::Type::Array;
+    for (auto& n : names) arr.arr.push_back(JsonValue::make_string(n));
+    body.set("AttributeNames", std::move(arr));
+    body.set("QueueUrl", JsonValue::make_string(queue_url));
+    req.body = json_serialize(body);
+    req.headers.emplace_back("Content-Type", "application/x-amz-json-1.0");
+    req.headers.emplace_back("X-Amz-Target", "AmazonSQS.GetQueueAttributes");
+  }
+  std::string path = req.target;
+  std::string query;
+  size_t q = path.find('?');
+  if (q != std::string::npos) {
+    query = path.substr(q + 1);
+    path = path.substr(0, q);
+  }
+  signer_.sign(cr.value, clock_->unix_nanos(), req.method, path, query, &req.headers, req.body);
+
+  HttpResponse resp;
+  Status s = http_->round_trip(req, &resp);
+  if (!s.ok()) {
+    *retryable = true;
+    return Result<AttrMap>::Err(Status::Err("RequestError: send request failed\ncaused by: Post \"" +
+                                            endpoint_ + req.target + "\": " + s.message()));
+  }
+  const std::string request_id = !resp.header("x-amzn-RequestId").empty()
+                                     ? resp.header("x-amzn-RequestId")
+                                     : resp.header("x-amz-request-id");
+  if (resp.status >= 300) {
+    std::string code, message, rid = request_id;
+    if (opts_.protocol == SqsProtocol::Query) {
+      bool found = false;
+      code = xml_first_text(resp.body, "Code", &found);
+      message = xml_first_text(resp.body, "Message", &found);
+      if (rid.empty()) rid = xml_first_text(resp.body, "RequestId", &found);
+    } else {
+      auto j = json_parse(resp.body);
+      if (j.ok()) {
+        const JsonValue* t = j.value.get("__type");
+        if (!t) t = j.value.get("code");
+        code = t ? t->string_or("") : "";
+        size_t hash = code.rfind('#');
+        if (hash != std::string::npos) code = code.substr(hash + 1);
+        const JsonValue* m = j.value.get("message");
+        if (!m) m = j.value.get("Message");
+        message = m ? m->string_or("") : "";
+      }
+      // Query-compatible error code, when the service provides one.
+      std::string qe = resp.header("x-amzn-query-error");
+      if (!qe.empty()) code = qe.substr(0, qe.find(';'));
+    }
+    if (code.empty()) code = resp.status >= 500 ? "InternalFailure" : "SerializationError";
+    static const char* throttle_codes[] = {
+        "Throttling", "ThrottlingException", "ThrottledException", "RequestThrottledException",
+        "TooManyRequestsException", "ProvisionedThroughputExceededException",
+        "TransactionInProgressException", "RequestLimitExceeded", "BandwidthLimitExceeded",
+        "LimitExceededException", "RequestThrottled", "SlowDown", "PriorRequestNotComplete",
+        "EC2ThrottledException", "AWS.SimpleQueueService.RequestThrottled"};
+    for (const char* tc : throttle_codes)
+      if (code == tc) *throttle = true;
+    if (code == "ExpiredToken" || code == "ExpiredTokenException" || code == "RequestExpired")
+      *expired = true;
+    *retryable = *throttle || *expired || resp.status >= 500 || resp.status == 429;
+    return Result<AttrMap>::Err(
+        Status::Err(aws_request_failure(code, message, resp.status, rid), resp.status));
+  }
+
+  AttrMap out;
+  if (opts_.protocol == SqsProtocol::Query) {
+    for (auto& [k, v] : xml_sqs_attributes(resp.body)) out[k] = v;
+  } else {
+    auto j = json_parse(resp.body);
+    if (!j.ok())
+      return Result<AttrMap>::Err(Status::Err("SerializationError: failed decoding JSON RPC response\ncaused by: " +
+                                              j.status.message()));
+    const JsonValue* attrs = j.value.get("Attributes");
+    if (attrs && attrs->is_object())
+      for (auto& [k, v] : attrs->obj) out[k] = v.is_string() ? v.str : json_serialize(v);
+  }
+  return Result<AttrMap>::Ok(std::move(out));
+}
+
+Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
+                                                 const std::vector<std::string>& names) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.calls++;
+  }
+  if (!endpoint_status_.ok()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.errors++;
+    return Result<AttrMap>::Err(endpoint_status_);
+  }
+  Result<AttrMap> r;
+  for (int attempt = 0;; ++attempt) {
+    bool retryable, throttle, expired;
+    r = call_once(queue_url, names, &retryable, &throttle, &expired);
+    if (r.ok() || !retryable || attempt >= opts_.max_retries) break;
+    if (expired) creds_.invalidate();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.retries++;
+    }
+    clock_->sleep(retry_delay(attempt, throttle), nullptr);
+  }
+  if (!r.ok()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.errors++;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------
+// Fakes
+
+MockSqsApi::MockSqsApi(AttrMap initial) : attrs_(std::move(initial)) {}
+
+Result<AttrMap> MockSqsApi::get_queue_attributes(const std::string&,
+                                                 const std::vector<std::string>&) {
+  std::lock_guard<std::mutex> lk(mu_);
+  calls_++;
+  if (clock_) clock_->advance(latency_);
+  if (fail_n_ > 0) {
+    fail_n_--;
+    return Result<AttrMap>::Err(Status::Err(fail_msg_));
+  }
+  return Result<AttrMap>::Ok(attrs_);
+}
+
+void MockSqsApi::set_attributes(AttrMap attrs) {
+  std::lock_guard<std::mutex> lk(mu_);
+  attrs_ = std::move(attrs);
+}
+
+void MockSqsApi::set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call) {
+  std::lock_guard<std::mutex> lk(mu_);
+  clock_ = std::move(clock);
+  latency_ = per_call;
+}
+
+void MockSqsApi::fail_next(int n, std::string message) {
+  std::lock_guard<std::mutex> lk(mu_);
+  fail_n_ = n;
+  fail_msg_ = std::move(message);
+}
+
+uint64_t MockSqsApi::calls() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return calls_;
+}
+
+TraceSqsApi::TraceSqsApi(std::shared_ptr<Clock> clock,
+                         std::vector<std::pair<Nanos, AttrMap>> segments, Nanos per_call_latency)
+    : clock_(std::move(clock)), segments_(std::move(segments)), latency_(per_call_latency) {
+  std::stable_sort(segments_.begin(), segments_.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+}
+
+Result<AttrMap> TraceSqsApi::get_queue_attributes(const std::string&,
+                                                  const std::vector<std::string>&) {
+  // Sampled at call start, then the call "takes" latency_.
+  Nanos t = clock_->now();
+  AttrMap cur;
+  for (auto& seg : segments_) {
+    if (seg.first <= t) cur = seg.second;
+    else break;
+  }
+  if (latency_ > 0) clock_->sleep(latency_, nullptr);
+  return Result<AttrMap>::Ok(std::move(cur));
+}
+
+// ---------------------------------------------------------------------------------------
+// SqsClient
+
+SqsClient::SqsClient(std::shared_ptr<SqsApi> api, std::string queue_url,
+                     std::vector<std::string> attribute_names)
+    : api_(std::move(api)), queue_url_(std::move(queue_url)), names_(std::move(attribute_names)) {}
+
+Result<int64_t> SqsClient::num_messages() {
+  auto out = api_->get_queue_attributes(queue_url_, names_);
+  if (!out.ok()) return Result<int64_t>::Err(out.status.wrap("Failed to get messages in SQS"));
+  int64_t messages = 0;
+  for (const auto& attr : names_) {
+    auto it = out.value.find(attr);
+    if (it == out.value.end()) {
+      return Result<int64_t>::Err(
+          Status::Err("attribute not present in GetQueueAttributes response")
+              .wrap("Failed to get '" + attr + "' number of messages in queue"));
+    }
+    auto n = go_atoi(it->second);
+    if (!n.ok())
+      return Result<int64_t>::Err(n.status.wrap("Failed to get '" + attr + "' number of messages in queue"));
+    messages = wrap_add64(messages, n.value);
+  }
+  return Result<int64_t>::Ok(messages);
+}
+
+}  // namespace ksa

@@ -1,0 +1,150 @@
+// Queue-depth source: SQS GetQueueAttributes + attribute summing.
+//
+// Mirrors the reference's two-level design (/root/reference/sqs/sqs.go):
+//   * SqsApi       -- the injectable service seam (the reference's `SQS` interface,
+//                     sqs.go:14-18); HttpSqsApi is the real client (Query or JSON protocol,
+//                     SigV4-signed, SDK-style retries), MockSqsApi/TraceSqsApi are fakes.
+//   * SqsClient    -- NumMessages(): request the configured attribute names and sum their
+//                     strconv.Atoi values (sqs.go:45-67), with the reference's error texts.
+// Deliberate deviation: a requested attribute that is absent from the
+// response is an error, not a nil-pointer panic (sqs.go:58).
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "clock.h"
+#include "http.h"
+#include "sigv4.h"
+#include "status.h"
+
+namespace ksa {
+
+using AttrMap = std::map<std::string, std::string>;
+
+// sqs.go:26-33
+const std::vector<std::string>& default_attribute_names();
+
+class SqsApi {
+ public:
+  virtual ~SqsApi() = default;
+  virtual Result<AttrMap> get_queue_attributes(const std::string& queue_url,
+                                               const std::vector<std::string>& names) = 0;
+};
+
+enum class SqsProtocol { Query, Json };
+
+struct SqsHttpOptions {
+  std::string region;
+  std::string endpoint;  // override (e.g. http://127.0.0.1:9324); empty = regional endpoint
+  SqsProtocol protocol = SqsProtocol::Query;
+  Nanos timeout = 30 * kSecond;
+  int max_retries = 3;  // aws-sdk-go v1 DefaultRetryer.NumMaxRetries
+  Nanos min_retry_delay = 30 * kMillisecond;
+  Nanos min_throttle_delay = 500 * kMillisecond;
+  Nanos max_retry_delay = 300 * kSecond;
+  TlsOptions tls;
+};
+
+struct SqsApiStats {
+  uint64_t calls = 0;
+  uint64_t retries = 0;
+  uint64_t errors = 0;
+  HttpClientStats http;
+};
+
+class HttpSqsApi final : public SqsApi {
+ public:
+  HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider> creds,
+             std::shared_ptr<Clock> clock);
+  Result<AttrMap> get_queue_attributes(const std::string& queue_url,
+                                       const std::vector<std::string>& names) override;
+  SqsApiStats stats() const;
+  // Regional endpoint aws-sdk-go would resolve for `region` ("" if region is empty).
+  static std::string endpoint_for_region(const std::string& region);
+  std::string endpoint() const { return endpoint_; }
+
+ private:
+  Result<AttrMap> call_once(const std::string& queue_url, const std::vector<std::string>& names,
+                            bool* retryable, bool* throttle, bool* expired);
+  Nanos retry_delay(int retry_count, bool throttle);
+
+  SqsHttpOptions opts_;
+  std::shared_ptr<Clock> clock_;
+  CachedCredentials creds_;
+  SigV4Signer signer_;
+  std::string endpoint_;
+  Status endpoint_status_;
+  Url url_;
+  std::unique_ptr<HttpClient> http_;
+  mutable std::mutex mu_;
+  SqsApiStats stats_;
+  uint64_t rng_ = 0x9E3779B97F4A7C15ULL;
+};
+
+// In-memory fake, the MockSQS of /root/reference/sqs/sqs_test.go:27-59: returns the stored
+// attribute map; set_attributes() is the SetQueueAttributes test hook. Optionally advances
+// a VirtualClock per call (API latency model) and injects failures.
+class MockSqsApi final : public SqsApi {
+ public:
+  explicit MockSqsApi(AttrMap initial = {});
+  Result<AttrMap> get_queue_attributes(const std::string& queue_url,
+                                       const std::vector<std::string>& names) override;
+  void set_attributes(AttrMap attrs);
+  void set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call);
+  // The next `n` calls fail with `message`.
+  void fail_next(int n, std::string message);
+  uint64_t calls() const;
+
+ private:
+  mutable std::mutex mu_;
+  AttrMap attrs_;
+  std::shared_ptr<VirtualClock> clock_;
+  Nanos latency_ = 0;
+  int fail_n_ = 0;
+  std::string fail_msg_;
+  uint64_t calls_ = 0;
+};
+
+// Time-driven fake: the attribute map is a piecewise-constant function of the clock
+// (segments sorted by start time). The decision-parity harness drives the reference's
+// synthetic traces through this.
+class TraceSqsApi final : public SqsApi {
+ public:
+  TraceSqsApi(std::shared_ptr<Clock> clock, std::vector<std::pair<Nanos, AttrMap>> segments,
+              Nanos per_call_latency);
+  Result<AttrMap> get_queue_attributes(const std::string& queue_url,
+                                       const std::vector<std::string>& names) override;
+
+ private:
+  std::shared_ptr<Clock> clock_;
+  std::vector<std::pair<Nanos, AttrMap>> segments_;
+  Nanos latency_;
+};
+
+class SqsClient {
+ public:
+  SqsClient(std::shared_ptr<SqsApi> api, std::string queue_url,
+            std::vector<std::string> attribute_names);
+  // sqs.go:45-67
+  Result<int64_t> num_messages();
+  const std::string& queue_url() const { return queue_url_; }
+  const std::vector<std::string>& attribute_names() const { return names_; }
+  std::shared_ptr<SqsApi> api() const { return api_; }
+
+ private:
+  std::shared_ptr<SqsApi> api_;
+  std::string queue_url_;
+  std::vector<std::string> names_;
+};
+
+// Formats an aws-sdk-go awserr.RequestFailure message.
+std::string aws_request_failure(const std::string& code, const std::string& message, int status,
+                                const std::string& request_id);
+
+}  // namespace ksa

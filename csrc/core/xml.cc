@@ -1,0 +1,167 @@
+#include "xml.h"
+
+#include <cstdlib>
+
+namespace ksa {
+
+namespace {
+
+void put_utf8(std::string* s, unsigned long cp) {
+  if (cp < 0x80) {
+    s->push_back(static_cast<char>(cp));
+  } else if (cp < 0x800) {
+    s->push_back(static_cast<char>(0xC0 | (cp >> 6)));
+    s->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else if (cp < 0x10000) {
+    s->push_back(static_cast<char>(0xE0 | (cp >> 12)));
+    s->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    s->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else {
+    s->push_back(static_cast<char>(0xF0 | (cp >> 18)));
+    s->push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+    s->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    s->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  }
+}
+
+// Finds the next start tag whose local name equals `tag` at or after `pos` (before `to`).
+// Returns the offset just past '>' of the start tag, or npos. *self_closing set for <x/>.
+size_t find_start(const std::string& doc, const std::string& tag, size_t pos, size_t to,
+                  bool* self_closing) {
+  while (true) {
+    size_t lt = doc.find('<', pos);
+    if (lt == std::string::npos || lt >= to) return std::string::npos;
+    size_t p = lt + 1;
+    if (p < doc.size() && (doc[p] == '/' || doc[p] == '?' || doc[p] == '!')) {
+      pos = p;
+      continue;
+    }
+    size_t name_end = p;
+    while (name_end < doc.size() && doc[name_end] != '>' && doc[name_end] != ' ' &&
+           doc[name_end] != '/' && doc[name_end] != '\t' && doc[name_end] != '\n' &&
+           doc[name_end] != '\r')
+      ++name_end;
+    std::string name = doc.substr(p, name_end - p);
+    size_t colon = name.find(':');
+    if (colon != std::string::npos) name = name.substr(colon + 1);
+    size_t gt = doc.find('>', name_end);
+    if (gt == std::string::npos) return std::string::npos;
+    if (name == tag) {
+      *self_closing = gt > 0 && doc[gt - 1] == '/';
+      return gt + 1;
+    }
+    pos = gt + 1;
+  }
+}
+
+size_t find_end(const std::string& doc, const std::string& tag, size_t pos, size_t to) {
+  while (true) {
+    size_t lt = doc.find("</", pos);
+    if (lt == std::string::npos || lt >= to) return std::string::npos;
+    size_t p = lt + 2;
+    size_t gt = doc.find('>', p);
+    if (gt == std::string::npos) return std::string::npos;
+    std::string name = doc.substr(p, gt - p);
+    while (!name.empty() && (name.back() == ' ' || name.back() == '\t')) name.pop_back();
+    size_t colon = name.find(':');
+    if (colon != std::string::npos) name = name.substr(colon + 1);
+    if (name == tag) return lt;
+    pos = gt + 1;
+  }
+}
+
+}  // namespace
+
+std::string xml_unescape(const std::string& s) {
+  std::string out;
+  out.reserve(s.size());
+  size_t i = 0;
+  while (i < s.size()) {
+    if (s[i] != '&') {
+      out.push_back(s[i++]);
+      continue;
+    }
+    size_t semi = s.find(';', i);
+    if (semi == std::string::npos || semi - i > 12) {
+      out.push_back(s[i++]);
+      continue;
+    }
+    std::string ent = s.substr(i + 1, semi - i - 1);
+    if (ent == "amp") out.push_back('&');
+    else if (ent == "lt") out.push_back('<');
+    else if (ent == "gt") out.push_back('>');
+    else if (ent == "quot") out.push_back('"');
+    else if (ent == "apos") out.push_back('\'');
+    else if (!ent.empty() && ent[0] == '#') {
+      unsigned long cp = (ent.size() > 1 && (ent[1] == 'x' || ent[1] == 'X'))
+                             ? std::strtoul(ent.c_str() + 2, nullptr, 16)
+                             : std::strtoul(ent.c_str() + 1, nullptr, 10);
+      put_utf8(&out, cp);
+    } else {
+      out.append(s, i, semi - i + 1);
+    }
+    i = semi + 1;
+  }
+  return out;
+}
+
+std::string xml_escape(const std::string& s) {
+  std::string out;
+  out.reserve(s.size());
+  for (char c : s) {
+    switch (c) {
+      case '&': out += "&amp;"; break;
+      case '<': out += "&lt;"; break;
+      case '>': out += "&gt;"; break;
+      case '"': out += "&quot;"; break;
+      case '\'': out += "&apos;"; break;
+      default: out.push_back(c);
+    }
+  }
+  return out;
+}
+
+std::string xml_first_text(const std::string& doc, const std::string& tag, bool* found,
+                           size_t from, size_t to) {
+  if (to > doc.size()) to = doc.size();
+  bool self_closing = false;
+  size_t start = find_start(doc, tag, from, to, &self_closing);
+  if (start == std::string::npos) {
+    if (found) *found = false;
+    return "";
+  }
+  if (found) *found = true;
+  if (self_closing) return "";
+  size_t end = find_end(doc, tag, start, to);
+  if (end == std::string::npos) end = to;
+  std::string raw = doc.substr(start, end - start);
+  // CDATA sections are passed through verbatim.
+  if (raw.compare(0, 9, "<![CDATA[") == 0 && raw.size() >= 12 &&
+      raw.compare(raw.size() - 3, 3, "]]>") == 0)
+    return raw.substr(9, raw.size() - 12);
+  return xml_unescape(raw);
+}
+
+std::vector<std::pair<std::string, std::string>> xml_sqs_attributes(const std::string& doc) {
+  std::vector<std::pair<std::string, std::string>> out;
+  size_t pos = 0;
+  while (true) {
+    bool sc = false;
+    size_t start = find_start(doc, "Attribute", pos, doc.size(), &sc);
+    if (start == std::string::npos) break;
+    if (sc) {
+      pos = start;
+      continue;
+    }
+    size_t end = find_end(doc, "Attribute", start, doc.size());
+    if (end == std::string::npos) break;
+    bool has_name = false, has_value = false;
+    std::string name = xml_first_text(doc, "Name", &has_name, start, end);
+    std::string value = xml_first_text(doc, "Value", &has_value, start, end);
+    if (has_name) out.emplace_back(name, value);
+    pos = end + 1;
+  }
+  return out;
+}
+
+}  // namespace ksa

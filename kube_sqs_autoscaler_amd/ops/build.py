@@ -1,0 +1,155 @@
+"""In-tree build of the native runtime and the gfx950 GPU probe.
+
+Artifacts (git-ignored, but they travel to the GPU box with the gpurun snapshot):
+
+* ``kube_sqs_autoscaler_amd/ops/_ksa_native<EXT_SUFFIX>`` -- pybind11 module linking the C++
+  core in ``csrc/core`` (control loop, SigV4, HTTP/TLS transport, SQS + Kubernetes clients,
+  fake endpoints) against OpenSSL.
+* ``kube_sqs_autoscaler_amd/ops/libksa_gpu.so`` -- ``hipcc --offload-arch=gfx950`` build of
+  ``csrc/hip/gpu_probe.hip`` (GPU inventory + HBM health check), loaded with ctypes.
+* ``build/native_tests[_asan|_tsan]`` -- host-only C++ test binaries (sanitizer builds).
+
+Objects are compiled in parallel and reused when neither the source nor any header under
+``csrc/`` changed, so an incremental rebuild after touching one file takes seconds.
+
+Usage: ``python -m kube_sqs_autoscaler_amd.ops.build [--no-hip] [--sanitizers]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+CSRC = ROOT / "csrc"
+OPS = Path(__file__).resolve().parent
+BUILD = ROOT / "build"
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+NATIVE_SO = OPS / f"_ksa_native{EXT_SUFFIX}"
+GPU_SO = OPS / "libksa_gpu.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+GPU_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+CXXFLAGS = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread"]
+LIBS = ["-lssl", "-lcrypto", "-pthread"]
+
+
+def _core_sources() -> list[Path]:
+    return sorted((CSRC / "core").glob("*.cc"))
+
+
+def _newest_header() -> float:
+    hs = list(CSRC.rglob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _stale(target: Path, deps: list[Path], header_mtime: float) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps) or header_mtime > t
+
+
+def _run(cmd: list[str]) -> None:
+    proc = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"command failed ({proc.returncode}): {' '.join(cmd)}\n{proc.stdout}{proc.stderr}")
+
+
+def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: int) -> list[Path]:
+    objdir = BUILD / f"obj-{variant}"
+    objdir.mkdir(parents=True, exist_ok=True)
+    hm = _newest_header()
+    todo, objs = [], []
+    for src in sources:
+        obj = objdir / (src.stem + ".o")
+        objs.append(obj)
+        if _stale(obj, [src], hm):
+            todo.append([CXX, *CXXFLAGS, *extra, "-c", str(src), "-o", str(obj)])
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for f in [ex.submit(_run, c) for c in todo]:
+                f.result()
+    return objs
+
+
+def build_native(jobs: int = 8, verbose: bool = True) -> Path:
+    """Builds the pybind11 extension in place; returns its path."""
+    import pybind11
+
+    py_inc = sysconfig.get_paths()["include"]
+    extra = ["-fvisibility=hidden"]
+    core = _compile_objects("release", extra, _core_sources(), jobs)
+    mod_src = CSRC / "bindings" / "module.cc"
+    mod_obj = BUILD / "obj-release" / "module.o"
+    if _stale(mod_obj, [mod_src], _newest_header()):
+        _run([CXX, *CXXFLAGS, *extra, f"-I{pybind11.get_include()}", f"-I{py_inc}", "-c", str(mod_src), "-o", str(mod_obj)])
+    deps = core + [mod_obj]
+    if _stale(NATIVE_SO, deps, 0.0):
+        tmp = NATIVE_SO.with_suffix(".tmp.so")
+        _run([CXX, "-shared", "-o", str(tmp), *map(str, deps), *LIBS])
+        os.replace(tmp, NATIVE_SO)
+        if verbose:
+            print(f"[build] linked {NATIVE_SO.relative_to(ROOT)}")
+    return NATIVE_SO
+
+
+def build_gpu_probe(verbose: bool = True) -> Path | None:
+    """Compiles the HIP probe for gfx950 (cross-compiles without a GPU)."""
+    src = CSRC / "hip" / "gpu_probe.hip"
+    if not Path(HIPCC).exists() and shutil.which("hipcc") is None:
+        raise RuntimeError("hipcc not found; cannot build the gfx950 GPU probe")
+    hipcc = HIPCC if Path(HIPCC).exists() else "hipcc"
+    if _stale(GPU_SO, [src], 0.0):
+        tmp = GPU_SO.with_suffix(".tmp.so")
+        _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", str(src), "-o", str(tmp)])
+        os.replace(tmp, GPU_SO)
+        if verbose:
+            print(f"[build] hipcc --offload-arch={GPU_ARCH} -> {GPU_SO.relative_to(ROOT)}")
+    return GPU_SO
+
+
+def build_native_tests(sanitizer: str | None = None, jobs: int = 8) -> Path:
+    """Host-only C++ unit-test binary; `sanitizer` in {None, 'asan', 'tsan'}."""
+    flags = {
+        None: ["-g"],
+        "asan": ["-g", "-O1", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+        "tsan": ["-g", "-O1", "-fsanitize=thread"],
+    }[sanitizer]
+    variant = sanitizer or "test"
+    srcs = _core_sources() + [CSRC / "tests" / "native_tests.cc"]
+    objs = _compile_objects(variant, flags, srcs, jobs)
+    out = BUILD / ("native_tests" + (f"_{sanitizer}" if sanitizer else ""))
+    if _stale(out, objs, 0.0):
+        _run([CXX, *flags, "-o", str(out), *map(str, objs), *LIBS])
+    return out
+
+
+def build_all(hip: bool = True, jobs: int = 8) -> dict:
+    out = {"native": str(build_native(jobs=jobs))}
+    if hip:
+        out["gpu_probe"] = str(build_gpu_probe())
+    return out
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--no-hip", action="store_true", help="skip the gfx950 probe")
+    ap.add_argument("--sanitizers", action="store_true", help="also build ASan/UBSan and TSan test binaries")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    args = ap.parse_args(argv)
+    print(build_all(hip=not args.no_hip, jobs=args.jobs))
+    if args.sanitizers:
+        for s in (None, "asan", "tsan"):
+            print(build_native_tests(s, jobs=args.jobs))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
