@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Headline benchmark: poll -> scale-patch p50 latency (ms) + decision parity.
+
+BASELINE.json names the metric "poll->scale-patch p50 latency (ms); decision parity vs ref on
+synthetic trace", reported at 1/2/4/8 concurrently tracked queues. The reference publishes no
+number (BASELINE.json ``published: {}``), so ``vs_baseline`` is null.
+
+One rank per GPU (``torch.distributed``; backend ``nccl`` = RCCL on ROCm when a GPU is present,
+``gloo`` otherwise). Each rank is one autoscaler process tracking ``--queues`` queues (default
+1) against its own localhost fake SQS + fake kube-apiserver, so the job tracks
+``N x queues`` queues in total (weak scaling). A "step" is one control-loop iteration on every
+tracked queue: SigV4-signed SQS GetQueueAttributes -> Deployment GET -> replica write (the trace
+alternates 200/0 messages, so every iteration scales). K timed steps are bracketed by a barrier
++ ``torch.cuda.synchronize()``; ``value`` is the p50 over every sample of every rank.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--queues Q] [--mode scale]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "poll→scale-patch p50 latency (ms); decision parity vs ref on synthetic trace"
+
+
+def _parity_summary() -> dict:
+    from kube_sqs_autoscaler_amd.models import parity, traces
+
+    out = {}
+    agree = total = 0
+    for sc in traces.baseline_scenarios():
+        r = parity.compare(sc)
+        out[sc.name] = f"{r.agree}/{r.polls}"
+        agree += r.agree
+        total += r.polls
+    out["fraction"] = agree / total if total else 1.0
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--queues", type=int, default=1, help="tracked queues per rank")
+    ap.add_argument("--mode", default="scale", choices=["scale", "deployment", "patch"])
+    ap.add_argument("--no-sweep", action="store_true", help="skip the 1/2/4/8-queue sweep (single rank only)")
+    args = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+    device = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("nccl" if use_cuda else "gloo")
+
+    def barrier_sync():
+        if world > 1:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+
+    from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, measure
+    from kube_sqs_autoscaler_amd.ops import native
+
+    native()  # build/load before timing
+    env = BenchEnv(args.queues, args.mode)
+    try:
+        if args.warmup:
+            env.run(args.warmup)
+        env.clear()
+        barrier_sync()
+        t0 = time.perf_counter()
+        env.run(args.steps)
+        barrier_sync()
+        wall = time.perf_counter() - t0
+        res = env.collect(args.steps, wall)
+    finally:
+        env.close()
+
+    samples = torch.tensor(sorted(res.samples), dtype=torch.int64, device=device)
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        gathered = [torch.empty_like(samples) for _ in range(world)]
+        dist.all_gather(gathered, samples)
+        samples = torch.cat(gathered)
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    all_ns = sorted(samples.cpu().tolist())
+    wall_max = float(wall_t.item())
+
+    def pct(v, p):
+        import math
+
+        k = max(1, math.ceil(p / 100.0 * len(v)))
+        return v[min(k, len(v)) - 1] / 1e6
+
+    out = None
+    if rank == 0:
+        p50 = pct(all_ns, 50)
+        extra = {
+            "p90_ms": round(pct(all_ns, 90), 4),
+            "p99_ms": round(pct(all_ns, 99), 4),
+            "samples": len(all_ns),
+            "tracked_queues": args.queues * world,
+            "scale_mode": args.mode,
+            "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
+            "signature_failures": res.signature_failures,
+            "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
+        }
+        if world == 1 and not args.no_sweep:
+            sweep = {}
+            for q in (1, 2, 4, 8):
+                r = measure(q, min(args.steps, 2000), min(args.warmup, 200), args.mode)
+                sweep[str(q)] = r.summary()["p50_ms"]
+            extra["p50_ms_by_tracked_queues"] = sweep
+            ref = measure(1, min(args.steps, 2000), min(args.warmup, 200), "deployment")
+            extra["reference_equivalent_p50_ms"] = ref.summary()["p50_ms"]
+        extra["decision_parity"] = _parity_summary()
+        out = {
+            "metric": METRIC,
+            "value": round(p50, 4),
+            "unit": "ms",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max * 1000.0 / args.steps, 5),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",  # control-plane service: no tensor compute (BASELINE.json north_star)
+            "data": "synthetic: 200/0 step trace served by localhost fake SQS + fake kube-apiserver (SigV4 + bearer auth verified)",
+            "config": {
+                "model": "kube-sqs-autoscaler control loop (single queue step trace 0->200->0, scale-up-messages=100 / scale-down-messages=10, min 1 / max 8)",
+                "global_batch": args.queues * world,
+                "seq_len": 1,
+                "parallelism": f"dp{world}",
+            },
+            "extra": extra,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

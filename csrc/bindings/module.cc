@@ -296,6 +296,15 @@ PYBIND11_MODULE(_ksa_native, m) {
                }
              });
            })
+      .def("set_sink_fd",
+           [](Logger& l, int fd) {
+             // Native fd sink (no GIL): one write(2) per line, like logrus on os.Stderr.
+             l.set_sink([fd](const std::string& line) {
+               std::string s = line + "\n";
+               ssize_t r = ::write(fd, s.data(), s.size());
+               (void)r;
+             });
+           })
       .def("set_time_source",
            [](Logger& l, std::shared_ptr<Clock> c) {
              l.set_time_source([c] { return c->unix_nanos(); });
@@ -671,6 +680,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_property_readonly("cert_pem", &FakeSqsServer::cert_pem)
       .def("set_attributes", &FakeSqsServer::set_attributes)
       .def("set_default_attributes", &FakeSqsServer::set_default_attributes)
+      .def("set_attribute_cycle", &FakeSqsServer::set_attribute_cycle)
       .def("inject", &FakeSqsServer::inject)
       .def("set_latency", &FakeSqsServer::set_latency)
       .def("drop_connections", &FakeSqsServer::drop_connections)

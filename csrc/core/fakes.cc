@@ -88,6 +88,15 @@ void FakeSqsServer::set_attributes(const std::string& queue_url, AttrMap attrs) 
   queues_[queue_url] = std::move(attrs);
 }
 
+void FakeSqsServer::set_attribute_cycle(const std::string& queue_url, std::vector<AttrMap> cycle) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (cycle.empty()) {
+    cycles_.erase(queue_url);
+    return;
+  }
+  cycles_[queue_url] = Cycle{std::move(cycle), 0};
+}
+
 void FakeSqsServer::set_default_attributes(AttrMap attrs) {
   std::lock_guard<std::mutex> lk(mu_);
   default_attrs_ = std::move(attrs);
@@ -201,8 +210,12 @@ void FakeSqsServer::handle(const HttpRequest& req, HttpResponse* resp) {
   AttrMap attrs;
   {
     std::lock_guard<std::mutex> lk(mu_);
+    auto cy = cycles_.find(queue_url);
     auto it = queues_.find(queue_url);
-    if (it != queues_.end()) attrs = it->second;
+    if (cy != cycles_.end()) {
+      attrs = cy->second.maps[cy->second.next];
+      cy->second.next = (cy->second.next + 1) % cy->second.maps.size();
+    } else if (it != queues_.end()) attrs = it->second;
     else if (!default_attrs_.empty()) attrs = default_attrs_;
     else {
       error(400, "AWS.SimpleQueueService.NonExistentQueue", "The specified queue does not exist for this wsdl version.");

@@ -45,6 +45,9 @@ class FakeSqsServer {
 
   void set_attributes(const std::string& queue_url, AttrMap attrs);
   void set_default_attributes(AttrMap attrs);  // for queues not set explicitly
+  // Successive GetQueueAttributes calls for `queue_url` return cycle[0], cycle[1], ... and wrap
+  // around (a step trace driven by call count; the latency benchmark's 200 <-> 0 trace).
+  void set_attribute_cycle(const std::string& queue_url, std::vector<AttrMap> cycle);
   void inject(int count, InjectedFault fault);
   void set_latency(Nanos per_request);
   void drop_connections();
@@ -63,6 +66,11 @@ class FakeSqsServer {
   std::string cert_pem_, key_pem_;
   mutable std::mutex mu_;
   std::map<std::string, AttrMap> queues_;
+  struct Cycle {
+    std::vector<AttrMap> maps;
+    size_t next = 0;
+  };
+  std::map<std::string, Cycle> cycles_;
   AttrMap default_attrs_;
   bool verify_ = false;
   std::string akid_, secret_, region_;

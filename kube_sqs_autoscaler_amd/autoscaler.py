@@ -1,0 +1,120 @@
+"""Component factories: configuration -> native control-loop objects.
+
+These are the constructors of the reference, rebuilt over the native runtime:
+
+* :func:`new_pod_autoscaler` -- ``scale.NewPodAutoScaler`` (/root/reference/scale/scale.go:31-52):
+  kube config from ``KUBE_CONFIG_PATH`` (in-cluster when empty), a REST client scoped to the
+  namespace, and the clamp parameters.
+* :func:`new_sqs_client` -- ``kubesqs.NewSqsClient`` (/root/reference/sqs/sqs.go:35-43): a
+  SigV4-signing SQS client for ``region`` over a persistent HTTPS connection, plus the
+  attribute list to sum.
+* :func:`new_runner` -- the state ``Run`` keeps (/root/reference/main.go:35-38): one
+  independent loop per tracked queue, with its own clients and timers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Mapping, Optional
+
+from .config import Config, TargetConfig
+from .kube.config import RestConfig, build_config_from_flags
+from .ops import native
+from .sqs.credentials import make_chain_provider
+from .utils.goflag import SECOND
+
+_SCALE_MODES = {"deployment": "Deployment", "scale": "Scale", "patch": "Patch"}
+
+
+def scale_mode(name: str):
+    return getattr(native().ScaleMode, _SCALE_MODES[name])
+
+
+def tls_options(rc: RestConfig):
+    nat = native()
+    t = nat.TlsOptions()
+    t.insecure_skip_verify = rc.insecure
+    t.ca_pem = rc.ca_pem
+    t.cert_pem = rc.cert_pem
+    t.key_pem = rc.key_pem
+    t.server_name = rc.server_name
+    return t
+
+
+def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", timeout_ns: int = 30 * SECOND, clock=None):
+    """The ``DeploymentInterface`` seam over REST (/root/reference/scale/scale.go:44)."""
+    nat = native()
+    o = nat.KubeOptions()
+    o.server = rc.host
+    o.namespace = namespace
+    o.mode = scale_mode(mode)
+    o.tls = tls_options(rc)
+    o.timeout_ns = timeout_ns
+    if rc.bearer_token_file:
+        o.token = nat.FileTokenProvider(rc.bearer_token_file, clock or nat.RealClock(), 60 * SECOND)
+    elif rc.bearer_token:
+        o.token = nat.StaticTokenProvider(rc.bearer_token)
+    o.basic_user = rc.username
+    o.basic_password = rc.password
+    return nat.KubeRestDeployments(o)
+
+
+def new_pod_autoscaler(target: TargetConfig, api, logger, clock):
+    nat = native()
+    return nat.PodAutoScaler(api, target.deployment, target.namespace, target.max_pods, target.min_pods,
+                             target.scale_up_pods, target.scale_down_pods, logger, clock)
+
+
+def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query", timeout_ns: int = 30 * SECOND,
+                credentials=None, environ: Optional[Mapping[str, str]] = None, tls=None):
+    nat = native()
+    o = nat.SqsHttpOptions()
+    o.region = region
+    o.endpoint = endpoint
+    o.protocol = nat.SqsProtocol.Json if protocol == "json" else nat.SqsProtocol.Query
+    o.timeout_ns = timeout_ns
+    if tls is not None:
+        o.tls = tls
+    creds = credentials if credentials is not None else make_chain_provider(environ=environ, region=region)
+    return nat.HttpSqsApi(o, creds, clock)
+
+
+def new_sqs_client(target: TargetConfig, api):
+    return native().SqsClient(api, target.queue_url, list(target.attribute_names))
+
+
+def loop_config(target: TargetConfig):
+    c = native().LoopConfig()
+    c.poll_period_ns = target.poll_period_ns
+    c.scale_down_cool_down_ns = target.scale_down_cool_down_ns
+    c.scale_up_cool_down_ns = target.scale_up_cool_down_ns
+    c.scale_up_messages = target.scale_up_messages
+    c.scale_down_messages = target.scale_down_messages
+    return c
+
+
+@dataclass
+class Worker:
+    target: TargetConfig
+    runner: object
+    sqs_api: object
+    kube_api: object
+    logger: object
+
+
+def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger, clock,
+               credentials=None, environ: Optional[Mapping[str, str]] = None, tag_queue: bool = False) -> Worker:
+    nat = native()
+    log = base_logger
+    if tag_queue:
+        log = base_logger.with_fields([("deployment", target.name), ("queue", target.queue_url)])
+    kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock)
+    scaler = new_pod_autoscaler(target, kube_api, log, clock)
+    sqs_api = new_sqs_api(cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
+                          credentials, environ)
+    sqs = new_sqs_client(target, sqs_api)
+    runner = nat.Runner(loop_config(target), sqs, scaler, clock, log)
+    return Worker(target, runner, sqs_api, kube_api, log)
+
+
+def load_rest_config(cfg: Config, environ: Optional[Mapping[str, str]] = None) -> RestConfig:
+    return build_config_from_flags(cfg.kube_config_path, environ)

@@ -1,0 +1,174 @@
+"""Poll -> scale-patch latency benchmark against localhost fake SQS / kube-apiserver servers.
+
+BASELINE.json's metric is the p50 of the time from the end of the poll sleep to the end of the
+replica write (``Runner`` records it per iteration, csrc/core/runner.cc), at 1/2/4/8
+concurrently tracked queues. Every tracked queue gets its own native worker thread, its own
+persistent connections and its own Deployment; all of them share one fake SQS endpoint and one
+fake apiserver (as production shares AWS and the apiserver).
+
+The wire path is the production one: SigV4-signed ``GetQueueAttributes`` (verified by the
+fake), bearer-token kube REST calls with resourceVersion preconditions, real attribute summing
+and clamp arithmetic, info-level logrus lines written to a file descriptor.
+
+Trace: the fake serves the BASELINE.json "step trace" 200 -> 0 -> 200 ... one value per poll,
+with scale-up-messages=100 / scale-down-messages=10, min 1 / max 8 and zero poll period and
+cool-downs, so *every* iteration performs SQS + GET + write (the 3-round-trip scaling path of
+SURVEY.md §3.2) -- the path whose latency the metric names.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from ..autoscaler import new_deployment_api, new_pod_autoscaler, new_sqs_api, new_sqs_client
+from ..config import TargetConfig
+from ..kube.config import RestConfig
+from ..ops import native
+from ..sqs.credentials import static_provider
+
+AKID = "AKIDBENCHEXAMPLE"
+SECRET = "bench/secret/key/EXAMPLEKEY"
+TOKEN = "bench-bearer-token"
+REGION = "us-east-1"
+
+
+@dataclass
+class LatencyResult:
+    queues: int
+    mode: str
+    steps: int
+    samples: List[int] = field(default_factory=list)  # ns
+    wall_s: float = 0.0
+    sqs_requests: int = 0
+    kube_requests: int = 0
+    sqs_connections: int = 0
+    kube_connections: int = 0
+    signature_failures: int = 0
+    final_replicas: List[int] = field(default_factory=list)
+
+    def pct(self, p: float) -> float:
+        """Nearest-rank percentile in milliseconds."""
+        if not self.samples:
+            return float("nan")
+        v = sorted(self.samples)
+        import math
+
+        k = max(1, math.ceil(p / 100.0 * len(v)))
+        return v[min(k, len(v)) - 1] / 1e6
+
+    def summary(self) -> Dict[str, float]:
+        return {
+            "queues": self.queues,
+            "mode": self.mode,
+            "p50_ms": round(self.pct(50), 4),
+            "p90_ms": round(self.pct(90), 4),
+            "p99_ms": round(self.pct(99), 4),
+            "samples": len(self.samples),
+            "iterations_per_s": round(self.queues * self.steps / self.wall_s, 1) if self.wall_s else 0.0,
+        }
+
+
+class BenchEnv:
+    """Fake servers + one worker per queue."""
+
+    def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
+                 kube_latency_ns: int = 0, log_fd: Optional[int] = None):
+        nat = native()
+        self.nat = nat
+        self.mode = mode
+        self.sqs = nat.FakeSqsServer()
+        self.sqs.require_signature(AKID, SECRET, REGION)
+        self.sqs.start("127.0.0.1", 0, tls)
+        self.sqs.set_latency(sqs_latency_ns)
+        self.kube = nat.FakeKubeServer()
+        self.kube.require_token(TOKEN)
+        self.kube.start("127.0.0.1", 0, tls)
+        self.kube.set_latency(kube_latency_ns)
+        self.clock = nat.RealClock()
+        self.log = nat.Logger()
+        self._devnull = None
+        if log_fd is None:
+            self._devnull = os.open(os.devnull, os.O_WRONLY)
+            log_fd = self._devnull
+        self.log.set_sink_fd(log_fd)
+        high = {"ApproximateNumberOfMessages": "150", "ApproximateNumberOfMessagesDelayed": "20",
+                "ApproximateNumberOfMessagesNotVisible": "30"}
+        low = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed": "0",
+               "ApproximateNumberOfMessagesNotVisible": "0"}
+        rest = RestConfig(host=self.kube.url, bearer_token=TOKEN, insecure=tls)
+        sqs_tls = None
+        if tls:
+            sqs_tls = nat.TlsOptions()
+            sqs_tls.ca_pem = self.sqs.cert_pem
+            rest.insecure = False
+            rest.ca_pem = self.kube.cert_pem
+        creds = static_provider(AKID, SECRET)
+        self.runners = []
+        self.targets = []
+        for q in range(queues):
+            url = f"{self.sqs.url}/000000000000/bench-queue-{q}"
+            name = f"gpu-worker-{q}"
+            self.sqs.set_attribute_cycle(url, [high, low])
+            self.kube.add_deployment("bench", name, 1)
+            t = TargetConfig(queue_url=url, deployment=name, namespace="bench", poll_period_ns=0,
+                             scale_up_cool_down_ns=0, scale_down_cool_down_ns=0, scale_up_messages=100,
+                             scale_down_messages=10, max_pods=8, min_pods=1)
+            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock)
+            scaler = new_pod_autoscaler(t, kube_api, self.log, self.clock)
+            sqs_api = new_sqs_api(REGION, self.clock, endpoint=self.sqs.url, credentials=creds, tls=sqs_tls)
+            client = new_sqs_client(t, sqs_api)
+            cfg = nat.LoopConfig()
+            cfg.poll_period_ns = 0
+            cfg.scale_up_cool_down_ns = 0
+            cfg.scale_down_cool_down_ns = 0
+            cfg.scale_up_messages = 100
+            cfg.scale_down_messages = 10
+            self.runners.append(nat.Runner(cfg, client, scaler, self.clock, self.log))
+            self.targets.append(t)
+
+    def run(self, iterations: int) -> float:
+        """All workers run ``iterations`` polls concurrently; returns wall seconds."""
+        sup = self.nat.Supervisor()
+        for r in self.runners:
+            sup.add(r)
+        t0 = time.perf_counter()
+        sup.start(iterations)
+        sup.join()
+        return time.perf_counter() - t0
+
+    def collect(self, steps: int, wall: float) -> LatencyResult:
+        res = LatencyResult(queues=len(self.runners), mode=self.mode, steps=steps, wall_s=wall)
+        for r in self.runners:
+            res.samples.extend(r.latencies())
+        res.sqs_requests = self.sqs.requests()
+        res.kube_requests = self.kube.requests()
+        res.sqs_connections = self.sqs.connections()
+        res.kube_connections = self.kube.connections()
+        res.signature_failures = self.sqs.signature_failures()
+        res.final_replicas = [self.kube.replicas("bench", t.deployment) for t in self.targets]
+        return res
+
+    def clear(self) -> None:
+        for r in self.runners:
+            r.clear_latencies()
+
+    def close(self) -> None:
+        self.sqs.stop()
+        self.kube.stop()
+        if self._devnull is not None:
+            os.close(self._devnull)
+            self._devnull = None
+
+
+def measure(queues: int, steps: int, warmup: int, mode: str = "scale", **kw) -> LatencyResult:
+    env = BenchEnv(queues, mode, **kw)
+    try:
+        if warmup:
+            env.run(warmup)
+        env.clear()
+        wall = env.run(steps)
+        return env.collect(steps, wall)
+    finally:
+        env.close()

@@ -1,0 +1,231 @@
+"""CLI surface and configuration model.
+
+Reference parity (C1/C2 in SURVEY.md §2.1):
+
+* the 14 flags of /root/reference/main.go:83-97 with the same names, types, help texts and
+  defaults -- except ``--max-pods``, which defaults to 8 (one GPU-worker pod per MI355X on an
+  8-GPU node; BASELINE.json north_star);
+* the attribute-name rule of /root/reference/main.go:103-110: only when ``--attribute-names``
+  differs *as a string* from the default is it split on ``,`` and each piece ``TrimSpace``d;
+  empty pieces are kept (the reference then panics at /root/reference/sqs/sqs.go:58, this build
+  reports an error for that poll instead);
+* ``KUBE_CONFIG_PATH`` selects a kubeconfig file, empty means in-cluster
+  (/root/reference/scale/scale.go:32-33).
+
+Extensions (all off or reference-equivalent by default):
+
+* ``--queue`` (repeatable): track several queue -> Deployment pairs from one process, one
+  independent worker each (BASELINE.json: 1/2/4/8 tracked queues). Each spec is
+  ``url=<sqs-url>,deployment=<name>[,namespace=..][,<flag>=<value>...]`` where ``<flag>`` is
+  any per-target flag below (``attribute-names`` uses ``|`` between names).
+* ``--scale-mode``: ``scale`` (autoscaling/v1 ``/scale`` subresource, default), ``deployment``
+  (full-object GET+PUT exactly like the reference), ``patch`` (merge patch with a
+  resourceVersion precondition).
+* ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
+  ``--log-format``, ``--metrics-addr``, ``--gpu-aware-max``.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field, replace
+from typing import Dict, List, Optional
+
+from .utils.goflag import SECOND, FlagError, FlagSet, parse_duration, parse_int
+
+DEFAULT_ATTRIBUTE_NAMES = (
+    "ApproximateNumberOfMessages,ApproximateNumberOfMessagesDelayed,ApproximateNumberOfMessagesNotVisible"
+)  # /root/reference/main.go:28
+
+REFERENCE_MAX_PODS = 5  # /root/reference/main.go:90
+MI355X_MAX_PODS = 8  # one GPU-worker pod per MI355X of an 8-GPU node
+
+SCALE_MODES = ("scale", "deployment", "patch")
+SQS_PROTOCOLS = ("query", "json")
+
+
+@dataclass
+class TargetConfig:
+    """One tracked queue and the Deployment it drives (the whole reference process)."""
+
+    queue_url: str = ""
+    deployment: str = ""
+    namespace: str = "default"
+    attribute_names: List[str] = field(default_factory=lambda: DEFAULT_ATTRIBUTE_NAMES.split(","))
+    poll_period_ns: int = 5 * SECOND
+    scale_down_cool_down_ns: int = 30 * SECOND
+    scale_up_cool_down_ns: int = 10 * SECOND
+    scale_up_messages: int = 100
+    scale_down_messages: int = 10
+    scale_up_pods: int = 1
+    scale_down_pods: int = 1
+    max_pods: int = MI355X_MAX_PODS
+    min_pods: int = 1
+
+    @property
+    def name(self) -> str:
+        return f"{self.namespace}/{self.deployment}"
+
+
+@dataclass
+class Config:
+    targets: List[TargetConfig] = field(default_factory=list)
+    aws_region: str = ""
+    scale_mode: str = "scale"
+    sqs_endpoint: str = ""
+    sqs_protocol: str = "query"
+    api_timeout_ns: int = 30 * SECOND
+    log_level: str = "info"
+    log_format: str = "text"
+    metrics_addr: str = ""
+    gpu_aware_max: str = ""
+    kube_config_path: str = ""
+
+
+def parse_attribute_names(value: str) -> List[str]:
+    """/root/reference/main.go:103-110 (string inequality with the default, then split+trim)."""
+    if value == DEFAULT_ATTRIBUTE_NAMES:
+        return DEFAULT_ATTRIBUTE_NAMES.split(",")
+    return [piece.strip() for piece in value.split(",")]
+
+
+def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
+    fs = FlagSet(program=program)
+    # /root/reference/main.go:83-97, verbatim help texts
+    fs.duration("poll-period", 5 * SECOND, "The interval in seconds for checking if scaling is required")
+    fs.duration("scale-down-cool-down", 30 * SECOND, "The cool down period for scaling down")
+    fs.duration("scale-up-cool-down", 10 * SECOND, "The cool down period for scaling up")
+    fs.int("scale-up-messages", 100, "Number of sqs messages queued up required for scaling up")
+    fs.int("scale-down-messages", 10, "Number of messages required to scaling down")
+    fs.int("scale-up-pods", 1, "Number of Pod in scaling up")
+    fs.int("scale-down-pods", 1, "Number of Pod in scaling down")
+    fs.int("max-pods", MI355X_MAX_PODS, "Max pods that kube-sqs-autoscaler can scale")
+    fs.int("min-pods", 1, "Min pods that kube-sqs-autoscaler can scale")
+    fs.string("aws-region", "", "Your AWS region")
+    fs.string(
+        "attribute-names",
+        DEFAULT_ATTRIBUTE_NAMES,
+        "A comma-separated list of queue attribute names to query in calculating the number of messages",
+    )
+    fs.string("sqs-queue-url", "", "The sqs queue url")
+    fs.string("kubernetes-deployment", "", "Kubernetes Deployment to scale. This field is required")
+    fs.string("kubernetes-namespace", "default", "The namespace your deployment is running in")
+    # ---- extensions ----
+    fs.strings(
+        "queue",
+        "Additional queue to track (repeatable): url=<sqs-url>,deployment=<name>[,namespace=<ns>][,<flag>=<value>...]",
+    )
+    fs.string("scale-mode", "scale", "How replicas are written: scale (/scale subresource), deployment (GET+PUT of the whole Deployment, like the reference) or patch")
+    fs.string("sqs-endpoint", "", "Override the SQS endpoint URL (VPC endpoint, local fake); empty uses the regional endpoint")
+    fs.string("sqs-protocol", "query", "SQS wire protocol: query (AWS Query/XML) or json (AWS JSON 1.0)")
+    fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
+    fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
+    fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
+    fs.string("metrics-addr", "", "Serve Prometheus metrics and /healthz on host:port (disabled when empty)")
+    fs.string("gpu-aware-max", "", "Cap max-pods at the healthy GPU count: local (probe this node's GPUs); empty disables")
+    return fs
+
+
+# per-target keys accepted inside --queue specs
+_TARGET_INT_KEYS = {
+    "scale-up-messages": "scale_up_messages",
+    "scale-down-messages": "scale_down_messages",
+    "scale-up-pods": "scale_up_pods",
+    "scale-down-pods": "scale_down_pods",
+    "max-pods": "max_pods",
+    "min-pods": "min_pods",
+}
+_TARGET_DURATION_KEYS = {
+    "poll-period": "poll_period_ns",
+    "scale-down-cool-down": "scale_down_cool_down_ns",
+    "scale-up-cool-down": "scale_up_cool_down_ns",
+}
+
+
+def parse_queue_spec(spec: str, base: TargetConfig) -> TargetConfig:
+    """Parses one ``--queue`` value on top of the top-level flags."""
+    t = replace(base, attribute_names=list(base.attribute_names))
+    seen_url = False
+    for item in spec.split(","):
+        if not item.strip():
+            continue
+        if "=" not in item:
+            raise FlagError(f'invalid value "{spec}" for flag -queue: expected key=value, got "{item}"')
+        k, v = item.split("=", 1)
+        k = k.strip()
+        v = v.strip()
+        try:
+            if k in ("url", "sqs-queue-url"):
+                t.queue_url = v
+                seen_url = True
+            elif k in ("deployment", "kubernetes-deployment"):
+                t.deployment = v
+            elif k in ("namespace", "kubernetes-namespace"):
+                t.namespace = v
+            elif k == "attribute-names":
+                t.attribute_names = parse_attribute_names(v.replace("|", ","))
+            elif k in _TARGET_INT_KEYS:
+                setattr(t, _TARGET_INT_KEYS[k], parse_int(v))
+            elif k in _TARGET_DURATION_KEYS:
+                setattr(t, _TARGET_DURATION_KEYS[k], parse_duration(v))
+            else:
+                raise FlagError(f'invalid value "{spec}" for flag -queue: unknown key "{k}"')
+        except ValueError:
+            raise FlagError(f'invalid value "{spec}" for flag -queue: parse error')
+    if not seen_url:
+        raise FlagError(f'invalid value "{spec}" for flag -queue: missing url=')
+    return t
+
+
+def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> Config:
+    env = os.environ if environ is None else environ
+    base = TargetConfig(
+        queue_url=fs["sqs-queue-url"],
+        deployment=fs["kubernetes-deployment"],
+        namespace=fs["kubernetes-namespace"],
+        attribute_names=parse_attribute_names(fs["attribute-names"]),
+        poll_period_ns=fs["poll-period"],
+        scale_down_cool_down_ns=fs["scale-down-cool-down"],
+        scale_up_cool_down_ns=fs["scale-up-cool-down"],
+        scale_up_messages=fs["scale-up-messages"],
+        scale_down_messages=fs["scale-down-messages"],
+        scale_up_pods=fs["scale-up-pods"],
+        scale_down_pods=fs["scale-down-pods"],
+        max_pods=fs["max-pods"],
+        min_pods=fs["min-pods"],
+    )
+    targets: List[TargetConfig] = []
+    queue_specs: List[str] = fs["queue"]
+    # The single-queue reference form is always honoured when --sqs-queue-url is given or no
+    # --queue is used (the reference accepts an empty URL and fails on every poll instead).
+    if fs.was_set("sqs-queue-url") or not queue_specs:
+        targets.append(base)
+    for spec in queue_specs:
+        targets.append(parse_queue_spec(spec, base))
+    cfg = Config(
+        targets=targets,
+        aws_region=fs["aws-region"],
+        scale_mode=fs["scale-mode"],
+        sqs_endpoint=fs["sqs-endpoint"],
+        sqs_protocol=fs["sqs-protocol"],
+        api_timeout_ns=fs["api-timeout"],
+        log_level=fs["log-level"],
+        log_format=fs["log-format"],
+        metrics_addr=fs["metrics-addr"],
+        gpu_aware_max=fs["gpu-aware-max"],
+        kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
+    )
+    if cfg.scale_mode not in SCALE_MODES:
+        raise FlagError(f'invalid value "{cfg.scale_mode}" for flag -scale-mode: must be one of {", ".join(SCALE_MODES)}')
+    if cfg.sqs_protocol not in SQS_PROTOCOLS:
+        raise FlagError(f'invalid value "{cfg.sqs_protocol}" for flag -sqs-protocol: must be query or json')
+    if cfg.log_format not in ("text", "json"):
+        raise FlagError(f'invalid value "{cfg.log_format}" for flag -log-format: must be text or json')
+    if cfg.gpu_aware_max not in ("", "local"):
+        raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty or local')
+    return cfg
+
+
+def parse_args(argv: List[str], environ: Optional[Dict[str, str]] = None) -> Config:
+    fs = new_flag_set()
+    fs.parse(argv)
+    return config_from_flags(fs, environ)

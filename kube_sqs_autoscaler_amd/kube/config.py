@@ -1,0 +1,157 @@
+"""Kubernetes client configuration: in-cluster service account or a kubeconfig file.
+
+Mirrors ``clientcmd.BuildConfigFromFlags("", os.Getenv("KUBE_CONFIG_PATH"))``
+(/root/reference/scale/scale.go:32-33, client-go v0.19.4, go.mod:17):
+
+* path empty -> in-cluster config (``KUBERNETES_SERVICE_HOST``/``_PORT``, the projected SA
+  token and CA under ``/var/run/secrets/kubernetes.io/serviceaccount``); if that fails, the
+  empty explicit-path loading rules yield "no configuration has been provided";
+* path set -> that kubeconfig only (``KUBECONFIG`` is *not* consulted, matching the
+  reference's ``ExplicitPath`` loading rules): current-context -> cluster + user.
+
+Supported kubeconfig auth: bearer ``token`` / ``tokenFile``, client certificates (file or
+``-data``), basic auth; TLS via ``certificate-authority[-data]``, ``insecure-skip-tls-verify``,
+``tls-server-name``. ``exec`` / ``auth-provider`` plugins are out of scope and reported as
+errors. The reference turns any failure here into
+``panic("Failed to configure incluster or local config")`` (scale.go:35); the CLI keeps that
+text and exits non-zero.
+"""
+from __future__ import annotations
+
+import base64
+import os
+from dataclasses import dataclass, field
+from typing import Mapping, Optional
+
+import yaml
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class KubeConfigError(RuntimeError):
+    pass
+
+
+@dataclass
+class RestConfig:
+    host: str
+    bearer_token: str = ""
+    bearer_token_file: str = ""
+    username: str = ""
+    password: str = ""
+    ca_pem: str = ""
+    ca_file: str = ""
+    cert_pem: str = ""
+    key_pem: str = ""
+    insecure: bool = False
+    server_name: str = ""
+    source: str = ""
+    warnings: list = field(default_factory=list)
+
+
+def in_cluster_config(environ: Optional[Mapping[str, str]] = None, sa_dir: str = SA_DIR) -> RestConfig:
+    env = os.environ if environ is None else environ
+    host, port = env.get("KUBERNETES_SERVICE_HOST", ""), env.get("KUBERNETES_SERVICE_PORT", "")
+    if not host or not port:
+        raise KubeConfigError(
+            "unable to load in-cluster configuration, KUBERNETES_SERVICE_HOST and KUBERNETES_SERVICE_PORT must be defined")
+    token_file = os.path.join(sa_dir, "token")
+    try:
+        with open(token_file) as f:
+            token = f.read().strip()
+    except OSError as e:
+        raise KubeConfigError(f"open {token_file}: {e.strerror.lower() if e.strerror else e}")
+    ca_file = os.path.join(sa_dir, "ca.crt")
+    ca_pem = ""
+    if os.path.exists(ca_file):
+        with open(ca_file) as f:
+            ca_pem = f.read()
+    h = f"[{host}]" if ":" in host and not host.startswith("[") else host
+    return RestConfig(host=f"https://{h}:{port}", bearer_token=token, bearer_token_file=token_file,
+                      ca_pem=ca_pem, ca_file=ca_file if ca_pem else "", source="in-cluster")
+
+
+def _b64(s: str) -> str:
+    return base64.b64decode(s).decode()
+
+
+def _read_rel(base_dir: str, path: str) -> str:
+    p = path if os.path.isabs(path) else os.path.join(base_dir, path)
+    with open(p) as f:
+        return f.read()
+
+
+def load_kubeconfig(path: str, context: str = "") -> RestConfig:
+    try:
+        with open(path) as f:
+            doc = yaml.safe_load(f) or {}
+    except OSError as e:
+        raise KubeConfigError(f"stat {path}: no such file or directory" if not os.path.exists(path) else str(e))
+    except yaml.YAMLError as e:
+        raise KubeConfigError(f"error loading config file \"{path}\": {e}")
+    base = os.path.dirname(os.path.abspath(path))
+
+    def by_name(kind: str, name: str) -> dict:
+        for item in doc.get(kind) or []:
+            if item.get("name") == name:
+                return item.get(kind[:-1]) or {}
+        raise KubeConfigError(f'invalid configuration: {kind[:-1]} "{name}" not found')
+
+    ctx_name = context or doc.get("current-context") or ""
+    if not ctx_name:
+        raise KubeConfigError("invalid configuration: no configuration has been provided, try setting KUBERNETES_MASTER environment variable")
+    ctx = by_name("contexts", ctx_name)
+    cluster = by_name("clusters", ctx.get("cluster", ""))
+    user = by_name("users", ctx.get("user", "")) if ctx.get("user") else {}
+    server = cluster.get("server", "")
+    if not server:
+        raise KubeConfigError("invalid configuration: no server found for cluster")
+    rc = RestConfig(host=server, source=f"kubeconfig:{path}")
+    rc.insecure = bool(cluster.get("insecure-skip-tls-verify", False))
+    rc.server_name = cluster.get("tls-server-name", "")
+    try:
+        if cluster.get("certificate-authority-data"):
+            rc.ca_pem = _b64(cluster["certificate-authority-data"])
+        elif cluster.get("certificate-authority"):
+            rc.ca_pem = _read_rel(base, cluster["certificate-authority"])
+        if user.get("client-certificate-data"):
+            rc.cert_pem = _b64(user["client-certificate-data"])
+        elif user.get("client-certificate"):
+            rc.cert_pem = _read_rel(base, user["client-certificate"])
+        if user.get("client-key-data"):
+            rc.key_pem = _b64(user["client-key-data"])
+        elif user.get("client-key"):
+            rc.key_pem = _read_rel(base, user["client-key"])
+        if user.get("token"):
+            rc.bearer_token = user["token"]
+        elif user.get("tokenFile"):
+            tf = user["tokenFile"]
+            rc.bearer_token_file = tf if os.path.isabs(tf) else os.path.join(base, tf)
+            rc.bearer_token = _read_rel(base, tf).strip()
+    except OSError as e:
+        raise KubeConfigError(f"unable to read referenced file: {e}")
+    except (ValueError, TypeError) as e:
+        raise KubeConfigError(f"illegal base64 data in kubeconfig: {e}")
+    rc.username = user.get("username", "")
+    rc.password = user.get("password", "")
+    if user.get("exec") or user.get("auth-provider"):
+        raise KubeConfigError("exec and auth-provider credential plugins are not supported; use a token or client certificate")
+    if bool(rc.cert_pem) != bool(rc.key_pem):
+        raise KubeConfigError("invalid configuration: client-cert and client-key must be specified together")
+    return rc
+
+
+def build_config_from_flags(kube_config_path: str, environ: Optional[Mapping[str, str]] = None,
+                            sa_dir: str = SA_DIR) -> RestConfig:
+    """clientcmd.BuildConfigFromFlags("", kube_config_path)."""
+    if not kube_config_path:
+        warnings = ["Neither --kubeconfig nor --master was specified.  Using the inClusterConfig.  This might not work."]
+        try:
+            rc = in_cluster_config(environ, sa_dir)
+            rc.warnings = warnings
+            return rc
+        except KubeConfigError as e:
+            raise KubeConfigError(
+                f"error creating inClusterConfig, falling back to default config: {e}; "
+                "invalid configuration: no configuration has been provided, try setting KUBERNETES_MASTER environment variable")
+    return load_kubeconfig(kube_config_path)

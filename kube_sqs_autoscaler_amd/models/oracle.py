@@ -1,0 +1,214 @@
+"""Reference-semantics oracle: the decision model of the reference, in its simplest form.
+
+This is a deliberately naive, I/O-free restatement of /root/reference/main.go:35-78 plus
+/root/reference/scale/scale.go:54-107 over a virtual clock. It shares no code with the native
+control loop (csrc/core/runner.cc) so the parity harness compares two independent
+implementations of SURVEY.md §3.3:
+
+1. timers armed at ``Run()`` entry (main.go:37-38);
+2. independent up/down timers;
+3. a no-op at a bound refreshes that direction's timer (scale.go:62-65,89-92 + main.go:62,76);
+4. a failure does not refresh it (main.go:57-60,71-74);
+5. a cool-down skip or failed scale-up ``continue``s past the scale-down check (main.go:54,59);
+6. proceed iff ``now >= last + cool`` (``After`` is strict; main.go:52,66), ``now`` re-read at
+   every comparison, so API latency moves later comparisons;
+7. asymmetric clamping with Go int32 arithmetic (scale.go:62-69,89-97);
+8. depth is the 64-bit sum of the requested attributes (sqs.go:56-64);
+9. the first poll happens one period after start (main.go:41), sleep-then-work (no ticker).
+
+Time model (shared with the native in-memory fakes): the SQS trace is sampled at call start,
+then every API call advances the clock by its latency.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
+
+INT32_MIN = -(1 << 31)
+
+
+def int32(v: int) -> int:
+    """Go ``int32(v)`` (two's-complement wrap)."""
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+def atoi(s: str) -> int:
+    """strconv.Atoi on a 64-bit platform; raises ValueError like the reference's error path."""
+    if s is None:
+        raise ValueError("missing attribute")
+    t = s
+    if t[:1] in ("+", "-"):
+        t = t[1:]
+    if not t or not t.isascii() or not t.isdigit():
+        raise ValueError(f'strconv.Atoi: parsing "{s}": invalid syntax')
+    v = int(s)
+    if v < -(1 << 63) or v > (1 << 63) - 1:
+        raise ValueError(f'strconv.Atoi: parsing "{s}": value out of range')
+    return v
+
+
+@dataclass(frozen=True)
+class Params:
+    poll_ns: int
+    up_cool_ns: int
+    down_cool_ns: int
+    up_msgs: int
+    down_msgs: int
+    up_pods: int = 1
+    down_pods: int = 1
+    max_pods: int = 8
+    min_pods: int = 1
+
+
+@dataclass(frozen=True)
+class Latency:
+    sqs_ns: int = 1_000_000
+    get_ns: int = 1_000_000
+    update_ns: int = 1_000_000
+
+
+AttrMap = Dict[str, str]
+Trace = Sequence[Tuple[int, AttrMap]]  # piecewise-constant (start_ns, attributes), sorted
+
+
+@dataclass
+class Event:
+    """One poll, in the vocabulary the native runner reports (runner.h IterationRecord)."""
+
+    index: int
+    t_poll_ns: int
+    depth: Optional[int]  # None when the depth read failed
+    up: str = "none"  # none | cooldown | scaled | noop | failed
+    down: str = "none"
+    replicas: int = 0  # Deployment replicas after the poll
+    up_replicas: Optional[int] = None  # replicas right after a scale-up write
+
+    def key(self) -> Tuple:
+        return (self.index, self.depth, self.up, self.down, self.replicas)
+
+
+@dataclass
+class Faults:
+    """Injected failures keyed by 1-based poll index."""
+
+    sqs: Set[int] = field(default_factory=set)
+    up_get: Set[int] = field(default_factory=set)
+    up_update: Set[int] = field(default_factory=set)
+    down_get: Set[int] = field(default_factory=set)
+    down_update: Set[int] = field(default_factory=set)
+
+
+def sample(trace: Trace, t: int) -> AttrMap:
+    cur: AttrMap = {}
+    for start, attrs in trace:
+        if start <= t:
+            cur = attrs
+        else:
+            break
+    return cur
+
+
+def depth_of(attrs: AttrMap, names: Sequence[str]) -> int:
+    total = 0
+    for n in names:
+        total += atoi(attrs.get(n))  # type: ignore[arg-type]
+    # Go int is 64-bit and wraps
+    total &= (1 << 64) - 1
+    return total - (1 << 64) if total >= 1 << 63 else total
+
+
+def simulate(
+    p: Params,
+    trace: Trace,
+    names: Sequence[str],
+    polls: int,
+    init_replicas: int,
+    lat: Latency = Latency(),
+    faults: Optional[Faults] = None,
+) -> List[Event]:
+    f = faults or Faults()
+    now = 0
+    last_up = now  # main.go:37
+    last_down = now  # main.go:38
+    replicas = int32(init_replicas)
+    out: List[Event] = []
+    for k in range(1, polls + 1):
+        now += max(p.poll_ns, 0)  # main.go:41 time.Sleep (negative/zero: no sleep)
+        ev = Event(index=k, t_poll_ns=now, depth=None)
+        out.append(ev)
+        attrs = sample(trace, now)
+        now += lat.sqs_ns
+        if k in f.sqs:
+            ev.replicas = replicas
+            continue
+        try:
+            n = depth_of(attrs, names)
+        except (ValueError, TypeError):
+            ev.replicas = replicas
+            continue  # main.go:44-47
+        ev.depth = n
+
+        if n >= p.up_msgs:  # main.go:51
+            if last_up + p.up_cool_ns > now:  # main.go:52
+                ev.up = "cooldown"
+                ev.replicas = replicas
+                continue
+            now += lat.get_ns
+            if k in f.up_get:
+                ev.up = "failed"
+                ev.replicas = replicas
+                continue
+            if replicas >= int32(p.max_pods):  # scale.go:62
+                ev.up = "noop"
+            else:
+                nxt = int32(replicas + int32(p.up_pods))
+                if nxt > int32(p.max_pods):
+                    nxt = int32(p.max_pods)
+                now += lat.update_ns
+                if k in f.up_update:
+                    ev.up = "failed"
+                    ev.replicas = replicas
+                    continue
+                replicas = nxt
+                ev.up = "scaled"
+                ev.up_replicas = replicas
+            last_up = now  # main.go:62
+
+        if n <= p.down_msgs:  # main.go:65
+            if last_down + p.down_cool_ns > now:  # main.go:66
+                ev.down = "cooldown"
+                ev.replicas = replicas
+                continue
+            now += lat.get_ns
+            if k in f.down_get:
+                ev.down = "failed"
+                ev.replicas = replicas
+                continue
+            if replicas <= int32(p.min_pods):  # scale.go:89
+                ev.down = "noop"
+            else:
+                nxt = int32(replicas - int32(p.down_pods))
+                if nxt < int32(p.min_pods):
+                    nxt = int32(p.min_pods)
+                now += lat.update_ns
+                if k in f.down_update:
+                    ev.down = "failed"
+                    ev.replicas = replicas
+                    continue
+                replicas = nxt
+                ev.down = "scaled"
+            last_down = now  # main.go:76
+        ev.replicas = replicas
+    return out
+
+
+def scale_events(events: Sequence[Event]) -> List[Tuple[str, int, int]]:
+    """(direction, poll index, replicas after) for every write -- the compact golden form."""
+    out = []
+    for e in events:
+        if e.up == "scaled":
+            out.append(("up", e.index, e.up_replicas))
+        if e.down == "scaled":
+            out.append(("down", e.index, e.replicas))
+    return out

@@ -1,0 +1,312 @@
+"""AWS credential chain (what ``session.NewSession()`` resolves for the reference).
+
+The reference builds its SQS client with ``sqs.New(session.Must(session.NewSession()), ...)``
+(/root/reference/sqs/sqs.go:36) and never names a credential source, so it gets aws-sdk-go
+v1.35.35's resolution order (go.mod:6):
+
+1. static keys from the environment (``AWS_ACCESS_KEY_ID``/``AWS_ACCESS_KEY`` +
+   ``AWS_SECRET_ACCESS_KEY``/``AWS_SECRET_KEY`` [+ ``AWS_SESSION_TOKEN``]);
+2. web identity (IRSA): ``AWS_WEB_IDENTITY_TOKEN_FILE`` + ``AWS_ROLE_ARN`` ->
+   STS ``AssumeRoleWithWebIdentity``;
+3. the shared credentials file (``AWS_SHARED_CREDENTIALS_FILE`` or ``~/.aws/credentials``,
+   profile ``AWS_PROFILE`` / ``AWS_DEFAULT_PROFILE`` / ``default``), including
+   ``credential_process``;
+4. remote: ECS task role (``AWS_CONTAINER_CREDENTIALS_RELATIVE_URI`` /
+   ``AWS_CONTAINER_CREDENTIALS_FULL_URI`` + ``AWS_CONTAINER_AUTHORIZATION_TOKEN``), otherwise
+   the EC2 instance role through IMDSv2 (token PUT, falling back to IMDSv1).
+
+Resolution is lazy: nothing is fetched until the first poll (like the SDK), and the native
+``CachedCredentials`` (csrc/core/sigv4.h) only calls :meth:`ChainProvider.retrieve` again
+when the cached keys are within 5 minutes of expiry or after an ``ExpiredToken`` response.
+"""
+from __future__ import annotations
+
+import configparser
+import json
+import os
+import subprocess
+import threading
+import urllib.error
+import urllib.parse
+import urllib.request
+from datetime import datetime, timezone
+from typing import Callable, Dict, List, Mapping, Optional, Tuple
+
+from ..ops import native
+
+ECS_HOST = "http://169.254.170.2"
+IMDS_HOST = "http://169.254.169.254"
+
+
+class CredentialsError(RuntimeError):
+    pass
+
+
+def parse_expiration(s: str) -> int:
+    """ISO-8601 (``2024-05-01T12:00:00Z`` or with offset / fraction) -> unix nanoseconds."""
+    s = s.strip()
+    if s.endswith("Z"):
+        s = s[:-1] + "+00:00"
+    dt = datetime.fromisoformat(s)
+    if dt.tzinfo is None:
+        dt = dt.replace(tzinfo=timezone.utc)
+    return int(dt.timestamp()) * 1_000_000_000 + dt.microsecond * 1000
+
+
+Fetch = Callable[[str, str, Dict[str, str], bytes, float], Tuple[int, bytes]]
+
+
+def urllib_fetch(method: str, url: str, headers: Dict[str, str], body: bytes, timeout: float) -> Tuple[int, bytes]:
+    req = urllib.request.Request(url, data=body if body else None, method=method, headers=headers)
+    try:
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return r.status, r.read()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read()
+
+
+def _make(akid: str, secret: str, token: str, expires_ns: int, name: str):
+    return native().Credentials(akid, secret, token, expires_ns, name)
+
+
+class _Provider:
+    name = "provider"
+
+    def fetch(self):  # -> native Credentials
+        raise NotImplementedError
+
+
+class EnvProvider(_Provider):
+    name = "EnvProvider"
+
+    def __init__(self, environ: Mapping[str, str]):
+        self.env = environ
+
+    def available(self) -> bool:
+        e = self.env
+        return bool((e.get("AWS_ACCESS_KEY_ID") or e.get("AWS_ACCESS_KEY")) and (
+            e.get("AWS_SECRET_ACCESS_KEY") or e.get("AWS_SECRET_KEY")))
+
+    def fetch(self):
+        e = self.env
+        akid = e.get("AWS_ACCESS_KEY_ID") or e.get("AWS_ACCESS_KEY") or ""
+        secret = e.get("AWS_SECRET_ACCESS_KEY") or e.get("AWS_SECRET_KEY") or ""
+        if not akid:
+            raise CredentialsError("EnvAccessKeyNotFound: AWS_ACCESS_KEY_ID or AWS_ACCESS_KEY not found in environment")
+        if not secret:
+            raise CredentialsError("EnvSecretNotFound: AWS_SECRET_ACCESS_KEY or AWS_SECRET_KEY not found in environment")
+        return _make(akid, secret, e.get("AWS_SESSION_TOKEN", ""), 0, self.name)
+
+
+class SharedFileProvider(_Provider):
+    name = "SharedCredentialsProvider"
+
+    def __init__(self, environ: Mapping[str, str]):
+        self.env = environ
+        home = environ.get("HOME") or os.path.expanduser("~")
+        self.path = environ.get("AWS_SHARED_CREDENTIALS_FILE") or os.path.join(home, ".aws", "credentials")
+        self.profile = environ.get("AWS_PROFILE") or environ.get("AWS_DEFAULT_PROFILE") or "default"
+
+    def _section(self) -> Optional[Mapping[str, str]]:
+        if not os.path.exists(self.path):
+            return None
+        cp = configparser.RawConfigParser()
+        try:
+            cp.read(self.path)
+        except configparser.Error as e:
+            raise CredentialsError(f"SharedCredsLoad: failed to load shared credentials file: {e}")
+        if not cp.has_section(self.profile):
+            return None
+        return dict(cp.items(self.profile))
+
+    def available(self) -> bool:
+        try:
+            sec = self._section()
+        except CredentialsError:
+            return True  # surface the parse error from fetch()
+        return bool(sec and (sec.get("aws_access_key_id") or sec.get("credential_process")))
+
+    def fetch(self):
+        sec = self._section()
+        if sec is None:
+            raise CredentialsError(f"SharedCredsLoad: failed to get profile {self.profile!r} from {self.path}")
+        if sec.get("aws_access_key_id"):
+            secret = sec.get("aws_secret_access_key", "")
+            if not secret:
+                raise CredentialsError(
+                    f"SharedCredsAccessKey: shared credentials {self.profile} in {self.path} did not contain aws_secret_access_key")
+            return _make(sec["aws_access_key_id"], secret, sec.get("aws_session_token", ""), 0, self.name)
+        if sec.get("credential_process"):
+            return process_credentials(sec["credential_process"])
+        raise CredentialsError(f"SharedCredsAccessKey: shared credentials {self.profile} in {self.path} did not contain aws_access_key_id")
+
+
+def process_credentials(command: str, timeout: float = 60.0):
+    """credential_process: runs the command and parses its Version 1 JSON output."""
+    try:
+        out = subprocess.run(command, shell=True, capture_output=True, timeout=timeout, check=True).stdout
+    except (subprocess.SubprocessError, OSError) as e:
+        raise CredentialsError(f"ProcessProviderExecutionError: error in credential_process: {e}")
+    try:
+        j = json.loads(out)
+    except ValueError as e:
+        raise CredentialsError(f"ProcessProviderParseError: parse failed of process output: {e}")
+    if j.get("Version") != 1:
+        raise CredentialsError("ProcessProviderVersionError: credential_process output must have Version 1")
+    exp = parse_expiration(j["Expiration"]) if j.get("Expiration") else 0
+    return _make(j.get("AccessKeyId", ""), j.get("SecretAccessKey", ""), j.get("SessionToken", ""), exp,
+                 "ProcessProvider")
+
+
+class WebIdentityProvider(_Provider):
+    """STS AssumeRoleWithWebIdentity (unsigned Query call), the IRSA path on EKS."""
+
+    name = "WebIdentityCredentials"
+
+    def __init__(self, environ: Mapping[str, str], region: str, fetch: Fetch = urllib_fetch, sts_endpoint: str = ""):
+        self.token_file = environ.get("AWS_WEB_IDENTITY_TOKEN_FILE", "")
+        self.role_arn = environ.get("AWS_ROLE_ARN", "")
+        self.session_name = environ.get("AWS_ROLE_SESSION_NAME", "")
+        self.region = region
+        self.http = fetch
+        self.endpoint = sts_endpoint or environ.get("AWS_STS_ENDPOINT", "") or (
+            f"https://sts.{region}.amazonaws.com" if region else "https://sts.amazonaws.com")
+
+    def available(self) -> bool:
+        return bool(self.token_file)
+
+    def fetch(self):
+        if not self.role_arn:
+            raise CredentialsError("WebIdentityErr: role ARN is not set")
+        try:
+            with open(self.token_file, "r") as f:
+                token = f.read().strip()
+        except OSError as e:
+            raise CredentialsError(f"WebIdentityErr: unable to read file at {self.token_file}: {e}")
+        session = self.session_name or f"{int(datetime.now(timezone.utc).timestamp() * 1e9)}"
+        form = urllib.parse.urlencode({
+            "Action": "AssumeRoleWithWebIdentity",
+            "RoleArn": self.role_arn,
+            "RoleSessionName": session,
+            "Version": "2011-06-15",
+            "WebIdentityToken": token,
+        }).encode()
+        status, body = self.http("POST", self.endpoint + "/", {"Content-Type": "application/x-www-form-urlencoded"},
+                                 form, 10.0)
+        nat = native()
+        text = body.decode(errors="replace")
+        if status != 200:
+            code = nat.xml_first_text(text, "Code") or f"HTTP {status}"
+            msg = nat.xml_first_text(text, "Message") or ""
+            raise CredentialsError(f"WebIdentityErr: failed to retrieve credentials: {code}: {msg}")
+        akid = nat.xml_first_text(text, "AccessKeyId")
+        secret = nat.xml_first_text(text, "SecretAccessKey")
+        tok = nat.xml_first_text(text, "SessionToken")
+        exp = nat.xml_first_text(text, "Expiration")
+        if not akid or not secret:
+            raise CredentialsError("WebIdentityErr: STS response carried no credentials")
+        return _make(akid, secret, tok or "", parse_expiration(exp) if exp else 0, self.name)
+
+
+class RemoteProvider(_Provider):
+    """ECS container credentials when configured, otherwise EC2 IMDS (v2 with v1 fallback)."""
+
+    def __init__(self, environ: Mapping[str, str], fetch: Fetch = urllib_fetch, imds_endpoint: str = ""):
+        self.env = environ
+        self.http = fetch
+        self.imds = imds_endpoint or environ.get("AWS_EC2_METADATA_SERVICE_ENDPOINT", "") or IMDS_HOST
+        self.name = "ECSCredentialsProvider" if self._ecs_url() else "EC2RoleProvider"
+
+    def _ecs_url(self) -> str:
+        rel = self.env.get("AWS_CONTAINER_CREDENTIALS_RELATIVE_URI", "")
+        if rel:
+            return ECS_HOST + rel
+        return self.env.get("AWS_CONTAINER_CREDENTIALS_FULL_URI", "")
+
+    def available(self) -> bool:
+        return self.env.get("AWS_EC2_METADATA_DISABLED", "").lower() != "true" or bool(self._ecs_url())
+
+    def fetch(self):
+        url = self._ecs_url()
+        if url:
+            headers = {}
+            if self.env.get("AWS_CONTAINER_AUTHORIZATION_TOKEN"):
+                headers["Authorization"] = self.env["AWS_CONTAINER_AUTHORIZATION_TOKEN"]
+            status, body = self.http("GET", url, headers, b"", 5.0)
+            if status != 200:
+                raise CredentialsError(f"CredentialsEndpointError: failed to load credentials (HTTP {status})")
+            j = json.loads(body)
+            return _make(j["AccessKeyId"], j["SecretAccessKey"], j.get("Token", ""),
+                         parse_expiration(j["Expiration"]) if j.get("Expiration") else 0, self.name)
+        if self.env.get("AWS_EC2_METADATA_DISABLED", "").lower() == "true":
+            raise CredentialsError("EC2RoleRequestError: EC2 IMDS access disabled via AWS_EC2_METADATA_DISABLED")
+        base = self.imds.rstrip("/")
+        headers: Dict[str, str] = {}
+        try:
+            status, tok = self.http("PUT", base + "/latest/api/token",
+                                    {"X-aws-ec2-metadata-token-ttl-seconds": "21600"}, b"", 1.0)
+            if status == 200:
+                headers["X-aws-ec2-metadata-token"] = tok.decode().strip()
+        except OSError:
+            pass  # IMDSv1 fallback
+        try:
+            status, roles = self.http("GET", base + "/latest/meta-data/iam/security-credentials/", headers, b"", 1.0)
+        except OSError as e:
+            raise CredentialsError(f"NoCredentialProviders: no valid providers in chain ({e})")
+        if status != 200 or not roles.strip():
+            raise CredentialsError("EC2RoleRequestError: no EC2 instance role found")
+        role = roles.decode().splitlines()[0].strip()
+        status, body = self.http("GET", base + "/latest/meta-data/iam/security-credentials/" + role, headers, b"", 1.0)
+        if status != 200:
+            raise CredentialsError(f"EC2RoleRequestError: failed to get {role} EC2 instance role credentials")
+        j = json.loads(body)
+        if j.get("Code", "Success") != "Success":
+            raise CredentialsError(f"EC2RoleRequestError: {j.get('Code')}: {j.get('Message', '')}")
+        return _make(j["AccessKeyId"], j["SecretAccessKey"], j.get("Token", ""),
+                     parse_expiration(j["Expiration"]) if j.get("Expiration") else 0, self.name)
+
+
+def default_chain(environ: Optional[Mapping[str, str]] = None, region: str = "", fetch: Fetch = urllib_fetch) -> List[_Provider]:
+    env = dict(os.environ if environ is None else environ)
+    return [EnvProvider(env), WebIdentityProvider(env, region, fetch), SharedFileProvider(env), RemoteProvider(env, fetch)]
+
+
+def make_chain_provider(providers: Optional[List[_Provider]] = None, environ: Optional[Mapping[str, str]] = None,
+                        region: str = "", fetch: Fetch = urllib_fetch):
+    """A native ``CredentialsProvider`` backed by the chain (first available provider wins)."""
+    nat = native()
+    chain = providers if providers is not None else default_chain(environ, region, fetch)
+
+    class ChainProvider(nat.CredentialsProvider):
+        def __init__(self) -> None:
+            super().__init__()
+            self.providers = chain
+            self.lock = threading.Lock()
+            self.last_provider = ""
+
+        def retrieve(self):
+            with self.lock:
+                errors = []
+                for p in self.providers:
+                    if hasattr(p, "available") and not p.available():
+                        continue
+                    try:
+                        c = p.fetch()
+                    except CredentialsError as e:
+                        errors.append(str(e))
+                        # env/web-identity/shared are authoritative once configured (SDK behaviour)
+                        if not isinstance(p, RemoteProvider):
+                            raise
+                        continue
+                    self.last_provider = p.name
+                    return c
+                raise CredentialsError(
+                    "NoCredentialProviders: no valid providers in chain. Deprecated.\n\tFor verbose messaging see "
+                    "aws.Config.CredentialsChainVerboseErrors" + (f" ({'; '.join(errors)})" if errors else ""))
+
+    return ChainProvider()
+
+
+def static_provider(akid: str, secret: str, token: str = ""):
+    nat = native()
+    return nat.StaticCredentialsProvider(nat.Credentials(akid, secret, token, 0, "StaticProvider"))

@@ -1,0 +1,36 @@
+"""Tests that need the MI355X: the gfx950 probe kernels and the driver smoke path."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_probe_inventory():
+    from kube_sqs_autoscaler_amd.ops import gpu
+
+    n = gpu.device_count()
+    assert n >= 1
+    info = gpu.device_info(0)
+    assert info.arch.startswith("gfx950"), info
+    assert info.wavefront_size == 64
+    assert info.compute_units >= 256
+    assert info.total_mem_bytes > 250 << 30  # 288 GB HBM3E
+
+
+def test_hbm_health_check_matches_host_checksum():
+    from kube_sqs_autoscaler_amd.ops import gpu
+
+    h = gpu.health_check(0, 256 << 20)
+    assert h.ok and h.mismatches == 0 and h.checksum == h.expected_checksum
+    assert h.read_gbps > 500  # well above PCIe: really on HBM
+
+
+def test_healthy_gpu_count():
+    from kube_sqs_autoscaler_amd.ops import gpu
+
+    assert gpu.healthy_gpu_count(16 << 20) == gpu.device_count()
+
+
+def test_graft_smoke():
+    import __graft_entry__ as g
+
+    g.smoke()
