@@ -1,0 +1,111 @@
+"""Process entry point: ``python -m kube_sqs_autoscaler_amd [flags]`` (the reference's ``main``).
+
+/root/reference/main.go:82-116: parse flags -> ``NewPodAutoScaler`` (panics when no kube config
+can be built, scale.go:35) -> attribute list -> ``NewSqsClient`` -> log
+``Starting kube-sqs-autoscaler`` -> ``Run`` forever. Exit codes follow Go: 2 for a flag error
+(after printing the message and usage), 0 for ``-h``/``-help``, 2 for a start-up panic.
+Extensions: several ``--queue`` targets, SIGTERM/SIGINT graceful stop (exit 0), optional
+Prometheus endpoint and GPU-aware ``max-pods`` cap.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import List, Mapping, Optional
+
+from . import autoscaler
+from .config import config_from_flags, new_flag_set
+from .kube.config import KubeConfigError
+from .utils.goflag import FlagError
+from .utils.log import make_logger
+
+
+def _program_name(argv0: str) -> str:
+    base = os.path.basename(argv0 or "")
+    return "kube-sqs-autoscaler" if base in ("", "__main__.py", "-c", "-m") else argv0
+
+
+def _panic(msg: str, cause: str = "") -> int:
+    # Go prints "panic: <msg>" plus the goroutine trace and exits with status 2.
+    sys.stderr.write(f"panic: {msg}\n")
+    if cause:
+        sys.stderr.write(f"\ncause: {cause}\n")
+    sys.stderr.flush()
+    return 2
+
+
+def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] = None,
+         max_iterations: int = -1) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    env = os.environ if environ is None else environ
+    fs = new_flag_set(_program_name(sys.argv[0] if sys.argv else ""))
+    try:
+        fs.parse(argv)
+        cfg = config_from_flags(fs, env)
+    except FlagError as e:
+        if e.help:
+            fs.print_usage(sys.stderr)
+            return 0
+        sys.stderr.write(f"{e}\n")
+        fs.print_usage(sys.stderr)
+        return 2
+
+    from .ops import native
+
+    nat = native()
+    clock = nat.RealClock()
+    log = make_logger(cfg.log_level, cfg.log_format, clock=None)
+
+    # scale.NewPodAutoScaler -> clientcmd.BuildConfigFromFlags("", KUBE_CONFIG_PATH)
+    try:
+        rest = autoscaler.load_rest_config(cfg, env)
+    except KubeConfigError as e:
+        return _panic("Failed to configure incluster or local config", str(e))
+    for w in rest.warnings:
+        log.log("warning", w)
+
+    if cfg.gpu_aware_max == "local":
+        from .ops import gpu
+
+        try:
+            healthy = gpu.healthy_gpu_count()
+        except gpu.GpuProbeError as e:
+            healthy = 0
+            log.log("warning", f"GPU probe failed, max-pods not capped: {e}")
+        if healthy > 0:
+            for t in cfg.targets:
+                if t.max_pods > healthy:
+                    t.max_pods = healthy
+            log.log("info", f"Capping max-pods at {healthy} healthy GPUs", [("gpus", str(healthy))])
+
+    multi = len(cfg.targets) > 1
+    workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
+
+    from .parallel.fleet import Fleet
+
+    fleet = Fleet(workers)
+    metrics = None
+    if cfg.metrics_addr:
+        from .metrics import MetricsServer
+
+        metrics = MetricsServer(fleet, cfg.metrics_addr)
+        metrics.start()
+        log.log("info", f"Serving metrics on {cfg.metrics_addr}")
+
+    log.log("info", "Starting kube-sqs-autoscaler")  # main.go:114
+    try:
+        if max_iterations > 0:
+            fleet.start(max_iterations)
+            fleet.join()
+        else:
+            sig = fleet.run_until_signalled(on_signal=lambda s: log.log("info", f"Received signal {s}, stopping"))
+            if sig:
+                log.log("info", "Stopped kube-sqs-autoscaler")
+    finally:
+        if metrics is not None:
+            metrics.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -96,6 +96,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     lib.ksa_gpu_get_info.restype = ctypes.c_int
     lib.ksa_gpu_health_check.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_Health)]
     lib.ksa_gpu_health_check.restype = ctypes.c_int
+    lib.ksa_gpu_health_check_ex.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(_Health)]
+    lib.ksa_gpu_health_check_ex.restype = ctypes.c_int
     _LIB = lib
     return lib
 
@@ -131,11 +133,15 @@ def device_info(index: int) -> GpuInfo:
     )
 
 
-def health_check(index: int, nbytes: int = 256 << 20) -> GpuHealth:
-    """HBM fill + verify over ``nbytes`` on device ``index`` (default 256 MiB)."""
+def health_check(index: int, nbytes: int = 256 << 20, reps: int = 3) -> GpuHealth:
+    """HBM fill + verify over ``nbytes`` on device ``index``: one warm-up, then best of ``reps``.
+
+    Bandwidth figures are HBM figures only for buffers well past the 256 MiB Infinity Cache
+    (use >= 1 GiB); the health verdict holds for any size.
+    """
     lib = load()
     h = _Health()
-    rc = lib.ksa_gpu_health_check(index, nbytes, ctypes.byref(h))
+    rc = lib.ksa_gpu_health_check_ex(index, nbytes, reps, ctypes.byref(h))
     if rc < 0:
         raise GpuProbeError(_err(lib))
     return GpuHealth(
@@ -155,4 +161,4 @@ def health_check(index: int, nbytes: int = 256 << 20) -> GpuHealth:
 def healthy_gpu_count(nbytes: int = 64 << 20) -> int:
     """Number of local GPUs that pass :func:`health_check` (0 when there is no GPU)."""
     n = device_count()
-    return sum(1 for i in range(n) if health_check(i, nbytes).ok)
+    return sum(1 for i in range(n) if health_check(i, nbytes, reps=1).ok)

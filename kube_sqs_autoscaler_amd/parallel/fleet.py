@@ -1,0 +1,84 @@
+"""Multi-queue execution: one native worker thread per tracked queue.
+
+The reference runs exactly one loop per process (``Run`` never returns, /root/reference/main.go:35-80;
+one URL and one Deployment, main.go:95-97). BASELINE.json asks for 1/2/4/8 concurrently tracked
+queues, so a :class:`Fleet` owns N independent ``Runner`` objects and drives them from the
+native ``Supervisor`` (csrc/core/runner.h): each worker has its own clients, connections,
+timers and stats, and nothing is shared between workers (SURVEY.md §5.2 -- no cross-queue
+locks, so no races by construction). Stopping is cooperative: a stop request interrupts every
+worker's poll sleep, so SIGTERM ends the process within one in-flight API call (the reference
+has no graceful shutdown, main.go:36).
+"""
+from __future__ import annotations
+
+import signal
+import threading
+from typing import Callable, List, Optional, Sequence
+
+from ..ops import native
+
+
+class Fleet:
+    def __init__(self, workers: Sequence) -> None:
+        self.workers = list(workers)
+        self._sup = native().Supervisor()
+        for w in self.workers:
+            self._sup.add(w.runner)
+        self._started = False
+        self._lock = threading.Lock()
+
+    def start(self, max_iterations: int = -1) -> None:
+        with self._lock:
+            if self._started:
+                raise RuntimeError("fleet already started")
+            self._started = True
+        self._sup.start(max_iterations)
+
+    def stop(self) -> None:
+        self._sup.stop()
+
+    @property
+    def stopped(self) -> bool:
+        return self._sup.stopped()
+
+    def wait(self, timeout_s: float) -> bool:
+        """True when every worker has exited (max_iterations reached or stopped)."""
+        return self._sup.wait(max(int(timeout_s * 1e9), 1))
+
+    def join(self) -> None:
+        self._sup.join()
+
+    def stats(self) -> List[dict]:
+        out = []
+        for w in self.workers:
+            s = dict(w.runner.stats())
+            s["deployment"] = w.target.name
+            s["queue"] = w.target.queue_url
+            out.append(s)
+        return out
+
+    def run_until_signalled(self, signals=(signal.SIGTERM, signal.SIGINT),
+                            on_signal: Optional[Callable[[int], None]] = None, poll_s: float = 0.2) -> int:
+        """Starts the workers and blocks until a signal (or all workers finish); returns the signal."""
+        got: List[int] = []
+        prev = {}
+
+        def handler(signum, _frame):
+            got.append(signum)
+            if on_signal:
+                on_signal(signum)
+            self.stop()
+
+        if threading.current_thread() is threading.main_thread():
+            for s in signals:
+                prev[s] = signal.signal(s, handler)
+        try:
+            self.start()
+            while not self.wait(poll_s):
+                pass
+        finally:
+            self.stop()
+            self.join()
+            for s, h in prev.items():
+                signal.signal(s, h)
+        return got[0] if got else 0

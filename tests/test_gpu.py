@@ -19,9 +19,11 @@ def test_probe_inventory():
 def test_hbm_health_check_matches_host_checksum():
     from kube_sqs_autoscaler_amd.ops import gpu
 
-    h = gpu.health_check(0, 256 << 20)
+    h = gpu.health_check(0, 2 << 30, reps=5)  # 2 GiB >> 256 MiB Infinity Cache: HBM-bound
     assert h.ok and h.mismatches == 0 and h.checksum == h.expected_checksum
-    assert h.read_gbps > 500  # well above PCIe: really on HBM
+    print(f"HBM write {h.write_gbps:.0f} GB/s, read+verify {h.read_gbps:.0f} GB/s")
+    # streaming kernels should reach a large fraction of the ~6.3 TB/s achievable
+    assert h.read_gbps > 3000 and h.write_gbps > 3000, h
 
 
 def test_healthy_gpu_count():
