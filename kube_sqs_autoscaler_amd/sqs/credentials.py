@@ -24,6 +24,7 @@ from __future__ import annotations
 import configparser
 import json
 import os
+import re
 import subprocess
 import threading
 import urllib.error
@@ -45,8 +46,13 @@ class CredentialsError(RuntimeError):
 def parse_expiration(s: str) -> int:
     """ISO-8601 (``2024-05-01T12:00:00Z`` or with offset / fraction) -> unix nanoseconds."""
     s = s.strip()
-    if s.endswith("Z"):
+    if s.endswith("Z") or s.endswith("z"):
         s = s[:-1] + "+00:00"
+    # Python 3.10's fromisoformat wants exactly 3 or 6 fractional digits
+    m = re.match(r"^(.*T\d\d:\d\d:\d\d)(?:\.(\d+))?(.*)$", s)
+    if m:
+        frac = (m.group(2) or "")[:6]
+        s = m.group(1) + ("." + frac.ljust(6, "0") if frac else "") + m.group(3)
     dt = datetime.fromisoformat(s)
     if dt.tzinfo is None:
         dt = dt.replace(tzinfo=timezone.utc)

@@ -1,0 +1,44 @@
+"""bench.py contract: one JSON line; multi-rank path over torch.distributed (gloo on CPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _json_line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def _check(out, n, steps, warmup):
+    assert out["metric"].startswith("poll") and out["unit"] == "ms" and out["higher_is_better"] is False
+    assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
+    assert out["value"] > 0 and out["ms_per_step"] > 0 and out["scaling"] == "weak"
+    assert out["config"]["parallelism"] == f"dp{n}" and out["vs_baseline"] is None
+    assert out["extra"]["decision_parity"]["fraction"] == 1.0
+    assert out["extra"]["samples"] == steps * n and out["extra"]["signature_failures"] == 0
+
+
+def test_bench_single_rank():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "200", "--warmup", "20", "--no-sweep"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    _check(_json_line(r.stdout), 1, 200, 20)
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ)
+    env["CUDA_VISIBLE_DEVICES"] = ""  # CPU ranks: gloo backend
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29611", "bench.py", "--gpus", "2", "--steps", "150",
+                        "--warmup", "10"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = _json_line(r.stdout)
+    _check(out, 2, 150, 10)
+    assert out["extra"]["tracked_queues"] == 2

@@ -1,0 +1,147 @@
+"""AWS credential chain (aws-sdk-go v1 session defaults the reference relies on, sqs/sqs.go:36)."""
+import json
+import os
+
+import pytest
+
+from kube_sqs_autoscaler_amd.sqs import credentials as cr
+
+
+def chain(env, fetch=None, region="us-east-1"):
+    return cr.make_chain_provider(environ=env, region=region, fetch=fetch or (lambda *a: (404, b"")))
+
+
+def test_env_credentials(nat):
+    c = chain({"AWS_ACCESS_KEY_ID": "AK", "AWS_SECRET_ACCESS_KEY": "SK", "AWS_SESSION_TOKEN": "T"}).retrieve()
+    assert (c.access_key_id, c.secret_access_key, c.session_token, c.provider_name) == ("AK", "SK", "T", "EnvProvider")
+    c = chain({"AWS_ACCESS_KEY": "AK2", "AWS_SECRET_KEY": "SK2"}).retrieve()
+    assert c.access_key_id == "AK2"
+
+
+def test_shared_file_profiles(tmp_path, nat):
+    f = tmp_path / "credentials"
+    f.write_text("[default]\naws_access_key_id = D\naws_secret_access_key = DS\n\n[prod]\naws_access_key_id=P\naws_secret_access_key=PS\naws_session_token=PT\n")
+    env = {"AWS_SHARED_CREDENTIALS_FILE": str(f)}
+    assert chain(env).retrieve().access_key_id == "D"
+    c = chain({**env, "AWS_PROFILE": "prod"}).retrieve()
+    assert (c.access_key_id, c.session_token, c.provider_name) == ("P", "PT", "SharedCredentialsProvider")
+    with pytest.raises(Exception, match="aws_secret_access_key"):
+        f.write_text("[default]\naws_access_key_id = D\n")
+        chain(env).retrieve()
+
+
+def test_env_beats_shared_file(tmp_path, nat):
+    f = tmp_path / "credentials"
+    f.write_text("[default]\naws_access_key_id = D\naws_secret_access_key = DS\n")
+    env = {"AWS_SHARED_CREDENTIALS_FILE": str(f), "AWS_ACCESS_KEY_ID": "E", "AWS_SECRET_ACCESS_KEY": "ES"}
+    assert chain(env).retrieve().access_key_id == "E"
+
+
+def test_credential_process(tmp_path, nat):
+    out = {"Version": 1, "AccessKeyId": "CP", "SecretAccessKey": "CPS", "SessionToken": "CPT",
+           "Expiration": "2030-01-01T00:00:00Z"}
+    script = tmp_path / "proc.sh"
+    script.write_text("#!/bin/sh\necho '" + json.dumps(out) + "'\n")
+    script.chmod(0o755)
+    f = tmp_path / "credentials"
+    f.write_text(f"[default]\ncredential_process = {script}\n")
+    c = chain({"AWS_SHARED_CREDENTIALS_FILE": str(f)}).retrieve()
+    assert c.access_key_id == "CP" and c.expires_unix_ns == cr.parse_expiration("2030-01-01T00:00:00Z")
+
+
+def test_web_identity(tmp_path, nat):
+    tok = tmp_path / "token"
+    tok.write_text("jwt-token\n")
+    seen = {}
+
+    def fetch(method, url, headers, body, timeout):
+        seen.update(method=method, url=url, body=body.decode())
+        return 200, (b"<AssumeRoleWithWebIdentityResponse><AssumeRoleWithWebIdentityResult><Credentials>"
+                     b"<AccessKeyId>ASIAWEB</AccessKeyId><SecretAccessKey>WS</SecretAccessKey>"
+                     b"<SessionToken>WT</SessionToken><Expiration>2031-02-03T04:05:06Z</Expiration>"
+                     b"</Credentials></AssumeRoleWithWebIdentityResult></AssumeRoleWithWebIdentityResponse>")
+
+    env = {"AWS_WEB_IDENTITY_TOKEN_FILE": str(tok), "AWS_ROLE_ARN": "arn:aws:iam::1:role/r", "AWS_ROLE_SESSION_NAME": "s"}
+    c = chain(env, fetch, region="us-west-2").retrieve()
+    assert (c.access_key_id, c.secret_access_key, c.session_token) == ("ASIAWEB", "WS", "WT")
+    assert seen["url"] == "https://sts.us-west-2.amazonaws.com/" and "Action=AssumeRoleWithWebIdentity" in seen["body"]
+    assert "WebIdentityToken=jwt-token" in seen["body"] and "RoleArn=arn%3Aaws%3Aiam%3A%3A1%3Arole%2Fr" in seen["body"]
+
+
+def test_web_identity_error(tmp_path, nat):
+    tok = tmp_path / "token"
+    tok.write_text("t")
+    fetch = lambda *a: (403, b"<ErrorResponse><Error><Code>AccessDenied</Code><Message>nope</Message></Error></ErrorResponse>")
+    with pytest.raises(Exception, match="AccessDenied: nope"):
+        chain({"AWS_WEB_IDENTITY_TOKEN_FILE": str(tok), "AWS_ROLE_ARN": "a"}, fetch).retrieve()
+
+
+def test_ecs_container_credentials(nat):
+    def fetch(method, url, headers, body, timeout):
+        assert url == "http://169.254.170.2/v2/credentials/abc" and headers.get("Authorization") == "Bearer x"
+        return 200, json.dumps({"AccessKeyId": "ECS", "SecretAccessKey": "S", "Token": "T", "Expiration": "2030-01-01T00:00:00Z"}).encode()
+
+    c = chain({"AWS_CONTAINER_CREDENTIALS_RELATIVE_URI": "/v2/credentials/abc", "AWS_CONTAINER_AUTHORIZATION_TOKEN": "Bearer x"}, fetch).retrieve()
+    assert c.access_key_id == "ECS" and c.provider_name == "ECSCredentialsProvider"
+
+
+def test_imds_v2(nat):
+    calls = []
+
+    def fetch(method, url, headers, body, timeout):
+        calls.append((method, url, dict(headers)))
+        if url.endswith("/latest/api/token"):
+            return 200, b"imds-token"
+        if url.endswith("/security-credentials/"):
+            assert headers["X-aws-ec2-metadata-token"] == "imds-token"
+            return 200, b"node-role\n"
+        if url.endswith("/security-credentials/node-role"):
+            return 200, json.dumps({"Code": "Success", "AccessKeyId": "EC2", "SecretAccessKey": "S", "Token": "T",
+                                    "Expiration": "2030-01-01T00:00:00Z"}).encode()
+        return 404, b""
+
+    c = chain({}, fetch).retrieve()
+    assert c.access_key_id == "EC2" and c.provider_name == "EC2RoleProvider"
+    assert calls[0][0] == "PUT" and calls[0][2]["X-aws-ec2-metadata-token-ttl-seconds"] == "21600"
+
+
+def test_no_credentials(nat):
+    with pytest.raises(Exception, match="NoCredentialProviders"):
+        chain({"AWS_EC2_METADATA_DISABLED": "true"}).retrieve()
+
+
+def test_parse_expiration():
+    assert cr.parse_expiration("1970-01-01T00:00:01Z") == 10**9
+    assert cr.parse_expiration("1970-01-01T01:00:00+01:00") == 0
+    assert cr.parse_expiration("1970-01-01T00:00:00.5Z") == 5 * 10**8
+
+
+def test_chain_feeds_native_signer_lazily_and_caches(nat):
+    """The native client asks the Python chain only when its cache is cold."""
+    calls = []
+
+    class P(cr._Provider):
+        name = "counting"
+
+        def available(self):
+            return True
+
+        def fetch(self):
+            calls.append(1)
+            return nat.Credentials("AKIDTEST", "secret/KEY", "", 0, "counting")
+
+    s = nat.FakeSqsServer()
+    s.require_signature("AKIDTEST", "secret/KEY", "eu-west-1")
+    s.start()
+    try:
+        from kube_sqs_autoscaler_amd.autoscaler import new_sqs_api
+
+        api = new_sqs_api("eu-west-1", nat.RealClock(), endpoint=s.url, credentials=cr.make_chain_provider([P()]))
+        assert calls == []  # lazy, like session.NewSession
+        url = s.url + "/1/q"
+        s.set_attributes(url, {"A": "1"})
+        c = nat.SqsClient(api, url, ["A"])
+        assert c.num_messages() == 1 and c.num_messages() == 1
+        assert len(calls) == 1 and s.signature_failures() == 0
+    finally:
+        s.stop()

@@ -1,0 +1,225 @@
+"""End-to-end over real sockets: native SQS/kube REST clients against the native fake servers."""
+import pytest
+
+from kube_sqs_autoscaler_amd.autoscaler import new_deployment_api, new_sqs_api
+from kube_sqs_autoscaler_amd.kube.config import RestConfig
+from kube_sqs_autoscaler_amd.sqs.credentials import static_provider
+from kube_sqs_autoscaler_amd.utils.log import capture_logger
+
+AKID, SECRET, REGION, TOKEN = "AKIDTEST", "secret/KEY", "eu-west-1", "tok-123"
+ATTRS = {"ApproximateNumberOfMessages": "11", "ApproximateNumberOfMessagesDelayed": "2",
+         "ApproximateNumberOfMessagesNotVisible": "5", "VisibilityTimeout": "30"}
+NAMES = ["ApproximateNumberOfMessages", "ApproximateNumberOfMessagesDelayed", "ApproximateNumberOfMessagesNotVisible"]
+
+
+@pytest.fixture
+def sqs_server(nat):
+    s = nat.FakeSqsServer()
+    s.require_signature(AKID, SECRET, REGION)
+    s.start()
+    yield s
+    s.stop()
+
+
+@pytest.fixture
+def kube_server(nat):
+    k = nat.FakeKubeServer()
+    k.require_token(TOKEN)
+    k.start()
+    k.add_deployment("ml", "worker", 3)
+    yield k
+    k.stop()
+
+
+def sqs_client(nat, server, protocol="query", secret=SECRET, tls=None, retries=None):
+    api = new_sqs_api(REGION, nat.RealClock(), endpoint=server.url, protocol=protocol,
+                      credentials=static_provider(AKID, secret), tls=tls)
+    url = f"{server.url}/123456789012/jobs"
+    return nat.SqsClient(api, url, NAMES), api, url
+
+
+@pytest.mark.parametrize("protocol", ["query", "json"])
+def test_get_queue_attributes_signed(nat, sqs_server, protocol):
+    c, api, url = sqs_client(nat, sqs_server, protocol)
+    sqs_server.set_attributes(url, ATTRS)
+    assert c.num_messages() == 18
+    assert c.num_messages() == 18
+    assert sqs_server.signature_failures() == 0
+    assert sqs_server.connections() == 1  # keep-alive: one connection for both polls
+    body = sqs_server.last_body()
+    if protocol == "query":
+        assert "Action=GetQueueAttributes" in body and "AttributeName.1=ApproximateNumberOfMessages" in body
+        assert "Version=2012-11-05" in body
+    else:
+        assert '"AttributeNames"' in body and dict(sqs_server.last_headers())["X-Amz-Target"] == "AmazonSQS.GetQueueAttributes"
+
+
+def test_bad_signature_is_rejected(nat, sqs_server):
+    c, api, url = sqs_client(nat, sqs_server, secret="wrong")
+    sqs_server.set_attributes(url, ATTRS)
+    with pytest.raises(nat.NativeError, match="^Failed to get messages in SQS: SignatureDoesNotMatch"):
+        c.num_messages()
+    assert sqs_server.signature_failures() >= 1
+
+
+def test_nonexistent_queue(nat, sqs_server):
+    c, api, url = sqs_client(nat, sqs_server)
+    with pytest.raises(nat.NativeError, match="NonExistentQueue"):
+        c.num_messages()
+
+
+def test_sdk_style_retries_on_5xx(nat, sqs_server):
+    c, api, url = sqs_client(nat, sqs_server)
+    sqs_server.set_attributes(url, ATTRS)
+    sqs_server.inject(2, nat.InjectedFault(500, "oops"))
+    assert c.num_messages() == 18  # DefaultRetryer: up to 3 retries
+    assert api.stats()["retries"] == 2
+    sqs_server.inject(4, nat.InjectedFault(503, "down"))
+    with pytest.raises(nat.NativeError):
+        c.num_messages()
+
+
+def test_no_retry_on_4xx(nat, sqs_server):
+    c, api, url = sqs_client(nat, sqs_server)
+    sqs_server.set_attributes(url, ATTRS)
+    sqs_server.inject(1, nat.InjectedFault(400, "<ErrorResponse><Error><Code>InvalidAttributeName</Code><Message>bad</Message></Error></ErrorResponse>", "text/xml"))
+    with pytest.raises(nat.NativeError, match="InvalidAttributeName"):
+        c.num_messages()
+    assert api.stats()["retries"] == 0
+
+
+def test_reconnect_after_server_closed_idle_connection(nat, sqs_server):
+    c, api, url = sqs_client(nat, sqs_server)
+    sqs_server.set_attributes(url, ATTRS)
+    assert c.num_messages() == 18
+    sqs_server.drop_connections()
+    assert c.num_messages() == 18
+    assert sqs_server.connections() == 2
+
+
+def test_missing_region_fails_every_poll(nat, sqs_server):
+    api = new_sqs_api("", nat.RealClock(), credentials=static_provider(AKID, SECRET))
+    c = nat.SqsClient(api, "https://sqs.example/1/q", NAMES)
+    with pytest.raises(nat.NativeError, match="region"):
+        c.num_messages()
+
+
+def test_tls_sqs(nat):
+    s = nat.FakeSqsServer()
+    s.require_signature(AKID, SECRET, REGION)
+    s.start("127.0.0.1", 0, True)
+    try:
+        tls = nat.TlsOptions()
+        tls.ca_pem = s.cert_pem
+        c, api, url = sqs_client(nat, s, tls=tls)
+        assert url.startswith("https://")
+        s.set_attributes(url, ATTRS)
+        assert c.num_messages() == 18
+        # untrusted CA -> verification failure
+        c2, _, _ = sqs_client(nat, s, tls=nat.TlsOptions())
+        with pytest.raises(nat.NativeError):
+            c2.num_messages()
+    finally:
+        s.stop()
+
+
+def scaler(nat, kube_server, mode, token=TOKEN, max_=5, min_=1, lines=None):
+    api = new_deployment_api(RestConfig(host=kube_server.url, bearer_token=token), "ml", mode)
+    log = capture_logger(lines if lines is not None else [])
+    return nat.PodAutoScaler(api, "worker", "ml", max_, min_, 1, 1, log, nat.RealClock()), api
+
+
+@pytest.mark.parametrize("mode,path,verb", [
+    ("deployment", "/apis/apps/v1/namespaces/ml/deployments/worker", "PUT"),
+    ("scale", "/apis/apps/v1/namespaces/ml/deployments/worker/scale", "PUT"),
+    ("patch", "/apis/apps/v1/namespaces/ml/deployments/worker/scale", "PATCH"),
+])
+def test_kube_modes(nat, kube_server, mode, path, verb):
+    p, api = scaler(nat, kube_server, mode)
+    p.scale_up()
+    assert kube_server.replicas("ml", "worker") == 4
+    assert kube_server.last_method() == verb and kube_server.last_path() == path
+    p.scale_down()
+    p.scale_down()
+    assert kube_server.replicas("ml", "worker") == 2
+    assert kube_server.connections() == 1 and kube_server.auth_failures() == 0
+    if mode == "deployment":
+        import json
+
+        body = json.loads(kube_server.last_body())
+        assert body["kind"] == "Deployment" and body["spec"]["replicas"] == 2
+        assert body["metadata"]["resourceVersion"]  # optimistic concurrency, like client-go Update
+
+
+def test_kube_noop_does_not_write(nat, kube_server):
+    p, api = scaler(nat, kube_server, "scale", max_=3)
+    writes = kube_server.writes()
+    p.scale_up()
+    assert kube_server.writes() == writes and kube_server.replicas("ml", "worker") == 3
+
+
+@pytest.mark.parametrize("mode", ["deployment", "scale", "patch"])
+def test_kube_conflict_surfaces_as_error(nat, kube_server, mode):
+    p, api = scaler(nat, kube_server, mode)
+    kube_server.conflict_next(1)
+    with pytest.raises(nat.NativeError, match="^Failed to scale up: .*the object has been modified"):
+        p.scale_up()
+    assert kube_server.replicas("ml", "worker") == 3
+    p.scale_up()  # next poll retries with a fresh GET
+    assert kube_server.replicas("ml", "worker") == 4
+
+
+def test_kube_unauthorized(nat, kube_server):
+    p, api = scaler(nat, kube_server, "scale", token="nope")
+    with pytest.raises(nat.NativeError, match="no scale up occurred: Unauthorized"):
+        p.scale_up()
+    assert kube_server.auth_failures() == 1
+
+
+def test_kube_not_found_and_5xx(nat, kube_server):
+    api = new_deployment_api(RestConfig(host=kube_server.url, bearer_token=TOKEN), "ml", "scale")
+    p = nat.PodAutoScaler(api, "ghost", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+    with pytest.raises(nat.NativeError, match="not found"):
+        p.scale_up()
+    p2, _ = scaler(nat, kube_server, "scale")
+    kube_server.inject(1, nat.InjectedFault(500, "boom"))
+    with pytest.raises(nat.NativeError, match="no scale up occurred"):
+        p2.scale_up()
+
+
+def test_kube_tls_with_ca(nat):
+    k = nat.FakeKubeServer()
+    k.require_token(TOKEN)
+    k.start("127.0.0.1", 0, True)
+    try:
+        k.add_deployment("ml", "worker", 1)
+        api = new_deployment_api(RestConfig(host=k.url, bearer_token=TOKEN, ca_pem=k.cert_pem), "ml", "scale")
+        p = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+        p.scale_up()
+        assert k.replicas("ml", "worker") == 2
+    finally:
+        k.stop()
+
+
+def test_full_loop_over_the_wire(nat, sqs_server, kube_server):
+    """Runner + real clients: scale up under backlog, down when drained (C2-shaped)."""
+    c, _, url = sqs_client(nat, sqs_server)
+    p, _ = scaler(nat, kube_server, "scale", max_=5)
+    cfg = nat.LoopConfig()
+    cfg.poll_period_ns = 0
+    cfg.scale_up_cool_down_ns = 0
+    cfg.scale_down_cool_down_ns = 0
+    lines = []
+    r = nat.Runner(cfg, c, p, nat.RealClock(), capture_logger(lines))
+    r.arm()
+    sqs_server.set_attributes(url, {n: "100" for n in NAMES})
+    recs = r.steps(4)
+    assert [x["up"] for x in recs] == ["scaled", "scaled", "noop", "noop"]
+    assert kube_server.replicas("ml", "worker") == 5
+    sqs_server.set_attributes(url, {n: "0" for n in NAMES})
+    recs = r.steps(5)
+    assert [x["down"] for x in recs] == ["scaled"] * 4 + ["noop"]
+    assert kube_server.replicas("ml", "worker") == 1
+    assert all(x["patch_latency_ns"] > 0 for x in recs[:4])
+    st = r.stats()
+    assert st["scale_ups"] == 2 and st["scale_downs"] == 4 and st["polls"] == 9
