@@ -17,6 +17,20 @@
 namespace ksa {
 
 using Nanos = int64_t;
+
+// Timed condition wait. libstdc++ implements wait_for() with pthread_cond_clockwait
+// (CLOCK_MONOTONIC), which GCC 11's ThreadSanitizer does not intercept -- it then misses the
+// unlock inside the wait and reports a false "double lock". Under TSan only, wait on the
+// system clock (pthread_cond_timedwait, intercepted); production keeps the monotonic clock so
+// poll sleeps are immune to wall-clock steps.
+template <class Lock, class Pred>
+bool cv_wait_for(std::condition_variable& cv, Lock& lk, int64_t ns, Pred pred) {
+#if defined(__SANITIZE_THREAD__)
+  return cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::nanoseconds(ns), pred);
+#else
+  return cv.wait_for(lk, std::chrono::nanoseconds(ns), pred);
+#endif
+}
 constexpr Nanos kMicrosecond = 1000;
 constexpr Nanos kMillisecond = 1000 * kMicrosecond;
 constexpr Nanos kSecond = 1000 * kMillisecond;
@@ -38,7 +52,7 @@ class StopFlag {
   bool wait_for(Nanos d) {
     std::unique_lock<std::mutex> lk(mu_);
     if (d <= 0) return !stopped();
-    return !cv_.wait_for(lk, std::chrono::nanoseconds(d), [&] { return stopped(); });
+    return !cv_wait_for(cv_, lk, d, [&] { return stopped(); });
   }
 
  private:

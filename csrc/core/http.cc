@@ -1,5 +1,8 @@
 #include "http.h"
 
+#include <csignal>
+#include <mutex>
+
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -19,6 +22,21 @@
 #include <cstring>
 
 namespace ksa {
+
+namespace {
+// OpenSSL writes through a socket BIO (plain write(2)), so a peer that closes mid-stream would
+// raise SIGPIPE and kill a process that has not ignored it (Python does; a C++ embedder may not).
+// Like Go's runtime, ignore SIGPIPE process-wide -- only if nobody installed a handler -- and
+// let the write fail with EPIPE instead. Plain sockets additionally use MSG_NOSIGNAL.
+void ignore_sigpipe_once() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    struct sigaction cur;
+    if (sigaction(SIGPIPE, nullptr, &cur) == 0 && cur.sa_handler == SIG_DFL) signal(SIGPIPE, SIG_IGN);
+  });
+}
+}  // namespace
+
 
 namespace {
 
@@ -479,6 +497,7 @@ HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
     : origin_(origin), tls_(std::move(tls)), timeout_(timeout) {
   if (!origin_.tls()) return;
   ensure_ssl();
+  ignore_sigpipe_once();
   ctx_ = SSL_CTX_new(TLS_client_method());
   if (!ctx_) {
     ctx_status_ = Status::Err("SSL_CTX_new: " + ssl_error_string());
@@ -700,6 +719,7 @@ HttpServer::~HttpServer() {
 
 Status HttpServer::enable_tls(const std::string& cert_pem, const std::string& key_pem) {
   ensure_ssl();
+  ignore_sigpipe_once();
   ctx_ = SSL_CTX_new(TLS_server_method());
   if (!ctx_) return Status::Err("SSL_CTX_new: " + ssl_error_string());
   return use_cert_key(ctx_, cert_pem, key_pem);

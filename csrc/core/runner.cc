@@ -218,7 +218,7 @@ bool Supervisor::wait(Nanos timeout) {
     cv_.wait(lk, [&] { return running_ == 0; });
     return true;
   }
-  return cv_.wait_for(lk, std::chrono::nanoseconds(timeout), [&] { return running_ == 0; });
+  return cv_wait_for(cv_, lk, timeout, [&] { return running_ == 0; });
 }
 
 void Supervisor::join() {

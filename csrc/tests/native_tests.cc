@@ -1,0 +1,352 @@
+// Host-only unit tests of the native runtime, built plain, with ASan+UBSan and with TSan
+// (kube_sqs_autoscaler_amd/ops/build.py build_native_tests; `make sanitize`).
+//
+// The reference never ran its tests under the race detector (Makefile:7) and
+// its loop tests leak goroutines that race on package globals. Here the multi-queue supervisor,
+// the threaded fake servers and the keep-alive clients are exercised concurrently so TSan can
+// see every cross-thread access of the runtime.
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../core/clock.h"
+#include "../core/fakes.h"
+#include "../core/goutil.h"
+#include "../core/http.h"
+#include "../core/json.h"
+#include "../core/kube.h"
+#include "../core/log.h"
+#include "../core/runner.h"
+#include "../core/sigv4.h"
+#include "../core/sqs.h"
+#include "../core/xml.h"
+
+using namespace ksa;
+
+namespace {
+
+int g_failed = 0;
+int g_checks = 0;
+
+#define CHECK(cond)                                                                 \
+  do {                                                                              \
+    ++g_checks;                                                                     \
+    if (!(cond)) {                                                                  \
+      std::fprintf(stderr, "  CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++g_failed;                                                                   \
+    }                                                                               \
+  } while (0)
+
+#define CHECK_EQ(a, b)                                                                        \
+  do {                                                                                        \
+    ++g_checks;                                                                               \
+    auto va = (a);                                                                            \
+    auto vb = (b);                                                                            \
+    if (!(va == vb)) {                                                                        \
+      std::fprintf(stderr, "  CHECK_EQ failed %s:%d: %s != %s\n", __FILE__, __LINE__, #a, #b); \
+      ++g_failed;                                                                             \
+    }                                                                                         \
+  } while (0)
+
+struct Test {
+  const char* name;
+  std::function<void()> fn;
+};
+std::vector<Test>& registry() {
+  static std::vector<Test> t;
+  return t;
+}
+struct Reg {
+  Reg(const char* n, std::function<void()> f) { registry().push_back({n, std::move(f)}); }
+};
+#define TEST(name)                       \
+  void name();                           \
+  Reg reg_##name(#name, name);           \
+  void name()
+
+std::shared_ptr<Logger> quiet_logger() {
+  auto l = std::make_shared<Logger>();
+  l->set_level(Level::Panic);
+  return l;
+}
+
+AttrMap attrs(int64_t visible, int64_t delayed = 0, int64_t not_visible = 0) {
+  return {{"ApproximateNumberOfMessages", std::to_string(visible)},
+          {"ApproximateNumberOfMessagesDelayed", std::to_string(delayed)},
+          {"ApproximateNumberOfMessagesNotVisible", std::to_string(not_visible)}};
+}
+
+// ---------------------------------------------------------------------------------------
+
+TEST(go_atoi_semantics) {
+  CHECK_EQ(go_atoi("42").value, 42);
+  CHECK_EQ(go_atoi("-7").value, -7);
+  CHECK_EQ(go_atoi("+7").value, 7);
+  CHECK_EQ(go_atoi("9223372036854775807").value, INT64_MAX);
+  CHECK(!go_atoi("").ok());
+  CHECK(!go_atoi("1_0").ok());
+  CHECK(!go_atoi(" 1").ok());
+  auto r = go_atoi("9223372036854775808");
+  CHECK(!r.ok());
+  CHECK_EQ(r.status.message(), std::string("strconv.Atoi: parsing \"9223372036854775808\": value out of range"));
+}
+
+TEST(int32_wrap) {
+  CHECK_EQ(go_int32(INT64_C(4294967299)), 3);
+  CHECK_EQ(wrap_add32(INT32_MAX, 1), INT32_MIN);
+  CHECK_EQ(wrap_sub32(INT32_MIN, 1), INT32_MAX);
+}
+
+TEST(json_splice_replicas) {
+  std::string raw = R"({"kind":"Deployment","metadata":{"resourceVersion":"12"},"spec":{"replicas":3,"x":1}})";
+  auto s = set_spec_replicas(raw, 5);
+  CHECK(s.ok());
+  auto o = parse_scale_object(s.value, false);
+  CHECK(o.ok() && o.value.replicas == 5 && o.value.resource_version == "12");
+  auto s2 = set_spec_replicas(R"({"spec":{}})", 2);
+  CHECK(s2.ok() && parse_scale_object(s2.value, false).value.replicas == 2);
+  auto scale = parse_scale_object(R"({"kind":"Scale","spec":{}})", true);
+  CHECK(scale.ok() && scale.value.has_replicas && scale.value.replicas == 0);
+  CHECK(!json_parse("{\"a\":").ok());
+}
+
+TEST(xml_attributes) {
+  auto a = xml_sqs_attributes(
+      "<GetQueueAttributesResult><Attribute><Name>A</Name><Value>1</Value></Attribute>"
+      "<Attribute><Name>B&amp;C</Name><Value>&lt;2&gt;</Value></Attribute></GetQueueAttributesResult>");
+  CHECK_EQ(a.size(), size_t(2));
+  CHECK(a[1].first == "B&C" && a[1].second == "<2>");
+}
+
+TEST(sigv4_published_vector) {
+  SigV4Signer s("us-east-1", "service");
+  Credentials c;
+  c.access_key_id = "AKIDEXAMPLE";
+  c.secret_access_key = "wJalrXUtnFEMI/K7MDENG+bPxRfiCYEXAMPLEKEY";
+  Headers h{{"Host", "example.amazonaws.com"}};
+  SignDebug d;
+  s.sign(c, INT64_C(1440938160) * kSecond, "GET", "/", "", &h, "", &d);
+  CHECK_EQ(d.signature, std::string("5fa00fa31553b73ebf1942676e86291e8372ff2a2260956d9b8aae1d763fbf31"));
+  CHECK(sigv4_verify("GET", "/", "", h, "", "AKIDEXAMPLE", c.secret_access_key, "us-east-1", "service").ok());
+}
+
+TEST(logger_text_format) {
+  Logger l;
+  CHECK_EQ(l.format(Level::Info, "Found 3 messages in the queue", {}, INT64_C(1700000000) * kSecond),
+           std::string("time=\"2023-11-14T22:13:20Z\" level=info msg=\"Found 3 messages in the queue\""));
+}
+
+// Appendix C, config C2: UP at 60..120 s, DOWN at 180..360 s every 30 s.
+TEST(runner_c2_golden_virtual_clock) {
+  auto clock = std::make_shared<VirtualClock>(0);
+  auto api = std::make_shared<TraceSqsApi>(
+      clock, std::vector<std::pair<Nanos, AttrMap>>{{0, attrs(0)}, {60 * kSecond, attrs(200)}, {180 * kSecond, attrs(0)}},
+      kMillisecond);
+  auto fake = std::make_shared<FakeDeployments>("default");
+  fake->add("w", 1);
+  fake->set_latency(clock, kMillisecond);
+  auto log = quiet_logger();
+  auto sqs = std::make_shared<SqsClient>(api, "q", default_attribute_names());
+  auto scaler = std::make_shared<PodAutoScaler>(fake, "w", "default", 8, 1, 1, 1, log, clock);
+  Runner r(LoopConfig{}, sqs, scaler, clock, log);
+  r.arm();
+  std::vector<std::pair<int64_t, int>> ups, downs;
+  for (int i = 0; i < 100; ++i) {
+    auto rec = r.step();
+    if (rec.up == Action::Scaled) ups.emplace_back(rec.t_poll / kSecond, rec.replicas_after);
+    if (rec.down == Action::Scaled) downs.emplace_back(rec.t_poll / kSecond, rec.replicas_after);
+  }
+  CHECK_EQ(ups.size(), size_t(7));
+  CHECK_EQ(downs.size(), size_t(7));
+  for (size_t i = 0; i < ups.size() && i < 7; ++i) {
+    CHECK_EQ(ups[i].first, int64_t(60 + 10 * i));
+    CHECK_EQ(ups[i].second, int(2 + i));
+  }
+  for (size_t i = 0; i < downs.size() && i < 7; ++i) {
+    CHECK_EQ(downs[i].first, int64_t(180 + 30 * i));
+    CHECK_EQ(downs[i].second, int(7 - i));
+  }
+  CHECK_EQ(fake->replicas("w"), 1);
+}
+
+TEST(http_keepalive_roundtrips) {
+  std::atomic<int> served{0};
+  HttpServer srv([&](const HttpRequest& req, HttpResponse* resp) {
+    served++;
+    resp->status = 200;
+    resp->body = req.method + " " + req.target + " " + req.body;
+  });
+  CHECK(srv.listen("127.0.0.1", 0).ok());
+  auto u = parse_url("http://127.0.0.1:" + std::to_string(srv.port()));
+  HttpClient c(u.value, TlsOptions{}, 5 * kSecond);
+  for (int i = 0; i < 50; ++i) {
+    HttpRequest req;
+    req.method = "POST";
+    req.target = "/x?i=" + std::to_string(i);
+    req.body = std::string(1000 + i, 'b');
+    HttpResponse resp;
+    CHECK(c.round_trip(req, &resp).ok());
+    CHECK_EQ(resp.status, 200);
+    CHECK_EQ(resp.body.size(), std::string("POST /x?i=" + std::to_string(i) + " ").size() + 1000 + i);
+  }
+  CHECK_EQ(c.stats().connects, uint64_t(1));
+  srv.drop_connections();
+  HttpRequest req;
+  HttpResponse resp;
+  CHECK(c.round_trip(req, &resp).ok());  // transparent reconnect
+  CHECK_EQ(c.stats().connects, uint64_t(2));
+  srv.stop();
+}
+
+TEST(http_tls_roundtrip) {
+  std::string cert, key;
+  CHECK(generate_self_signed("127.0.0.1", &cert, &key).ok());
+  HttpServer srv([](const HttpRequest&, HttpResponse* resp) {
+    resp->status = 200;
+    resp->body = "tls-ok";
+  });
+  CHECK(srv.enable_tls(cert, key).ok());
+  CHECK(srv.listen("127.0.0.1", 0).ok());
+  auto u = parse_url("https://127.0.0.1:" + std::to_string(srv.port()));
+  TlsOptions tls;
+  tls.ca_pem = cert;
+  HttpClient c(u.value, tls, 5 * kSecond);
+  for (int i = 0; i < 5; ++i) {
+    HttpRequest req;
+    HttpResponse resp;
+    CHECK(c.round_trip(req, &resp).ok());
+    CHECK_EQ(resp.body, std::string("tls-ok"));
+  }
+  HttpClient bad(u.value, TlsOptions{}, 5 * kSecond);  // no CA: must fail verification
+  HttpRequest req;
+  HttpResponse resp;
+  CHECK(!bad.round_trip(req, &resp).ok());
+  srv.stop();
+}
+
+TEST(http_timeout) {
+  HttpServer srv([](const HttpRequest&, HttpResponse* resp) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(300));
+    resp->status = 200;
+  });
+  CHECK(srv.listen("127.0.0.1", 0).ok());
+  auto u = parse_url("http://127.0.0.1:" + std::to_string(srv.port()));
+  HttpClient c(u.value, TlsOptions{}, 50 * kMillisecond);
+  HttpRequest req;
+  HttpResponse resp;
+  CHECK(!c.round_trip(req, &resp).ok());
+  srv.stop();
+}
+
+// Eight queues on eight native worker threads against shared threaded fake servers: the
+// concurrency the reference never ran under a race detector.
+TEST(supervisor_multi_queue_over_wire) {
+  FakeSqsServer sqs;
+  sqs.require_signature("AKID", "SECRET", "us-east-1");
+  CHECK(sqs.start().ok());
+  FakeKubeServer kube;
+  kube.require_token("tok");
+  CHECK(kube.start().ok());
+  auto clock = std::make_shared<RealClock>();
+  auto log = quiet_logger();
+  Credentials cr;
+  cr.access_key_id = "AKID";
+  cr.secret_access_key = "SECRET";
+  auto creds = std::make_shared<StaticCredentialsProvider>(cr);
+  Supervisor sup;
+  const int kQueues = 8, kIters = 40;
+  for (int q = 0; q < kQueues; ++q) {
+    std::string url = sqs.url() + "/1/q" + std::to_string(q);
+    sqs.set_attribute_cycle(url, {attrs(150), attrs(0)});
+    kube.add_deployment("ns", "w" + std::to_string(q), 1);
+    SqsHttpOptions so;
+    so.region = "us-east-1";
+    so.endpoint = sqs.url();
+    so.protocol = (q % 2) ? SqsProtocol::Json : SqsProtocol::Query;
+    auto api = std::make_shared<HttpSqsApi>(so, creds, clock);
+    KubeOptions ko;
+    ko.server = kube.url();
+    ko.namespace_ = "ns";
+    ko.mode = static_cast<ScaleMode>(q % 3);
+    ko.token = std::make_shared<StaticTokenProvider>("tok");
+    auto dep = std::make_shared<KubeRestDeployments>(ko);
+    auto scaler = std::make_shared<PodAutoScaler>(dep, "w" + std::to_string(q), "ns", 8, 1, 1, 1, log, clock);
+    LoopConfig lc;
+    lc.poll_period = 0;
+    lc.scale_up_cool_down = 0;
+    lc.scale_down_cool_down = 0;
+    sup.add(std::make_shared<Runner>(lc, std::make_shared<SqsClient>(api, url, default_attribute_names()), scaler,
+                                     clock, log));
+  }
+  sup.start(kIters);
+  CHECK(sup.wait(60 * kSecond));
+  sup.join();
+  for (int q = 0; q < kQueues; ++q) {
+    auto st = sup.runner(q)->stats();
+    CHECK_EQ(st.polls, uint64_t(kIters));
+    CHECK_EQ(st.scale_ups, uint64_t(kIters / 2));
+    CHECK_EQ(st.scale_downs, uint64_t(kIters / 2));
+    CHECK_EQ(kube.replicas("ns", "w" + std::to_string(q)), 1);
+    CHECK_EQ(sup.runner(q)->latencies().size(), size_t(kIters));
+  }
+  CHECK_EQ(sqs.signature_failures(), uint64_t(0));
+  sqs.stop();
+  kube.stop();
+}
+
+TEST(supervisor_stop_interrupts_sleep) {
+  auto clock = std::make_shared<RealClock>();
+  auto log = quiet_logger();
+  auto api = std::make_shared<MockSqsApi>(attrs(0));
+  auto fake = std::make_shared<FakeDeployments>("ns");
+  fake->add("w", 1);
+  Supervisor sup;
+  LoopConfig lc;
+  lc.poll_period = 3600 * kSecond;
+  for (int i = 0; i < 4; ++i)
+    sup.add(std::make_shared<Runner>(lc, std::make_shared<SqsClient>(api, "q", default_attribute_names()),
+                                     std::make_shared<PodAutoScaler>(fake, "w", "ns", 8, 1, 1, 1, log, clock), clock,
+                                     log));
+  sup.start();
+  CHECK(!sup.wait(50 * kMillisecond));
+  sup.stop();
+  CHECK(sup.wait(5 * kSecond));
+  sup.join();
+  CHECK_EQ(api->calls(), uint64_t(0));
+}
+
+TEST(concurrent_logger_lines_are_whole) {
+  auto lines = std::make_shared<std::vector<std::string>>();
+  auto mu = std::make_shared<std::mutex>();
+  auto log = std::make_shared<Logger>();
+  log->set_sink([lines, mu](const std::string& l) {
+    std::lock_guard<std::mutex> g(*mu);
+    lines->push_back(l);
+  });
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([log, t] {
+      auto child = log->with_fields({{"queue", "q" + std::to_string(t)}});
+      for (int i = 0; i < 200; ++i) child->info("Found " + std::to_string(i) + " messages in the queue");
+    });
+  for (auto& t : ts) t.join();
+  CHECK_EQ(lines->size(), size_t(1600));
+  for (auto& l : *lines) CHECK(l.rfind("time=\"", 0) == 0 && l.find(" queue=q") != std::string::npos);
+}
+
+}  // namespace
+
+int main() {
+  for (auto& t : registry()) {
+    int before = g_failed;
+    t.fn();
+    std::fprintf(stderr, "[%s] %s\n", g_failed == before ? " ok " : "FAIL", t.name);
+  }
+  std::fprintf(stderr, "%d checks, %d failed\n", g_checks, g_failed);
+  return g_failed ? 1 : 0;
+}

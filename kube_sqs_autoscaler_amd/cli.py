@@ -107,5 +107,10 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     return 0
 
 
+def main_entry() -> None:
+    """Console-script entry point (``kube-sqs-autoscaler`` on PATH, like the reference binary)."""
+    sys.exit(main())
+
+
 if __name__ == "__main__":
     sys.exit(main())
