@@ -51,6 +51,7 @@ def main(argv=None) -> int:
     ap.add_argument("--queues", type=int, default=1, help="tracked queues per rank")
     ap.add_argument("--mode", default="scale", choices=["scale", "deployment", "patch"])
     ap.add_argument("--no-sweep", action="store_true", help="skip the 1/2/4/8-queue sweep (single rank only)")
+    ap.add_argument("--no-pipeline", action="store_true", help="strictly sequential SQS -> GET -> write")
     args = ap.parse_args(argv)
 
     import torch
@@ -76,7 +77,8 @@ def main(argv=None) -> int:
     from kube_sqs_autoscaler_amd.ops import native
 
     native()  # build/load before timing
-    env = BenchEnv(args.queues, args.mode)
+    pipeline = not args.no_pipeline
+    env = BenchEnv(args.queues, args.mode, pipeline=pipeline)
     try:
         if args.warmup:
             env.run(args.warmup)
@@ -115,6 +117,7 @@ def main(argv=None) -> int:
             "samples": len(all_ns),
             "tracked_queues": args.queues * world,
             "scale_mode": args.mode,
+            "pipeline_reads": pipeline,
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
@@ -122,10 +125,12 @@ def main(argv=None) -> int:
         if world == 1 and not args.no_sweep:
             sweep = {}
             for q in (1, 2, 4, 8):
-                r = measure(q, min(args.steps, 2000), min(args.warmup, 200), args.mode)
+                r = measure(q, min(args.steps, 2000), min(args.warmup, 200), args.mode, pipeline=pipeline)
                 sweep[str(q)] = r.summary()["p50_ms"]
             extra["p50_ms_by_tracked_queues"] = sweep
-            ref = measure(1, min(args.steps, 2000), min(args.warmup, 200), "deployment")
+            seq = measure(1, min(args.steps, 2000), min(args.warmup, 200), args.mode, pipeline=False)
+            extra["sequential_scale_p50_ms"] = seq.summary()["p50_ms"]
+            ref = measure(1, min(args.steps, 2000), min(args.warmup, 200), "deployment", pipeline=False)
             extra["reference_equivalent_p50_ms"] = ref.summary()["p50_ms"]
         extra["decision_parity"] = _parity_summary()
         out = {

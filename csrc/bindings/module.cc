@@ -139,6 +139,7 @@ py::dict record_dict(const IterationRecord& r) {
   d["down"] = action_name(r.down);
   d["replicas_before"] = r.replicas_before;
   d["replicas_after"] = r.replicas_after;
+  d["prefetched"] = r.prefetched;
   d["depth_ns"] = r.depth_ns;
   d["get_ns"] = r.get_ns;
   d["update_ns"] = r.update_ns;
@@ -533,6 +534,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("fail_next_get", &FakeDeployments::fail_next_get)
       .def("fail_next_update", &FakeDeployments::fail_next_update)
       .def("conflict_next", &FakeDeployments::conflict_next)
+      .def("enable_pipelining", &FakeDeployments::enable_pipelining)
       .def("gets", &FakeDeployments::gets)
       .def("updates", &FakeDeployments::updates);
 
@@ -542,6 +544,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readonly("read", &ScaleSpan::read)
       .def_readonly("wrote", &ScaleSpan::wrote)
       .def_readonly("before", &ScaleSpan::before)
+      .def_readonly("used_prefetch", &ScaleSpan::used_prefetch)
+      .def_readonly("refetched", &ScaleSpan::refetched)
       .def_readonly("after", &ScaleSpan::after);
 
   py::class_<PodAutoScaler, std::shared_ptr<PodAutoScaler>>(m, "PodAutoScaler")
@@ -559,6 +563,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         if (!s.ok()) raise_status(s);
         return span;
       })
+      .def("prefetch", &PodAutoScaler::prefetch)
+      .def("discard_prefetch", &PodAutoScaler::discard_prefetch)
       .def("scale_down", [](PodAutoScaler& p) {
         ScaleSpan span;
         Status s;
@@ -584,7 +590,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("scale_down_cool_down_ns", &LoopConfig::scale_down_cool_down)
       .def_readwrite("scale_up_cool_down_ns", &LoopConfig::scale_up_cool_down)
       .def_readwrite("scale_up_messages", &LoopConfig::scale_up_messages)
-      .def_readwrite("scale_down_messages", &LoopConfig::scale_down_messages);
+      .def_readwrite("scale_down_messages", &LoopConfig::scale_down_messages)
+      .def_readwrite("prefetch", &LoopConfig::prefetch);
 
   py::class_<Runner, std::shared_ptr<Runner>>(m, "Runner")
       .def(py::init<LoopConfig, std::shared_ptr<SqsClient>, std::shared_ptr<PodAutoScaler>, std::shared_ptr<Clock>,

@@ -606,8 +606,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   return Status::OK();
 }
 
-Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
-                           bool* retryable) {
+Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable) {
   *retryable = false;
   if (!conn_) {
     Status s = connect_locked(deadline_ns);
@@ -639,7 +638,15 @@ Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t d
     return s;
   }
   stats_.bytes_out += wire.size();
+  return Status::OK();
+}
 
+Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
+                                 bool* retryable) {
+  *retryable = false;
+  if (!conn_) return Status::Err("connection closed before the response");
+  const bool reused = conn_->uses > 1;
+  Status s;
   Reader rd(conn_->stream.get(), &conn_->rbuf);
   std::string head;
   bool got_any = false;
@@ -694,8 +701,16 @@ Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t d
   return Status::OK();
 }
 
+Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
+                           bool* retryable) {
+  Status s = write_request(req, deadline_ns, retryable);
+  if (!s.ok()) return s;
+  return read_response(req, resp, deadline_ns, retryable);
+}
+
 Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) {
   std::lock_guard<std::mutex> lk(mu_);
+  if (in_flight_) return Status::Err("http: a pipelined request is still in flight");
   const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
   stats_.requests++;
   bool retryable = false;
@@ -705,6 +720,42 @@ Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) {
     s = attempt(req, resp, deadline, &retryable);
   }
   return s;
+}
+
+Status HttpClient::send(const HttpRequest& req) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (in_flight_) return Status::Err("http: a pipelined request is still in flight");
+  const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
+  stats_.requests++;
+  bool retryable = false;
+  Status s = write_request(req, deadline, &retryable);
+  if (!s.ok() && retryable) {
+    stats_.reconnect_retries++;
+    s = write_request(req, deadline, &retryable);
+  }
+  if (!s.ok()) return s;
+  pending_ = req;
+  pending_deadline_ = deadline;
+  in_flight_ = true;
+  return Status::OK();
+}
+
+Status HttpClient::receive(HttpResponse* resp) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!in_flight_) return Status::Err("http: no request in flight");
+  in_flight_ = false;
+  bool retryable = false;
+  Status s = read_response(pending_, resp, pending_deadline_, &retryable);
+  if (!s.ok() && retryable) {  // the reused connection was dead: replay on a fresh one
+    stats_.reconnect_retries++;
+    s = attempt(pending_, resp, pending_deadline_, &retryable);
+  }
+  return s;
+}
+
+bool HttpClient::in_flight() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return in_flight_;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -86,6 +86,14 @@ class HttpClient {
   // response byte arrived, reconnects and retries once (what Go's transport does for
   // requests that are safe to replay).
   Status round_trip(const HttpRequest& req, HttpResponse* resp);
+  // Pipelined use: send() writes the request and returns at once; receive() reads its
+  // response. Between the two the caller is free to do other I/O -- the control loop sends the
+  // Deployment GET, then makes the SQS call on another connection, so both round trips overlap.
+  // One request may be in flight per client. A dead reused connection is replayed once, as in
+  // round_trip().
+  Status send(const HttpRequest& req);
+  Status receive(HttpResponse* resp);
+  bool in_flight() const;
   void close();
   HttpClientStats stats() const;
   const Url& origin() const { return origin_; }
@@ -96,6 +104,9 @@ class HttpClient {
   Status connect_locked(int64_t deadline_ns);
   Status attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
                  bool* retryable);
+  Status write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable);
+  Status read_response(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
+                       bool* retryable);
 
   Url origin_;
   TlsOptions tls_;
@@ -105,6 +116,9 @@ class HttpClient {
   mutable std::mutex mu_;
   std::unique_ptr<Conn> conn_;
   HttpClientStats stats_;
+  bool in_flight_ = false;
+  HttpRequest pending_;
+  int64_t pending_deadline_ = 0;
 };
 
 // Threaded HTTP/1.1 server (accept thread + one thread per connection). Used by the fake

@@ -167,8 +167,7 @@ std::string base64(const std::string& in) {
 
 }  // namespace
 
-Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest* req,
-                                       HttpResponse* resp, const std::string& name) {
+Status KubeRestDeployments::add_auth(HttpRequest* req) {
   req->headers.emplace_back("Accept", "application/json, */*");
   if (opts_.token) {
     auto t = opts_.token->token();
@@ -178,20 +177,64 @@ Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest
     req->headers.emplace_back("Authorization",
                               "Basic " + base64(opts_.basic_user + ":" + opts_.basic_password));
   }
-  Status s = http_->round_trip(*req, resp);
-  if (!s.ok()) {
-    std::string m = req->method;
+  return Status::OK();
+}
+
+Status KubeRestDeployments::check_response(const std::string& verb_desc, const HttpRequest& req,
+                                           const HttpResponse& resp, const std::string& name,
+                                           const Status& transport) {
+  if (!transport.ok()) {
+    std::string m = req.method;
     std::string verb = m.substr(0, 1) + std::string(m.begin() + 1, m.end());
     for (size_t i = 1; i < verb.size(); ++i) verb[i] = static_cast<char>(std::tolower(verb[i]));
-    return Status::Err(verb + " \"" + url_.origin() + req->target + "\": " + s.message());
+    return Status::Err(verb + " \"" + url_.origin() + req.target + "\": " + transport.message());
   }
-  if (resp->status < 200 || resp->status >= 300) {
+  if (resp.status < 200 || resp.status >= 300) {
     const std::string resource = "deployments.apps";
     std::lock_guard<std::mutex> lk(mu_);
-    if (resp->status == 409) stats_.conflicts++;
-    return Status::Err(kube_error_message(*resp, verb_desc, name, resource), resp->status);
+    if (resp.status == 409) stats_.conflicts++;
+    return Status::Err(kube_error_message(resp, verb_desc, name, resource), resp.status);
   }
   return Status::OK();
+}
+
+Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest* req,
+                                       HttpResponse* resp, const std::string& name) {
+  Status a = add_auth(req);
+  if (!a.ok()) return a;
+  return check_response(verb_desc, *req, *resp, name, http_->round_trip(*req, resp));
+}
+
+Result<ScaleObject> KubeRestDeployments::parse_get(const Status& s, const HttpResponse& resp) {
+  if (!s.ok()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.errors++;
+    return Result<ScaleObject>::Err(s);
+  }
+  return parse_scale_object(resp.body, opts_.mode != ScaleMode::Deployment);
+}
+
+bool KubeRestDeployments::begin_get(const std::string& name) {
+  if (!init_status_.ok() || name.empty() || http_->in_flight()) return false;
+  HttpRequest req;
+  req.method = "GET";
+  req.target = path_for(name);
+  if (!add_auth(&req).ok()) return false;
+  if (!http_->send(req).ok()) return false;  // the synchronous GET will report the error
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.gets++;
+  }
+  pending_name_ = name;
+  pending_req_ = std::move(req);
+  return true;
+}
+
+Result<ScaleObject> KubeRestDeployments::finish_get() {
+  if (!http_->in_flight()) return Result<ScaleObject>::Err(Status::Err("no pipelined GET in flight"));
+  HttpResponse resp;
+  Status t = http_->receive(&resp);
+  return parse_get(check_response("get", pending_req_, resp, pending_name_, t), resp);
 }
 
 Result<ScaleObject> KubeRestDeployments::get(const std::string& name) {
@@ -205,15 +248,7 @@ Result<ScaleObject> KubeRestDeployments::get(const std::string& name) {
   req.method = "GET";
   req.target = path_for(name);
   HttpResponse resp;
-  Status s = do_request("get", &req, &resp, name);
-  if (!s.ok()) {
-    std::lock_guard<std::mutex> lk(mu_);
-    stats_.errors++;
-    return Result<ScaleObject>::Err(s);
-  }
-  auto o = parse_scale_object(resp.body, opts_.mode != ScaleMode::Deployment);
-  if (!o.ok()) return Result<ScaleObject>::Err(o.status);
-  return o;
+  return parse_get(do_request("get", &req, &resp, name), resp);
 }
 
 Status KubeRestDeployments::update(const std::string& name, const ScaleObject& fetched,
@@ -268,10 +303,8 @@ void FakeDeployments::add_without_replicas(const std::string& name) {
   objs_[name] = o;
 }
 
-Result<ScaleObject> FakeDeployments::get(const std::string& name) {
-  std::lock_guard<std::mutex> lk(mu_);
+Result<ScaleObject> FakeDeployments::get_locked(const std::string& name) {
   gets_++;
-  if (clock_) clock_->advance(latency_);
   if (fail_get_ > 0) {
     fail_get_--;
     return Result<ScaleObject>::Err(Status::Err(fail_get_msg_, 500));
@@ -288,6 +321,34 @@ Result<ScaleObject> FakeDeployments::get(const std::string& name) {
     it->second.rv = ++rv_counter_;  // a concurrent writer (e.g. the deployment controller)
   }
   return Result<ScaleObject>::Ok(o);
+}
+
+Result<ScaleObject> FakeDeployments::get(const std::string& name) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (clock_) clock_->advance(latency_);
+  return get_locked(name);
+}
+
+void FakeDeployments::enable_pipelining(bool on) {
+  std::lock_guard<std::mutex> lk(mu_);
+  pipelining_ = on;
+}
+
+bool FakeDeployments::begin_get(const std::string& name) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!pipelining_ || pending_) return false;
+  pending_result_ = get_locked(name);  // the server reads the object when the request arrives
+  pending_done_at_ = clock_ ? clock_->now() + latency_ : 0;
+  pending_ = true;
+  return true;
+}
+
+Result<ScaleObject> FakeDeployments::finish_get() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!pending_) return Result<ScaleObject>::Err(Status::Err("no pipelined GET in flight"));
+  pending_ = false;
+  if (clock_ && clock_->now() < pending_done_at_) clock_->advance(pending_done_at_ - clock_->now());
+  return pending_result_;
 }
 
 Status FakeDeployments::update(const std::string& name, const ScaleObject& fetched,
@@ -376,68 +437,89 @@ PodAutoScaler::PodAutoScaler(std::shared_ptr<DeploymentApi> api, std::string dep
       log_(std::move(log)),
       clock_(std::move(clock)) {}
 
-Status PodAutoScaler::scale_up(ScaleSpan* span) {
-  Nanos t0 = clock_->now();
-  auto d = api_->get(deployment_);
-  Nanos t1 = clock_->now();
-  if (span) span->get_ns = t1 - t0;
-  if (!d.ok()) return d.status.wrap("Failed to get deployment from kube server, no scale up occurred");
-  if (!d.value.has_replicas)  // the reference dereferences a nil pointer here (scale.go:60)
-    return Status::Err("deployment has no spec.replicas")
-        .wrap("Failed to get deployment from kube server, no scale up occurred");
-  const int32_t cur = d.value.replicas;
-  if (span) {
-    span->read = true;
-    span->before = span->after = cur;
-  }
-  const int32_t max32 = go_int32(max_);
-  if (cur >= max32) {
-    log_->info("More than max pods running. No scale up. Replicas: " + std::to_string(cur));
-    return Status::OK();
-  }
-  int32_t next = wrap_add32(cur, go_int32(up_));
-  if (next > max32) next = max32;
-  Status s = api_->update(deployment_, d.value, next);
-  if (span) {
-    span->update_ns = clock_->now() - t1;
-    span->wrote = s.ok();
-    if (s.ok()) span->after = next;
-  }
-  if (!s.ok()) return s.wrap("Failed to scale up");
-  log_->info("Scale up successful. Replicas: " + std::to_string(next));
-  return Status::OK();
+bool PodAutoScaler::prefetch() {
+  if (prefetch_pending_) return true;
+  prefetch_pending_ = api_->begin_get(deployment_);
+  return prefetch_pending_;
 }
 
-Status PodAutoScaler::scale_down(ScaleSpan* span) {
+void PodAutoScaler::discard_prefetch() {
+  if (!prefetch_pending_) return;
+  prefetch_pending_ = false;
+  (void)api_->finish_get();  // drain the response so the connection stays in sync
+}
+
+Result<ScaleObject> PodAutoScaler::read(ScaleSpan* span, bool* from_prefetch) {
+  *from_prefetch = false;
+  if (prefetch_pending_) {
+    prefetch_pending_ = false;
+    auto r = api_->finish_get();
+    if (r.ok()) {
+      *from_prefetch = true;
+      return r;
+    }
+    // A failed speculative read is not reported: fall through to the reference's own GET.
+  }
+  return api_->get(deployment_);
+}
+
+Status PodAutoScaler::scale(bool up, ScaleSpan* span) {
+  ScaleSpan local;
+  if (!span) span = &local;
+  const std::string dir = up ? "up" : "down";
+  const std::string get_ctx = "Failed to get deployment from kube server, no scale " + dir + " occurred";
   Nanos t0 = clock_->now();
-  auto d = api_->get(deployment_);
-  Nanos t1 = clock_->now();
-  if (span) span->get_ns = t1 - t0;
-  if (!d.ok()) return d.status.wrap("Failed to get deployment from kube server, no scale down occurred");
-  if (!d.value.has_replicas)
-    return Status::Err("deployment has no spec.replicas")
-        .wrap("Failed to get deployment from kube server, no scale down occurred");
-  const int32_t cur = d.value.replicas;
-  if (span) {
+  bool from_prefetch = false;
+  auto d = read(span, &from_prefetch);
+  span->get_ns = clock_->now() - t0;
+  span->used_prefetch = from_prefetch;
+  for (int attempt = 0;; ++attempt) {
+    if (!d.ok()) return d.status.wrap(get_ctx);
+    if (!d.value.has_replicas)  // the reference dereferences a nil pointer here (scale.go:60,87)
+      return Status::Err("deployment has no spec.replicas").wrap(get_ctx);
+    const int32_t cur = d.value.replicas;
     span->read = true;
     span->before = span->after = cur;
-  }
-  const int32_t min32 = go_int32(min_);
-  if (cur <= min32) {
-    log_->info("Less than min pods running. No scale down. Replicas: " + std::to_string(cur));
+    int32_t next;
+    if (up) {
+      const int32_t max32 = go_int32(max_);  // scale.go:62-69
+      if (cur >= max32) {
+        log_->info("More than max pods running. No scale up. Replicas: " + std::to_string(cur));
+        return Status::OK();
+      }
+      next = wrap_add32(cur, go_int32(up_));
+      if (next > max32) next = max32;
+    } else {
+      const int32_t min32 = go_int32(min_);  // scale.go:89-97
+      if (cur <= min32) {
+        log_->info("Less than min pods running. No scale down. Replicas: " + std::to_string(cur));
+        return Status::OK();
+      }
+      next = wrap_sub32(cur, go_int32(down_));
+      if (next < min32) next = min32;
+    }
+    Nanos tw = clock_->now();
+    Status s = api_->update(deployment_, d.value, next);
+    span->update_ns += clock_->now() - tw;
+    if (!s.ok() && s.code() == 409 && from_prefetch && attempt == 0) {
+      // The object changed after the pipelined read: re-read and decide again, which is the
+      // reference's GET-after-poll. Only a conflict on this fresh read is reported.
+      Nanos tg = clock_->now();
+      d = api_->get(deployment_);
+      span->get_ns += clock_->now() - tg;
+      span->refetched = true;
+      from_prefetch = false;
+      continue;
+    }
+    span->wrote = s.ok();
+    if (!s.ok()) return s.wrap("Failed to scale " + dir);
+    span->after = next;
+    log_->info("Scale " + dir + " successful. Replicas: " + std::to_string(next));
     return Status::OK();
   }
-  int32_t next = wrap_sub32(cur, go_int32(down_));
-  if (next < min32) next = min32;
-  Status s = api_->update(deployment_, d.value, next);
-  if (span) {
-    span->update_ns = clock_->now() - t1;
-    span->wrote = s.ok();
-    if (s.ok()) span->after = next;
-  }
-  if (!s.ok()) return s.wrap("Failed to scale down");
-  log_->info("Scale down successful. Replicas: " + std::to_string(next));
-  return Status::OK();
 }
+
+Status PodAutoScaler::scale_up(ScaleSpan* span) { return scale(true, span); }      // scale.go:54-79
+Status PodAutoScaler::scale_down(ScaleSpan* span) { return scale(false, span); }  // scale.go:81-107
 
 }  // namespace ksa

@@ -44,6 +44,13 @@ class DeploymentApi {
   virtual Result<ScaleObject> get(const std::string& name) = 0;
   // Writes `fetched` back with spec.replicas = replicas.
   virtual Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) = 0;
+  // Pipelined read: begin_get() starts a GET and returns without waiting (false: not
+  // supported, nothing started); finish_get() returns its result. Implementations that
+  // cannot overlap I/O keep the defaults and the control loop reads synchronously.
+  virtual bool begin_get(const std::string& name) { return false; }
+  virtual Result<ScaleObject> finish_get() {
+    return Result<ScaleObject>::Err(Status::Err("no pipelined GET in flight"));
+  }
 };
 
 class TokenProvider {
@@ -103,12 +110,21 @@ class KubeRestDeployments final : public DeploymentApi {
   explicit KubeRestDeployments(KubeOptions opts);
   Result<ScaleObject> get(const std::string& name) override;
   Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override;
+  bool begin_get(const std::string& name) override;
+  Result<ScaleObject> finish_get() override;
   KubeStats stats() const;
   std::string path_for(const std::string& name) const;
 
  private:
   Status do_request(const std::string& verb_desc, HttpRequest* req, HttpResponse* resp,
                     const std::string& name);
+  Status add_auth(HttpRequest* req);
+  Status check_response(const std::string& verb_desc, const HttpRequest& req, const HttpResponse& resp,
+                        const std::string& name, const Status& transport);
+  Result<ScaleObject> parse_get(const Status& s, const HttpResponse& resp);
+  std::string pending_name_;
+  HttpRequest pending_req_;
+  Status pending_status_;
 
   KubeOptions opts_;
   Status init_status_;
@@ -132,6 +148,12 @@ class FakeDeployments final : public DeploymentApi {
   void add_without_replicas(const std::string& name);
   Result<ScaleObject> get(const std::string& name) override;
   Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override;
+  // Pipelined read in virtual time: the snapshot is taken when the GET starts, and
+  // finish_get() only advances a VirtualClock to start + latency (the GET ran concurrently with
+  // whatever the caller did in between). Disabled unless enable_pipelining(true).
+  bool begin_get(const std::string& name) override;
+  Result<ScaleObject> finish_get() override;
+  void enable_pipelining(bool on);
 
   int32_t replicas(const std::string& name) const;  // -1 if absent
   void set_replicas(const std::string& name, int32_t r);  // out-of-band edit (kubectl scale)
@@ -159,6 +181,11 @@ class FakeDeployments final : public DeploymentApi {
   std::string fail_get_msg_, fail_update_msg_;
   uint64_t gets_ = 0, updates_ = 0;
   uint64_t rv_counter_ = 1000;
+  bool pipelining_ = false;
+  bool pending_ = false;
+  Nanos pending_done_at_ = 0;
+  Result<ScaleObject> pending_result_;
+  Result<ScaleObject> get_locked(const std::string& name);
 };
 
 // Per-call timing of one ScaleUp/ScaleDown (for poll->patch latency spans).
@@ -169,6 +196,8 @@ struct ScaleSpan {
   bool wrote = false;
   int32_t before = 0;
   int32_t after = 0;
+  bool used_prefetch = false;  // the decision used the pipelined GET
+  bool refetched = false;      // the pipelined object was stale (409) and was re-read
 };
 
 class PodAutoScaler {
@@ -178,6 +207,15 @@ class PodAutoScaler {
                 std::shared_ptr<Logger> log, std::shared_ptr<Clock> clock);
   Status scale_up(ScaleSpan* span = nullptr);    // scale.go:54-79
   Status scale_down(ScaleSpan* span = nullptr);  // scale.go:81-107
+
+  // Pipelined read (optimisation, decisions unchanged): prefetch() starts the Deployment GET
+  // before the SQS poll so the two round trips overlap; the next scale_up/scale_down consumes
+  // it instead of issuing its own GET. If the write then fails with 409 (the object changed
+  // after the prefetch) the call re-reads and retries once -- exactly the GET-then-write the
+  // reference would have done at that point. discard_prefetch() drains an unused prefetch.
+  bool prefetch();
+  void discard_prefetch();
+  bool prefetch_pending() const { return prefetch_pending_; }
 
   std::shared_ptr<DeploymentApi> api() const { return api_; }
   const std::string& deployment() const { return deployment_; }
@@ -194,6 +232,10 @@ class PodAutoScaler {
   int64_t max_, min_, up_, down_;
   std::shared_ptr<Logger> log_;
   std::shared_ptr<Clock> clock_;
+  bool prefetch_pending_ = false;
+
+  Result<ScaleObject> read(ScaleSpan* span, bool* from_prefetch);
+  Status scale(bool up, ScaleSpan* span);
 };
 
 }  // namespace ksa

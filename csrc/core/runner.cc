@@ -54,6 +54,8 @@ IterationRecord Runner::step(StopFlag* stop) {
   rec.index = ++index_;
   const Nanos t0 = clock_->now();
   rec.t_poll = t0;
+  // Pipelined read: the Deployment GET goes out before the SQS call and overlaps it.
+  if (cfg_.prefetch) rec.prefetched = scaler_->prefetch();
 
   // main.go:43-47
   auto depth = sqs_->num_messages();
@@ -62,6 +64,7 @@ IterationRecord Runner::step(StopFlag* stop) {
   if (!depth.ok()) {
     rec.error = depth.status.message();
     log_->error("Failed to get SQS messages: " + depth.status.message());
+    scaler_->discard_prefetch();
     rec.total_ns = clock_->now() - t0;
     record(rec);
     return rec;
@@ -72,6 +75,7 @@ IterationRecord Runner::step(StopFlag* stop) {
   log_->info("Found " + std::to_string(n) + " messages in the queue");  // main.go:49
 
   auto finish = [&]() -> IterationRecord& {
+    scaler_->discard_prefetch();  // unused (no action this poll): drain it
     rec.total_ns = clock_->now() - t0;
     record(rec);
     return rec;

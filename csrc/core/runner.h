@@ -41,6 +41,9 @@ struct LoopConfig {
   Nanos scale_up_cool_down = 10 * kSecond;    // --scale-up-cool-down    main.go:85
   int64_t scale_up_messages = 100;            // --scale-up-messages     main.go:86
   int64_t scale_down_messages = 10;           // --scale-down-messages   main.go:87
+  // Overlap the Deployment GET with the SQS poll (PodAutoScaler::prefetch). Decisions are the
+  // reference's; only the read is issued earlier and validated by the write's resourceVersion.
+  bool prefetch = false;                      // --pipeline-reads
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };
@@ -56,6 +59,7 @@ struct IterationRecord {
   Action down = Action::None;
   int32_t replicas_before = -1;  // as read by the last GET of the iteration (-1: not read)
   int32_t replicas_after = -1;
+  bool prefetched = false;     // a pipelined GET was issued with the poll
   Nanos depth_ns = 0;          // SQS GetQueueAttributes round trip
   Nanos get_ns = 0;            // Deployment GET(s)
   Nanos update_ns = 0;         // Deployment PUT/PATCH(es)

@@ -1,7 +1,11 @@
 #include "sigv4.h"
 
-#include <openssl/evp.h>
-#include <openssl/hmac.h>
+// The low-level SHA256_* API is deprecated in OpenSSL 3 but it is the fast path: EVP one-shots
+// pay a provider fetch per call, which dominated signing time (see HmacSha256Key).
+#define OPENSSL_SUPPRESS_DEPRECATED
+#include <openssl/sha.h>
+
+#include <cstring>
 
 #include <algorithm>
 #include <cctype>
@@ -21,19 +25,72 @@ std::string hex_encode(const std::string& raw) {
   return out;
 }
 
+namespace {
+
+void sha256_raw(const void* data, size_t n, unsigned char out[32]) {
+  SHA256_CTX c;
+  SHA256_Init(&c);
+  SHA256_Update(&c, data, n);
+  SHA256_Final(out, &c);
+}
+
+std::string hex32(const unsigned char* md) {
+  static const char* hex = "0123456789abcdef";
+  std::string out(64, '0');
+  for (int i = 0; i < 32; ++i) {
+    out[2 * i] = hex[md[i] >> 4];
+    out[2 * i + 1] = hex[md[i] & 0xF];
+  }
+  return out;
+}
+
+}  // namespace
+
 std::string sha256_hex(const std::string& data) {
-  unsigned char md[EVP_MAX_MD_SIZE];
-  unsigned int len = 0;
-  EVP_Digest(data.data(), data.size(), md, &len, EVP_sha256(), nullptr);
-  return hex_encode(std::string(reinterpret_cast<char*>(md), len));
+  unsigned char md[32];
+  sha256_raw(data.data(), data.size(), md);
+  return hex32(md);
+}
+
+struct HmacSha256Key::State {
+  SHA256_CTX inner, outer;
+};
+
+HmacSha256Key::HmacSha256Key() : HmacSha256Key(std::string()) {}
+
+HmacSha256Key::HmacSha256Key(const std::string& key) : st_(std::make_unique<State>()) {
+  unsigned char k[64] = {0};
+  if (key.size() > 64) sha256_raw(key.data(), key.size(), k);
+  else std::memcpy(k, key.data(), key.size());
+  unsigned char pad[64];
+  for (int i = 0; i < 64; ++i) pad[i] = k[i] ^ 0x36;
+  SHA256_Init(&st_->inner);
+  SHA256_Update(&st_->inner, pad, 64);
+  for (int i = 0; i < 64; ++i) pad[i] = k[i] ^ 0x5c;
+  SHA256_Init(&st_->outer);
+  SHA256_Update(&st_->outer, pad, 64);
+}
+
+HmacSha256Key::HmacSha256Key(const HmacSha256Key& o) : st_(std::make_unique<State>(*o.st_)) {}
+HmacSha256Key& HmacSha256Key::operator=(const HmacSha256Key& o) {
+  if (this != &o) *st_ = *o.st_;
+  return *this;
+}
+HmacSha256Key::~HmacSha256Key() = default;
+
+std::string HmacSha256Key::mac(const std::string& data) const {
+  SHA256_CTX c = st_->inner;
+  unsigned char in[32], out[32];
+  SHA256_Update(&c, data.data(), data.size());
+  SHA256_Final(in, &c);
+  c = st_->outer;
+  SHA256_Update(&c, in, 32);
+  SHA256_Final(out, &c);
+  return std::string(reinterpret_cast<char*>(out), 32);
 }
 
 std::string hmac_sha256(const std::string& key, const std::string& data) {
-  unsigned char md[EVP_MAX_MD_SIZE];
-  unsigned int len = 0;
-  HMAC(EVP_sha256(), key.data(), static_cast<int>(key.size()),
-       reinterpret_cast<const unsigned char*>(data.data()), data.size(), md, &len);
-  return std::string(reinterpret_cast<char*>(md), len);
+  return HmacSha256Key(key).mac(data);
 }
 
 std::string aws_uri_encode(const std::string& s, bool keep_slash) {
@@ -211,17 +268,30 @@ CanonicalParts sigv4_canonical(const std::string& method, const std::string& pat
   return parts;
 }
 
+namespace {
+std::string derive_key(const std::string& secret, const std::string& date, const std::string& region,
+                       const std::string& service) {
+  std::string k = hmac_sha256("AWS4" + secret, date);
+  k = hmac_sha256(k, region);
+  k = hmac_sha256(k, service);
+  return hmac_sha256(k, "aws4_request");
+}
+}  // namespace
+
 std::string SigV4Signer::signing_key(const std::string& secret, const std::string& date) {
   std::lock_guard<std::mutex> lk(mu_);
   if (!key_.empty() && key_secret_ == secret && key_date_ == date) return key_;
-  std::string k = hmac_sha256("AWS4" + secret, date);
-  k = hmac_sha256(k, region_);
-  k = hmac_sha256(k, service_);
-  k = hmac_sha256(k, "aws4_request");
+  key_ = derive_key(secret, date, region_, service_);
   key_secret_ = secret;
   key_date_ = date;
-  key_ = k;
-  return k;
+  key_mac_ = HmacSha256Key(key_);
+  return key_;
+}
+
+HmacSha256Key SigV4Signer::signing_mac(const std::string& secret, const std::string& date) {
+  signing_key(secret, date);
+  std::lock_guard<std::mutex> lk(mu_);
+  return key_mac_;
 }
 
 void SigV4Signer::sign(const Credentials& creds, int64_t unix_ns, const std::string& method,
@@ -237,7 +307,7 @@ void SigV4Signer::sign(const Credentials& creds, int64_t unix_ns, const std::str
   const std::string scope = date + "/" + region_ + "/" + service_ + "/aws4_request";
   const std::string sts =
       "AWS4-HMAC-SHA256\n" + amzdate + "\n" + scope + "\n" + sha256_hex(parts.canonical_request);
-  const std::string sig = hex_encode(hmac_sha256(signing_key(creds.secret_access_key, date), sts));
+  const std::string sig = hex_encode(signing_mac(creds.secret_access_key, date).mac(sts));
   headers->emplace_back("Authorization", "AWS4-HMAC-SHA256 Credential=" + creds.access_key_id +
                                              "/" + scope + ", SignedHeaders=" +
                                              parts.signed_headers + ", Signature=" + sig);
@@ -297,13 +367,19 @@ Status sigv4_verify(const std::string& method, const std::string& path,
   if (std::find(only.begin(), only.end(), "host") == only.end())
     return Status::Err("SignatureDoesNotMatch: host not signed", 403);
   CanonicalParts parts = sigv4_canonical(method, path, raw_query, headers, &only, sha256_hex(body));
-  std::string k = hmac_sha256("AWS4" + secret, date);
-  k = hmac_sha256(k, region);
-  k = hmac_sha256(k, service);
-  k = hmac_sha256(k, "aws4_request");
+  // Derived keys change once a day per secret: cache the last one per thread (server workers).
+  thread_local std::string c_secret, c_date, c_region, c_service;
+  thread_local HmacSha256Key c_mac;
+  if (c_secret != secret || c_date != date || c_region != region || c_service != service) {
+    c_mac = HmacSha256Key(derive_key(secret, date, region, service));
+    c_secret = secret;
+    c_date = date;
+    c_region = region;
+    c_service = service;
+  }
   const std::string sts = "AWS4-HMAC-SHA256\n" + amzdate + "\n" + want_scope + "\n" +
                           sha256_hex(parts.canonical_request);
-  const std::string want = hex_encode(hmac_sha256(k, sts));
+  const std::string want = hex_encode(c_mac.mac(sts));
   if (want != sig) return Status::Err("SignatureDoesNotMatch", 403);
   return Status::OK();
 }

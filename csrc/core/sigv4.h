@@ -25,6 +25,25 @@ std::string sha256_hex(const std::string& data);
 std::string hmac_sha256(const std::string& key, const std::string& data);  // raw bytes
 std::string hex_encode(const std::string& raw);
 
+// HMAC-SHA256 with the key schedule precomputed: the SHA-256 states after absorbing
+// key^ipad and key^opad are kept, so each MAC costs only the message blocks plus one
+// outer block (~0.3 us for a SigV4 string-to-sign) instead of OpenSSL 3's one-shot HMAC()
+// (~2.5 us of provider dispatch per call). The SigV4 signing key changes once a day, so the
+// signer keeps one of these per (secret, date).
+class HmacSha256Key {
+ public:
+  HmacSha256Key();
+  explicit HmacSha256Key(const std::string& key);
+  HmacSha256Key(const HmacSha256Key&);
+  HmacSha256Key& operator=(const HmacSha256Key&);
+  ~HmacSha256Key();
+  std::string mac(const std::string& data) const;  // raw 32 bytes
+
+ private:
+  struct State;
+  std::unique_ptr<State> st_;
+};
+
 // RFC 3986 percent-encoding of everything outside [A-Za-z0-9-_.~]; '/' kept when
 // `keep_slash` (canonical URI) -- this equals Go's url.QueryEscape with '+' -> "%20".
 std::string aws_uri_encode(const std::string& s, bool keep_slash);
@@ -97,6 +116,8 @@ class SigV4Signer {
 
   // Derived key for (secret, yyyymmdd); cached per day.
   std::string signing_key(const std::string& secret, const std::string& date);
+  // HMAC schedule of that key (what sign() uses).
+  HmacSha256Key signing_mac(const std::string& secret, const std::string& date);
 
   const std::string& region() const { return region_; }
   const std::string& service() const { return service_; }
@@ -105,6 +126,7 @@ class SigV4Signer {
   std::string region_, service_;
   std::mutex mu_;
   std::string key_secret_, key_date_, key_;
+  HmacSha256Key key_mac_;
 };
 
 // Builds the canonical request pieces; shared with the fake server's verifier.

@@ -10,6 +10,10 @@ The wire path is the production one: SigV4-signed ``GetQueueAttributes`` (verifi
 fake), bearer-token kube REST calls with resourceVersion preconditions, real attribute summing
 and clamp arithmetic, info-level logrus lines written to a file descriptor.
 
+Two paths are measured: the optimised default (``/scale`` subresource + pipelined read: the
+Deployment GET overlaps the SQS call) and the reference-equivalent one (full-object GET+PUT,
+strictly sequential -- what /root/reference/scale/scale.go:54-107 does after sqs.go:51).
+
 Trace: the fake serves the BASELINE.json "step trace" 200 -> 0 -> 200 ... one value per poll,
 with scale-up-messages=100 / scale-down-messages=10, min 1 / max 8 and zero poll period and
 cool-downs, so *every* iteration performs SQS + GET + write (the 3-round-trip scaling path of
@@ -39,6 +43,7 @@ class LatencyResult:
     queues: int
     mode: str
     steps: int
+    pipeline: bool = True
     samples: List[int] = field(default_factory=list)  # ns
     wall_s: float = 0.0
     sqs_requests: int = 0
@@ -62,6 +67,7 @@ class LatencyResult:
         return {
             "queues": self.queues,
             "mode": self.mode,
+            "pipeline_reads": self.pipeline,
             "p50_ms": round(self.pct(50), 4),
             "p90_ms": round(self.pct(90), 4),
             "p99_ms": round(self.pct(99), 4),
@@ -74,10 +80,11 @@ class BenchEnv:
     """Fake servers + one worker per queue."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
-                 kube_latency_ns: int = 0, log_fd: Optional[int] = None):
+                 kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True):
         nat = native()
         self.nat = nat
         self.mode = mode
+        self.pipeline = pipeline
         self.sqs = nat.FakeSqsServer()
         self.sqs.require_signature(AKID, SECRET, REGION)
         self.sqs.start("127.0.0.1", 0, tls)
@@ -125,6 +132,7 @@ class BenchEnv:
             cfg.scale_down_cool_down_ns = 0
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
+            cfg.prefetch = pipeline
             self.runners.append(nat.Runner(cfg, client, scaler, self.clock, self.log))
             self.targets.append(t)
 
@@ -139,7 +147,7 @@ class BenchEnv:
         return time.perf_counter() - t0
 
     def collect(self, steps: int, wall: float) -> LatencyResult:
-        res = LatencyResult(queues=len(self.runners), mode=self.mode, steps=steps, wall_s=wall)
+        res = LatencyResult(queues=len(self.runners), mode=self.mode, steps=steps, pipeline=self.pipeline, wall_s=wall)
         for r in self.runners:
             res.samples.extend(r.latencies())
         res.sqs_requests = self.sqs.requests()

@@ -21,6 +21,9 @@ Extensions (all off or reference-equivalent by default):
 * ``--scale-mode``: ``scale`` (autoscaling/v1 ``/scale`` subresource, default), ``deployment``
   (full-object GET+PUT exactly like the reference), ``patch`` (merge patch with a
   resourceVersion precondition).
+* ``--pipeline-reads`` (default on): overlap the Deployment GET with the SQS poll; the write's
+  resourceVersion precondition validates the early read and a conflict re-reads once, so the
+  decisions are the reference's (``models/oracle.py`` ``prefetch``).
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
   ``--log-format``, ``--metrics-addr``, ``--gpu-aware-max``.
 """
@@ -79,6 +82,7 @@ class Config:
     metrics_addr: str = ""
     gpu_aware_max: str = ""
     kube_config_path: str = ""
+    pipeline_reads: bool = True
 
 
 def parse_attribute_names(value: str) -> List[str]:
@@ -118,6 +122,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("sqs-endpoint", "", "Override the SQS endpoint URL (VPC endpoint, local fake); empty uses the regional endpoint")
     fs.string("sqs-protocol", "query", "SQS wire protocol: query (AWS Query/XML) or json (AWS JSON 1.0)")
     fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
+    fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
     fs.string("metrics-addr", "", "Serve Prometheus metrics and /healthz on host:port (disabled when empty)")
@@ -213,6 +218,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         metrics_addr=fs["metrics-addr"],
         gpu_aware_max=fs["gpu-aware-max"],
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
+        pipeline_reads=fs["pipeline-reads"],
     )
     if cfg.scale_mode not in SCALE_MODES:
         raise FlagError(f'invalid value "{cfg.scale_mode}" for flag -scale-mode: must be one of {", ".join(SCALE_MODES)}')

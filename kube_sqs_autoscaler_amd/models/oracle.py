@@ -126,80 +126,94 @@ def simulate(
     init_replicas: int,
     lat: Latency = Latency(),
     faults: Optional[Faults] = None,
+    prefetch: bool = False,
 ) -> List[Event]:
+    """Runs ``polls`` iterations of the reference loop on a virtual clock.
+
+    ``prefetch`` models the pipelined read (``--pipeline-reads``): the Deployment GET is sent
+    with the SQS call, so the first GET of a poll costs ``max(0, get - sqs)`` extra instead of
+    ``get``, and an unused prefetch is drained at the end of the poll. The decision rules are
+    unchanged -- only when ``now`` is read moves.
+    """
     f = faults or Faults()
-    now = 0
-    last_up = now  # main.go:37
-    last_down = now  # main.go:38
-    replicas = int32(init_replicas)
+    st = {"now": 0, "last_up": 0, "last_down": 0, "replicas": int32(init_replicas)}  # main.go:37-38
     out: List[Event] = []
-    for k in range(1, polls + 1):
-        now += max(p.poll_ns, 0)  # main.go:41 time.Sleep (negative/zero: no sleep)
-        ev = Event(index=k, t_poll_ns=now, depth=None)
-        out.append(ev)
-        attrs = sample(trace, now)
-        now += lat.sqs_ns
+
+    def read(k: int, pf: dict, fail_set: Set[int]) -> bool:
+        """One GET; returns False when it fails (injected fault)."""
+        if pf["pending"]:
+            pf["pending"] = False
+            st["now"] = max(st["now"], pf["done"])
+        else:
+            st["now"] += lat.get_ns
+        return k not in fail_set
+
+    def scale(k: int, ev: Event, up: bool, pf: dict) -> bool:
+        """ScaleUp/ScaleDown + timer refresh; False means `continue` (failure)."""
+        if not read(k, pf, f.up_get if up else f.down_get):
+            setattr(ev, "up" if up else "down", "failed")
+            return False
+        r = st["replicas"]
+        if up:
+            if r >= int32(p.max_pods):  # scale.go:62
+                ev.up = "noop"
+            else:
+                nxt = int32(r + int32(p.up_pods))
+                nxt = int32(p.max_pods) if nxt > int32(p.max_pods) else nxt
+                st["now"] += lat.update_ns
+                if k in f.up_update:
+                    ev.up = "failed"
+                    return False
+                st["replicas"] = nxt
+                ev.up = "scaled"
+                ev.up_replicas = nxt
+            st["last_up"] = st["now"]  # main.go:62
+        else:
+            if r <= int32(p.min_pods):  # scale.go:89
+                ev.down = "noop"
+            else:
+                nxt = int32(r - int32(p.down_pods))
+                nxt = int32(p.min_pods) if nxt < int32(p.min_pods) else nxt
+                st["now"] += lat.update_ns
+                if k in f.down_update:
+                    ev.down = "failed"
+                    return False
+                st["replicas"] = nxt
+                ev.down = "scaled"
+            st["last_down"] = st["now"]  # main.go:76
+        return True
+
+    def poll(k: int, ev: Event, pf: dict) -> None:
+        attrs = sample(trace, st["now"])
+        st["now"] += lat.sqs_ns
         if k in f.sqs:
-            ev.replicas = replicas
-            continue
+            return
         try:
             n = depth_of(attrs, names)
         except (ValueError, TypeError):
-            ev.replicas = replicas
-            continue  # main.go:44-47
+            return  # main.go:44-47
         ev.depth = n
-
         if n >= p.up_msgs:  # main.go:51
-            if last_up + p.up_cool_ns > now:  # main.go:52
+            if st["last_up"] + p.up_cool_ns > st["now"]:  # main.go:52
                 ev.up = "cooldown"
-                ev.replicas = replicas
-                continue
-            now += lat.get_ns
-            if k in f.up_get:
-                ev.up = "failed"
-                ev.replicas = replicas
-                continue
-            if replicas >= int32(p.max_pods):  # scale.go:62
-                ev.up = "noop"
-            else:
-                nxt = int32(replicas + int32(p.up_pods))
-                if nxt > int32(p.max_pods):
-                    nxt = int32(p.max_pods)
-                now += lat.update_ns
-                if k in f.up_update:
-                    ev.up = "failed"
-                    ev.replicas = replicas
-                    continue
-                replicas = nxt
-                ev.up = "scaled"
-                ev.up_replicas = replicas
-            last_up = now  # main.go:62
-
+                return
+            if not scale(k, ev, True, pf):
+                return
         if n <= p.down_msgs:  # main.go:65
-            if last_down + p.down_cool_ns > now:  # main.go:66
+            if st["last_down"] + p.down_cool_ns > st["now"]:  # main.go:66
                 ev.down = "cooldown"
-                ev.replicas = replicas
-                continue
-            now += lat.get_ns
-            if k in f.down_get:
-                ev.down = "failed"
-                ev.replicas = replicas
-                continue
-            if replicas <= int32(p.min_pods):  # scale.go:89
-                ev.down = "noop"
-            else:
-                nxt = int32(replicas - int32(p.down_pods))
-                if nxt < int32(p.min_pods):
-                    nxt = int32(p.min_pods)
-                now += lat.update_ns
-                if k in f.down_update:
-                    ev.down = "failed"
-                    ev.replicas = replicas
-                    continue
-                replicas = nxt
-                ev.down = "scaled"
-            last_down = now  # main.go:76
-        ev.replicas = replicas
+                return
+            scale(k, ev, False, pf)
+
+    for k in range(1, polls + 1):
+        st["now"] += max(p.poll_ns, 0)  # main.go:41 time.Sleep (<= 0: no sleep)
+        ev = Event(index=k, t_poll_ns=st["now"], depth=None)
+        out.append(ev)
+        pf = {"pending": prefetch, "done": st["now"] + lat.get_ns}
+        poll(k, ev, pf)
+        if pf["pending"]:  # drain an unused prefetch
+            st["now"] = max(st["now"], pf["done"])
+        ev.replicas = st["replicas"]
     return out
 
 

@@ -102,6 +102,7 @@ def run_native(
     scenario: Scenario,
     faults: Optional[Faults] = None,
     log_sink=None,
+    prefetch: bool = False,
 ) -> List[Event]:
     """Runs ``scenario`` through the native control loop and returns per-poll events."""
     nat = native()
@@ -120,10 +121,13 @@ def run_native(
         kube = nat.FakeDeployments("default")
         kube.add("target", scenario.init_replicas)
         kube.set_latency(clock, lat.get_ns)
+        kube.enable_pipelining(prefetch)
         if lat.update_ns != lat.get_ns:
             raise ValueError("FakeDeployments models one latency for GET and PUT")
         counter = None
     else:
+        if prefetch:
+            raise ValueError("fault-injection parity runs without pipelined reads")
         counter = _PollCounter()
         sqs_api, dep_cls = _faulty_fakes(nat, clock, scenario, faults, counter)
         kube = dep_cls(scenario.init_replicas)
@@ -136,6 +140,7 @@ def run_native(
     cfg.scale_down_cool_down_ns = p.down_cool_ns
     cfg.scale_up_messages = p.up_msgs
     cfg.scale_down_messages = p.down_msgs
+    cfg.prefetch = prefetch
     runner = nat.Runner(cfg, sqs, scaler, clock, log)
     runner.arm()
     if counter is None:
@@ -174,11 +179,12 @@ class ParityResult:
         return self.agree == self.polls
 
 
-def compare(scenario: Scenario, faults: Optional[Faults] = None) -> ParityResult:
+def compare(scenario: Scenario, faults: Optional[Faults] = None, prefetch: bool = False) -> ParityResult:
     ref = simulate(
-        scenario.params, scenario.trace, scenario.names, scenario.polls, scenario.init_replicas, scenario.latency, faults
+        scenario.params, scenario.trace, scenario.names, scenario.polls, scenario.init_replicas, scenario.latency, faults,
+        prefetch=prefetch,
     )
-    got = run_native(scenario, faults)
+    got = run_native(scenario, faults, prefetch=prefetch)
     res = ParityResult(scenario=scenario.name, polls=len(ref), agree=0)
     for a, b in zip(ref, got):
         if a.key() == b.key() and a.t_poll_ns == b.t_poll_ns:

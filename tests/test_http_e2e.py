@@ -223,3 +223,81 @@ def test_full_loop_over_the_wire(nat, sqs_server, kube_server):
     assert all(x["patch_latency_ns"] > 0 for x in recs[:4])
     st = r.stats()
     assert st["scale_ups"] == 2 and st["scale_downs"] == 4 and st["polls"] == 9
+
+
+@pytest.mark.parametrize("mode", ["deployment", "scale", "patch"])
+def test_prefetched_get_is_consumed(nat, kube_server, mode):
+    p, api = scaler(nat, kube_server, mode)
+    gets = kube_server.gets()
+    assert p.prefetch()
+    span = p.scale_up()
+    assert span.used_prefetch and not span.refetched and span.wrote
+    assert kube_server.gets() == gets + 1  # no second GET
+    assert kube_server.replicas("ml", "worker") == 4
+
+
+def test_unused_prefetch_is_drained(nat, kube_server):
+    p, api = scaler(nat, kube_server, "scale")
+    assert p.prefetch()
+    p.discard_prefetch()
+    p.scale_down()  # the connection is still in sync
+    assert kube_server.replicas("ml", "worker") == 2 and kube_server.connections() == 1
+
+
+@pytest.mark.parametrize("mode", ["deployment", "scale", "patch"])
+def test_stale_prefetch_falls_back_to_fresh_read(nat, kube_server, mode):
+    """A write conflict on the prefetched object re-reads and retries once (the reference's
+    GET-after-poll); the caller sees a success, not a 409."""
+    p, api = scaler(nat, kube_server, mode)
+    kube_server.conflict_next(1)  # a concurrent writer right after the prefetched GET
+    assert p.prefetch()
+    span = p.scale_up()
+    assert span.used_prefetch and span.refetched and span.wrote
+    assert kube_server.replicas("ml", "worker") == 4
+    assert kube_server.conflicts() == 1
+
+
+def test_stale_prefetch_reevaluates_bounds(nat, kube_server):
+    """After a conflict the decision is re-made on the fresh object (e.g. now at max -> no-op)."""
+    import time
+
+    p, api = scaler(nat, kube_server, "scale", max_=5)
+    gets = kube_server.gets()
+    assert p.prefetch()  # sees 3
+    while kube_server.gets() == gets:  # the server has answered the pipelined GET
+        time.sleep(0.001)
+    kube_server.set_replicas("ml", "worker", 5)  # someone scaled to max meanwhile
+    span = p.scale_up()
+    assert span.refetched and not span.wrote
+    assert kube_server.replicas("ml", "worker") == 5
+
+
+def test_failed_prefetch_falls_back(nat, kube_server):
+    p, api = scaler(nat, kube_server, "scale")
+    kube_server.inject(1, nat.InjectedFault(500, "flaky"))
+    assert p.prefetch()
+    span = p.scale_up()  # the failed speculative GET is not reported; a fresh GET is made
+    assert not span.used_prefetch and span.wrote
+    assert kube_server.replicas("ml", "worker") == 4
+
+
+def test_full_loop_pipelined_over_the_wire(nat, sqs_server, kube_server):
+    c, _, url = sqs_client(nat, sqs_server)
+    p, _ = scaler(nat, kube_server, "scale", max_=5)
+    cfg = nat.LoopConfig()
+    cfg.poll_period_ns = 0
+    cfg.scale_up_cool_down_ns = 0
+    cfg.scale_down_cool_down_ns = 0
+    cfg.prefetch = True
+    r = nat.Runner(cfg, c, p, nat.RealClock(), capture_logger([]))
+    r.arm()
+    sqs_server.set_attributes(url, {n: "100" for n in NAMES})
+    recs = r.steps(4)
+    assert [x["up"] for x in recs] == ["scaled", "scaled", "noop", "noop"] and all(x["prefetched"] for x in recs)
+    sqs_server.set_attributes(url, {n: "50" for n in NAMES})  # dead band: prefetch drained
+    r.steps(3)
+    sqs_server.set_attributes(url, {n: "0" for n in NAMES})
+    recs = r.steps(5)
+    assert [x["down"] for x in recs] == ["scaled"] * 4 + ["noop"]
+    assert kube_server.replicas("ml", "worker") == 1 and kube_server.connections() == 1
+    assert kube_server.gets() == 12  # exactly one GET per poll

@@ -62,3 +62,13 @@ def test_fault_injection_parity():
     assert by[17].up == "failed" and by[18].up == "scaled"
     assert by[36].down == "failed" and by[37].down == "scaled"
     assert by[43].down == "failed" and by[44].down == "scaled"
+
+
+@pytest.mark.parametrize("sc", traces.baseline_scenarios(), ids=lambda s: s.name)
+def test_pipelined_reads_parity_and_goldens(sc):
+    """--pipeline-reads: the native loop matches the pipelined-time oracle, and the decisions
+    are still the reference's Appendix C goldens."""
+    r = parity.compare(sc, prefetch=True)
+    assert r.ok, r.mismatches[:3]
+    ev = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True)
+    assert traces.golden_from_events(ev, sc.params.poll_ns) == sc.golden

@@ -33,11 +33,24 @@ def scenarios(draw, with_faults=False):
 
 
 @settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
-@given(scenarios())
-def test_native_equals_oracle(case):
+@given(scenarios(), st.booleans())
+def test_native_equals_oracle(case, prefetch):
     sc, _ = case
-    r = parity.compare(sc)
+    r = parity.compare(sc, prefetch=prefetch)
     assert r.ok, r.mismatches[:2]
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(scenarios())
+def test_pipelined_reads_keep_reference_decisions(case):
+    """With API latency far below the poll period (ms vs s), overlapping the GET with the SQS
+    call changes no decision: same depth, actions and replicas at every poll."""
+    sc, _ = case
+    if sc.params.poll_ns < 500 * MILLISECOND:
+        return
+    a = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency)
+    b = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True)
+    assert [e.key() for e in a] == [e.key() for e in b]
 
 
 @settings(max_examples=120, deadline=None, suppress_health_check=[HealthCheck.too_slow])
