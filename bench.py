@@ -132,6 +132,13 @@ def main(argv=None) -> int:
             extra["sequential_scale_p50_ms"] = seq.summary()["p50_ms"]
             ref = measure(1, min(args.steps, 2000), min(args.warmup, 200), "deployment", pipeline=False)
             extra["reference_equivalent_p50_ms"] = ref.summary()["p50_ms"]
+            # Regional-RTT model: the fakes add 2 ms (SQS) / 1 ms (apiserver) per request, so the
+            # structural round-trip savings show at production scale (200 polls each).
+            wan = {}
+            for name, mode, pl in (("optimised", args.mode, pipeline), ("reference_equivalent", "deployment", False)):
+                r = measure(1, 200, 5, mode, pipeline=pl, sqs_latency_ns=2_000_000, kube_latency_ns=1_000_000)
+                wan[name] = r.summary()["p50_ms"]
+            extra["wan_model_sqs2ms_kube1ms_p50_ms"] = wan
         extra["decision_parity"] = _parity_summary()
         out = {
             "metric": METRIC,

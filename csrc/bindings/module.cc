@@ -639,6 +639,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["latency_samples"] = s.latency_samples;
         return d;
       })
+      .def("set_trace_fd", &Runner::set_trace_fd)
       .def("latencies", &Runner::latencies)
       .def("clear_latencies", &Runner::clear_latencies)
       .def_property_readonly("sqs", &Runner::sqs)

@@ -1,8 +1,12 @@
 #include "runner.h"
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <cmath>
 #include <limits>
+
+#include "json.h"
 
 namespace ksa {
 
@@ -166,7 +170,33 @@ void Runner::record(const IterationRecord& r) {
       }
     }
   }
+  if (trace_fd_ >= 0) write_trace(r);
   if (observer_) observer_(r);
+}
+
+std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std::string& queue,
+                           const std::string& deployment) {
+  std::string j = "{\"ts\":" + std::to_string(unix_ns) + ",\"queue\":" + json_quote(queue) +
+                  ",\"deployment\":" + json_quote(deployment) + ",\"poll\":" + std::to_string(r.index) +
+                  ",\"depth\":" + (r.depth_ok ? std::to_string(r.depth) : std::string("null")) +
+                  ",\"up\":\"" + action_name(r.up) + "\",\"down\":\"" + action_name(r.down) +
+                  "\",\"replicas_before\":" + std::to_string(r.replicas_before) +
+                  ",\"replicas_after\":" + std::to_string(r.replicas_after) +
+                  ",\"prefetched\":" + (r.prefetched ? "true" : "false") +
+                  ",\"depth_ns\":" + std::to_string(r.depth_ns) + ",\"get_ns\":" + std::to_string(r.get_ns) +
+                  ",\"update_ns\":" + std::to_string(r.update_ns) + ",\"total_ns\":" + std::to_string(r.total_ns) +
+                  ",\"patch_latency_ns\":" + std::to_string(r.patch_latency_ns);
+  if (!r.error.empty()) j += ",\"error\":" + json_quote(r.error);
+  j += "}";
+  return j;
+}
+
+void Runner::write_trace(const IterationRecord& r) {
+  std::string line = iteration_json(r, clock_->unix_nanos(), sqs_->queue_url(),
+                                    scaler_->namespace_() + "/" + scaler_->deployment());
+  line.push_back('\n');
+  ssize_t n = ::write(trace_fd_, line.data(), line.size());
+  (void)n;
 }
 
 void Runner::run(StopFlag* stop, int64_t max_iterations) {

@@ -102,6 +102,9 @@ class Runner {
   void clear_latencies();
   // Optional per-iteration observer (metrics export, tests). Called on the runner thread.
   void set_observer(std::function<void(const IterationRecord&)> f) { observer_ = std::move(f); }
+  // Span tracing: one JSON object per iteration, written with a single write(2) to `fd`
+  // (an O_APPEND file shared by all workers stays line-atomic). -1 disables.
+  void set_trace_fd(int fd) { trace_fd_ = fd; }
   const LoopConfig& config() const { return cfg_; }
   std::shared_ptr<SqsClient> sqs() const { return sqs_; }
   std::shared_ptr<PodAutoScaler> scaler() const { return scaler_; }
@@ -119,6 +122,8 @@ class Runner {
   Nanos last_up_ = 0, last_down_ = 0;
   uint64_t index_ = 0;
   std::function<void(const IterationRecord&)> observer_;
+  int trace_fd_ = -1;
+  void write_trace(const IterationRecord& r);
 
   mutable std::mutex mu_;
   RunnerStats stats_;
@@ -150,6 +155,10 @@ class Supervisor {
   std::condition_variable cv_;
   size_t running_ = 0;
 };
+
+// JSON line of an iteration record (span trace format).
+std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std::string& queue,
+                           const std::string& deployment);
 
 // Percentile (nearest-rank on a sorted copy), p in [0, 100].
 Nanos percentile(std::vector<Nanos> v, double p);

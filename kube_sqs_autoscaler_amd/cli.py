@@ -81,6 +81,12 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     multi = len(cfg.targets) > 1
     workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
 
+    trace_fd = -1
+    if cfg.trace_file:
+        trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
+        for w in workers:
+            w.runner.set_trace_fd(trace_fd)
+
     from .parallel.fleet import Fleet
 
     fleet = Fleet(workers)
@@ -104,6 +110,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     finally:
         if metrics is not None:
             metrics.stop()
+        if trace_fd >= 0:
+            os.close(trace_fd)
     return 0
 
 

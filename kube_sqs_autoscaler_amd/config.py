@@ -25,7 +25,7 @@ Extensions (all off or reference-equivalent by default):
   resourceVersion precondition validates the early read and a conflict re-reads once, so the
   decisions are the reference's (``models/oracle.py`` ``prefetch``).
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
-  ``--log-format``, ``--metrics-addr``, ``--gpu-aware-max``.
+  ``--log-format``, ``--metrics-addr``, ``--trace-file``, ``--gpu-aware-max``.
 """
 from __future__ import annotations
 
@@ -83,6 +83,7 @@ class Config:
     gpu_aware_max: str = ""
     kube_config_path: str = ""
     pipeline_reads: bool = True
+    trace_file: str = ""
 
 
 def parse_attribute_names(value: str) -> List[str]:
@@ -125,6 +126,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
+    fs.string("trace-file", "", "Append one JSON span per poll (depth, decisions, per-call latencies) to this file; empty disables")
     fs.string("metrics-addr", "", "Serve Prometheus metrics and /healthz on host:port (disabled when empty)")
     fs.string("gpu-aware-max", "", "Cap max-pods at the healthy GPU count: local (probe this node's GPUs); empty disables")
     return fs
@@ -219,6 +221,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         gpu_aware_max=fs["gpu-aware-max"],
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
         pipeline_reads=fs["pipeline-reads"],
+        trace_file=fs["trace-file"],
     )
     if cfg.scale_mode not in SCALE_MODES:
         raise FlagError(f'invalid value "{cfg.scale_mode}" for flag -scale-mode: must be one of {", ".join(SCALE_MODES)}')

@@ -131,3 +131,25 @@ def test_sigterm_graceful_shutdown(servers):
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_trace_file_spans(servers, tmp_path):
+    import json
+
+    from kube_sqs_autoscaler_amd.cli import main
+
+    sqs, kube, env = servers
+    url = sqs.url + "/123/jobs"
+    sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500"})
+    kube.add_deployment("gpu", "workers", 1)
+    trace = tmp_path / "trace.jsonl"
+    rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=workers", "--kubernetes-namespace=gpu",
+               f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+               "--attribute-names=ApproximateNumberOfMessages", f"--trace-file={trace}", "--log-level=error"],
+              environ=env, max_iterations=3)
+    assert rc == 0
+    spans = [json.loads(l) for l in trace.read_text().splitlines()]
+    assert [s["poll"] for s in spans] == [1, 2, 3]
+    assert spans[0]["depth"] == 500 and spans[0]["up"] == "scaled" and spans[0]["replicas_after"] == 2
+    assert spans[0]["deployment"] == "gpu/workers" and spans[0]["queue"] == url and spans[0]["prefetched"] is True
+    assert spans[0]["patch_latency_ns"] > 0 and spans[0]["depth_ns"] > 0
