@@ -715,6 +715,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("replicas", &FakeKubeServer::replicas)
       .def("set_replicas", &FakeKubeServer::set_replicas)
       .def("deployment_json", &FakeKubeServer::deployment_json)
+      .def("lease_json", &FakeKubeServer::lease_json)
       .def("inject", &FakeKubeServer::inject)
       .def("conflict_next", &FakeKubeServer::conflict_next)
       .def("set_latency", &FakeKubeServer::set_latency)

@@ -303,6 +303,96 @@ void FakeKubeServer::set_replicas(const std::string& ns, const std::string& name
   o.generation++;
 }
 
+std::string FakeKubeServer::lease_json(const std::string& ns, const std::string& name) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = leases_.find(ns + "/" + name);
+  return it == leases_.end() ? "" : it->second.json;
+}
+
+void FakeKubeServer::handle_lease(const HttpRequest& req, const std::vector<std::string>& parts,
+                                  HttpResponse* resp) {
+  auto fail = [&](int code, const std::string& reason, const std::string& msg) {
+    resp->status = code;
+    resp->body = status_json(code, reason, msg);
+  };
+  // parts: {ns, "leases"} (collection) or {ns, "leases", name}
+  if (parts.size() < 2 || parts.size() > 3 || parts[1] != "leases") {
+    fail(404, "NotFound", "the server could not find the requested resource");
+    return;
+  }
+  const std::string& ns = parts[0];
+  std::lock_guard<std::mutex> lk(mu_);
+  auto store = [&](const std::string& key, const JsonValue& body, uint64_t rv) {
+    JsonValue obj = body;
+    JsonValue* md = obj.get("metadata");
+    if (!md || !md->is_object()) {
+      obj.set("metadata", JsonValue::make_object());
+      md = obj.get("metadata");
+    }
+    md->set("resourceVersion", JsonValue::make_string(std::to_string(rv)));
+    md->set("namespace", JsonValue::make_string(ns));
+    leases_[key] = Lease{json_serialize(obj), rv};
+    resp->status = 200;
+    resp->body = leases_[key].json;
+  };
+  if (parts.size() == 2) {
+    if (req.method != "POST") {
+      fail(405, "MethodNotAllowed", "the server does not allow this method on the requested resource");
+      return;
+    }
+    auto body = json_parse(req.body);
+    const JsonValue* nm = body.ok() ? body.value.path({"metadata", "name"}) : nullptr;
+    if (!nm || !nm->is_string() || nm->str.empty()) {
+      fail(422, "Invalid", "metadata.name: Required value: name or generateName is required");
+      return;
+    }
+    const std::string key = ns + "/" + nm->str;
+    if (leases_.count(key)) {
+      fail(409, "AlreadyExists", "leases.coordination.k8s.io \"" + nm->str + "\" already exists");
+      return;
+    }
+    writes_++;
+    store(key, body.value, ++rv_counter_);
+    resp->status = 201;
+    return;
+  }
+  const std::string& name = parts[2];
+  const std::string key = ns + "/" + name;
+  auto it = leases_.find(key);
+  if (req.method == "GET") {
+    if (it == leases_.end()) {
+      fail(404, "NotFound", "leases.coordination.k8s.io \"" + name + "\" not found");
+      return;
+    }
+    resp->status = 200;
+    resp->body = it->second.json;
+    return;
+  }
+  if (req.method != "PUT") {
+    fail(405, "MethodNotAllowed", "the server does not allow this method on the requested resource");
+    return;
+  }
+  if (it == leases_.end()) {
+    fail(404, "NotFound", "leases.coordination.k8s.io \"" + name + "\" not found");
+    return;
+  }
+  auto body = json_parse(req.body);
+  if (!body.ok() || !body.value.is_object()) {
+    fail(400, "BadRequest", "the body of the request was in an unknown format");
+    return;
+  }
+  const JsonValue* rv = body.value.path({"metadata", "resourceVersion"});
+  if (!rv || rv->string_or("") != std::to_string(it->second.rv)) {
+    conflicts_++;
+    fail(409, "Conflict",
+         "Operation cannot be fulfilled on leases.coordination.k8s.io \"" + name +
+             "\": the object has been modified; please apply your changes to the latest version and try again");
+    return;
+  }
+  writes_++;
+  store(key, body.value, ++rv_counter_);
+}
+
 std::string FakeKubeServer::deployment_json(const std::string& ns, const std::string& name) const {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = objs_.find(ns + "/" + name);
@@ -423,6 +513,19 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   if (!token.empty() && req.header("Authorization") != "Bearer " + token) {
     auth_failures_++;
     fail(401, "Unauthorized", "Unauthorized");
+    return;
+  }
+  static const std::string lease_prefix = "/apis/coordination.k8s.io/v1/namespaces/";
+  if (path.compare(0, lease_prefix.size(), lease_prefix) == 0) {
+    std::vector<std::string> lp;
+    size_t j = lease_prefix.size();
+    while (j <= path.size()) {
+      size_t e = path.find('/', j);
+      if (e == std::string::npos) e = path.size();
+      lp.push_back(url_decode(path.substr(j, e - j), false));
+      j = e + 1;
+    }
+    handle_lease(req, lp, resp);
     return;
   }
   // /apis/apps/v1/namespaces/{ns}/deployments/{name}[/scale]

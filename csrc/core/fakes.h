@@ -103,6 +103,10 @@ class FakeKubeServer {
   void set_latency(Nanos per_request);
   void drop_connections();
 
+  // coordination.k8s.io/v1 Leases (leader election): raw JSON objects with resourceVersion
+  // optimistic concurrency; POST creates (409 AlreadyExists), PUT replaces (409 Conflict).
+  std::string lease_json(const std::string& ns, const std::string& name) const;  // "" if absent
+
   uint64_t requests() const { return requests_.load(); }
   uint64_t gets() const { return gets_.load(); }
   uint64_t writes() const { return writes_.load(); }
@@ -129,6 +133,12 @@ class FakeKubeServer {
   std::string cert_pem_, key_pem_;
   mutable std::mutex mu_;
   std::map<std::string, Obj> objs_;  // key: ns + "/" + name
+  struct Lease {
+    std::string json;
+    uint64_t rv = 0;
+  };
+  std::map<std::string, Lease> leases_;  // key: ns + "/" + name
+  void handle_lease(const HttpRequest& req, const std::vector<std::string>& parts, HttpResponse* resp);
   std::string token_;
   std::vector<InjectedFault> faults_;
   int conflict_ = 0;

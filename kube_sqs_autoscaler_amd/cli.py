@@ -10,7 +10,9 @@ Prometheus endpoint and GPU-aware ``max-pods`` cap.
 from __future__ import annotations
 
 import os
+import signal
 import sys
+import threading
 from typing import List, Mapping, Optional
 
 from . import autoscaler
@@ -98,16 +100,61 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         metrics.start()
         log.log("info", f"Serving metrics on {cfg.metrics_addr}")
 
-    log.log("info", "Starting kube-sqs-autoscaler")  # main.go:114
+    # Signals: stop whatever phase we are in (election wait, control loop) and exit 0.
+    stop = threading.Event()
+    got: List[int] = []
+
+    def on_signal(signum, _frame):
+        got.append(signum)
+        log.log("info", f"Received signal {signum}, stopping")
+        stop.set()
+        fleet.stop()
+
+    prev = {}
+    if threading.current_thread() is threading.main_thread():
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            prev[sig] = signal.signal(sig, on_signal)
+
+    elector = None
+    lost = threading.Event()
+    renew_stop = threading.Event()
+    renewer = None
     try:
-        if max_iterations > 0:
-            fleet.start(max_iterations)
-            fleet.join()
-        else:
-            sig = fleet.run_until_signalled(on_signal=lambda s: log.log("info", f"Received signal {s}, stopping"))
-            if sig:
-                log.log("info", "Stopped kube-sqs-autoscaler")
+        if cfg.leader_elect:
+            from .kube.leader import LeaderElector, LeaseLock, default_identity
+
+            lock = LeaseLock(rest, cfg.leader_elect_namespace, cfg.leader_elect_lease_name)
+            elector = LeaderElector(lock, cfg.leader_elect_identity or default_identity(),
+                                    cfg.leader_elect_lease_duration_ns / 1e9, cfg.leader_elect_renew_deadline_ns / 1e9,
+                                    cfg.leader_elect_retry_period_ns / 1e9, log=lambda lvl, m: log.log(lvl, m))
+            if not elector.acquire(stop):
+                return 0
+
+            def on_lost():
+                lost.set()
+                fleet.stop()
+
+            renewer = threading.Thread(target=elector.renew_loop, args=(renew_stop, on_lost), name="ksa-lease", daemon=True)
+            renewer.start()
+
+        log.log("info", "Starting kube-sqs-autoscaler")  # main.go:114
+        fleet.start(max_iterations)
+        while not fleet.wait(0.2):
+            pass
+        fleet.join()
+        if lost.is_set():
+            log.log("fatal", "leaderelection lost")
+            return 1
+        if got:
+            log.log("info", "Stopped kube-sqs-autoscaler")
     finally:
+        renew_stop.set()
+        if renewer is not None:
+            renewer.join(timeout=5)
+        if elector is not None and not lost.is_set():
+            elector.release()
+        for sig, h in prev.items():
+            signal.signal(sig, h)
         if metrics is not None:
             metrics.stop()
         if trace_fd >= 0:

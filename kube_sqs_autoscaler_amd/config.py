@@ -26,6 +26,8 @@ Extensions (all off or reference-equivalent by default):
   decisions are the reference's (``models/oracle.py`` ``prefetch``).
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
   ``--log-format``, ``--metrics-addr``, ``--trace-file``, ``--gpu-aware-max``.
+* ``--leader-elect`` (+ lease name/namespace/identity/timings): Lease-based leader election so
+  several replicas can run (the reference must run exactly one, README.md:27).
 """
 from __future__ import annotations
 
@@ -84,6 +86,13 @@ class Config:
     kube_config_path: str = ""
     pipeline_reads: bool = True
     trace_file: str = ""
+    leader_elect: bool = False
+    leader_elect_lease_name: str = "kube-sqs-autoscaler"
+    leader_elect_namespace: str = ""
+    leader_elect_identity: str = ""
+    leader_elect_lease_duration_ns: int = 15 * SECOND
+    leader_elect_renew_deadline_ns: int = 10 * SECOND
+    leader_elect_retry_period_ns: int = 2 * SECOND
 
 
 def parse_attribute_names(value: str) -> List[str]:
@@ -128,6 +137,13 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
     fs.string("trace-file", "", "Append one JSON span per poll (depth, decisions, per-call latencies) to this file; empty disables")
     fs.string("metrics-addr", "", "Serve Prometheus metrics and /healthz on host:port (disabled when empty)")
+    fs.bool("leader-elect", False, "Run several replicas safely: only the holder of a coordination.k8s.io Lease scales")
+    fs.string("leader-elect-lease-name", "kube-sqs-autoscaler", "Name of the leader-election Lease")
+    fs.string("leader-elect-namespace", "", "Namespace of the leader-election Lease (default: --kubernetes-namespace)")
+    fs.string("leader-elect-identity", "", "Holder identity in the Lease (default: $POD_NAME or hostname_pid)")
+    fs.duration("leader-elect-lease-duration", 15 * SECOND, "How long a lease is valid without renewal")
+    fs.duration("leader-elect-renew-deadline", 10 * SECOND, "How long the leader retries renewing before giving up leadership")
+    fs.duration("leader-elect-retry-period", 2 * SECOND, "Interval between lease acquire/renew attempts")
     fs.string("gpu-aware-max", "", "Cap max-pods at the healthy GPU count: local (probe this node's GPUs); empty disables")
     return fs
 
@@ -222,6 +238,13 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
         pipeline_reads=fs["pipeline-reads"],
         trace_file=fs["trace-file"],
+        leader_elect=fs["leader-elect"],
+        leader_elect_lease_name=fs["leader-elect-lease-name"],
+        leader_elect_namespace=fs["leader-elect-namespace"] or fs["kubernetes-namespace"],
+        leader_elect_identity=fs["leader-elect-identity"],
+        leader_elect_lease_duration_ns=fs["leader-elect-lease-duration"],
+        leader_elect_renew_deadline_ns=fs["leader-elect-renew-deadline"],
+        leader_elect_retry_period_ns=fs["leader-elect-retry-period"],
     )
     if cfg.scale_mode not in SCALE_MODES:
         raise FlagError(f'invalid value "{cfg.scale_mode}" for flag -scale-mode: must be one of {", ".join(SCALE_MODES)}')
@@ -229,6 +252,9 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         raise FlagError(f'invalid value "{cfg.sqs_protocol}" for flag -sqs-protocol: must be query or json')
     if cfg.log_format not in ("text", "json"):
         raise FlagError(f'invalid value "{cfg.log_format}" for flag -log-format: must be text or json')
+    if cfg.leader_elect and not (cfg.leader_elect_lease_duration_ns > cfg.leader_elect_renew_deadline_ns
+                                 > cfg.leader_elect_retry_period_ns > 0):
+        raise FlagError("leader election needs lease-duration > renew-deadline > retry-period > 0")
     if cfg.gpu_aware_max not in ("", "local"):
         raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty or local')
     return cfg

@@ -1,0 +1,258 @@
+"""Lease-based leader election (extension: high availability).
+
+The reference has no leader election: two replicas would both scale, so its README deploys
+``replicas: 1`` (/root/reference/README.md:27). With ``--leader-elect`` several
+autoscaler replicas can run and exactly one drives the Deployments.
+
+The algorithm is client-go's ``leaderelection`` with a ``coordination.k8s.io/v1`` Lease lock:
+
+* ``try_acquire_or_renew``: read the Lease. Create it if it is missing. If another holder's
+  record is still valid, give up. Validity is measured with the *local* clock from when this
+  replica last saw the record change, never the remote ``renewTime``, so clock skew cannot
+  cause two leaders. Otherwise write ourselves as holder, guarded by ``resourceVersion``; a 409
+  means another candidate won.
+* the leader renews every ``retry_period``; if no renewal succeeds within ``renew_deadline`` it
+  has lost the lease and must stop scaling;
+* on graceful shutdown the leader releases the lease (empty holder, 1 s duration), so a standby
+  takes over without waiting ``lease_duration``.
+
+Timers follow the reference: a replica that becomes leader starts its control loop fresh, with
+cool-downs armed at that moment (main.go:37-38), the same as a restart.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import threading
+import time
+from dataclasses import dataclass
+from datetime import datetime, timezone
+from typing import Callable, Optional, Tuple
+
+from ..ops import native
+from .config import RestConfig
+
+LEASE_API = "/apis/coordination.k8s.io/v1/namespaces/{ns}/leases"
+
+
+def micro_time(unix_s: float) -> str:
+    """metav1.MicroTime wire format (RFC3339 with microseconds)."""
+    return datetime.fromtimestamp(unix_s, tz=timezone.utc).strftime("%Y-%m-%dT%H:%M:%S.%fZ")
+
+
+def default_identity() -> str:
+    # client-go examples use the pod name; fall back to hostname + pid
+    return os.environ.get("POD_NAME") or f"{socket.gethostname()}_{os.getpid()}"
+
+
+class LeaseError(RuntimeError):
+    def __init__(self, msg: str, status: int = 0):
+        super().__init__(msg)
+        self.status = status
+
+
+@dataclass
+class LeaderElectionRecord:
+    holder: str = ""
+    lease_duration_s: int = 15
+    acquire_time: str = ""
+    renew_time: str = ""
+    transitions: int = 0
+
+    def spec(self) -> dict:
+        s = {"holderIdentity": self.holder, "leaseDurationSeconds": self.lease_duration_s,
+             "leaseTransitions": self.transitions}
+        if self.acquire_time:
+            s["acquireTime"] = self.acquire_time
+        if self.renew_time:
+            s["renewTime"] = self.renew_time
+        return s
+
+    @staticmethod
+    def from_spec(spec: dict) -> "LeaderElectionRecord":
+        return LeaderElectionRecord(
+            holder=spec.get("holderIdentity") or "", lease_duration_s=int(spec.get("leaseDurationSeconds") or 0),
+            acquire_time=spec.get("acquireTime") or "", renew_time=spec.get("renewTime") or "",
+            transitions=int(spec.get("leaseTransitions") or 0))
+
+
+class LeaseLock:
+    """Lease CRUD over the native keep-alive HTTP client (TLS, CA, bearer/basic auth)."""
+
+    def __init__(self, rest: RestConfig, namespace: str, name: str, timeout_s: float = 10.0):
+        nat = native()
+        from ..autoscaler import tls_options
+
+        self.rest = rest
+        self.namespace = namespace
+        self.name = name
+        self.http = nat.HttpClient(rest.host, tls_options(rest), int(timeout_s * 1e9))
+        self._rv = ""
+        self._token_file_mtime = 0.0
+
+    def _headers(self, body: bool = False):
+        h = [("Accept", "application/json")]
+        token = self.rest.bearer_token
+        if self.rest.bearer_token_file:
+            try:  # projected SA tokens rotate
+                with open(self.rest.bearer_token_file) as f:
+                    token = f.read().strip() or token
+            except OSError:
+                pass
+        if token:
+            h.append(("Authorization", f"Bearer {token}"))
+        elif self.rest.username:
+            import base64
+
+            h.append(("Authorization", "Basic " + base64.b64encode(f"{self.rest.username}:{self.rest.password}".encode()).decode()))
+        if body:
+            h.append(("Content-Type", "application/json"))
+        return h
+
+    def _path(self, with_name: bool = True) -> str:
+        base = LEASE_API.format(ns=self.namespace)
+        return f"{base}/{self.name}" if with_name else base
+
+    def _call(self, method: str, path: str, body: Optional[dict] = None) -> Tuple[int, dict]:
+        nat = native()
+        try:
+            status, _, raw = self.http.request(method, path, self._headers(body is not None),
+                                               json.dumps(body).encode() if body is not None else b"")
+        except nat.NativeError as e:
+            raise LeaseError(str(e))
+        try:
+            return status, json.loads(raw) if raw else {}
+        except ValueError:
+            return status, {}
+
+    def get(self) -> Optional[LeaderElectionRecord]:
+        status, obj = self._call("GET", self._path())
+        if status == 404:
+            return None
+        if status != 200:
+            raise LeaseError(obj.get("message") or f"GET lease: HTTP {status}", status)
+        self._rv = obj.get("metadata", {}).get("resourceVersion", "")
+        return LeaderElectionRecord.from_spec(obj.get("spec") or {})
+
+    def create(self, rec: LeaderElectionRecord) -> None:
+        body = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                "metadata": {"name": self.name, "namespace": self.namespace}, "spec": rec.spec()}
+        status, obj = self._call("POST", self._path(False), body)
+        if status not in (200, 201):
+            raise LeaseError(obj.get("message") or f"POST lease: HTTP {status}", status)
+        self._rv = obj.get("metadata", {}).get("resourceVersion", "")
+
+    def update(self, rec: LeaderElectionRecord) -> None:
+        body = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                "metadata": {"name": self.name, "namespace": self.namespace, "resourceVersion": self._rv},
+                "spec": rec.spec()}
+        status, obj = self._call("PUT", self._path(), body)
+        if status != 200:
+            raise LeaseError(obj.get("message") or f"PUT lease: HTTP {status}", status)
+        self._rv = obj.get("metadata", {}).get("resourceVersion", "")
+
+    def describe(self) -> str:
+        return f"{self.namespace}/{self.name}"
+
+
+class LeaderElector:
+    def __init__(self, lock: LeaseLock, identity: str, lease_duration_s: float = 15.0, renew_deadline_s: float = 10.0,
+                 retry_period_s: float = 2.0, monotonic: Callable[[], float] = time.monotonic,
+                 wall: Callable[[], float] = time.time, log: Optional[Callable[[str, str], None]] = None):
+        if not lease_duration_s > renew_deadline_s > retry_period_s > 0:
+            raise ValueError("need lease_duration > renew_deadline > retry_period > 0")
+        self.lock = lock
+        self.identity = identity
+        self.lease_duration = lease_duration_s
+        self.renew_deadline = renew_deadline_s
+        self.retry_period = retry_period_s
+        self.monotonic = monotonic
+        self.wall = wall
+        self.log = log or (lambda level, msg: None)
+        self.observed: Optional[LeaderElectionRecord] = None
+        self.observed_at = 0.0
+        self._leader = False
+
+    @property
+    def is_leader(self) -> bool:
+        return self._leader
+
+    def try_acquire_or_renew(self) -> bool:
+        now_wall = micro_time(self.wall())
+        desired = LeaderElectionRecord(self.identity, int(self.lease_duration), now_wall, now_wall, 0)
+        try:
+            old = self.lock.get()
+        except LeaseError as e:
+            self.log("error", f"error retrieving resource lock {self.lock.describe()}: {e}")
+            return False
+        if old is None:
+            try:
+                self.lock.create(desired)
+            except LeaseError as e:
+                self.log("error", f"error initially creating leader election record: {e}")
+                return False
+            self._observe(desired)
+            return True
+        if self.observed is None or old.spec() != self.observed.spec():
+            self._observe(old)
+        held_by_other = old.holder and old.holder != self.identity
+        if held_by_other and self.observed_at + max(old.lease_duration_s, 1) > self.monotonic():
+            return False  # another replica holds a valid lease
+        if old.holder == self.identity:
+            desired.acquire_time = old.acquire_time
+            desired.transitions = old.transitions
+        else:
+            desired.transitions = old.transitions + 1
+        try:
+            self.lock.update(desired)
+        except LeaseError as e:
+            if e.status != 409:
+                self.log("error", f"Failed to update lock: {e}")
+            return False  # lost the race
+        self._observe(desired)
+        return True
+
+    def _observe(self, rec: LeaderElectionRecord) -> None:
+        self.observed = rec
+        self.observed_at = self.monotonic()
+
+    def acquire(self, stop: threading.Event) -> bool:
+        """Blocks until this replica holds the lease (True) or ``stop`` is set (False)."""
+        self.log("info", f"attempting to acquire leader lease {self.lock.describe()}...")
+        while not stop.is_set():
+            if self.try_acquire_or_renew():
+                self._leader = True
+                self.log("info", f"successfully acquired lease {self.lock.describe()}")
+                return True
+            stop.wait(self.retry_period)
+        return False
+
+    def renew_loop(self, stop: threading.Event, on_lost: Callable[[], None]) -> None:
+        """Renews every retry_period; calls ``on_lost`` if renew_deadline passes without success."""
+        last_ok = self.monotonic()
+        while not stop.wait(self.retry_period):
+            if self.try_acquire_or_renew():
+                last_ok = self.monotonic()
+                continue
+            if self.monotonic() - last_ok >= self.renew_deadline:
+                self._leader = False
+                self.log("error", f"failed to renew lease {self.lock.describe()}: timed out waiting for the condition")
+                on_lost()
+                return
+
+    def release(self) -> bool:
+        """Gives the lease up (ReleaseOnCancel) so a standby can take over at once."""
+        if not self._leader:
+            return False
+        self._leader = False
+        try:
+            old = self.lock.get()
+            if old is None or old.holder != self.identity:
+                return False
+            now_wall = micro_time(self.wall())
+            self.lock.update(LeaderElectionRecord("", 1, now_wall, now_wall, old.transitions))
+            return True
+        except LeaseError as e:
+            self.log("error", f"Failed to release lock: {e}")
+            return False
