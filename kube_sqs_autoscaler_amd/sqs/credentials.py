@@ -10,7 +10,10 @@ v1.35.35's resolution order (go.mod:6):
    STS ``AssumeRoleWithWebIdentity``;
 3. the shared credentials file (``AWS_SHARED_CREDENTIALS_FILE`` or ``~/.aws/credentials``,
    profile ``AWS_PROFILE`` / ``AWS_DEFAULT_PROFILE`` / ``default``), including
-   ``credential_process``;
+   ``credential_process``; with ``AWS_SDK_LOAD_CONFIG`` also ``~/.aws/config``
+   (``AWS_CONFIG_FILE``) profiles, and ``role_arn`` + ``source_profile`` /
+   ``credential_source`` profiles resolve through a SigV4-signed STS ``AssumeRole`` (chains
+   allowed);
 4. remote: ECS task role (``AWS_CONTAINER_CREDENTIALS_RELATIVE_URI`` /
    ``AWS_CONTAINER_CREDENTIALS_FULL_URI`` + ``AWS_CONTAINER_AUTHORIZATION_TOKEN``), otherwise
    the EC2 instance role through IMDSv2 (token PUT, falling back to IMDSv1).
@@ -272,9 +275,121 @@ class RemoteProvider(_Provider):
                      parse_expiration(j["Expiration"]) if j.get("Expiration") else 0, self.name)
 
 
+def _truthy(v: Optional[str]) -> bool:
+    return bool(v) and v.lower() not in ("0", "false", "no")
+
+
+def load_profiles(environ: Mapping[str, str]) -> Dict[str, Dict[str, str]]:
+    """Merged shared credentials + (with AWS_SDK_LOAD_CONFIG) shared config profiles.
+
+    Config-file sections are ``[profile name]`` except ``[default]``; credentials-file values
+    win, as in aws-sdk-go v1.
+    """
+    home = environ.get("HOME") or os.path.expanduser("~")
+    out: Dict[str, Dict[str, str]] = {}
+    if _truthy(environ.get("AWS_SDK_LOAD_CONFIG")):
+        cfg_path = environ.get("AWS_CONFIG_FILE") or os.path.join(home, ".aws", "config")
+        cp = configparser.RawConfigParser()
+        try:
+            cp.read(cfg_path)
+        except configparser.Error as e:
+            raise CredentialsError(f"SharedConfigLoadError: failed to load config file {cfg_path}: {e}")
+        for sec in cp.sections():
+            name = sec[len("profile "):].strip() if sec.startswith("profile ") else sec
+            out.setdefault(name, {}).update(dict(cp.items(sec)))
+    cred_path = environ.get("AWS_SHARED_CREDENTIALS_FILE") or os.path.join(home, ".aws", "credentials")
+    cp = configparser.RawConfigParser()
+    try:
+        cp.read(cred_path)
+    except configparser.Error as e:
+        raise CredentialsError(f"SharedCredsLoad: failed to load shared credentials file: {e}")
+    for sec in cp.sections():
+        out.setdefault(sec, {}).update(dict(cp.items(sec)))
+    return out
+
+
+class AssumeRoleProvider(_Provider):
+    """``role_arn`` + ``source_profile`` / ``credential_source`` in a shared profile:
+    STS ``AssumeRole``, SigV4-signed with the source credentials (aws-sdk-go v1 behaviour)."""
+
+    name = "AssumeRoleProvider"
+
+    def __init__(self, environ: Mapping[str, str], region: str, fetch: Fetch = urllib_fetch, sts_endpoint: str = ""):
+        self.env = dict(environ)
+        self.profile = environ.get("AWS_PROFILE") or environ.get("AWS_DEFAULT_PROFILE") or "default"
+        self.region = region
+        self.http = fetch
+        self.sts_endpoint = sts_endpoint or environ.get("AWS_STS_ENDPOINT", "")
+
+    def _section(self) -> Optional[Dict[str, str]]:
+        try:
+            return load_profiles(self.env).get(self.profile)
+        except CredentialsError:
+            return None
+
+    def available(self) -> bool:
+        sec = self._section()
+        return bool(sec and sec.get("role_arn") and not sec.get("aws_access_key_id"))
+
+    def _source(self, sec: Dict[str, str]):
+        if sec.get("source_profile"):
+            src_env = dict(self.env)
+            src_env["AWS_PROFILE"] = sec["source_profile"]
+            profiles = load_profiles(self.env)
+            src = profiles.get(sec["source_profile"])
+            if src is None:
+                raise CredentialsError(f"SharedConfigAssumeRoleError: source profile {sec['source_profile']} not found")
+            if src.get("role_arn") and not src.get("aws_access_key_id"):
+                if sec["source_profile"] == self.profile:
+                    raise CredentialsError("SharedConfigAssumeRoleError: source_profile refers to itself")
+                return AssumeRoleProvider(src_env, self.region, self.http, self.sts_endpoint).fetch()  # role chaining
+            if src.get("aws_access_key_id"):
+                return _make(src["aws_access_key_id"], src.get("aws_secret_access_key", ""), src.get("aws_session_token", ""),
+                             0, "SharedCredentialsProvider")
+            if src.get("credential_process"):
+                return process_credentials(src["credential_process"])
+            raise CredentialsError(f"SharedConfigAssumeRoleError: source profile {sec['source_profile']} has no credentials")
+        cs = sec.get("credential_source", "")
+        if cs == "Environment":
+            return EnvProvider(self.env).fetch()
+        if cs in ("Ec2InstanceMetadata", "EcsContainer"):
+            return RemoteProvider(self.env, self.http).fetch()
+        raise CredentialsError("SharedConfigAssumeRoleError: role_arn needs source_profile or credential_source")
+
+    def fetch(self):
+        nat = native()
+        sec = self._section() or {}
+        src = self._source(sec)
+        region = self.region or sec.get("region", "") or "us-east-1"
+        endpoint = self.sts_endpoint or (f"https://sts.{region}.amazonaws.com" if self.region else "https://sts.amazonaws.com")
+        params = {"Action": "AssumeRole", "RoleArn": sec["role_arn"], "Version": "2011-06-15",
+                  "RoleSessionName": sec.get("role_session_name") or f"{int(datetime.now(timezone.utc).timestamp() * 1e9)}"}
+        if sec.get("external_id"):
+            params["ExternalId"] = sec["external_id"]
+        if sec.get("duration_seconds"):
+            params["DurationSeconds"] = sec["duration_seconds"]
+        body = "&".join(f"{nat.aws_uri_encode(k, False)}={nat.aws_uri_encode(v, False)}" for k, v in sorted(params.items()))
+        host = urllib.parse.urlsplit(endpoint).netloc
+        headers = [("Host", host), ("Content-Type", "application/x-www-form-urlencoded; charset=utf-8")]
+        signer = nat.SigV4Signer(region if self.region or self.sts_endpoint else "us-east-1", "sts")
+        signed, _ = signer.sign(src, int(datetime.now(timezone.utc).timestamp() * 1e9), "POST", "/", "", headers, body.encode())
+        status, resp = self.http("POST", endpoint + "/", {k: v for k, v in signed if k != "Host"}, body.encode(), 10.0)
+        text = resp.decode(errors="replace")
+        if status != 200:
+            code = nat.xml_first_text(text, "Code") or f"HTTP {status}"
+            raise CredentialsError(f"AssumeRoleError: {code}: {nat.xml_first_text(text, 'Message') or ''}")
+        akid, secret = nat.xml_first_text(text, "AccessKeyId"), nat.xml_first_text(text, "SecretAccessKey")
+        if not akid or not secret:
+            raise CredentialsError("AssumeRoleError: STS response carried no credentials")
+        exp = nat.xml_first_text(text, "Expiration")
+        return _make(akid, secret, nat.xml_first_text(text, "SessionToken") or "", parse_expiration(exp) if exp else 0,
+                     self.name)
+
+
 def default_chain(environ: Optional[Mapping[str, str]] = None, region: str = "", fetch: Fetch = urllib_fetch) -> List[_Provider]:
     env = dict(os.environ if environ is None else environ)
-    return [EnvProvider(env), WebIdentityProvider(env, region, fetch), SharedFileProvider(env), RemoteProvider(env, fetch)]
+    return [EnvProvider(env), WebIdentityProvider(env, region, fetch), AssumeRoleProvider(env, region, fetch),
+            SharedFileProvider(env), RemoteProvider(env, fetch)]
 
 
 def make_chain_provider(providers: Optional[List[_Provider]] = None, environ: Optional[Mapping[str, str]] = None,

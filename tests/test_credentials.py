@@ -145,3 +145,42 @@ def test_chain_feeds_native_signer_lazily_and_caches(nat):
         assert len(calls) == 1 and s.signature_failures() == 0
     finally:
         s.stop()
+
+
+def test_assume_role_from_shared_config(tmp_path, nat):
+    (tmp_path / "credentials").write_text("[base]\naws_access_key_id = AKIDBASE\naws_secret_access_key = basesecret\n")
+    (tmp_path / "config").write_text("[profile deploy]\nrole_arn = arn:aws:iam::123:role/ksa\nsource_profile = base\n"
+                                     "external_id = ext-1\nrole_session_name = ksa-session\n")
+    seen = {}
+
+    def fetch(method, url, headers, body, timeout):
+        seen.update(url=url, headers=headers, body=body.decode())
+        return 200, (b"<AssumeRoleResponse><AssumeRoleResult><Credentials><AccessKeyId>ASIAROLE</AccessKeyId>"
+                     b"<SecretAccessKey>RS</SecretAccessKey><SessionToken>RT</SessionToken>"
+                     b"<Expiration>2031-01-01T00:00:00Z</Expiration></Credentials></AssumeRoleResult></AssumeRoleResponse>")
+
+    env = {"AWS_SHARED_CREDENTIALS_FILE": str(tmp_path / "credentials"), "AWS_CONFIG_FILE": str(tmp_path / "config"),
+           "AWS_SDK_LOAD_CONFIG": "1", "AWS_PROFILE": "deploy"}
+    c = chain(env, fetch, region="eu-west-1").retrieve()
+    assert (c.access_key_id, c.session_token, c.provider_name) == ("ASIAROLE", "RT", "AssumeRoleProvider")
+    assert seen["url"] == "https://sts.eu-west-1.amazonaws.com/"
+    assert "Action=AssumeRole" in seen["body"] and "ExternalId=ext-1" in seen["body"] and "RoleSessionName=ksa-session" in seen["body"]
+    auth = seen["headers"]["Authorization"]
+    assert auth.startswith("AWS4-HMAC-SHA256 Credential=AKIDBASE/") and "/eu-west-1/sts/aws4_request" in auth
+
+
+def test_assume_role_needs_sdk_load_config(tmp_path, nat):
+    (tmp_path / "config").write_text("[profile deploy]\nrole_arn = arn:aws:iam::123:role/ksa\nsource_profile = base\n")
+    env = {"AWS_CONFIG_FILE": str(tmp_path / "config"), "AWS_PROFILE": "deploy", "AWS_EC2_METADATA_DISABLED": "true",
+           "AWS_SHARED_CREDENTIALS_FILE": str(tmp_path / "none")}
+    with pytest.raises(Exception, match="NoCredentialProviders"):
+        chain(env).retrieve()  # aws-sdk-go v1 ignores ~/.aws/config without AWS_SDK_LOAD_CONFIG
+
+
+def test_assume_role_error(tmp_path, nat):
+    (tmp_path / "credentials").write_text("[base]\naws_access_key_id = A\naws_secret_access_key = S\n"
+                                          "[deploy]\nrole_arn = arn:aws:iam::1:role/r\nsource_profile = base\n")
+    fetch = lambda *a: (403, b"<ErrorResponse><Error><Code>AccessDenied</Code><Message>not allowed</Message></Error></ErrorResponse>")
+    env = {"AWS_SHARED_CREDENTIALS_FILE": str(tmp_path / "credentials"), "AWS_PROFILE": "deploy"}
+    with pytest.raises(Exception, match="AccessDenied: not allowed"):
+        chain(env, fetch).retrieve()
