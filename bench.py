@@ -52,6 +52,7 @@ def main(argv=None) -> int:
     ap.add_argument("--mode", default="scale", choices=["scale", "deployment", "patch"])
     ap.add_argument("--no-sweep", action="store_true", help="skip the 1/2/4/8-queue sweep (single rank only)")
     ap.add_argument("--no-pipeline", action="store_true", help="strictly sequential SQS -> GET -> write")
+    ap.add_argument("--busy-poll-us", type=int, default=25, help="adaptive client busy-poll window (CLI default --busy-poll=25us; 0: block)")
     args = ap.parse_args(argv)
 
     import torch
@@ -78,7 +79,8 @@ def main(argv=None) -> int:
 
     native()  # build/load before timing
     pipeline = not args.no_pipeline
-    env = BenchEnv(args.queues, args.mode, pipeline=pipeline)
+    bp = args.busy_poll_us * 1000
+    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp)
     try:
         if args.warmup:
             env.run(args.warmup)
@@ -118,6 +120,7 @@ def main(argv=None) -> int:
             "tracked_queues": args.queues * world,
             "scale_mode": args.mode,
             "pipeline_reads": pipeline,
+            "busy_poll_us": args.busy_poll_us,
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
@@ -125,7 +128,7 @@ def main(argv=None) -> int:
         if world == 1 and not args.no_sweep:
             sweep = {}
             for q in (1, 2, 4, 8):
-                r = measure(q, min(args.steps, 2000), min(args.warmup, 200), args.mode, pipeline=pipeline)
+                r = measure(q, min(args.steps, 2000), min(args.warmup, 200), args.mode, pipeline=pipeline, busy_poll_ns=bp)
                 sweep[str(q)] = r.summary()["p50_ms"]
             extra["p50_ms_by_tracked_queues"] = sweep
             seq = measure(1, min(args.steps, 2000), min(args.warmup, 200), args.mode, pipeline=False)

@@ -366,6 +366,8 @@ PYBIND11_MODULE(_ksa_native, m) {
              return py::make_tuple(resp.status, resp.headers, py::bytes(resp.body));
            },
            py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""))
+      .def("set_busy_poll", &HttpClient::set_busy_poll)
+      .def("rtt_ewma", &HttpClient::rtt_ewma)
       .def("close", &HttpClient::close)
       .def("stats", [](HttpClient& c) { return http_stats_dict(c.stats()); });
   m.def("parse_url", [](const std::string& s) {
@@ -388,6 +390,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("endpoint", &SqsHttpOptions::endpoint)
       .def_readwrite("protocol", &SqsHttpOptions::protocol)
       .def_readwrite("timeout_ns", &SqsHttpOptions::timeout)
+      .def_readwrite("busy_poll_ns", &SqsHttpOptions::busy_poll)
       .def_readwrite("max_retries", &SqsHttpOptions::max_retries)
       .def_readwrite("min_retry_delay_ns", &SqsHttpOptions::min_retry_delay)
       .def_readwrite("min_throttle_delay_ns", &SqsHttpOptions::min_throttle_delay)
@@ -491,7 +494,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("token", &KubeOptions::token)
       .def_readwrite("basic_user", &KubeOptions::basic_user)
       .def_readwrite("basic_password", &KubeOptions::basic_password)
-      .def_readwrite("timeout_ns", &KubeOptions::timeout);
+      .def_readwrite("timeout_ns", &KubeOptions::timeout)
+      .def_readwrite("busy_poll_ns", &KubeOptions::busy_poll);
 
   py::class_<DeploymentApi, PyDeploymentApi, py::smart_holder>(m, "DeploymentApi")
       .def(py::init<>())

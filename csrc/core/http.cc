@@ -182,6 +182,7 @@ class Stream {
       }
       if (errno == EINTR) continue;
       if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        if (spin_ns_ > 0 && spin_for_data()) continue;
         Status s = wait_fd(fd_, POLLIN, deadline_ns);
         if (!s.ok()) return s;
         continue;
@@ -223,9 +224,29 @@ class Stream {
     return Status::OK();
   }
 
+ void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
+
  private:
+  // Busy-poll: peek the socket for up to spin_ns_ before sleeping in poll(2). A response that
+  // lands within the window is picked up without a scheduler wake-up (several microseconds on
+  // every round trip); past it the thread blocks as usual, so idle waits cost no CPU.
+  bool spin_for_data() {
+    const int64_t end = mono_ns() + spin_ns_;
+    char c;
+    for (int i = 0;; ++i) {
+      ssize_t n = ::recv(fd_, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+      if (n > 0 || n == 0) return true;  // data or orderly close: let the caller read it
+      if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return true;  // surface the error
+      if ((i & 15) == 15 && mono_ns() >= end) return false;
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
+
   int fd_;
   SSL* ssl_;
+  int64_t spin_ns_ = 0;
 };
 
 // Incremental HTTP/1.1 message framing over a Stream with a carry-over buffer.
@@ -638,7 +659,19 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
     return s;
   }
   stats_.bytes_out += wire.size();
+  sent_at_ = mono_ns();
   return Status::OK();
+}
+
+Nanos HttpClient::spin_window() const {
+  if (spin_ns_ <= 0) return 0;
+  if (ewma_ns_ < 0) return spin_ns_;  // no sample yet: try
+  return ewma_ns_ <= 4 * spin_ns_ ? spin_ns_ : 0;
+}
+
+Nanos HttpClient::rtt_ewma() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return ewma_ns_;
 }
 
 Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
@@ -647,6 +680,7 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   if (!conn_) return Status::Err("connection closed before the response");
   const bool reused = conn_->uses > 1;
   Status s;
+  conn_->stream->set_spin_ns(spin_window());
   Reader rd(conn_->stream.get(), &conn_->rbuf);
   std::string head;
   bool got_any = false;
@@ -697,6 +731,10 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
     return s;
   }
   stats_.bytes_in += head.size() + resp->body.size();
+  {
+    const Nanos rtt = mono_ns() - sent_at_;
+    ewma_ns_ = ewma_ns_ < 0 ? rtt : (ewma_ns_ * 7 + rtt) / 8;
+  }
   if (close_after) conn_.reset();
   return Status::OK();
 }

@@ -98,6 +98,11 @@ class HttpClient {
   HttpClientStats stats() const;
   const Url& origin() const { return origin_; }
   void set_timeout(Nanos t) { timeout_ = t; }
+  // Adaptive busy-poll: while the peer's response-time EWMA is within 4x `ns`, a read spins for
+  // up to `ns` before blocking in poll(2) (saves the scheduler wake-up on fast local peers); for
+  // slower peers (real AWS / apiserver RTTs of milliseconds) it never spins. 0 disables.
+  void set_busy_poll(Nanos ns) { spin_ns_ = ns; }
+  Nanos rtt_ewma() const;
 
  private:
   struct Conn;
@@ -116,6 +121,10 @@ class HttpClient {
   mutable std::mutex mu_;
   std::unique_ptr<Conn> conn_;
   HttpClientStats stats_;
+  Nanos spin_ns_ = 0;
+  Nanos ewma_ns_ = -1;   // response-time EWMA (-1: no sample yet)
+  int64_t sent_at_ = 0;  // mono time the current request finished writing
+  Nanos spin_window() const;
   bool in_flight_ = false;
   HttpRequest pending_;
   int64_t pending_deadline_ = 0;

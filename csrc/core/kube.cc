@@ -90,6 +90,7 @@ KubeRestDeployments::KubeRestDeployments(KubeOptions opts) : opts_(std::move(opt
   }
   url_ = u.value;
   http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
+  http_->set_busy_poll(opts_.busy_poll);
 }
 
 KubeStats KubeRestDeployments::stats() const {

@@ -95,6 +95,7 @@ struct KubeOptions {
   std::shared_ptr<TokenProvider> token;  // bearer token (may be null)
   std::string basic_user, basic_password;  // legacy kubeconfig basic auth
   Nanos timeout = 30 * kSecond;
+  Nanos busy_poll = 0;  // HttpClient::set_busy_poll
 };
 
 struct KubeStats {

@@ -52,6 +52,7 @@ HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider>
   }
   url_ = u.value;
   http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
+  http_->set_busy_poll(opts_.busy_poll);
 }
 
 SqsApiStats HttpSqsApi::stats() const {

@@ -44,6 +44,7 @@ struct SqsHttpOptions {
   std::string endpoint;  // override (e.g. http://127.0.0.1:9324); empty = regional endpoint
   SqsProtocol protocol = SqsProtocol::Query;
   Nanos timeout = 30 * kSecond;
+  Nanos busy_poll = 0;  // HttpClient::set_busy_poll
   int max_retries = 3;  // aws-sdk-go v1 DefaultRetryer.NumMaxRetries
   Nanos min_retry_delay = 30 * kMillisecond;
   Nanos min_throttle_delay = 500 * kMillisecond;

@@ -40,7 +40,8 @@ def tls_options(rc: RestConfig):
     return t
 
 
-def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", timeout_ns: int = 30 * SECOND, clock=None):
+def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", timeout_ns: int = 30 * SECOND, clock=None,
+                       busy_poll_ns: int = 0):
     """The ``DeploymentInterface`` seam over REST (/root/reference/scale/scale.go:44)."""
     nat = native()
     o = nat.KubeOptions()
@@ -49,6 +50,7 @@ def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", time
     o.mode = scale_mode(mode)
     o.tls = tls_options(rc)
     o.timeout_ns = timeout_ns
+    o.busy_poll_ns = busy_poll_ns
     if rc.bearer_token_file:
         o.token = nat.FileTokenProvider(rc.bearer_token_file, clock or nat.RealClock(), 60 * SECOND)
     elif rc.bearer_token:
@@ -65,13 +67,14 @@ def new_pod_autoscaler(target: TargetConfig, api, logger, clock):
 
 
 def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query", timeout_ns: int = 30 * SECOND,
-                credentials=None, environ: Optional[Mapping[str, str]] = None, tls=None):
+                credentials=None, environ: Optional[Mapping[str, str]] = None, tls=None, busy_poll_ns: int = 0):
     nat = native()
     o = nat.SqsHttpOptions()
     o.region = region
     o.endpoint = endpoint
     o.protocol = nat.SqsProtocol.Json if protocol == "json" else nat.SqsProtocol.Query
     o.timeout_ns = timeout_ns
+    o.busy_poll_ns = busy_poll_ns
     if tls is not None:
         o.tls = tls
     creds = credentials if credentials is not None else make_chain_provider(environ=environ, region=region)
@@ -108,10 +111,11 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     log = base_logger
     if tag_queue:
         log = base_logger.with_fields([("deployment", target.name), ("queue", target.queue_url)])
-    kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock)
+    kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock,
+                                  busy_poll_ns=cfg.busy_poll_ns)
     scaler = new_pod_autoscaler(target, kube_api, log, clock)
     sqs_api = new_sqs_api(cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
-                          credentials, environ)
+                          credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
     runner = nat.Runner(loop_config(target, cfg.pipeline_reads), sqs, scaler, clock, log)
     return Worker(target, runner, sqs_api, kube_api, log)

@@ -80,7 +80,8 @@ class BenchEnv:
     """Fake servers + one worker per queue."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
-                 kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True):
+                 kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
+                 busy_poll_ns: int = 0):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -122,9 +123,10 @@ class BenchEnv:
             t = TargetConfig(queue_url=url, deployment=name, namespace="bench", poll_period_ns=0,
                              scale_up_cool_down_ns=0, scale_down_cool_down_ns=0, scale_up_messages=100,
                              scale_down_messages=10, max_pods=8, min_pods=1)
-            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock)
+            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=busy_poll_ns)
             scaler = new_pod_autoscaler(t, kube_api, self.log, self.clock)
-            sqs_api = new_sqs_api(REGION, self.clock, endpoint=self.sqs.url, credentials=creds, tls=sqs_tls)
+            sqs_api = new_sqs_api(REGION, self.clock, endpoint=self.sqs.url, credentials=creds, tls=sqs_tls,
+                                  busy_poll_ns=busy_poll_ns)
             client = new_sqs_client(t, sqs_api)
             cfg = nat.LoopConfig()
             cfg.poll_period_ns = 0

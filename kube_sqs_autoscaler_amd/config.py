@@ -85,6 +85,7 @@ class Config:
     gpu_aware_max: str = ""
     kube_config_path: str = ""
     pipeline_reads: bool = True
+    busy_poll_ns: int = 25_000
     trace_file: str = ""
     leader_elect: bool = False
     leader_elect_lease_name: str = "kube-sqs-autoscaler"
@@ -133,6 +134,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("sqs-protocol", "query", "SQS wire protocol: query (AWS Query/XML) or json (AWS JSON 1.0)")
     fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
+    fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
     fs.string("trace-file", "", "Append one JSON span per poll (depth, decisions, per-call latencies) to this file; empty disables")
@@ -237,6 +239,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         gpu_aware_max=fs["gpu-aware-max"],
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
         pipeline_reads=fs["pipeline-reads"],
+        busy_poll_ns=fs["busy-poll"],
         trace_file=fs["trace-file"],
         leader_elect=fs["leader-elect"],
         leader_elect_lease_name=fs["leader-elect-lease-name"],

@@ -301,3 +301,16 @@ def test_full_loop_pipelined_over_the_wire(nat, sqs_server, kube_server):
     assert [x["down"] for x in recs] == ["scaled"] * 4 + ["noop"]
     assert kube_server.replicas("ml", "worker") == 1 and kube_server.connections() == 1
     assert kube_server.gets() == 12  # exactly one GET per poll
+
+
+def test_adaptive_busy_poll_tracks_peer_rtt(nat, kube_server):
+    c = nat.HttpClient(kube_server.url)
+    c.set_busy_poll(25_000)
+    kube_server.set_latency(3_000_000)  # a "remote" peer: spinning would only burn CPU
+    for _ in range(4):
+        c.request("GET", "/healthz", [("Authorization", f"Bearer {TOKEN}")])
+    assert c.rtt_ewma() > 4 * 25_000  # -> spin window 0
+    kube_server.set_latency(0)
+    for _ in range(60):
+        c.request("GET", "/healthz", [("Authorization", f"Bearer {TOKEN}")])
+    assert c.rtt_ewma() < 4 * 25_000  # fast local peer again -> spinning re-enabled
