@@ -9,12 +9,14 @@
 //   * fill:   every lane stores 4 x 16 B per iteration with nontemporal stores (no L2 pollution),
 //             a 32-bit address-derived pattern (one v_mul_lo_u32 per dword), and accumulates the
 //             checksum of what it *intended* to write;
-//   * verify: 4 x 16 B nontemporal loads in flight per lane per iteration (64 B/lane, ~64 KiB per CU
-//             with 4 waves x 4 workgroups), compares each dword against the pattern and sums
+//   * verify: 8 x 16 B nontemporal loads in flight per lane per iteration (128 B/lane, 64 KiB per
+//             CU with 4 waves x 2 workgroups), compares each dword against the pattern and sums
 //             what it *read*;
 //   * both:   wave64 butterfly (__shfl_xor) -> LDS across the 4 waves -> ONE 64-bit atomic per
-//             workgroup; grid = CUs x 4 workgroups of 256 threads (>= 1024 workgroups, all 8 XCDs),
-//             grid-stride so every wave reaches the exit whatever the buffer size;
+//             workgroup; grid = CUs x 2 workgroups of 256 threads (512 workgroups over all 8 XCDs),
+//             grid-stride so every wave reaches the exit whatever the buffer size. 2/CU with deep
+//             unrolling beat 4, 8 and 16/CU in the tune_probe sweep (fewer waves contending for
+//             the same channels, same bytes in flight);
 //   * timing: one untimed warm-up launch of each kernel, then best-of-`reps` with hipEvents over a
 //             buffer >= the 256 MiB Infinity Cache, so the numbers are HBM numbers.
 // Healthy <=> zero mismatches AND read checksum == written checksum.
@@ -29,7 +31,9 @@ namespace {
 
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
-constexpr int kUnroll = 4;   // 16-byte vectors per lane per iteration
+constexpr int kUnrollFill = 4;    // 16-byte stores per lane per iteration
+constexpr int kUnrollVerify = 8;  // 16-byte loads in flight per lane per iteration
+constexpr int kBlocksPerCu = 2;   // measured best (csrc/tools/tune_probe.hip, profiles/r01_tune_probe.jsonl)
 
 thread_local std::string g_last_error;
 
@@ -79,9 +83,9 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(u32x4* __restrict__ buf, u
   unsigned long long acc = 0;
   uint64_t v = tid;
   // main body: kUnroll independent 16-B stores per lane per iteration, lanes coalesced per store
-  for (; v + (kUnroll - 1) * nthreads < n_vec; v += kUnroll * nthreads) {
+  for (; v + (kUnrollFill - 1) * nthreads < n_vec; v += kUnrollFill * nthreads) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kUnrollFill; ++u) {
       const uint64_t w = v + u * nthreads;
       const u32x4 x = pattern4(w, seed);
       acc += static_cast<unsigned long long>(x.x) + x.y + x.z + x.w;
@@ -103,12 +107,12 @@ __global__ __launch_bounds__(kBlock) void verify_kernel(const u32x4* __restrict_
   const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   unsigned long long acc = 0, bad = 0;
   uint64_t v = tid;
-  for (; v + (kUnroll - 1) * nthreads < n_vec; v += kUnroll * nthreads) {
-    u32x4 x[kUnroll];
+  for (; v + (kUnrollVerify - 1) * nthreads < n_vec; v += kUnrollVerify * nthreads) {
+    u32x4 x[kUnrollVerify];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) x[u] = __builtin_nontemporal_load(buf + v + u * nthreads);  // all in flight
+    for (int u = 0; u < kUnrollVerify; ++u) x[u] = __builtin_nontemporal_load(buf + v + u * nthreads);  // all in flight
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < kUnrollVerify; ++u) {
       const u32x4 p = pattern4(v + u * nthreads, seed);
       acc += static_cast<unsigned long long>(x[u].x) + x[u].y + x[u].z + x[u].w;
       bad += (x[u].x != p.x) + (x[u].y != p.y) + (x[u].z != p.z) + (x[u].w != p.w);
@@ -210,7 +214,7 @@ int ksa_gpu_health_check_ex(int dev, uint64_t bytes, int reps, ksa_gpu_health* o
     if (!check(hipMalloc(&counters, 3 * sizeof(unsigned long long)), "hipMalloc")) break;
     if (!check(hipEventCreate(&e0), "hipEventCreate") || !check(hipEventCreate(&e1), "hipEventCreate")) break;
     const uint64_t want = (n_vec + kBlock - 1) / kBlock;
-    const uint64_t cap = static_cast<uint64_t>(p.multiProcessorCount > 0 ? p.multiProcessorCount : 256) * 4;
+    const uint64_t cap = static_cast<uint64_t>(p.multiProcessorCount > 0 ? p.multiProcessorCount : 256) * kBlocksPerCu;
     const int grid = static_cast<int>(want < cap ? want : cap);
     float best_fill = 1e30f, best_verify = 1e30f;
     bool ok = true;
