@@ -720,6 +720,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_replicas", &FakeKubeServer::set_replicas)
       .def("deployment_json", &FakeKubeServer::deployment_json)
       .def("lease_json", &FakeKubeServer::lease_json)
+      .def("add_node", &FakeKubeServer::add_node, py::arg("name"), py::arg("labels"), py::arg("resource"),
+           py::arg("gpus"), py::arg("unschedulable") = false)
       .def("inject", &FakeKubeServer::inject)
       .def("conflict_next", &FakeKubeServer::conflict_next)
       .def("set_latency", &FakeKubeServer::set_latency)

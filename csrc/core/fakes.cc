@@ -303,6 +303,51 @@ void FakeKubeServer::set_replicas(const std::string& ns, const std::string& name
   o.generation++;
 }
 
+void FakeKubeServer::add_node(const std::string& name, const std::map<std::string, std::string>& labels,
+                              const std::string& resource, int64_t gpus, bool unschedulable) {
+  std::lock_guard<std::mutex> lk(mu_);
+  nodes_[name] = Node{labels, resource, gpus, unschedulable};
+}
+
+void FakeKubeServer::handle_nodes(const std::string& query, HttpResponse* resp) {
+  std::vector<std::pair<std::string, std::string>> want;
+  for (auto& [k, v] : parse_query(query)) {
+    if (k != "labelSelector" || v.empty()) continue;
+    size_t i = 0;
+    while (i <= v.size()) {
+      size_t c = v.find(',', i);
+      if (c == std::string::npos) c = v.size();
+      std::string term = v.substr(i, c - i);
+      size_t eq = term.find('=');
+      if (eq != std::string::npos) {
+        std::string key = term.substr(0, eq), val = term.substr(eq + 1);
+        if (!val.empty() && val[0] == '=') val.erase(0, 1);  // "=="
+        want.emplace_back(key, val);
+      }
+      i = c + 1;
+    }
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  std::string items;
+  for (auto& [name, n] : nodes_) {
+    bool match = true;
+    for (auto& [k, v] : want) {
+      auto it = n.labels.find(k);
+      if (it == n.labels.end() || it->second != v) match = false;
+    }
+    if (!match) continue;
+    std::string labels;
+    for (auto& [k, v] : n.labels) labels += (labels.empty() ? "" : ",") + json_quote(k) + ":" + json_quote(v);
+    if (!items.empty()) items += ",";
+    items += "{\"metadata\":{\"name\":" + json_quote(name) + ",\"labels\":{" + labels + "}},\"spec\":{" +
+             (n.unschedulable ? "\"unschedulable\":true" : "") + "},\"status\":{\"allocatable\":{\"cpu\":\"192\"," +
+             json_quote(n.resource) + ":\"" + std::to_string(n.gpus) + "\"}}}";
+  }
+  resp->status = 200;
+  resp->body = "{\"kind\":\"NodeList\",\"apiVersion\":\"v1\",\"metadata\":{\"resourceVersion\":\"" +
+               std::to_string(rv_counter_) + "\"},\"items\":[" + items + "]}";
+}
+
 std::string FakeKubeServer::lease_json(const std::string& ns, const std::string& name) const {
   std::lock_guard<std::mutex> lk(mu_);
   auto it = leases_.find(ns + "/" + name);
@@ -513,6 +558,14 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   if (!token.empty() && req.header("Authorization") != "Bearer " + token) {
     auth_failures_++;
     fail(401, "Unauthorized", "Unauthorized");
+    return;
+  }
+  if (path == "/api/v1/nodes") {
+    if (req.method != "GET") {
+      fail(405, "MethodNotAllowed", "the server does not allow this method on the requested resource");
+      return;
+    }
+    handle_nodes(query, resp);
     return;
   }
   static const std::string lease_prefix = "/apis/coordination.k8s.io/v1/namespaces/";

@@ -106,6 +106,10 @@ class FakeKubeServer {
   // coordination.k8s.io/v1 Leases (leader election): raw JSON objects with resourceVersion
   // optimistic concurrency; POST creates (409 AlreadyExists), PUT replaces (409 Conflict).
   std::string lease_json(const std::string& ns, const std::string& name) const;  // "" if absent
+  // core/v1 Nodes for GPU-capacity discovery: GET /api/v1/nodes[?labelSelector=k=v,k2=v2]
+  // (equality selectors) returns a NodeList with status.allocatable[resource] = gpus.
+  void add_node(const std::string& name, const std::map<std::string, std::string>& labels,
+                const std::string& resource, int64_t gpus, bool unschedulable = false);
 
   uint64_t requests() const { return requests_.load(); }
   uint64_t gets() const { return gets_.load(); }
@@ -138,6 +142,14 @@ class FakeKubeServer {
     uint64_t rv = 0;
   };
   std::map<std::string, Lease> leases_;  // key: ns + "/" + name
+  struct Node {
+    std::map<std::string, std::string> labels;
+    std::string resource;
+    int64_t gpus = 0;
+    bool unschedulable = false;
+  };
+  std::map<std::string, Node> nodes_;
+  void handle_nodes(const std::string& query, HttpResponse* resp);
   void handle_lease(const HttpRequest& req, const std::vector<std::string>& parts, HttpResponse* resp);
   std::string token_;
   std::vector<InjectedFault> faults_;

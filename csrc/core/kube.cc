@@ -483,7 +483,7 @@ Status PodAutoScaler::scale(bool up, ScaleSpan* span) {
     span->before = span->after = cur;
     int32_t next;
     if (up) {
-      const int32_t max32 = go_int32(max_);  // scale.go:62-69
+      const int32_t max32 = go_int32(max_.load(std::memory_order_relaxed));  // scale.go:62-69
       if (cur >= max32) {
         log_->info("More than max pods running. No scale up. Replicas: " + std::to_string(cur));
         return Status::OK();

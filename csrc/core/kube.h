@@ -18,6 +18,7 @@
 //                            log messages; a no-op at a bound returns OK (scale.go:62-65,89-92).
 #pragma once
 
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -221,16 +222,18 @@ class PodAutoScaler {
   std::shared_ptr<DeploymentApi> api() const { return api_; }
   const std::string& deployment() const { return deployment_; }
   const std::string& namespace_() const { return ns_; }
-  int64_t max() const { return max_; }
+  int64_t max() const { return max_.load(std::memory_order_relaxed); }
   int64_t min() const { return min_; }
   int64_t scale_up_pods() const { return up_; }
   int64_t scale_down_pods() const { return down_; }
-  void set_max(int64_t m) { max_ = m; }
+  // Safe to call from another thread while the loop runs (GPU-capacity refresh).
+  void set_max(int64_t m) { max_.store(m, std::memory_order_relaxed); }
 
  private:
   std::shared_ptr<DeploymentApi> api_;
   std::string deployment_, ns_;
-  int64_t max_, min_, up_, down_;
+  std::atomic<int64_t> max_;
+  int64_t min_, up_, down_;
   std::shared_ptr<Logger> log_;
   std::shared_ptr<Clock> clock_;
   bool prefetch_pending_ = false;

@@ -66,22 +66,25 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     for w in rest.warnings:
         log.log("warning", w)
 
-    if cfg.gpu_aware_max == "local":
-        from .ops import gpu
-
-        try:
-            healthy = gpu.healthy_gpu_count()
-        except gpu.GpuProbeError as e:
-            healthy = 0
-            log.log("warning", f"GPU probe failed, max-pods not capped: {e}")
-        if healthy > 0:
-            for t in cfg.targets:
-                if t.max_pods > healthy:
-                    t.max_pods = healthy
-            log.log("info", f"Capping max-pods at {healthy} healthy GPUs", [("gpus", str(healthy))])
-
     multi = len(cfg.targets) > 1
     workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
+
+    capper = None
+    if cfg.gpu_aware_max:
+        from .kube.gpus import ClusterGpuCapacity, MaxPodsCapper
+
+        if cfg.gpu_aware_max == "local":
+            from .ops import gpu
+
+            def capacity() -> int:
+                return gpu.healthy_gpu_count() // cfg.gpus_per_pod
+        else:
+            capacity = ClusterGpuCapacity(rest, cfg.gpu_resource, cfg.gpu_node_selector, cfg.gpus_per_pod).pod_capacity
+        capper = MaxPodsCapper([w.runner.scaler for w in workers], [t.max_pods for t in cfg.targets], capacity,
+                               cfg.gpu_refresh_period_ns / 1e9, log=lambda lvl, m: log.log(lvl, m))
+        capper.refresh()
+        if cfg.gpu_aware_max == "cluster":
+            capper.start()
 
     trace_fd = -1
     if cfg.trace_file:
@@ -155,6 +158,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
             elector.release()
         for sig, h in prev.items():
             signal.signal(sig, h)
+        if capper is not None:
+            capper.stop()
         if metrics is not None:
             metrics.stop()
         if trace_fd >= 0:

@@ -83,6 +83,10 @@ class Config:
     log_format: str = "text"
     metrics_addr: str = ""
     gpu_aware_max: str = ""
+    gpu_resource: str = "amd.com/gpu"
+    gpu_node_selector: str = ""
+    gpus_per_pod: int = 1
+    gpu_refresh_period_ns: int = 60 * SECOND
     kube_config_path: str = ""
     pipeline_reads: bool = True
     busy_poll_ns: int = 25_000
@@ -146,7 +150,11 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.duration("leader-elect-lease-duration", 15 * SECOND, "How long a lease is valid without renewal")
     fs.duration("leader-elect-renew-deadline", 10 * SECOND, "How long the leader retries renewing before giving up leadership")
     fs.duration("leader-elect-retry-period", 2 * SECOND, "Interval between lease acquire/renew attempts")
-    fs.string("gpu-aware-max", "", "Cap max-pods at the healthy GPU count: local (probe this node's GPUs); empty disables")
+    fs.string("gpu-aware-max", "", "Cap max-pods at GPU capacity: local (GPUs on this node passing the HBM probe) or cluster (allocatable --gpu-resource on selected nodes); empty disables")
+    fs.string("gpu-resource", "amd.com/gpu", "Extended resource name of the GPUs (AMD GPU device plugin)")
+    fs.string("gpu-node-selector", "", "Label selector of the GPU nodes counted by --gpu-aware-max=cluster")
+    fs.int("gpus-per-pod", 1, "GPUs each worker pod requests")
+    fs.duration("gpu-refresh-period", 60 * SECOND, "How often --gpu-aware-max=cluster re-reads node capacity")
     return fs
 
 
@@ -237,6 +245,10 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         log_format=fs["log-format"],
         metrics_addr=fs["metrics-addr"],
         gpu_aware_max=fs["gpu-aware-max"],
+        gpu_resource=fs["gpu-resource"],
+        gpu_node_selector=fs["gpu-node-selector"],
+        gpus_per_pod=fs["gpus-per-pod"],
+        gpu_refresh_period_ns=fs["gpu-refresh-period"],
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
         pipeline_reads=fs["pipeline-reads"],
         busy_poll_ns=fs["busy-poll"],
@@ -258,8 +270,10 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
     if cfg.leader_elect and not (cfg.leader_elect_lease_duration_ns > cfg.leader_elect_renew_deadline_ns
                                  > cfg.leader_elect_retry_period_ns > 0):
         raise FlagError("leader election needs lease-duration > renew-deadline > retry-period > 0")
-    if cfg.gpu_aware_max not in ("", "local"):
-        raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty or local')
+    if cfg.gpu_aware_max not in ("", "local", "cluster"):
+        raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty, local or cluster')
+    if cfg.gpus_per_pod < 1:
+        raise FlagError(f'invalid value "{cfg.gpus_per_pod}" for flag -gpus-per-pod: must be >= 1')
     return cfg
 
 

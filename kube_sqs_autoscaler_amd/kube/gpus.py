@@ -1,0 +1,132 @@
+"""GPU-capacity cap for ``--max-pods`` (extension: the MI355X specialisation).
+
+The scaled Deployment is GPU-worker pods, one (or ``--gpus-per-pod``) MI355X each. Scaling past
+the GPUs the scheduler can place only creates Pending pods, so ``--gpu-aware-max`` caps the
+effective max-pods:
+
+* ``local`` -- GPUs on this node that pass the gfx950 HBM probe (``ops/gpu.py``), measured once
+  at start-up (sidecar deployments on the GPU node);
+* ``cluster`` -- the sum of ``status.allocatable[--gpu-resource]`` (default ``amd.com/gpu``, what
+  the AMD GPU device plugin advertises) over schedulable nodes matching ``--gpu-node-selector``,
+  divided by ``--gpus-per-pod``, refreshed every ``--gpu-refresh-period``.
+
+The cap is ``min(--max-pods, capacity)`` and is applied through the native actuator's atomic
+``set_max``, so a refresh never races a running scale decision. A failed refresh keeps the last
+good cap (never scales to zero capacity by accident); no capacity read yet means no cap.
+"""
+from __future__ import annotations
+
+import json
+import threading
+import urllib.parse
+from typing import Callable, List, Optional, Sequence
+
+from ..ops import native
+from .config import RestConfig
+
+
+class CapacityError(RuntimeError):
+    pass
+
+
+def _quantity(v) -> int:
+    """Integer resource quantity ("8", 8, "8000m" -> 8)."""
+    if isinstance(v, int):
+        return v
+    s = str(v).strip()
+    if s.endswith("m"):
+        return int(s[:-1]) // 1000
+    for suffix, mul in (("k", 1000), ("Ki", 1024)):
+        if s.endswith(suffix):
+            return int(s[: -len(suffix)]) * mul
+    return int(s)
+
+
+class ClusterGpuCapacity:
+    def __init__(self, rest: RestConfig, resource: str = "amd.com/gpu", node_selector: str = "",
+                 gpus_per_pod: int = 1, timeout_s: float = 10.0):
+        from ..autoscaler import tls_options
+
+        if gpus_per_pod < 1:
+            raise ValueError("gpus-per-pod must be >= 1")
+        self.rest = rest
+        self.resource = resource
+        self.selector = node_selector
+        self.gpus_per_pod = gpus_per_pod
+        self.http = native().HttpClient(rest.host, tls_options(rest), int(timeout_s * 1e9))
+
+    def _headers(self):
+        h = [("Accept", "application/json")]
+        token = self.rest.bearer_token
+        if self.rest.bearer_token_file:
+            try:
+                with open(self.rest.bearer_token_file) as f:
+                    token = f.read().strip() or token
+            except OSError:
+                pass
+        if token:
+            h.append(("Authorization", f"Bearer {token}"))
+        return h
+
+    def allocatable_gpus(self) -> int:
+        path = "/api/v1/nodes"
+        if self.selector:
+            path += "?labelSelector=" + urllib.parse.quote(self.selector, safe="=,!")
+        try:
+            status, _, body = self.http.request("GET", path, self._headers())
+        except native().NativeError as e:
+            raise CapacityError(f"list nodes: {e}")
+        if status != 200:
+            raise CapacityError(f"list nodes: HTTP {status}: {body[:200]!r}")
+        total = 0
+        for node in json.loads(body).get("items", []):
+            if (node.get("spec") or {}).get("unschedulable"):
+                continue
+            alloc = (node.get("status") or {}).get("allocatable") or {}
+            if self.resource in alloc:
+                total += _quantity(alloc[self.resource])
+        return total
+
+    def pod_capacity(self) -> int:
+        return self.allocatable_gpus() // self.gpus_per_pod
+
+
+class MaxPodsCapper:
+    """Applies ``min(configured max, capacity)`` to actuators, periodically."""
+
+    def __init__(self, scalers: Sequence, configured_max: Sequence[int], capacity: Callable[[], int],
+                 refresh_s: float = 60.0, log: Optional[Callable[[str, str], None]] = None):
+        self.scalers = list(scalers)
+        self.configured = list(configured_max)
+        self.capacity = capacity
+        self.refresh_s = refresh_s
+        self.log = log or (lambda lvl, m: None)
+        self.cap: Optional[int] = None
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+
+    def refresh(self) -> Optional[int]:
+        try:
+            cap = self.capacity()
+        except Exception as e:  # keep the last good cap
+            self.log("warning", f"GPU capacity refresh failed, keeping max-pods cap {self.cap}: {e}")
+            return self.cap
+        if cap != self.cap:
+            self.log("info", f"GPU capacity: {cap} pods; effective max-pods {[min(m, cap) for m in self.configured]}")
+        self.cap = cap
+        for s, m in zip(self.scalers, self.configured):
+            s.max = min(m, cap)
+        return cap
+
+    def start(self) -> None:
+        self._thread = threading.Thread(target=self._loop, name="ksa-gpu-capacity", daemon=True)
+        self._thread.start()
+
+    def _loop(self) -> None:
+        while not self._stop.wait(self.refresh_s):
+            self.refresh()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)

@@ -115,6 +115,20 @@ def build_gpu_probe(verbose: bool = True) -> Path | None:
     return GPU_SO
 
 
+def build_tools(verbose: bool = True) -> list[Path]:
+    """HIP tuning tools (csrc/tools/*.hip) -> kube_sqs_autoscaler_amd/ops/<name>.bin."""
+    hipcc = HIPCC if Path(HIPCC).exists() else "hipcc"
+    out = []
+    for src in sorted((CSRC / "tools").glob("*.hip")):
+        exe = OPS / (src.stem + ".bin")
+        if _stale(exe, [src], 0.0):
+            _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-w", str(src), "-o", str(exe)])
+            if verbose:
+                print(f"[build] hipcc --offload-arch={GPU_ARCH} -> {exe.relative_to(ROOT)}")
+        out.append(exe)
+    return out
+
+
 def build_native_tests(sanitizer: str | None = None, jobs: int = 8) -> Path:
     """Host-only C++ unit-test binary; `sanitizer` in {None, 'asan', 'tsan'}."""
     flags = {
@@ -135,6 +149,7 @@ def build_all(hip: bool = True, jobs: int = 8) -> dict:
     out = {"native": str(build_native(jobs=jobs))}
     if hip:
         out["gpu_probe"] = str(build_gpu_probe())
+        out["tools"] = [str(p) for p in build_tools()]
     return out
 
 
