@@ -36,3 +36,35 @@ def test_graft_smoke():
     import __graft_entry__ as g
 
     g.smoke()
+
+
+def test_cli_gpu_aware_max_local(tmp_path, capfd):
+    """--gpu-aware-max=local: the gfx950 probe counts healthy GPUs and caps max-pods at them."""
+    import yaml
+
+    from kube_sqs_autoscaler_amd.cli import main
+    from kube_sqs_autoscaler_amd.ops import gpu, native
+
+    nat = native()
+    n_gpus = gpu.device_count()
+    sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs.start()
+    kube.start()
+    try:
+        url = sqs.url + "/1/q"
+        sqs.set_attributes(url, {"ApproximateNumberOfMessages": "1000"})
+        kube.add_deployment("ml", "w", 1)
+        kc = tmp_path / "kc"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": "x"}}], "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"AWS_ACCESS_KEY_ID": "a", "AWS_SECRET_ACCESS_KEY": "b", "KUBE_CONFIG_PATH": str(kc)}
+        rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=w", "--kubernetes-namespace=ml", "--aws-region=us-east-1",
+                   f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s", "--max-pods=64",
+                   "--attribute-names=ApproximateNumberOfMessages", "--gpu-aware-max=local"], environ=env, max_iterations=100)
+        assert rc == 0
+        assert kube.replicas("ml", "w") == min(64, n_gpus)
+        assert f"GPU capacity: {n_gpus} pods" in capfd.readouterr().err
+    finally:
+        sqs.stop()
+        kube.stop()
