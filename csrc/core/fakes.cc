@@ -603,21 +603,26 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   const std::string& ns = parts[0];
   const std::string& name = parts[2];
   const bool scale = parts.size() == 4;
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = objs_.find(ns + "/" + name);
-  if (it == objs_.end()) {
-    fail(404, "NotFound", "deployments.apps \"" + name + "\" not found");
-    return;
-  }
-  Obj& o = it->second;
+  // Critical sections cover only the object state; rendering happens outside the lock so
+  // concurrent workers are not serialised by the fake (a real apiserver serves them in parallel).
+  Obj snapshot;
   if (req.method == "GET") {
-    gets_++;
-    resp->status = 200;
-    resp->body = scale ? render_scale(ns, name, o) : render_deployment(ns, name, o);
-    if (conflict_ > 0) {
-      conflict_--;
-      o.rv = ++rv_counter_;  // concurrent status update by the deployment controller
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = objs_.find(ns + "/" + name);
+      if (it == objs_.end()) {
+        fail(404, "NotFound", "deployments.apps \"" + name + "\" not found");
+        return;
+      }
+      gets_++;
+      snapshot = it->second;
+      if (conflict_ > 0) {
+        conflict_--;
+        it->second.rv = ++rv_counter_;  // concurrent status update by the deployment controller
+      }
     }
+    resp->status = 200;
+    resp->body = scale ? render_scale(ns, name, snapshot) : render_deployment(ns, name, snapshot);
     return;
   }
   if (req.method != "PUT" && req.method != "PATCH") {
@@ -635,34 +640,44 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
     fail(422, "Invalid", "metadata.resourceVersion: Invalid value: 0x0: must be specified for an update");
     return;
   }
-  if (!rvs.empty() && rvs != std::to_string(o.rv)) {
-    conflicts_++;
-    fail(409, "Conflict",
-         "Operation cannot be fulfilled on deployments.apps \"" + name +
-             "\": the object has been modified; please apply your changes to the latest version and try again");
-    return;
-  }
   const JsonValue* r = body.value.path({"spec", "replicas"});
   int64_t nr = 0;
   if (r && !r->as_int64(&nr)) {
     fail(400, "BadRequest", "spec.replicas must be an integer");
     return;
   }
-  if (!r) {
-    if (req.method == "PATCH") nr = o.replicas;   // merge patch without replicas: unchanged
-    else nr = scale ? 0 : 1;                      // Scale omitempty / Deployment defaulting
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = objs_.find(ns + "/" + name);
+    if (it == objs_.end()) {
+      fail(404, "NotFound", "deployments.apps \"" + name + "\" not found");
+      return;
+    }
+    Obj& o = it->second;
+    if (!rvs.empty() && rvs != std::to_string(o.rv)) {
+      conflicts_++;
+      fail(409, "Conflict",
+           "Operation cannot be fulfilled on deployments.apps \"" + name +
+               "\": the object has been modified; please apply your changes to the latest version and try again");
+      return;
+    }
+    if (!r) {
+      if (req.method == "PATCH") nr = o.replicas;  // merge patch without replicas: unchanged
+      else nr = scale ? 0 : 1;                     // Scale omitempty / Deployment defaulting
+    }
+    if (nr < 0) {
+      fail(422, "Invalid", "spec.replicas: Invalid value: " + std::to_string(nr) +
+                               ": must be greater than or equal to 0");
+      return;
+    }
+    writes_++;
+    if (o.replicas != static_cast<int32_t>(nr)) o.generation++;
+    o.replicas = static_cast<int32_t>(nr);
+    o.rv = ++rv_counter_;
+    snapshot = o;
   }
-  if (nr < 0) {
-    fail(422, "Invalid", "spec.replicas: Invalid value: " + std::to_string(nr) +
-                             ": must be greater than or equal to 0");
-    return;
-  }
-  writes_++;
-  if (o.replicas != static_cast<int32_t>(nr)) o.generation++;
-  o.replicas = static_cast<int32_t>(nr);
-  o.rv = ++rv_counter_;
   resp->status = 200;
-  resp->body = scale ? render_scale(ns, name, o) : render_deployment(ns, name, o);
+  resp->body = scale ? render_scale(ns, name, snapshot) : render_deployment(ns, name, snapshot);
 }
 
 }  // namespace ksa
