@@ -567,6 +567,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         if (!s.ok()) raise_status(s);
         return span;
       })
+      .def_property("dry_run", &PodAutoScaler::dry_run, &PodAutoScaler::set_dry_run)
       .def("prefetch", &PodAutoScaler::prefetch)
       .def("discard_prefetch", &PodAutoScaler::discard_prefetch)
       .def("scale_down", [](PodAutoScaler& p) {

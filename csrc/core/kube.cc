@@ -499,6 +499,13 @@ Status PodAutoScaler::scale(bool up, ScaleSpan* span) {
       next = wrap_sub32(cur, go_int32(down_));
       if (next < min32) next = min32;
     }
+    if (dry_run_) {
+      // Shadow mode: the decision is made and logged exactly as for a write, nothing is sent.
+      span->after = next;
+      log_->info("Dry run: would scale " + dir + ". Replicas: " + std::to_string(cur) + " -> " +
+                 std::to_string(next));
+      return Status::OK();
+    }
     Nanos tw = clock_->now();
     Status s = api_->update(deployment_, d.value, next);
     span->update_ns += clock_->now() - tw;

@@ -226,6 +226,9 @@ class PodAutoScaler {
   int64_t min() const { return min_; }
   int64_t scale_up_pods() const { return up_; }
   int64_t scale_down_pods() const { return down_; }
+  // Shadow mode (--dry-run): decide and log "Dry run: would scale ...", never write.
+  void set_dry_run(bool on) { dry_run_ = on; }
+  bool dry_run() const { return dry_run_; }
   // Safe to call from another thread while the loop runs (GPU-capacity refresh).
   void set_max(int64_t m) { max_.store(m, std::memory_order_relaxed); }
 
@@ -237,6 +240,7 @@ class PodAutoScaler {
   std::shared_ptr<Logger> log_;
   std::shared_ptr<Clock> clock_;
   bool prefetch_pending_ = false;
+  bool dry_run_ = false;
 
   Result<ScaleObject> read(ScaleSpan* span, bool* from_prefetch);
   Status scale(bool up, ScaleSpan* span);

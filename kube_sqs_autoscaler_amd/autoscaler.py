@@ -114,7 +114,8 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock,
                                   busy_poll_ns=cfg.busy_poll_ns)
     scaler = new_pod_autoscaler(target, kube_api, log, clock)
-    sqs_api = new_sqs_api(cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
+    scaler.dry_run = cfg.dry_run
+    sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
                           credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
     runner = nat.Runner(loop_config(target, cfg.pipeline_reads), sqs, scaler, clock, log)

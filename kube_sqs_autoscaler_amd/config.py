@@ -16,8 +16,10 @@ Extensions (all off or reference-equivalent by default):
 
 * ``--queue`` (repeatable): track several queue -> Deployment pairs from one process, one
   independent worker each (BASELINE.json: 1/2/4/8 tracked queues). Each spec is
-  ``url=<sqs-url>,deployment=<name>[,namespace=..][,<flag>=<value>...]`` where ``<flag>`` is
-  any per-target flag below (``attribute-names`` uses ``|`` between names).
+  ``url=<sqs-url>,deployment=<name>[,namespace=..][,region=..][,<flag>=<value>...]`` where
+  ``<flag>`` is any per-target flag below (``attribute-names`` uses ``|`` between names).
+* ``--dry-run``: shadow mode next to a running autoscaler -- same polls and decisions, logged
+  as ``Dry run: would scale ...``, no writes.
 * ``--scale-mode``: ``scale`` (autoscaling/v1 ``/scale`` subresource, default), ``deployment``
   (full-object GET+PUT exactly like the reference), ``patch`` (merge patch with a
   resourceVersion precondition).
@@ -65,6 +67,7 @@ class TargetConfig:
     scale_down_pods: int = 1
     max_pods: int = MI355X_MAX_PODS
     min_pods: int = 1
+    region: str = ""  # per-queue AWS region (--queue region=...); "" = --aws-region
 
     @property
     def name(self) -> str:
@@ -89,6 +92,7 @@ class Config:
     gpu_refresh_period_ns: int = 60 * SECOND
     kube_config_path: str = ""
     pipeline_reads: bool = True
+    dry_run: bool = False
     busy_poll_ns: int = 25_000
     trace_file: str = ""
     leader_elect: bool = False
@@ -137,6 +141,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("sqs-endpoint", "", "Override the SQS endpoint URL (VPC endpoint, local fake); empty uses the regional endpoint")
     fs.string("sqs-protocol", "query", "SQS wire protocol: query (AWS Query/XML) or json (AWS JSON 1.0)")
     fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
+    fs.bool("dry-run", False, "Shadow mode: poll and decide as usual, log the scaling that would happen, never write")
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
@@ -194,6 +199,8 @@ def parse_queue_spec(spec: str, base: TargetConfig) -> TargetConfig:
                 t.deployment = v
             elif k in ("namespace", "kubernetes-namespace"):
                 t.namespace = v
+            elif k in ("region", "aws-region"):
+                t.region = v
             elif k == "attribute-names":
                 t.attribute_names = parse_attribute_names(v.replace("|", ","))
             elif k in _TARGET_INT_KEYS:
@@ -251,6 +258,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         gpu_refresh_period_ns=fs["gpu-refresh-period"],
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
         pipeline_reads=fs["pipeline-reads"],
+        dry_run=fs["dry-run"],
         busy_poll_ns=fs["busy-poll"],
         trace_file=fs["trace-file"],
         leader_elect=fs["leader-elect"],

@@ -153,3 +153,33 @@ def test_trace_file_spans(servers, tmp_path):
     assert spans[0]["depth"] == 500 and spans[0]["up"] == "scaled" and spans[0]["replicas_after"] == 2
     assert spans[0]["deployment"] == "gpu/workers" and spans[0]["queue"] == url and spans[0]["prefetched"] is True
     assert spans[0]["patch_latency_ns"] > 0 and spans[0]["depth_ns"] > 0
+
+
+def test_dry_run_shadow_mode(servers, capfd):
+    from kube_sqs_autoscaler_amd.cli import main
+
+    sqs, kube, env = servers
+    url = sqs.url + "/123/jobs"
+    sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500"})
+    kube.add_deployment("gpu", "workers", 2)
+    writes = kube.writes()
+    rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=workers", "--kubernetes-namespace=gpu",
+               f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+               "--attribute-names=ApproximateNumberOfMessages", "--dry-run"], environ=env, max_iterations=3)
+    assert rc == 0 and kube.writes() == writes and kube.replicas("gpu", "workers") == 2
+    err = capfd.readouterr().err
+    assert err.count('msg="Dry run: would scale up. Replicas: 2 -> 3"') == 3
+
+
+def test_queue_spec_region(servers):
+    from kube_sqs_autoscaler_amd.cli import main
+
+    sqs, kube, env = servers
+    # the fake verifies signatures for REGION only: a queue signed for another region fails,
+    # the one with region=REGION works although --aws-region is wrong
+    sqs.set_attributes(sqs.url + "/1/a", {"ApproximateNumberOfMessages": "500"})
+    kube.add_deployment("gpu", "a", 1)
+    rc = main(["--aws-region=eu-central-1", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+               "--attribute-names=ApproximateNumberOfMessages",
+               "--queue", f"url={sqs.url}/1/a,deployment=a,namespace=gpu,region={REGION}"], environ=env, max_iterations=2)
+    assert rc == 0 and kube.replicas("gpu", "a") == 3 and sqs.signature_failures() == 0
