@@ -66,7 +66,10 @@ def main(argv=None) -> int:
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
     device = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl" if use_cuda else "gloo")
+        if use_cuda:  # RCCL; eager init bound to this rank's GPU
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     def barrier_sync():
         if world > 1:
