@@ -37,11 +37,12 @@ __global__ __launch_bounds__(256) void fill(u32x4* __restrict__ buf, uint64_t n,
   if ((threadIdx.x & 63) == 0) atomicAdd(sum, acc);
 }
 
-template <int U, bool NT>
+// SUM: also accumulate the 64-bit checksum of what was read (what the shipped probe does).
+template <int U, bool NT, bool SUM = false>
 __global__ __launch_bounds__(256) void verify(const u32x4* __restrict__ buf, uint64_t n, unsigned long long* bad_out) {
   const uint64_t nt = static_cast<uint64_t>(gridDim.x) * 256;
   uint64_t v = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
-  unsigned long long bad = 0;
+  unsigned long long bad = 0, acc = 0;
   for (; v + (U - 1) * nt < n; v += U * nt) {
     u32x4 x[U];
 #pragma unroll
@@ -49,11 +50,18 @@ __global__ __launch_bounds__(256) void verify(const u32x4* __restrict__ buf, uin
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const u32x4 p = pattern4(v + u * nt);
+      if (SUM) acc += static_cast<unsigned long long>(x[u].x) + x[u].y + x[u].z + x[u].w;
       bad += (x[u].x != p.x) + (x[u].y != p.y) + (x[u].z != p.z) + (x[u].w != p.w);
     }
   }
-  for (int off = 32; off > 0; off >>= 1) bad += __shfl_xor(bad, off, 64);
-  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(bad_out, bad);
+  for (int off = 32; off > 0; off >>= 1) {
+    bad += __shfl_xor(bad, off, 64);
+    if (SUM) acc += __shfl_xor(acc, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (bad) atomicAdd(bad_out, bad);
+    if (SUM) atomicAdd(bad_out + 1, acc);
+  }
 }
 
 template <class K>
@@ -76,16 +84,16 @@ float best_ms(K launch, int reps) {
   return best;
 }
 
-template <int U, bool NT>
+template <int U, bool NT, bool SUM = false>
 void run(u32x4* buf, uint64_t n, unsigned long long* ctr, int cus, int bpc) {
   const int grid = cus * bpc;
   const double bytes = static_cast<double>(n) * 16;
   float f = best_ms([&] { hipLaunchKernelGGL((fill<U, NT>), dim3(grid), dim3(256), 0, nullptr, buf, n, ctr); }, 5);
-  float v = best_ms([&] { hipLaunchKernelGGL((verify<U, NT>), dim3(grid), dim3(256), 0, nullptr, buf, n, ctr + 1); }, 5);
-  unsigned long long h[2];
+  float v = best_ms([&] { hipLaunchKernelGGL((verify<U, NT, SUM>), dim3(grid), dim3(256), 0, nullptr, buf, n, ctr + 1); }, 5);
+  unsigned long long h[3];
   hipMemcpy(h, ctr, sizeof h, hipMemcpyDeviceToHost);
-  std::printf("{\"unroll\":%d,\"nontemporal\":%s,\"blocks_per_cu\":%d,\"write_GBps\":%.1f,\"read_verify_GBps\":%.1f,\"mismatches\":%llu}\n",
-              U, NT ? "true" : "false", bpc, bytes / (f * 1e6), bytes / (v * 1e6), h[1]);
+  std::printf("{\"unroll\":%d,\"nontemporal\":%s,\"checksum\":%s,\"blocks_per_cu\":%d,\"write_GBps\":%.1f,\"read_verify_GBps\":%.1f,\"mismatches\":%llu}\n",
+              U, NT ? "true" : "false", SUM ? "true" : "false", bpc, bytes / (f * 1e6), bytes / (v * 1e6), h[1]);
 }
 
 int main() {
@@ -96,13 +104,14 @@ int main() {
   u32x4* buf;
   unsigned long long* ctr;
   hipMalloc(&buf, bytes);
-  hipMalloc(&ctr, 16);
-  hipMemset(ctr, 0, 16);
-  for (int bpc : {2, 4, 8, 16}) {
+  hipMalloc(&ctr, 32);
+  hipMemset(ctr, 0, 32);
+  for (int bpc : {2, 4, 8}) {
     run<4, true>(buf, n, ctr, p.multiProcessorCount, bpc);
-    run<4, false>(buf, n, ctr, p.multiProcessorCount, bpc);
     run<8, true>(buf, n, ctr, p.multiProcessorCount, bpc);
-    run<8, false>(buf, n, ctr, p.multiProcessorCount, bpc);
+    run<4, true, true>(buf, n, ctr, p.multiProcessorCount, bpc);
+    run<8, true, true>(buf, n, ctr, p.multiProcessorCount, bpc);
+    run<16, true, true>(buf, n, ctr, p.multiProcessorCount, bpc);
   }
   hipFree(buf);
   hipFree(ctr);

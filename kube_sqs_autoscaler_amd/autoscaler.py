@@ -13,6 +13,7 @@ These are the constructors of the reference, rebuilt over the native runtime:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Mapping, Optional
 
@@ -75,8 +76,13 @@ def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query",
     o.protocol = nat.SqsProtocol.Json if protocol == "json" else nat.SqsProtocol.Query
     o.timeout_ns = timeout_ns
     o.busy_poll_ns = busy_poll_ns
+    env = os.environ if environ is None else environ
     if tls is not None:
         o.tls = tls
+    elif env.get("AWS_CA_BUNDLE"):  # aws-sdk-go v1 session: custom CA bundle for AWS endpoints
+        t = nat.TlsOptions()
+        t.ca_file = env["AWS_CA_BUNDLE"]
+        o.tls = t
     creds = credentials if credentials is not None else make_chain_provider(environ=environ, region=region)
     return nat.HttpSqsApi(o, creds, clock)
 

@@ -183,3 +183,39 @@ def test_queue_spec_region(servers):
                "--attribute-names=ApproximateNumberOfMessages",
                "--queue", f"url={sqs.url}/1/a,deployment=a,namespace=gpu,region={REGION}"], environ=env, max_iterations=2)
     assert rc == 0 and kube.replicas("gpu", "a") == 3 and sqs.signature_failures() == 0
+
+
+def test_main_end_to_end_over_tls(nat, tmp_path, capfd):
+    """Both endpoints on TLS: kubeconfig CA data for the apiserver, AWS_CA_BUNDLE for SQS."""
+    import base64
+
+    from kube_sqs_autoscaler_amd.cli import main
+
+    sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs.require_signature(AKID, SECRET, REGION)
+    sqs.start("127.0.0.1", 0, True)
+    kube.require_token(TOKEN)
+    kube.start("127.0.0.1", 0, True)
+    try:
+        bundle = tmp_path / "aws-ca.pem"
+        bundle.write_text(sqs.cert_pem)
+        kc = tmp_path / "kc"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t",
+            "clusters": [{"name": "c", "cluster": {"server": kube.url,
+                                                   "certificate-authority-data": base64.b64encode(kube.cert_pem.encode()).decode()}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}], "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"AWS_ACCESS_KEY_ID": AKID, "AWS_SECRET_ACCESS_KEY": SECRET, "KUBE_CONFIG_PATH": str(kc),
+               "AWS_CA_BUNDLE": str(bundle)}
+        url = sqs.url + "/123/jobs"
+        assert url.startswith("https://") and kube.url.startswith("https://")
+        sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500"})
+        kube.add_deployment("gpu", "workers", 1)
+        rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=workers", "--kubernetes-namespace=gpu",
+                   f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+                   "--attribute-names=ApproximateNumberOfMessages"], environ=env, max_iterations=3)
+        assert rc == 0 and kube.replicas("gpu", "workers") == 4
+        assert "level=error" not in capfd.readouterr().err
+    finally:
+        sqs.stop()
+        kube.stop()
