@@ -19,7 +19,7 @@ from __future__ import annotations
 import json
 import threading
 import urllib.parse
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, Optional, Sequence
 
 from ..ops import native
 from .config import RestConfig

@@ -22,7 +22,7 @@ then every API call advances the clock by its latency.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
+from typing import Dict, List, Optional, Sequence, Set, Tuple
 
 INT32_MIN = -(1 << 31)
 

@@ -12,11 +12,8 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 from ..ops import native
-from .oracle import Event, Faults, Latency, Params, depth_of, simulate
+from .oracle import Event, Faults, depth_of, simulate
 from .traces import Scenario
-
-_DIRECTIONS = ("none", "cooldown", "scaled", "noop", "failed")
-
 
 def _records_to_events(recs: Sequence[dict], init_replicas: int) -> List[Event]:
     out = []
@@ -72,9 +69,6 @@ def _faulty_fakes(nat, clock, scenario: Scenario, faults: Faults, counter: _Poll
             self.replicas = replicas
             self.rv = 1
             self.direction = "up"
-
-        def _dir(self) -> str:
-            return self.direction
 
         def get(self, name):
             counter.gets_this_poll += 1
