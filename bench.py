@@ -145,6 +145,12 @@ def main(argv=None) -> int:
                 r = measure(1, 200, 5, mode, pipeline=pl, sqs_latency_ns=2_000_000, kube_latency_ns=1_000_000)
                 wan[name] = r.summary()["p50_ms"]
             extra["wan_model_sqs2ms_kube1ms_p50_ms"] = wan
+            from kube_sqs_autoscaler_amd.bench.latency import phase_breakdown
+
+            extra["phase_median_us"] = {
+                "default": phase_breakdown(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp),
+                "reference_equivalent": phase_breakdown(mode="deployment", pipeline=False),
+            }
         extra["decision_parity"] = _parity_summary()
         out = {
             "metric": METRIC,

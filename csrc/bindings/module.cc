@@ -254,6 +254,21 @@ PYBIND11_MODULE(_ksa_native, m) {
              d["scope"] = dbg.scope;
              return py::make_tuple(h, d);
            })
+      .def("sign_prepared",
+           [](SigV4Signer& s, const Credentials& c, int64_t unix_ns, const std::string& method,
+              const std::string& path, const std::string& query, py::object headers, py::bytes body) {
+             // prepare() + sign_prepared(): the per-queue fast path HttpSqsApi uses
+             SigV4Prepared p = s.prepare(method, path, query, headers_from(headers), std::string(body));
+             Headers h;
+             SignDebug dbg;
+             s.sign_prepared(p, c, unix_ns, &h, &dbg);
+             py::dict d;
+             d["canonical_request"] = dbg.canonical_request;
+             d["string_to_sign"] = dbg.string_to_sign;
+             d["signed_headers"] = dbg.signed_headers;
+             d["signature"] = dbg.signature;
+             return py::make_tuple(h, d);
+           })
       .def("signing_key_hex", [](SigV4Signer& s, const std::string& secret, const std::string& date) {
         return hex_encode(s.signing_key(secret, date));
       });

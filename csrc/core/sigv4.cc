@@ -320,6 +320,104 @@ void SigV4Signer::sign(const Credentials& creds, int64_t unix_ns, const std::str
   }
 }
 
+SigV4Prepared SigV4Signer::prepare(const std::string& method, const std::string& path,
+                                   const std::string& raw_query, const Headers& headers,
+                                   const std::string& body) const {
+  SigV4Prepared p;
+  p.method = method;
+  p.path = path;
+  p.raw_query = raw_query;
+  p.headers = headers;
+  p.payload_hash = sha256_hex(body);
+  // Reuse the generic canonicaliser for the fixed parts so both paths agree by construction.
+  Headers fixed;
+  for (auto& [k, v] : headers) {
+    std::string lk = lower(k);
+    if (lk == "x-amz-date" || lk == "x-amz-security-token" || ignored_header(lk)) continue;
+    fixed.emplace_back(k, v);
+  }
+  std::vector<std::pair<std::string, std::string>> hs;
+  for (auto& [k, v] : fixed) {
+    std::string lk = lower(k);
+    bool merged = false;
+    for (auto& h : hs)
+      if (h.first == lk) {
+        h.second += "," + trimall(v);
+        merged = true;
+      }
+    if (!merged) hs.emplace_back(lk, trimall(v));
+  }
+  std::sort(hs.begin(), hs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  p.canon = std::move(hs);
+  p.canonical_uri = path.empty() ? "/" : aws_uri_encode(path, true);
+  auto params = parse_query(raw_query);
+  std::sort(params.begin(), params.end());
+  for (size_t i = 0; i < params.size(); ++i) {
+    if (i) p.canonical_query.push_back('&');
+    p.canonical_query += aws_uri_encode(params[i].first, false) + "=" + aws_uri_encode(params[i].second, false);
+  }
+  return p;
+}
+
+void SigV4Signer::sign_prepared(const SigV4Prepared& p, const Credentials& creds, int64_t unix_ns, Headers* out,
+                                SignDebug* debug) {
+  const std::string amzdate = amz_date(unix_ns);
+  const std::string date = amzdate.substr(0, 8);
+  *out = p.headers;
+  out->emplace_back("X-Amz-Date", amzdate);
+  if (!creds.session_token.empty()) out->emplace_back("X-Amz-Security-Token", creds.session_token);
+  // merge the two per-request headers into the sorted fixed ones
+  std::pair<std::string, std::string> extra[2] = {{"x-amz-date", amzdate},
+                                                  {"x-amz-security-token", trimall(creds.session_token)}};
+  const int n_extra = creds.session_token.empty() ? 1 : 2;
+  std::string ch, sh;
+  ch.reserve(256);
+  size_t i = 0;
+  int e = 0;
+  auto emit = [&](const std::string& k, const std::string& v) {
+    ch += k;
+    ch.push_back(':');
+    ch += v;
+    ch.push_back('\n');
+    if (!sh.empty()) sh.push_back(';');
+    sh += k;
+  };
+  while (i < p.canon.size() || e < n_extra) {
+    if (e < n_extra && (i >= p.canon.size() || extra[e].first < p.canon[i].first)) {
+      emit(extra[e].first, extra[e].second);
+      ++e;
+    } else {
+      emit(p.canon[i].first, p.canon[i].second);
+      ++i;
+    }
+  }
+  std::string creq;
+  creq.reserve(p.method.size() + p.canonical_uri.size() + p.canonical_query.size() + ch.size() + sh.size() + 80);
+  creq += p.method;
+  creq.push_back('\n');
+  creq += p.canonical_uri;
+  creq.push_back('\n');
+  creq += p.canonical_query;
+  creq.push_back('\n');
+  creq += ch;
+  creq.push_back('\n');
+  creq += sh;
+  creq.push_back('\n');
+  creq += p.payload_hash;
+  const std::string scope = date + "/" + region_ + "/" + service_ + "/aws4_request";
+  const std::string sts = "AWS4-HMAC-SHA256\n" + amzdate + "\n" + scope + "\n" + sha256_hex(creq);
+  const std::string sig = hex_encode(signing_mac(creds.secret_access_key, date).mac(sts));
+  out->emplace_back("Authorization", "AWS4-HMAC-SHA256 Credential=" + creds.access_key_id + "/" + scope +
+                                         ", SignedHeaders=" + sh + ", Signature=" + sig);
+  if (debug) {
+    debug->canonical_request = creq;
+    debug->string_to_sign = sts;
+    debug->signed_headers = sh;
+    debug->signature = sig;
+    debug->scope = scope;
+  }
+}
+
 Status sigv4_verify(const std::string& method, const std::string& path,
                     const std::string& raw_query, const Headers& headers,
                     const std::string& body, const std::string& expected_access_key,

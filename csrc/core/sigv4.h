@@ -102,6 +102,17 @@ struct SignDebug {
   std::string scope;
 };
 
+// Signing state precomputed for a request that is re-sent unchanged except for its date (the
+// per-queue SQS poll): body hash, canonical URI/query and the canonical form of every fixed
+// header are built once, so a poll only hashes the small canonical request and MACs it.
+struct SigV4Prepared {
+  std::string method, path, raw_query;
+  Headers headers;            // fixed headers as sent (Host, Content-Type, ...)
+  std::string payload_hash;   // hex SHA-256 of the body
+  std::vector<std::pair<std::string, std::string>> canon;  // lower-case name, trimmed value; sorted
+  std::string canonical_uri, canonical_query;
+};
+
 class SigV4Signer {
  public:
   SigV4Signer(std::string region, std::string service)
@@ -113,6 +124,12 @@ class SigV4Signer {
   void sign(const Credentials& creds, int64_t unix_ns, const std::string& method,
             const std::string& path, const std::string& raw_query, Headers* headers,
             const std::string& body, SignDebug* debug = nullptr);
+
+  SigV4Prepared prepare(const std::string& method, const std::string& path, const std::string& raw_query,
+                        const Headers& headers, const std::string& body) const;
+  // Same result as sign() on (prepared headers, body), without re-deriving the fixed parts.
+  void sign_prepared(const SigV4Prepared& p, const Credentials& creds, int64_t unix_ns, Headers* out,
+                     SignDebug* debug = nullptr);
 
   // Derived key for (secret, yyyymmdd); cached per day.
   std::string signing_key(const std::string& secret, const std::string& date);

@@ -88,44 +88,59 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
   auto cr = creds_.get(clock_->unix_nanos());
   if (!cr.ok()) return Result<AttrMap>::Err(cr.status);
 
+  std::unique_lock<std::mutex> prep_lock(prep_mu_);
+  std::string key = queue_url;
+  for (auto& n : names) {
+    key.push_back('\x1f');
+    key += n;
+  }
+  if (key != prepared_key_) {
+    HttpRequest proto;
+    proto.method = "POST";
+    proto.target = url_.path.empty() ? "/" : url_.path;
+    proto.headers.emplace_back("Host", url_.host_header());
+    if (opts_.protocol == SqsProtocol::Query) {
+      // url.Values.Encode(): keys sorted, QueryEscape'd.
+      std::vector<std::pair<std::string, std::string>> params;
+      params.emplace_back("Action", "GetQueueAttributes");
+      for (size_t i = 0; i < names.size(); ++i)
+        params.emplace_back("AttributeName." + std::to_string(i + 1), names[i]);
+      params.emplace_back("QueueUrl", queue_url);
+      params.emplace_back("Version", "2012-11-05");
+      std::stable_sort(params.begin(), params.end(),
+                       [](const auto& a, const auto& b) { return a.first < b.first; });
+      for (size_t i = 0; i < params.size(); ++i) {
+        if (i) proto.body.push_back('&');
+        proto.body += aws_uri_encode(params[i].first, false) + "=" + aws_uri_encode(params[i].second, false);
+      }
+      proto.headers.emplace_back("Content-Type", "application/x-www-form-urlencoded; charset=utf-8");
+    } else {
+      JsonValue body = JsonValue::make_object();
+      JsonValue arr;
+      arr.type = JsonValue::Type::Array;
+      for (auto& n : names) arr.arr.push_back(JsonValue::make_string(n));
+      body.set("AttributeNames", std::move(arr));
+      body.set("QueueUrl", JsonValue::make_string(queue_url));
+      proto.body = json_serialize(body);
+      proto.headers.emplace_back("Content-Type", "application/x-amz-json-1.0");
+      proto.headers.emplace_back("X-Amz-Target", "AmazonSQS.GetQueueAttributes");
+    }
+    std::string path = proto.target, query;
+    size_t q = path.find('?');
+    if (q != std::string::npos) {
+      query = path.substr(q + 1);
+      path = path.substr(0, q);
+    }
+    prepared_ = signer_.prepare("POST", path, query, proto.headers, proto.body);
+    prepared_body_ = std::move(proto.body);
+    prepared_key_ = std::move(key);
+  }
   HttpRequest req;
   req.method = "POST";
   req.target = url_.path.empty() ? "/" : url_.path;
-  req.headers.emplace_back("Host", url_.host_header());
-  if (opts_.protocol == SqsProtocol::Query) {
-    // url.Values.Encode(): keys sorted, QueryEscape'd.
-    std::vector<std::pair<std::string, std::string>> params;
-    params.emplace_back("Action", "GetQueueAttributes");
-    for (size_t i = 0; i < names.size(); ++i)
-      params.emplace_back("AttributeName." + std::to_string(i + 1), names[i]);
-    params.emplace_back("QueueUrl", queue_url);
-    params.emplace_back("Version", "2012-11-05");
-    std::stable_sort(params.begin(), params.end(),
-                     [](const auto& a, const auto& b) { return a.first < b.first; });
-    for (size_t i = 0; i < params.size(); ++i) {
-      if (i) req.body.push_back('&');
-      req.body += aws_uri_encode(params[i].first, false) + "=" + aws_uri_encode(params[i].second, false);
-    }
-    req.headers.emplace_back("Content-Type", "application/x-www-form-urlencoded; charset=utf-8");
-  } else {
-    JsonValue body = JsonValue::make_object();
-    JsonValue arr;
-    arr.type = JsonValue::Type::Array;
-    for (auto& n : names) arr.arr.push_back(JsonValue::make_string(n));
-    body.set("AttributeNames", std::move(arr));
-    body.set("QueueUrl", JsonValue::make_string(queue_url));
-    req.body = json_serialize(body);
-    req.headers.emplace_back("Content-Type", "application/x-amz-json-1.0");
-    req.headers.emplace_back("X-Amz-Target", "AmazonSQS.GetQueueAttributes");
-  }
-  std::string path = req.target;
-  std::string query;
-  size_t q = path.find('?');
-  if (q != std::string::npos) {
-    query = path.substr(q + 1);
-    path = path.substr(0, q);
-  }
-  signer_.sign(cr.value, clock_->unix_nanos(), req.method, path, query, &req.headers, req.body);
+  req.body = prepared_body_;
+  signer_.sign_prepared(prepared_, cr.value, clock_->unix_nanos(), &req.headers);
+  prep_lock.unlock();
 
   HttpResponse resp;
   Status s = http_->round_trip(req, &resp);

@@ -83,6 +83,12 @@ class HttpSqsApi final : public SqsApi {
   Status endpoint_status_;
   Url url_;
   std::unique_ptr<HttpClient> http_;
+  // Prepared request for the last (queue, attribute names): the body and every fixed signing
+  // input are built once per queue instead of once per poll.
+  std::mutex prep_mu_;  // guards the prepared request (an HttpSqsApi may be shared by workers)
+  std::string prepared_key_;
+  SigV4Prepared prepared_;
+  std::string prepared_body_;
   mutable std::mutex mu_;
   SqsApiStats stats_;
   uint64_t rng_ = 0x9E3779B97F4A7C15ULL;

@@ -172,6 +172,33 @@ class BenchEnv:
             self._devnull = None
 
 
+def phase_breakdown(steps: int = 2000, warmup: int = 200, **kw) -> Dict[str, float]:
+    """Median per-phase times (us) of the scaling iteration, from the native span trace.
+
+    ``depth_us`` is the SQS call (the pipelined GET is in flight during it), ``get_wait_us`` the
+    extra wait for the GET response afterwards (0 when it arrived during the SQS call),
+    ``write_us`` the replica write, ``patch_us`` the poll->patch span the metric reports.
+    """
+    import json
+    import statistics
+    import tempfile
+
+    env = BenchEnv(1, **kw)
+    try:
+        env.run(warmup)
+        with tempfile.TemporaryFile() as f:
+            env.runners[0].set_trace_fd(f.fileno())
+            env.run(steps)
+            env.runners[0].set_trace_fd(-1)
+            f.seek(0)
+            spans = [json.loads(l) for l in f.read().decode().splitlines()]
+    finally:
+        env.close()
+    med = lambda k: round(statistics.median(s[k] for s in spans) / 1e3, 2)
+    return {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
+            "patch_us": med("patch_latency_ns")}
+
+
 def measure(queues: int, steps: int, warmup: int, mode: str = "scale", **kw) -> LatencyResult:
     env = BenchEnv(queues, mode, **kw)
     try:
