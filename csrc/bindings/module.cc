@@ -618,6 +618,14 @@ PYBIND11_MODULE(_ksa_native, m) {
                     std::shared_ptr<Logger>>(),
            py::arg("config"), py::arg("sqs"), py::arg("scaler"), py::arg("clock"), py::arg("logger"))
       .def("arm", &Runner::arm)
+      .def("poll_once", [](Runner& r) {
+        IterationRecord rec;
+        {
+          py::gil_scoped_release rel;
+          rec = r.poll_once();
+        }
+        return record_dict(rec);
+      })
       .def("step", [](Runner& r) {
         IterationRecord rec;
         {
@@ -677,6 +685,20 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("join", &Supervisor::join, py::call_guard<py::gil_scoped_release>())
       .def("__len__", &Supervisor::size)
       .def("runner", &Supervisor::runner);
+
+  py::class_<Scheduler, std::shared_ptr<Scheduler>>(m, "Scheduler")
+      .def(py::init([](size_t threads) { return std::make_shared<Scheduler>(threads); }), py::arg("threads"))
+      .def("add", &Scheduler::add)
+      .def("start", &Scheduler::start, py::arg("max_iterations") = -1)
+      .def("stop", &Scheduler::stop)
+      .def("stopped", &Scheduler::stopped)
+      .def("wait", &Scheduler::wait, py::arg("timeout_ns"), py::call_guard<py::gil_scoped_release>())
+      .def("join", &Scheduler::join, py::call_guard<py::gil_scoped_release>())
+      .def("__len__", &Scheduler::size)
+      .def("threads", &Scheduler::threads)
+      .def("runner", &Scheduler::runner)
+      .def("late_polls", &Scheduler::late_polls)
+      .def("max_lateness_ns", &Scheduler::max_lateness);
 
   m.def("percentile", &percentile);
 

@@ -3,6 +3,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <limits>
 
@@ -49,12 +50,17 @@ void Runner::arm() {
 }
 
 IterationRecord Runner::step(StopFlag* stop) {
-  IterationRecord rec;
   // main.go:41 -- sleep BEFORE the poll.
   if (!clock_->sleep(cfg_.poll_period, stop)) {
+    IterationRecord rec;
     rec.stopped = true;
     return rec;
   }
+  return poll_once();
+}
+
+IterationRecord Runner::poll_once() {
+  IterationRecord rec;
   rec.index = ++index_;
   const Nanos t0 = clock_->now();
   rec.t_poll = t0;
@@ -264,6 +270,101 @@ void Supervisor::join() {
 Supervisor::~Supervisor() {
   stop();
   join();
+}
+
+// ---------------------------------------------------------------------------------------
+
+Scheduler::Scheduler(size_t threads, std::shared_ptr<Clock> clock)
+    : nthreads_(threads < 1 ? 1 : threads), clock_(std::move(clock)) {}
+
+Scheduler::~Scheduler() {
+  stop();
+  join();
+}
+
+void Scheduler::start(int64_t max_iterations) {
+  std::lock_guard<std::mutex> lk(mu_);
+  max_iter_ = max_iterations;
+  done_.assign(runners_.size(), 0);
+  heap_.clear();
+  for (size_t i = 0; i < runners_.size(); ++i) {
+    runners_[i]->arm();
+    heap_.push_back(Item{clock_->now() + std::max<Nanos>(runners_[i]->config().poll_period, 0), i});
+  }
+  std::make_heap(heap_.begin(), heap_.end(), std::greater<Item>());
+  finished_ = 0;
+  running_ = nthreads_;
+  for (size_t t = 0; t < nthreads_; ++t) threads_.emplace_back([this] { worker(); });
+}
+
+void Scheduler::worker() {
+  std::unique_lock<std::mutex> lk(mu_);
+  while (!stop_.load() && finished_ < runners_.size()) {
+    if (heap_.empty()) {  // every runner is being polled by another worker
+      cv_.wait(lk, [&] { return stop_.load() || !heap_.empty() || finished_ >= runners_.size(); });
+      continue;
+    }
+    const Nanos now = clock_->now();
+    const Item top = heap_.front();
+    if (top.due > now) {
+      cv_wait_for(cv_, lk, top.due - now, [&] {
+        return stop_.load() || heap_.empty() || heap_.front().due != top.due || heap_.front().idx != top.idx ||
+               clock_->now() >= top.due;
+      });
+      continue;
+    }
+    std::pop_heap(heap_.begin(), heap_.end(), std::greater<Item>());
+    heap_.pop_back();
+    if (now - top.due > kMillisecond) {
+      late_++;
+      max_late_ = std::max(max_late_, now - top.due);
+    }
+    lk.unlock();
+    runners_[top.idx]->poll_once();
+    lk.lock();
+    if (max_iter_ > 0 && ++done_[top.idx] >= max_iter_) {
+      ++finished_;
+    } else {
+      heap_.push_back(Item{clock_->now() + std::max<Nanos>(runners_[top.idx]->config().poll_period, 0), top.idx});
+      std::push_heap(heap_.begin(), heap_.end(), std::greater<Item>());
+    }
+    cv_.notify_all();
+  }
+  --running_;
+  cv_.notify_all();
+}
+
+void Scheduler::stop() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_.store(true);
+  }
+  cv_.notify_all();
+}
+
+bool Scheduler::wait(Nanos timeout) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (timeout <= 0) {
+    cv_.wait(lk, [&] { return running_ == 0; });
+    return true;
+  }
+  return cv_wait_for(cv_, lk, timeout, [&] { return running_ == 0; });
+}
+
+void Scheduler::join() {
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+uint64_t Scheduler::late_polls() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return late_;
+}
+
+Nanos Scheduler::max_lateness() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return max_late_;
 }
 
 Nanos percentile(std::vector<Nanos> v, double p) {

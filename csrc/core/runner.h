@@ -93,6 +93,9 @@ class Runner {
   void arm();
   // One loop iteration; `stop` may interrupt the sleep.
   IterationRecord step(StopFlag* stop = nullptr);
+  // The iteration without the leading sleep (main.go:43-77); used by Scheduler, which owns
+  // the waiting between polls.
+  IterationRecord poll_once();
   // The reference's Run(): arm(), then step() until stopped (or max_iterations > 0 reached).
   void run(StopFlag* stop, int64_t max_iterations = -1);
 
@@ -159,6 +162,55 @@ class Supervisor {
 // JSON line of an iteration record (span trace format).
 std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std::string& queue,
                            const std::string& deployment);
+
+// N runners on K worker threads (K << N for processes tracking many queues). Each runner keeps
+// the reference's cadence: its next poll is due one poll period after its previous poll
+// finished (sleep-then-work, main.go:41), and a runner never has two polls in flight, so its
+// decisions are exactly those of a dedicated thread. If more polls are due than there are
+// workers, a poll starts late -- what an oversleeping time.Sleep would do; the cool-down
+// comparisons read the clock at decision time either way.
+class Scheduler {
+ public:
+  explicit Scheduler(size_t threads, std::shared_ptr<Clock> clock = std::make_shared<RealClock>());
+  ~Scheduler();
+  void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
+  // Arms every runner (timers start now, main.go:37-38) and starts the workers; each runner
+  // stops after max_iterations polls (<= 0: until stop()).
+  void start(int64_t max_iterations = -1);
+  void stop();
+  bool stopped() const { return stop_.load(); }
+  bool wait(Nanos timeout);  // true when all workers exited
+  void join();
+  size_t size() const { return runners_.size(); }
+  size_t threads() const { return nthreads_; }
+  std::shared_ptr<Runner> runner(size_t i) const { return runners_.at(i); }
+  // Polls that started later than due (scheduler saturation), and the worst lateness.
+  uint64_t late_polls() const;
+  Nanos max_lateness() const;
+
+ private:
+  struct Item {
+    Nanos due;
+    size_t idx;
+    bool operator>(const Item& o) const { return due != o.due ? due > o.due : idx > o.idx; }
+  };
+  void worker();
+
+  size_t nthreads_;
+  std::shared_ptr<Clock> clock_;
+  std::vector<std::shared_ptr<Runner>> runners_;
+  std::vector<std::thread> threads_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Item> heap_;  // min-heap on due
+  std::vector<int64_t> done_;
+  int64_t max_iter_ = -1;
+  size_t finished_ = 0;  // runners that reached max_iter_
+  size_t running_ = 0;   // live worker threads
+  std::atomic<bool> stop_{false};
+  uint64_t late_ = 0;
+  Nanos max_late_ = 0;
+};
 
 // Percentile (nearest-rank on a sorted copy), p in [0, 100].
 Nanos percentile(std::vector<Nanos> v, double p);

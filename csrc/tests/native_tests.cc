@@ -320,6 +320,74 @@ TEST(supervisor_stop_interrupts_sleep) {
   CHECK_EQ(api->calls(), uint64_t(0));
 }
 
+// 32 queues on 3 workers against the threaded fakes (TSan target for the scheduler heap).
+TEST(scheduler_many_queues_few_threads) {
+  FakeSqsServer sqs;
+  CHECK(sqs.start().ok());
+  FakeKubeServer kube;
+  CHECK(kube.start().ok());
+  auto clock = std::make_shared<RealClock>();
+  auto log = quiet_logger();
+  Credentials cr;
+  cr.access_key_id = "AKID";
+  cr.secret_access_key = "SECRET";
+  auto creds = std::make_shared<StaticCredentialsProvider>(cr);
+  Scheduler sched(3, clock);
+  const int kQueues = 32, kIters = 10;
+  for (int q = 0; q < kQueues; ++q) {
+    std::string url = sqs.url() + "/1/s" + std::to_string(q);
+    sqs.set_attribute_cycle(url, {attrs(150), attrs(0)});
+    kube.add_deployment("ns", "s" + std::to_string(q), 1);
+    SqsHttpOptions so;
+    so.region = "us-east-1";
+    so.endpoint = sqs.url();
+    auto api = std::make_shared<HttpSqsApi>(so, creds, clock);
+    KubeOptions ko;
+    ko.server = kube.url();
+    ko.namespace_ = "ns";
+    auto dep = std::make_shared<KubeRestDeployments>(ko);
+    auto scaler = std::make_shared<PodAutoScaler>(dep, "s" + std::to_string(q), "ns", 8, 1, 1, 1, log, clock);
+    LoopConfig lc;
+    lc.poll_period = kMillisecond;
+    lc.scale_up_cool_down = 0;
+    lc.scale_down_cool_down = 0;
+    lc.prefetch = (q % 2) == 0;
+    sched.add(std::make_shared<Runner>(lc, std::make_shared<SqsClient>(api, url, default_attribute_names()), scaler,
+                                       clock, log));
+  }
+  sched.start(kIters);
+  CHECK(sched.wait(60 * kSecond));
+  sched.join();
+  for (int q = 0; q < kQueues; ++q) {
+    auto st = sched.runner(q)->stats();
+    CHECK_EQ(st.polls, uint64_t(kIters));
+    CHECK_EQ(st.scale_ups + st.scale_downs, uint64_t(kIters));
+  }
+  sqs.stop();
+  kube.stop();
+}
+
+TEST(scheduler_stop) {
+  auto clock = std::make_shared<RealClock>();
+  auto log = quiet_logger();
+  auto api = std::make_shared<MockSqsApi>(attrs(0));
+  auto fake = std::make_shared<FakeDeployments>("ns");
+  fake->add("w", 1);
+  Scheduler sched(2, clock);
+  LoopConfig lc;
+  lc.poll_period = 3600 * kSecond;
+  for (int i = 0; i < 5; ++i)
+    sched.add(std::make_shared<Runner>(lc, std::make_shared<SqsClient>(api, "q", default_attribute_names()),
+                                       std::make_shared<PodAutoScaler>(fake, "w", "ns", 8, 1, 1, 1, log, clock), clock,
+                                       log));
+  sched.start();
+  CHECK(!sched.wait(50 * kMillisecond));
+  sched.stop();
+  CHECK(sched.wait(5 * kSecond));
+  sched.join();
+  CHECK_EQ(api->calls(), uint64_t(0));
+}
+
 TEST(concurrent_logger_lines_are_whole) {
   auto lines = std::make_shared<std::vector<std::string>>();
   auto mu = std::make_shared<std::mutex>();

@@ -94,7 +94,7 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
     from .parallel.fleet import Fleet
 
-    fleet = Fleet(workers)
+    fleet = Fleet(workers, cfg.worker_threads)
     metrics = None
     if cfg.metrics_addr:
         from .metrics import MetricsServer

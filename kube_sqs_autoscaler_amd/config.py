@@ -93,6 +93,7 @@ class Config:
     kube_config_path: str = ""
     pipeline_reads: bool = True
     dry_run: bool = False
+    worker_threads: int = 0
     busy_poll_ns: int = 25_000
     trace_file: str = ""
     leader_elect: bool = False
@@ -141,6 +142,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("sqs-endpoint", "", "Override the SQS endpoint URL (VPC endpoint, local fake); empty uses the regional endpoint")
     fs.string("sqs-protocol", "query", "SQS wire protocol: query (AWS Query/XML) or json (AWS JSON 1.0)")
     fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
+    fs.int("worker-threads", 0, "Threads polling the tracked queues; 0 = one per queue (use fewer for hundreds of queues)")
     fs.bool("dry-run", False, "Shadow mode: poll and decide as usual, log the scaling that would happen, never write")
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
@@ -259,6 +261,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         kube_config_path=env.get("KUBE_CONFIG_PATH", ""),
         pipeline_reads=fs["pipeline-reads"],
         dry_run=fs["dry-run"],
+        worker_threads=fs["worker-threads"],
         busy_poll_ns=fs["busy-poll"],
         trace_file=fs["trace-file"],
         leader_elect=fs["leader-elect"],

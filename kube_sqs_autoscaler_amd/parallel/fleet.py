@@ -19,9 +19,16 @@ from ..ops import native
 
 
 class Fleet:
-    def __init__(self, workers: Sequence) -> None:
+    """``threads`` <= 0 or >= len(workers): one native thread per queue (``Supervisor``);
+    otherwise ``threads`` workers share the queues through the native ``Scheduler`` (a timer
+    heap that keeps every queue's sleep-then-poll cadence), for processes tracking hundreds of
+    queues."""
+
+    def __init__(self, workers: Sequence, threads: int = 0) -> None:
         self.workers = list(workers)
-        self._sup = native().Supervisor()
+        nat = native()
+        self.pooled = 0 < threads < len(self.workers)
+        self._sup = nat.Scheduler(threads) if self.pooled else nat.Supervisor()
         for w in self.workers:
             self._sup.add(w.runner)
         self._started = False
@@ -47,6 +54,10 @@ class Fleet:
 
     def join(self) -> None:
         self._sup.join()
+
+    def late_polls(self) -> int:
+        """Polls a pooled scheduler started >1 ms after they were due (0 for thread-per-queue)."""
+        return self._sup.late_polls() if self.pooled else 0
 
     def stats(self) -> List[dict]:
         out = []

@@ -72,3 +72,60 @@ def test_metrics_endpoints(nat):
             m.stop()
     finally:
         env.close()
+
+
+def test_pooled_scheduler_many_queues_few_threads(nat):
+    """64 queues on 4 native threads: every queue polls, decisions match a dedicated loop."""
+    env = BenchEnv(64)
+    try:
+        cfg = nat.LoopConfig()
+        cfg.poll_period_ns = 2_000_000  # 2 ms between a queue's polls
+        cfg.scale_up_cool_down_ns = 0
+        cfg.scale_down_cool_down_ns = 0
+        runners = [nat.Runner(cfg, r.sqs, r.scaler, nat.RealClock(), env.log) for r in env.runners]
+        fleet = Fleet([W(r, t) for r, t in zip(runners, env.targets)], threads=4)
+        assert fleet.pooled
+        fleet.start(12)
+        assert fleet.wait(60)
+        fleet.join()
+        stats = fleet.stats()
+        assert all(s["polls"] == 12 for s in stats)
+        # 200/0 alternation from the fake: 6 scale-ups then 6 scale-downs interleaved, per queue
+        assert all(s["scale_ups"] == 6 and s["scale_downs"] == 6 for s in stats)
+        assert [env.kube.replicas("bench", t.deployment) for t in env.targets] == [1] * 64
+        assert env.sqs.signature_failures() == 0
+    finally:
+        env.close()
+
+
+def test_pooled_scheduler_keeps_cadence(nat, tmp_path):
+    """A queue's consecutive polls are at least one poll period apart (sleep-then-work)."""
+    import json
+
+    env = BenchEnv(8)
+    try:
+        cfg = nat.LoopConfig()
+        cfg.poll_period_ns = 20_000_000
+        trace = tmp_path / "spans.jsonl"
+        fd = __import__("os").open(str(trace), __import__("os").O_WRONLY | __import__("os").O_CREAT)
+        runners = []
+        for r in env.runners:
+            rr = nat.Runner(cfg, r.sqs, r.scaler, nat.RealClock(), env.log)
+            rr.set_trace_fd(fd)
+            runners.append(rr)
+        fleet = Fleet([W(r, t) for r, t in zip(runners, env.targets)], threads=2)
+        fleet.start(6)
+        fleet.join()
+        __import__("os").close(fd)
+        spans = [json.loads(l) for l in trace.read_text().splitlines()]
+        by_q = {}
+        for s in spans:
+            by_q.setdefault(s["deployment"], []).append(s)
+        assert len(by_q) == 8 and all(len(v) == 6 for v in by_q.values())
+        for v in by_q.values():
+            v.sort(key=lambda s: s["poll"])
+            for a, b in zip(v, v[1:]):
+                # next poll starts >= period after the previous poll ended
+                assert b["ts"] - (a["ts"]) >= 20_000_000 - 1_000_000
+    finally:
+        env.close()
