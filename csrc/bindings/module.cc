@@ -153,6 +153,7 @@ py::dict http_stats_dict(const HttpClientStats& s) {
   py::dict d;
   d["requests"] = s.requests;
   d["connects"] = s.connects;
+  d["tls_resumptions"] = s.tls_resumptions;
   d["reconnect_retries"] = s.reconnect_retries;
   d["bytes_out"] = s.bytes_out;
   d["bytes_in"] = s.bytes_in;

@@ -225,6 +225,7 @@ class Stream {
   }
 
  void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
+  SSL* ssl() const { return ssl_; }
 
  private:
   // Busy-poll: peek the socket for up to spin_ns_ before sleeping in poll(2). A response that
@@ -512,6 +513,7 @@ struct HttpClient::Conn {
   std::unique_ptr<Stream> stream;
   std::string rbuf;
   uint64_t uses = 0;
+  bool session_saved = false;
 };
 
 HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
@@ -542,10 +544,16 @@ HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
     ctx_status_ = use_cert_key(ctx_, tls_.cert_pem, tls_.key_pem);
   // Session resumption makes reconnects after an idle close cheap.
   SSL_CTX_set_session_cache_mode(ctx_, SSL_SESS_CACHE_CLIENT);
+  // Peers (AWS endpoints included) often close idle keep-alive connections without
+  // close_notify; treat that as a plain EOF instead of a protocol error.
+#ifdef SSL_OP_IGNORE_UNEXPECTED_EOF
+  SSL_CTX_set_options(ctx_, SSL_OP_IGNORE_UNEXPECTED_EOF);
+#endif
 }
 
 HttpClient::~HttpClient() {
   conn_.reset();
+  if (session_) SSL_SESSION_free(session_);
   if (ctx_) SSL_CTX_free(ctx_);
 }
 
@@ -609,6 +617,9 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
       if (is_ip_literal(name)) X509_VERIFY_PARAM_set1_ip_asc(param, name.c_str());
       else X509_VERIFY_PARAM_set1_host(param, name.c_str(), 0);
     }
+    // Resume the previous session (abbreviated handshake) when the peer closed an idle
+    // keep-alive connection -- AWS endpoints do after about a minute.
+    if (session_) SSL_set_session(ssl, session_);
   }
   auto stream = std::make_unique<Stream>(fd, ssl);
   if (ssl) {
@@ -620,6 +631,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
                            std::string(X509_verify_cert_error_string(vr)));
       return h;
     }
+    if (SSL_session_reused(ssl)) stats_.tls_resumptions++;
   }
   conn_ = std::make_unique<Conn>();
   conn_->stream = std::move(stream);
@@ -734,6 +746,21 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   {
     const Nanos rtt = mono_ns() - sent_at_;
     ewma_ns_ = ewma_ns_ < 0 ? rtt : (ewma_ns_ * 7 + rtt) / 8;
+  }
+  // TLS 1.3 tickets arrive after the handshake (with the first response): keep the session of
+  // each new connection once, for resumption on the next reconnect.
+  if (!conn_->session_saved && conn_->stream->ssl()) {
+    conn_->session_saved = true;
+    // A private copy: OpenSSL flags the live session non-resumable if this connection later
+    // dies without close_notify, which must not cost us the ticket.
+    SSL_SESSION* live = SSL_get0_session(conn_->stream->ssl());
+    if (live && SSL_SESSION_is_resumable(live)) {
+      SSL_SESSION* copy = SSL_SESSION_dup(live);
+      if (copy) {
+        if (session_) SSL_SESSION_free(session_);
+        session_ = copy;
+      }
+    }
   }
   if (close_after) conn_.reset();
   return Status::OK();

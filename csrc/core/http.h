@@ -25,6 +25,7 @@
 #include "status.h"
 
 typedef struct ssl_ctx_st SSL_CTX;
+typedef struct ssl_session_st SSL_SESSION;
 
 namespace ksa {
 
@@ -67,6 +68,7 @@ struct HttpResponse {
 struct HttpClientStats {
   uint64_t requests = 0;
   uint64_t connects = 0;
+  uint64_t tls_resumptions = 0;  // reconnects that resumed the previous TLS session
   uint64_t reconnect_retries = 0;
   uint64_t bytes_out = 0;
   uint64_t bytes_in = 0;
@@ -121,6 +123,7 @@ class HttpClient {
   mutable std::mutex mu_;
   std::unique_ptr<Conn> conn_;
   HttpClientStats stats_;
+  SSL_SESSION* session_ = nullptr;  // last resumable TLS session
   Nanos spin_ns_ = 0;
   Nanos ewma_ns_ = -1;   // response-time EWMA (-1: no sample yet)
   int64_t sent_at_ = 0;  // mono time the current request finished writing

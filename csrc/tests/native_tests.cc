@@ -222,6 +222,13 @@ TEST(http_tls_roundtrip) {
     CHECK(c.round_trip(req, &resp).ok());
     CHECK_EQ(resp.body, std::string("tls-ok"));
   }
+  srv.drop_connections();  // reconnect must resume the TLS session
+  {
+    HttpRequest req;
+    HttpResponse resp;
+    CHECK(c.round_trip(req, &resp).ok());
+    CHECK_EQ(c.stats().tls_resumptions, uint64_t(1));
+  }
   HttpClient bad(u.value, TlsOptions{}, 5 * kSecond);  // no CA: must fail verification
   HttpRequest req;
   HttpResponse resp;

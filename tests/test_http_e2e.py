@@ -314,3 +314,24 @@ def test_adaptive_busy_poll_tracks_peer_rtt(nat, kube_server):
     for _ in range(60):
         c.request("GET", "/healthz", [("Authorization", f"Bearer {TOKEN}")])
     assert c.rtt_ewma() < 4 * 25_000  # fast local peer again -> spinning re-enabled
+
+
+def test_tls_reconnect_resumes_session(nat):
+    """After the peer closes an idle keep-alive connection, the reconnect resumes the TLS
+    session (abbreviated handshake) instead of a full one."""
+    import time
+
+    k = nat.FakeKubeServer()
+    k.start("127.0.0.1", 0, True)
+    try:
+        t = nat.TlsOptions()
+        t.ca_pem = k.cert_pem
+        c = nat.HttpClient(k.url, t)
+        for _ in range(4):
+            assert c.request("GET", "/x")[0] == 404
+            k.drop_connections()
+            time.sleep(0.02)
+        st = c.stats()
+        assert st["connects"] == 4 and st["tls_resumptions"] == 3
+    finally:
+        k.stop()
