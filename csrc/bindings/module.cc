@@ -688,7 +688,11 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("runner", &Supervisor::runner);
 
   py::class_<Scheduler, std::shared_ptr<Scheduler>>(m, "Scheduler")
-      .def(py::init([](size_t threads) { return std::make_shared<Scheduler>(threads); }), py::arg("threads"))
+      .def(py::init([](size_t threads, bool stagger) {
+             return std::make_shared<Scheduler>(threads, std::make_shared<RealClock>(), stagger);
+           }),
+           py::arg("threads"), py::arg("stagger") = true)
+      .def("reset_lateness", &Scheduler::reset_lateness)
       .def("add", &Scheduler::add)
       .def("start", &Scheduler::start, py::arg("max_iterations") = -1)
       .def("stop", &Scheduler::stop)

@@ -274,8 +274,8 @@ Supervisor::~Supervisor() {
 
 // ---------------------------------------------------------------------------------------
 
-Scheduler::Scheduler(size_t threads, std::shared_ptr<Clock> clock)
-    : nthreads_(threads < 1 ? 1 : threads), clock_(std::move(clock)) {}
+Scheduler::Scheduler(size_t threads, std::shared_ptr<Clock> clock, bool stagger)
+    : nthreads_(threads < 1 ? 1 : threads), clock_(std::move(clock)), stagger_(stagger) {}
 
 Scheduler::~Scheduler() {
   stop();
@@ -287,9 +287,16 @@ void Scheduler::start(int64_t max_iterations) {
   max_iter_ = max_iterations;
   done_.assign(runners_.size(), 0);
   heap_.clear();
-  for (size_t i = 0; i < runners_.size(); ++i) {
-    runners_[i]->arm();
-    heap_.push_back(Item{clock_->now() + std::max<Nanos>(runners_[i]->config().poll_period, 0), i});
+  const Nanos t0 = clock_->now();
+  const size_t n = runners_.size();
+  for (size_t i = 0; i < n; ++i) {
+    const Nanos period = std::max<Nanos>(runners_[i]->config().poll_period, 0);
+    if (stagger_ && n > 1 && period > 0) {
+      heap_.push_back(Item{t0 + static_cast<Nanos>(static_cast<double>(period) * i / n), i, true});
+    } else {
+      runners_[i]->arm();
+      heap_.push_back(Item{t0 + period, i, false});
+    }
   }
   std::make_heap(heap_.begin(), heap_.end(), std::greater<Item>());
   finished_ = 0;
@@ -315,6 +322,13 @@ void Scheduler::worker() {
     }
     std::pop_heap(heap_.begin(), heap_.end(), std::greater<Item>());
     heap_.pop_back();
+    if (top.arm) {  // staggered start: Run() entry for this queue
+      runners_[top.idx]->arm();
+      heap_.push_back(Item{clock_->now() + std::max<Nanos>(runners_[top.idx]->config().poll_period, 0), top.idx, false});
+      std::push_heap(heap_.begin(), heap_.end(), std::greater<Item>());
+      cv_.notify_all();
+      continue;
+    }
     if (now - top.due > kMillisecond) {
       late_++;
       max_late_ = std::max(max_late_, now - top.due);
@@ -365,6 +379,12 @@ uint64_t Scheduler::late_polls() const {
 Nanos Scheduler::max_lateness() const {
   std::lock_guard<std::mutex> lk(mu_);
   return max_late_;
+}
+
+void Scheduler::reset_lateness() {
+  std::lock_guard<std::mutex> lk(mu_);
+  late_ = 0;
+  max_late_ = 0;
 }
 
 Nanos percentile(std::vector<Nanos> v, double p) {

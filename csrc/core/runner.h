@@ -171,7 +171,11 @@ std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std:
 // comparisons read the clock at decision time either way.
 class Scheduler {
  public:
-  explicit Scheduler(size_t threads, std::shared_ptr<Clock> clock = std::make_shared<RealClock>());
+  // stagger: runner i starts (arms its timers, main.go:37-38) at i/N of its poll period instead
+  // of all at once -- as if N reference processes had been launched a little apart -- so the
+  // first polls do not arrive as one burst. Per-queue semantics are unchanged.
+  explicit Scheduler(size_t threads, std::shared_ptr<Clock> clock = std::make_shared<RealClock>(),
+                     bool stagger = true);
   ~Scheduler();
   void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
   // Arms every runner (timers start now, main.go:37-38) and starts the workers; each runner
@@ -187,11 +191,13 @@ class Scheduler {
   // Polls that started later than due (scheduler saturation), and the worst lateness.
   uint64_t late_polls() const;
   Nanos max_lateness() const;
+  void reset_lateness();
 
  private:
   struct Item {
     Nanos due;
     size_t idx;
+    bool arm = false;  // start event: arm the runner, first poll one period later
     bool operator>(const Item& o) const { return due != o.due ? due > o.due : idx > o.idx; }
   };
   void worker();
@@ -210,6 +216,7 @@ class Scheduler {
   std::atomic<bool> stop_{false};
   uint64_t late_ = 0;
   Nanos max_late_ = 0;
+  bool stagger_ = true;
 };
 
 // Percentile (nearest-rank on a sorted copy), p in [0, 100].

@@ -8,6 +8,7 @@ timeout -k 10 300 python -m pytest tests -m gpu -x -q -s > gpurun_out/pytest_gpu
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err &&
 timeout -k 10 300 python bench.py --queues 8 --no-sweep > gpurun_out/bench_q8.json 2> gpurun_out/bench_q8.err &&
+timeout -k 10 300 python -m kube_sqs_autoscaler_amd.bench.capacity > gpurun_out/capacity.jsonl 2> gpurun_out/capacity.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o probe -- python3 scripts/probe_bench.py > gpurun_out/prof_probe.log 2>&1
 rc=$?
 echo "exit $rc"
