@@ -8,6 +8,7 @@
 // (SqsApi, DeploymentApi), so Python fakes plug into the native loop exactly like the
 // reference's Go mocks plug into Run().
 #include <pybind11/functional.h>
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <unistd.h>
@@ -22,6 +23,7 @@
 #include "../core/runner.h"
 #include "../core/sigv4.h"
 #include "../core/sqs.h"
+#include "../core/sweep.h"
 #include "../core/xml.h"
 
 namespace py = pybind11;
@@ -706,6 +708,29 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("max_lateness_ns", &Scheduler::max_lateness);
 
   m.def("percentile", &percentile);
+
+  // ---- what-if policy sweep (CPU path; the gfx950 kernel is in libksa_gpu.so) ----
+  using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+  using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+  m.def("sweep_cpu",
+        [](I64 trace_t, I64 trace_d, int32_t init, int64_t horizon, I64 latency, I64 params, int threads) {
+          if (trace_t.ndim() != 1 || trace_d.ndim() != 1 || trace_t.shape(0) != trace_d.shape(0) || trace_t.shape(0) < 1)
+            throw py::value_error("trace_t / trace_d must be 1-D arrays of equal non-zero length");
+          if (trace_t.at(0) != 0) throw py::value_error("the trace must start at t=0");
+          if (latency.size() != 3) throw py::value_error("latency must be (sqs, get, update) ns");
+          if (params.ndim() != 2 || params.shape(0) != 9) throw py::value_error("params must have shape (9, m)");
+          const int64_t m = params.shape(1);
+          I64 out64({int64_t(3), m});
+          I32 out32({int64_t(7), m});
+          {
+            py::gil_scoped_release rel;
+            sweep_cpu(trace_t.data(), trace_d.data(), static_cast<int32_t>(trace_t.shape(0)), init, horizon,
+                      latency.data(), params.data(), m, out64.mutable_data(), out32.mutable_data(), threads);
+          }
+          return py::make_tuple(out64, out32);
+        },
+        py::arg("trace_t"), py::arg("trace_d"), py::arg("init_replicas"), py::arg("horizon_ns"), py::arg("latency"),
+        py::arg("params"), py::arg("threads") = 8);
 
   // ---- fakes ----
   py::class_<InjectedFault>(m, "InjectedFault")

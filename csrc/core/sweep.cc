@@ -1,0 +1,62 @@
+// CPU path of the what-if policy sweep: the same ksa_sim::simulate the gfx950 kernel runs
+// (csrc/sim/policy_sim.h), over configurations split across std::threads. Used on hosts without
+// a GPU and as the exactness/speed baseline of the kernel.
+#include "sweep.h"
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace ksa {
+
+void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads) {
+  if (m <= 0 || n < 1) return;
+  const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+  auto work = [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      ksa_sim::Params p;
+      p.poll_ns = params[0 * m + i];
+      p.up_cool_ns = params[1 * m + i];
+      p.down_cool_ns = params[2 * m + i];
+      p.up_msgs = params[3 * m + i];
+      p.down_msgs = params[4 * m + i];
+      p.up_pods = params[5 * m + i];
+      p.down_pods = params[6 * m + i];
+      p.max_pods = params[7 * m + i];
+      p.min_pods = params[8 * m + i];
+      const ksa_sim::Result r = ksa_sim::simulate(p, lat, trace_t, trace_d, n, init_replicas, horizon_ns);
+      out64[0 * m + i] = r.pod_ms;
+      out64[1 * m + i] = r.backlog;
+      out64[2 * m + i] = r.first_up_ns;
+      out32[0 * m + i] = r.ups;
+      out32[1 * m + i] = r.downs;
+      out32[2 * m + i] = r.noop_ups;
+      out32[3 * m + i] = r.noop_downs;
+      out32[4 * m + i] = r.final_replicas;
+      out32[5 * m + i] = r.max_replicas;
+      out32[6 * m + i] = r.polls;
+    }
+  };
+  int t = std::max(1, threads);
+  if (t > m) t = static_cast<int>(m);
+  if (t == 1) {
+    work(0, m);
+    return;
+  }
+  // Interleaved chunks balance the (period-dependent) cost across threads.
+  std::vector<std::thread> pool;
+  const int64_t chunk = 256;
+  std::atomic<int64_t> next{0};
+  for (int k = 0; k < t; ++k)
+    pool.emplace_back([&] {
+      for (;;) {
+        const int64_t lo = next.fetch_add(chunk);
+        if (lo >= m) return;
+        work(lo, std::min(m, lo + chunk));
+      }
+    });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace ksa

@@ -1,0 +1,147 @@
+// gfx950 what-if policy sweep: one candidate configuration per lane.
+//
+// Each lane runs ksa_sim::simulate (csrc/sim/policy_sim.h: the reference's decision rules,
+// bit-identical to the CPU path and the Python oracle) over the same queue-depth trace. The
+// work is a branchy integer state machine -- no matrix math, so no MFMA -- and the layout is
+// chosen for that:
+//   * parameters and results are structure-of-arrays ([field][config]), so the 64 lanes of a
+//     wave load and store each field as one contiguous 512-byte (int64) segment;
+//   * the trace (segment start times + depths) is staged once per workgroup into LDS when it fits
+//     (kLdsTraceMax segments = 64 KiB), so the per-poll depth lookups -- every lane walks its own
+//     forward-only cursor -- hit LDS instead of L2;
+//   * the host orders configurations with the poll period outermost, so neighbouring lanes share
+//     trip counts and a wave's lanes retire together (less divergence at the loop exit);
+//   * grid-stride loop over configurations, grid = CUs x 4 workgroups of 256 (>= 1024 workgroups
+//     over the 8 XCDs); every lane's loop is bounded by horizon / max(poll, sqs latency).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "../sim/policy_sim.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kLdsTraceMax = 4096;  // segments staged in LDS (2 x 8 B x 4096 = 64 KiB)
+
+thread_local std::string g_sweep_error;
+
+enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPods, kMaxPods, kMinPods, kNumParams };
+enum : int { kPodMs = 0, kBacklog, kFirstUp, kNumOut64 };
+enum : int { kUps = 0, kDowns, kNoopUps, kNoopDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
+
+__global__ __launch_bounds__(kBlock) void sweep_kernel(const int64_t* __restrict__ params, int64_t m,
+                                                       ksa_sim::Latency lat, const int64_t* __restrict__ g_t,
+                                                       const int64_t* __restrict__ g_d, int32_t n, int32_t init,
+                                                       int64_t horizon, int64_t* __restrict__ out64,
+                                                       int32_t* __restrict__ out32) {
+  __shared__ int64_t s_t[kLdsTraceMax];
+  __shared__ int64_t s_d[kLdsTraceMax];
+  const bool in_lds = n <= kLdsTraceMax;
+  if (in_lds) {
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+      s_t[i] = g_t[i];
+      s_d[i] = g_d[i];
+    }
+    __syncthreads();
+  }
+  const int64_t* t = in_lds ? s_t : g_t;
+  const int64_t* d = in_lds ? s_d : g_d;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += stride) {
+    ksa_sim::Params p;
+    p.poll_ns = params[kPoll * m + i];
+    p.up_cool_ns = params[kUpCool * m + i];
+    p.down_cool_ns = params[kDownCool * m + i];
+    p.up_msgs = params[kUpMsgs * m + i];
+    p.down_msgs = params[kDownMsgs * m + i];
+    p.up_pods = params[kUpPods * m + i];
+    p.down_pods = params[kDownPods * m + i];
+    p.max_pods = params[kMaxPods * m + i];
+    p.min_pods = params[kMinPods * m + i];
+    const ksa_sim::Result r = ksa_sim::simulate(p, lat, t, d, n, init, horizon);
+    out64[kPodMs * m + i] = r.pod_ms;
+    out64[kBacklog * m + i] = r.backlog;
+    out64[kFirstUp * m + i] = r.first_up_ns;
+    out32[kUps * m + i] = r.ups;
+    out32[kDowns * m + i] = r.downs;
+    out32[kNoopUps * m + i] = r.noop_ups;
+    out32[kNoopDowns * m + i] = r.noop_downs;
+    out32[kFinal * m + i] = r.final_replicas;
+    out32[kMaxRep * m + i] = r.max_replicas;
+    out32[kPolls * m + i] = r.polls;
+  }
+}
+
+bool ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  g_sweep_error = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ksa_sweep_last_error() { return g_sweep_error.c_str(); }
+
+// params: [9][m] int64 (poll, up_cool, down_cool, up_msgs, down_msgs, up_pods, down_pods, max, min)
+// out64:  [3][m] int64 (pod_ms, backlog, first_up_ns); out32: [7][m] int32 (ups, downs, noop_ups,
+// noop_downs, final, max_replicas, polls). latency: {sqs, get, update} ns. Returns 0 on success.
+int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas,
+                  int64_t horizon_ns, const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64,
+                  int32_t* out32, double* kernel_ms) {
+  if (n < 1 || trace_t[0] != 0) {
+    g_sweep_error = "trace must have at least one segment starting at t=0";
+    return -1;
+  }
+  if (m <= 0) return 0;
+  if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
+  hipDeviceProp_t prop;
+  if (!ok(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties")) return -1;
+  int64_t *d_t = nullptr, *d_d = nullptr, *d_p = nullptr, *d_o64 = nullptr;
+  int32_t* d_o32 = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = -1;
+  do {
+    if (!ok(hipMalloc(&d_t, n * sizeof(int64_t)), "hipMalloc") || !ok(hipMalloc(&d_d, n * sizeof(int64_t)), "hipMalloc") ||
+        !ok(hipMalloc(&d_p, kNumParams * m * sizeof(int64_t)), "hipMalloc") ||
+        !ok(hipMalloc(&d_o64, kNumOut64 * m * sizeof(int64_t)), "hipMalloc") ||
+        !ok(hipMalloc(&d_o32, kNumOut32 * m * sizeof(int32_t)), "hipMalloc"))
+      break;
+    if (!ok(hipMemcpy(d_t, trace_t, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
+        !ok(hipMemcpy(d_d, trace_d, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
+        !ok(hipMemcpy(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy"))
+      break;
+    if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
+    const int64_t want = (m + kBlock - 1) / kBlock;
+    const int64_t cap = static_cast<int64_t>(prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256) * 4;
+    const int grid = static_cast<int>(want < cap ? want : cap);
+    const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+    hipEventRecord(e0, nullptr);
+    hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), 0, nullptr, d_p, m, lat, d_t, d_d, n, init_replicas,
+                       horizon_ns, d_o64, d_o32);
+    if (!ok(hipGetLastError(), "sweep_kernel launch")) break;
+    hipEventRecord(e1, nullptr);
+    if (!ok(hipEventSynchronize(e1), "hipEventSynchronize")) break;
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (kernel_ms) *kernel_ms = ms;
+    if (!ok(hipMemcpy(out64, d_o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy") ||
+        !ok(hipMemcpy(out32, d_o32, kNumOut32 * m * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
+      break;
+    rc = 0;
+  } while (false);
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipFree(d_t);
+  hipFree(d_d);
+  hipFree(d_p);
+  hipFree(d_o64);
+  hipFree(d_o32);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+// Reference-semantics policy simulation for what-if sweeps (extension: tuning tool).
+//
+// One call simulates one candidate configuration of the reference's loop
+// (/root/reference/main.go:35-78, /root/reference/scale/scale.go:54-107 -- the rules of
+// SURVEY.md §3.3, identical to kube_sqs_autoscaler_amd/models/oracle.py) over a recorded or
+// synthetic queue-depth trace, on a virtual clock with a constant per-call latency model, up to a
+// time horizon. It is written once and compiled twice: into the gfx950 sweep kernel
+// (csrc/hip/policy_sweep.hip, one configuration per lane) and into the multithreaded CPU path
+// (csrc/core/sweep.cc). All arithmetic is integer, so both paths and the Python oracle agree
+// exactly.
+//
+// Metrics, accumulated as a left Riemann sum between successive polls (and from t=0 to the first
+// poll, and from the last poll to the horizon):
+//   pod_ms      = sum(replicas * dt_ms)                 -- cost (pod-milliseconds)
+//   backlog     = sum(depth * dt_ms / max(replicas, 1)) -- queue pressure per pod (msg-ms/pod)
+// where depth/replicas are the values observed/set at the left poll (the trace's depth at t=0 and
+// the initial replicas before the first poll).
+#pragma once
+
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define KSA_HD __host__ __device__ __forceinline__
+#else
+#define KSA_HD inline
+#endif
+
+namespace ksa_sim {
+
+// Hard per-configuration bound on simulated polls, so every GPU lane reaches its exit even for
+// a degenerate request (the host also refuses sweeps whose estimated work exceeds a budget).
+constexpr int32_t kMaxPolls = 1 << 26;
+
+struct Params {
+  int64_t poll_ns, up_cool_ns, down_cool_ns;
+  int64_t up_msgs, down_msgs;
+  int64_t up_pods, down_pods, max_pods, min_pods;  // as given on the command line (Go int)
+};
+
+struct Latency {
+  int64_t sqs_ns, get_ns, update_ns;
+};
+
+struct Result {
+  int64_t pod_ms = 0;
+  int64_t backlog = 0;
+  int32_t ups = 0, downs = 0, noop_ups = 0, noop_downs = 0;
+  int32_t final_replicas = 0, max_replicas = 0;
+  int64_t first_up_ns = -1;
+  int32_t polls = 0;
+};
+
+KSA_HD int32_t go_i32(int64_t v) { return static_cast<int32_t>(static_cast<uint32_t>(static_cast<uint64_t>(v))); }
+KSA_HD int32_t add_i32(int32_t a, int32_t b) { return static_cast<int32_t>(static_cast<uint32_t>(a) + static_cast<uint32_t>(b)); }
+KSA_HD int32_t sub_i32(int32_t a, int32_t b) { return static_cast<int32_t>(static_cast<uint32_t>(a) - static_cast<uint32_t>(b)); }
+
+// Trace: n segments, segment i covers [t_ns[i], t_ns[i+1]) with depth[i]; t_ns[0] must be 0.
+KSA_HD int64_t depth_at(const int64_t* t_ns, const int64_t* depth, int32_t n, int32_t* cursor, int64_t t) {
+  int32_t c = *cursor;
+  while (c + 1 < n && t_ns[c + 1] <= t) ++c;  // times only move forward
+  *cursor = c;
+  return depth[c];
+}
+
+KSA_HD void accumulate(Result* r, int64_t dt_ns, int32_t replicas, int64_t depth) {
+  const int64_t dt_ms = dt_ns / 1000000;
+  r->pod_ms += static_cast<int64_t>(replicas) * dt_ms;
+  const int64_t div = replicas > 0 ? replicas : 1;
+  r->backlog += depth * dt_ms / div;
+}
+
+KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns, const int64_t* depth, int32_t n,
+                       int32_t init_replicas, int64_t horizon_ns) {
+  Result res;
+  int32_t cursor = 0;
+  int64_t now = 0;
+  int64_t last_up = 0, last_down = 0;  // main.go:37-38
+  int32_t replicas = init_replicas;
+  const int32_t max32 = go_i32(p.max_pods), min32 = go_i32(p.min_pods);
+  const int32_t up32 = go_i32(p.up_pods), down32 = go_i32(p.down_pods);
+  const int64_t period = p.poll_ns > 0 ? p.poll_ns : 0;
+  int64_t prev_t = 0;
+  int32_t prev_r = replicas;
+  int64_t prev_d = depth_at(t_ns, depth, n, &cursor, 0);
+  res.max_replicas = replicas;
+  // Guard: a zero period with zero latency would never advance time.
+  const bool advances = period > 0 || lat.sqs_ns > 0;
+  while (advances && res.polls < kMaxPolls) {
+    const int64_t t_poll = now + period;  // main.go:41 sleep, then poll
+    if (t_poll > horizon_ns) break;
+    now = t_poll;
+    accumulate(&res, now - prev_t, prev_r, prev_d);
+    prev_t = now;
+    res.polls++;
+    const int64_t d = depth_at(t_ns, depth, n, &cursor, now);  // sampled at call start
+    now += lat.sqs_ns;
+    bool cont = false;
+    if (d >= p.up_msgs) {  // main.go:51
+      if (last_up + p.up_cool_ns > now) {  // main.go:52 (strict After)
+        cont = true;
+      } else {
+        now += lat.get_ns;
+        if (replicas >= max32) {  // scale.go:62
+          res.noop_ups++;
+        } else {
+          int32_t next = add_i32(replicas, up32);
+          if (next > max32) next = max32;
+          now += lat.update_ns;
+          replicas = next;
+          res.ups++;
+          if (res.first_up_ns < 0) res.first_up_ns = t_poll;
+        }
+        last_up = now;  // main.go:62 (also after a no-op)
+      }
+    }
+    if (!cont && d <= p.down_msgs) {  // main.go:65
+      if (!(last_down + p.down_cool_ns > now)) {
+        now += lat.get_ns;
+        if (replicas <= min32) {  // scale.go:89
+          res.noop_downs++;
+        } else {
+          int32_t next = sub_i32(replicas, down32);
+          if (next < min32) next = min32;
+          now += lat.update_ns;
+          replicas = next;
+          res.downs++;
+        }
+        last_down = now;  // main.go:76
+      }
+    }
+    if (replicas > res.max_replicas) res.max_replicas = replicas;
+    prev_r = replicas;
+    prev_d = d;
+  }
+  if (horizon_ns > prev_t) accumulate(&res, horizon_ns - prev_t, prev_r, prev_d);
+  res.final_replicas = replicas;
+  return res;
+}
+
+}  // namespace ksa_sim

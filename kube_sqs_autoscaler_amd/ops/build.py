@@ -45,7 +45,7 @@ def _core_sources() -> list[Path]:
 
 
 def _newest_header() -> float:
-    hs = list(CSRC.rglob("*.h"))
+    hs = list(CSRC.rglob("*.h"))  # includes csrc/sim/policy_sim.h
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
@@ -101,14 +101,16 @@ def build_native(jobs: int = 8, verbose: bool = True) -> Path:
 
 
 def build_gpu_probe(verbose: bool = True) -> Path | None:
-    """Compiles the HIP probe for gfx950 (cross-compiles without a GPU)."""
-    src = CSRC / "hip" / "gpu_probe.hip"
+    """Compiles the gfx950 kernels -- HBM probe + what-if policy sweep -- into one .so
+    (cross-compiles without a GPU)."""
+    srcs = [CSRC / "hip" / "gpu_probe.hip", CSRC / "hip" / "policy_sweep.hip"]
+    deps = srcs + [CSRC / "sim" / "policy_sim.h"]
     if not Path(HIPCC).exists() and shutil.which("hipcc") is None:
-        raise RuntimeError("hipcc not found; cannot build the gfx950 GPU probe")
+        raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")
     hipcc = HIPCC if Path(HIPCC).exists() else "hipcc"
-    if _stale(GPU_SO, [src], 0.0):
+    if _stale(GPU_SO, deps, 0.0):
         tmp = GPU_SO.with_suffix(".tmp.so")
-        _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", str(src), "-o", str(tmp)])
+        _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", *map(str, srcs), "-o", str(tmp)])
         os.replace(tmp, GPU_SO)
         if verbose:
             print(f"[build] hipcc --offload-arch={GPU_ARCH} -> {GPU_SO.relative_to(ROOT)}")

@@ -1,0 +1,123 @@
+"""``python -m kube_sqs_autoscaler_amd.tune``: rank autoscaler settings against a queue trace.
+
+Example -- replay a day of recorded polls, sweep cool-downs and thresholds, keep configurations
+whose queue pressure stays under a bound, and rank them by pod cost::
+
+    python -m kube_sqs_autoscaler_amd.tune --trace spans.jsonl --horizon 24h \\
+        --grid scale-up-cool-down=0s:10m:10s --grid scale-down-cool-down=30s:30m:30s \\
+        --grid scale-up-messages=50,100,200,400 --grid max-pods=8 \\
+        --max-backlog 5e9 --objective pod_ms --top 10
+
+Grid keys are the autoscaler's own flag names; values use its syntax (Go durations, base-0 ints),
+as comma lists or ``start:stop:step`` ranges (stop inclusive). The sweep runs on the MI355X
+(``--device gpu``) or on CPU threads; both give identical numbers.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from typing import Dict, List
+
+import numpy as np
+
+from ..utils.goflag import parse_duration, parse_int
+from . import sweep
+
+FLAG_TO_FIELD = {
+    "poll-period": ("poll_ns", parse_duration),
+    "scale-up-cool-down": ("up_cool_ns", parse_duration),
+    "scale-down-cool-down": ("down_cool_ns", parse_duration),
+    "scale-up-messages": ("up_msgs", parse_int),
+    "scale-down-messages": ("down_msgs", parse_int),
+    "scale-up-pods": ("up_pods", parse_int),
+    "scale-down-pods": ("down_pods", parse_int),
+    "max-pods": ("max_pods", parse_int),
+    "min-pods": ("min_pods", parse_int),
+}
+
+
+def parse_values(spec: str, conv) -> List[int]:
+    out: List[int] = []
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if ":" in part:
+            a, b, c = (conv(x) for x in part.split(":"))
+            if c <= 0:
+                raise ValueError(f"range step must be positive: {part}")
+            out.extend(range(a, b + 1, c))
+        else:
+            out.append(conv(part))
+    if not out:
+        raise ValueError(f"no values in {spec!r}")
+    return out
+
+
+def parse_grid(items: List[str]) -> Dict[str, List[int]]:
+    g: Dict[str, List[int]] = {}
+    for item in items:
+        key, _, spec = item.partition("=")
+        if key not in FLAG_TO_FIELD:
+            raise ValueError(f"unknown grid key {key!r}; expected one of {sorted(FLAG_TO_FIELD)}")
+        field, conv = FLAG_TO_FIELD[key]
+        g[field] = parse_values(spec, conv)
+    return g
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m kube_sqs_autoscaler_amd.tune", description=__doc__.splitlines()[0])
+    ap.add_argument("--trace", required=True, help="--trace-file span log (.jsonl) or seconds,depth CSV")
+    ap.add_argument("--queue", default=None, help="queue URL or ns/deployment to select from a multi-queue span log")
+    ap.add_argument("--horizon", default="", help="simulated time (Go duration); default: trace length + 1 poll period")
+    ap.add_argument("--init-replicas", type=int, default=1)
+    ap.add_argument("--latency", default="1ms,1ms,1ms", help="SQS, GET, write latency (Go durations)")
+    ap.add_argument("--grid", action="append", default=[], help="flag=values (repeatable)")
+    ap.add_argument("--objective", default="pod_ms", choices=["pod_ms", "backlog", "ups", "downs"])
+    ap.add_argument("--max-backlog", type=float, default=None, help="keep configs with backlog <= this")
+    ap.add_argument("--top", type=int, default=10)
+    ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
+    ap.add_argument("--json", action="store_true", help="print JSON lines instead of a table")
+    a = ap.parse_args(argv)
+
+    tr = sweep.Trace.from_spans(a.trace, a.queue) if a.trace.endswith((".jsonl", ".json")) else sweep.Trace.from_csv(a.trace)
+    lat = tuple(parse_duration(x) for x in a.latency.split(","))
+    if len(lat) != 3:
+        ap.error("--latency needs three durations")
+    values = parse_grid(a.grid)
+    params = sweep.grid(**values)
+    horizon = parse_duration(a.horizon) if a.horizon else int(tr.t_ns[-1]) + int(params[0].max())
+    t0 = time.perf_counter()
+    res = sweep.run(tr, params, a.init_replicas, horizon, lat, a.device)
+    wall = time.perf_counter() - t0
+    ok = np.ones(len(res), dtype=bool)
+    if a.max_backlog is not None:
+        ok &= res.out["backlog"] <= a.max_backlog
+    idx = np.flatnonzero(ok)
+    order = idx[np.argsort(res.out[a.objective][idx], kind="stable")][: a.top]
+    baseline = sweep.run(tr, sweep.grid(), a.init_replicas, horizon, lat, "cpu").row(0)
+    summary = {"configs": len(res), "feasible": int(ok.sum()), "device": res.device, "wall_s": round(wall, 4),
+               "kernel_ms": round(res.kernel_ms, 3), "simulated_polls": int(res.out["polls"].sum()),
+               "horizon_ns": horizon, "reference_defaults": baseline}
+    if a.json:
+        print(json.dumps(summary))
+        for i in order:
+            print(json.dumps(res.row(int(i))))
+        return 0
+    print(f"{len(res)} configs ({int(ok.sum())} feasible) on {res.device} in {wall:.3f} s, "
+          f"{summary['simulated_polls']:.3g} polls simulated")
+    print(f"reference defaults: pod_ms={baseline['pod_ms']} backlog={baseline['backlog']} "
+          f"ups={baseline['ups']} downs={baseline['downs']}")
+    cols = ["poll_ns", "up_cool_ns", "down_cool_ns", "up_msgs", "down_msgs", "up_pods", "down_pods", "max_pods",
+            "min_pods", "pod_ms", "backlog", "ups", "downs", "max_replicas"]
+    print("\t".join(cols))
+    for i in order:
+        r = res.row(int(i))
+        print("\t".join(str(r[c]) for c in cols))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

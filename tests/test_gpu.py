@@ -68,3 +68,40 @@ def test_cli_gpu_aware_max_local(tmp_path, capfd):
     finally:
         sqs.stop()
         kube.stop()
+
+
+def _random_walk_trace(n, seed):
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    rng = np.random.default_rng(seed)
+    t = np.concatenate([[0], np.cumsum(rng.integers(1, 20, n - 1)) * 1_000_000_000])
+    d = np.maximum(0, np.cumsum(rng.integers(-40, 41, n)) + 100)
+    return sweep.Trace(t, d)
+
+
+def test_sweep_kernel_equals_cpu_and_oracle():
+    """gfx950 sweep kernel: bit-identical to the CPU path on a 30k-config grid (trace in LDS and
+    trace in global memory), and to the Python oracle on a sample."""
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    S = 1_000_000_000
+    grid = sweep.grid(poll_ns=[2 * S, 5 * S], up_cool_ns=list(range(0, 300 * S, 20 * S)),
+                      down_cool_ns=list(range(0, 600 * S, 60 * S)), up_msgs=[50, 100, 200, 400, 800],
+                      down_msgs=[5, 50], up_pods=[1, 2], max_pods=[8, 16], min_pods=[1])
+    assert grid.shape[1] == 2 * 15 * 10 * 5 * 2 * 2 * 2
+    for n in (1000, 6000):  # <= 4096 segments are staged in LDS, more are read from global memory
+        tr = _random_walk_trace(n, n)
+        horizon = int(tr.t_ns[-1]) + 5 * S
+        g = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="gpu")
+        c = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="cpu")
+        assert g.device == "gpu" and g.kernel_ms > 0
+        for k in g.out:
+            assert np.array_equal(g.out[k], c.out[k]), k
+        assert int(g.out["ups"].sum()) > 0 and int(g.out["downs"].sum()) > 0
+        for i in range(0, len(g), len(g) // 7):
+            o = sweep.oracle_row(tr, g.config(i), 2, horizon, (2_000_000, 1_000_000, 1_000_000))
+            assert {k: g.row(i)[k] for k in o} == o

@@ -1,0 +1,103 @@
+"""What-if policy sweep: the native simulator (CPU path here, gfx950 kernel in test_gpu.py)
+must reproduce the reference-semantics oracle exactly."""
+import json
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from kube_sqs_autoscaler_amd.tune import sweep
+from kube_sqs_autoscaler_amd.tune.__main__ import main as tune_main, parse_values
+from kube_sqs_autoscaler_amd.utils.goflag import SECOND, parse_duration
+
+S = SECOND
+
+
+def step_trace():
+    return sweep.Trace.from_segments([(0, 0), (60 * S, 200), (180 * S, 0), (400 * S, 5000), (500 * S, 3)])
+
+
+def test_grid_shape_and_order():
+    p = sweep.grid(poll_ns=[1 * S, 5 * S], up_msgs=[10, 20, 30])
+    assert p.shape == (9, 6)
+    assert list(p[0]) == [S, S, S, 5 * S, 5 * S, 5 * S]  # poll period outermost
+    assert list(p[3]) == [10, 20, 30, 10, 20, 30]
+    assert (p[7] == 8).all()  # default max-pods
+
+
+def test_reference_defaults_match_appendix_c2():
+    """Defaults on the C2 step trace: 7 ups (60..120 s) then 7 downs -- SURVEY.md Appendix C."""
+    tr = sweep.Trace.from_segments([(0, 0), (60 * S, 200), (180 * S, 0)])
+    r = sweep.run(tr, sweep.grid(), 1, 500 * S, device="cpu").row(0)
+    assert r["ups"] == 7 and r["downs"] == 7 and r["first_up_ns"] // S == 60 and r["final_replicas"] == 1
+
+
+def test_cpu_equals_oracle_on_a_grid():
+    tr = step_trace()
+    p = sweep.grid(poll_ns=[1 * S, 5 * S], up_cool_ns=[0, 10 * S, 300 * S], down_cool_ns=[10 * S, 30 * S],
+                   up_msgs=[50, 300], down_msgs=[3, 10], up_pods=[1, 3], max_pods=[4, 8])
+    res = sweep.run(tr, p, 1, 900 * S, device="cpu")
+    for i in range(len(res)):
+        o = sweep.oracle_row(tr, res.config(i), 1, 900 * S, (10**6, 10**6, 10**6))
+        assert {k: res.row(i)[k] for k in o} == o, res.config(i)
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(
+    segs=st.lists(st.tuples(st.integers(1, 600), st.integers(0, 600)), min_size=0, max_size=8),
+    d0=st.integers(0, 600),
+    poll=st.sampled_from([500_000_000, S, 5 * S, 7 * S]),
+    up_cool=st.sampled_from([0, S, 10 * S, 60 * S]), down_cool=st.sampled_from([0, 5 * S, 30 * S]),
+    up_msgs=st.integers(-5, 400), down_msgs=st.integers(-5, 400), up_pods=st.integers(-2, 5),
+    down_pods=st.integers(-2, 5), max_pods=st.integers(0, 12), min_pods=st.integers(0, 12),
+    init=st.integers(0, 14), lat_ms=st.sampled_from([0, 1, 3]), horizon_s=st.integers(1, 900),
+)
+def test_cpu_equals_oracle_property(segs, d0, poll, up_cool, down_cool, up_msgs, down_msgs, up_pods, down_pods,
+                                    max_pods, min_pods, init, lat_ms, horizon_s):
+    tr = sweep.Trace.from_segments([(0, d0)] + sorted((t * S, d) for t, d in segs))
+    cfg = dict(poll_ns=[poll], up_cool_ns=[up_cool], down_cool_ns=[down_cool], up_msgs=[up_msgs],
+               down_msgs=[down_msgs], up_pods=[up_pods], down_pods=[down_pods], max_pods=[max_pods], min_pods=[min_pods])
+    lat = (lat_ms * 10**6,) * 3
+    res = sweep.run(tr, sweep.grid(**cfg), init, horizon_s * S, lat, device="cpu")
+    o = sweep.oracle_row(tr, res.config(0), init, horizon_s * S, lat)
+    assert {k: res.row(0)[k] for k in o} == o
+
+
+def test_work_budget_guard():
+    with pytest.raises(ValueError, match="sweep too large"):
+        sweep.run(step_trace(), sweep.grid(poll_ns=[1], up_msgs=list(range(5000))), 1, 10**18, (0, 0, 0), device="cpu")
+    with pytest.raises(ValueError, match="zero poll period"):
+        sweep.run(step_trace(), sweep.grid(poll_ns=[0]), 1, 10 * S, (0, 0, 0), device="cpu")
+
+
+def test_trace_loaders(tmp_path):
+    spans = tmp_path / "s.jsonl"
+    spans.write_text("\n".join(json.dumps({"ts": 10**12 + i * 5 * S, "depth": d, "queue": "q", "deployment": "ns/d"})
+                               for i, d in enumerate([0, 0, 200, 200, 0])) + "\n")
+    tr = sweep.Trace.from_spans(str(spans))
+    assert list(tr.t_ns) == [0, 5 * S, 10 * S, 15 * S, 20 * S] and list(tr.depth) == [0, 0, 200, 200, 0]
+    csv = tmp_path / "t.csv"
+    csv.write_text("seconds,depth\n100,5\n160,50\n")
+    tr = sweep.Trace.from_csv(str(csv))
+    assert list(tr.t_ns) == [0, 60 * S] and list(tr.depth) == [5, 50]
+
+
+def test_parse_values():
+    assert parse_values("10s:30s:10s", parse_duration) == [10 * S, 20 * S, 30 * S]
+    from kube_sqs_autoscaler_amd.utils.goflag import parse_int
+
+    assert parse_values("1,0x10", parse_int) == [1, 16]
+
+
+def test_tune_cli(tmp_path, capsys):
+    csv = tmp_path / "t.csv"
+    csv.write_text("0,0\n60,200\n180,0\n400,5000\n500,3\n")
+    rc = tune_main(["--trace", str(csv), "--horizon", "15m", "--grid", "scale-up-cool-down=0s:60s:10s",
+                    "--grid", "scale-up-messages=50,100,300", "--grid", "max-pods=4,8", "--objective", "pod_ms",
+                    "--top", "3", "--device", "cpu", "--json"])
+    assert rc == 0
+    lines = [json.loads(l) for l in capsys.readouterr().out.splitlines()]
+    assert lines[0]["configs"] == 7 * 3 * 2 and lines[0]["reference_defaults"]["ups"] > 0
+    pods = [l["pod_ms"] for l in lines[1:]]
+    assert len(pods) == 3 and pods == sorted(pods)
