@@ -6,13 +6,17 @@
 // chosen for that:
 //   * parameters and results are structure-of-arrays ([field][config]), so the 64 lanes of a
 //     wave load and store each field as one contiguous 512-byte (int64) segment;
-//   * the trace (segment start times + depths) is staged once per workgroup into LDS when it fits
-//     (kLdsTraceMax segments = 64 KiB), so the per-poll depth lookups -- every lane walks its own
-//     forward-only cursor -- hit LDS instead of L2;
+//   * the trace (segment start times + depths) is staged once per workgroup into dynamically
+//     sized LDS when it fits (kLdsTraceMax segments = 32 KiB), so the per-poll depth lookups --
+//     every lane walks its own forward-only cursor -- hit LDS; longer traces are read from
+//     global memory (lanes advance through it nearly in lockstep, so L1/L2 serve them) and then
+//     no LDS is allocated at all, leaving occupancy to the VGPR budget;
+//   * no 64-bit integer division per poll (the backlog metric divides once per replica run);
 //   * the host orders configurations with the poll period outermost, so neighbouring lanes share
 //     trip counts and a wave's lanes retire together (less divergence at the loop exit);
-//   * grid-stride loop over configurations, grid = CUs x 4 workgroups of 256 (>= 1024 workgroups
-//     over the 8 XCDs); every lane's loop is bounded by horizon / max(poll, sqs latency).
+//   * grid-stride loop over configurations, grid = CUs x 8 workgroups of 256 (what 58 VGPRs
+//     keep resident: 8 waves/SIMD; 2048 workgroups over the 8 XCDs); every lane's loop is bounded
+//     by horizon / max(poll, sqs latency) and ksa_sim::kMaxPolls.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -24,7 +28,7 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kLdsTraceMax = 4096;  // segments staged in LDS (2 x 8 B x 4096 = 64 KiB)
+constexpr int kLdsTraceMax = 2048;  // segments staged in LDS (2 x 8 B x 2048 = 32 KiB -> 5 WG/CU)
 
 thread_local std::string g_sweep_error;
 
@@ -37,8 +41,11 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(const int64_t* __restrict
                                                        const int64_t* __restrict__ g_d, int32_t n, int32_t init,
                                                        int64_t horizon, int64_t* __restrict__ out64,
                                                        int32_t* __restrict__ out32) {
-  __shared__ int64_t s_t[kLdsTraceMax];
-  __shared__ int64_t s_d[kLdsTraceMax];
+  // Dynamic LDS: 16 B per segment when the trace is staged, none otherwise -- a static
+  // allocation would cap occupancy even for traces that are read from global memory.
+  extern __shared__ int64_t s_lds[];
+  int64_t* s_t = s_lds;
+  int64_t* s_d = s_lds + (n <= kLdsTraceMax ? n : 0);
   const bool in_lds = n <= kLdsTraceMax;
   if (in_lds) {
     for (int i = threadIdx.x; i < n; i += kBlock) {
@@ -117,11 +124,13 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
       break;
     if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
     const int64_t want = (m + kBlock - 1) / kBlock;
-    const int64_t cap = static_cast<int64_t>(prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256) * 4;
+    // 58 VGPRs -> 8 waves/SIMD: 8 resident 256-thread workgroups per CU
+    const int64_t cap = static_cast<int64_t>(prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256) * 8;
     const int grid = static_cast<int>(want < cap ? want : cap);
     const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
     hipEventRecord(e0, nullptr);
-    hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), 0, nullptr, d_p, m, lat, d_t, d_d, n, init_replicas,
+    const size_t lds = n <= kLdsTraceMax ? 2 * static_cast<size_t>(n) * sizeof(int64_t) : 0;
+    hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), lds, nullptr, d_p, m, lat, d_t, d_d, n, init_replicas,
                        horizon_ns, d_o64, d_o32);
     if (!ok(hipGetLastError(), "sweep_kernel launch")) break;
     hipEventRecord(e1, nullptr);

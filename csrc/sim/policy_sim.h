@@ -11,10 +11,12 @@
 //
 // Metrics, accumulated as a left Riemann sum between successive polls (and from t=0 to the first
 // poll, and from the last poll to the horizon):
-//   pod_ms      = sum(replicas * dt_ms)                 -- cost (pod-milliseconds)
-//   backlog     = sum(depth * dt_ms / max(replicas, 1)) -- queue pressure per pod (msg-ms/pod)
+//   pod_ms   = sum(replicas * dt_ms)                          -- cost (pod-milliseconds)
+//   backlog  = sum over runs of constant replicas r of
+//              floor(sum(depth * dt_ms) / max(r, 1))          -- queue pressure per pod (msg-ms/pod)
 // where depth/replicas are the values observed/set at the left poll (the trace's depth at t=0 and
-// the initial replicas before the first poll).
+// the initial replicas before the first poll). Dividing once per run instead of once per poll
+// keeps a 64-bit integer division (a long expansion on the GPU) out of the per-poll path.
 #pragma once
 
 #include <cstdint>
@@ -62,16 +64,32 @@ KSA_HD int64_t depth_at(const int64_t* t_ns, const int64_t* depth, int32_t n, in
   return depth[c];
 }
 
-KSA_HD void accumulate(Result* r, int64_t dt_ns, int32_t replicas, int64_t depth) {
+struct Accum {
+  int64_t run = 0;      // sum(depth * dt_ms) over the current run of constant replicas
+  int32_t run_r = 0;    // replicas of the current run
+};
+
+KSA_HD void flush(Result* r, Accum* a) {
+  const int64_t div = a->run_r > 0 ? a->run_r : 1;
+  r->backlog += a->run / div;
+  a->run = 0;
+}
+
+KSA_HD void accumulate(Result* r, Accum* a, int64_t dt_ns, int32_t replicas, int64_t depth) {
   const int64_t dt_ms = dt_ns / 1000000;
   r->pod_ms += static_cast<int64_t>(replicas) * dt_ms;
-  const int64_t div = replicas > 0 ? replicas : 1;
-  r->backlog += depth * dt_ms / div;
+  if (replicas != a->run_r) {
+    flush(r, a);
+    a->run_r = replicas;
+  }
+  a->run += depth * dt_ms;
 }
 
 KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns, const int64_t* depth, int32_t n,
                        int32_t init_replicas, int64_t horizon_ns) {
   Result res;
+  Accum acc;
+  acc.run_r = init_replicas;
   int32_t cursor = 0;
   int64_t now = 0;
   int64_t last_up = 0, last_down = 0;  // main.go:37-38
@@ -89,7 +107,7 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
     const int64_t t_poll = now + period;  // main.go:41 sleep, then poll
     if (t_poll > horizon_ns) break;
     now = t_poll;
-    accumulate(&res, now - prev_t, prev_r, prev_d);
+    accumulate(&res, &acc, now - prev_t, prev_r, prev_d);
     prev_t = now;
     res.polls++;
     const int64_t d = depth_at(t_ns, depth, n, &cursor, now);  // sampled at call start
@@ -132,7 +150,8 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
     prev_r = replicas;
     prev_d = d;
   }
-  if (horizon_ns > prev_t) accumulate(&res, horizon_ns - prev_t, prev_r, prev_d);
+  if (horizon_ns > prev_t) accumulate(&res, &acc, horizon_ns - prev_t, prev_r, prev_d);
+  flush(&res, &acc);
   res.final_replicas = replicas;
   return res;
 }

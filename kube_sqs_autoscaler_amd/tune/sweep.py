@@ -16,7 +16,8 @@ Inputs:
 
 Outputs per configuration:
 
-* ``pod_ms`` (cost), ``backlog`` (msg-ms per pod, queue pressure);
+* ``pod_ms`` (cost), ``backlog`` (msg-ms per pod, queue pressure; one integer division per run
+  of constant replicas, see csrc/sim/policy_sim.h);
 * scale-up/down counts and no-ops;
 * final and peak replicas, first scale-up time, poll count.
 """
@@ -216,12 +217,20 @@ def oracle_row(trace: Trace, cfg: Dict[str, int], init_replicas: int, horizon_ns
     r = {"pod_ms": 0, "backlog": 0, "first_up_ns": -1, "ups": 0, "downs": 0, "noop_ups": 0, "noop_downs": 0}
     prev_t, prev_r, prev_d = 0, oracle.int32(init_replicas), int(trace.depth[0])
     peak = prev_r
+    run = {"sum": 0, "r": prev_r}
+
+    def flush():
+        x, y = run["sum"], max(run["r"], 1)
+        r["backlog"] += x // y if x >= 0 else -((-x) // y)  # C++ integer division truncates
+        run["sum"] = 0
 
     def acc(dt_ns, reps, d):
         dt_ms = dt_ns // 1_000_000
         r["pod_ms"] += reps * dt_ms
-        x, y = d * dt_ms, max(reps, 1)
-        r["backlog"] += x // y if x >= 0 else -((-x) // y)  # C++ integer division truncates
+        if reps != run["r"]:
+            flush()
+            run["r"] = reps
+        run["sum"] += d * dt_ms
 
     for e in ev:
         acc(e.t_poll_ns - prev_t, prev_r, prev_d)
@@ -235,5 +244,6 @@ def oracle_row(trace: Trace, cfg: Dict[str, int], init_replicas: int, horizon_ns
         peak = max(peak, e.replicas)
     if horizon_ns > prev_t:
         acc(horizon_ns - prev_t, prev_r, prev_d)
+    flush()
     r.update(final_replicas=prev_r, max_replicas=peak, polls=len(ev))
     return r

@@ -93,7 +93,7 @@ def test_sweep_kernel_equals_cpu_and_oracle():
                       down_cool_ns=list(range(0, 600 * S, 60 * S)), up_msgs=[50, 100, 200, 400, 800],
                       down_msgs=[5, 50], up_pods=[1, 2], max_pods=[8, 16], min_pods=[1])
     assert grid.shape[1] == 2 * 15 * 10 * 5 * 2 * 2 * 2
-    for n in (1000, 6000):  # <= 4096 segments are staged in LDS, more are read from global memory
+    for n in (1000, 6000):  # <= 2048 segments are staged in LDS, more are read from global memory
         tr = _random_walk_trace(n, n)
         horizon = int(tr.t_ns[-1]) + 5 * S
         g = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="gpu")
