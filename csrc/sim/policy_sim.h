@@ -20,6 +20,7 @@
 #pragma once
 
 #include <cstdint>
+#include <climits>
 
 #if defined(__HIPCC__)
 #define KSA_HD __host__ __device__ __forceinline__
@@ -57,11 +58,37 @@ KSA_HD int32_t add_i32(int32_t a, int32_t b) { return static_cast<int32_t>(stati
 KSA_HD int32_t sub_i32(int32_t a, int32_t b) { return static_cast<int32_t>(static_cast<uint32_t>(a) - static_cast<uint32_t>(b)); }
 
 // Trace: n segments, segment i covers [t_ns[i], t_ns[i+1]) with depth[i]; t_ns[0] must be 0.
-KSA_HD int64_t depth_at(const int64_t* t_ns, const int64_t* depth, int32_t n, int32_t* cursor, int64_t t) {
-  int32_t c = *cursor;
-  while (c + 1 < n && t_ns[c + 1] <= t) ++c;  // times only move forward
-  *cursor = c;
-  return depth[c];
+// Forward-only cursor with the next boundary and depth held in registers: advancing issues the
+// loads for the segment after next right away, so on the GPU their latency overlaps the rest of
+// the poll instead of stalling the next lookup (lookups are one per poll and times only grow).
+struct Cursor {
+  int32_t c;
+  int64_t cur_d, next_t, next_d;
+};
+
+constexpr int64_t kNever = INT64_MAX;
+
+KSA_HD Cursor cursor_init(const int64_t* t_ns, const int64_t* depth, int32_t n) {
+  Cursor k;
+  k.c = 0;
+  k.cur_d = depth[0];
+  k.next_t = n > 1 ? t_ns[1] : kNever;
+  k.next_d = n > 1 ? depth[1] : 0;
+  return k;
+}
+
+KSA_HD int64_t depth_at(const int64_t* t_ns, const int64_t* depth, int32_t n, Cursor* k, int64_t t) {
+  while (t >= k->next_t) {
+    k->c++;
+    k->cur_d = k->next_d;
+    if (k->c + 1 < n) {
+      k->next_t = t_ns[k->c + 1];
+      k->next_d = depth[k->c + 1];
+    } else {
+      k->next_t = kNever;
+    }
+  }
+  return k->cur_d;
 }
 
 struct Accum {
@@ -90,7 +117,7 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
   Result res;
   Accum acc;
   acc.run_r = init_replicas;
-  int32_t cursor = 0;
+  Cursor cursor = cursor_init(t_ns, depth, n);
   int64_t now = 0;
   int64_t last_up = 0, last_down = 0;  // main.go:37-38
   int32_t replicas = init_replicas;
