@@ -78,6 +78,7 @@ def main(argv=None) -> int:
     ap.add_argument("--objective", default="pod_ms", choices=["pod_ms", "backlog", "ups", "downs"])
     ap.add_argument("--max-backlog", type=float, default=None, help="keep configs with backlog <= this")
     ap.add_argument("--top", type=int, default=10)
+    ap.add_argument("--pareto", action="store_true", help="list the cost/pressure Pareto front instead of a ranking")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--json", action="store_true", help="print JSON lines instead of a table")
     a = ap.parse_args(argv)
@@ -96,7 +97,11 @@ def main(argv=None) -> int:
     if a.max_backlog is not None:
         ok &= res.out["backlog"] <= a.max_backlog
     idx = np.flatnonzero(ok)
-    order = idx[np.argsort(res.out[a.objective][idx], kind="stable")][: a.top]
+    if a.pareto:
+        front = sweep.pareto_front(res.out["pod_ms"][idx], res.out["backlog"][idx])
+        order = idx[front][: a.top] if a.top > 0 else idx[front]
+    else:
+        order = idx[np.argsort(res.out[a.objective][idx], kind="stable")][: a.top]
     baseline = sweep.run(tr, sweep.grid(), a.init_replicas, horizon, lat, "cpu").row(0)
     summary = {"configs": len(res), "feasible": int(ok.sum()), "device": res.device, "wall_s": round(wall, 4),
                "kernel_ms": round(res.kernel_ms, 3), "simulated_polls": int(res.out["polls"].sum()),

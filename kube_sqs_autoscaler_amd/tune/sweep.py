@@ -201,6 +201,19 @@ def run(trace: Trace, params: np.ndarray, init_replicas: int = 1, horizon_ns: in
     return SweepResult(params, out, device, kernel_ms)
 
 
+def pareto_front(pod_ms: np.ndarray, backlog: np.ndarray) -> np.ndarray:
+    """Indices of configurations not dominated on (pod_ms, backlog), cheapest first."""
+    order = np.lexsort((backlog, pod_ms))  # by cost, then pressure
+    front = []
+    best = None
+    for i in order:
+        b = backlog[i]
+        if best is None or b < best:
+            front.append(int(i))
+            best = b
+    return np.array(front, dtype=np.int64)
+
+
 def oracle_row(trace: Trace, cfg: Dict[str, int], init_replicas: int, horizon_ns: int,
                latency_ns: Tuple[int, int, int]) -> Dict[str, int]:
     """The same metrics from the independent Python oracle (exactness tests)."""

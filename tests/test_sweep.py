@@ -101,3 +101,11 @@ def test_tune_cli(tmp_path, capsys):
     assert lines[0]["configs"] == 7 * 3 * 2 and lines[0]["reference_defaults"]["ups"] > 0
     pods = [l["pod_ms"] for l in lines[1:]]
     assert len(pods) == 3 and pods == sorted(pods)
+
+
+def test_pareto_front():
+    pod = np.array([5, 1, 3, 2, 4, 1])
+    bl = np.array([1, 9, 4, 8, 2, 7])
+    f = sweep.pareto_front(pod, bl)
+    # (pod, backlog): (1,7) (3,4) (4,2) (5,1); (1,9) and (2,8) are dominated by (1,7)
+    assert list(f) == [5, 2, 4, 0]
