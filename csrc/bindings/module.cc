@@ -385,6 +385,12 @@ PYBIND11_MODULE(_ksa_native, m) {
            },
            py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""))
       .def("set_busy_poll", &HttpClient::set_busy_poll)
+      .def("set_proxy",
+           [](HttpClient& c, const std::string& url) {
+             Status s = c.set_proxy(url);
+             if (!s.ok()) raise_status(s);
+           })
+      .def_property_readonly("proxied", &HttpClient::proxied)
       .def("rtt_ewma", &HttpClient::rtt_ewma)
       .def("close", &HttpClient::close)
       .def("stats", [](HttpClient& c) { return http_stats_dict(c.stats()); });
@@ -409,6 +415,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("protocol", &SqsHttpOptions::protocol)
       .def_readwrite("timeout_ns", &SqsHttpOptions::timeout)
       .def_readwrite("busy_poll_ns", &SqsHttpOptions::busy_poll)
+      .def_readwrite("proxy", &SqsHttpOptions::proxy)
       .def_readwrite("max_retries", &SqsHttpOptions::max_retries)
       .def_readwrite("min_retry_delay_ns", &SqsHttpOptions::min_retry_delay)
       .def_readwrite("min_throttle_delay_ns", &SqsHttpOptions::min_throttle_delay)
@@ -513,7 +520,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("basic_user", &KubeOptions::basic_user)
       .def_readwrite("basic_password", &KubeOptions::basic_password)
       .def_readwrite("timeout_ns", &KubeOptions::timeout)
-      .def_readwrite("busy_poll_ns", &KubeOptions::busy_poll);
+      .def_readwrite("busy_poll_ns", &KubeOptions::busy_poll)
+      .def_readwrite("proxy", &KubeOptions::proxy);
 
   py::class_<DeploymentApi, PyDeploymentApi, py::smart_holder>(m, "DeploymentApi")
       .def(py::init<>())

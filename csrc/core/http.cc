@@ -10,6 +10,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <openssl/err.h>
+#include <openssl/evp.h>
 #include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
@@ -224,8 +225,9 @@ class Stream {
     return Status::OK();
   }
 
- void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
+  void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
   SSL* ssl() const { return ssl_; }
+  void attach_ssl(SSL* ssl) { ssl_ = ssl; }  // TLS inside an established CONNECT tunnel
 
  private:
   // Busy-poll: peek the socket for up to spin_ns_ before sleeping in poll(2). A response that
@@ -416,6 +418,28 @@ Status use_cert_key(SSL_CTX* ctx, const std::string& cert_pem, const std::string
   return Status::OK();
 }
 
+std::string percent_decode(const std::string& in) {
+  std::string out;
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (in[i] == '%' && i + 2 < in.size() && std::isxdigit(static_cast<unsigned char>(in[i + 1])) &&
+        std::isxdigit(static_cast<unsigned char>(in[i + 2]))) {
+      out.push_back(static_cast<char>(std::stoi(in.substr(i + 1, 2), nullptr, 16)));
+      i += 2;
+    } else {
+      out.push_back(in[i]);
+    }
+  }
+  return out;
+}
+
+std::string base64(const std::string& in) {
+  std::string out(4 * ((in.size() + 2) / 3) + 1, '\0');
+  int n = EVP_EncodeBlock(reinterpret_cast<unsigned char*>(&out[0]),
+                          reinterpret_cast<const unsigned char*>(in.data()), static_cast<int>(in.size()));
+  out.resize(n > 0 ? static_cast<size_t>(n) : 0);
+  return out;
+}
+
 bool is_ip_literal(const std::string& h) {
   unsigned char buf[16];
   return inet_pton(AF_INET, h.c_str(), buf) == 1 || inet_pton(AF_INET6, h.c_str(), buf) == 1;
@@ -567,18 +591,43 @@ HttpClientStats HttpClient::stats() const {
   return stats_;
 }
 
-Status HttpClient::connect_locked(int64_t deadline_ns) {
-  if (!ctx_status_.ok()) return ctx_status_;
+Status HttpClient::set_proxy(const std::string& proxy_url) {
+  std::lock_guard<std::mutex> lk(mu_);
+  conn_.reset();
+  has_proxy_ = false;
+  proxy_auth_.clear();
+  if (proxy_url.empty()) return Status::OK();
+  auto u = parse_url(proxy_url);
+  if (!u.status.ok()) return Status::Err("proxy: " + u.status.message());
+  if (u.value.tls()) return Status::Err("proxy: https:// proxies are not supported (use http://)");
+  // userinfo (parse_url drops it): scheme://user[:pass]@host
+  const size_t a = proxy_url.find("://") + 3;
+  const size_t end = proxy_url.find_first_of("/?#", a);
+  const std::string authority = proxy_url.substr(a, end == std::string::npos ? std::string::npos : end - a);
+  const size_t at = authority.rfind('@');
+  if (at != std::string::npos) {
+    std::string info = authority.substr(0, at);
+    const size_t colon = info.find(':');
+    std::string user = percent_decode(info.substr(0, colon));
+    std::string pass = colon == std::string::npos ? "" : percent_decode(info.substr(colon + 1));
+    proxy_auth_ = "Basic " + base64(user + ":" + pass);
+  }
+  proxy_ = u.value;
+  has_proxy_ = true;
+  return Status::OK();
+}
+
+Status HttpClient::dial(const Url& to, int64_t deadline_ns, int* fd_out) {
   struct addrinfo hints;
   std::memset(&hints, 0, sizeof hints);
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
   struct addrinfo* res = nullptr;
-  std::string port = std::to_string(origin_.port);
-  int gai = getaddrinfo(origin_.host.c_str(), port.c_str(), &hints, &res);
+  std::string port = std::to_string(to.port);
+  int gai = getaddrinfo(to.host.c_str(), port.c_str(), &hints, &res);
   if (gai != 0)
-    return Status::Err("dial tcp: lookup " + origin_.host + ": " + gai_strerror(gai));
-  Status last = Status::Err("dial tcp " + origin_.host_header() + ": no addresses");
+    return Status::Err("dial tcp: lookup " + to.host + ": " + gai_strerror(gai));
+  Status last = Status::Err("dial tcp " + to.host_header() + ": no addresses");
   int fd = -1;
   for (auto* ai = res; ai; ai = ai->ai_next) {
     fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, ai->ai_protocol);
@@ -593,11 +642,11 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
       getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
       if (w.ok() && err == 0) r = 0;
       else {
-        last = Status::Err("dial tcp " + origin_.host_header() + ": " +
+        last = Status::Err("dial tcp " + to.host_header() + ": " +
                            (w.ok() ? std::strerror(err) : w.message()));
       }
     } else if (r != 0) {
-      last = Status::Err("dial tcp " + origin_.host_header() + ": " + std::strerror(errno));
+      last = Status::Err("dial tcp " + to.host_header() + ": " + std::strerror(errno));
     }
     if (r == 0) break;
     ::close(fd);
@@ -605,10 +654,46 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   }
   freeaddrinfo(res);
   if (fd < 0) return last;
+  *fd_out = fd;
+  return Status::OK();
+}
+
+Status HttpClient::connect_locked(int64_t deadline_ns) {
+  if (!ctx_status_.ok()) return ctx_status_;
+  int fd = -1;
+  Status d = dial(has_proxy_ ? proxy_ : origin_, deadline_ns, &fd);
+  if (!d.ok()) return has_proxy_ ? Status::Err("proxyconnect tcp: " + d.message()) : d;
+  auto stream = std::make_unique<Stream>(fd, nullptr);
+  std::string rbuf;
+  if (has_proxy_ && origin_.tls()) {
+    // CONNECT tunnel: the proxy relays bytes; TLS (and its verification) is end to end.
+    std::string authority = origin_.host.find(':') != std::string::npos ? "[" + origin_.host + "]" : origin_.host;
+    authority += ":" + std::to_string(origin_.port);
+    std::string wire = "CONNECT " + authority + " HTTP/1.1\r\nHost: " + authority + "\r\n";
+    if (!proxy_auth_.empty()) wire += "Proxy-Authorization: " + proxy_auth_ + "\r\n";
+    wire += "\r\n";
+    Status w = stream->write_all(wire, deadline_ns);
+    if (!w.ok()) return Status::Err("proxyconnect tcp: " + w.message());
+    Reader rd(stream.get(), &rbuf);
+    std::string head;
+    bool got_any = false;
+    Status r = rd.read_head(&head, deadline_ns, &got_any);
+    if (!r.ok()) return Status::Err("proxyconnect tcp: " + r.message());
+    const std::string status_line = head.substr(0, head.find("\r\n"));
+    const size_t sp = status_line.find(' ');
+    const int code = sp == std::string::npos ? 0 : std::atoi(status_line.c_str() + sp + 1);
+    if (status_line.compare(0, 5, "HTTP/") != 0 || code < 200 || code > 299)
+      return Status::Err("proxy CONNECT " + authority + ": " +
+                         (sp == std::string::npos ? status_line : status_line.substr(sp + 1)));
+    // The server speaks only after our ClientHello, so nothing may follow the proxy's reply.
+    if (!rbuf.empty()) return Status::Err("proxy CONNECT " + authority + ": unexpected data after the reply");
+    stats_.bytes_out += wire.size();
+  }
 
   SSL* ssl = nullptr;
   if (origin_.tls()) {
     ssl = SSL_new(ctx_);
+    stream->attach_ssl(ssl);
     SSL_set_fd(ssl, fd);
     const std::string& name = tls_.server_name.empty() ? origin_.host : tls_.server_name;
     if (!is_ip_literal(name)) SSL_set_tlsext_host_name(ssl, name.c_str());
@@ -621,7 +706,6 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
     // keep-alive connection -- AWS endpoints do after about a minute.
     if (session_) SSL_set_session(ssl, session_);
   }
-  auto stream = std::make_unique<Stream>(fd, ssl);
   if (ssl) {
     Status h = stream->handshake(false, deadline_ns);
     if (!h.ok()) {
@@ -635,6 +719,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   }
   conn_ = std::make_unique<Conn>();
   conn_->stream = std::move(stream);
+  conn_->rbuf = std::move(rbuf);
   stats_.connects++;
   return Status::OK();
 }
@@ -652,9 +737,12 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   wire.reserve(256 + req.body.size());
   wire += req.method;
   wire.push_back(' ');
+  // A plain-HTTP origin behind a proxy gets the absolute-form target (RFC 9112 §3.2.2).
+  if (has_proxy_ && !origin_.tls()) wire += origin_.origin();
   wire += req.target.empty() ? "/" : req.target;
   wire += " HTTP/1.1\r\n";
   if (!has_header(req.headers, "Host")) wire += "Host: " + origin_.host_header() + "\r\n";
+  if (has_proxy_ && !origin_.tls() && !proxy_auth_.empty()) wire += "Proxy-Authorization: " + proxy_auth_ + "\r\n";
   if (!has_header(req.headers, "User-Agent")) wire += "User-Agent: kube-sqs-autoscaler-amd/1.0\r\n";
   for (auto& [k, v] : req.headers) wire += k + ": " + v + "\r\n";
   if (!req.body.empty() || req.method == "POST" || req.method == "PUT" || req.method == "PATCH") {
@@ -919,6 +1007,12 @@ void HttpServer::serve(int fd) {
       if (a == std::string::npos || b == a) break;
       req.method = line.substr(0, a);
       req.target = line.substr(a + 1, b - a - 1);
+      // absolute-form (what clients send to a proxy; servers must accept it): keep path+query
+      if (req.target.compare(0, 7, "http://") == 0 || req.target.compare(0, 8, "https://") == 0) {
+        const size_t slash = req.target.find_first_of("/?", req.target.find("://") + 3);
+        req.target = slash == std::string::npos ? "/" : req.target.substr(slash);
+        if (req.target[0] == '?') req.target = "/" + req.target;
+      }
       const bool http10 = line.compare(b + 1, 8, "HTTP/1.0") == 0;
       if (eol != std::string::npos) parse_header_lines(head, eol + 2, &req.headers);
       Status s;

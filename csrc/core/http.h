@@ -105,10 +105,18 @@ class HttpClient {
   // slower peers (real AWS / apiserver RTTs of milliseconds) it never spins. 0 disables.
   void set_busy_poll(Nanos ns) { spin_ns_ = ns; }
   Nanos rtt_ewma() const;
+  // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller):
+  // "http://[user:pass@]host:port". An https origin is reached through a CONNECT tunnel (TLS
+  // runs end to end inside it); an http origin gets absolute-form requests sent to the proxy.
+  // Credentials in the URL become Proxy-Authorization: Basic. Empty = connect directly. Call
+  // before the first request.
+  Status set_proxy(const std::string& proxy_url);
+  bool proxied() const { return has_proxy_; }
 
  private:
   struct Conn;
   Status connect_locked(int64_t deadline_ns);
+  Status dial(const Url& to, int64_t deadline_ns, int* fd_out);
   Status attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
                  bool* retryable);
   Status write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable);
@@ -128,6 +136,9 @@ class HttpClient {
   Nanos ewma_ns_ = -1;   // response-time EWMA (-1: no sample yet)
   int64_t sent_at_ = 0;  // mono time the current request finished writing
   Nanos spin_window() const;
+  bool has_proxy_ = false;
+  Url proxy_;
+  std::string proxy_auth_;  // "Basic ..." or empty
   bool in_flight_ = false;
   HttpRequest pending_;
   int64_t pending_deadline_ = 0;

@@ -91,6 +91,8 @@ KubeRestDeployments::KubeRestDeployments(KubeOptions opts) : opts_(std::move(opt
   url_ = u.value;
   http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
   http_->set_busy_poll(opts_.busy_poll);
+  Status ps = http_->set_proxy(opts_.proxy);
+  if (!ps.ok()) init_status_ = ps;
 }
 
 KubeStats KubeRestDeployments::stats() const {

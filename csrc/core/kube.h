@@ -97,6 +97,7 @@ struct KubeOptions {
   std::string basic_user, basic_password;  // legacy kubeconfig basic auth
   Nanos timeout = 30 * kSecond;
   Nanos busy_poll = 0;  // HttpClient::set_busy_poll
+  std::string proxy;    // HttpClient::set_proxy ("" = direct)
 };
 
 struct KubeStats {

@@ -53,6 +53,8 @@ HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider>
   url_ = u.value;
   http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
   http_->set_busy_poll(opts_.busy_poll);
+  Status ps = http_->set_proxy(opts_.proxy);
+  if (!ps.ok()) endpoint_status_ = ps;
 }
 
 SqsApiStats HttpSqsApi::stats() const {

@@ -50,6 +50,7 @@ struct SqsHttpOptions {
   Nanos min_throttle_delay = 500 * kMillisecond;
   Nanos max_retry_delay = 300 * kSecond;
   TlsOptions tls;
+  std::string proxy;    // HttpClient::set_proxy ("" = direct)
 };
 
 struct SqsApiStats {

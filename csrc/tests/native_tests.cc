@@ -5,11 +5,18 @@
 // its loop tests leak goroutines that race on package globals. Here the multi-queue supervisor,
 // the threaded fake servers and the keep-alive clients are exercised concurrently so TSan can
 // see every cross-thread access of the runtime.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -233,6 +240,112 @@ TEST(http_tls_roundtrip) {
   HttpRequest req;
   HttpResponse resp;
   CHECK(!bad.round_trip(req, &resp).ok());
+  srv.stop();
+}
+
+// Minimal CONNECT relay (one tunnel): records the request head, dials the target, relays bytes.
+class ConnectRelay {
+ public:
+  ConnectRelay() {
+    lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    ::bind(lfd_, reinterpret_cast<sockaddr*>(&a), sizeof a);
+    ::listen(lfd_, 4);
+    socklen_t len = sizeof a;
+    getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &len);
+    port_ = ntohs(a.sin_port);
+    th_ = std::thread([this] { run(); });
+  }
+  ~ConnectRelay() {
+    ::shutdown(lfd_, SHUT_RDWR);
+    th_.join();
+    ::close(lfd_);
+  }
+  int port() const { return port_; }
+  std::string head() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return head_;
+  }
+
+ private:
+  void run() {
+    int c = ::accept(lfd_, nullptr, nullptr);
+    if (c < 0) return;
+    std::string buf;
+    char tmp[4096];
+    while (buf.find("\r\n\r\n") == std::string::npos) {
+      ssize_t n = ::recv(c, tmp, sizeof tmp, 0);
+      if (n <= 0) {
+        ::close(c);
+        return;
+      }
+      buf.append(tmp, static_cast<size_t>(n));
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      head_ = buf.substr(0, buf.find("\r\n\r\n"));
+    }
+    // "CONNECT 127.0.0.1:PORT HTTP/1.1"
+    const size_t colon = buf.find(':'), sp = buf.find(' ', colon);
+    const int up_port = std::atoi(buf.substr(colon + 1, sp - colon - 1).c_str());
+    int u = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    a.sin_port = htons(static_cast<uint16_t>(up_port));
+    if (::connect(u, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0) {
+      const char ok[] = "HTTP/1.1 200 Connection established\r\n\r\n";
+      ::send(c, ok, sizeof ok - 1, MSG_NOSIGNAL);
+      pollfd p[2] = {{c, POLLIN, 0}, {u, POLLIN, 0}};
+      while (::poll(p, 2, 5000) > 0) {
+        bool done = false;
+        for (int i = 0; i < 2; ++i) {
+          if (!(p[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+          ssize_t n = ::recv(p[i].fd, tmp, sizeof tmp, 0);
+          if (n <= 0 || ::send(p[1 - i].fd, tmp, static_cast<size_t>(n), MSG_NOSIGNAL) != n) done = true;
+        }
+        if (done) break;
+      }
+    }
+    ::close(u);
+    ::close(c);
+  }
+
+  int lfd_ = -1, port_ = 0;
+  std::thread th_;
+  std::mutex mu_;
+  std::string head_;
+};
+
+TEST(http_tls_through_connect_proxy) {
+  std::string cert, key;
+  CHECK(generate_self_signed("127.0.0.1", &cert, &key).ok());
+  HttpServer srv([](const HttpRequest& req, HttpResponse* resp) {
+    resp->status = 200;
+    resp->body = "via-proxy " + req.target;
+  });
+  CHECK(srv.enable_tls(cert, key).ok());
+  CHECK(srv.listen("127.0.0.1", 0).ok());
+  ConnectRelay relay;
+  TlsOptions tls;
+  tls.ca_pem = cert;
+  HttpClient c(parse_url("https://127.0.0.1:" + std::to_string(srv.port())).value, tls, 5 * kSecond);
+  CHECK(c.set_proxy("http://user:p%40ss@127.0.0.1:" + std::to_string(relay.port())).ok());
+  for (int i = 0; i < 3; ++i) {
+    HttpRequest req;
+    req.target = "/x";
+    HttpResponse resp;
+    CHECK(c.round_trip(req, &resp).ok());
+    CHECK_EQ(resp.body, std::string("via-proxy /x"));
+  }
+  CHECK_EQ(c.stats().connects, uint64_t(1));
+  const std::string head = relay.head();
+  CHECK(head.rfind("CONNECT 127.0.0.1:" + std::to_string(srv.port()) + " HTTP/1.1\r\n", 0) == 0);
+  CHECK(head.find("Proxy-Authorization: Basic dXNlcjpwQHNz") != std::string::npos);  // user:p@ss
+  CHECK(!c.set_proxy("https://127.0.0.1:1").ok());
+  c.close();
   srv.stop();
 }
 

@@ -21,6 +21,7 @@ from .config import Config, TargetConfig
 from .kube.config import RestConfig, build_config_from_flags
 from .ops import native
 from .sqs.credentials import make_chain_provider
+from .utils import proxy
 from .utils.goflag import SECOND
 
 _SCALE_MODES = {"deployment": "Deployment", "scale": "Scale", "patch": "Patch"}
@@ -41,12 +42,25 @@ def tls_options(rc: RestConfig):
     return t
 
 
+def kube_proxy(rc: RestConfig, environ: Optional[Mapping[str, str]] = None) -> str:
+    """client-go: the kubeconfig ``proxy-url``, else ``http.ProxyFromEnvironment``."""
+    return proxy.select(rc.host, environ, rc.proxy_url)
+
+
+def new_http_client(rc: RestConfig, timeout_ns: int, environ: Optional[Mapping[str, str]] = None):
+    """A native keep-alive client to the apiserver (leader election, node listing)."""
+    c = native().HttpClient(rc.host, tls_options(rc), timeout_ns)
+    c.set_proxy(kube_proxy(rc, environ))
+    return c
+
+
 def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", timeout_ns: int = 30 * SECOND, clock=None,
-                       busy_poll_ns: int = 0):
+                       busy_poll_ns: int = 0, environ: Optional[Mapping[str, str]] = None):
     """The ``DeploymentInterface`` seam over REST (/root/reference/scale/scale.go:44)."""
     nat = native()
     o = nat.KubeOptions()
     o.server = rc.host
+    o.proxy = kube_proxy(rc, environ)
     o.namespace = namespace
     o.mode = scale_mode(mode)
     o.tls = tls_options(rc)
@@ -77,6 +91,8 @@ def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query",
     o.timeout_ns = timeout_ns
     o.busy_poll_ns = busy_poll_ns
     env = os.environ if environ is None else environ
+    # aws-sdk-go's default client: http.ProxyFromEnvironment on the resolved endpoint
+    o.proxy = proxy.select(endpoint or nat.HttpSqsApi.endpoint_for_region(region), env)
     if tls is not None:
         o.tls = tls
     elif env.get("AWS_CA_BUNDLE"):  # aws-sdk-go v1 session: custom CA bundle for AWS endpoints
@@ -118,7 +134,7 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     if tag_queue:
         log = base_logger.with_fields([("deployment", target.name), ("queue", target.queue_url)])
     kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock,
-                                  busy_poll_ns=cfg.busy_poll_ns)
+                                  busy_poll_ns=cfg.busy_poll_ns, environ=environ)
     scaler = new_pod_autoscaler(target, kube_api, log, clock)
     scaler.dry_run = cfg.dry_run
     sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,

@@ -45,6 +45,7 @@ class RestConfig:
     key_pem: str = ""
     insecure: bool = False
     server_name: str = ""
+    proxy_url: str = ""  # kubeconfig cluster proxy-url (client-go v0.19); "" = environment
     source: str = ""
     warnings: list = field(default_factory=list)
 
@@ -109,6 +110,7 @@ def load_kubeconfig(path: str, context: str = "") -> RestConfig:
     rc = RestConfig(host=server, source=f"kubeconfig:{path}")
     rc.insecure = bool(cluster.get("insecure-skip-tls-verify", False))
     rc.server_name = cluster.get("tls-server-name", "")
+    rc.proxy_url = cluster.get("proxy-url", "") or ""
     try:
         if cluster.get("certificate-authority-data"):
             rc.ca_pem = _b64(cluster["certificate-authority-data"])

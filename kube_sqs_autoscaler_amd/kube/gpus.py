@@ -45,7 +45,7 @@ def _quantity(v) -> int:
 class ClusterGpuCapacity:
     def __init__(self, rest: RestConfig, resource: str = "amd.com/gpu", node_selector: str = "",
                  gpus_per_pod: int = 1, timeout_s: float = 10.0):
-        from ..autoscaler import tls_options
+        from ..autoscaler import new_http_client
 
         if gpus_per_pod < 1:
             raise ValueError("gpus-per-pod must be >= 1")
@@ -53,7 +53,7 @@ class ClusterGpuCapacity:
         self.resource = resource
         self.selector = node_selector
         self.gpus_per_pod = gpus_per_pod
-        self.http = native().HttpClient(rest.host, tls_options(rest), int(timeout_s * 1e9))
+        self.http = new_http_client(rest, int(timeout_s * 1e9))
 
     def _headers(self):
         h = [("Accept", "application/json")]

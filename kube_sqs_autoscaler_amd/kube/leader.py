@@ -81,13 +81,12 @@ class LeaseLock:
     """Lease CRUD over the native keep-alive HTTP client (TLS, CA, bearer/basic auth)."""
 
     def __init__(self, rest: RestConfig, namespace: str, name: str, timeout_s: float = 10.0):
-        nat = native()
-        from ..autoscaler import tls_options
+        from ..autoscaler import new_http_client
 
         self.rest = rest
         self.namespace = namespace
         self.name = name
-        self.http = nat.HttpClient(rest.host, tls_options(rest), int(timeout_s * 1e9))
+        self.http = new_http_client(rest, int(timeout_s * 1e9))
         self._rv = ""
         self._token_file_mtime = 0.0
 

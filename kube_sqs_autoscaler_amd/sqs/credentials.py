@@ -37,6 +37,7 @@ from datetime import datetime, timezone
 from typing import Callable, Dict, List, Mapping, Optional, Tuple
 
 from ..ops import native
+from ..utils import proxy
 
 ECS_HOST = "http://169.254.170.2"
 IMDS_HOST = "http://169.254.169.254"
@@ -67,8 +68,11 @@ Fetch = Callable[[str, str, Dict[str, str], bytes, float], Tuple[int, bytes]]
 
 def urllib_fetch(method: str, url: str, headers: Dict[str, str], body: bytes, timeout: float) -> Tuple[int, bytes]:
     req = urllib.request.Request(url, data=body if body else None, method=method, headers=headers)
+    # Go's proxy rules (NO_PROXY CIDRs, loopback), not urllib's own environment handling
+    p = proxy.select(url)
+    opener = urllib.request.build_opener(urllib.request.ProxyHandler({urllib.parse.urlsplit(url).scheme: p} if p else {}))
     try:
-        with urllib.request.urlopen(req, timeout=timeout) as r:
+        with opener.open(req, timeout=timeout) as r:
             return r.status, r.read()
     except urllib.error.HTTPError as e:
         return e.code, e.read()
