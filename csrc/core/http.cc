@@ -593,6 +593,7 @@ HttpClientStats HttpClient::stats() const {
 
 Status HttpClient::set_proxy(const std::string& proxy_url) {
   std::lock_guard<std::mutex> lk(mu_);
+  if (in_flight_) return Status::Err("http: a pipelined request is still in flight");
   conn_.reset();
   has_proxy_ = false;
   proxy_auth_.clear();

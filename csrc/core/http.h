@@ -111,7 +111,10 @@ class HttpClient {
   // Credentials in the URL become Proxy-Authorization: Basic. Empty = connect directly. Call
   // before the first request.
   Status set_proxy(const std::string& proxy_url);
-  bool proxied() const { return has_proxy_; }
+  bool proxied() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return has_proxy_;
+  }
 
  private:
   struct Conn;
