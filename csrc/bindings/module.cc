@@ -499,7 +499,8 @@ PYBIND11_MODULE(_ksa_native, m) {
           r = t.token();
         }
         return unwrap(r);
-      });
+      })
+      .def("invalidate", [](TokenProvider& t, const std::string& used) { t.invalidate(used); }, py::arg("used"));
   py::class_<StaticTokenProvider, TokenProvider, py::smart_holder>(m, "StaticTokenProvider")
       .def(py::init<std::string>());
   py::class_<FileTokenProvider, TokenProvider, py::smart_holder>(m, "FileTokenProvider")

@@ -35,6 +35,11 @@ Result<std::string> FileTokenProvider::token() {
   return Result<std::string>::Ok(cached_);
 }
 
+void FileTokenProvider::invalidate(const std::string& used) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (have_ && cached_ == used) read_at_ = clock_->now() - refresh_;  // re-read on next use
+}
+
 // ---------------------------------------------------------------------------------------
 // Object helpers
 
@@ -191,6 +196,10 @@ Status KubeRestDeployments::check_response(const std::string& verb_desc, const H
     std::string verb = m.substr(0, 1) + std::string(m.begin() + 1, m.end());
     for (size_t i = 1; i < verb.size(); ++i) verb[i] = static_cast<char>(std::tolower(verb[i]));
     return Status::Err(verb + " \"" + url_.origin() + req.target + "\": " + transport.message());
+  }
+  if (resp.status == 401 && opts_.token) {
+    const std::string auth = req.header("Authorization");
+    if (auth.compare(0, 7, "Bearer ") == 0) opts_.token->invalidate(auth.substr(7));
   }
   if (resp.status < 200 || resp.status >= 300) {
     const std::string resource = "deployments.apps";

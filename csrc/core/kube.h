@@ -58,6 +58,10 @@ class TokenProvider {
  public:
   virtual ~TokenProvider() = default;
   virtual Result<std::string> token() = 0;
+  // The apiserver answered 401 to a request carrying `used`: drop it if it is still the cached
+  // token, so the next token() fetches a fresh one (client-go's exec authenticator and token
+  // file source both refresh on 401).
+  virtual void invalidate(const std::string& used) { (void)used; }
 };
 
 class StaticTokenProvider final : public TokenProvider {
@@ -75,6 +79,7 @@ class FileTokenProvider final : public TokenProvider {
  public:
   FileTokenProvider(std::string path, std::shared_ptr<Clock> clock, Nanos refresh = 60 * kSecond);
   Result<std::string> token() override;
+  void invalidate(const std::string& used) override;
 
  private:
   std::string path_;

@@ -94,3 +94,42 @@ def test_file_token_provider_rotation(tmp_path, nat):
     f.unlink()
     clock.advance(61 * nat.SECOND)
     assert tp.token() == "two"  # keeps the last good token if the file vanishes
+
+
+def test_401_rereads_rotated_token_file(tmp_path, nat):
+    """A projected token rotated early is picked up on the next request after the apiserver
+    rejects the old one, not only after the periodic re-read (virtual clock: never advances)."""
+    from kube_sqs_autoscaler_amd.autoscaler import new_deployment_api
+    from kube_sqs_autoscaler_amd.kube.config import RestConfig
+    from kube_sqs_autoscaler_amd.utils.log import capture_logger
+
+    f = tmp_path / "token"
+    f.write_text("old")
+    k = nat.FakeKubeServer()
+    k.require_token("new")
+    k.start()
+    try:
+        k.add_deployment("ml", "worker", 1)
+        clock = nat.VirtualClock(0)
+        api = new_deployment_api(RestConfig(host=k.url, bearer_token_file=str(f)), "ml", "scale", clock=clock)
+        p = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), clock)
+        with pytest.raises(nat.NativeError, match="Unauthorized"):
+            p.scale_up()  # "old" is read, cached and rejected ...
+        f.write_text("new")  # ... the kubelet rotates the file ...
+        p.scale_up()  # ... and the 401 made the provider re-read it (the clock never moved)
+        assert k.replicas("ml", "worker") == 2
+    finally:
+        k.stop()
+
+
+def test_invalidate_only_drops_the_rejected_token(tmp_path, nat):
+    f = tmp_path / "token"
+    f.write_text("one")
+    clock = nat.VirtualClock(0)
+    tp = nat.FileTokenProvider(str(f), clock, 60 * nat.SECOND)
+    assert tp.token() == "one"
+    f.write_text("two")
+    tp.invalidate("stale-from-another-request")
+    assert tp.token() == "one"  # a different token was rejected: keep the cache
+    tp.invalidate("one")
+    assert tp.token() == "two"
