@@ -142,6 +142,7 @@ py::dict record_dict(const IterationRecord& r) {
   d["replicas_before"] = r.replicas_before;
   d["replicas_after"] = r.replicas_after;
   d["prefetched"] = r.prefetched;
+  d["prefetch_used"] = r.prefetch_used;
   d["depth_ns"] = r.depth_ns;
   d["get_ns"] = r.get_ns;
   d["update_ns"] = r.update_ns;
@@ -674,6 +675,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["cooldown_skips_down"] = s.cooldown_skips_down;
         d["failed_ups"] = s.failed_ups;
         d["failed_downs"] = s.failed_downs;
+        d["speculative_reads"] = s.speculative_reads;
+        d["speculative_reads_used"] = s.speculative_reads_used;
         d["last_depth"] = s.last_depth;
         d["last_replicas"] = s.last_replicas;
         d["latency_samples"] = s.latency_samples;

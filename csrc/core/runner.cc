@@ -102,6 +102,7 @@ IterationRecord Runner::poll_once() {
     Status s = scaler_->scale_up(&span);
     rec.get_ns += span.get_ns;
     rec.update_ns += span.update_ns;
+    rec.prefetch_used |= span.used_prefetch;
     if (span.read) {
       rec.replicas_before = span.before;
       rec.replicas_after = span.after;
@@ -128,6 +129,7 @@ IterationRecord Runner::poll_once() {
     Status s = scaler_->scale_down(&span);
     rec.get_ns += span.get_ns;
     rec.update_ns += span.update_ns;
+    rec.prefetch_used |= span.used_prefetch;
     if (span.read) {
       if (rec.replicas_before < 0) rec.replicas_before = span.before;
       rec.replicas_after = span.after;
@@ -149,6 +151,8 @@ void Runner::record(const IterationRecord& r) {
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.polls++;
+    if (r.prefetched) stats_.speculative_reads++;
+    if (r.prefetch_used) stats_.speculative_reads_used++;
     if (!r.depth_ok) stats_.depth_errors++;
     else stats_.last_depth = r.depth;
     switch (r.up) {
@@ -189,6 +193,7 @@ std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std:
                   "\",\"replicas_before\":" + std::to_string(r.replicas_before) +
                   ",\"replicas_after\":" + std::to_string(r.replicas_after) +
                   ",\"prefetched\":" + (r.prefetched ? "true" : "false") +
+                  ",\"prefetch_used\":" + (r.prefetch_used ? "true" : "false") +
                   ",\"depth_ns\":" + std::to_string(r.depth_ns) + ",\"get_ns\":" + std::to_string(r.get_ns) +
                   ",\"update_ns\":" + std::to_string(r.update_ns) + ",\"total_ns\":" + std::to_string(r.total_ns) +
                   ",\"patch_latency_ns\":" + std::to_string(r.patch_latency_ns);

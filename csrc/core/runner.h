@@ -60,6 +60,7 @@ struct IterationRecord {
   int32_t replicas_before = -1;  // as read by the last GET of the iteration (-1: not read)
   int32_t replicas_after = -1;
   bool prefetched = false;     // a pipelined GET was issued with the poll
+  bool prefetch_used = false;  // ... and a scale decision consumed it
   Nanos depth_ns = 0;          // SQS GetQueueAttributes round trip
   Nanos get_ns = 0;            // Deployment GET(s)
   Nanos update_ns = 0;         // Deployment PUT/PATCH(es)
@@ -79,6 +80,8 @@ struct RunnerStats {
   uint64_t cooldown_skips_down = 0;
   uint64_t failed_ups = 0;
   uint64_t failed_downs = 0;
+  uint64_t speculative_reads = 0;       // pipelined GETs issued (one per poll with --pipeline-reads)
+  uint64_t speculative_reads_used = 0;  // ... consumed by a scale decision (the rest are extra API load)
   int64_t last_depth = 0;
   int32_t last_replicas = -1;
   uint64_t latency_samples = 0;

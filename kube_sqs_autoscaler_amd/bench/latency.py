@@ -114,6 +114,7 @@ class BenchEnv:
             rest.ca_pem = self.kube.cert_pem
         creds = static_provider(AKID, SECRET)
         self.runners = []
+        self.kube_apis, self.sqs_apis = [], []
         self.targets = []
         for q in range(queues):
             url = f"{self.sqs.url}/000000000000/bench-queue-{q}"
@@ -128,6 +129,8 @@ class BenchEnv:
             sqs_api = new_sqs_api(REGION, self.clock, endpoint=self.sqs.url, credentials=creds, tls=sqs_tls,
                                   busy_poll_ns=busy_poll_ns)
             client = new_sqs_client(t, sqs_api)
+            self.kube_apis.append(kube_api)
+            self.sqs_apis.append(sqs_api)
             cfg = nat.LoopConfig()
             cfg.poll_period_ns = 0
             cfg.scale_up_cool_down_ns = 0

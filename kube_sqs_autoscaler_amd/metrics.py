@@ -29,7 +29,27 @@ _COUNTERS = [
     ("cooldown_skips_down", "Scale-downs skipped by the cool-down"),
     ("failed_ups", "Scale-ups that failed"),
     ("failed_downs", "Scale-downs that failed"),
+    ("speculative_reads", "Deployment GETs sent with the SQS poll (--pipeline-reads)"),
+    ("speculative_reads_used", "Speculative GETs consumed by a scale decision"),
 ]
+
+# Per-worker API client counters: (metric, help, client attribute, stats key)
+_API_COUNTERS = [
+    ("apiserver_gets", "Deployment/scale GETs sent to the kube-apiserver", "kube_api", "gets"),
+    ("apiserver_writes", "Deployment/scale PUT/PATCH requests sent to the kube-apiserver", "kube_api", "updates"),
+    ("apiserver_conflicts", "Writes rejected with 409 Conflict", "kube_api", "conflicts"),
+    ("apiserver_errors", "kube-apiserver requests that failed", "kube_api", "errors"),
+    ("sqs_calls", "GetQueueAttributes calls (including SDK-style retries)", "sqs_api", "calls"),
+    ("sqs_retries", "GetQueueAttributes retries", "sqs_api", "retries"),
+    ("sqs_errors", "GetQueueAttributes calls that failed", "sqs_api", "errors"),
+]
+
+
+def _client_stats(client) -> dict:
+    try:
+        return dict(client.stats())
+    except (AttributeError, TypeError):  # in-process fakes without transport counters
+        return {}
 
 
 class FleetCollector:
@@ -43,15 +63,21 @@ class FleetCollector:
         depth = GaugeMetricFamily("ksa_queue_depth", "Last observed queue depth (sum of attributes)", labels=labels)
         reps = GaugeMetricFamily("ksa_replicas", "Last observed Deployment replicas", labels=labels)
         lat = SummaryMetricFamily("ksa_poll_to_patch_seconds", "Poll end -> replica write latency", labels=labels)
+        api = {k: CounterMetricFamily(f"ksa_{k}", h, labels=labels) for k, h, _, _ in _API_COUNTERS}
         for w, s in zip(self.fleet.workers, stats):
             lv = [s["deployment"], s["queue"]]
             for k, _ in _COUNTERS:
                 fams[k].add_metric(lv, s[k])
+            clients = {a: _client_stats(getattr(w, a, None)) for a in ("kube_api", "sqs_api")}
+            for k, _, attr, key in _API_COUNTERS:
+                if key in clients[attr]:
+                    api[k].add_metric(lv, clients[attr][key])
             depth.add_metric(lv, s["last_depth"])
             reps.add_metric(lv, s["last_replicas"])
             samples = w.runner.latencies()
             lat.add_metric(lv, count_value=s["latency_samples"], sum_value=sum(samples) / 1e9)
         yield from fams.values()
+        yield from (f for f in api.values() if f.samples)
         yield depth
         yield reps
         yield lat

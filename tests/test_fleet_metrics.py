@@ -9,8 +9,9 @@ from kube_sqs_autoscaler_amd.parallel.fleet import Fleet
 
 
 class W:
-    def __init__(self, runner, target):
+    def __init__(self, runner, target, kube_api=None, sqs_api=None):
         self.runner, self.target = runner, target
+        self.kube_api, self.sqs_api = kube_api, sqs_api
 
 
 def test_fleet_runs_queues_independently(nat):
@@ -52,7 +53,7 @@ def test_fleet_stop_interrupts_sleep(nat):
 def test_metrics_endpoints(nat):
     env = BenchEnv(2)
     try:
-        fleet = Fleet([W(r, t) for r, t in zip(env.runners, env.targets)])
+        fleet = Fleet([W(*a) for a in zip(env.runners, env.targets, env.kube_apis, env.sqs_apis)])
         m = MetricsServer(fleet, "127.0.0.1:0")
         m.start()
         try:
@@ -66,6 +67,14 @@ def test_metrics_endpoints(nat):
             assert 'ksa_polls_total{deployment="bench/gpu-worker-0"' in body
             assert "ksa_scale_ups_total" in body and "ksa_poll_to_patch_seconds_count" in body
             assert 'ksa_replicas{deployment="bench/gpu-worker-1"' in body
+            # API load: every poll sends one speculative GET (pipelined reads) and one SQS call;
+            # all 10 polls act on the 200/0 trace, so every speculative read is consumed
+            q0 = '{deployment="bench/gpu-worker-0",queue='
+            metric = {line.split("{")[0] + ("" if q0 in line else "#other"): float(line.rsplit(" ", 1)[1])
+                      for line in body.splitlines() if line.startswith("ksa_") and q0 in line}
+            assert metric["ksa_speculative_reads_total"] == 10 == metric["ksa_speculative_reads_used_total"]
+            assert metric["ksa_sqs_calls_total"] == 10 and metric["ksa_apiserver_writes_total"] == 10
+            assert metric["ksa_apiserver_gets_total"] == 10 and metric["ksa_apiserver_conflicts_total"] == 0
             assert urllib.request.urlopen(base + "/readyz").read() == b"ok"
             assert urllib.request.urlopen(base + "/healthz").status == 200
         finally:
