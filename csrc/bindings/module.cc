@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include "../core/clock.h"
+#include "../core/exec_auth.h"
 #include "../core/fakes.h"
 #include "../core/goutil.h"
 #include "../core/http.h"
@@ -507,6 +508,54 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<FileTokenProvider, TokenProvider, py::smart_holder>(m, "FileTokenProvider")
       .def(py::init<std::string, std::shared_ptr<Clock>, Nanos>(), py::arg("path"), py::arg("clock"),
            py::arg("refresh_ns") = 60 * kSecond);
+
+  py::class_<ExecConfig>(m, "ExecConfig")
+      .def(py::init<>())
+      .def_readwrite("command", &ExecConfig::command)
+      .def_readwrite("args", &ExecConfig::args)
+      .def_readwrite("env", &ExecConfig::env)
+      .def_readwrite("api_version", &ExecConfig::api_version)
+      .def_readwrite("install_hint", &ExecConfig::install_hint)
+      .def_readwrite("timeout_ns", &ExecConfig::timeout);
+  py::class_<ExecCredential>(m, "ExecCredential")
+      .def(py::init<>())
+      .def_readonly("token", &ExecCredential::token)
+      .def_readonly("cert_pem", &ExecCredential::cert_pem)
+      .def_readonly("key_pem", &ExecCredential::key_pem)
+      .def_readonly("has_expiry", &ExecCredential::has_expiry)
+      .def_readonly("expiry_unix_ns", &ExecCredential::expiry_unix_ns);
+  m.def("validate_exec_config", [](const ExecConfig& c) {
+    Status s = validate_exec_config(c);
+    if (!s.ok()) raise_status(s);
+  });
+  m.def(
+      "run_exec_plugin",
+      [](const ExecConfig& c, int code) {
+        Result<ExecCredential> r;
+        {
+          py::gil_scoped_release rel;
+          r = run_exec_plugin(c, code);
+        }
+        return unwrap(r);
+      },
+      py::arg("config"), py::arg("response_code") = 0);
+  py::class_<ExecTokenProvider, TokenProvider, py::smart_holder>(m, "ExecTokenProvider")
+      .def(py::init<ExecConfig, std::shared_ptr<Clock>>(), py::arg("config"), py::arg("clock"))
+      .def("credential",
+           [](ExecTokenProvider& p) {
+             Result<ExecCredential> r;
+             {
+               py::gil_scoped_release rel;
+               r = p.credential();
+             }
+             return unwrap(r);
+           })
+      .def_property_readonly("runs", &ExecTokenProvider::runs);
+  m.def("parse_rfc3339", [](const std::string& s) -> py::object {
+    int64_t ns;
+    if (!parse_rfc3339(s, &ns)) return py::none();
+    return py::int_(ns);
+  });
 
   py::enum_<ScaleMode>(m, "ScaleMode")
       .value("Deployment", ScaleMode::Deployment)

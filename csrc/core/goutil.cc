@@ -153,6 +153,74 @@ std::string rfc3339_utc(int64_t unix_nanos) {
   return buf;
 }
 
+namespace {
+
+// Days since 1970-01-01 of a proleptic Gregorian date (H. Hinnant's days_from_civil).
+int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = static_cast<unsigned>(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + static_cast<int64_t>(doe) - 719468;
+}
+
+bool fixed_digits(const std::string& s, size_t pos, size_t n, int* out) {
+  if (pos + n > s.size()) return false;
+  int v = 0;
+  for (size_t i = pos; i < pos + n; ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (s[i] - '0');
+  }
+  *out = v;
+  return true;
+}
+
+}  // namespace
+
+bool parse_rfc3339(const std::string& s, int64_t* unix_nanos) {
+  int Y, M, D, h, m, sec;
+  if (!fixed_digits(s, 0, 4, &Y) || s.size() < 20 || s[4] != '-' || !fixed_digits(s, 5, 2, &M) || s[7] != '-' ||
+      !fixed_digits(s, 8, 2, &D) || (s[10] != 'T' && s[10] != 't') || !fixed_digits(s, 11, 2, &h) ||
+      s[13] != ':' || !fixed_digits(s, 14, 2, &m) || s[16] != ':' || !fixed_digits(s, 17, 2, &sec))
+    return false;
+  static const int kDays[] = {31, 29, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const bool leap = (Y % 4 == 0 && Y % 100 != 0) || Y % 400 == 0;
+  if (M < 1 || M > 12 || D < 1 || D > kDays[M - 1] || (M == 2 && D == 29 && !leap) || h > 23 || m > 59 || sec > 59)
+    return false;
+  size_t i = 19;
+  int64_t frac = 0;
+  if (i < s.size() && s[i] == '.') {
+    size_t j = i + 1;
+    int64_t scale = 100000000;
+    while (j < s.size() && s[j] >= '0' && s[j] <= '9') {
+      frac += (s[j] - '0') * scale;
+      scale /= 10;
+      ++j;
+    }
+    if (j == i + 1) return false;
+    i = j;
+  }
+  int64_t offset = 0;
+  if (i < s.size() && (s[i] == 'Z' || s[i] == 'z')) {
+    ++i;
+  } else if (i < s.size() && (s[i] == '+' || s[i] == '-')) {
+    int oh, om;
+    if (!fixed_digits(s, i + 1, 2, &oh) || i + 3 >= s.size() || s[i + 3] != ':' || !fixed_digits(s, i + 4, 2, &om) ||
+        oh > 23 || om > 59)
+      return false;
+    offset = (oh * 3600 + om * 60) * (s[i] == '-' ? -1 : 1);
+    i += 6;
+  } else {
+    return false;
+  }
+  if (i != s.size()) return false;
+  const int64_t secs = days_from_civil(Y, static_cast<unsigned>(M), static_cast<unsigned>(D)) * 86400 +
+                       h * 3600 + m * 60 + sec - offset;
+  *unix_nanos = secs * 1000000000LL + frac;
+  return true;
+}
+
 std::string amz_date(int64_t unix_nanos) {
   time_t secs = static_cast<time_t>(unix_nanos / 1000000000LL);
   struct tm tm;

@@ -23,6 +23,8 @@ std::string go_quote(const std::string& s);
 
 // RFC3339 ("2006-01-02T15:04:05Z07:00") in UTC for the given unix time.
 std::string rfc3339_utc(int64_t unix_nanos);
+// time.Parse(time.RFC3339, s): "2006-01-02T15:04:05[.frac](Z|+07:00)". false on bad input.
+bool parse_rfc3339(const std::string& s, int64_t* unix_nanos);
 // ISO-8601 basic format used by SigV4: "20150830T123600Z" and its date part "20150830".
 std::string amz_date(int64_t unix_nanos);
 

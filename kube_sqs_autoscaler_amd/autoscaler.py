@@ -47,6 +47,89 @@ def kube_proxy(rc: RestConfig, environ: Optional[Mapping[str, str]] = None) -> s
     return proxy.select(rc.host, environ, rc.proxy_url)
 
 
+class KubeClientError(RuntimeError):
+    """``kubernetes.NewForConfig`` failed (the reference panics "Failed to configure client",
+    /root/reference/scale/scale.go:38-40)."""
+
+
+def exec_config(rc: RestConfig, timeout_ns: int = 0):
+    nat = native()
+    e = nat.ExecConfig()
+    p = rc.exec_plugin
+    e.command, e.args, e.env = p.command, list(p.args), list(p.env)
+    e.api_version, e.install_hint, e.timeout_ns = p.api_version, p.install_hint, timeout_ns
+    return e
+
+
+def token_provider(rc: RestConfig, clock=None, timeout_ns: int = 0):
+    """The bearer-token source for ``rc`` (None: no bearer auth).
+
+    A static ``token`` wins over everything (client-go skips the exec plugin when the config
+    already carries a token); a ``tokenFile`` / in-cluster SA token is re-read every 60 s; an
+    ``exec`` plugin is run natively and its credential cached until it expires or a 401 comes
+    back. The exec provider is shared by every client built from ``rc``, so N tracked queues
+    run the plugin once, not N times.
+    """
+    nat = native()
+    if rc.bearer_token_file:
+        return nat.FileTokenProvider(rc.bearer_token_file, clock or nat.RealClock(), 60 * SECOND)
+    if rc.bearer_token:
+        return nat.StaticTokenProvider(rc.bearer_token)
+    if rc.exec_plugin is not None:
+        p = rc.shared.get("exec")
+        if p is None:
+            p = rc.shared["exec"] = nat.ExecTokenProvider(exec_config(rc, timeout_ns), clock or nat.RealClock())
+        return p
+    return None
+
+
+def prepare_kube_auth(rc: RestConfig, clock=None, timeout_ns: int = 0) -> Optional[str]:
+    """Client construction checks (``kubernetes.NewForConfig``, scale.go:38).
+
+    Raises :class:`KubeClientError` for an ``auth-provider`` user (the reference links no
+    auth-provider plugins). For an ``exec`` plugin that hands out client certificates, runs it
+    once so the certificate is in the TLS config before the first connection; a plugin failure
+    here is returned as a warning and retried on the first request, where client-go would run
+    it.
+    """
+    if rc.auth_provider and not rc.bearer_token and not rc.bearer_token_file:
+        raise KubeClientError(f'no Auth Provider found for name "{rc.auth_provider}"')
+    if rc.exec_plugin is None or rc.bearer_token or rc.bearer_token_file or rc.cert_pem:
+        return None
+    p = token_provider(rc, clock, timeout_ns)
+    try:
+        cred = p.credential()
+    except native().NativeError as e:
+        return f"exec credential plugin: {e}"
+    if cred.cert_pem:
+        rc.cert_pem, rc.key_pem = cred.cert_pem, cred.key_pem
+    return None
+
+
+def auth_headers(rc: RestConfig) -> list:
+    """Authorization header for ad-hoc apiserver calls (Leases, Nodes), from the same sources
+    as the actuator's requests."""
+    p = token_provider(rc)
+    if p is not None:
+        t = p.token()
+        return [("Authorization", f"Bearer {t}")] if t else []
+    if rc.username:
+        import base64
+
+        return [("Authorization", "Basic " + base64.b64encode(f"{rc.username}:{rc.password}".encode()).decode())]
+    return []
+
+
+def note_status(rc: RestConfig, headers: list, status: int) -> None:
+    """A 401 on a bearer token drops it from the cache so the next call fetches a fresh one."""
+    if status != 401:
+        return
+    p = token_provider(rc)
+    for k, v in headers:
+        if p is not None and k == "Authorization" and v.startswith("Bearer "):
+            p.invalidate(v[7:])
+
+
 def new_http_client(rc: RestConfig, timeout_ns: int, environ: Optional[Mapping[str, str]] = None):
     """A native keep-alive client to the apiserver (leader election, node listing)."""
     c = native().HttpClient(rc.host, tls_options(rc), timeout_ns)
@@ -66,10 +149,9 @@ def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", time
     o.tls = tls_options(rc)
     o.timeout_ns = timeout_ns
     o.busy_poll_ns = busy_poll_ns
-    if rc.bearer_token_file:
-        o.token = nat.FileTokenProvider(rc.bearer_token_file, clock or nat.RealClock(), 60 * SECOND)
-    elif rc.bearer_token:
-        o.token = nat.StaticTokenProvider(rc.bearer_token)
+    tp = token_provider(rc, clock, timeout_ns)
+    if tp is not None:
+        o.token = tp
     o.basic_user = rc.username
     o.basic_password = rc.password
     return nat.KubeRestDeployments(o)

@@ -65,6 +65,12 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         return _panic("Failed to configure incluster or local config", str(e))
     for w in rest.warnings:
         log.log("warning", w)
+    try:
+        w = autoscaler.prepare_kube_auth(rest, clock, cfg.api_timeout_ns)
+    except autoscaler.KubeClientError as e:
+        return _panic("Failed to configure client", str(e))
+    if w:
+        log.log("warning", w)
 
     multi = len(cfg.targets) > 1
     workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]

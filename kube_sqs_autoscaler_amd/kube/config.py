@@ -10,11 +10,14 @@ Mirrors ``clientcmd.BuildConfigFromFlags("", os.Getenv("KUBE_CONFIG_PATH"))``
   reference's ``ExplicitPath`` loading rules): current-context -> cluster + user.
 
 Supported kubeconfig auth: bearer ``token`` / ``tokenFile``, client certificates (file or
-``-data``), basic auth; TLS via ``certificate-authority[-data]``, ``insecure-skip-tls-verify``,
-``tls-server-name``. ``exec`` / ``auth-provider`` plugins are out of scope and reported as
-errors. The reference turns any failure here into
+``-data``), basic auth, and ``exec`` credential plugins (``client.authentication.k8s.io``
+v1alpha1/v1beta1, e.g. ``aws eks get-token``; run natively by ``ExecTokenProvider``,
+``csrc/core/exec_auth.cc``); TLS via ``certificate-authority[-data]``,
+``insecure-skip-tls-verify``, ``tls-server-name``. The reference turns any failure here into
 ``panic("Failed to configure incluster or local config")`` (scale.go:35); the CLI keeps that
-text and exits non-zero.
+text and exits non-zero. An ``auth-provider`` user loads here but, as in the reference (which
+imports no ``client-go/plugin/pkg/client/auth`` provider), fails when the client is built:
+``panic("Failed to configure client")`` (scale.go:40).
 """
 from __future__ import annotations
 
@@ -46,8 +49,48 @@ class RestConfig:
     insecure: bool = False
     server_name: str = ""
     proxy_url: str = ""  # kubeconfig cluster proxy-url (client-go v0.19); "" = environment
+    exec_plugin: Optional["ExecPlugin"] = None
+    auth_provider: str = ""  # kubeconfig auth-provider name (unsupported, like the reference)
     source: str = ""
     warnings: list = field(default_factory=list)
+    # shared per-config state (the exec authenticator), like client-go's authenticator cache
+    shared: dict = field(default_factory=dict, repr=False, compare=False)
+
+
+EXEC_API_VERSIONS = ("client.authentication.k8s.io/v1alpha1", "client.authentication.k8s.io/v1beta1")
+
+
+@dataclass
+class ExecPlugin:
+    """A kubeconfig ``users[].user.exec`` stanza (client-go v0.19 ``api.ExecConfig``)."""
+
+    command: str
+    args: list = field(default_factory=list)
+    env: list = field(default_factory=list)  # [(name, value)], applied over the process env
+    api_version: str = ""
+    install_hint: str = ""
+
+
+def _exec_plugin(spec: dict, base_dir: str) -> ExecPlugin:
+    if not isinstance(spec, dict):
+        raise KubeConfigError("invalid configuration: exec must be a mapping")
+    cmd = str(spec.get("command") or "")
+    # clientcmd resolves a command with a path separator relative to the kubeconfig file;
+    # a bare name is looked up on PATH at run time.
+    if "/" in cmd and not os.path.isabs(cmd):
+        cmd = os.path.join(base_dir, cmd)
+    env = []
+    for e in spec.get("env") or []:
+        if not isinstance(e, dict) or "name" not in e:
+            raise KubeConfigError("invalid configuration: exec env entries need a name")
+        env.append((str(e["name"]), str(e.get("value", ""))))
+    p = ExecPlugin(command=cmd, args=[str(a) for a in spec.get("args") or []], env=env,
+                   api_version=str(spec.get("apiVersion") or ""), install_hint=str(spec.get("installHint") or ""))
+    if p.api_version not in EXEC_API_VERSIONS:
+        raise KubeConfigError(f'exec plugin: invalid apiVersion "{p.api_version}"')
+    if not p.command:
+        raise KubeConfigError("invalid configuration: exec plugin command must be specified")
+    return p
 
 
 def in_cluster_config(environ: Optional[Mapping[str, str]] = None, sa_dir: str = SA_DIR) -> RestConfig:
@@ -136,8 +179,12 @@ def load_kubeconfig(path: str, context: str = "") -> RestConfig:
         raise KubeConfigError(f"illegal base64 data in kubeconfig: {e}")
     rc.username = user.get("username", "")
     rc.password = user.get("password", "")
-    if user.get("exec") or user.get("auth-provider"):
-        raise KubeConfigError("exec and auth-provider credential plugins are not supported; use a token or client certificate")
+    if user.get("exec"):
+        rc.exec_plugin = _exec_plugin(user["exec"], base)
+    if user.get("auth-provider"):
+        if rc.exec_plugin is not None:
+            raise KubeConfigError("invalid configuration: authProvider cannot be provided in combination with an exec plugin")
+        rc.auth_provider = str((user["auth-provider"] or {}).get("name", ""))
     if bool(rc.cert_pem) != bool(rc.key_pem):
         raise KubeConfigError("invalid configuration: client-cert and client-key must be specified together")
     return rc

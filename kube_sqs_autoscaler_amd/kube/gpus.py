@@ -56,26 +56,22 @@ class ClusterGpuCapacity:
         self.http = new_http_client(rest, int(timeout_s * 1e9))
 
     def _headers(self):
-        h = [("Accept", "application/json")]
-        token = self.rest.bearer_token
-        if self.rest.bearer_token_file:
-            try:
-                with open(self.rest.bearer_token_file) as f:
-                    token = f.read().strip() or token
-            except OSError:
-                pass
-        if token:
-            h.append(("Authorization", f"Bearer {token}"))
-        return h
+        from ..autoscaler import auth_headers
+
+        return [("Accept", "application/json")] + auth_headers(self.rest)
 
     def allocatable_gpus(self) -> int:
         path = "/api/v1/nodes"
         if self.selector:
             path += "?labelSelector=" + urllib.parse.quote(self.selector, safe="=,!")
+        from ..autoscaler import note_status
+
         try:
-            status, _, body = self.http.request("GET", path, self._headers())
+            headers = self._headers()
+            status, _, body = self.http.request("GET", path, headers)
         except native().NativeError as e:
             raise CapacityError(f"list nodes: {e}")
+        note_status(self.rest, headers, status)
         if status != 200:
             raise CapacityError(f"list nodes: HTTP {status}: {body[:200]!r}")
         total = 0

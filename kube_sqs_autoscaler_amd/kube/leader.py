@@ -88,23 +88,11 @@ class LeaseLock:
         self.name = name
         self.http = new_http_client(rest, int(timeout_s * 1e9))
         self._rv = ""
-        self._token_file_mtime = 0.0
 
     def _headers(self, body: bool = False):
-        h = [("Accept", "application/json")]
-        token = self.rest.bearer_token
-        if self.rest.bearer_token_file:
-            try:  # projected SA tokens rotate
-                with open(self.rest.bearer_token_file) as f:
-                    token = f.read().strip() or token
-            except OSError:
-                pass
-        if token:
-            h.append(("Authorization", f"Bearer {token}"))
-        elif self.rest.username:
-            import base64
+        from ..autoscaler import auth_headers
 
-            h.append(("Authorization", "Basic " + base64.b64encode(f"{self.rest.username}:{self.rest.password}".encode()).decode()))
+        h = [("Accept", "application/json")] + auth_headers(self.rest)
         if body:
             h.append(("Content-Type", "application/json"))
         return h
@@ -115,11 +103,15 @@ class LeaseLock:
 
     def _call(self, method: str, path: str, body: Optional[dict] = None) -> Tuple[int, dict]:
         nat = native()
+        from ..autoscaler import note_status
+
         try:
-            status, _, raw = self.http.request(method, path, self._headers(body is not None),
+            headers = self._headers(body is not None)
+            status, _, raw = self.http.request(method, path, headers,
                                                json.dumps(body).encode() if body is not None else b"")
         except nat.NativeError as e:
             raise LeaseError(str(e))
+        note_status(self.rest, headers, status)
         try:
             return status, json.loads(raw) if raw else {}
         except ValueError:

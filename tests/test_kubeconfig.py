@@ -63,7 +63,7 @@ def test_kubeconfig_insecure_and_basic(tmp_path):
 
 
 @pytest.mark.parametrize("cluster,user,match", [
-    ({"server": "https://a"}, {"exec": {"command": "aws"}}, "not supported"),
+    ({"server": "https://a"}, {"exec": {"command": "aws"}}, "invalid apiVersion"),
     ({}, {"token": "t"}, "no server"),
     ({"server": "https://a"}, {"client-certificate-data": base64.b64encode(b"C").decode()}, "together"),
 ])
