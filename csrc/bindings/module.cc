@@ -438,6 +438,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def(py::init<SqsHttpOptions, std::shared_ptr<CredentialsProvider>, std::shared_ptr<Clock>>(),
            py::arg("options"), py::arg("credentials"), py::arg("clock"))
       .def_static("endpoint_for_region", &HttpSqsApi::endpoint_for_region)
+      .def_static("signing_region", &HttpSqsApi::signing_region)
       .def("endpoint", &HttpSqsApi::endpoint)
       .def("stats", [](HttpSqsApi& a) {
         auto s = a.stats();

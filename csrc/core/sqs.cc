@@ -26,11 +26,39 @@ std::string aws_request_failure(const std::string& code, const std::string& mess
 // ---------------------------------------------------------------------------------------
 // HttpSqsApi
 
+namespace {
+
+// aws-sdk-go v1.35 endpoints model: the partition is chosen by region pattern (aws-cn, aws-iso,
+// aws-iso-b, otherwise the commercial/GovCloud suffix) and "sqs" uses the default hostname
+// template "{service}.{region}.{dnsSuffix}". The "fips-<region>" pseudo-regions map to
+// "sqs-fips.<region>" and sign for <region> (their credentialScope).
+std::string dns_suffix(const std::string& region) {
+  if (region.rfind("cn-", 0) == 0) return "amazonaws.com.cn";
+  if (region.rfind("us-isob-", 0) == 0) return "sc2s.sgov.gov";
+  if (region.rfind("us-iso-", 0) == 0) return "c2s.ic.gov";
+  return "amazonaws.com";
+}
+
+bool fips_region(const std::string& region, std::string* base) {
+  if (region.rfind("fips-", 0) == 0 && region.size() > 5) {
+    *base = region.substr(5);
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+
 std::string HttpSqsApi::endpoint_for_region(const std::string& region) {
   if (region.empty()) return "";
-  std::string suffix = "amazonaws.com";
-  if (region.rfind("cn-", 0) == 0) suffix = "amazonaws.com.cn";
-  return "https://sqs." + region + "." + suffix;
+  std::string base;
+  if (fips_region(region, &base)) return "https://sqs-fips." + base + "." + dns_suffix(base);
+  return "https://sqs." + region + "." + dns_suffix(region);
+}
+
+std::string HttpSqsApi::signing_region(const std::string& region) {
+  std::string base;
+  return fips_region(region, &base) ? base : region;
 }
 
 HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider> creds,
@@ -38,7 +66,7 @@ HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider>
     : opts_(std::move(opts)),
       clock_(std::move(clock)),
       creds_(std::move(creds), 5LL * 60 * kSecond),
-      signer_(opts_.region, "sqs") {
+      signer_(signing_region(opts_.region), "sqs") {
   endpoint_ = opts_.endpoint.empty() ? endpoint_for_region(opts_.region) : opts_.endpoint;
   if (opts_.region.empty()) {
     // aws-sdk-go v1 validates the region before sending (request.ValidateEndpointHandler).

@@ -69,6 +69,7 @@ class HttpSqsApi final : public SqsApi {
   SqsApiStats stats() const;
   // Regional endpoint aws-sdk-go would resolve for `region` ("" if region is empty).
   static std::string endpoint_for_region(const std::string& region);
+  static std::string signing_region(const std::string& region);
   std::string endpoint() const { return endpoint_; }
 
  private:

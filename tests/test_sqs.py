@@ -85,3 +85,36 @@ def test_python_sqs_api_plugs_into_native_client(nat):
             return {"A": "2", "B": "3"}
 
     assert nat.SqsClient(Api(), "q", ["A", "B"]).num_messages() == 5
+
+
+@pytest.mark.parametrize("region,endpoint,signing", [
+    ("us-east-1", "https://sqs.us-east-1.amazonaws.com", "us-east-1"),
+    ("us-gov-west-1", "https://sqs.us-gov-west-1.amazonaws.com", "us-gov-west-1"),
+    ("cn-northwest-1", "https://sqs.cn-northwest-1.amazonaws.com.cn", "cn-northwest-1"),
+    ("us-iso-east-1", "https://sqs.us-iso-east-1.c2s.ic.gov", "us-iso-east-1"),
+    ("us-isob-east-1", "https://sqs.us-isob-east-1.sc2s.sgov.gov", "us-isob-east-1"),
+    ("fips-us-west-2", "https://sqs-fips.us-west-2.amazonaws.com", "us-west-2"),
+    ("", "", ""),
+])
+def test_endpoint_partitions(nat, region, endpoint, signing):
+    """aws-sdk-go v1 endpoint resolution for "sqs" (partition by region pattern; fips-<region>
+    pseudo-regions sign for <region>)."""
+    assert nat.HttpSqsApi.endpoint_for_region(region) == endpoint
+    assert nat.HttpSqsApi.signing_region(region) == signing
+
+
+def test_fips_region_signs_for_base_region(nat):
+    from kube_sqs_autoscaler_amd.autoscaler import new_sqs_api
+    from kube_sqs_autoscaler_amd.sqs.credentials import static_provider
+
+    s = nat.FakeSqsServer()
+    s.require_signature("AKID", "SECRET", "us-east-1")
+    s.start()
+    try:
+        api = new_sqs_api("fips-us-east-1", nat.RealClock(), endpoint=s.url, credentials=static_provider("AKID", "SECRET"))
+        url = s.url + "/1/q"
+        s.set_attributes(url, {n: "1" for n in DEFAULT})
+        assert nat.SqsClient(api, url, list(DEFAULT)).num_messages() == 3
+        assert s.signature_failures() == 0
+    finally:
+        s.stop()
