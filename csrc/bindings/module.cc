@@ -295,8 +295,10 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_format", [](Logger& l, const std::string& f) {
         if (f == "text") l.set_format(LogFormat::Text);
         else if (f == "json") l.set_format(LogFormat::Json);
+        else if (f == "text-color") l.set_format(LogFormat::TextColor);
         else throw py::value_error("log format must be text or json");
       })
+      .def("set_base_time", &Logger::set_base_time, py::arg("unix_ns"))
       .def("set_sink",
            [](Logger& l, py::object cb) {
              if (cb.is_none()) {

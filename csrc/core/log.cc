@@ -1,6 +1,7 @@
 #include "log.h"
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <unistd.h>
@@ -49,7 +50,11 @@ bool logrus_needs_quoting(const std::string& s) {
   return false;
 }
 
-Logger::Logger() : shared_(std::make_shared<Shared>()) {
+Logger::Logger()
+    : base_unix_ns_(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::system_clock::now().time_since_epoch())
+                        .count()),
+      shared_(std::make_shared<Shared>()) {
   shared_->sink = [](const std::string& line) {
     std::string l = line;
     l.push_back('\n');
@@ -109,6 +114,35 @@ std::string Logger::format(Level l, const std::string& msg, const Fields& fields
       out += json_quote(kv.second);
     }
     out.push_back('}');
+    return out;
+  }
+  if (format_ == LogFormat::TextColor) {
+    // logrus TextFormatter.printColored (non-FullTimestamp): colour by level, upper-case
+    // level truncated to 4 letters, [seconds since baseTimestamp], message %-44s.
+    int color = 36;  // info (and unknown): blue
+    if (l == Level::Debug || l == Level::Trace) color = 37;
+    else if (l == Level::Warn) color = 33;
+    else if (l == Level::Error || l == Level::Fatal || l == Level::Panic) color = 31;
+    std::string lvl = level_name(l);
+    for (auto& c : lvl) c = static_cast<char>(std::toupper(static_cast<unsigned char>(c)));
+    lvl = lvl.substr(0, 4);
+    std::string m = msg;
+    if (!m.empty() && m.back() == '\n') m.pop_back();
+    char head[64];
+    std::snprintf(head, sizeof head, "\x1b[%dm%s\x1b[0m[%04lld] ", color, lvl.c_str(),
+                  static_cast<long long>((unix_ns - base_unix_ns_) / 1000000000LL));
+    out = head;
+    out += m;
+    if (m.size() < 44) out.append(44 - m.size(), ' ');
+    out.push_back(' ');
+    for (auto& kv : data) {
+      char key[32];
+      std::snprintf(key, sizeof key, " \x1b[%dm", color);
+      out += key;
+      out += kv.first;
+      out += "\x1b[0m=";
+      out += logrus_needs_quoting(kv.second) ? go_quote(kv.second) : kv.second;
+    }
     return out;
   }
   auto append = [&](const std::string& k, const std::string& v) {

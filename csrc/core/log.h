@@ -6,8 +6,13 @@
 //   time="2024-01-01T00:00:00Z" level=info msg="Found 3 messages in the queue"
 // This formatter reproduces that layout (fixed keys time/level/msg, then the remaining
 // fields sorted by key, values quoted with Go %q only when they contain characters outside
-// [A-Za-z0-9-._/@^+]) so log-based parity diffs against the reference work. A JSON
-// formatter (logrus.JSONFormatter layout) is offered as an extension.
+// [A-Za-z0-9-._/@^+]) so log-based parity diffs against the reference work. On a TTY logrus
+// switches to its coloured layout, e.g.
+//   \x1b[36mINFO\x1b[0m[0005] Found 3 messages in the queue
+// (4-letter level, seconds since process start, message padded to 44 columns, fields as
+// " \x1b[36mkey\x1b[0m=value"); LogFormat::TextColor is that layout and the CLI picks it when
+// stderr is a terminal, as logrus does. A JSON formatter (logrus.JSONFormatter layout) is
+// offered as an extension.
 #pragma once
 
 #include <functional>
@@ -26,7 +31,7 @@ bool parse_level(const std::string& s, Level* out);
 
 using Fields = std::vector<std::pair<std::string, std::string>>;
 
-enum class LogFormat { Text, Json };
+enum class LogFormat { Text, Json, TextColor };
 
 class Logger {
  public:
@@ -39,6 +44,7 @@ class Logger {
   void set_level(Level l) { level_ = l; }
   Level level() const { return level_; }
   void set_format(LogFormat f) { format_ = f; }
+  void set_base_time(int64_t unix_ns) { base_unix_ns_ = unix_ns; }
   // Replaces the output (default: stderr). The sink receives the line without '\n'.
   void set_sink(Sink s);
   void set_time_source(TimeSource t);
@@ -57,6 +63,7 @@ class Logger {
   std::string format(Level l, const std::string& msg, const Fields& fields, int64_t unix_ns) const;
 
  private:
+  int64_t base_unix_ns_;  // logrus' baseTimestamp (package init) for the TTY layout
   struct Shared {
     std::mutex mu;
     Sink sink;

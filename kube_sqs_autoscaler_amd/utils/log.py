@@ -10,6 +10,7 @@ Python and poll lines written from the C++ workers share one formatter and one s
 """
 from __future__ import annotations
 
+import os
 import sys
 from typing import Optional
 
@@ -23,13 +24,15 @@ def make_logger(level: str = "info", fmt: str = "text", fd: Optional[int] = None
     log = nat.Logger()
     log.set_level(level)
     log.set_format(fmt)
-    if fd is not None:
-        log.set_sink_fd(fd)
-    else:
+    if fd is None:
         try:
-            log.set_sink_fd(sys.stderr.fileno())
+            fd = sys.stderr.fileno()
         except (AttributeError, ValueError, OSError):  # stderr replaced (pytest capture)
             log.set_sink(lambda line: sys.stderr.write(line + "\n"))
+    if fd is not None:
+        log.set_sink_fd(fd)
+        if fmt == "text" and os.isatty(fd):
+            log.set_format("text-color")  # logrus TextFormatter on a terminal
     if clock is not None:
         log.set_time_source(clock)
     return log

@@ -66,3 +66,38 @@ def test_loop_log_catalogue(nat):
     assert 'level=error msg="Failed to get SQS messages: Failed to get messages in SQS: injected SQS failure"' in text
     assert "Failed scaling up: Failed to get deployment from kube server, no scale up occurred: injected GET failure" in text
     assert "Failed scaling up: Failed to scale up: injected PUT failure" in text
+
+
+def test_tty_colored_layout_matches_logrus(nat):
+    """logrus TextFormatter.printColored (the layout on a terminal): coloured 4-letter level,
+    [seconds since start], message padded to 44 columns, coloured field keys."""
+    log = nat.Logger()
+    log.set_format("text-color")
+    base = 1_700_000_000 * 10**9
+    log.set_base_time(base)
+    line = log.format("info", "Starting kube-sqs-autoscaler", [], base + 5 * 10**9 + 1)
+    assert line == "\x1b[36mINFO\x1b[0m[0005] Starting kube-sqs-autoscaler" + " " * 16 + " "
+    assert log.format("warning", "w", [], base).startswith("\x1b[33mWARN\x1b[0m[0000] w")
+    assert log.format("error", "Failed scaling up: x", [], base).startswith("\x1b[31mERRO\x1b[0m[0000] ")
+    assert log.format("debug", "d", [], base).startswith("\x1b[37mDEBU\x1b[0m")
+    long = "m" * 50
+    with_fields = log.format("info", long, [("queue", "a b"), ("deployment", "w")], base + 12 * 10**9)
+    assert with_fields == f"\x1b[36mINFO\x1b[0m[0012] {long}  \x1b[36mdeployment\x1b[0m=w \x1b[36mqueue\x1b[0m=\"a b\""
+
+
+def test_make_logger_picks_colors_on_a_tty(nat):
+    import os
+    import pty
+
+    from kube_sqs_autoscaler_amd.utils.log import make_logger
+
+    master, slave = pty.openpty()
+    r, w = os.pipe()
+    try:
+        make_logger(fd=slave).log("info", "on a tty")
+        make_logger(fd=w).log("info", "on a pipe")
+        assert b"\x1b[36mINFO\x1b[0m" in os.read(master, 4096)
+        assert os.read(r, 4096).startswith(b"time=")
+    finally:
+        for fd in (master, slave, r, w):
+            os.close(fd)
