@@ -1,5 +1,5 @@
 # Mirrors the reference Makefile targets (test / compile / build / push) for this build.
-.PHONY: test test-gpu compile native sanitize ci bench build push clean
+.PHONY: test test-gpu compile native sanitize fuzz ci bench build push clean
 
 IMAGE ?= kube-sqs-autoscaler-amd
 VERSION ?= v0.1.0
@@ -17,6 +17,10 @@ compile native:  ## native runtime + gfx950 probe, in-tree
 sanitize:        ## host C++ unit tests under ASan/UBSan and TSan
 	$(PY) -m kube_sqs_autoscaler_amd.ops.build --no-hip --sanitizers
 	./build/native_tests && ./build/native_tests_asan && ./build/native_tests_tsan
+
+fuzz:            ## libFuzzer + ASan/UBSan over the wire parsers (10 minutes)
+	$(PY) -m kube_sqs_autoscaler_amd.ops.build --no-hip --fuzz
+	mkdir -p build/fuzz_corpus && ./build/fuzz_wire -max_total_time=600 -timeout=10 build/fuzz_corpus csrc/tests/fuzz_corpus
 
 ci:              ## what CI runs (no network, no package installs)
 	bash scripts/ci.sh

@@ -1,5 +1,6 @@
 #include "goutil.h"
 
+#include <cstdint>
 #include <cstdio>
 #include <ctime>
 
@@ -217,7 +218,16 @@ bool parse_rfc3339(const std::string& s, int64_t* unix_nanos) {
   if (i != s.size()) return false;
   const int64_t secs = days_from_civil(Y, static_cast<unsigned>(M), static_cast<unsigned>(D)) * 86400 +
                        h * 3600 + m * 60 + sec - offset;
-  *unix_nanos = secs * 1000000000LL + frac;
+  // int64 nanoseconds span 1677..2262; Go's time.Time reaches further. Saturate, which keeps
+  // every comparison with a representable instant (an expiry in 3000 simply never passes).
+  constexpr int64_t kMaxSecs = INT64_MAX / 1000000000LL - 1;
+  if (secs > kMaxSecs) {
+    *unix_nanos = INT64_MAX;
+  } else if (secs < -kMaxSecs) {
+    *unix_nanos = INT64_MIN;
+  } else {
+    *unix_nanos = secs * 1000000000LL + frac;
+  }
   return true;
 }
 

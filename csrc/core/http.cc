@@ -977,9 +977,26 @@ void HttpServer::accept_loop() {
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     accepted_++;
-    std::lock_guard<std::mutex> lk(mu_);
-    open_fds_.push_back(fd);
-    workers_.emplace_back([this, fd] { serve(fd); });
+    std::vector<std::thread> finished;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto it = workers_.begin(); it != workers_.end();) {
+        if (it->done->load(std::memory_order_acquire)) {
+          finished.push_back(std::move(it->thread));
+          it = workers_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      open_fds_.push_back(fd);
+      auto done = std::make_shared<std::atomic<bool>>(false);
+      workers_.push_back(Worker{std::thread([this, fd, done] {
+                                  serve(fd);
+                                  done->store(true, std::memory_order_release);
+                                }),
+                                done});
+    }
+    for (auto& t : finished) t.join();  // already returned (or about to): no blocking
   }
 }
 
@@ -1062,14 +1079,14 @@ void HttpServer::stop() {
     ::close(listen_fd_);
     listen_fd_ = -1;
   }
-  std::vector<std::thread> ws;
+  std::vector<Worker> ws;
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (int fd : open_fds_) ::shutdown(fd, SHUT_RDWR);
     ws.swap(workers_);
   }
-  for (auto& t : ws)
-    if (t.joinable()) t.join();
+  for (auto& w : ws)
+    if (w.thread.joinable()) w.thread.join();
 }
 
 // ---------------------------------------------------------------------------------------

@@ -177,7 +177,13 @@ class HttpServer {
   std::thread acceptor_;
   std::mutex mu_;
   std::vector<int> open_fds_;
-  std::vector<std::thread> workers_;
+  // Connection threads; finished ones are joined on the next accept, so a long-lived fake
+  // serving many short connections does not accumulate dead threads (and their stacks).
+  struct Worker {
+    std::thread thread;
+    std::shared_ptr<std::atomic<bool>> done;
+  };
+  std::vector<Worker> workers_;
   std::atomic<uint64_t> served_{0};
   std::atomic<uint64_t> accepted_{0};
 };

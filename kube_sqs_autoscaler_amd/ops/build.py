@@ -8,11 +8,13 @@ Artifacts (git-ignored, but they travel to the GPU box with the gpurun snapshot)
 * ``kube_sqs_autoscaler_amd/ops/libksa_gpu.so`` -- ``hipcc --offload-arch=gfx950`` build of
   ``csrc/hip/gpu_probe.hip`` (GPU inventory + HBM health check), loaded with ctypes.
 * ``build/native_tests[_asan|_tsan]`` -- host-only C++ test binaries (sanitizer builds).
+* ``build/fuzz_wire`` -- libFuzzer + ASan/UBSan harness over every wire/plugin parser
+  (``csrc/tests/fuzz_wire.cc``), built with ROCm's clang.
 
 Objects are compiled in parallel and reused when neither the source nor any header under
 ``csrc/`` changed, so an incremental rebuild after touching one file takes seconds.
 
-Usage: ``python -m kube_sqs_autoscaler_amd.ops.build [--no-hip] [--sanitizers]``
+Usage: ``python -m kube_sqs_autoscaler_amd.ops.build [--no-hip] [--sanitizers] [--fuzz]``
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ NATIVE_SO = OPS / f"_ksa_native{EXT_SUFFIX}"
 GPU_SO = OPS / "libksa_gpu.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
+CLANGXX = os.environ.get("FUZZ_CXX", "/opt/rocm/llvm/bin/clang++")
 GPU_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 CXXFLAGS = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread"]
@@ -62,7 +65,7 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"command failed ({proc.returncode}): {' '.join(cmd)}\n{proc.stdout}{proc.stderr}")
 
 
-def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: int) -> list[Path]:
+def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: int, cxx: str = "") -> list[Path]:
     objdir = BUILD / f"obj-{variant}"
     objdir.mkdir(parents=True, exist_ok=True)
     hm = _newest_header()
@@ -71,7 +74,7 @@ def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: 
         obj = objdir / (src.stem + ".o")
         objs.append(obj)
         if _stale(obj, [src], hm):
-            todo.append([CXX, *CXXFLAGS, *extra, "-c", str(src), "-o", str(obj)])
+            todo.append([cxx or CXX, *CXXFLAGS, *extra, "-c", str(src), "-o", str(obj)])
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
             for f in [ex.submit(_run, c) for c in todo]:
@@ -147,6 +150,25 @@ def build_native_tests(sanitizer: str | None = None, jobs: int = 8) -> Path:
     return out
 
 
+# Globals are left uninstrumented: ROCm clang registers some merged string literals twice under
+# -O1 -g and aborts on a false ODR violation that ASAN_OPTIONS cannot switch off.
+FUZZ_FLAGS = ["-g", "-O1", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+              "-mllvm", "-asan-globals=0"]
+
+
+def build_fuzzer(jobs: int = 8) -> Path:
+    """libFuzzer harness over the wire parsers (needs a clang with libFuzzer: ROCm's has it)."""
+    if not Path(CLANGXX).exists() and shutil.which(CLANGXX) is None:
+        raise RuntimeError(f"{CLANGXX} not found; cannot build the fuzzer")
+    # the fakes and the loop are not wire parsers (and fakes.cc trips a clang ODR false positive)
+    srcs = [p for p in _core_sources() if p.stem not in ("fakes", "runner", "sweep")] + [CSRC / "tests" / "fuzz_wire.cc"]
+    objs = _compile_objects("fuzz", FUZZ_FLAGS + ["-fsanitize=fuzzer-no-link"], srcs, jobs, cxx=CLANGXX)
+    out = BUILD / "fuzz_wire"
+    if _stale(out, objs, 0.0):
+        _run([CLANGXX, *FUZZ_FLAGS, "-fsanitize=fuzzer", "-o", str(out), *map(str, objs), *LIBS])
+    return out
+
+
 def build_all(hip: bool = True, jobs: int = 8) -> dict:
     out = {"native": str(build_native(jobs=jobs))}
     if hip:
@@ -159,12 +181,15 @@ def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--no-hip", action="store_true", help="skip the gfx950 probe")
     ap.add_argument("--sanitizers", action="store_true", help="also build ASan/UBSan and TSan test binaries")
+    ap.add_argument("--fuzz", action="store_true", help="also build the libFuzzer wire-parser harness")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     args = ap.parse_args(argv)
     print(build_all(hip=not args.no_hip, jobs=args.jobs))
     if args.sanitizers:
         for s in (None, "asan", "tsan"):
             print(build_native_tests(s, jobs=args.jobs))
+    if args.fuzz:
+        print(build_fuzzer(jobs=args.jobs))
     return 0
 
 
