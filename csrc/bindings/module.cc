@@ -554,6 +554,7 @@ PYBIND11_MODULE(_ksa_native, m) {
              return unwrap(r);
            })
       .def_property_readonly("runs", &ExecTokenProvider::runs);
+  m.def("aws_dns_suffix", &aws_dns_suffix);
   m.def("parse_rfc3339", [](const std::string& s) -> py::object {
     int64_t ns;
     if (!parse_rfc3339(s, &ns)) return py::none();

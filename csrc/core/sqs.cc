@@ -26,18 +26,18 @@ std::string aws_request_failure(const std::string& code, const std::string& mess
 // ---------------------------------------------------------------------------------------
 // HttpSqsApi
 
-namespace {
-
 // aws-sdk-go v1.35 endpoints model: the partition is chosen by region pattern (aws-cn, aws-iso,
 // aws-iso-b, otherwise the commercial/GovCloud suffix) and "sqs" uses the default hostname
 // template "{service}.{region}.{dnsSuffix}". The "fips-<region>" pseudo-regions map to
 // "sqs-fips.<region>" and sign for <region> (their credentialScope).
-std::string dns_suffix(const std::string& region) {
+std::string aws_dns_suffix(const std::string& region) {
   if (region.rfind("cn-", 0) == 0) return "amazonaws.com.cn";
   if (region.rfind("us-isob-", 0) == 0) return "sc2s.sgov.gov";
   if (region.rfind("us-iso-", 0) == 0) return "c2s.ic.gov";
   return "amazonaws.com";
 }
+
+namespace {
 
 bool fips_region(const std::string& region, std::string* base) {
   if (region.rfind("fips-", 0) == 0 && region.size() > 5) {
@@ -52,8 +52,8 @@ bool fips_region(const std::string& region, std::string* base) {
 std::string HttpSqsApi::endpoint_for_region(const std::string& region) {
   if (region.empty()) return "";
   std::string base;
-  if (fips_region(region, &base)) return "https://sqs-fips." + base + "." + dns_suffix(base);
-  return "https://sqs." + region + "." + dns_suffix(region);
+  if (fips_region(region, &base)) return "https://sqs-fips." + base + "." + aws_dns_suffix(base);
+  return "https://sqs." + region + "." + aws_dns_suffix(region);
 }
 
 std::string HttpSqsApi::signing_region(const std::string& region) {

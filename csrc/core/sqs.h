@@ -30,6 +30,10 @@ using AttrMap = std::map<std::string, std::string>;
 // sqs.go:26-33
 const std::vector<std::string>& default_attribute_names();
 
+// DNS suffix of the AWS partition `region` belongs to (aws-sdk-go v1 endpoints model):
+// amazonaws.com, amazonaws.com.cn, c2s.ic.gov or sc2s.sgov.gov.
+std::string aws_dns_suffix(const std::string& region);
+
 class SqsApi {
  public:
   virtual ~SqsApi() = default;

@@ -171,6 +171,52 @@ def process_credentials(command: str, timeout: float = 60.0):
                  "ProcessProvider")
 
 
+# aws-sdk-go v1 endpoints/legacy_regions.go: under the default ("legacy") STS endpoint setting
+# these regions resolve STS to the global endpoint sts.amazonaws.com (signed for us-east-1);
+# AWS_STS_REGIONAL_ENDPOINTS=regional (or sts_regional_endpoints in the shared config) sends
+# them to sts.<region>.<partition suffix> like every other region.
+LEGACY_GLOBAL_STS_REGIONS = frozenset({
+    "ap-northeast-1", "ap-south-1", "ap-southeast-1", "ap-southeast-2", "ca-central-1", "eu-central-1",
+    "eu-north-1", "eu-west-1", "eu-west-2", "eu-west-3", "sa-east-1", "us-east-1", "us-east-2", "us-west-1",
+    "us-west-2"})
+
+
+def session_region(environ: Mapping[str, str], fallback: str = "") -> str:
+    """The region ``session.NewSession()`` resolves for its own clients (STS): ``AWS_REGION``;
+    with ``AWS_SDK_LOAD_CONFIG`` also ``AWS_DEFAULT_REGION`` and the profile's ``region``.
+
+    The reference applies ``--aws-region`` to the SQS client only (sqs/sqs.go:36), so STS never
+    sees it; here it is the fallback when the session has no region (where aws-sdk-go would
+    use the global endpoint, which the legacy rule below picks for most regions anyway).
+    """
+    r = environ.get("AWS_REGION", "")
+    if not r and _truthy(environ.get("AWS_SDK_LOAD_CONFIG")):
+        r = environ.get("AWS_DEFAULT_REGION", "")
+        if not r:
+            try:
+                prof = environ.get("AWS_PROFILE") or environ.get("AWS_DEFAULT_PROFILE") or "default"
+                r = (load_profiles(environ).get(prof) or {}).get("region", "")
+            except CredentialsError:
+                r = ""
+    return r or fallback
+
+
+def resolve_sts_endpoint(region: str, environ: Mapping[str, str]) -> Tuple[str, str]:
+    """(endpoint URL, signing region) for STS as aws-sdk-go v1.35 resolves it."""
+    if environ.get("AWS_STS_ENDPOINT"):  # extension: VPC endpoint / test double
+        return environ["AWS_STS_ENDPOINT"].rstrip("/"), region or "us-east-1"
+    mode = environ.get("AWS_STS_REGIONAL_ENDPOINTS", "").lower()
+    if not mode and _truthy(environ.get("AWS_SDK_LOAD_CONFIG")):
+        try:
+            prof = environ.get("AWS_PROFILE") or environ.get("AWS_DEFAULT_PROFILE") or "default"
+            mode = (load_profiles(environ).get(prof) or {}).get("sts_regional_endpoints", "").lower()
+        except CredentialsError:
+            mode = ""
+    if not region or (mode != "regional" and region in LEGACY_GLOBAL_STS_REGIONS):
+        return "https://sts.amazonaws.com", "us-east-1"
+    return f"https://sts.{region}.{native().aws_dns_suffix(region)}", region
+
+
 class WebIdentityProvider(_Provider):
     """STS AssumeRoleWithWebIdentity (unsigned Query call), the IRSA path on EKS."""
 
@@ -182,8 +228,7 @@ class WebIdentityProvider(_Provider):
         self.session_name = environ.get("AWS_ROLE_SESSION_NAME", "")
         self.region = region
         self.http = fetch
-        self.endpoint = sts_endpoint or environ.get("AWS_STS_ENDPOINT", "") or (
-            f"https://sts.{region}.amazonaws.com" if region else "https://sts.amazonaws.com")
+        self.endpoint = sts_endpoint or resolve_sts_endpoint(session_region(environ, region), environ)[0]
 
     def available(self) -> bool:
         return bool(self.token_file)
@@ -323,7 +368,7 @@ class AssumeRoleProvider(_Provider):
         self.profile = environ.get("AWS_PROFILE") or environ.get("AWS_DEFAULT_PROFILE") or "default"
         self.region = region
         self.http = fetch
-        self.sts_endpoint = sts_endpoint or environ.get("AWS_STS_ENDPOINT", "")
+        self.sts_endpoint = sts_endpoint
 
     def _section(self) -> Optional[Dict[str, str]]:
         try:
@@ -364,8 +409,10 @@ class AssumeRoleProvider(_Provider):
         nat = native()
         sec = self._section() or {}
         src = self._source(sec)
-        region = self.region or sec.get("region", "") or "us-east-1"
-        endpoint = self.sts_endpoint or (f"https://sts.{region}.amazonaws.com" if self.region else "https://sts.amazonaws.com")
+        if self.sts_endpoint:
+            endpoint, region = self.sts_endpoint, self.region or "us-east-1"
+        else:
+            endpoint, region = resolve_sts_endpoint(session_region(self.env, self.region), self.env)
         params = {"Action": "AssumeRole", "RoleArn": sec["role_arn"], "Version": "2011-06-15",
                   "RoleSessionName": sec.get("role_session_name") or f"{int(datetime.now(timezone.utc).timestamp() * 1e9)}"}
         if sec.get("external_id"):
@@ -375,7 +422,7 @@ class AssumeRoleProvider(_Provider):
         body = "&".join(f"{nat.aws_uri_encode(k, False)}={nat.aws_uri_encode(v, False)}" for k, v in sorted(params.items()))
         host = urllib.parse.urlsplit(endpoint).netloc
         headers = [("Host", host), ("Content-Type", "application/x-www-form-urlencoded; charset=utf-8")]
-        signer = nat.SigV4Signer(region if self.region or self.sts_endpoint else "us-east-1", "sts")
+        signer = nat.SigV4Signer(region, "sts")
         signed, _ = signer.sign(src, int(datetime.now(timezone.utc).timestamp() * 1e9), "POST", "/", "", headers, body.encode())
         status, resp = self.http("POST", endpoint + "/", {k: v for k, v in signed if k != "Host"}, body.encode(), 10.0)
         text = resp.decode(errors="replace")

@@ -64,7 +64,8 @@ def test_web_identity(tmp_path, nat):
     env = {"AWS_WEB_IDENTITY_TOKEN_FILE": str(tok), "AWS_ROLE_ARN": "arn:aws:iam::1:role/r", "AWS_ROLE_SESSION_NAME": "s"}
     c = chain(env, fetch, region="us-west-2").retrieve()
     assert (c.access_key_id, c.secret_access_key, c.session_token) == ("ASIAWEB", "WS", "WT")
-    assert seen["url"] == "https://sts.us-west-2.amazonaws.com/" and "Action=AssumeRoleWithWebIdentity" in seen["body"]
+    # us-west-2 is a legacy-global STS region in aws-sdk-go v1: the default resolves to sts.amazonaws.com
+    assert seen["url"] == "https://sts.amazonaws.com/" and "Action=AssumeRoleWithWebIdentity" in seen["body"]
     assert "WebIdentityToken=jwt-token" in seen["body"] and "RoleArn=arn%3Aaws%3Aiam%3A%3A1%3Arole%2Fr" in seen["body"]
 
 
@@ -163,10 +164,14 @@ def test_assume_role_from_shared_config(tmp_path, nat):
            "AWS_SDK_LOAD_CONFIG": "1", "AWS_PROFILE": "deploy"}
     c = chain(env, fetch, region="eu-west-1").retrieve()
     assert (c.access_key_id, c.session_token, c.provider_name) == ("ASIAROLE", "RT", "AssumeRoleProvider")
-    assert seen["url"] == "https://sts.eu-west-1.amazonaws.com/"
+    assert seen["url"] == "https://sts.amazonaws.com/"  # legacy-global region, default setting
     assert "Action=AssumeRole" in seen["body"] and "ExternalId=ext-1" in seen["body"] and "RoleSessionName=ksa-session" in seen["body"]
     auth = seen["headers"]["Authorization"]
-    assert auth.startswith("AWS4-HMAC-SHA256 Credential=AKIDBASE/") and "/eu-west-1/sts/aws4_request" in auth
+    assert auth.startswith("AWS4-HMAC-SHA256 Credential=AKIDBASE/") and "/us-east-1/sts/aws4_request" in auth
+    seen.clear()
+    chain({**env, "AWS_STS_REGIONAL_ENDPOINTS": "regional"}, fetch, region="eu-west-1").retrieve()
+    assert seen["url"] == "https://sts.eu-west-1.amazonaws.com/"
+    assert "/eu-west-1/sts/aws4_request" in seen["headers"]["Authorization"]
 
 
 def test_assume_role_needs_sdk_load_config(tmp_path, nat):
@@ -184,3 +189,28 @@ def test_assume_role_error(tmp_path, nat):
     env = {"AWS_SHARED_CREDENTIALS_FILE": str(tmp_path / "credentials"), "AWS_PROFILE": "deploy"}
     with pytest.raises(Exception, match="AccessDenied: not allowed"):
         chain(env, fetch).retrieve()
+
+
+@pytest.mark.parametrize("env,flag,want", [
+    ({}, "us-west-2", ("https://sts.amazonaws.com", "us-east-1")),           # legacy-global region
+    ({}, "ap-east-1", ("https://sts.ap-east-1.amazonaws.com", "ap-east-1")),  # not in the legacy list
+    ({}, "", ("https://sts.amazonaws.com", "us-east-1")),                     # no region: global
+    ({"AWS_STS_REGIONAL_ENDPOINTS": "regional"}, "us-west-2", ("https://sts.us-west-2.amazonaws.com", "us-west-2")),
+    ({"AWS_REGION": "eu-central-1", "AWS_STS_REGIONAL_ENDPOINTS": "regional"}, "us-west-2",
+     ("https://sts.eu-central-1.amazonaws.com", "eu-central-1")),           # the session region wins over the flag
+    ({"AWS_DEFAULT_REGION": "ap-east-1"}, "", ("https://sts.amazonaws.com", "us-east-1")),  # only with LOAD_CONFIG
+    ({"AWS_DEFAULT_REGION": "ap-east-1", "AWS_SDK_LOAD_CONFIG": "1"}, "", ("https://sts.ap-east-1.amazonaws.com", "ap-east-1")),
+    ({}, "cn-north-1", ("https://sts.cn-north-1.amazonaws.com.cn", "cn-north-1")),
+    ({}, "us-gov-west-1", ("https://sts.us-gov-west-1.amazonaws.com", "us-gov-west-1")),
+    ({"AWS_STS_ENDPOINT": "https://vpce-1.sts.example/"}, "eu-west-1", ("https://vpce-1.sts.example", "eu-west-1")),
+])
+def test_sts_endpoint_resolution(nat, env, flag, want):
+    """aws-sdk-go v1.35 STS endpoint rules (endpoints/legacy_regions.go, AWS_STS_REGIONAL_ENDPOINTS)."""
+    assert cr.resolve_sts_endpoint(cr.session_region(env, flag), env) == want
+
+
+def test_sts_regional_endpoints_from_shared_config(tmp_path, nat):
+    (tmp_path / "config").write_text("[default]\nsts_regional_endpoints = regional\nregion = eu-west-2\n")
+    env = {"AWS_CONFIG_FILE": str(tmp_path / "config"), "AWS_SHARED_CREDENTIALS_FILE": str(tmp_path / "none"),
+           "AWS_SDK_LOAD_CONFIG": "true"}
+    assert cr.resolve_sts_endpoint(cr.session_region(env, "us-east-1"), env) == ("https://sts.eu-west-2.amazonaws.com", "eu-west-2")
