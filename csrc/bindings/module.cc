@@ -735,6 +735,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["latency_samples"] = s.latency_samples;
         return d;
       })
+      .def("idle_ns", &Runner::idle_ns)
       .def("set_trace_fd", &Runner::set_trace_fd)
       .def("latencies", &Runner::latencies)
       .def("clear_latencies", &Runner::clear_latencies)

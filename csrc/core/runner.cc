@@ -42,11 +42,13 @@ Runner::Runner(LoopConfig cfg, std::shared_ptr<SqsClient> sqs, std::shared_ptr<P
       clock_(std::move(clock)),
       log_(std::move(log)) {
   lat_ring_.reserve(1024);
+  progress_ns_.store(clock_->now(), std::memory_order_release);
 }
 
 void Runner::arm() {
   last_up_ = clock_->now();
   last_down_ = clock_->now();
+  progress_ns_.store(clock_->now(), std::memory_order_release);
 }
 
 IterationRecord Runner::step(StopFlag* stop) {
@@ -148,6 +150,7 @@ IterationRecord Runner::poll_once() {
 }
 
 void Runner::record(const IterationRecord& r) {
+  progress_ns_.store(clock_->now(), std::memory_order_release);
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.polls++;

@@ -103,6 +103,9 @@ class Runner {
   void run(StopFlag* stop, int64_t max_iterations = -1);
 
   RunnerStats stats() const;
+  // Time since the loop last made progress (armed, or finished a poll) -- the liveness signal:
+  // a worker wedged inside a call, or whose thread died, stops resetting it.
+  Nanos idle_ns() const { return clock_->now() - progress_ns_.load(std::memory_order_acquire); }
   // Recent poll->patch latencies (ns), oldest first; bounded ring.
   std::vector<Nanos> latencies() const;
   void clear_latencies();
@@ -132,6 +135,7 @@ class Runner {
   void write_trace(const IterationRecord& r);
 
   mutable std::mutex mu_;
+  std::atomic<Nanos> progress_ns_{0};
   RunnerStats stats_;
   std::vector<Nanos> lat_ring_;
   size_t lat_pos_ = 0;

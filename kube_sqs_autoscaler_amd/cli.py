@@ -102,10 +102,13 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
     fleet = Fleet(workers, cfg.worker_threads)
     metrics = None
+    health = None
     if cfg.metrics_addr:
-        from .metrics import MetricsServer
+        from .metrics import Health, MetricsServer
 
-        metrics = MetricsServer(fleet, cfg.metrics_addr)
+        health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets],
+                        leader_elect=cfg.leader_elect)
+        metrics = MetricsServer(fleet, cfg.metrics_addr, health)
         metrics.start()
         log.log("info", f"Serving metrics on {cfg.metrics_addr}")
 
@@ -145,6 +148,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
             renewer = threading.Thread(target=elector.renew_loop, args=(renew_stop, on_lost), name="ksa-lease", daemon=True)
             renewer.start()
+            if health is not None:
+                health.set_role("leader")
 
         log.log("info", "Starting kube-sqs-autoscaler")  # main.go:114
         fleet.start(max_iterations)

@@ -4,14 +4,14 @@ Pull model: nothing runs per poll on the Python side. On each scrape the collect
 native per-worker counters (``Runner.stats()``) and the latency ring (``Runner.latencies()``),
 so the control loop never takes the GIL for observability.
 
-Endpoints on ``--metrics-addr``: ``/metrics`` (Prometheus text format), ``/healthz`` (process
-alive and workers not stopped), ``/readyz`` (every worker completed at least one poll).
+Endpoints on ``--metrics-addr``: ``/metrics`` (Prometheus text format), ``/healthz`` and
+``/readyz`` (see :class:`Health`).
 """
 from __future__ import annotations
 
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 from prometheus_client import CollectorRegistry, generate_latest
 from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, SummaryMetricFamily
@@ -83,29 +83,76 @@ class FleetCollector:
         yield lat
 
 
+class Health:
+    """Liveness and readiness of the process.
+
+    * ``/healthz`` fails when the fleet is stopping, or when a running worker has made no
+      progress for longer than its budget: ``poll period + 8 x api timeout + 60 s``. The
+      budget covers an SQS call with 3 SDK retries, the GET, the write, and a 409 re-read, each
+      bounded by ``--api-timeout``. A worker stuck past all of them is wedged, and a restart
+      (Kubernetes' liveness probe) is the recovery. The reference has no probes and hangs on a
+      stalled call.
+    * ``/readyz`` is OK for a standby replica under ``--leader-elect``, since waiting for the
+      lease is its healthy state. Otherwise it is OK once every worker has completed a poll.
+      A standby that never became ready would stall every rolling update of a 2-replica
+      Deployment.
+    """
+
+    def __init__(self, fleet: Fleet, stale_after_ns: Optional[Sequence[int]] = None, leader_elect: bool = False) -> None:
+        self.fleet = fleet
+        self.stale_after_ns = list(stale_after_ns) if stale_after_ns is not None else None
+        self.role = "standby" if leader_elect else "active"
+
+    @staticmethod
+    def budget_ns(poll_period_ns: int, api_timeout_ns: int) -> int:
+        return poll_period_ns + 8 * api_timeout_ns + 60 * 10**9
+
+    def set_role(self, role: str) -> None:
+        self.role = role
+
+    def live(self) -> Tuple[bool, str]:
+        if self.fleet.stopped:
+            return False, "stopping"
+        if self.role == "standby" or not self.fleet.started or self.stale_after_ns is None:
+            return True, "ok"
+        for w, limit in zip(self.fleet.workers, self.stale_after_ns):
+            idle = w.runner.idle_ns()
+            if idle > limit:
+                return False, f"worker {w.target.name} made no progress for {idle / 1e9:.0f}s (budget {limit / 1e9:.0f}s)"
+        return True, "ok"
+
+    def ready(self) -> Tuple[bool, str]:
+        if self.role == "standby" and not self.fleet.stopped:
+            return True, "standby"
+        ok, why = self.live()
+        if not ok:
+            return False, why
+        if not all(s["polls"] > 0 for s in self.fleet.stats()):
+            return False, "waiting for first poll"
+        return True, "ok"
+
+
 def parse_addr(addr: str) -> Tuple[str, int]:
     host, _, port = addr.rpartition(":")
     return (host or "0.0.0.0"), int(port)
 
 
 class MetricsServer:
-    def __init__(self, fleet: Fleet, addr: str) -> None:
+    def __init__(self, fleet: Fleet, addr: str, health: Optional[Health] = None) -> None:
         self.fleet = fleet
+        self.health = health or Health(fleet)
+        hl = self.health
         self.registry = CollectorRegistry()
         self.registry.register(FleetCollector(fleet))
         reg = self.registry
-        fl = fleet
 
         class Handler(BaseHTTPRequestHandler):
             def do_GET(self):  # noqa: N802
                 if self.path == "/metrics":
                     body, code, ctype = generate_latest(reg), 200, "text/plain; version=0.0.4; charset=utf-8"
-                elif self.path == "/healthz":
-                    ok = not fl.stopped
-                    body, code, ctype = (b"ok" if ok else b"stopping"), (200 if ok else 503), "text/plain"
-                elif self.path == "/readyz":
-                    ok = all(s["polls"] > 0 for s in fl.stats())
-                    body, code, ctype = (b"ok" if ok else b"waiting for first poll"), (200 if ok else 503), "text/plain"
+                elif self.path in ("/healthz", "/readyz"):
+                    ok, why = hl.live() if self.path == "/healthz" else hl.ready()
+                    body, code, ctype = why.encode(), (200 if ok else 503), "text/plain"
                 else:
                     body, code, ctype = b"not found", 404, "text/plain"
                 self.send_response(code)

@@ -45,6 +45,10 @@ class Fleet:
         self._sup.stop()
 
     @property
+    def started(self) -> bool:
+        return self._started
+
+    @property
     def stopped(self) -> bool:
         return self._sup.stopped()
 

@@ -138,3 +138,60 @@ def test_pooled_scheduler_keeps_cadence(nat, tmp_path):
                 assert b["ts"] - (a["ts"]) >= 20_000_000 - 1_000_000
     finally:
         env.close()
+
+
+def test_liveness_detects_a_wedged_worker(nat):
+    """/healthz fails once a running worker makes no progress for longer than its budget
+    (here an SQS call that takes 1.5 s against a 0.2 s budget)."""
+    import time
+
+    from kube_sqs_autoscaler_amd.metrics import Health
+
+    env = BenchEnv(1, sqs_latency_ns=1_500_000_000)
+    try:
+        fleet = Fleet([W(*a) for a in zip(env.runners, env.targets, env.kube_apis, env.sqs_apis)])
+        h = Health(fleet, [200_000_000])
+        assert h.live() == (True, "ok")  # not started: nothing to judge yet
+        fleet.start(1)
+        time.sleep(0.5)
+        ok, why = h.live()
+        assert not ok and "made no progress" in why and "gpu-worker-0" in why
+        assert not h.ready()[0]
+        fleet.join()
+        assert h.live() == (True, "ok")  # the poll completed: progress again
+    finally:
+        env.close()
+
+
+def test_standby_replica_is_ready(nat):
+    """Under --leader-elect a standby never polls; it must still be Ready, or a rolling update
+    of the 2-replica Deployment would wait on it forever."""
+    from kube_sqs_autoscaler_amd.metrics import Health
+
+    env = BenchEnv(1)
+    try:
+        fleet = Fleet([W(*a) for a in zip(env.runners, env.targets, env.kube_apis, env.sqs_apis)])
+        h = Health(fleet, [Health.budget_ns(0, 30 * nat.SECOND)], leader_elect=True)
+        m = MetricsServer(fleet, "127.0.0.1:0", h)
+        m.start()
+        try:
+            base = f"http://127.0.0.1:{m.port}"
+            assert urllib.request.urlopen(base + "/readyz").read() == b"standby"
+            assert urllib.request.urlopen(base + "/healthz").read() == b"ok"
+            h.set_role("leader")  # acquired the lease: ready only after the first poll
+            with pytest.raises(urllib.error.HTTPError) as e:
+                urllib.request.urlopen(base + "/readyz")
+            assert e.value.code == 503
+            fleet.start(3)
+            fleet.join()
+            assert urllib.request.urlopen(base + "/readyz").read() == b"ok"
+        finally:
+            m.stop()
+    finally:
+        env.close()
+
+
+def test_health_budget_covers_retries():
+    from kube_sqs_autoscaler_amd.metrics import Health
+
+    assert Health.budget_ns(5 * 10**9, 30 * 10**9) == (5 + 240 + 60) * 10**9
