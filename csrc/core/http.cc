@@ -252,6 +252,11 @@ class Stream {
   int64_t spin_ns_ = 0;
 };
 
+// Largest message body either side accepts. Scale objects and Deployments are a few KiB and a
+// NodeList of a large cluster a few tens of MiB; a peer announcing more (or a chunked /
+// read-to-EOF body that keeps growing) is cut off instead of exhausting the 200 MiB pod.
+constexpr size_t kMaxBody = 128u << 20;
+
 // Incremental HTTP/1.1 message framing over a Stream with a carry-over buffer.
 class Reader {
  public:
@@ -277,6 +282,7 @@ class Reader {
   }
 
   Status read_exact(size_t n, std::string* out, int64_t deadline_ns) {
+    if (n > kMaxBody || out->size() + n > kMaxBody) return Status::Err("message body too large");
     while (buf_->size() < n) {
       bool eof = false;
       Status s = s_->read_some(buf_, deadline_ns, &eof);
@@ -296,6 +302,7 @@ class Reader {
         buf_->erase(0, p + 2);
         return Status::OK();
       }
+      if (buf_->size() > 1 << 20) return Status::Err("line too long");
       bool eof = false;
       Status s = s_->read_some(buf_, deadline_ns, &eof);
       if (!s.ok()) return s;
@@ -312,8 +319,10 @@ class Reader {
       std::string hex = trim(semi == std::string::npos ? line : line.substr(0, semi));
       if (hex.empty()) return Status::Err("malformed chunk size");
       char* end = nullptr;
+      errno = 0;
       unsigned long long n = std::strtoull(hex.c_str(), &end, 16);
-      if (*end != '\0') return Status::Err("malformed chunk size");
+      if (*end != '\0' || errno == ERANGE) return Status::Err("malformed chunk size");
+      if (n > kMaxBody || out->size() + n > kMaxBody) return Status::Err("message body too large");
       if (n == 0) {
         // trailers until blank line
         while (true) {
@@ -340,6 +349,7 @@ class Reader {
       Status s = s_->read_some(&tmp, deadline_ns, &eof);
       if (!s.ok()) return s;
       if (eof) return Status::OK();
+      if (out->size() + tmp.size() > kMaxBody) return Status::Err("message body too large");
       out->append(tmp);
     }
   }
@@ -821,7 +831,7 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
     s = rd.read_chunked(&resp->body, deadline_ns);
   } else if (!resp->header("Content-Length").empty()) {
     long long n = std::atoll(resp->header("Content-Length").c_str());
-    if (n < 0) s = Status::Err("bad Content-Length");
+    if (n < 0 || static_cast<unsigned long long>(n) > kMaxBody) s = Status::Err("bad Content-Length");
     else s = rd.read_exact(static_cast<size_t>(n), &resp->body, deadline_ns);
   } else {
     s = rd.read_to_eof(&resp->body, deadline_ns);
