@@ -219,3 +219,16 @@ def test_main_end_to_end_over_tls(nat, tmp_path, capfd):
     finally:
         sqs.stop()
         kube.stop()
+
+
+def test_reference_command_path_launcher():
+    """The image installs deploy/bin/kube-sqs-autoscaler at /kube-sqs-autoscaler, so the
+    reference's `command: [/kube-sqs-autoscaler, ...]` manifests run unchanged; like a Go
+    binary, usage names the program by its argv[0]."""
+    exe = os.path.join(ROOT, "deploy", "bin", "kube-sqs-autoscaler")
+    assert os.access(exe, os.X_OK)
+    e = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([exe, "-h"], env=e, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stderr.startswith(f"Usage of {exe}:\n  -api-timeout duration")
+    r = subprocess.run([exe, "--max-pods=x"], env=e, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and r.stderr.startswith('invalid value "x" for flag -max-pods: parse error')
