@@ -12,6 +12,8 @@ namespace ksa {
 void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
                const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads) {
   if (m <= 0 || n < 1) return;
+  for (int k = 0; k < 3; ++k)
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return;  // sweep.py validates first
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
   auto work = [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {

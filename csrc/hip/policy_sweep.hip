@@ -11,15 +11,20 @@
 //     every lane walks its own forward-only cursor -- hit LDS; longer traces are read from
 //     global memory (lanes advance through it nearly in lockstep, so L1/L2 serve them) and then
 //     no LDS is allocated at all, leaving occupancy to the VGPR budget;
-//   * no 64-bit integer division per poll (the backlog metric divides once per replica run);
+//   * no 64-bit integer division per poll: the backlog metric divides once per replica run, and
+//     the poll-to-poll interval in ms is picked from six precomputed floors (policy_sim.h);
 //   * the host orders configurations with the poll period outermost, so neighbouring lanes share
 //     trip counts and a wave's lanes retire together (less divergence at the loop exit);
-//   * grid-stride loop over configurations, grid = CUs x 8 workgroups of 256 (what 58 VGPRs
-//     keep resident: 8 waves/SIMD; 2048 workgroups over the 8 XCDs); every lane's loop is bounded
-//     by horizon / max(poll, sqs latency) and ksa_sim::kMaxPolls.
+//   * grid-stride loop over configurations; the grid is one resident wave of workgroups
+//     (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs: 74 VGPRs -> 6 waves/SIMD -> 6
+//     workgroups of 256 per CU, 1536 over the 8 XCDs), so no workgroup waits for a second round
+//     (a fixed CUs x 8 grid cost 10% in that tail). Forcing 7 waves/SIMD spills and is slower;
+//     every lane's loop is bounded by horizon / max(poll, sqs latency) and ksa_sim::kMaxPolls.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -36,7 +41,11 @@ enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPo
 enum : int { kPodMs = 0, kBacklog, kFirstUp, kNumOut64 };
 enum : int { kUps = 0, kDowns, kNoopUps, kNoopDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
 
-__global__ __launch_bounds__(kBlock) void sweep_kernel(const int64_t* __restrict__ params, int64_t m,
+#ifndef KSA_SWEEP_WAVES_PER_EU
+#define KSA_SWEEP_WAVES_PER_EU 6
+#endif
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEEP_WAVES_PER_EU))) void sweep_kernel(const int64_t* __restrict__ params, int64_t m,
                                                        ksa_sim::Latency lat, const int64_t* __restrict__ g_t,
                                                        const int64_t* __restrict__ g_d, int32_t n, int32_t init,
                                                        int64_t horizon, int64_t* __restrict__ out64,
@@ -104,6 +113,12 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
     g_sweep_error = "trace must have at least one segment starting at t=0";
     return -1;
   }
+  for (int k = 0; k < 3; ++k) {
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) {
+      g_sweep_error = "latencies must be within [0, 1 h]";
+      return -1;
+    }
+  }
   if (m <= 0) return 0;
   if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
   hipDeviceProp_t prop;
@@ -124,12 +139,18 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
       break;
     if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
     const int64_t want = (m + kBlock - 1) / kBlock;
-    // 58 VGPRs -> 8 waves/SIMD: 8 resident 256-thread workgroups per CU
-    const int64_t cap = static_cast<int64_t>(prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256) * 8;
+    const size_t lds = n <= kLdsTraceMax ? 2 * static_cast<size_t>(n) * sizeof(int64_t) : 0;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel, kBlock, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int64_t cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    int64_t cap = cus * per_cu;  // one wave of resident workgroups
+    if (const char* g = std::getenv("KSA_SWEEP_GRID")) {  // tuning knob: "tiles" or N x resident
+      cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
+    }
     const int grid = static_cast<int>(want < cap ? want : cap);
     const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
     hipEventRecord(e0, nullptr);
-    const size_t lds = n <= kLdsTraceMax ? 2 * static_cast<size_t>(n) * sizeof(int64_t) : 0;
     hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), lds, nullptr, d_p, m, lat, d_t, d_d, n, init_replicas,
                        horizon_ns, d_o64, d_o32);
     if (!ok(hipGetLastError(), "sweep_kernel launch")) break;

@@ -28,11 +28,22 @@
 #define KSA_HD inline
 #endif
 
+// Keeps the compiler from folding select(c, x / k, y / k) back into select(c, x, y) / k,
+// which would put the 64-bit division by 10^6 straight back into the per-poll loop.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KSA_OPAQUE(x) __asm__ volatile("" : "+v"(x))
+#else
+#define KSA_OPAQUE(x) __asm__ volatile("" : "+r"(x))
+#endif
+
 namespace ksa_sim {
 
 // Hard per-configuration bound on simulated polls, so every GPU lane reaches its exit even for
 // a degenerate request (the host also refuses sweeps whose estimated work exceeds a budget).
 constexpr int32_t kMaxPolls = 1 << 26;
+// Per-call latency bound of the model (hosts reject larger values): keeps the per-poll interval
+// offsets below in 32 bits.
+constexpr int64_t kMaxLatencyNs = 3600LL * 1000000000LL;
 
 struct Params {
   int64_t poll_ns, up_cool_ns, down_cool_ns;
@@ -102,8 +113,7 @@ KSA_HD void flush(Result* r, Accum* a) {
   a->run = 0;
 }
 
-KSA_HD void accumulate(Result* r, Accum* a, int64_t dt_ns, int32_t replicas, int64_t depth) {
-  const int64_t dt_ms = dt_ns / 1000000;
+KSA_HD void accumulate_ms(Result* r, Accum* a, int64_t dt_ms, int32_t replicas, int64_t depth) {
   r->pod_ms += static_cast<int64_t>(replicas) * dt_ms;
   if (replicas != a->run_r) {
     flush(r, a);
@@ -125,32 +135,53 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
   const int32_t up32 = go_i32(p.up_pods), down32 = go_i32(p.down_pods);
   const int64_t period = p.poll_ns > 0 ? p.poll_ns : 0;
   int64_t prev_t = 0;
-  int32_t prev_r = replicas;
   int64_t prev_d = depth_at(t_ns, depth, n, &cursor, 0);
   res.max_replicas = replicas;
+  // The time between two polls is the period plus the earlier poll's API latency: sqs plus 0-2
+  // GETs and at most as many writes, so one of six values. Their millisecond floors are taken
+  // once here; the per-poll metric update then selects one instead of dividing a 64-bit
+  // interval (a long multiply-high expansion on the GPU). Exact: same operands, same division.
+  const int64_t base = period + lat.sqs_ns;
+  const int64_t ms_g0 = base / 1000000;
+  // The other five differ from ms_g0 by at most the latencies (bounded by the host: <= 1 h each),
+  // so they are kept as 32-bit offsets -- fewer registers, more resident waves.
+  int32_t off_g1u0 = static_cast<int32_t>((base + lat.get_ns) / 1000000 - ms_g0);
+  int32_t off_g1u1 = static_cast<int32_t>((base + lat.get_ns + lat.update_ns) / 1000000 - ms_g0);
+  int32_t off_g2u0 = static_cast<int32_t>((base + 2 * lat.get_ns) / 1000000 - ms_g0);
+  int32_t off_g2u1 = static_cast<int32_t>((base + 2 * lat.get_ns + lat.update_ns) / 1000000 - ms_g0);
+  int32_t off_g2u2 = static_cast<int32_t>((base + 2 * lat.get_ns + 2 * lat.update_ns) / 1000000 - ms_g0);
+  KSA_OPAQUE(off_g1u0);
+  KSA_OPAQUE(off_g1u1);
+  KSA_OPAQUE(off_g2u0);
+  KSA_OPAQUE(off_g2u1);
+  KSA_OPAQUE(off_g2u2);
+  int64_t dt_ms = period / 1000000;  // t=0 -> first poll: no latency before it
   // Guard: a zero period with zero latency would never advance time.
   const bool advances = period > 0 || lat.sqs_ns > 0;
   while (advances && res.polls < kMaxPolls) {
     const int64_t t_poll = now + period;  // main.go:41 sleep, then poll
     if (t_poll > horizon_ns) break;
     now = t_poll;
-    accumulate(&res, &acc, now - prev_t, prev_r, prev_d);
+    accumulate_ms(&res, &acc, dt_ms, replicas, prev_d);  // replicas as set by the previous poll
     prev_t = now;
     res.polls++;
     const int64_t d = depth_at(t_ns, depth, n, &cursor, now);  // sampled at call start
     now += lat.sqs_ns;
+    int32_t gets = 0, writes = 0;
     bool cont = false;
     if (d >= p.up_msgs) {  // main.go:51
       if (last_up + p.up_cool_ns > now) {  // main.go:52 (strict After)
         cont = true;
       } else {
         now += lat.get_ns;
+        gets++;
         if (replicas >= max32) {  // scale.go:62
           res.noop_ups++;
         } else {
           int32_t next = add_i32(replicas, up32);
           if (next > max32) next = max32;
           now += lat.update_ns;
+          writes++;
           replicas = next;
           res.ups++;
           if (res.first_up_ns < 0) res.first_up_ns = t_poll;
@@ -161,12 +192,14 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
     if (!cont && d <= p.down_msgs) {  // main.go:65
       if (!(last_down + p.down_cool_ns > now)) {
         now += lat.get_ns;
+        gets++;
         if (replicas <= min32) {  // scale.go:89
           res.noop_downs++;
         } else {
           int32_t next = sub_i32(replicas, down32);
           if (next < min32) next = min32;
           now += lat.update_ns;
+          writes++;
           replicas = next;
           res.downs++;
         }
@@ -174,10 +207,11 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
       }
     }
     if (replicas > res.max_replicas) res.max_replicas = replicas;
-    prev_r = replicas;
     prev_d = d;
+    const int32_t g2 = writes == 0 ? off_g2u0 : (writes == 1 ? off_g2u1 : off_g2u2);
+    dt_ms = ms_g0 + (gets == 0 ? 0 : (gets == 1 ? (writes == 0 ? off_g1u0 : off_g1u1) : g2));
   }
-  if (horizon_ns > prev_t) accumulate(&res, &acc, horizon_ns - prev_t, prev_r, prev_d);
+  if (horizon_ns > prev_t) accumulate_ms(&res, &acc, (horizon_ns - prev_t) / 1000000, replicas, prev_d);
   flush(&res, &acc);
   res.final_replicas = replicas;
   return res;

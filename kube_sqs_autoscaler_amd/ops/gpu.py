@@ -75,7 +75,9 @@ class GpuHealth:
 
 
 def lib_path() -> Path:
-    return Path(__file__).resolve().parent / "libksa_gpu.so"
+    """The in-tree gfx950 library; ``KSA_GPU_LIB`` points at another build (A/B kernel runs)."""
+    override = os.environ.get("KSA_GPU_LIB")
+    return Path(override) if override else Path(__file__).resolve().parent / "libksa_gpu.so"
 
 
 def load(build_if_missing: bool = True) -> ctypes.CDLL:
