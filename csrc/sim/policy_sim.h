@@ -122,6 +122,10 @@ KSA_HD void accumulate_ms(Result* r, Accum* a, int64_t dt_ms, int32_t replicas, 
   a->run += depth * dt_ms;
 }
 
+constexpr int64_t kTimeBound = int64_t(1) << 61;
+
+KSA_HD int64_t clamp_cool(int64_t c) { return c > kTimeBound ? kTimeBound : (c < -kTimeBound ? -kTimeBound : c); }
+
 KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns, const int64_t* depth, int32_t n,
                        int32_t init_replicas, int64_t horizon_ns) {
   Result res;
@@ -133,7 +137,10 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
   int32_t replicas = init_replicas;
   const int32_t max32 = go_i32(p.max_pods), min32 = go_i32(p.min_pods);
   const int32_t up32 = go_i32(p.up_pods), down32 = go_i32(p.down_pods);
-  const int64_t period = p.poll_ns > 0 ? p.poll_ns : 0;
+  const int64_t period = p.poll_ns > 0 ? (p.poll_ns < kTimeBound ? p.poll_ns : kTimeBound) : 0;
+  // Timers stay below 2^61 (the host bounds horizon and latencies), so clamping the cool-downs
+  // to +-2^61 keeps `last + cool` from overflowing without changing any comparison with `now`.
+  const int64_t up_cool = clamp_cool(p.up_cool_ns), down_cool = clamp_cool(p.down_cool_ns);
   int64_t prev_t = 0;
   int64_t prev_d = depth_at(t_ns, depth, n, &cursor, 0);
   res.max_replicas = replicas;
@@ -170,7 +177,7 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
     int32_t gets = 0, writes = 0;
     bool cont = false;
     if (d >= p.up_msgs) {  // main.go:51
-      if (last_up + p.up_cool_ns > now) {  // main.go:52 (strict After)
+      if (last_up + up_cool > now) {  // main.go:52 (strict After)
         cont = true;
       } else {
         now += lat.get_ns;
@@ -190,7 +197,7 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
       }
     }
     if (!cont && d <= p.down_msgs) {  // main.go:65
-      if (!(last_down + p.down_cool_ns > now)) {
+      if (!(last_down + down_cool > now)) {
         now += lat.get_ns;
         gets++;
         if (replicas <= min32) {  // scale.go:89

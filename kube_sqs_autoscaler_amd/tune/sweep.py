@@ -167,6 +167,8 @@ def run(trace: Trace, params: np.ndarray, init_replicas: int = 1, horizon_ns: in
     params = np.ascontiguousarray(params, dtype=np.int64)
     if params.ndim != 2 or params.shape[0] != len(PARAM_FIELDS):
         raise ValueError("params must have shape (9, m); build it with grid()")
+    if not 0 < horizon_ns < 2**60:
+        raise ValueError("horizon must be positive and below 2^60 ns (36 years)")
     if any(not 0 <= int(x) <= 3600 * 10**9 for x in latency_ns):
         raise ValueError("latencies must be within [0, 1 h] (ksa_sim::kMaxLatencyNs)")
     if np.any((params[0] <= 0) & (latency_ns[0] <= 0)):

@@ -109,3 +109,22 @@ def test_pareto_front():
     f = sweep.pareto_front(pod, bl)
     # (pod, backlog): (1,7) (3,4) (4,2) (5,1); (1,9) and (2,8) are dominated by (1,7)
     assert list(f) == [5, 2, 4, 0]
+
+
+def test_extreme_cool_downs_and_periods_do_not_overflow(nat):
+    """Cool-downs and poll periods near the int64 limit: the simulator clamps them (no signed
+    overflow) and still agrees with the oracle, which has unbounded integers."""
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    S = 1_000_000_000
+    tr = sweep.Trace.from_segments([(0, 500), (60 * S, 0)])
+    big = 2**63 - 1
+    grid = sweep.grid(poll_ns=[5 * S, big], up_cool_ns=[0, big, -big], down_cool_ns=[0, big], max_pods=[8])
+    r = sweep.run(tr, grid, 1, 300 * S, device="cpu")
+    for j in range(grid.shape[1]):
+        want = sweep.oracle_row(tr, r.config(j), 1, 300 * S, (1_000_000, 1_000_000, 1_000_000))
+        got = {k: int(r.out[k][j]) for k in want}
+        assert got == want, (r.config(j), got, want)
+    assert np.all(r.out["polls"][grid[0] == big] == 0)
