@@ -576,7 +576,14 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("basic_password", &KubeOptions::basic_password)
       .def_readwrite("timeout_ns", &KubeOptions::timeout)
       .def_readwrite("busy_poll_ns", &KubeOptions::busy_poll)
-      .def_readwrite("proxy", &KubeOptions::proxy);
+      .def_readwrite("proxy", &KubeOptions::proxy)
+      .def_readwrite("qps", &KubeOptions::qps)
+      .def_readwrite("burst", &KubeOptions::burst)
+      .def_readwrite("clock", &KubeOptions::clock);
+  py::class_<TokenBucket>(m, "TokenBucket")
+      .def(py::init<double, int, std::shared_ptr<Clock>>(), py::arg("qps"), py::arg("burst"), py::arg("clock"))
+      .def("reserve", &TokenBucket::reserve)
+      .def("take", &TokenBucket::take, py::call_guard<py::gil_scoped_release>());
 
   py::class_<DeploymentApi, PyDeploymentApi, py::smart_holder>(m, "DeploymentApi")
       .def(py::init<>())
@@ -606,6 +613,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["updates"] = s.updates;
         d["errors"] = s.errors;
         d["conflicts"] = s.conflicts;
+        d["throttled"] = s.throttled;
+        d["throttle_ns"] = s.throttle_ns;
         d["http"] = http_stats_dict(s.http);
         return d;
       });

@@ -1,6 +1,8 @@
 #include "kube.h"
 
+#include <algorithm>
 #include <cctype>
+#include <cmath>
 #include <fstream>
 #include <sstream>
 
@@ -38,6 +40,34 @@ Result<std::string> FileTokenProvider::token() {
 void FileTokenProvider::invalidate(const std::string& used) {
   std::lock_guard<std::mutex> lk(mu_);
   if (have_ && cached_ == used) read_at_ = clock_->now() - refresh_;  // re-read on next use
+}
+
+// ---------------------------------------------------------------------------------------
+// Client-side throttle
+
+TokenBucket::TokenBucket(double qps, int burst, std::shared_ptr<Clock> clock)
+    : qps_(qps), burst_(burst < 1 ? 1 : burst), tokens_(0), clock_(std::move(clock)) {}
+
+Nanos TokenBucket::reserve() {
+  std::lock_guard<std::mutex> lk(mu_);
+  const Nanos now = clock_->now();
+  if (!started_) {
+    started_ = true;
+    tokens_ = burst_;
+    last_ = now;
+  } else if (now > last_) {
+    tokens_ = std::min(burst_, tokens_ + static_cast<double>(now - last_) * qps_ / 1e9);
+    last_ = now;
+  }
+  tokens_ -= 1;
+  if (tokens_ >= 0) return 0;
+  return static_cast<Nanos>(std::ceil(-tokens_ / qps_ * 1e9));
+}
+
+Nanos TokenBucket::take() {
+  const Nanos wait = reserve();
+  if (wait > 0) clock_->sleep(wait, nullptr);
+  return wait;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -98,6 +128,20 @@ KubeRestDeployments::KubeRestDeployments(KubeOptions opts) : opts_(std::move(opt
   http_->set_busy_poll(opts_.busy_poll);
   Status ps = http_->set_proxy(opts_.proxy);
   if (!ps.ok()) init_status_ = ps;
+  if (opts_.qps > 0) {
+    limiter_ = std::make_unique<TokenBucket>(opts_.qps, opts_.burst,
+                                             opts_.clock ? opts_.clock : std::make_shared<RealClock>());
+  }
+}
+
+void KubeRestDeployments::throttle() {
+  if (!limiter_) return;
+  const Nanos waited = limiter_->take();
+  if (waited > 0) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.throttled++;
+    stats_.throttle_ns += waited;
+  }
 }
 
 KubeStats KubeRestDeployments::stats() const {
@@ -214,6 +258,7 @@ Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest
                                        HttpResponse* resp, const std::string& name) {
   Status a = add_auth(req);
   if (!a.ok()) return a;
+  throttle();
   return check_response(verb_desc, *req, *resp, name, http_->round_trip(*req, resp));
 }
 
@@ -232,6 +277,7 @@ bool KubeRestDeployments::begin_get(const std::string& name) {
   req.method = "GET";
   req.target = path_for(name);
   if (!add_auth(&req).ok()) return false;
+  throttle();
   if (!http_->send(req).ok()) return false;  // the synchronous GET will report the error
   {
     std::lock_guard<std::mutex> lk(mu_);

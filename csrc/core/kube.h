@@ -91,6 +91,26 @@ class FileTokenProvider final : public TokenProvider {
   std::string cached_;
 };
 
+// Client-side request throttle: client-go's rest.Config default (QPS 5, burst 10) through
+// flowcontrol.NewTokenBucketRateLimiter, whose Accept() reserves a token from a
+// golang.org/x/time/rate limiter and sleeps until it is due. The bucket starts full; a reservation
+// takes its token at once (the count may go negative), so waiters are served in order.
+class TokenBucket {
+ public:
+  TokenBucket(double qps, int burst, std::shared_ptr<Clock> clock);
+  // Reserves one token; returns how long the caller must wait before using it.
+  Nanos reserve();
+  // reserve() + sleep on the clock. Returns the time waited.
+  Nanos take();
+
+ private:
+  std::mutex mu_;
+  double qps_, burst_, tokens_;
+  Nanos last_ = 0;
+  bool started_ = false;
+  std::shared_ptr<Clock> clock_;
+};
+
 enum class ScaleMode { Deployment, Scale, Patch };
 
 struct KubeOptions {
@@ -103,6 +123,10 @@ struct KubeOptions {
   Nanos timeout = 30 * kSecond;
   Nanos busy_poll = 0;  // HttpClient::set_busy_poll
   std::string proxy;    // HttpClient::set_proxy ("" = direct)
+  // Per-client throttle (client-go: QPS 5, burst 10 per clientset). qps <= 0: unthrottled.
+  double qps = 0;
+  int burst = 0;
+  std::shared_ptr<Clock> clock;  // for the throttle's waits (null: RealClock)
 };
 
 struct KubeStats {
@@ -110,6 +134,8 @@ struct KubeStats {
   uint64_t updates = 0;
   uint64_t errors = 0;
   uint64_t conflicts = 0;
+  uint64_t throttled = 0;     // requests that waited for the client-side throttle
+  int64_t throttle_ns = 0;    // total time spent waiting
   HttpClientStats http;
 };
 
@@ -138,6 +164,8 @@ class KubeRestDeployments final : public DeploymentApi {
   Status init_status_;
   Url url_;
   std::unique_ptr<HttpClient> http_;
+  std::unique_ptr<TokenBucket> limiter_;
+  void throttle();
   mutable std::mutex mu_;
   KubeStats stats_;
 };

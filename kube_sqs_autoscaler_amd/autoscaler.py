@@ -138,8 +138,12 @@ def new_http_client(rc: RestConfig, timeout_ns: int, environ: Optional[Mapping[s
 
 
 def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", timeout_ns: int = 30 * SECOND, clock=None,
-                       busy_poll_ns: int = 0, environ: Optional[Mapping[str, str]] = None):
-    """The ``DeploymentInterface`` seam over REST (/root/reference/scale/scale.go:44)."""
+                       busy_poll_ns: int = 0, environ: Optional[Mapping[str, str]] = None, qps: float = 0.0,
+                       burst: int = 0):
+    """The ``DeploymentInterface`` seam over REST (/root/reference/scale/scale.go:44).
+
+    ``qps``/``burst``: the client-side throttle of this client (client-go's clientset default is
+    5/10, which the CLI passes; 0 leaves it unthrottled)."""
     nat = native()
     o = nat.KubeOptions()
     o.server = rc.host
@@ -149,6 +153,9 @@ def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", time
     o.tls = tls_options(rc)
     o.timeout_ns = timeout_ns
     o.busy_poll_ns = busy_poll_ns
+    if qps > 0:
+        o.qps, o.burst = float(qps), int(burst)
+        o.clock = clock or nat.RealClock()
     tp = token_provider(rc, clock, timeout_ns)
     if tp is not None:
         o.token = tp
@@ -216,7 +223,8 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     if tag_queue:
         log = base_logger.with_fields([("deployment", target.name), ("queue", target.queue_url)])
     kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock,
-                                  busy_poll_ns=cfg.busy_poll_ns, environ=environ)
+                                  busy_poll_ns=cfg.busy_poll_ns, environ=environ, qps=cfg.kube_api_qps,
+                                  burst=cfg.kube_api_burst)
     scaler = new_pod_autoscaler(target, kube_api, log, clock)
     scaler.dry_run = cfg.dry_run
     sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,

@@ -95,6 +95,8 @@ class Config:
     dry_run: bool = False
     worker_threads: int = 0
     busy_poll_ns: int = 25_000
+    kube_api_qps: float = 5.0
+    kube_api_burst: int = 10
     trace_file: str = ""
     leader_elect: bool = False
     leader_elect_lease_name: str = "kube-sqs-autoscaler"
@@ -145,6 +147,8 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.int("worker-threads", 0, "Threads polling the tracked queues; 0 = one per queue (use fewer for hundreds of queues)")
     fs.bool("dry-run", False, "Shadow mode: poll and decide as usual, log the scaling that would happen, never write")
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
+    fs.float64("kube-api-qps", 5.0, "Client-side limit on kube-apiserver requests per second for each tracked queue, as client-go's default rest client (0 disables)")
+    fs.int("kube-api-burst", 10, "Requests allowed in a burst above -kube-api-qps (client-go default)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
@@ -263,6 +267,8 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         dry_run=fs["dry-run"],
         worker_threads=fs["worker-threads"],
         busy_poll_ns=fs["busy-poll"],
+        kube_api_qps=fs["kube-api-qps"],
+        kube_api_burst=fs["kube-api-burst"],
         trace_file=fs["trace-file"],
         leader_elect=fs["leader-elect"],
         leader_elect_lease_name=fs["leader-elect-lease-name"],

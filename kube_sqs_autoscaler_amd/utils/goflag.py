@@ -206,6 +206,79 @@ def parse_duration(s: str) -> int:
     return d
 
 
+def parse_float(s: str) -> float:
+    """strconv.ParseFloat(s, 64): decimal or hex (``0x1p-2``) literals, ``_`` between digits,
+    ``inf``/``infinity``/``nan`` in any case; no surrounding space. Overflow is ErrRange."""
+    s0 = s
+
+    def syntax() -> GoSyntaxError:
+        return GoSyntaxError(f'strconv.ParseFloat: parsing "{s0}": invalid syntax')
+
+    if not s or not s.isascii() or s != s.strip():
+        raise syntax()
+    neg = s[0] == "-"
+    body = s[1:] if s[0] in "+-" else s
+    special = body.lower()
+    if special in ("inf", "infinity"):
+        return float("-inf") if neg else float("inf")
+    if special == "nan":
+        if body != s:  # Go accepts no sign on NaN
+            raise syntax()
+        return float("nan")
+    if "_" in s:
+        if not _underscore_ok(s):
+            raise syntax()
+        s = s.replace("_", "")
+        body = s[1:] if s[0] in "+-" else s
+    hexa = body[:2].lower() == "0x"
+    if hexa:
+        if "p" not in body.lower():  # Go requires the binary exponent on hex floats
+            raise syntax()
+        try:
+            v = float.fromhex(s)
+        except OverflowError:
+            raise GoRangeError(f'strconv.ParseFloat: parsing "{s0}": value out of range')
+        except ValueError:
+            raise syntax()
+    else:
+        if any(c not in "0123456789.eE+-" for c in body) or not any(c.isdigit() for c in body):
+            raise syntax()
+        try:
+            v = float(s)
+        except ValueError:
+            raise syntax()
+    if v in (float("inf"), float("-inf")):
+        raise GoRangeError(f'strconv.ParseFloat: parsing "{s0}": value out of range')
+    return v
+
+
+def format_float(v: float) -> str:
+    """strconv.FormatFloat(v, 'g', -1, 64) -- flag.Float64's String(): shortest round-trip
+    digits, %e form when the decimal exponent is < -4 or >= 6 (eprec is 6 for shortest)."""
+    import math
+    from decimal import Decimal
+
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "+Inf" if v > 0 else "-Inf"
+    if v == 0:
+        return "-0" if math.copysign(1.0, v) < 0 else "0"
+    sign, digits, exp10 = Decimal(repr(v)).normalize().as_tuple()
+    ds = "".join(map(str, digits))
+    dp = len(ds) + exp10  # position of the decimal point within ds
+    exp = dp - 1
+    neg = "-" if sign else ""
+    if exp < -4 or exp >= 6:
+        mant = ds[0] + ("." + ds[1:] if len(ds) > 1 else "")
+        return f"{neg}{mant}e{'-' if exp < 0 else '+'}{abs(exp):02d}"
+    if dp <= 0:
+        return f"{neg}0.{'0' * -dp}{ds}"
+    if dp >= len(ds):
+        return f"{neg}{ds}{'0' * (dp - len(ds))}"
+    return f"{neg}{ds[:dp]}.{ds[dp:]}"
+
+
 def _fmt_frac(v: int, prec: int) -> tuple[str, int]:
     out = ""
     printed = False
@@ -277,7 +350,7 @@ class Flag:
         return self.formatter(self.default)
 
     def is_zero_default(self) -> bool:
-        zero = {"duration": "0s", "int": "0", "string": "", "bool": "false", "value": ""}.get(self.kind, "")
+        zero = {"duration": "0s", "int": "0", "float": "0", "string": "", "bool": "false", "value": ""}.get(self.kind, "")
         return self.default_text == zero
 
 
@@ -303,6 +376,9 @@ class FlagSet:
 
     def int(self, name: str, default: int, usage: str) -> Flag:
         return self._add(Flag(name, "int", default, usage, parse_int, str))
+
+    def float64(self, name: str, default: float, usage: str) -> Flag:
+        return self._add(Flag(name, "float", default, usage, parse_float, format_float))
 
     def string(self, name: str, default: str, usage: str) -> Flag:
         return self._add(Flag(name, "string", default, usage, lambda s: s, lambda v: v))
@@ -427,7 +503,7 @@ def _unquote_usage(f: Flag) -> tuple[str, str]:
         if j >= 0:
             name = usage[i + 1 : j]
             return name, usage[:i] + name + usage[j + 1 :]
-    return {"bool": "", "duration": "duration", "int": "int", "string": "string"}.get(f.kind, "value"), usage
+    return {"bool": "", "duration": "duration", "int": "int", "float": "float", "string": "string"}.get(f.kind, "value"), usage
 
 
 def _go_quote(s: str) -> str:

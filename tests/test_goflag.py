@@ -139,3 +139,50 @@ def test_usage_matches_go_print_defaults():
         "  -poll-period duration\n    \tThe interval (default 5s)\n"
         "  -v\tverbose\n"
     )
+
+
+@pytest.mark.parametrize("text,want", [
+    ("5", 5.0), ("0.5", 0.5), ("1e3", 1000.0), ("1_000.5", 1000.5), ("0x1p-2", 0.25), ("+2", 2.0), (".5", 0.5),
+    ("Inf", float("inf")), ("-infinity", float("-inf")),
+])
+def test_parse_float_like_strconv(text, want):
+    from kube_sqs_autoscaler_amd.utils.goflag import parse_float
+
+    assert parse_float(text) == want
+
+
+@pytest.mark.parametrize("text,err", [
+    ("", "invalid syntax"), (" 1", "invalid syntax"), ("1__0", "invalid syntax"), ("0x10", "invalid syntax"),
+    ("+nan", "invalid syntax"), ("1e400", "value out of range"), ("abc", "invalid syntax"), ("١", "invalid syntax"),
+])
+def test_parse_float_errors(text, err):
+    from kube_sqs_autoscaler_amd.utils.goflag import GoRangeError, GoSyntaxError, parse_float
+
+    with pytest.raises((GoSyntaxError, GoRangeError), match=err):
+        parse_float(text)
+
+
+@pytest.mark.parametrize("v,text", [(5.0, "5"), (0.5, "0.5"), (1e6, "1e+06"), (123456.0, "123456"),
+                                    (1234567.0, "1.234567e+06"), (1e-4, "0.0001"), (1e-5, "1e-05"), (-3.25, "-3.25")])
+def test_format_float_like_go(v, text):
+    """flag.Float64's default text is strconv.FormatFloat(v, 'g', -1, 64)."""
+    from kube_sqs_autoscaler_amd.utils.goflag import format_float
+
+    assert format_float(v) == text
+
+
+def test_float_flag_usage_and_errors():
+    from kube_sqs_autoscaler_amd.utils.goflag import FlagError, FlagSet
+
+    fs = FlagSet(program="p")
+    fs.float64("qps", 5.0, "requests per second")
+    fs.float64("zero", 0.0, "no default shown")
+    assert fs.usage() == "Usage of p:\n  -qps float\n    \trequests per second (default 5)\n  -zero float\n    \tno default shown\n"
+    fs.parse(["-qps", "2.5"])
+    assert fs["qps"] == 2.5
+    bad = FlagSet(program="p")
+    bad.float64("qps", 5.0, "u")
+    with pytest.raises(FlagError, match='invalid value "x" for flag -qps: parse error'):
+        bad.parse(["-qps=x"])
+    with pytest.raises(FlagError, match='invalid value "1e999" for flag -qps: value out of range'):
+        bad.parse(["-qps=1e999"])
