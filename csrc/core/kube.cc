@@ -61,7 +61,7 @@ Nanos TokenBucket::reserve() {
   }
   tokens_ -= 1;
   if (tokens_ >= 0) return 0;
-  return static_cast<Nanos>(std::ceil(-tokens_ / qps_ * 1e9));
+  return static_cast<Nanos>(std::ceil(-tokens_ * 1e9 / qps_));
 }
 
 Nanos TokenBucket::take() {

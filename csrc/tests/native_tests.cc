@@ -9,6 +9,7 @@
 #include <netinet/in.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -22,6 +23,7 @@
 #include <vector>
 
 #include "../core/clock.h"
+#include "../core/exec_auth.h"
 #include "../core/fakes.h"
 #include "../core/goutil.h"
 #include "../core/http.h"
@@ -525,6 +527,65 @@ TEST(concurrent_logger_lines_are_whole) {
   for (auto& t : ts) t.join();
   CHECK_EQ(lines->size(), size_t(1600));
   for (auto& l : *lines) CHECK(l.rfind("time=\"", 0) == 0 && l.find(" queue=q") != std::string::npos);
+}
+
+TEST(token_bucket_concurrent_reservations) {
+  // 8 threads x 50 reservations on one bucket: the wait each caller is handed is the queue
+  // position beyond the burst, so the sum over all callers is fixed whatever the interleaving.
+  auto clock = std::make_shared<VirtualClock>(0);
+  TokenBucket b(1000.0, 100, clock);
+  std::atomic<int64_t> total{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([&] {
+      for (int i = 0; i < 50; ++i) total += b.reserve();
+    });
+  for (auto& t : ts) t.join();
+  // 400 reservations, 100 free, the k-th beyond waits k ms: sum_{k=1..300} k ms
+  CHECK_EQ(total.load(), int64_t(300) * 301 / 2 * kMillisecond);
+}
+
+TEST(exec_provider_shared_across_threads) {
+  // One authenticator shared by 8 workers: the plugin runs once, every thread gets its token.
+  char dir[] = "/tmp/ksa_exec_XXXXXX";
+  if (!mkdtemp(dir)) {
+    CHECK(false);
+    return;
+  }
+  const std::string script = std::string(dir) + "/plugin.sh";
+  {
+    std::FILE* f = std::fopen(script.c_str(), "w");
+    std::fputs("#!/bin/sh\necho x >> \"$(dirname \"$0\")/runs\"\n"
+               "echo '{\"kind\":\"ExecCredential\",\"apiVersion\":\"client.authentication.k8s.io/v1beta1\","
+               "\"status\":{\"token\":\"tok-'$KSA_SUFFIX'\"}}'\n",
+               f);
+    std::fclose(f);
+  }
+  chmod(script.c_str(), 0755);
+  ExecConfig cfg;
+  cfg.command = script;
+  cfg.api_version = "client.authentication.k8s.io/v1beta1";
+  cfg.env = {{"KSA_SUFFIX", "42"}};
+  cfg.timeout = 10 * kSecond;
+  auto p = std::make_shared<ExecTokenProvider>(cfg, std::make_shared<RealClock>());
+  std::atomic<int> good{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([&] {
+      for (int i = 0; i < 20; ++i) {
+        auto r = p->token();
+        if (r.ok() && r.value == "tok-42") ++good;
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK_EQ(good.load(), 160);
+  CHECK_EQ(p->runs(), uint64_t(1));
+  p->invalidate("tok-42");
+  CHECK(p->token().ok());
+  CHECK_EQ(p->runs(), uint64_t(2));
+  std::remove((std::string(dir) + "/runs").c_str());
+  std::remove(script.c_str());
+  rmdir(dir);
 }
 
 }  // namespace

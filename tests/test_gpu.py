@@ -61,7 +61,8 @@ def test_cli_gpu_aware_max_local(tmp_path, capfd):
         env = {"AWS_ACCESS_KEY_ID": "a", "AWS_SECRET_ACCESS_KEY": "b", "KUBE_CONFIG_PATH": str(kc)}
         rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=w", "--kubernetes-namespace=ml", "--aws-region=us-east-1",
                    f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s", "--max-pods=64",
-                   "--attribute-names=ApproximateNumberOfMessages", "--gpu-aware-max=local"], environ=env, max_iterations=100)
+                   "--attribute-names=ApproximateNumberOfMessages", "--gpu-aware-max=local", "--kube-api-qps=0"],
+                  environ=env, max_iterations=100)
         assert rc == 0
         assert kube.replicas("ml", "w") == min(64, n_gpus)
         assert f"GPU capacity: {n_gpus} pods" in capfd.readouterr().err
