@@ -447,6 +447,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         py::dict d;
         d["calls"] = s.calls;
         d["retries"] = s.retries;
+        d["throttle_retries"] = s.throttle_retries;
         d["errors"] = s.errors;
         d["http"] = http_stats_dict(s.http);
         return d;
@@ -615,6 +616,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["conflicts"] = s.conflicts;
         d["throttled"] = s.throttled;
         d["throttle_ns"] = s.throttle_ns;
+        d["speculative_skipped"] = s.speculative_skipped;
         d["http"] = http_stats_dict(s.http);
         return d;
       });

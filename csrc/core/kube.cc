@@ -48,8 +48,7 @@ void FileTokenProvider::invalidate(const std::string& used) {
 TokenBucket::TokenBucket(double qps, int burst, std::shared_ptr<Clock> clock)
     : qps_(qps), burst_(burst < 1 ? 1 : burst), tokens_(0), clock_(std::move(clock)) {}
 
-Nanos TokenBucket::reserve() {
-  std::lock_guard<std::mutex> lk(mu_);
+void TokenBucket::refill_locked() {
   const Nanos now = clock_->now();
   if (!started_) {
     started_ = true;
@@ -59,6 +58,19 @@ Nanos TokenBucket::reserve() {
     tokens_ = std::min(burst_, tokens_ + static_cast<double>(now - last_) * qps_ / 1e9);
     last_ = now;
   }
+}
+
+bool TokenBucket::try_take() {
+  std::lock_guard<std::mutex> lk(mu_);
+  refill_locked();
+  if (tokens_ < 1) return false;
+  tokens_ -= 1;
+  return true;
+}
+
+Nanos TokenBucket::reserve() {
+  std::lock_guard<std::mutex> lk(mu_);
+  refill_locked();
   tokens_ -= 1;
   if (tokens_ >= 0) return 0;
   return static_cast<Nanos>(std::ceil(-tokens_ * 1e9 / qps_));
@@ -277,7 +289,14 @@ bool KubeRestDeployments::begin_get(const std::string& name) {
   req.method = "GET";
   req.target = path_for(name);
   if (!add_auth(&req).ok()) return false;
-  throttle();
+  // A speculative read never waits for the throttle: without a free token it is skipped and
+  // the decision (if any) does the reference's own throttled GET. So the extra reads of
+  // --pipeline-reads cannot slow polls down at a fast --poll-period.
+  if (limiter_ && !limiter_->try_take()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.speculative_skipped++;
+    return false;
+  }
   if (!http_->send(req).ok()) return false;  // the synchronous GET will report the error
   {
     std::lock_guard<std::mutex> lk(mu_);

@@ -102,8 +102,11 @@ class TokenBucket {
   Nanos reserve();
   // reserve() + sleep on the clock. Returns the time waited.
   Nanos take();
+  // Takes a token only if one is available right now (never waits, never goes into debt).
+  bool try_take();
 
  private:
+  void refill_locked();
   std::mutex mu_;
   double qps_, burst_, tokens_;
   Nanos last_ = 0;
@@ -136,6 +139,7 @@ struct KubeStats {
   uint64_t conflicts = 0;
   uint64_t throttled = 0;     // requests that waited for the client-side throttle
   int64_t throttle_ns = 0;    // total time spent waiting
+  uint64_t speculative_skipped = 0;  // pipelined GETs not sent: no throttle token free
   HttpClientStats http;
 };
 

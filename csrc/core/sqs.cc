@@ -97,6 +97,7 @@ Nanos HttpSqsApi::retry_delay(int retry_count, bool throttle) {
   // capped at jitter(maxDelay/2).
   Nanos min_delay = throttle ? opts_.min_throttle_delay : opts_.min_retry_delay;
   Nanos max_delay = opts_.max_retry_delay;
+  std::lock_guard<std::mutex> lk(mu_);  // rng_ (an HttpSqsApi may be shared by workers)
   auto jitter = [&](Nanos d) -> Nanos {
     if (d <= 0) return 0;
     rng_ ^= rng_ << 13;
@@ -214,9 +215,19 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
         "EC2ThrottledException", "AWS.SimpleQueueService.RequestThrottled"};
     for (const char* tc : throttle_codes)
       if (code == tc) *throttle = true;
+    // Request.IsErrorThrottle: these statuses are throttles whatever the error code says.
+    const int st = resp.status;
+    if (st == 429 || st == 502 || st == 503 || st == 504) *throttle = true;
     if (code == "ExpiredToken" || code == "ExpiredTokenException" || code == "RequestExpired")
       *expired = true;
-    *retryable = *throttle || *expired || resp.status >= 500 || resp.status == 429;
+    // Request.IsErrorRetryable: the retryable codes, expired credentials, and HTTP 500. A 501
+    // (Not Implemented) or any other status without such a code is final.
+    static const char* retry_codes[] = {"RequestError", "RequestTimeout", "ResponseTimeout",
+                                        "RequestTimeoutException"};
+    bool retry_code = false;
+    for (const char* rc : retry_codes)
+      if (code == rc) retry_code = true;
+    *retryable = *throttle || *expired || retry_code || st == 500;
     return Result<AttrMap>::Err(
         Status::Err(aws_request_failure(code, message, resp.status, rid), resp.status));
   }
@@ -256,6 +267,7 @@ Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
     {
       std::lock_guard<std::mutex> lk(mu_);
       stats_.retries++;
+      if (throttle) stats_.throttle_retries++;
     }
     clock_->sleep(retry_delay(attempt, throttle), nullptr);
   }

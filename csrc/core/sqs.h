@@ -60,6 +60,7 @@ struct SqsHttpOptions {
 struct SqsApiStats {
   uint64_t calls = 0;
   uint64_t retries = 0;
+  uint64_t throttle_retries = 0;  // retries with the throttle back-off (429/502/503/504, throttle codes)
   uint64_t errors = 0;
   HttpClientStats http;
 };

@@ -171,9 +171,14 @@ def new_pod_autoscaler(target: TargetConfig, api, logger, clock):
 
 
 def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query", timeout_ns: int = 30 * SECOND,
-                credentials=None, environ: Optional[Mapping[str, str]] = None, tls=None, busy_poll_ns: int = 0):
+                credentials=None, environ: Optional[Mapping[str, str]] = None, tls=None, busy_poll_ns: int = 0,
+                retry_delays_ns: Optional[tuple] = None):
+    """``retry_delays_ns``: (min, min for throttles) back-off bases; default aws-sdk-go v1's
+    DefaultRetryer (30 ms / 500 ms). Tests shorten them."""
     nat = native()
     o = nat.SqsHttpOptions()
+    if retry_delays_ns is not None:
+        o.min_retry_delay_ns, o.min_throttle_delay_ns = retry_delays_ns
     o.region = region
     o.endpoint = endpoint
     o.protocol = nat.SqsProtocol.Json if protocol == "json" else nat.SqsProtocol.Query

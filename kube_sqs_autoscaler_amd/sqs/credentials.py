@@ -293,9 +293,7 @@ class RemoteProvider(_Provider):
             status, body = self.http("GET", url, headers, b"", 5.0)
             if status != 200:
                 raise CredentialsError(f"CredentialsEndpointError: failed to load credentials (HTTP {status})")
-            j = json.loads(body)
-            return _make(j["AccessKeyId"], j["SecretAccessKey"], j.get("Token", ""),
-                         parse_expiration(j["Expiration"]) if j.get("Expiration") else 0, self.name)
+            return self._parse(body, "CredentialsEndpointError")
         if self.env.get("AWS_EC2_METADATA_DISABLED", "").lower() == "true":
             raise CredentialsError("EC2RoleRequestError: EC2 IMDS access disabled via AWS_EC2_METADATA_DISABLED")
         base = self.imds.rstrip("/")
@@ -317,11 +315,20 @@ class RemoteProvider(_Provider):
         status, body = self.http("GET", base + "/latest/meta-data/iam/security-credentials/" + role, headers, b"", 1.0)
         if status != 200:
             raise CredentialsError(f"EC2RoleRequestError: failed to get {role} EC2 instance role credentials")
-        j = json.loads(body)
-        if j.get("Code", "Success") != "Success":
-            raise CredentialsError(f"EC2RoleRequestError: {j.get('Code')}: {j.get('Message', '')}")
-        return _make(j["AccessKeyId"], j["SecretAccessKey"], j.get("Token", ""),
-                     parse_expiration(j["Expiration"]) if j.get("Expiration") else 0, self.name)
+        return self._parse(body, "EC2RoleRequestError")
+
+    def _parse(self, body: bytes, err: str):
+        """The ECS / IMDS credentials document; anything malformed is a CredentialsError."""
+        try:
+            j = json.loads(body)
+            if j.get("Code", "Success") != "Success":
+                raise CredentialsError(f"{err}: {j.get('Code')}: {j.get('Message', '')}")
+            return _make(j["AccessKeyId"], j["SecretAccessKey"], j.get("Token", "") or "",
+                         parse_expiration(j["Expiration"]) if j.get("Expiration") else 0, self.name)
+        except CredentialsError:
+            raise
+        except (ValueError, KeyError, TypeError, AttributeError) as e:
+            raise CredentialsError(f"{err}: malformed credentials response: {e!r}")
 
 
 def _truthy(v: Optional[str]) -> bool:

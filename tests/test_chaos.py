@@ -16,7 +16,7 @@ AKID, SECRET, REGION, TOKEN = "AKIDCHAOS", "chaos-secret", "us-east-1", "chaos-t
 def make_loop(nat, sqs, kube, mode, prefetch, timeout_ns=2 * 10**9, lines=None):
     url = sqs.url + "/1/chaos"
     api = new_sqs_api(REGION, nat.RealClock(), endpoint=sqs.url, credentials=static_provider(AKID, SECRET),
-                      timeout_ns=timeout_ns)
+                      timeout_ns=timeout_ns, retry_delays_ns=(1_000_000, 5_000_000))  # SDK back-off, shortened
     client = nat.SqsClient(api, url, ["ApproximateNumberOfMessages"])
     dep = new_deployment_api(RestConfig(host=kube.url, bearer_token=TOKEN), "ml", mode, timeout_ns)
     log = capture_logger(lines if lines is not None else [])

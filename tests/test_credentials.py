@@ -214,3 +214,15 @@ def test_sts_regional_endpoints_from_shared_config(tmp_path, nat):
     env = {"AWS_CONFIG_FILE": str(tmp_path / "config"), "AWS_SHARED_CREDENTIALS_FILE": str(tmp_path / "none"),
            "AWS_SDK_LOAD_CONFIG": "true"}
     assert cr.resolve_sts_endpoint(cr.session_region(env, "us-east-1"), env) == ("https://sts.eu-west-2.amazonaws.com", "eu-west-2")
+
+
+@pytest.mark.parametrize("body", [b"not json", b"[]", b'{"AccessKeyId": "A"}', b'{"Code": "Failure", "Message": "no role"}'])
+def test_malformed_remote_credentials_are_credential_errors(nat, body):
+    """A broken ECS / IMDS credentials document surfaces as a CredentialsError (logged per poll),
+    never as a stray exception from the provider chain."""
+    def fetch(method, url, headers, b, timeout):
+        return 200, body
+
+    p = cr.RemoteProvider({"AWS_CONTAINER_CREDENTIALS_FULL_URI": "http://169.254.170.2/creds"}, fetch)
+    with pytest.raises(cr.CredentialsError):
+        p.fetch()

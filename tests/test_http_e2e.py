@@ -73,10 +73,29 @@ def test_sdk_style_retries_on_5xx(nat, sqs_server):
     sqs_server.set_attributes(url, ATTRS)
     sqs_server.inject(2, nat.InjectedFault(500, "oops"))
     assert c.num_messages() == 18  # DefaultRetryer: up to 3 retries
-    assert api.stats()["retries"] == 2
-    sqs_server.inject(4, nat.InjectedFault(503, "down"))
+    assert api.stats()["retries"] == 2 and api.stats()["throttle_retries"] == 0
+    sqs_server.inject(4, nat.InjectedFault(500, "down"))
     with pytest.raises(nat.NativeError):
         c.num_messages()
+    assert api.stats()["retries"] == 5  # 3 more: DefaultRetryer.NumMaxRetries
+
+
+@pytest.mark.parametrize("status,retried,throttled", [
+    (503, True, True), (502, True, True), (504, True, True), (429, True, True),  # IsErrorThrottle
+    (500, True, False),                                                          # IsErrorRetryable
+    (501, False, False), (505, False, False), (403, False, False),                # final
+])
+def test_retry_classification_like_aws_sdk_go_v1(nat, sqs_server, status, retried, throttled):
+    c, api, url = sqs_client(nat, sqs_server)
+    sqs_server.set_attributes(url, ATTRS)
+    sqs_server.inject(1, nat.InjectedFault(status, "x"))
+    if retried:
+        assert c.num_messages() == 18
+    else:
+        with pytest.raises(nat.NativeError):
+            c.num_messages()
+    st = api.stats()
+    assert (st["retries"], st["throttle_retries"]) == (int(retried), int(throttled))
 
 
 def test_no_retry_on_4xx(nat, sqs_server):

@@ -87,3 +87,33 @@ def test_throttled_loop_keeps_reference_decisions(nat):
         assert api.stats()["throttled"] >= 10
     finally:
         env.close()
+
+
+def test_speculative_read_never_waits_for_the_throttle(nat):
+    """--pipeline-reads sends a GET with every poll, which the reference does not. Once the bucket
+    is empty the speculative GET is skipped rather than delayed, and only the reference's own
+    GET (when a decision needs one) waits."""
+    from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
+
+    env = BenchEnv(1)
+    try:
+        rc = RestConfig(host=env.kube.url, bearer_token="bench-bearer-token")
+        api = new_deployment_api(rc, "bench", "scale", 5 * S, qps=1.0, burst=3)
+        scaler = nat.PodAutoScaler(api, "gpu-worker-0", "bench", 8, 1, 1, 1, env.log, env.clock)
+        cfg = nat.LoopConfig()
+        cfg.poll_period_ns = 0
+        cfg.scale_up_cool_down_ns = 3600 * S  # every poll is a cool-down skip: no GET needed
+        cfg.scale_down_cool_down_ns = 3600 * S
+        cfg.scale_up_messages = 100
+        cfg.scale_down_messages = 10
+        cfg.prefetch = True
+        r = nat.Runner(cfg, env.runners[0].sqs, scaler, env.clock, env.log)
+        r.arm()
+        t0 = time.perf_counter()
+        recs = [r.poll_once() for _ in range(20)]
+        assert time.perf_counter() - t0 < 0.5  # no poll waited for a token
+        st = api.stats()
+        assert sum(x["prefetched"] for x in recs) == 3 and st["speculative_skipped"] == 17
+        assert st["throttled"] == 0
+    finally:
+        env.close()
