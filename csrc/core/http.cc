@@ -455,6 +455,54 @@ bool is_ip_literal(const std::string& h) {
   return inet_pton(AF_INET, h.c_str(), buf) == 1 || inet_pton(AF_INET6, h.c_str(), buf) == 1;
 }
 
+// getaddrinfo(3) has no timeout, so a stuck resolver would hold a worker far past
+// --api-timeout (Go's dialer bounds the lookup by the request's context). Names are resolved on
+// a helper thread and the caller stops waiting at the deadline; a late answer is freed by the
+// helper. IP literals (and calls without a deadline) resolve inline.
+Status resolve(const std::string& host, const std::string& port, int64_t deadline_ns, struct addrinfo** out) {
+  struct addrinfo hints;
+  std::memset(&hints, 0, sizeof hints);
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  const bool literal = is_ip_literal(host);
+  if (literal || deadline_ns == 0) {
+    if (literal) hints.ai_flags = AI_NUMERICHOST;
+    int gai = getaddrinfo(host.c_str(), port.c_str(), &hints, out);
+    if (gai != 0) return Status::Err("dial tcp: lookup " + host + ": " + gai_strerror(gai));
+    return Status::OK();
+  }
+  struct Lookup {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    int rc = 0;
+    struct addrinfo* res = nullptr;
+  };
+  auto st = std::make_shared<Lookup>();
+  std::thread([st, host, port, hints] {
+    struct addrinfo* r = nullptr;
+    const int rc = getaddrinfo(host.c_str(), port.c_str(), &hints, &r);
+    std::lock_guard<std::mutex> lk(st->mu);
+    if (st->abandoned) {
+      if (r) freeaddrinfo(r);
+      return;
+    }
+    st->rc = rc;
+    st->res = r;
+    st->done = true;
+    st->cv.notify_all();
+  }).detach();
+  std::unique_lock<std::mutex> lk(st->mu);
+  const int64_t left = deadline_ns - mono_ns();
+  if (left <= 0 || !cv_wait_for(st->cv, lk, left, [&] { return st->done; })) {
+    st->abandoned = true;
+    return Status::Err("dial tcp: lookup " + host + ": i/o timeout");
+  }
+  if (st->rc != 0) return Status::Err("dial tcp: lookup " + host + ": " + gai_strerror(st->rc));
+  *out = st->res;
+  return Status::OK();
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -629,15 +677,9 @@ Status HttpClient::set_proxy(const std::string& proxy_url) {
 }
 
 Status HttpClient::dial(const Url& to, int64_t deadline_ns, int* fd_out) {
-  struct addrinfo hints;
-  std::memset(&hints, 0, sizeof hints);
-  hints.ai_family = AF_UNSPEC;
-  hints.ai_socktype = SOCK_STREAM;
   struct addrinfo* res = nullptr;
-  std::string port = std::to_string(to.port);
-  int gai = getaddrinfo(to.host.c_str(), port.c_str(), &hints, &res);
-  if (gai != 0)
-    return Status::Err("dial tcp: lookup " + to.host + ": " + gai_strerror(gai));
+  Status rs = resolve(to.host, std::to_string(to.port), deadline_ns, &res);
+  if (!rs.ok()) return rs;
   Status last = Status::Err("dial tcp " + to.host_header() + ": no addresses");
   int fd = -1;
   for (auto* ai = res; ai; ai = ai->ai_next) {

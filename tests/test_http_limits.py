@@ -52,3 +52,23 @@ def test_client_bounds_hostile_responses(nat, payload, trickle, msg):
         c.close()
     finally:
         srv.close()
+
+
+def test_hostname_resolution_works_and_is_bounded(nat):
+    """Names resolve on a helper thread bounded by the call deadline (getaddrinfo has none)."""
+    import time
+
+    kube = nat.FakeKubeServer()
+    kube.start()
+    try:
+        kube.add_deployment("ml", "w", 2)
+        c = nat.HttpClient(f"http://localhost:{kube.port}", nat.TlsOptions(), 5 * nat.SECOND)
+        status, _, body = c.request("GET", "/apis/apps/v1/namespaces/ml/deployments/w/scale", [], b"")
+        assert status == 200 and b'"replicas":2' in body
+    finally:
+        kube.stop()
+    c = nat.HttpClient("http://ksa-no-such-host.invalid:80", nat.TlsOptions(), 500_000_000)
+    t0 = time.perf_counter()
+    with pytest.raises(nat.NativeError, match="lookup ksa-no-such-host.invalid"):
+        c.request("GET", "/", [], b"")
+    assert time.perf_counter() - t0 < 2.0
