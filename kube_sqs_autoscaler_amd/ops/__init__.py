@@ -25,6 +25,12 @@ class NativeUnavailable(RuntimeError):
     """The C++ runtime could not be built or imported."""
 
 
+def _sources_present() -> bool:
+    from pathlib import Path
+
+    return (Path(__file__).resolve().parents[2] / "csrc" / "core").is_dir()
+
+
 def native() -> ModuleType:
     """Returns the ``_ksa_native`` module, building it in-tree if needed."""
     global _mod
@@ -33,7 +39,8 @@ def native() -> ModuleType:
     with _lock:
         if _mod is not None:
             return _mod
-        if os.environ.get("KSA_NO_AUTOBUILD") != "1":
+        # An installed copy (wheel) ships the built module and no csrc/: nothing to build.
+        if os.environ.get("KSA_NO_AUTOBUILD") != "1" and _sources_present():
             from . import build
 
             try:
