@@ -134,6 +134,8 @@ class Stream {
       }
       int e = SSL_get_error(ssl_, r);
       if (e == SSL_ERROR_WANT_READ) {
+        // Busy-poll applies to TLS too: the record's bytes land on the raw socket.
+        if (spin_ns_ > 0 && spin_for_data()) continue;
         Status s = wait_fd(fd_, POLLIN, deadline_ns);
         if (!s.ok()) return s;
       } else if (e == SSL_ERROR_WANT_WRITE) {
