@@ -628,6 +628,9 @@ HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
     ctx_status_ = use_cert_key(ctx_, tls_.cert_pem, tls_.key_pem);
   // Session resumption makes reconnects after an idle close cheap.
   SSL_CTX_set_session_cache_mode(ctx_, SSL_SESS_CACHE_CLIENT);
+  // Read-ahead: pull whatever the socket holds in one read(2) instead of a 5-byte record
+  // header and then the body -- one syscall less per response record on the hot path.
+  SSL_CTX_set_read_ahead(ctx_, 1);
   // Peers (AWS endpoints included) often close idle keep-alive connections without
   // close_notify; treat that as a plain EOF instead of a protocol error.
 #ifdef SSL_OP_IGNORE_UNEXPECTED_EOF
