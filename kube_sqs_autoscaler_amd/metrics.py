@@ -42,7 +42,14 @@ _API_COUNTERS = [
     ("sqs_calls", "GetQueueAttributes calls (including SDK-style retries)", "sqs_api", "calls"),
     ("sqs_retries", "GetQueueAttributes retries", "sqs_api", "retries"),
     ("sqs_errors", "GetQueueAttributes calls that failed", "sqs_api", "errors"),
+    ("sqs_throttle_retries", "Retries with the throttle back-off (429/502/503/504 or a throttling code)", "sqs_api",
+     "throttle_retries"),
+    ("apiserver_throttled", "Requests that waited for the client-side --kube-api-qps throttle", "kube_api", "throttled"),
+    ("apiserver_throttle_seconds", "Time spent waiting for the client-side throttle", "kube_api", "throttle_ns"),
+    ("speculative_reads_skipped", "Pipelined GETs not sent because no throttle token was free", "kube_api",
+     "speculative_skipped"),
 ]
+_NS_COUNTERS = {"throttle_ns"}  # exported in seconds
 
 
 def _client_stats(client) -> dict:
@@ -71,7 +78,8 @@ class FleetCollector:
             clients = {a: _client_stats(getattr(w, a, None)) for a in ("kube_api", "sqs_api")}
             for k, _, attr, key in _API_COUNTERS:
                 if key in clients[attr]:
-                    api[k].add_metric(lv, clients[attr][key])
+                    v = clients[attr][key]
+                    api[k].add_metric(lv, v / 1e9 if key in _NS_COUNTERS else v)
             depth.add_metric(lv, s["last_depth"])
             reps.add_metric(lv, s["last_replicas"])
             samples = w.runner.latencies()

@@ -75,6 +75,8 @@ def test_metrics_endpoints(nat):
             assert metric["ksa_speculative_reads_total"] == 10 == metric["ksa_speculative_reads_used_total"]
             assert metric["ksa_sqs_calls_total"] == 10 and metric["ksa_apiserver_writes_total"] == 10
             assert metric["ksa_apiserver_gets_total"] == 10 and metric["ksa_apiserver_conflicts_total"] == 0
+            assert metric["ksa_apiserver_throttled_total"] == 0 and metric["ksa_apiserver_throttle_seconds_total"] == 0
+            assert metric["ksa_sqs_throttle_retries_total"] == 0 and metric["ksa_speculative_reads_skipped_total"] == 0
             assert urllib.request.urlopen(base + "/readyz").read() == b"ok"
             assert urllib.request.urlopen(base + "/healthz").status == 200
         finally:
