@@ -584,7 +584,7 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<TokenBucket>(m, "TokenBucket")
       .def(py::init<double, int, std::shared_ptr<Clock>>(), py::arg("qps"), py::arg("burst"), py::arg("clock"))
       .def("reserve", &TokenBucket::reserve)
-      .def("take", &TokenBucket::take, py::call_guard<py::gil_scoped_release>());
+      .def("take", [](TokenBucket& b) { return b.take(nullptr); }, py::call_guard<py::gil_scoped_release>());
 
   py::class_<DeploymentApi, PyDeploymentApi, py::smart_holder>(m, "DeploymentApi")
       .def(py::init<>())

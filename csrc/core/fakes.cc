@@ -11,10 +11,6 @@ namespace ksa {
 
 namespace {
 
-void sleep_ns(Nanos d) {
-  if (d > 0) std::this_thread::sleep_for(std::chrono::nanoseconds(d));
-}
-
 bool pop_fault(std::vector<InjectedFault>* faults, InjectedFault* out) {
   if (faults->empty()) return false;
   *out = faults->front();
@@ -71,6 +67,7 @@ Status FakeSqsServer::start(const std::string& host, int port, bool tls) {
 }
 
 void FakeSqsServer::stop() {
+  shutdown_.request_stop();
   if (server_) server_->stop();
 }
 
@@ -143,7 +140,7 @@ void FakeSqsServer::handle(const HttpRequest& req, HttpResponse* resp) {
     secret = secret_;
     region = region_;
   }
-  sleep_ns(latency);
+  if (latency > 0) shutdown_.wait_for(latency);
   if (faulted) {
     apply_fault(fault, resp);
     return;
@@ -269,6 +266,7 @@ Status FakeKubeServer::start(const std::string& host, int port, bool tls) {
 }
 
 void FakeKubeServer::stop() {
+  shutdown_.request_stop();
   if (server_) server_->stop();
 }
 
@@ -545,7 +543,7 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
     faulted = pop_fault(&faults_, &fault);
     token = token_;
   }
-  sleep_ns(latency);
+  if (latency > 0) shutdown_.wait_for(latency);
   if (faulted) {
     apply_fault(fault, resp);
     return;

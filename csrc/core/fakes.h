@@ -62,6 +62,7 @@ class FakeSqsServer {
   void handle(const HttpRequest& req, HttpResponse* resp);
 
   std::unique_ptr<HttpServer> server_;
+  StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;
   mutable std::mutex mu_;
@@ -133,6 +134,7 @@ class FakeKubeServer {
   static std::string status_json(int code, const std::string& reason, const std::string& message);
 
   std::unique_ptr<HttpServer> server_;
+  StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;
   mutable std::mutex mu_;

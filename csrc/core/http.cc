@@ -15,6 +15,7 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <poll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -88,8 +89,9 @@ std::string ssl_error_string() {
   return buf;
 }
 
-// Waits for `events` on fd until the absolute deadline (0 = forever).
-Status wait_fd(int fd, short events, int64_t deadline_ns) {
+// Waits for `events` on fd until the absolute deadline (0 = forever). A readable `cancel_fd`
+// (HttpClient::cancel) ends the wait with "request canceled".
+Status wait_fd(int fd, short events, int64_t deadline_ns, int cancel_fd = -1) {
   while (true) {
     int timeout_ms = -1;
     if (deadline_ns) {
@@ -97,8 +99,9 @@ Status wait_fd(int fd, short events, int64_t deadline_ns) {
       if (left <= 0) return Status::Err("i/o timeout");
       timeout_ms = static_cast<int>((left + 999999) / 1000000);
     }
-    struct pollfd p{fd, events, 0};
-    int r = ::poll(&p, 1, timeout_ms);
+    struct pollfd p[2] = {{fd, events, 0}, {cancel_fd, POLLIN, 0}};
+    int r = ::poll(p, cancel_fd >= 0 ? 2 : 1, timeout_ms);
+    if (r > 0 && cancel_fd >= 0 && (p[1].revents & POLLIN)) return Status::Err("request canceled");
     if (r > 0) return Status::OK();
     if (r == 0) {
       if (deadline_ns && mono_ns() >= deadline_ns) return Status::Err("i/o timeout");
@@ -136,10 +139,10 @@ class Stream {
       if (e == SSL_ERROR_WANT_READ) {
         // Busy-poll applies to TLS too: the record's bytes land on the raw socket.
         if (spin_ns_ > 0 && spin_for_data()) continue;
-        Status s = wait_fd(fd_, POLLIN, deadline_ns);
+        Status s = wait_fd(fd_, POLLIN, deadline_ns, cancel_fd_);
         if (!s.ok()) return s;
       } else if (e == SSL_ERROR_WANT_WRITE) {
-        Status s = wait_fd(fd_, POLLOUT, deadline_ns);
+        Status s = wait_fd(fd_, POLLOUT, deadline_ns, cancel_fd_);
         if (!s.ok()) return s;
       } else if (e == SSL_ERROR_ZERO_RETURN) {
         *out = 0;
@@ -186,7 +189,7 @@ class Stream {
       if (errno == EINTR) continue;
       if (errno == EAGAIN || errno == EWOULDBLOCK) {
         if (spin_ns_ > 0 && spin_for_data()) continue;
-        Status s = wait_fd(fd_, POLLIN, deadline_ns);
+        Status s = wait_fd(fd_, POLLIN, deadline_ns, cancel_fd_);
         if (!s.ok()) return s;
         continue;
       }
@@ -218,7 +221,7 @@ class Stream {
       }
       if (n < 0 && errno == EINTR) continue;
       if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        Status s = wait_fd(fd_, POLLOUT, deadline_ns);
+        Status s = wait_fd(fd_, POLLOUT, deadline_ns, cancel_fd_);
         if (!s.ok()) return s;
         continue;
       }
@@ -228,6 +231,7 @@ class Stream {
   }
 
   void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
+  void set_cancel_fd(int fd) { cancel_fd_ = fd; }
   SSL* ssl() const { return ssl_; }
   void attach_ssl(SSL* ssl) { ssl_ = ssl; }  // TLS inside an established CONNECT tunnel
 
@@ -252,6 +256,7 @@ class Stream {
   int fd_;
   SSL* ssl_;
   int64_t spin_ns_ = 0;
+  int cancel_fd_ = -1;
 };
 
 // Largest message body either side accepts. Scale objects and Deployments are a few KiB and a
@@ -602,6 +607,7 @@ struct HttpClient::Conn {
 
 HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
     : origin_(origin), tls_(std::move(tls)), timeout_(timeout) {
+  cancel_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   if (!origin_.tls()) return;
   ensure_ssl();
   ignore_sigpipe_once();
@@ -640,6 +646,7 @@ HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
 
 HttpClient::~HttpClient() {
   conn_.reset();
+  if (cancel_fd_ >= 0) ::close(cancel_fd_);
   if (session_) SSL_SESSION_free(session_);
   if (ctx_) SSL_CTX_free(ctx_);
 }
@@ -647,6 +654,16 @@ HttpClient::~HttpClient() {
 void HttpClient::close() {
   std::lock_guard<std::mutex> lk(mu_);
   conn_.reset();
+}
+
+void HttpClient::cancel() {
+  // Lock-free on purpose: the request being cancelled holds mu_ while it waits.
+  cancelled_.store(true, std::memory_order_release);
+  if (cancel_fd_ >= 0) {
+    const uint64_t one = 1;
+    ssize_t r = ::write(cancel_fd_, &one, sizeof one);
+    (void)r;
+  }
 }
 
 HttpClientStats HttpClient::stats() const {
@@ -694,7 +711,7 @@ Status HttpClient::dial(const Url& to, int64_t deadline_ns, int* fd_out) {
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     int r = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
     if (r != 0 && errno == EINPROGRESS) {
-      Status w = wait_fd(fd, POLLOUT, deadline_ns);
+      Status w = wait_fd(fd, POLLOUT, deadline_ns, cancel_fd_);
       int err = 0;
       socklen_t len = sizeof err;
       getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
@@ -722,6 +739,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   Status d = dial(has_proxy_ ? proxy_ : origin_, deadline_ns, &fd);
   if (!d.ok()) return has_proxy_ ? Status::Err("proxyconnect tcp: " + d.message()) : d;
   auto stream = std::make_unique<Stream>(fd, nullptr);
+  stream->set_cancel_fd(cancel_fd_);
   std::string rbuf;
   if (has_proxy_ && origin_.tls()) {
     // CONNECT tunnel: the proxy relays bytes; TLS (and its verification) is end to end.
@@ -922,11 +940,12 @@ Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t d
 Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) {
   std::lock_guard<std::mutex> lk(mu_);
   if (in_flight_) return Status::Err("http: a pipelined request is still in flight");
+  if (cancelled()) return Status::Err("request canceled");
   const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
   stats_.requests++;
   bool retryable = false;
   Status s = attempt(req, resp, deadline, &retryable);
-  if (!s.ok() && retryable) {
+  if (!s.ok() && retryable && !cancelled()) {
     stats_.reconnect_retries++;
     s = attempt(req, resp, deadline, &retryable);
   }
@@ -936,11 +955,12 @@ Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) {
 Status HttpClient::send(const HttpRequest& req) {
   std::lock_guard<std::mutex> lk(mu_);
   if (in_flight_) return Status::Err("http: a pipelined request is still in flight");
+  if (cancelled()) return Status::Err("request canceled");
   const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
   stats_.requests++;
   bool retryable = false;
   Status s = write_request(req, deadline, &retryable);
-  if (!s.ok() && retryable) {
+  if (!s.ok() && retryable && !cancelled()) {
     stats_.reconnect_retries++;
     s = write_request(req, deadline, &retryable);
   }
@@ -957,7 +977,7 @@ Status HttpClient::receive(HttpResponse* resp) {
   in_flight_ = false;
   bool retryable = false;
   Status s = read_response(pending_, resp, pending_deadline_, &retryable);
-  if (!s.ok() && retryable) {  // the reused connection was dead: replay on a fresh one
+  if (!s.ok() && retryable && !cancelled()) {  // the reused connection was dead: replay on a fresh one
     stats_.reconnect_retries++;
     s = attempt(pending_, resp, pending_deadline_, &retryable);
   }

@@ -97,6 +97,10 @@ class HttpClient {
   Status receive(HttpResponse* resp);
   bool in_flight() const;
   void close();
+  // Aborts any request in progress ("request canceled") and every later one: graceful shutdown
+  // must not wait for a slow or hung peer (the in-flight call's timeout can be 30 s). Sticky.
+  void cancel();
+  bool cancelled() const { return cancelled_.load(std::memory_order_acquire); }
   HttpClientStats stats() const;
   const Url& origin() const { return origin_; }
   void set_timeout(Nanos t) { timeout_ = t; }
@@ -143,6 +147,8 @@ class HttpClient {
   Url proxy_;
   std::string proxy_auth_;  // "Basic ..." or empty
   bool in_flight_ = false;
+  int cancel_fd_ = -1;  // eventfd signalled by cancel(); polled next to the socket
+  std::atomic<bool> cancelled_{false};
   HttpRequest pending_;
   int64_t pending_deadline_ = 0;
 };

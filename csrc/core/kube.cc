@@ -76,9 +76,9 @@ Nanos TokenBucket::reserve() {
   return static_cast<Nanos>(std::ceil(-tokens_ * 1e9 / qps_));
 }
 
-Nanos TokenBucket::take() {
+Nanos TokenBucket::take(StopFlag* stop) {
   const Nanos wait = reserve();
-  if (wait > 0) clock_->sleep(wait, nullptr);
+  if (wait > 0) clock_->sleep(wait, stop);
   return wait;
 }
 
@@ -146,9 +146,14 @@ KubeRestDeployments::KubeRestDeployments(KubeOptions opts) : opts_(std::move(opt
   }
 }
 
+void KubeRestDeployments::cancel() {
+  cancel_.request_stop();
+  if (http_) http_->cancel();
+}
+
 void KubeRestDeployments::throttle() {
   if (!limiter_) return;
-  const Nanos waited = limiter_->take();
+  const Nanos waited = limiter_->take(&cancel_);
   if (waited > 0) {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.throttled++;

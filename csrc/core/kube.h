@@ -52,6 +52,8 @@ class DeploymentApi {
   virtual Result<ScaleObject> finish_get() {
     return Result<ScaleObject>::Err(Status::Err("no pipelined GET in flight"));
   }
+  // Shutdown: abort the request in progress and any throttle wait (sticky). Default: nothing.
+  virtual void cancel() {}
 };
 
 class TokenProvider {
@@ -100,8 +102,8 @@ class TokenBucket {
   TokenBucket(double qps, int burst, std::shared_ptr<Clock> clock);
   // Reserves one token; returns how long the caller must wait before using it.
   Nanos reserve();
-  // reserve() + sleep on the clock. Returns the time waited.
-  Nanos take();
+  // reserve() + sleep on the clock (interrupted by `stop`). Returns the time waited.
+  Nanos take(StopFlag* stop = nullptr);
   // Takes a token only if one is available right now (never waits, never goes into debt).
   bool try_take();
 
@@ -151,6 +153,7 @@ class KubeRestDeployments final : public DeploymentApi {
   bool begin_get(const std::string& name) override;
   Result<ScaleObject> finish_get() override;
   KubeStats stats() const;
+  void cancel() override;
   std::string path_for(const std::string& name) const;
 
  private:
@@ -169,6 +172,7 @@ class KubeRestDeployments final : public DeploymentApi {
   Url url_;
   std::unique_ptr<HttpClient> http_;
   std::unique_ptr<TokenBucket> limiter_;
+  StopFlag cancel_;
   void throttle();
   mutable std::mutex mu_;
   KubeStats stats_;
@@ -258,6 +262,7 @@ class PodAutoScaler {
   bool prefetch_pending() const { return prefetch_pending_; }
 
   std::shared_ptr<DeploymentApi> api() const { return api_; }
+  void cancel() { api_->cancel(); }
   const std::string& deployment() const { return deployment_; }
   const std::string& namespace_() const { return ns_; }
   int64_t max() const { return max_.load(std::memory_order_relaxed); }

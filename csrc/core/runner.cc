@@ -276,7 +276,7 @@ void Supervisor::join() {
 }
 
 Supervisor::~Supervisor() {
-  stop();
+  stop_.request_stop();  // no cancel(): the clients may outlive this supervisor and be reused
   join();
 }
 
@@ -286,7 +286,11 @@ Scheduler::Scheduler(size_t threads, std::shared_ptr<Clock> clock, bool stagger)
     : nthreads_(threads < 1 ? 1 : threads), clock_(std::move(clock)), stagger_(stagger) {}
 
 Scheduler::~Scheduler() {
-  stop();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_.store(true);  // no cancel(): the clients may outlive this scheduler and be reused
+  }
+  cv_.notify_all();
   join();
 }
 
@@ -362,6 +366,7 @@ void Scheduler::stop() {
     stop_.store(true);
   }
   cv_.notify_all();
+  for (auto& r : runners_) r->cancel();  // in-flight polls end now instead of at their timeout
 }
 
 bool Scheduler::wait(Nanos timeout) {

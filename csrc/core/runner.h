@@ -99,6 +99,11 @@ class Runner {
   // The iteration without the leading sleep (main.go:43-77); used by Scheduler, which owns
   // the waiting between polls.
   IterationRecord poll_once();
+  // Shutdown: aborts this worker's API call in progress and its back-off/throttle waits.
+  void cancel() {
+    sqs_->cancel();
+    scaler_->cancel();
+  }
   // The reference's Run(): arm(), then step() until stopped (or max_iterations > 0 reached).
   void run(StopFlag* stop, int64_t max_iterations = -1);
 
@@ -147,7 +152,12 @@ class Supervisor {
   void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
   // Starts one thread per runner; each arms its timers then loops.
   void start(int64_t max_iterations = -1);
-  void stop() { stop_.request_stop(); }
+  // Stop request: interrupts poll sleeps and cancels every worker's in-flight API call, so a
+  // SIGTERM does not wait for a slow or hung endpoint (the call's own timeout can be 30 s).
+  void stop() {
+    stop_.request_stop();
+    for (auto& r : runners_) r->cancel();
+  }
   bool stopped() const { return stop_.stopped(); }
   // Waits up to `timeout` (<= 0: forever); true when every runner thread has exited.
   bool wait(Nanos timeout);

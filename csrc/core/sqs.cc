@@ -85,6 +85,11 @@ HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider>
   if (!ps.ok()) endpoint_status_ = ps;
 }
 
+void HttpSqsApi::cancel() {
+  cancel_.request_stop();
+  if (http_) http_->cancel();
+}
+
 SqsApiStats HttpSqsApi::stats() const {
   std::lock_guard<std::mutex> lk(mu_);
   SqsApiStats s = stats_;
@@ -262,14 +267,14 @@ Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
   for (int attempt = 0;; ++attempt) {
     bool retryable, throttle, expired;
     r = call_once(queue_url, names, &retryable, &throttle, &expired);
-    if (r.ok() || !retryable || attempt >= opts_.max_retries) break;
+    if (r.ok() || !retryable || attempt >= opts_.max_retries || cancel_.stopped()) break;
     if (expired) creds_.invalidate();
     {
       std::lock_guard<std::mutex> lk(mu_);
       stats_.retries++;
       if (throttle) stats_.throttle_retries++;
     }
-    clock_->sleep(retry_delay(attempt, throttle), nullptr);
+    if (!clock_->sleep(retry_delay(attempt, throttle), &cancel_)) break;  // cancelled mid back-off
   }
   if (!r.ok()) {
     std::lock_guard<std::mutex> lk(mu_);

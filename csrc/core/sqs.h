@@ -39,6 +39,8 @@ class SqsApi {
   virtual ~SqsApi() = default;
   virtual Result<AttrMap> get_queue_attributes(const std::string& queue_url,
                                                const std::vector<std::string>& names) = 0;
+  // Shutdown: abort the call in progress and any retry back-off (sticky). Default: nothing.
+  virtual void cancel() {}
 };
 
 enum class SqsProtocol { Query, Json };
@@ -72,6 +74,7 @@ class HttpSqsApi final : public SqsApi {
   Result<AttrMap> get_queue_attributes(const std::string& queue_url,
                                        const std::vector<std::string>& names) override;
   SqsApiStats stats() const;
+  void cancel() override;
   // Regional endpoint aws-sdk-go would resolve for `region` ("" if region is empty).
   static std::string endpoint_for_region(const std::string& region);
   static std::string signing_region(const std::string& region);
@@ -99,6 +102,7 @@ class HttpSqsApi final : public SqsApi {
   mutable std::mutex mu_;
   SqsApiStats stats_;
   uint64_t rng_ = 0x9E3779B97F4A7C15ULL;
+  StopFlag cancel_;  // cancel(): interrupts retry back-off sleeps
 };
 
 // In-memory fake, the MockSQS of /root/reference/sqs/sqs_test.go:27-59: returns the stored
@@ -150,6 +154,7 @@ class SqsClient {
   const std::string& queue_url() const { return queue_url_; }
   const std::vector<std::string>& attribute_names() const { return names_; }
   std::shared_ptr<SqsApi> api() const { return api_; }
+  void cancel() { api_->cancel(); }
 
  private:
   std::shared_ptr<SqsApi> api_;

@@ -197,3 +197,26 @@ def test_health_budget_covers_retries():
     from kube_sqs_autoscaler_amd.metrics import Health
 
     assert Health.budget_ns(5 * 10**9, 30 * 10**9) == (5 + 240 + 60) * 10**9
+
+
+@pytest.mark.parametrize("pooled", [False, True])
+def test_stop_cancels_in_flight_calls(nat, pooled):
+    """SIGTERM path: stopping the fleet aborts a worker's in-flight SQS call ("request canceled")
+    instead of waiting for its 30 s timeout, so the process exits well inside the pod's grace
+    period. (The reference has no graceful shutdown at all, main.go:36.)"""
+    import time
+
+    env = BenchEnv(2, sqs_latency_ns=20 * 10**9)  # the fake sits on every SQS call for 20 s
+    try:
+        fleet = Fleet([W(*a) for a in zip(env.runners, env.targets, env.kube_apis, env.sqs_apis)],
+                      threads=1 if pooled else 0)
+        fleet.start()
+        time.sleep(0.3)  # both workers are now blocked inside GetQueueAttributes
+        t0 = time.perf_counter()
+        fleet.stop()
+        assert fleet.wait(5)
+        fleet.join()
+        assert time.perf_counter() - t0 < 2.0
+        assert all(s["depth_errors"] >= 1 for s in fleet.stats()[: 1 if pooled else 2])
+    finally:
+        env.close()
