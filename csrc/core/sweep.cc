@@ -61,4 +61,54 @@ void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
   for (auto& th : pool) th.join();
 }
 
+void queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
+                     int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params, int64_t m,
+                     int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, int threads) {
+  const int64_t lanes = m * seeds;
+  if (lanes <= 0 || n < 1) return;
+  const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+  const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
+  auto work = [&](int64_t lo, int64_t hi) {
+    for (int64_t l = lo; l < hi; ++l) {
+      const int64_t i = l / seeds;
+      const int32_t s = static_cast<int32_t>(l - i * seeds);
+      ksa_sim::Params p;
+      p.poll_ns = params[0 * m + i];
+      p.up_cool_ns = params[1 * m + i];
+      p.down_cool_ns = params[2 * m + i];
+      p.up_msgs = params[3 * m + i];
+      p.down_msgs = params[4 * m + i];
+      p.up_pods = params[5 * m + i];
+      p.down_pods = params[6 * m + i];
+      p.max_pods = params[7 * m + i];
+      p.min_pods = params[8 * m + i];
+      const ksa_sim::QueueResult r = ksa_sim::simulate_queue(p, lat, qm, t_ms, rate_milli, n, init_replicas, horizon_ns,
+                                                             seed0 + static_cast<uint64_t>(s));
+      const int64_t o64[7] = {r.pod_ms, r.backlog_msg_ms, r.violation_ms, r.peak_backlog, r.arrived, r.served,
+                              r.final_backlog};
+      const int32_t o32[5] = {r.ups, r.downs, r.final_replicas, r.max_replicas, r.polls};
+      for (int f = 0; f < 7; ++f) out64[f * lanes + l] = o64[f];
+      for (int f = 0; f < 5; ++f) out32[f * lanes + l] = o32[f];
+    }
+  };
+  int t = std::max(1, threads);
+  if (t > lanes) t = static_cast<int>(lanes);
+  if (t == 1) {
+    work(0, lanes);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const int64_t chunk = 256;
+  std::atomic<int64_t> next{0};
+  for (int k = 0; k < t; ++k)
+    pool.emplace_back([&] {
+      for (;;) {
+        const int64_t lo = next.fetch_add(chunk);
+        if (lo >= lanes) return;
+        work(lo, std::min(lanes, lo + chunk));
+      }
+    });
+  for (auto& th : pool) th.join();
+}
+
 }  // namespace ksa

@@ -1,0 +1,148 @@
+// gfx950 closed-loop what-if sweep: one (configuration, seed) per lane.
+//
+// Each lane runs ksa_sim::simulate_queue (csrc/sim/queue_sim.h): the reference's decision rules
+// driving a queue that the replicas drain, with random arrivals from a counter-based stream
+// (integer-only, bit-identical to the CPU path). Lane l simulates configuration l / seeds with
+// seed l % seeds, so a wave holds consecutive seeds of one configuration. Layout as the open-loop
+// kernel (policy_sweep.hip): parameters [9][m] int64 (structure of arrays, read once per lane),
+// outputs [field][m * seeds]; the arrival-rate trace is read from global memory (all lanes walk
+// it nearly in lockstep, so L2 serves it). The grid is one resident wave of workgroups
+// (occupancy API x CUs) with a grid-stride loop; every lane's loop is bounded by the horizon
+// and ksa_sim::kMaxPolls.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "../sim/queue_sim.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPods, kMaxPods, kMinPods, kNumParams };
+enum : int { kPodMs = 0, kBacklogMsgMs, kViolationMs, kPeakBacklog, kArrived, kServed, kFinalBacklog, kNumOut64 };
+enum : int { kUps = 0, kDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
+
+thread_local std::string g_queue_error;
+
+__global__ __launch_bounds__(kBlock) void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m,
+                                                             int32_t seeds, uint64_t seed0, ksa_sim::Latency lat,
+                                                             ksa_sim::QueueModel model,
+                                                             const int64_t* __restrict__ t_ms,
+                                                             const int64_t* __restrict__ rate_milli, int32_t n,
+                                                             int32_t init, int64_t horizon,
+                                                             int64_t* __restrict__ out64,
+                                                             int32_t* __restrict__ out32) {
+  const int64_t lanes = m * seeds;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t l = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; l < lanes; l += stride) {
+    const int64_t i = l / seeds;
+    const int32_t s = static_cast<int32_t>(l - i * seeds);
+    ksa_sim::Params p;
+    p.poll_ns = params[kPoll * m + i];
+    p.up_cool_ns = params[kUpCool * m + i];
+    p.down_cool_ns = params[kDownCool * m + i];
+    p.up_msgs = params[kUpMsgs * m + i];
+    p.down_msgs = params[kDownMsgs * m + i];
+    p.up_pods = params[kUpPods * m + i];
+    p.down_pods = params[kDownPods * m + i];
+    p.max_pods = params[kMaxPods * m + i];
+    p.min_pods = params[kMinPods * m + i];
+    const ksa_sim::QueueResult r =
+        ksa_sim::simulate_queue(p, lat, model, t_ms, rate_milli, n, init, horizon, seed0 + static_cast<uint64_t>(s));
+    out64[kPodMs * lanes + l] = r.pod_ms;
+    out64[kBacklogMsgMs * lanes + l] = r.backlog_msg_ms;
+    out64[kViolationMs * lanes + l] = r.violation_ms;
+    out64[kPeakBacklog * lanes + l] = r.peak_backlog;
+    out64[kArrived * lanes + l] = r.arrived;
+    out64[kServed * lanes + l] = r.served;
+    out64[kFinalBacklog * lanes + l] = r.final_backlog;
+    out32[kUps * lanes + l] = r.ups;
+    out32[kDowns * lanes + l] = r.downs;
+    out32[kFinal * lanes + l] = r.final_replicas;
+    out32[kMaxRep * lanes + l] = r.max_replicas;
+    out32[kPolls * lanes + l] = r.polls;
+  }
+}
+
+bool ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  g_queue_error = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ksa_queue_sweep_last_error() { return g_queue_error.c_str(); }
+
+// trace: n segments (t_ms ascending from 0, rate in msgs/s x1000); model: {service_milli,
+// startup_ns, slo_backlog, init_backlog}; latency {sqs, get, update} ns; params [9][m];
+// out64 [7][m*seeds] (pod_ms, backlog_msg_ms, violation_ms, peak_backlog, arrived, served,
+// final_backlog); out32 [5][m*seeds] (ups, downs, final, max_replicas, polls). 0 on success.
+int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
+                        int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params,
+                        int64_t m, int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, double* kernel_ms) {
+  if (n < 1 || t_ms[0] != 0) {
+    g_queue_error = "arrival trace must have at least one segment starting at t=0";
+    return -1;
+  }
+  if (seeds < 1) {
+    g_queue_error = "seeds must be >= 1";
+    return -1;
+  }
+  const int64_t lanes = m * seeds;
+  if (lanes <= 0) return 0;
+  if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
+  hipDeviceProp_t prop;
+  if (!ok(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties")) return -1;
+  int64_t *d_t = nullptr, *d_r = nullptr, *d_p = nullptr, *d_o64 = nullptr;
+  int32_t* d_o32 = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = -1;
+  do {
+    if (!ok(hipMalloc(&d_t, n * sizeof(int64_t)), "hipMalloc") || !ok(hipMalloc(&d_r, n * sizeof(int64_t)), "hipMalloc") ||
+        !ok(hipMalloc(&d_p, kNumParams * m * sizeof(int64_t)), "hipMalloc") ||
+        !ok(hipMalloc(&d_o64, kNumOut64 * lanes * sizeof(int64_t)), "hipMalloc") ||
+        !ok(hipMalloc(&d_o32, kNumOut32 * lanes * sizeof(int32_t)), "hipMalloc"))
+      break;
+    if (!ok(hipMemcpy(d_t, t_ms, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
+        !ok(hipMemcpy(d_r, rate_milli, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
+        !ok(hipMemcpy(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy"))
+      break;
+    if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_sweep_kernel, kBlock, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int64_t cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    const int64_t want = (lanes + kBlock - 1) / kBlock;
+    const int grid = static_cast<int>(std::min<int64_t>(want, cus * per_cu));
+    const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+    const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
+    if (!ok(hipEventRecord(e0, nullptr), "hipEventRecord")) break;
+    hipLaunchKernelGGL(queue_sweep_kernel, dim3(grid), dim3(kBlock), 0, nullptr, d_p, m, seeds, seed0, lat, qm, d_t, d_r,
+                       n, init_replicas, horizon_ns, d_o64, d_o32);
+    if (!ok(hipGetLastError(), "queue_sweep_kernel launch")) break;
+    if (!ok(hipEventRecord(e1, nullptr), "hipEventRecord")) break;
+    if (!ok(hipEventSynchronize(e1), "hipEventSynchronize")) break;
+    float ms = 0;
+    if (!ok(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime")) break;
+    if (kernel_ms) *kernel_ms = ms;
+    if (!ok(hipMemcpy(out64, d_o64, kNumOut64 * lanes * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy") ||
+        !ok(hipMemcpy(out32, d_o32, kNumOut32 * lanes * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
+      break;
+    rc = 0;
+  } while (false);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(d_t);
+  (void)hipFree(d_r);
+  (void)hipFree(d_p);
+  (void)hipFree(d_o64);
+  (void)hipFree(d_o32);
+  return rc;
+}
+
+}  // extern "C"

@@ -126,47 +126,137 @@ constexpr int64_t kTimeBound = int64_t(1) << 61;
 
 KSA_HD int64_t clamp_cool(int64_t c) { return c > kTimeBound ? kTimeBound : (c < -kTimeBound ? -kTimeBound : c); }
 
+// Per-configuration constants of the decision rules (Go int -> int32 conversions done once).
+struct Rules {
+  int64_t up_msgs, down_msgs, up_cool, down_cool, period;
+  int32_t max32, min32, up32, down32;
+};
+
+KSA_HD Rules make_rules(const Params& p) {
+  Rules k;
+  k.up_msgs = p.up_msgs;
+  k.down_msgs = p.down_msgs;
+  // Timers stay below 2^61 (the host bounds horizon and latencies), so clamping the cool-downs
+  // to +-2^61 keeps `last + cool` from overflowing without changing any comparison with `now`.
+  k.up_cool = clamp_cool(p.up_cool_ns);
+  k.down_cool = clamp_cool(p.down_cool_ns);
+  k.period = p.poll_ns > 0 ? (p.poll_ns < kTimeBound ? p.poll_ns : kTimeBound) : 0;
+  k.max32 = go_i32(p.max_pods);
+  k.min32 = go_i32(p.min_pods);
+  k.up32 = go_i32(p.up_pods);
+  k.down32 = go_i32(p.down_pods);
+  return k;
+}
+
+// What one poll did: API calls made (for the virtual clock) and each direction's action.
+struct PollOutcome {
+  int32_t gets = 0, writes = 0;
+  int32_t up = 0, down = 0;  // 0: no action / cool-down skip, 1: scaled, 2: no-op at the bound
+};
+
+// One poll's decision, main.go:51-77 with scale.go:54-107, on the virtual clock. `now` is the
+// time the SQS call returned; each GET / write advances it by its latency, so later comparisons
+// see the later time, as the reference re-reads time.Now() at every comparison.
+KSA_HD PollOutcome decide(const Rules& k, const Latency& lat, int64_t d, int64_t* now, int64_t* last_up,
+                          int64_t* last_down, int32_t* replicas) {
+  PollOutcome o;
+  bool cont = false;
+  if (d >= k.up_msgs) {  // main.go:51
+    if (*last_up + k.up_cool > *now) {  // main.go:52 (strict After)
+      cont = true;
+    } else {
+      *now += lat.get_ns;
+      o.gets++;
+      if (*replicas >= k.max32) {  // scale.go:62
+        o.up = 2;
+      } else {
+        int32_t next = add_i32(*replicas, k.up32);
+        if (next > k.max32) next = k.max32;
+        *now += lat.update_ns;
+        o.writes++;
+        *replicas = next;
+        o.up = 1;
+      }
+      *last_up = *now;  // main.go:62 (also after a no-op)
+    }
+  }
+  if (!cont && d <= k.down_msgs) {  // main.go:65
+    if (!(*last_down + k.down_cool > *now)) {
+      *now += lat.get_ns;
+      o.gets++;
+      if (*replicas <= k.min32) {  // scale.go:89
+        o.down = 2;
+      } else {
+        int32_t next = sub_i32(*replicas, k.down32);
+        if (next < k.min32) next = k.min32;
+        *now += lat.update_ns;
+        o.writes++;
+        *replicas = next;
+        o.down = 1;
+      }
+      *last_down = *now;  // main.go:76
+    }
+  }
+  return o;
+}
+
+// The time between two polls is the period plus the earlier poll's API latency: sqs plus 0-2
+// GETs and at most as many writes, so one of six values. Their millisecond floors are taken once
+// per configuration; the per-poll metric update then selects one instead of dividing a 64-bit
+// interval (a long multiply-high expansion on the GPU). Exact: same operands, same division.
+// The other five differ from the first by at most the latencies (bounded by the host: <= 1 h
+// each), so they are kept as 32-bit offsets -- fewer registers, more resident waves.
+struct Intervals {
+  int64_t g0;
+  int32_t g1u0, g1u1, g2u0, g2u1, g2u2;
+};
+
+KSA_HD Intervals make_intervals(int64_t period, const Latency& lat) {
+  const int64_t base = period + lat.sqs_ns;
+  Intervals t;
+  t.g0 = base / 1000000;
+  int32_t g1u0 = static_cast<int32_t>((base + lat.get_ns) / 1000000 - t.g0);
+  int32_t g1u1 = static_cast<int32_t>((base + lat.get_ns + lat.update_ns) / 1000000 - t.g0);
+  int32_t g2u0 = static_cast<int32_t>((base + 2 * lat.get_ns) / 1000000 - t.g0);
+  int32_t g2u1 = static_cast<int32_t>((base + 2 * lat.get_ns + lat.update_ns) / 1000000 - t.g0);
+  int32_t g2u2 = static_cast<int32_t>((base + 2 * lat.get_ns + 2 * lat.update_ns) / 1000000 - t.g0);
+  KSA_OPAQUE(g1u0);
+  KSA_OPAQUE(g1u1);
+  KSA_OPAQUE(g2u0);
+  KSA_OPAQUE(g2u1);
+  KSA_OPAQUE(g2u2);
+  t.g1u0 = g1u0;
+  t.g1u1 = g1u1;
+  t.g2u0 = g2u0;
+  t.g2u1 = g2u1;
+  t.g2u2 = g2u2;
+  return t;
+}
+
+KSA_HD int64_t interval_ms(const Intervals& t, int32_t gets, int32_t writes) {
+  const int32_t g2 = writes == 0 ? t.g2u0 : (writes == 1 ? t.g2u1 : t.g2u2);
+  return t.g0 + (gets == 0 ? 0 : (gets == 1 ? (writes == 0 ? t.g1u0 : t.g1u1) : g2));
+}
+
 KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns, const int64_t* depth, int32_t n,
                        int32_t init_replicas, int64_t horizon_ns) {
   Result res;
   Accum acc;
   acc.run_r = init_replicas;
   Cursor cursor = cursor_init(t_ns, depth, n);
+  const Rules k = make_rules(p);
   int64_t now = 0;
   int64_t last_up = 0, last_down = 0;  // main.go:37-38
   int32_t replicas = init_replicas;
-  const int32_t max32 = go_i32(p.max_pods), min32 = go_i32(p.min_pods);
-  const int32_t up32 = go_i32(p.up_pods), down32 = go_i32(p.down_pods);
-  const int64_t period = p.poll_ns > 0 ? (p.poll_ns < kTimeBound ? p.poll_ns : kTimeBound) : 0;
-  // Timers stay below 2^61 (the host bounds horizon and latencies), so clamping the cool-downs
-  // to +-2^61 keeps `last + cool` from overflowing without changing any comparison with `now`.
-  const int64_t up_cool = clamp_cool(p.up_cool_ns), down_cool = clamp_cool(p.down_cool_ns);
   int64_t prev_t = 0;
   int64_t prev_d = depth_at(t_ns, depth, n, &cursor, 0);
   res.max_replicas = replicas;
-  // The time between two polls is the period plus the earlier poll's API latency: sqs plus 0-2
-  // GETs and at most as many writes, so one of six values. Their millisecond floors are taken
-  // once here; the per-poll metric update then selects one instead of dividing a 64-bit
-  // interval (a long multiply-high expansion on the GPU). Exact: same operands, same division.
-  const int64_t base = period + lat.sqs_ns;
-  const int64_t ms_g0 = base / 1000000;
-  // The other five differ from ms_g0 by at most the latencies (bounded by the host: <= 1 h each),
-  // so they are kept as 32-bit offsets -- fewer registers, more resident waves.
-  int32_t off_g1u0 = static_cast<int32_t>((base + lat.get_ns) / 1000000 - ms_g0);
-  int32_t off_g1u1 = static_cast<int32_t>((base + lat.get_ns + lat.update_ns) / 1000000 - ms_g0);
-  int32_t off_g2u0 = static_cast<int32_t>((base + 2 * lat.get_ns) / 1000000 - ms_g0);
-  int32_t off_g2u1 = static_cast<int32_t>((base + 2 * lat.get_ns + lat.update_ns) / 1000000 - ms_g0);
-  int32_t off_g2u2 = static_cast<int32_t>((base + 2 * lat.get_ns + 2 * lat.update_ns) / 1000000 - ms_g0);
-  KSA_OPAQUE(off_g1u0);
-  KSA_OPAQUE(off_g1u1);
-  KSA_OPAQUE(off_g2u0);
-  KSA_OPAQUE(off_g2u1);
-  KSA_OPAQUE(off_g2u2);
-  int64_t dt_ms = period / 1000000;  // t=0 -> first poll: no latency before it
+  const Intervals iv = make_intervals(k.period, lat);
+  int64_t dt_ms = k.period / 1000000;  // t=0 -> first poll: no latency before it
   // Guard: a zero period with zero latency would never advance time.
-  const bool advances = period > 0 || lat.sqs_ns > 0;
+  const bool advances = k.period > 0 || lat.sqs_ns > 0;
   while (advances && res.polls < kMaxPolls) {
-    const int64_t t_poll = now + period;  // main.go:41 sleep, then poll
+    const int64_t t_poll = now + k.period;  // main.go:41 sleep, then poll
     if (t_poll > horizon_ns) break;
     now = t_poll;
     accumulate_ms(&res, &acc, dt_ms, replicas, prev_d);  // replicas as set by the previous poll
@@ -174,49 +264,15 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
     res.polls++;
     const int64_t d = depth_at(t_ns, depth, n, &cursor, now);  // sampled at call start
     now += lat.sqs_ns;
-    int32_t gets = 0, writes = 0;
-    bool cont = false;
-    if (d >= p.up_msgs) {  // main.go:51
-      if (last_up + up_cool > now) {  // main.go:52 (strict After)
-        cont = true;
-      } else {
-        now += lat.get_ns;
-        gets++;
-        if (replicas >= max32) {  // scale.go:62
-          res.noop_ups++;
-        } else {
-          int32_t next = add_i32(replicas, up32);
-          if (next > max32) next = max32;
-          now += lat.update_ns;
-          writes++;
-          replicas = next;
-          res.ups++;
-          if (res.first_up_ns < 0) res.first_up_ns = t_poll;
-        }
-        last_up = now;  // main.go:62 (also after a no-op)
-      }
-    }
-    if (!cont && d <= p.down_msgs) {  // main.go:65
-      if (!(last_down + down_cool > now)) {
-        now += lat.get_ns;
-        gets++;
-        if (replicas <= min32) {  // scale.go:89
-          res.noop_downs++;
-        } else {
-          int32_t next = sub_i32(replicas, down32);
-          if (next < min32) next = min32;
-          now += lat.update_ns;
-          writes++;
-          replicas = next;
-          res.downs++;
-        }
-        last_down = now;  // main.go:76
-      }
-    }
+    const PollOutcome o = decide(k, lat, d, &now, &last_up, &last_down, &replicas);
+    res.ups += o.up == 1;
+    res.noop_ups += o.up == 2;
+    res.downs += o.down == 1;
+    res.noop_downs += o.down == 2;
+    if (o.up == 1 && res.first_up_ns < 0) res.first_up_ns = t_poll;
     if (replicas > res.max_replicas) res.max_replicas = replicas;
     prev_d = d;
-    const int32_t g2 = writes == 0 ? off_g2u0 : (writes == 1 ? off_g2u1 : off_g2u2);
-    dt_ms = ms_g0 + (gets == 0 ? 0 : (gets == 1 ? (writes == 0 ? off_g1u0 : off_g1u1) : g2));
+    dt_ms = interval_ms(iv, o.gets, o.writes);
   }
   if (horizon_ns > prev_t) accumulate_ms(&res, &acc, (horizon_ns - prev_t) / 1000000, replicas, prev_d);
   flush(&res, &acc);

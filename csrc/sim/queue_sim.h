@@ -1,0 +1,209 @@
+// Closed-loop what-if simulation (extension: tuning tool).
+//
+// policy_sim.h replays a recorded depth trace, so the autoscaler's decisions cannot change the
+// depth it sees. Here the depth is state that the replicas drain:
+//   * messages arrive at a piecewise-constant rate (a trace of msgs/s);
+//   * each ready pod drains `service` msgs/s (fluid service);
+//   * a scale-up's pods start draining only `startup` after the write returned (GPU workers pull
+//     an image and load a model first); a scale-down removes pending pods before ready ones;
+//   * the decisions are the reference's rules -- ksa_sim::decide, the same code policy_sim.h
+//     runs -- on the same virtual clock with the same API latency model.
+// Arrivals per poll interval are random: a normal approximation of Poisson built from a CLT of
+// 12 uniform 16-bit draws, integer-only, so the gfx950 kernel and the CPU path agree bit for bit.
+// The stream is counter-based on (seed, interval index) and the same seeds are used for every
+// configuration (common random numbers), so configurations are compared on the same arrival
+// sequences. Quantities are kept in milli-messages so fractional arrivals are not lost.
+//
+// One call simulates one (configuration, seed); the host reduces over seeds.
+#pragma once
+
+#include "policy_sim.h"
+
+namespace ksa_sim {
+
+struct QueueModel {
+  int64_t service_milli;  // msgs/s drained per ready pod, x1000
+  int64_t startup_ns;     // delay from a scale-up write to its pods taking work
+  int64_t slo_backlog;    // backlog (msgs) above which time counts as an SLO violation
+  int64_t init_backlog;   // msgs queued at t=0
+};
+
+struct QueueResult {
+  int64_t pod_ms = 0;          // sum(spec replicas x dt): cost (starting pods are billed too)
+  int64_t backlog_msg_ms = 0;  // sum(backlog x dt): mean backlog = / horizon_ms
+  int64_t violation_ms = 0;    // time with backlog > slo_backlog
+  int64_t peak_backlog = 0;    // msgs
+  int64_t arrived = 0, served = 0, final_backlog = 0;  // msgs
+  int32_t ups = 0, downs = 0, final_replicas = 0, max_replicas = 0, polls = 0;
+};
+
+// splitmix64 finaliser: the counter-based random stream.
+KSA_HD uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// floor(sqrt(x)) by integer Newton iteration (no floating point: identical on CPU and GPU).
+KSA_HD uint64_t isqrt64(uint64_t x) {
+  if (x < 2) return x;
+  uint64_t r = x, y = (r + 1) / 2;
+  while (y < r) {
+    r = y;
+    y = (r + x / r) / 2;
+  }
+  return r;
+}
+
+constexpr int64_t kSat = int64_t(1) << 62;
+
+// Saturating helpers for non-negative quantities: absurd inputs (a queue that never drains over
+// months) clamp instead of overflowing.
+KSA_HD int64_t sat_mul(int64_t a, int64_t b) {
+  if (a <= 0 || b <= 0) return 0;
+  return a > kSat / b ? kSat : a * b;
+}
+KSA_HD int64_t sat_add(int64_t a, int64_t b) { return a > kSat - b ? kSat : a + b; }
+// x_milli * dt_ms / 1000 without forming the full product.
+KSA_HD int64_t per_ms(int64_t x_milli, int64_t dt_ms) {
+  return sat_add(sat_mul(x_milli / 1000, dt_ms), sat_mul(x_milli % 1000, dt_ms) / 1000);
+}
+
+// Random arrivals (milli-messages) with mean `mean_milli`: mean + sqrt(mean) * Z, where Z is the
+// CLT of 12 uniform 16-bit integers (standard deviation 2^16 in fixed point).
+KSA_HD int64_t sample_arrivals_milli(int64_t mean_milli, uint64_t seed, uint64_t k) {
+  if (mean_milli <= 0) return 0;
+  const uint64_t base = seed * 0xD1B54A32D192ED03ULL + k * 3;
+  const uint64_t w0 = mix64(base), w1 = mix64(base + 1), w2 = mix64(base + 2);
+  int64_t z = -6 * 65536;
+  for (int i = 0; i < 4; ++i) {
+    z += static_cast<int64_t>((w0 >> (16 * i)) & 0xFFFF);
+    z += static_cast<int64_t>((w1 >> (16 * i)) & 0xFFFF);
+    z += static_cast<int64_t>((w2 >> (16 * i)) & 0xFFFF);
+  }
+  // sd in milli-messages = sqrt(mean_milli / 1000) * 1000 = sqrt(mean_milli * 1000)
+  const int64_t sd_milli = mean_milli < (int64_t(1) << 52)
+                               ? static_cast<int64_t>(isqrt64(static_cast<uint64_t>(mean_milli) * 1000))
+                               : static_cast<int64_t>(isqrt64(static_cast<uint64_t>(mean_milli))) * 31623 / 1000;
+  const int64_t a = mean_milli + sd_milli * z / 65536;
+  return a > 0 ? a : 0;
+}
+
+// Forward-only cursor over the arrival-rate trace.
+struct RateCursor {
+  int32_t c;
+};
+
+// Expected arrivals (milli-messages) over [t0_ms, t1_ms): the rate integrated segment by
+// segment. Segment i covers [t_ms[i], t_ms[i+1]); the last one extends to infinity. Times only
+// grow, so the cursor never moves back.
+KSA_HD int64_t expected_arrivals_milli(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, RateCursor* k,
+                                       int64_t t0_ms, int64_t t1_ms) {
+  while (k->c + 1 < n && t_ms[k->c + 1] <= t0_ms) k->c++;
+  int32_t i = k->c;
+  int64_t sum = 0, a = t0_ms;
+  while (a < t1_ms) {
+    const int64_t seg_end = i + 1 < n ? t_ms[i + 1] : t1_ms;
+    const int64_t b = seg_end < t1_ms ? seg_end : t1_ms;
+    sum = sat_add(sum, per_ms(rate_milli[i], b - a));
+    a = b;
+    if (i + 1 < n && a >= t_ms[i + 1]) ++i;
+  }
+  return sum;
+}
+
+struct QueueState {
+  int64_t q_milli;       // backlog
+  int32_t ready, pending;
+  int64_t pending_at_ms;  // when the pending pods start draining
+  uint64_t draws;
+};
+
+// Advances the queue over [t0_ms, t1_ms): random arrivals, then fluid service by the ready pods
+// (and by pending pods from the moment they become ready), accumulating the metrics with the
+// backlog and replicas at the start of the interval (left Riemann sum, as policy_sim.h).
+KSA_HD void advance(QueueState* s, QueueResult* r, const QueueModel& m, const int64_t* t_ms,
+                    const int64_t* rate_milli, int32_t n, RateCursor* cur, uint64_t seed, int64_t t0_ms, int64_t t1_ms,
+                    int32_t replicas) {
+  if (t1_ms <= t0_ms) return;
+  const int64_t dt = t1_ms - t0_ms;
+  const int64_t q0 = s->q_milli / 1000;
+  r->pod_ms = sat_add(r->pod_ms, sat_mul(replicas, dt));
+  r->backlog_msg_ms = sat_add(r->backlog_msg_ms, sat_mul(q0, dt));
+  if (q0 > m.slo_backlog) r->violation_ms += dt;
+  const int64_t mean = expected_arrivals_milli(t_ms, rate_milli, n, cur, t0_ms, t1_ms);
+  const int64_t a = sample_arrivals_milli(mean, seed, s->draws++);
+  s->q_milli = sat_add(s->q_milli, a);
+  r->arrived = sat_add(r->arrived, a);
+  // capacity: ready pods for the whole interval, pending ones from their ready time
+  int64_t cap = sat_mul(s->ready, per_ms(m.service_milli, dt));
+  if (s->pending > 0 && s->pending_at_ms < t1_ms) {
+    const int64_t from = s->pending_at_ms > t0_ms ? s->pending_at_ms : t0_ms;
+    cap = sat_add(cap, sat_mul(s->pending, per_ms(m.service_milli, t1_ms - from)));
+  }
+  const int64_t served = s->q_milli < cap ? s->q_milli : cap;
+  s->q_milli -= served;
+  r->served = sat_add(r->served, served);
+  if (s->pending > 0 && s->pending_at_ms <= t1_ms) {
+    s->ready += s->pending;
+    s->pending = 0;
+  }
+}
+
+KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const QueueModel& m, const int64_t* t_ms,
+                                  const int64_t* rate_milli, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+                                  uint64_t seed) {
+  QueueResult res;
+  const Rules k = make_rules(p);
+  QueueState s;
+  s.q_milli = m.init_backlog * 1000;
+  s.ready = init_replicas;
+  s.pending = 0;
+  s.pending_at_ms = 0;
+  s.draws = 0;
+  RateCursor cur{0};
+  int64_t now = 0, last_up = 0, last_down = 0;  // main.go:37-38
+  int32_t replicas = init_replicas;
+  res.max_replicas = replicas;
+  int64_t prev_ms = 0;
+  const int64_t horizon_ms = horizon_ns / 1000000;
+  const bool advances = k.period > 0 || lat.sqs_ns > 0;
+  while (advances && res.polls < kMaxPolls) {
+    const int64_t t_poll = now + k.period;  // main.go:41 sleep, then poll
+    if (t_poll > horizon_ns) break;
+    const int64_t t_poll_ms = t_poll / 1000000;
+    advance(&s, &res, m, t_ms, rate_milli, n, &cur, seed, prev_ms, t_poll_ms, replicas);
+    prev_ms = t_poll_ms;
+    now = t_poll;
+    res.polls++;
+    // depth the SQS call reports: every message not yet deleted (queued + in flight)
+    const int64_t d = s.q_milli / 1000;
+    now += lat.sqs_ns;
+    const int32_t before = replicas;
+    const PollOutcome o = decide(k, lat, d, &now, &last_up, &last_down, &replicas);
+    res.ups += o.up == 1;
+    res.downs += o.down == 1;
+    const int32_t delta = sub_i32(replicas, before);
+    if (delta > 0) {  // new pods: billed now, draining after the start-up delay
+      s.pending += delta;
+      s.pending_at_ms = (now + m.startup_ns) / 1000000;
+    } else if (delta < 0) {  // the Deployment controller removes not-yet-ready pods first
+      int32_t drop = -delta;
+      const int32_t from_pending = drop < s.pending ? drop : s.pending;
+      s.pending -= from_pending;
+      drop -= from_pending;
+      s.ready = s.ready > drop ? s.ready - drop : 0;
+    }
+    if (replicas > res.max_replicas) res.max_replicas = replicas;
+    if (s.q_milli / 1000 > res.peak_backlog) res.peak_backlog = s.q_milli / 1000;
+  }
+  if (horizon_ms > prev_ms) advance(&s, &res, m, t_ms, rate_milli, n, &cur, seed, prev_ms, horizon_ms, replicas);
+  res.final_replicas = replicas;
+  res.final_backlog = s.q_milli / 1000;
+  res.arrived /= 1000;
+  res.served /= 1000;
+  return res;
+}
+
+}  // namespace ksa_sim

@@ -104,10 +104,10 @@ def build_native(jobs: int = 8, verbose: bool = True) -> Path:
 
 
 def build_gpu_probe(verbose: bool = True) -> Path | None:
-    """Compiles the gfx950 kernels -- HBM probe + what-if policy sweep -- into one .so
+    """Compiles the gfx950 kernels -- HBM probe + open- and closed-loop what-if sweeps -- into one .so
     (cross-compiles without a GPU)."""
-    srcs = [CSRC / "hip" / "gpu_probe.hip", CSRC / "hip" / "policy_sweep.hip"]
-    deps = srcs + [CSRC / "sim" / "policy_sim.h"]
+    srcs = [CSRC / "hip" / "gpu_probe.hip", CSRC / "hip" / "policy_sweep.hip", CSRC / "hip" / "queue_sweep.hip"]
+    deps = srcs + [CSRC / "sim" / "policy_sim.h", CSRC / "sim" / "queue_sim.h"]
     if not Path(HIPCC).exists() and shutil.which("hipcc") is None:
         raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")
     hipcc = HIPCC if Path(HIPCC).exists() else "hipcc"

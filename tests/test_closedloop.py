@@ -1,0 +1,91 @@
+"""Closed-loop what-if sweep (csrc/sim/queue_sim.h): the native CPU path must agree exactly with
+the independent Python statement of the model, and the model must behave like a queue."""
+import numpy as np
+import pytest
+
+from kube_sqs_autoscaler_amd.tune import closedloop as cl
+from kube_sqs_autoscaler_amd.tune import sweep
+
+S = 1_000_000_000
+LAT = (2_000_000, 1_000_000, 1_000_000)
+
+
+def burst_trace():
+    # quiet, a 10-minute burst of 40 msgs/s, quiet again; 1.5 msgs/s fractional rate in between
+    return cl.ArrivalTrace.from_segments([(0, 0.5), (300, 40.0), (900, 1.5), (1500, 0.0)])
+
+
+def small_grid():
+    return sweep.grid(poll_ns=[5 * S, 7 * S], up_cool_ns=[0, 30 * S, 120 * S], down_cool_ns=[0, 60 * S],
+                      up_msgs=[20, 100], down_msgs=[5], max_pods=[4, 8], min_pods=[1])
+
+
+@pytest.mark.parametrize("startup_s,service", [(0, 5.0), (90, 5.0), (45, 12.5)])
+def test_cpu_path_equals_python_model(nat, startup_s, service):
+    tr, grid = burst_trace(), small_grid()
+    model = cl.QueueModel(service_rate=service, startup_ns=startup_s * S, slo_backlog=200, init_backlog=30)
+    horizon = 2400 * S
+    res = cl.run(tr, grid, model, 1, horizon, LAT, seeds=3, seed0=11, device="cpu")
+    for i in range(0, len(res), 5):
+        for s in range(3):
+            want = cl.reference_lane(tr, res.config(i), model, 1, horizon, LAT, 11 + s)
+            got = {k: int(v[i, s]) for k, v in res.out.items()}
+            assert got == want, (res.config(i), s)
+
+
+def test_queue_physics():
+    tr = burst_trace()
+    horizon = 2400 * S
+    base = dict(poll_ns=[5 * S], up_cool_ns=[10 * S], down_cool_ns=[30 * S], up_msgs=[50], down_msgs=[5], min_pods=[1])
+    res = cl.run(tr, sweep.grid(max_pods=[1, 2, 4, 8, 16], **base), cl.QueueModel(5.0, 30 * S, 100), 1, horizon, LAT,
+                 seeds=16, device="cpu")
+    summ = res.summary()
+    # more headroom drains the burst faster: mean backlog falls (weakly) and cost rises as max-pods grows
+    assert np.all(np.diff(summ["backlog_mean"]) <= 1e-9)
+    assert np.all(np.diff(summ["pod_hours_mean"]) >= -1e-9)
+    assert summ["backlog_mean"][0] > 5 * summ["backlog_mean"][-1]
+    # conservation: what arrived was served or is still queued (milli-message flooring: +-1 each)
+    arrived, served, final = (res.out[k] for k in ("arrived", "served", "final_backlog"))
+    assert np.all(np.abs(arrived - served - final) <= 2)
+    # the burst really arrives: ~40 msgs/s x 600 s
+    assert 20000 < arrived.mean() < 28000
+
+
+def test_startup_delay_costs_backlog():
+    tr, horizon = burst_trace(), 2400 * S
+    grid = sweep.grid(poll_ns=[5 * S], up_cool_ns=[10 * S], down_cool_ns=[30 * S], up_msgs=[50], max_pods=[8])
+    fast = cl.run(tr, grid, cl.QueueModel(5.0, 0, 100), 1, horizon, LAT, seeds=16, device="cpu").summary()
+    slow = cl.run(tr, grid, cl.QueueModel(5.0, 300 * S, 100), 1, horizon, LAT, seeds=16, device="cpu").summary()
+    assert slow["backlog_mean"][0] > fast["backlog_mean"][0]
+    assert slow["violation_s_mean"][0] > fast["violation_s_mean"][0]
+
+
+def test_common_random_numbers_and_seed_streams():
+    tr, horizon, grid = burst_trace(), 1800 * S, sweep.grid(max_pods=[4, 8])
+    m = cl.QueueModel(5.0, 30 * S, 100)
+    a = cl.run(tr, grid, m, 1, horizon, LAT, seeds=4, seed0=7, device="cpu")
+    b = cl.run(tr, grid, m, 1, horizon, LAT, seeds=4, seed0=7, device="cpu")
+    c = cl.run(tr, grid, m, 1, horizon, LAT, seeds=4, seed0=8, device="cpu")
+    assert all(np.array_equal(a.out[k], b.out[k]) for k in a.out)
+    assert not np.array_equal(a.out["arrived"], c.out["arrived"])
+    # every seed is its own arrival sequence
+    assert len(set(a.out["arrived"][0].tolist())) > 1
+
+
+def test_validation():
+    tr, grid = burst_trace(), sweep.grid()
+    with pytest.raises(ValueError, match="service rate"):
+        cl.run(tr, grid, cl.QueueModel(-1.0), device="cpu")
+    with pytest.raises(ValueError, match="startup"):
+        cl.run(tr, grid, cl.QueueModel(1.0, startup_ns=2 * 86400 * S), device="cpu")
+    with pytest.raises(ValueError, match="horizon"):
+        cl.run(tr, grid, cl.QueueModel(1.0), horizon_ns=40 * 86400 * S, device="cpu")
+    with pytest.raises(ValueError, match="arrival rates"):
+        cl.ArrivalTrace.from_segments([(0, -1.0)])
+
+
+def test_arrival_csv(tmp_path):
+    p = tmp_path / "arrivals.csv"
+    p.write_text("seconds,rate\n100,2\n160,10.5\n")
+    tr = cl.ArrivalTrace.from_csv(str(p))
+    assert tr.t_ms.tolist() == [0, 60000] and tr.rate_milli.tolist() == [2000, 10500]

@@ -106,3 +106,27 @@ def test_sweep_kernel_equals_cpu_and_oracle():
         for i in range(0, len(g), len(g) // 7):
             o = sweep.oracle_row(tr, g.config(i), 2, horizon, (2_000_000, 1_000_000, 1_000_000))
             assert {k: g.row(i)[k] for k in o} == o
+
+
+def test_closed_loop_kernel_equals_cpu_and_python_model():
+    """gfx950 closed-loop sweep: bit-identical to the CPU path over a grid x seeds, and to the
+    independent Python statement of the model on a sample of lanes."""
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import closedloop as cl
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    S = 1_000_000_000
+    tr = cl.ArrivalTrace.from_segments([(0, 0.5), (300, 40.0), (900, 1.5), (1500, 0.0)])
+    grid = sweep.grid(poll_ns=[5 * S, 7 * S], up_cool_ns=list(range(0, 300 * S, 30 * S)),
+                      down_cool_ns=[0, 60 * S, 300 * S], up_msgs=[20, 100, 400], max_pods=[4, 8, 16])
+    model = cl.QueueModel(service_rate=5.0, startup_ns=60 * S, slo_backlog=200, init_backlog=10)
+    lat = (2_000_000, 1_000_000, 1_000_000)
+    g = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="gpu")
+    c = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="cpu")
+    assert g.device == "gpu" and g.kernel_ms > 0
+    for k in g.out:
+        assert np.array_equal(g.out[k], c.out[k]), k
+    for i in range(0, len(g), 37):
+        want = cl.reference_lane(tr, g.config(i), model, 1, 2400 * S, lat, 1 + 5)
+        assert {k: int(v[i, 5]) for k, v in g.out.items()} == want

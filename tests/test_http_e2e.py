@@ -330,9 +330,13 @@ def test_adaptive_busy_poll_tracks_peer_rtt(nat, kube_server):
         c.request("GET", "/healthz", [("Authorization", f"Bearer {TOKEN}")])
     assert c.rtt_ewma() > 4 * 25_000  # -> spin window 0
     kube_server.set_latency(0)
-    for _ in range(60):
+    # fast local peer again -> spinning re-enabled; under a loaded test runner single round trips
+    # can take >100 us, so allow the EWMA a bounded number of requests to come back down
+    for _ in range(500):
         c.request("GET", "/healthz", [("Authorization", f"Bearer {TOKEN}")])
-    assert c.rtt_ewma() < 4 * 25_000  # fast local peer again -> spinning re-enabled
+        if c.rtt_ewma() < 4 * 25_000:
+            break
+    assert c.rtt_ewma() < 4 * 25_000
 
 
 def test_tls_reconnect_resumes_session(nat):
