@@ -20,13 +20,24 @@
 namespace {
 
 constexpr int kBlock = 256;
+
+// Minimum resident waves per SIMD the register allocator must allow (0: compiler's choice).
+// Measured on an MI355X (768k lanes x 24 h, same box): compiler's choice 107 VGPRs / 4 waves
+// 182.7 ms; 5 waves (96 VGPRs, 24 B scratch) 171.1 ms; 6 waves (80 VGPRs, 92 B scratch) 188.5 ms.
+#ifndef KSA_QUEUE_WAVES_PER_EU
+#define KSA_QUEUE_WAVES_PER_EU 5
+#endif
 enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPods, kMaxPods, kMinPods, kNumParams };
 enum : int { kPodMs = 0, kBacklogMsgMs, kViolationMs, kPeakBacklog, kArrived, kServed, kFinalBacklog, kNumOut64 };
 enum : int { kUps = 0, kDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
 
 thread_local std::string g_queue_error;
 
-__global__ __launch_bounds__(kBlock) void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m,
+__global__ __launch_bounds__(kBlock)
+#if KSA_QUEUE_WAVES_PER_EU > 0
+__attribute__((amdgpu_waves_per_eu(KSA_QUEUE_WAVES_PER_EU)))
+#endif
+void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m,
                                                              int32_t seeds, uint64_t seed0, ksa_sim::Latency lat,
                                                              ksa_sim::QueueModel model,
                                                              const int64_t* __restrict__ t_ms,

@@ -6,7 +6,7 @@
 //   * each ready pod drains `service` msgs/s (fluid service);
 //   * a scale-up's pods start draining only `startup` after the write returned (GPU workers pull
 //     an image and load a model first); a scale-down removes pending pods before ready ones;
-//   * the decisions are the reference's rules -- ksa_sim::decide, the same code policy_sim.h
+//   * the decisions are the reference's rules -- KSA_DECIDE, the same code policy_sim.h
 //     runs -- on the same virtual clock with the same API latency model.
 // Arrivals per poll interval are random: a normal approximation of Poisson built from a CLT of
 // 12 uniform 16-bit draws, integer-only, so the gfx950 kernel and the CPU path agree bit for bit.
@@ -45,14 +45,16 @@ KSA_HD uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// floor(sqrt(x)) by integer Newton iteration (no floating point: identical on CPU and GPU).
+// floor(sqrt(x)), exact on CPU and GPU: a double-precision estimate (within a unit or two
+// whatever the rounding of the conversion and the sqrt) corrected with integer arithmetic. (An
+// integer Newton iteration is exact too, but each step is a 64-bit division -- a long software
+// sequence on the GPU.)
 KSA_HD uint64_t isqrt64(uint64_t x) {
-  if (x < 2) return x;
-  uint64_t r = x, y = (r + 1) / 2;
-  while (y < r) {
-    r = y;
-    y = (r + x / r) / 2;
-  }
+  constexpr uint64_t kMax = 0xFFFFFFFFULL;  // floor(sqrt(2^64 - 1))
+  uint64_t r = static_cast<uint64_t>(__builtin_sqrt(static_cast<double>(x)));
+  if (r > kMax) r = kMax;
+  while (r * r > x) --r;
+  while (r < kMax && (r + 1) * (r + 1) <= x) ++r;
   return r;
 }
 
@@ -60,9 +62,14 @@ constexpr int64_t kSat = int64_t(1) << 62;
 
 // Saturating helpers for non-negative quantities: absurd inputs (a queue that never drains over
 // months) clamp instead of overflowing.
+// min(a*b, kSat) for a, b > 0 (0 otherwise). Operands below 2^31 -- nearly all of them -- cannot
+// reach kSat; the rest use the overflow builtin. No division (a variable 64-bit divide is a long
+// software sequence on the GPU).
 KSA_HD int64_t sat_mul(int64_t a, int64_t b) {
   if (a <= 0 || b <= 0) return 0;
-  return a > kSat / b ? kSat : a * b;
+  if (((a | b) >> 31) == 0) return a * b;
+  int64_t r;
+  return __builtin_mul_overflow(a, b, &r) || r > kSat ? kSat : r;
 }
 KSA_HD int64_t sat_add(int64_t a, int64_t b) { return a > kSat - b ? kSat : a + b; }
 // x_milli * dt_ms / 1000 without forming the full product.
@@ -181,9 +188,8 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
     const int64_t d = s.q_milli / 1000;
     now += lat.sqs_ns;
     const int32_t before = replicas;
-    const PollOutcome o = decide(k, lat, d, &now, &last_up, &last_down, &replicas);
-    res.ups += o.up == 1;
-    res.downs += o.down == 1;
+    int32_t gets = 0, writes = 0;
+    KSA_DECIDE(k, lat, d, now, last_up, last_down, replicas, gets, writes, res.ups++, (void)0, res.downs++, (void)0);
     const int32_t delta = sub_i32(replicas, before);
     if (delta > 0) {  // new pods: billed now, draining after the start-up delay
       s.pending += delta;

@@ -11,6 +11,16 @@ whose queue pressure stays under a bound, and rank them by pod cost::
 Grid keys are the autoscaler's own flag names; values use its syntax (Go durations, base-0 ints),
 as comma lists or ``start:stop:step`` ranges (stop inclusive). The sweep runs on the MI355X
 (``--device gpu``) or on CPU threads; both give identical numbers.
+
+Closed loop (:mod:`.closedloop`): with ``--arrivals`` (``seconds,msgs_per_second`` CSV) instead of
+``--trace`` the queue is simulated -- the candidate's replicas drain it at ``--service-rate``
+msgs/s per ready pod after ``--startup-delay`` -- over ``--seeds`` random arrival sequences, and
+configurations are ranked by mean pod-hours subject to the 95th-percentile time above
+``--slo-backlog``::
+
+    python -m kube_sqs_autoscaler_amd.tune --arrivals rate.csv --horizon 24h \
+        --service-rate 4 --startup-delay 90s --slo-backlog 500 --max-violation 10m --seeds 64 \
+        --grid scale-up-cool-down=0s:10m:30s --grid max-pods=8,16,32 --top 10
 """
 from __future__ import annotations
 
@@ -23,7 +33,7 @@ from typing import Dict, List
 import numpy as np
 
 from ..utils.goflag import parse_duration, parse_int
-from . import sweep
+from . import closedloop, sweep
 
 FLAG_TO_FIELD = {
     "poll-period": ("poll_ns", parse_duration),
@@ -69,19 +79,37 @@ def parse_grid(items: List[str]) -> Dict[str, List[int]]:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m kube_sqs_autoscaler_amd.tune", description=__doc__.splitlines()[0])
-    ap.add_argument("--trace", required=True, help="--trace-file span log (.jsonl) or seconds,depth CSV")
+    src = ap.add_mutually_exclusive_group(required=True)
+    src.add_argument("--trace", help="--trace-file span log (.jsonl) or seconds,depth CSV (open loop)")
+    src.add_argument("--arrivals", help="seconds,msgs_per_second CSV: simulate the queue (closed loop)")
     ap.add_argument("--queue", default=None, help="queue URL or ns/deployment to select from a multi-queue span log")
     ap.add_argument("--horizon", default="", help="simulated time (Go duration); default: trace length + 1 poll period")
     ap.add_argument("--init-replicas", type=int, default=1)
     ap.add_argument("--latency", default="1ms,1ms,1ms", help="SQS, GET, write latency (Go durations)")
     ap.add_argument("--grid", action="append", default=[], help="flag=values (repeatable)")
-    ap.add_argument("--objective", default="pod_ms", choices=["pod_ms", "backlog", "ups", "downs"])
+    ap.add_argument("--objective", default=None,
+                    help="open loop: pod_ms|backlog|ups|downs (default pod_ms); closed loop: a summary column "
+                         "(default pod_hours_mean)")
     ap.add_argument("--max-backlog", type=float, default=None, help="keep configs with backlog <= this")
     ap.add_argument("--top", type=int, default=10)
     ap.add_argument("--pareto", action="store_true", help="list the cost/pressure Pareto front instead of a ranking")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--json", action="store_true", help="print JSON lines instead of a table")
+    cl = ap.add_argument_group("closed loop (--arrivals)")
+    cl.add_argument("--service-rate", type=float, default=None, help="msgs/s one ready pod drains (required)")
+    cl.add_argument("--startup-delay", default="60s", help="scale-up write -> new pods taking work (Go duration)")
+    cl.add_argument("--slo-backlog", type=int, default=1000, help="backlog (msgs) above which time is a violation")
+    cl.add_argument("--init-backlog", type=int, default=0, help="msgs queued at t=0")
+    cl.add_argument("--max-violation", default=None, help="keep configs whose p95 time above --slo-backlog <= this")
+    cl.add_argument("--seeds", type=int, default=32, help="random arrival sequences per configuration")
+    cl.add_argument("--seed", type=int, default=1, help="first seed (the same seeds are used for every config)")
     a = ap.parse_args(argv)
+    if a.arrivals is not None:
+        return _closed_loop(ap, a)
+    if a.objective is None:
+        a.objective = "pod_ms"
+    if a.objective not in ("pod_ms", "backlog", "ups", "downs"):
+        ap.error(f"open-loop objective must be pod_ms, backlog, ups or downs, not {a.objective!r}")
 
     tr = sweep.Trace.from_spans(a.trace, a.queue) if a.trace.endswith((".jsonl", ".json")) else sweep.Trace.from_csv(a.trace)
     lat = tuple(parse_duration(x) for x in a.latency.split(","))
@@ -121,6 +149,59 @@ def main(argv=None) -> int:
     for i in order:
         r = res.row(int(i))
         print("\t".join(str(r[c]) for c in cols))
+    return 0
+
+
+CLOSED_COLS = ["poll_ns", "up_cool_ns", "down_cool_ns", "up_msgs", "down_msgs", "up_pods", "down_pods", "max_pods",
+               "min_pods", "pod_hours_mean", "backlog_mean", "violation_s_p95", "peak_backlog_p95", "ups_mean",
+               "downs_mean", "max_replicas_max"]
+
+
+def _closed_loop(ap: argparse.ArgumentParser, a) -> int:
+    if a.service_rate is None:
+        ap.error("--arrivals needs --service-rate")
+    objective = a.objective or "pod_hours_mean"
+    tr = closedloop.ArrivalTrace.from_csv(a.arrivals)
+    lat = tuple(parse_duration(x) for x in a.latency.split(","))
+    if len(lat) != 3:
+        ap.error("--latency needs three durations")
+    model = closedloop.QueueModel(a.service_rate, parse_duration(a.startup_delay), a.slo_backlog, a.init_backlog)
+    params = sweep.grid(**parse_grid(a.grid))
+    horizon = parse_duration(a.horizon) if a.horizon else int(tr.t_ms[-1]) * 1_000_000 + 3600 * closedloop.S
+    t0 = time.perf_counter()
+    res = closedloop.run(tr, params, model, a.init_replicas, horizon, lat, a.seeds, a.seed, a.device)
+    wall = time.perf_counter() - t0
+    summ = res.summary()
+    if objective not in summ:
+        ap.error(f"closed-loop objective must be one of {sorted(summ)}, not {objective!r}")
+    ok = np.ones(len(res), dtype=bool)
+    if a.max_violation is not None:
+        ok &= summ["violation_s_p95"] <= parse_duration(a.max_violation) / 1e9
+    if a.max_backlog is not None:
+        ok &= summ["backlog_mean"] <= a.max_backlog
+    idx = np.flatnonzero(ok)
+    if a.pareto:
+        front = sweep.pareto_front(summ["pod_hours_mean"][idx], summ["violation_s_p95"][idx])
+        order = idx[front][: a.top] if a.top > 0 else idx[front]
+    else:
+        order = idx[np.argsort(summ[objective][idx], kind="stable")][: a.top]
+    base = closedloop.run(tr, sweep.grid(), model, a.init_replicas, horizon, lat, a.seeds, a.seed, "cpu").row(0)
+    info = {"configs": len(res), "feasible": int(ok.sum()), "seeds": a.seeds, "device": res.device,
+            "wall_s": round(wall, 4), "kernel_ms": round(res.kernel_ms, 3),
+            "simulated_polls": int(res.out["polls"].sum()), "horizon_ns": horizon, "reference_defaults": base}
+    if a.json:
+        print(json.dumps(info))
+        for i in order:
+            print(json.dumps(res.row(int(i))))
+        return 0
+    print(f"{len(res)} configs x {a.seeds} seeds ({int(ok.sum())} feasible) on {res.device} in {wall:.3f} s, "
+          f"{info['simulated_polls']:.3g} polls simulated")
+    print(f"reference defaults: pod_hours={base['pod_hours_mean']:.3f} backlog={base['backlog_mean']:.1f} "
+          f"violation_p95={base['violation_s_p95']:.0f}s ups={base['ups_mean']:.1f}")
+    print("\t".join(CLOSED_COLS))
+    for i in order:
+        r = res.row(int(i))
+        print("\t".join(f"{r[c]:.4g}" if isinstance(r[c], float) else str(r[c]) for c in CLOSED_COLS))
     return 0
 
 

@@ -9,7 +9,7 @@ changes the next decision. ``csrc/sim/queue_sim.h`` models it:
   approximation of Poisson, counter-based per seed, the same seeds for every configuration);
 * each ready pod drains ``service_rate`` msgs/s; a scale-up's pods take work only
   ``startup`` after the write returned; a scale-down removes starting pods first;
-* the decisions are the reference's rules (``ksa_sim::decide``, shared with the open-loop
+* the decisions are the reference's rules (``KSA_DECIDE`` in ``policy_sim.h``, shared with the open-loop
   simulator that is exact against ``models/oracle.py``), on the same virtual clock and latency
   model.
 

@@ -10,7 +10,8 @@ timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 timeout -k 10 300 python bench.py --queues 8 --no-sweep > gpurun_out/bench_q8.json 2> gpurun_out/bench_q8.err &&
 timeout -k 10 300 python -m kube_sqs_autoscaler_amd.bench.capacity > gpurun_out/capacity.jsonl 2> gpurun_out/capacity.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o probe -- python3 scripts/probe_bench.py > gpurun_out/prof_probe.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o sweep -- python3 scripts/sweep_bench.py > gpurun_out/prof_sweep.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o sweep -- python3 scripts/sweep_bench.py > gpurun_out/prof_sweep.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o queue -- python3 scripts/queue_sweep_bench.py > gpurun_out/prof_queue.log 2>&1
 rc=$?
 echo "exit $rc"
 exit $rc

@@ -33,11 +33,13 @@ for device in ("gpu", "cpu"):
     polls = int(r.out["polls"].sum())
     results[device] = r
     summ = r.summary()
-    best = int(np.argmin(np.where(summ["violation_s_p95"] <= 600, summ["pod_hours_mean"], np.inf)))
+    feasible = summ["violation_s_p95"] <= 600
+    best = int(np.argmin(np.where(feasible, summ["pod_hours_mean"], np.inf))) if feasible.any() else None
     print(json.dumps({"device": device, "configs": sub.shape[1], "seeds": seeds, "lane_polls": polls,
                       "wall_s": round(wall, 4), "kernel_ms": round(r.kernel_ms, 3),
                       "lane_polls_per_s": round(polls / wall, 1),
-                      "best_under_10min_p95_violation": r.row(best)}), flush=True)
+                      "feasible": int(feasible.sum()),
+                      "best_under_10min_p95_violation": None if best is None else r.row(best)}), flush=True)
 if "gpu" in results and "cpu" in results:
     g, c = results["gpu"], results["cpu"]
     k = c.params.shape[1]

@@ -89,3 +89,46 @@ def test_arrival_csv(tmp_path):
     p.write_text("seconds,rate\n100,2\n160,10.5\n")
     tr = cl.ArrivalTrace.from_csv(str(p))
     assert tr.t_ms.tolist() == [0, 60000] and tr.rate_milli.tolist() == [2000, 10500]
+
+
+def test_tune_cli_closed_loop_ranks_under_violation_bound(tmp_path, capsys):
+    import json
+
+    from kube_sqs_autoscaler_amd.tune.__main__ import main
+
+    csv_path = tmp_path / "rate.csv"
+    csv_path.write_text("seconds,msgs_per_second\n0,2\n600,30\n1200,2\n")
+    argv = ["--arrivals", str(csv_path), "--horizon", "40m", "--service-rate", "5", "--startup-delay", "60s",
+            "--slo-backlog", "300", "--seeds", "8", "--device", "cpu", "--max-violation", "8m",
+            "--grid", "scale-up-cool-down=0s:4m:1m", "--grid", "scale-up-messages=50,200,800",
+            "--grid", "max-pods=2,8", "--json", "--top", "5"]
+    assert main(argv) == 0
+    lines = [json.loads(x) for x in capsys.readouterr().out.splitlines()]
+    info, rows = lines[0], lines[1:]
+    assert info["configs"] == 5 * 3 * 2 and info["seeds"] == 8 and info["device"] == "cpu"
+    assert 0 < len(rows) <= 5 and info["feasible"] >= len(rows)
+    assert all(r["violation_s_p95"] <= 480 for r in rows)
+    costs = [r["pod_hours_mean"] for r in rows]
+    assert costs == sorted(costs)
+    # two pods drain 10 msgs/s < 30 msgs/s arriving: the 10-minute burst backs up past the SLO
+    assert all(r["max_pods"] == 8 for r in rows)
+    assert "pod_hours_mean" in info["reference_defaults"]
+    # table output and the Pareto front
+    assert main(argv[:-3] + ["--pareto"]) == 0
+    out = capsys.readouterr().out
+    assert "configs x 8 seeds" in out and "pod_hours_mean" in out
+
+
+def test_tune_cli_closed_loop_argument_errors(tmp_path):
+    import pytest
+
+    from kube_sqs_autoscaler_amd.tune.__main__ import main
+
+    csv_path = tmp_path / "rate.csv"
+    csv_path.write_text("0,1\n")
+    with pytest.raises(SystemExit):
+        main(["--arrivals", str(csv_path)])  # no --service-rate
+    with pytest.raises(SystemExit):
+        main(["--arrivals", str(csv_path), "--service-rate", "1", "--objective", "nope", "--device", "cpu"])
+    with pytest.raises(SystemExit):
+        main(["--arrivals", str(csv_path), "--trace", str(csv_path), "--service-rate", "1"])
