@@ -72,8 +72,12 @@ KSA_HD int64_t sat_mul(int64_t a, int64_t b) {
   return __builtin_mul_overflow(a, b, &r) || r > kSat ? kSat : r;
 }
 KSA_HD int64_t sat_add(int64_t a, int64_t b) { return a > kSat - b ? kSat : a + b; }
-// x_milli * dt_ms / 1000 without forming the full product.
+// floor(x_milli * dt_ms / 1000) (saturating), without forming a product that could overflow.
+// Operands below 2^31 (rates <= 1e6 msgs/s, intervals < 24 days) take the one-multiply form;
+// x = 1000a + b gives floor(x dt / 1000) = a dt + floor(b dt / 1000), so both forms agree.
 KSA_HD int64_t per_ms(int64_t x_milli, int64_t dt_ms) {
+  if (x_milli <= 0 || dt_ms <= 0) return 0;
+  if (((x_milli | dt_ms) >> 31) == 0) return x_milli * dt_ms / 1000;
   return sat_add(sat_mul(x_milli / 1000, dt_ms), sat_mul(x_milli % 1000, dt_ms) / 1000);
 }
 

@@ -251,8 +251,14 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
              downs=0, final_replicas=0, max_replicas=init_replicas, polls=0)
     st = {"q": model.init_backlog * 1000, "ready": init_replicas, "pending": 0, "pending_at": 0, "draws": 0}
 
+    def sat_add(a: int, b: int) -> int:  # the C++ accumulators saturate at 2^62
+        return min(a + b, _SAT)
+
+    def sat_mul(a: int, b: int) -> int:
+        return 0 if a <= 0 or b <= 0 else min(a * b, _SAT)
+
     def per_ms(x_milli: int, dt: int) -> int:
-        return min(x_milli // 1000 * dt, _SAT) + min((x_milli % 1000) * dt, _SAT) // 1000
+        return sat_add(sat_mul(x_milli // 1000, dt), sat_mul(x_milli % 1000, dt) // 1000)
 
     def expected(t0: int, t1: int) -> int:
         total = 0
@@ -260,7 +266,7 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
             end = t_ms[i + 1] if i + 1 < len(t_ms) else max(t1, start)
             a, b = max(start, t0), min(end, t1)
             if b > a:
-                total += per_ms(rate[i], b - a)
+                total = sat_add(total, per_ms(rate[i], b - a))
         return total
 
     def advance(t0: int, t1: int, replicas: int) -> None:
@@ -268,20 +274,20 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
             return
         dt = t1 - t0
         q0 = st["q"] // 1000
-        r["pod_ms"] += max(replicas, 0) * dt
-        r["backlog_msg_ms"] += max(q0, 0) * dt
+        r["pod_ms"] = sat_add(r["pod_ms"], sat_mul(replicas, dt))
+        r["backlog_msg_ms"] = sat_add(r["backlog_msg_ms"], sat_mul(q0, dt))
         if q0 > model.slo_backlog:
             r["violation_ms"] += dt
         a = _sample_milli(expected(t0, t1), seed, st["draws"])
         st["draws"] += 1
-        st["q"] += a
-        r["arrived"] += a
-        cap = max(st["ready"], 0) * per_ms(service, dt)
+        st["q"] = sat_add(st["q"], a)
+        r["arrived"] = sat_add(r["arrived"], a)
+        cap = sat_mul(st["ready"], per_ms(service, dt))
         if st["pending"] > 0 and st["pending_at"] < t1:
-            cap += st["pending"] * per_ms(service, t1 - max(st["pending_at"], t0))
+            cap = sat_add(cap, sat_mul(st["pending"], per_ms(service, t1 - max(st["pending_at"], t0))))
         served = min(st["q"], cap)
         st["q"] -= served
-        r["served"] += served
+        r["served"] = sat_add(r["served"], served)
         if st["pending"] > 0 and st["pending_at"] <= t1:
             st["ready"] += st["pending"]
             st["pending"] = 0

@@ -132,3 +132,19 @@ def test_tune_cli_closed_loop_argument_errors(tmp_path):
         main(["--arrivals", str(csv_path), "--service-rate", "1", "--objective", "nope", "--device", "cpu"])
     with pytest.raises(SystemExit):
         main(["--arrivals", str(csv_path), "--trace", str(csv_path), "--service-rate", "1"])
+
+
+@pytest.mark.parametrize("rate,service,poll_s,init", [(1e6, 1e6, 20 * 86400, 10**12), (1e6, 0.001, 3, 10**12),
+                                                      (999_999.999, 1e6, 86400, 0), (0.001, 1e6, 1, 10**12)])
+def test_cpu_path_equals_python_model_at_extremes(nat, rate, service, poll_s, init):
+    """Bounds of the validated inputs: maximum rates, 20-day polls in a 30-day horizon (intervals
+    above 2^31 ms), a 1e12-message backlog -- the saturating and wide-operand paths."""
+    tr = cl.ArrivalTrace.from_segments([(0, rate), (7 * 86400, rate / 2)])
+    grid = sweep.grid(poll_ns=[poll_s * S], up_cool_ns=[0], down_cool_ns=[0], up_msgs=[1, 10**15], max_pods=[2**31 - 1, 50])
+    model = cl.QueueModel(service_rate=service, startup_ns=86400 * S, slo_backlog=0, init_backlog=init)
+    horizon = (30 * 86400 if poll_s > 86400 else 400) * S
+    res = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=2, seed0=5, device="cpu")
+    for i in range(len(res)):
+        for s in range(2):
+            want = cl.reference_lane(tr, res.config(i), model, 1, horizon, (0, 0, 0), 5 + s)
+            assert {k: int(v[i, s]) for k, v in res.out.items()} == want, (res.config(i), s)

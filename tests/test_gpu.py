@@ -130,3 +130,24 @@ def test_closed_loop_kernel_equals_cpu_and_python_model():
     for i in range(0, len(g), 37):
         want = cl.reference_lane(tr, g.config(i), model, 1, 2400 * S, lat, 1 + 5)
         assert {k: int(v[i, 5]) for k, v in g.out.items()} == want
+
+
+def test_closed_loop_kernel_equals_cpu_at_extremes():
+    """The saturating / wide-operand paths of the closed-loop model on the GPU: maximum rates,
+    20-day polls (intervals above 2^31 ms), a 1e12-message backlog."""
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import closedloop as cl
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    S = 1_000_000_000
+    for rate, service, poll_s, init in [(1e6, 1e6, 20 * 86400, 10**12), (1e6, 0.001, 3, 10**12), (0.001, 1e6, 1, 10**12)]:
+        tr = cl.ArrivalTrace.from_segments([(0, rate), (7 * 86400, rate / 2)])
+        grid = sweep.grid(poll_ns=[poll_s * S], up_cool_ns=[0], down_cool_ns=[0], up_msgs=[1, 10**15],
+                          max_pods=[2**31 - 1, 50])
+        model = cl.QueueModel(service_rate=service, startup_ns=86400 * S, slo_backlog=0, init_backlog=init)
+        horizon = (30 * 86400 if poll_s > 86400 else 400) * S
+        g = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=4, device="gpu")
+        c = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=4, device="cpu")
+        for k in g.out:
+            assert np.array_equal(g.out[k], c.out[k]), (rate, k)
