@@ -100,9 +100,18 @@ def main(argv=None) -> int:
     samples = torch.tensor(sorted(res.samples), dtype=torch.int64, device=device)
     wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
     if world > 1:
-        gathered = [torch.empty_like(samples) for _ in range(world)]
-        dist.all_gather(gathered, samples)
+        # Ranks can hold different sample counts (a poll whose write failed records none):
+        # all_gather needs equal shapes, so pad to the largest count with -1 and drop the padding.
+        count = torch.tensor([samples.numel()], dtype=torch.int64, device=device)
+        counts = [torch.empty_like(count) for _ in range(world)]
+        dist.all_gather(counts, count)
+        longest = max(int(c.item()) for c in counts)
+        padded = torch.full((longest,), -1, dtype=torch.int64, device=device)
+        padded[: samples.numel()] = samples
+        gathered = [torch.empty_like(padded) for _ in range(world)]
+        dist.all_gather(gathered, padded)
         samples = torch.cat(gathered)
+        samples = samples[samples >= 0]
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
     all_ns = sorted(samples.cpu().tolist())
     wall_max = float(wall_t.item())
