@@ -12,6 +12,7 @@
 #include <openssl/err.h>
 #include <openssl/evp.h>
 #include <openssl/pem.h>
+#include <openssl/rand.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <poll.h>
@@ -120,6 +121,10 @@ class Stream {
     if (ssl_) {
       SSL_shutdown(ssl_);
       SSL_free(ssl_);
+    }
+    if (outer_) {
+      SSL_shutdown(outer_);
+      SSL_free(outer_);
     }
     if (fd_ >= 0) ::close(fd_);
   }
@@ -234,6 +239,12 @@ class Stream {
   void set_cancel_fd(int fd) { cancel_fd_ = fd; }
   SSL* ssl() const { return ssl_; }
   void attach_ssl(SSL* ssl) { ssl_ = ssl; }  // TLS inside an established CONNECT tunnel
+  // TLS inside TLS (an https origin behind an https proxy): `inner` becomes the session the
+  // stream reads and writes; its BIO (tunnel_bio) carries its records through the current one.
+  void push_ssl(SSL* inner) {
+    outer_ = ssl_;
+    ssl_ = inner;
+  }
 
  private:
   // Busy-poll: peek the socket for up to spin_ns_ before sleeping in poll(2). A response that
@@ -255,9 +266,60 @@ class Stream {
 
   int fd_;
   SSL* ssl_;
+  SSL* outer_ = nullptr;  // the proxy's TLS session when ssl_ runs inside it
   int64_t spin_ns_ = 0;
   int cancel_fd_ = -1;
 };
+
+// BIO carrying one TLS session's records inside another (the https-proxy tunnel). Non-blocking
+// like the socket under it: when the outer session needs socket readiness the BIO reports a
+// retry, the inner SSL call returns WANT_READ / WANT_WRITE, and Stream::ssl_op waits on the fd.
+int tunnel_result(BIO* b, SSL* outer, int r) {
+  if (r > 0) return r;
+  switch (SSL_get_error(outer, r)) {
+    case SSL_ERROR_WANT_READ: BIO_set_retry_read(b); return -1;
+    case SSL_ERROR_WANT_WRITE: BIO_set_retry_write(b); return -1;
+    case SSL_ERROR_ZERO_RETURN: return 0;
+    default: return -1;
+  }
+}
+
+int tunnel_write(BIO* b, const char* buf, int len) {
+  BIO_clear_retry_flags(b);
+  SSL* outer = static_cast<SSL*>(BIO_get_data(b));
+  return tunnel_result(b, outer, SSL_write(outer, buf, len));
+}
+
+int tunnel_read(BIO* b, char* buf, int len) {
+  BIO_clear_retry_flags(b);
+  SSL* outer = static_cast<SSL*>(BIO_get_data(b));
+  return tunnel_result(b, outer, SSL_read(outer, buf, len));
+}
+
+long tunnel_ctrl(BIO* b, int cmd, long, void*) {
+  switch (cmd) {
+    case BIO_CTRL_FLUSH: return 1;
+    case BIO_CTRL_PENDING: return SSL_pending(static_cast<SSL*>(BIO_get_data(b)));
+    default: return 0;
+  }
+}
+
+BIO* tunnel_bio(SSL* outer) {
+  static BIO_METHOD* method = [] {
+    BIO_METHOD* m = BIO_meth_new(BIO_get_new_index() | BIO_TYPE_SOURCE_SINK, "tls-in-tls");
+    BIO_meth_set_write(m, tunnel_write);
+    BIO_meth_set_read(m, tunnel_read);
+    BIO_meth_set_ctrl(m, tunnel_ctrl);
+    BIO_meth_set_create(m, [](BIO* b) {
+      BIO_set_init(b, 1);
+      return 1;
+    });
+    return m;
+  }();
+  BIO* b = BIO_new(method);
+  if (b) BIO_set_data(b, outer);
+  return b;
+}
 
 // Largest message body either side accepts. Scale objects and Deployments are a few KiB and a
 // NodeList of a large cluster a few tens of MiB; a peer announcing more (or a chunked /
@@ -598,6 +660,101 @@ const char* http_reason(int status) {
 // ---------------------------------------------------------------------------------------
 // Client
 
+namespace {
+
+const char* socks5_reply_text(int code) {
+  switch (code) {
+    case 1: return "general SOCKS server failure";
+    case 2: return "connection not allowed by ruleset";
+    case 3: return "network unreachable";
+    case 4: return "host unreachable";
+    case 5: return "connection refused";
+    case 6: return "TTL expired";
+    case 7: return "command not supported";
+    case 8: return "address type not supported";
+    default: return "unknown code";
+  }
+}
+
+// SOCKS5 CONNECT to `origin` (RFC 1928), with username/password authentication (RFC 1929)
+// when the proxy URL carried credentials. Host names go to the proxy unresolved, as Go's
+// socks dialer sends them. Error texts follow Go's "socks connect tcp proxy->dst: reason".
+Status socks5_connect(Stream* stream, std::string* rbuf, const Url& proxy, const Url& origin, const std::string& user,
+                      const std::string& pass, int64_t deadline_ns) {
+  auto bracket = [](const std::string& h) { return h.find(':') != std::string::npos ? "[" + h + "]" : h; };
+  const std::string where = "socks connect tcp " + bracket(proxy.host) + ":" + std::to_string(proxy.port) + "->" +
+                            bracket(origin.host) + ":" + std::to_string(origin.port) + ": ";
+  const bool auth = !user.empty() || !pass.empty();
+  Reader rd(stream, rbuf);
+  std::string greet = auth ? std::string("\x05\x02\x00\x02", 4) : std::string("\x05\x01\x00", 3);
+  Status s = stream->write_all(greet, deadline_ns);
+  if (!s.ok()) return Status::Err(where + s.message());
+  std::string r;
+  s = rd.read_exact(2, &r, deadline_ns);
+  if (!s.ok()) return Status::Err(where + s.message());
+  if (r[0] != 0x05) return Status::Err(where + "unexpected protocol version " + std::to_string(static_cast<uint8_t>(r[0])));
+  const uint8_t method = static_cast<uint8_t>(r[1]);
+  if (method == 0x02 && auth) {
+    std::string up;
+    up.push_back(0x01);
+    up.push_back(static_cast<char>(user.size()));
+    up += user;
+    up.push_back(static_cast<char>(pass.size()));
+    up += pass;
+    s = stream->write_all(up, deadline_ns);
+    if (!s.ok()) return Status::Err(where + s.message());
+    r.clear();
+    s = rd.read_exact(2, &r, deadline_ns);
+    if (!s.ok()) return Status::Err(where + s.message());
+    if (r[1] != 0x00) return Status::Err(where + "username/password authentication failed");
+  } else if (method != 0x00) {
+    return Status::Err(where + "no acceptable authentication methods");
+  }
+  std::string req("\x05\x01\x00", 3);
+  unsigned char addr[16];
+  if (inet_pton(AF_INET, origin.host.c_str(), addr) == 1) {
+    req.push_back(0x01);
+    req.append(reinterpret_cast<char*>(addr), 4);
+  } else if (inet_pton(AF_INET6, origin.host.c_str(), addr) == 1) {
+    req.push_back(0x04);
+    req.append(reinterpret_cast<char*>(addr), 16);
+  } else {
+    if (origin.host.size() > 255) return Status::Err(where + "FQDN too long");
+    req.push_back(0x03);
+    req.push_back(static_cast<char>(origin.host.size()));
+    req += origin.host;
+  }
+  req.push_back(static_cast<char>((origin.port >> 8) & 0xFF));
+  req.push_back(static_cast<char>(origin.port & 0xFF));
+  s = stream->write_all(req, deadline_ns);
+  if (!s.ok()) return Status::Err(where + s.message());
+  r.clear();
+  s = rd.read_exact(4, &r, deadline_ns);
+  if (!s.ok()) return Status::Err(where + s.message());
+  if (r[0] != 0x05) return Status::Err(where + "unexpected protocol version " + std::to_string(static_cast<uint8_t>(r[0])));
+  if (r[1] != 0x00) return Status::Err(where + socks5_reply_text(static_cast<uint8_t>(r[1])));
+  size_t skip = 2;  // bound port
+  switch (static_cast<uint8_t>(r[3])) {
+    case 0x01: skip += 4; break;
+    case 0x04: skip += 16; break;
+    case 0x03: {
+      std::string n;
+      s = rd.read_exact(1, &n, deadline_ns);
+      if (!s.ok()) return Status::Err(where + s.message());
+      skip += static_cast<uint8_t>(n[0]);
+      break;
+    }
+    default: return Status::Err(where + "unknown address type " + std::to_string(static_cast<uint8_t>(r[3])));
+  }
+  std::string bound;
+  s = rd.read_exact(skip, &bound, deadline_ns);
+  if (!s.ok()) return Status::Err(where + s.message());
+  if (!rbuf->empty()) return Status::Err(where + "unexpected data after the reply");
+  return Status::OK();
+}
+
+}  // namespace
+
 struct HttpClient::Conn {
   std::unique_ptr<Stream> stream;
   std::string rbuf;
@@ -608,30 +765,33 @@ struct HttpClient::Conn {
 HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
     : origin_(origin), tls_(std::move(tls)), timeout_(timeout) {
   cancel_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-  if (!origin_.tls()) return;
+  if (origin_.tls()) ctx_status_ = init_tls_ctx();
+}
+
+// The client's TLS configuration: used for an https origin and for an https proxy (Go's
+// transport also dials an https proxy with its TLSClientConfig).
+Status HttpClient::init_tls_ctx() {
+  if (ctx_) return Status::OK();
   ensure_ssl();
   ignore_sigpipe_once();
   ctx_ = SSL_CTX_new(TLS_client_method());
-  if (!ctx_) {
-    ctx_status_ = Status::Err("SSL_CTX_new: " + ssl_error_string());
-    return;
-  }
+  if (!ctx_) return Status::Err("SSL_CTX_new: " + ssl_error_string());
+  Status st;
   SSL_CTX_set_min_proto_version(ctx_, TLS1_2_VERSION);
   if (tls_.insecure_skip_verify) {
     SSL_CTX_set_verify(ctx_, SSL_VERIFY_NONE, nullptr);
   } else {
     SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
     if (!tls_.ca_pem.empty()) {
-      ctx_status_ = load_ca_pem(ctx_, tls_.ca_pem);
+      st = load_ca_pem(ctx_, tls_.ca_pem);
     } else if (!tls_.ca_file.empty()) {
       if (SSL_CTX_load_verify_locations(ctx_, tls_.ca_file.c_str(), nullptr) != 1)
-        ctx_status_ = Status::Err("unable to load CA file " + tls_.ca_file + ": " + ssl_error_string());
+        st = Status::Err("unable to load CA file " + tls_.ca_file + ": " + ssl_error_string());
     } else {
       SSL_CTX_set_default_verify_paths(ctx_);
     }
   }
-  if (ctx_status_.ok() && !tls_.cert_pem.empty())
-    ctx_status_ = use_cert_key(ctx_, tls_.cert_pem, tls_.key_pem);
+  if (st.ok() && !tls_.cert_pem.empty()) st = use_cert_key(ctx_, tls_.cert_pem, tls_.key_pem);
   // Session resumption makes reconnects after an idle close cheap.
   SSL_CTX_set_session_cache_mode(ctx_, SSL_SESS_CACHE_CLIENT);
   // Read-ahead: pull whatever the socket holds in one read(2) instead of a 5-byte record
@@ -642,6 +802,7 @@ HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
 #ifdef SSL_OP_IGNORE_UNEXPECTED_EOF
   SSL_CTX_set_options(ctx_, SSL_OP_IGNORE_UNEXPECTED_EOF);
 #endif
+  return st;
 }
 
 HttpClient::~HttpClient() {
@@ -677,10 +838,34 @@ Status HttpClient::set_proxy(const std::string& proxy_url) {
   conn_.reset();
   has_proxy_ = false;
   proxy_auth_.clear();
+  proxy_user_.clear();
+  proxy_pass_.clear();
   if (proxy_url.empty()) return Status::OK();
-  auto u = parse_url(proxy_url);
+  const size_t sep = proxy_url.find("://");
+  const std::string scheme = sep == std::string::npos ? "" : lower(proxy_url.substr(0, sep));
+  ProxyKind kind = ProxyKind::Http;
+  std::string as_http = proxy_url;  // parse_url knows http(s) only; socks5 shares the syntax
+  if (scheme == "https") {
+    kind = ProxyKind::Https;
+  } else if (scheme == "socks5" || scheme == "socks5h") {
+    kind = ProxyKind::Socks5;
+    as_http = "http" + proxy_url.substr(sep);
+  } else if (scheme != "http") {
+    return Status::Err("proxy: unknown scheme \"" + scheme + "\" (http, https or socks5)");
+  }
+  auto u = parse_url(as_http);
   if (!u.status.ok()) return Status::Err("proxy: " + u.status.message());
-  if (u.value.tls()) return Status::Err("proxy: https:// proxies are not supported (use http://)");
+  if (kind == ProxyKind::Socks5) {  // no explicit port: 1080, not http's 80
+    std::string host_port = proxy_url.substr(sep + 3);
+    host_port = host_port.substr(0, host_port.find_first_of("/?#"));
+    host_port = host_port.substr(host_port.rfind('@') == std::string::npos ? 0 : host_port.rfind('@') + 1);
+    const size_t rb = host_port.rfind(']');
+    if (host_port.find(':', rb == std::string::npos ? 0 : rb) == std::string::npos) u.value.port = 1080;
+  }
+  if (kind == ProxyKind::Https) {
+    if (!ctx_) ctx_status_ = init_tls_ctx();
+    if (!ctx_status_.ok()) return Status::Err("proxy: " + ctx_status_.message());
+  }
   // userinfo (parse_url drops it): scheme://user[:pass]@host
   const size_t a = proxy_url.find("://") + 3;
   const size_t end = proxy_url.find_first_of("/?#", a);
@@ -691,9 +876,16 @@ Status HttpClient::set_proxy(const std::string& proxy_url) {
     const size_t colon = info.find(':');
     std::string user = percent_decode(info.substr(0, colon));
     std::string pass = colon == std::string::npos ? "" : percent_decode(info.substr(colon + 1));
-    proxy_auth_ = "Basic " + base64(user + ":" + pass);
+    if (kind == ProxyKind::Socks5) {
+      if (user.size() > 255 || pass.size() > 255) return Status::Err("proxy: socks5 user or password longer than 255 bytes");
+      proxy_user_ = user;
+      proxy_pass_ = pass;
+    } else {
+      proxy_auth_ = "Basic " + base64(user + ":" + pass);
+    }
   }
   proxy_ = u.value;
+  proxy_kind_ = kind;
   has_proxy_ = true;
   return Status::OK();
 }
@@ -741,7 +933,30 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   auto stream = std::make_unique<Stream>(fd, nullptr);
   stream->set_cancel_fd(cancel_fd_);
   std::string rbuf;
-  if (has_proxy_ && origin_.tls()) {
+  if (has_proxy_ && proxy_kind_ == ProxyKind::Https) {
+    // TLS to the proxy itself, verified like the origin would be but against the proxy's name.
+    SSL* outer = SSL_new(ctx_);
+    stream->attach_ssl(outer);
+    SSL_set_fd(outer, fd);
+    if (!is_ip_literal(proxy_.host)) SSL_set_tlsext_host_name(outer, proxy_.host.c_str());
+    if (!tls_.insecure_skip_verify) {
+      X509_VERIFY_PARAM* param = SSL_get0_param(outer);
+      if (is_ip_literal(proxy_.host)) X509_VERIFY_PARAM_set1_ip_asc(param, proxy_.host.c_str());
+      else X509_VERIFY_PARAM_set1_host(param, proxy_.host.c_str(), 0);
+    }
+    Status h = stream->handshake(false, deadline_ns);
+    if (!h.ok()) {
+      long vr = SSL_get_verify_result(outer);
+      if (vr != X509_V_OK)
+        return Status::Err("proxyconnect tcp: x509: certificate verification failed: " +
+                           std::string(X509_verify_cert_error_string(vr)));
+      return Status::Err("proxyconnect tcp: " + h.message());
+    }
+  }
+  if (has_proxy_ && proxy_kind_ == ProxyKind::Socks5) {
+    Status sc = socks5_connect(stream.get(), &rbuf, proxy_, origin_, proxy_user_, proxy_pass_, deadline_ns);
+    if (!sc.ok()) return sc;
+  } else if (has_proxy_ && origin_.tls()) {
     // CONNECT tunnel: the proxy relays bytes; TLS (and its verification) is end to end.
     std::string authority = origin_.host.find(':') != std::string::npos ? "[" + origin_.host + "]" : origin_.host;
     authority += ":" + std::to_string(origin_.port);
@@ -769,8 +984,18 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   SSL* ssl = nullptr;
   if (origin_.tls()) {
     ssl = SSL_new(ctx_);
-    stream->attach_ssl(ssl);
-    SSL_set_fd(ssl, fd);
+    if (stream->ssl()) {  // https proxy: the origin's TLS runs inside the proxy's
+      BIO* b = tunnel_bio(stream->ssl());
+      if (!b) {
+        SSL_free(ssl);
+        return Status::Err("tls: cannot create the tunnel BIO");
+      }
+      SSL_set_bio(ssl, b, b);
+      stream->push_ssl(ssl);
+    } else {
+      stream->attach_ssl(ssl);
+      SSL_set_fd(ssl, fd);
+    }
     const std::string& name = tls_.server_name.empty() ? origin_.host : tls_.server_name;
     if (!is_ip_literal(name)) SSL_set_tlsext_host_name(ssl, name.c_str());
     if (!tls_.insecure_skip_verify) {
@@ -814,11 +1039,11 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   wire += req.method;
   wire.push_back(' ');
   // A plain-HTTP origin behind a proxy gets the absolute-form target (RFC 9112 §3.2.2).
-  if (has_proxy_ && !origin_.tls()) wire += origin_.origin();
+  if (forward_proxy() && !origin_.tls()) wire += origin_.origin();
   wire += req.target.empty() ? "/" : req.target;
   wire += " HTTP/1.1\r\n";
   if (!has_header(req.headers, "Host")) wire += "Host: " + origin_.host_header() + "\r\n";
-  if (has_proxy_ && !origin_.tls() && !proxy_auth_.empty()) wire += "Proxy-Authorization: " + proxy_auth_ + "\r\n";
+  if (forward_proxy() && !origin_.tls() && !proxy_auth_.empty()) wire += "Proxy-Authorization: " + proxy_auth_ + "\r\n";
   if (!has_header(req.headers, "User-Agent")) wire += "User-Agent: kube-sqs-autoscaler-amd/1.0\r\n";
   for (auto& [k, v] : req.headers) wire += k + ": " + v + "\r\n";
   if (!req.body.empty() || req.method == "POST" || req.method == "PUT" || req.method == "PATCH") {
@@ -1182,6 +1407,15 @@ Status generate_self_signed(const std::string& host, std::string* cert_pem, std:
   X509_NAME* name = X509_get_subject_name(x);
   X509_NAME_add_entry_by_txt(name, "CN", MBSTRING_ASC,
                              reinterpret_cast<const unsigned char*>(host.c_str()), -1, -1, 0);
+  // A distinct subject per certificate: two self-signed certificates for the same host (a proxy
+  // and an apiserver, both trusted in one CA bundle) must not shadow each other in the store's
+  // lookup by subject name.
+  unsigned char rnd[8];
+  RAND_bytes(rnd, sizeof rnd);
+  char org[32];
+  std::snprintf(org, sizeof org, "ksa-%02x%02x%02x%02x%02x%02x%02x%02x", rnd[0], rnd[1], rnd[2], rnd[3], rnd[4],
+                rnd[5], rnd[6], rnd[7]);
+  X509_NAME_add_entry_by_txt(name, "O", MBSTRING_ASC, reinterpret_cast<const unsigned char*>(org), -1, -1, 0);
   X509_set_issuer_name(x, name);
   std::string san = (is_ip_literal(host) ? "IP:" : "DNS:") + host;
   X509V3_CTX v3;

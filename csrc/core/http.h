@@ -109,11 +109,20 @@ class HttpClient {
   // slower peers (real AWS / apiserver RTTs of milliseconds) it never spins. 0 disables.
   void set_busy_poll(Nanos ns) { spin_ns_ = ns; }
   Nanos rtt_ewma() const;
-  // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller):
-  // "http://[user:pass@]host:port". An https origin is reached through a CONNECT tunnel (TLS
-  // runs end to end inside it); an http origin gets absolute-form requests sent to the proxy.
-  // Credentials in the URL become Proxy-Authorization: Basic. Empty = connect directly. Call
-  // before the first request.
+  // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller), the
+  // three kinds Go's transport speaks:
+  //   "http://[user:pass@]host:port"   an https origin is reached through a CONNECT tunnel (TLS
+  //                                    runs end to end inside it); an http origin gets
+  //                                    absolute-form requests. Credentials become
+  //                                    Proxy-Authorization: Basic.
+  //   "https://[user:pass@]host:port"  the same, over TLS to the proxy (verified against the
+  //                                    client's trust settings and the proxy's host name, as
+  //                                    Go's transport does); an https origin then runs TLS
+  //                                    inside that TLS.
+  //   "socks5://[user:pass@]host:port" a SOCKS5 CONNECT (RFC 1928; user/password auth per
+  //                                    RFC 1929) with the origin's host name resolved by the
+  //                                    proxy; requests then go out as on a direct connection.
+  // Empty = connect directly. Call before the first request.
   Status set_proxy(const std::string& proxy_url);
   bool proxied() const {
     std::lock_guard<std::mutex> lk(mu_);
@@ -143,8 +152,13 @@ class HttpClient {
   Nanos ewma_ns_ = -1;   // response-time EWMA (-1: no sample yet)
   int64_t sent_at_ = 0;  // mono time the current request finished writing
   Nanos spin_window() const;
+  Status init_tls_ctx();
+  bool forward_proxy() const { return has_proxy_ && proxy_kind_ != ProxyKind::Socks5; }
+  enum class ProxyKind { Http, Https, Socks5 };
   bool has_proxy_ = false;
+  ProxyKind proxy_kind_ = ProxyKind::Http;
   Url proxy_;
+  std::string proxy_user_, proxy_pass_;  // socks5 credentials
   std::string proxy_auth_;  // "Basic ..." or empty
   bool in_flight_ = false;
   int cancel_fd_ = -1;  // eventfd signalled by cancel(); polled next to the socket

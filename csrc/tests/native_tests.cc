@@ -6,6 +6,8 @@
 // the threaded fake servers and the keep-alive clients are exercised concurrently so TSan can
 // see every cross-thread access of the runtime.
 #include <arpa/inet.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
 #include <netinet/in.h>
 #include <poll.h>
 #include <sys/socket.h>
@@ -248,7 +250,21 @@ TEST(http_tls_roundtrip) {
 // Minimal CONNECT relay (one tunnel): records the request head, dials the target, relays bytes.
 class ConnectRelay {
  public:
-  ConnectRelay() {
+  // With a certificate, the relay is an https:// proxy: clients reach it over TLS.
+  explicit ConnectRelay(const std::string& cert_pem = "", const std::string& key_pem = "") {
+    if (!cert_pem.empty()) {
+      ctx_ = SSL_CTX_new(TLS_server_method());
+      BIO* cb = BIO_new_mem_buf(cert_pem.data(), static_cast<int>(cert_pem.size()));
+      X509* x = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr);
+      BIO* kb = BIO_new_mem_buf(key_pem.data(), static_cast<int>(key_pem.size()));
+      EVP_PKEY* k = PEM_read_bio_PrivateKey(kb, nullptr, nullptr, nullptr);
+      SSL_CTX_use_certificate(ctx_, x);
+      SSL_CTX_use_PrivateKey(ctx_, k);
+      X509_free(x);
+      EVP_PKEY_free(k);
+      BIO_free(cb);
+      BIO_free(kb);
+    }
     lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
     sockaddr_in a{};
     a.sin_family = AF_INET;
@@ -264,6 +280,7 @@ class ConnectRelay {
     ::shutdown(lfd_, SHUT_RDWR);
     th_.join();
     ::close(lfd_);
+    if (ctx_) SSL_CTX_free(ctx_);
   }
   int port() const { return port_; }
   std::string head() {
@@ -272,14 +289,32 @@ class ConnectRelay {
   }
 
  private:
+  // Client side of the relay: plain socket or (https proxy) a blocking TLS session on it.
+  ssize_t crecv(int c, char* b, size_t n) { return ssl_ ? SSL_read(ssl_, b, static_cast<int>(n)) : ::recv(c, b, n, 0); }
+  ssize_t csend(int c, const char* b, size_t n) {
+    return ssl_ ? SSL_write(ssl_, b, static_cast<int>(n)) : ::send(c, b, n, MSG_NOSIGNAL);
+  }
+
   void run() {
     int c = ::accept(lfd_, nullptr, nullptr);
     if (c < 0) return;
+    if (ctx_) {
+      ssl_ = SSL_new(ctx_);
+      SSL_set_fd(ssl_, c);
+      if (SSL_accept(ssl_) != 1) {
+        SSL_free(ssl_);
+        ssl_ = nullptr;
+        ::close(c);
+        return;
+      }
+    }
     std::string buf;
     char tmp[4096];
     while (buf.find("\r\n\r\n") == std::string::npos) {
-      ssize_t n = ::recv(c, tmp, sizeof tmp, 0);
+      ssize_t n = crecv(c, tmp, sizeof tmp);
       if (n <= 0) {
+        if (ssl_) SSL_free(ssl_);
+        ssl_ = nullptr;
         ::close(c);
         return;
       }
@@ -299,23 +334,31 @@ class ConnectRelay {
     a.sin_port = htons(static_cast<uint16_t>(up_port));
     if (::connect(u, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0) {
       const char ok[] = "HTTP/1.1 200 Connection established\r\n\r\n";
-      ::send(c, ok, sizeof ok - 1, MSG_NOSIGNAL);
+      csend(c, ok, sizeof ok - 1);
       pollfd p[2] = {{c, POLLIN, 0}, {u, POLLIN, 0}};
-      while (::poll(p, 2, 5000) > 0) {
+      while ((ssl_ && SSL_pending(ssl_) > 0) || ::poll(p, 2, 5000) > 0) {
         bool done = false;
-        for (int i = 0; i < 2; ++i) {
-          if (!(p[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-          ssize_t n = ::recv(p[i].fd, tmp, sizeof tmp, 0);
-          if (n <= 0 || ::send(p[1 - i].fd, tmp, static_cast<size_t>(n), MSG_NOSIGNAL) != n) done = true;
+        if ((ssl_ && SSL_pending(ssl_) > 0) || (p[0].revents & (POLLIN | POLLHUP | POLLERR))) {
+          ssize_t n = crecv(c, tmp, sizeof tmp);
+          if (n <= 0 || ::send(u, tmp, static_cast<size_t>(n), MSG_NOSIGNAL) != n) done = true;
         }
+        if (p[1].revents & (POLLIN | POLLHUP | POLLERR)) {
+          ssize_t n = ::recv(u, tmp, sizeof tmp, 0);
+          if (n <= 0 || csend(c, tmp, static_cast<size_t>(n)) != n) done = true;
+        }
+        p[0].revents = p[1].revents = 0;
         if (done) break;
       }
     }
     ::close(u);
+    if (ssl_) SSL_free(ssl_);
+    ssl_ = nullptr;
     ::close(c);
   }
 
   int lfd_ = -1, port_ = 0;
+  SSL_CTX* ctx_ = nullptr;
+  SSL* ssl_ = nullptr;
   std::thread th_;
   std::mutex mu_;
   std::string head_;
@@ -346,7 +389,40 @@ TEST(http_tls_through_connect_proxy) {
   const std::string head = relay.head();
   CHECK(head.rfind("CONNECT 127.0.0.1:" + std::to_string(srv.port()) + " HTTP/1.1\r\n", 0) == 0);
   CHECK(head.find("Proxy-Authorization: Basic dXNlcjpwQHNz") != std::string::npos);  // user:p@ss
-  CHECK(!c.set_proxy("https://127.0.0.1:1").ok());
+  CHECK(!c.set_proxy("ftp://127.0.0.1:1").ok());
+  c.close();
+  srv.stop();
+}
+
+// https:// proxy: TLS to the proxy, then the origin's TLS inside it (the tunnel BIO), under
+// the sanitizer builds too.
+TEST(http_tls_inside_tls_proxy) {
+  std::string cert, key, pcert, pkey;
+  CHECK(generate_self_signed("127.0.0.1", &cert, &key).ok());
+  CHECK(generate_self_signed("127.0.0.1", &pcert, &pkey).ok());
+  HttpServer srv([](const HttpRequest& req, HttpResponse* resp) {
+    resp->status = 200;
+    resp->body = std::string(70000, 'z') + req.target;  // several TLS records each way
+  });
+  CHECK(srv.enable_tls(cert, key).ok());
+  CHECK(srv.listen("127.0.0.1", 0).ok());
+  ConnectRelay relay(pcert, pkey);
+  TlsOptions tls;
+  tls.ca_pem = cert + pcert;
+  HttpClient c(parse_url("https://127.0.0.1:" + std::to_string(srv.port())).value, tls, 5 * kSecond);
+  CHECK(c.set_proxy("https://127.0.0.1:" + std::to_string(relay.port())).ok());
+  for (int i = 0; i < 3; ++i) {
+    HttpRequest req;
+    req.method = "POST";
+    req.target = "/y" + std::to_string(i);
+    req.body = std::string(50000, 'q');
+    HttpResponse resp;
+    CHECK(c.round_trip(req, &resp).ok());
+    CHECK_EQ(resp.body.size(), size_t(70003));
+    CHECK_EQ(resp.body.substr(70000), "/y" + std::to_string(i));
+  }
+  CHECK_EQ(c.stats().connects, uint64_t(1));
+  CHECK(relay.head().rfind("CONNECT 127.0.0.1:" + std::to_string(srv.port()) + " HTTP/1.1\r\n", 0) == 0);
   c.close();
   srv.stop();
 }

@@ -5,7 +5,10 @@ client-go. Both use ``http.ProxyFromEnvironment`` (golang.org/x/net/http/httppro
 behind an egress proxy works when ``HTTPS_PROXY`` / ``NO_PROXY`` are set. client-go v0.19
 (``/root/reference/go.mod:15``) also honours a kubeconfig cluster's ``proxy-url``. This module
 picks the proxy the same way. The native ``HttpClient::set_proxy`` (``csrc/core/http.cc``)
-then tunnels https origins with CONNECT and sends absolute-form requests for http ones.
+speaks the three proxy kinds Go's transport does: ``http://`` and ``https://`` proxies (CONNECT
+tunnels for https origins, absolute-form requests for http ones; an https proxy is itself
+reached over verified TLS) and ``socks5://`` (a SOCKS5 CONNECT, host names resolved by the
+proxy).
 
 Rules (httpproxy ``Config.ProxyFunc``):
 
@@ -29,7 +32,7 @@ import urllib.parse
 from dataclasses import dataclass, field
 from typing import List, Mapping, Optional, Tuple
 
-SUPPORTED_SCHEMES = ("http",)  # what the native client speaks to a proxy
+SUPPORTED_SCHEMES = ("http", "https", "socks5", "socks5h")  # what the native client speaks to a proxy
 
 
 class ProxyError(ValueError):
@@ -50,7 +53,7 @@ def parse_proxy(value: str) -> str:
     if not value:
         return ""
     u = urllib.parse.urlsplit(value)
-    if u.scheme not in ("http", "https", "socks5") or not u.hostname:
+    if u.scheme not in SUPPORTED_SCHEMES or not u.hostname:
         u = urllib.parse.urlsplit("http://" + value)
         if not u.hostname:
             raise ProxyError(f"invalid proxy address {value!r}")
@@ -172,10 +175,10 @@ class ProxyConfig:
 
 
 def check_supported(proxy: str) -> str:
-    """Rejects proxy schemes the native client does not speak. Go's transport also speaks
-    https:// and socks5:// proxies; we fail loudly rather than connect directly."""
+    """Rejects a proxy scheme the native client does not speak (fail loudly rather than
+    connect directly)."""
     if proxy and urllib.parse.urlsplit(proxy).scheme not in SUPPORTED_SCHEMES:
-        raise ProxyError(f"proxy {redact(proxy)}: only http:// proxies are supported")
+        raise ProxyError(f"proxy {redact(proxy)}: only http://, https:// and socks5:// proxies are supported")
     return proxy
 
 

@@ -103,11 +103,13 @@ def test_cgi_environment_refuses_http_proxy():
     assert c.proxy_for("https://a.com") == ""  # HTTPS_PROXY is unaffected (and unset)
 
 
-def test_unsupported_schemes_fail_loudly():
-    with pytest.raises(proxy.ProxyError, match="only http://"):
-        proxy.select("https://a.com", {"HTTPS_PROXY": "socks5://p:1080"})
-    with pytest.raises(proxy.ProxyError, match="only http://"):
-        proxy.select("https://a.com", {}, override="https://p:3129")
+def test_proxy_schemes():
+    # Go's transport speaks http, https and socks5 proxies; other schemes get http:// prepended
+    assert proxy.select("https://a.com", {"HTTPS_PROXY": "socks5://p:1080"}) == "socks5://p:1080"
+    assert proxy.select("https://a.com", {}, override="https://u:pw@p:3129") == "https://u:pw@p:3129"
+    assert proxy.select("http://a.com", {"HTTP_PROXY": "socks5h://p"}) == "socks5h://p"
+    with pytest.raises(proxy.ProxyError, match="only http://, https:// and socks5://"):
+        proxy.check_supported("ftp://p:21")
     assert proxy.redact("http://u:secret@p:1") == "http://u:xxxxx@p:1"
     assert proxy.redact("http://p:1") == "http://p:1"
 
@@ -134,8 +136,10 @@ class _Proxy(socketserver.ThreadingTCPServer):
     daemon_threads = True
     allow_reuse_address = True
 
+    handler = None  # _Handler (set below)
+
     def __init__(self, reject_with=None):
-        super().__init__(("127.0.0.1", 0), _Handler)
+        super().__init__(("127.0.0.1", 0), type(self).handler)
         self.reject_with = reject_with
         self.connects, self.forwards, self.auth = [], [], []
         self.lock = threading.Lock()
@@ -208,6 +212,9 @@ class _Handler(socketserver.BaseRequestHandler):
                     (up if s is self.request else self.request).sendall(data)
         finally:
             up.close()
+
+
+_Proxy.handler = _Handler
 
 
 @pytest.fixture
@@ -310,8 +317,8 @@ def test_proxy_rejection_and_unreachable_proxy(nat):
         c.set_proxy(f"http://127.0.0.1:{port}")
         with pytest.raises(nat.NativeError, match="^proxyconnect tcp: dial tcp"):
             c.request("GET", "/version")
-        with pytest.raises(nat.NativeError, match="https:// proxies are not supported"):
-            c.set_proxy("https://127.0.0.1:1")
+        with pytest.raises(nat.NativeError, match="unknown scheme"):
+            c.set_proxy("ftp://127.0.0.1:1")
         c.set_proxy("")
         assert not c.proxied
     finally:
@@ -346,3 +353,273 @@ def test_server_accepts_absolute_form(nat):
         assert data.startswith(b"HTTP/1.1 200") and b'"replicas":2' in data.replace(b" ", b"")
     finally:
         k.stop()
+
+
+# ---------------------------------------------------------------------------------------------
+# https:// proxies (TLS to the proxy; TLS inside TLS for https origins) and socks5:// proxies
+
+
+class _TlsProxy(_Proxy):
+    """The CONNECT / absolute-form proxy above, reached over TLS."""
+
+    def __init__(self, cert_pem, key_pem, tmp_path, reject_with=None):
+        import ssl
+
+        (tmp_path / "proxy.crt").write_text(cert_pem)
+        (tmp_path / "proxy.key").write_text(key_pem)
+        self.ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        self.ctx.load_cert_chain(str(tmp_path / "proxy.crt"), str(tmp_path / "proxy.key"))
+        super().__init__(reject_with)
+
+    def get_request(self):
+        sock, addr = self.socket.accept()
+        return self.ctx.wrap_socket(sock, server_side=True, do_handshake_on_connect=False), addr
+
+    @property
+    def url(self):
+        return f"https://127.0.0.1:{self.server_address[1]}"
+
+
+class _TlsHandler(_Handler):
+    def setup(self):
+        try:
+            self.request.do_handshake()
+            self.ok = True
+        except OSError:  # the client rejected our certificate
+            self.ok = False
+
+    def handle(self):
+        if self.ok:
+            super().handle()
+
+    def _relay(self, up, first):
+        # like _Handler._relay, but decrypted bytes buffered in the TLS object are not visible
+        # to select(): drain them after every read
+        if first:
+            up.sendall(first)
+        try:
+            while True:
+                r, _, _ = select.select([self.request, up], [], [], 5)
+                if not r:
+                    return
+                for s in r:
+                    if s is self.request:
+                        data = self.request.recv(65536)
+                        while data and self.request.pending():
+                            data += self.request.recv(self.request.pending())
+                        if not data:
+                            return
+                        up.sendall(data)
+                    else:
+                        data = up.recv(65536)
+                        if not data:
+                            return
+                        self.request.sendall(data)
+        finally:
+            up.close()
+
+
+_TlsProxy.handler = _TlsHandler
+
+
+class _Socks5(socketserver.ThreadingTCPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+    def __init__(self, user=None, password=None, reply=0):
+        super().__init__(("127.0.0.1", 0), _Socks5Handler)
+        self.user, self.password, self.reply = user, password, reply
+        self.targets, self.methods, self.auth = [], [], []
+        self.thread = threading.Thread(target=self.serve_forever, daemon=True)
+        self.thread.start()
+
+    @property
+    def url(self):
+        return f"socks5://127.0.0.1:{self.server_address[1]}"
+
+    def close(self):
+        self.shutdown()
+        self.server_close()
+
+
+class _Socks5Handler(_Handler):
+    def _recv(self, n):
+        buf = b""
+        while len(buf) < n:
+            chunk = self.request.recv(n - len(buf))
+            if not chunk:
+                raise ConnectionError("eof")
+            buf += chunk
+        return buf
+
+    def handle(self):
+        srv = self.server
+        ver, n = self._recv(2)
+        methods = list(self._recv(n))
+        srv.methods.append(methods)
+        if srv.user is not None:
+            if 2 not in methods:
+                self.request.sendall(b"\x05\xff")
+                return
+            self.request.sendall(b"\x05\x02")
+            _, ulen = self._recv(2)
+            user = self._recv(ulen).decode()
+            (plen,) = self._recv(1)
+            password = self._recv(plen).decode()
+            srv.auth.append((user, password))
+            ok = (user, password) == (srv.user, srv.password)
+            self.request.sendall(b"\x01\x00" if ok else b"\x01\x01")
+            if not ok:
+                return
+        else:
+            self.request.sendall(b"\x05\x00")
+        ver, cmd, _, atyp = self._recv(4)
+        if atyp == 1:
+            host = socket.inet_ntop(socket.AF_INET, self._recv(4))
+        elif atyp == 4:
+            host = socket.inet_ntop(socket.AF_INET6, self._recv(16))
+        else:
+            (ln,) = self._recv(1)
+            host = self._recv(ln).decode()
+        port = int.from_bytes(self._recv(2), "big")
+        srv.targets.append((atyp, host, port))
+        if srv.reply:
+            self.request.sendall(bytes([5, srv.reply, 0, 1, 0, 0, 0, 0, 0, 0]))
+            return
+        up = socket.create_connection(("127.0.0.1" if host == "localhost" else host, port))
+        self.request.sendall(b"\x05\x00\x00\x01\x7f\x00\x00\x01\x00\x00")
+        self._relay(up, b"")
+
+
+def test_https_proxy_tls_inside_tls(nat, tmp_path):
+    """An https origin behind an https proxy: TLS to the proxy (verified with the client's trust
+    settings against the proxy's name, as Go's transport does), CONNECT, then the origin's TLS
+    inside it -- verified end to end, keep-alive across requests."""
+    cert, key = nat.generate_self_signed("127.0.0.1")
+    p = _TlsProxy(cert, key, tmp_path)
+    k = nat.FakeKubeServer()
+    k.require_token(TOKEN)
+    k.start("127.0.0.1", 0, True)
+    try:
+        k.add_deployment("ml", "worker", 1)
+        user_proxy = p.url.replace("https://", "https://ops:pw@")
+        rc = RestConfig(host=k.url, bearer_token=TOKEN, ca_pem=k.cert_pem + cert, proxy_url=user_proxy)
+        api = new_deployment_api(rc, "ml", "scale")
+        pa = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+        for _ in range(3):
+            pa.scale_up()
+        assert k.replicas("ml", "worker") == 4
+        assert p.connects == [f"127.0.0.1:{k.url.rsplit(':', 1)[1]}"]
+        assert p.auth == ["Basic " + base64.b64encode(b"ops:pw").decode()]
+        assert api.stats()["http"]["connects"] == 1
+    finally:
+        k.stop()
+        p.close()
+
+
+def test_https_proxy_certificate_is_verified(nat, tmp_path):
+    cert, key = nat.generate_self_signed("127.0.0.1")
+    p = _TlsProxy(cert, key, tmp_path)
+    k = nat.FakeKubeServer()
+    k.start("127.0.0.1", 0, True)
+    try:
+        k.add_deployment("ml", "worker", 1)
+        rc = RestConfig(host=k.url, ca_pem=k.cert_pem, proxy_url=p.url)  # the proxy's cert is not trusted
+        api = new_deployment_api(rc, "ml", "scale")
+        pa = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+        with pytest.raises(nat.NativeError, match="proxyconnect tcp: x509"):
+            pa.scale_up()
+        assert p.connects == []
+    finally:
+        k.stop()
+        p.close()
+
+
+def test_https_proxy_plain_http_origin(nat, tmp_path):
+    """An http origin (a local SQS endpoint) behind an https proxy: absolute-form requests over
+    the TLS connection to the proxy; SigV4 still verifies."""
+    cert, key = nat.generate_self_signed("127.0.0.1")
+    p = _TlsProxy(cert, key, tmp_path)
+    s = nat.FakeSqsServer()
+    s.require_signature(AKID, SECRET, REGION)
+    s.start()
+    try:
+        url = s.url + "/1/q"
+        s.set_attributes(url, {"ApproximateNumberOfMessages": "7"})
+        o = nat.SqsHttpOptions()
+        o.region, o.endpoint, o.proxy = REGION, s.url, p.url
+        tls = nat.TlsOptions()
+        tls.ca_pem = cert  # trust for the proxy's certificate
+        o.tls = tls
+        api = nat.HttpSqsApi(o, static_provider(AKID, SECRET), nat.RealClock())
+        client = nat.SqsClient(api, url, NAMES)
+        assert [client.num_messages() for _ in range(3)] == [7, 7, 7]
+        assert p.forwards[0].startswith("POST http://127.0.0.1:") and p.connects == []
+        assert s.signature_failures() == 0
+    finally:
+        s.stop()
+        p.close()
+
+
+def test_socks5_proxy_with_auth_to_tls_origin(nat):
+    sp = _Socks5(user="ops", password="p@ss")
+    k = nat.FakeKubeServer()
+    k.require_token(TOKEN)
+    k.start("127.0.0.1", 0, True)
+    try:
+        k.add_deployment("ml", "worker", 1)
+        rc = RestConfig(host=k.url, bearer_token=TOKEN, ca_pem=k.cert_pem,
+                        proxy_url=sp.url.replace("socks5://", "socks5://ops:p%40ss@"))
+        api = new_deployment_api(rc, "ml", "scale")
+        pa = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+        pa.scale_up()
+        pa.scale_up()
+        assert k.replicas("ml", "worker") == 3
+        port = int(k.url.rsplit(":", 1)[1])
+        assert sp.targets == [(1, "127.0.0.1", port)]  # one tunnel; an IP literal goes as IPv4
+        assert sp.methods == [[0, 2]] and sp.auth == [("ops", "p@ss")]
+    finally:
+        k.stop()
+        sp.close()
+
+
+def test_socks5_proxy_sends_host_names_unresolved(nat):
+    """A host name goes to the proxy as a domain (ATYP 3), and an http origin gets origin-form
+    requests (a SOCKS tunnel is not an HTTP proxy)."""
+    sp = _Socks5()
+    s = nat.FakeSqsServer()
+    s.start()
+    try:
+        port = int(s.url.rsplit(":", 1)[1])
+        c = nat.HttpClient(f"http://localhost:{port}", nat.TlsOptions(), 2_000_000_000)
+        c.set_proxy(sp.url)
+        status, _, _ = c.request("GET", "/")
+        assert status in (400, 404, 405)  # the fake answered over the tunnel
+        assert sp.targets == [(3, "localhost", port)] and sp.methods == [[0]]
+    finally:
+        s.stop()
+        sp.close()
+
+
+def test_socks5_errors(nat):
+    k = nat.FakeKubeServer()
+    k.start("127.0.0.1", 0, True)
+    refused, needs_auth = _Socks5(reply=5), _Socks5(user="u", password="p")
+    try:
+        c = nat.HttpClient(k.url, nat.TlsOptions(), 2_000_000_000)
+        c.set_proxy(refused.url)
+        with pytest.raises(nat.NativeError, match=r"^socks connect tcp 127\.0\.0\.1:[0-9]+->127\.0\.0\.1:[0-9]+: connection refused"):
+            c.request("GET", "/version")
+        c.set_proxy(needs_auth.url)  # no credentials in the URL
+        with pytest.raises(nat.NativeError, match="no acceptable authentication methods"):
+            c.request("GET", "/version")
+        c.set_proxy(needs_auth.url.replace("socks5://", "socks5://u:wrong@"))
+        with pytest.raises(nat.NativeError, match="authentication failed"):
+            c.request("GET", "/version")
+        c.set_proxy("socks5://127.0.0.1")  # default port 1080
+        with pytest.raises(nat.NativeError, match="proxyconnect tcp: dial tcp 127.0.0.1:1080"):
+            c.request("GET", "/version")
+    finally:
+        k.stop()
+        refused.close()
+        needs_auth.close()
