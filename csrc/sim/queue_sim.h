@@ -12,7 +12,8 @@
 // 12 uniform 16-bit draws, integer-only, so the gfx950 kernel and the CPU path agree bit for bit.
 // The stream is counter-based on (seed, interval index) and the same seeds are used for every
 // configuration (common random numbers), so configurations are compared on the same arrival
-// sequences. Quantities are kept in milli-messages so fractional arrivals are not lost.
+// sequences. The backlog is kept in micro-messages: a rate in milli-msgs/s times an interval in ms
+// is exactly that unit, so integrating rates needs no division.
 //
 // One call simulates one (configuration, seed); the host reduces over seeds.
 #pragma once
@@ -72,32 +73,24 @@ KSA_HD int64_t sat_mul(int64_t a, int64_t b) {
   return __builtin_mul_overflow(a, b, &r) || r > kSat ? kSat : r;
 }
 KSA_HD int64_t sat_add(int64_t a, int64_t b) { return a > kSat - b ? kSat : a + b; }
-// floor(x_milli * dt_ms / 1000) (saturating), without forming a product that could overflow.
-// Operands below 2^31 (rates <= 1e6 msgs/s, intervals < 24 days) take the one-multiply form;
-// x = 1000a + b gives floor(x dt / 1000) = a dt + floor(b dt / 1000), so both forms agree.
-KSA_HD int64_t per_ms(int64_t x_milli, int64_t dt_ms) {
-  if (x_milli <= 0 || dt_ms <= 0) return 0;
-  if (((x_milli | dt_ms) >> 31) == 0) return x_milli * dt_ms / 1000;
-  return sat_add(sat_mul(x_milli / 1000, dt_ms), sat_mul(x_milli % 1000, dt_ms) / 1000);
-}
+// Messages (micro-messages) a rate of x_milli milli-msgs/s delivers in dt_ms: the product,
+// saturating.
+KSA_HD int64_t per_ms(int64_t x_milli, int64_t dt_ms) { return sat_mul(x_milli, dt_ms); }
 
-// Random arrivals (milli-messages) with mean `mean_milli`: mean + sqrt(mean) * Z, where Z is the
-// CLT of 12 uniform 16-bit integers (standard deviation 2^16 in fixed point).
-KSA_HD int64_t sample_arrivals_milli(int64_t mean_milli, uint64_t seed, uint64_t k) {
-  if (mean_milli <= 0) return 0;
+// Random arrivals (micro-messages) with mean `mean`: mean + sqrt(mean) * Z, where Z is the CLT
+// of 12 uniform 16-bit integers (standard deviation 2^16 in fixed point).
+KSA_HD int64_t sample_arrivals(int64_t mean, uint64_t seed, uint64_t k) {
+  if (mean <= 0) return 0;
   const uint64_t base = seed * 0xD1B54A32D192ED03ULL + k * 3;
   const uint64_t w0 = mix64(base), w1 = mix64(base + 1), w2 = mix64(base + 2);
-  int64_t z = -6 * 65536;
-  for (int i = 0; i < 4; ++i) {
-    z += static_cast<int64_t>((w0 >> (16 * i)) & 0xFFFF);
-    z += static_cast<int64_t>((w1 >> (16 * i)) & 0xFFFF);
-    z += static_cast<int64_t>((w2 >> (16 * i)) & 0xFFFF);
-  }
-  // sd in milli-messages = sqrt(mean_milli / 1000) * 1000 = sqrt(mean_milli * 1000)
-  const int64_t sd_milli = mean_milli < (int64_t(1) << 52)
-                               ? static_cast<int64_t>(isqrt64(static_cast<uint64_t>(mean_milli) * 1000))
-                               : static_cast<int64_t>(isqrt64(static_cast<uint64_t>(mean_milli))) * 31623 / 1000;
-  const int64_t a = mean_milli + sd_milli * z / 65536;
+  // Sum of the twelve 16-bit fields, SWAR: the even and odd fields of each word are added in
+  // 32-bit lanes (6 x 65535 fits), then the two lanes are folded.
+  constexpr uint64_t kM = 0x0000FFFF0000FFFFULL;
+  const uint64_t lanes = (w0 & kM) + ((w0 >> 16) & kM) + (w1 & kM) + ((w1 >> 16) & kM) + (w2 & kM) + ((w2 >> 16) & kM);
+  const int64_t z = static_cast<int64_t>((lanes & 0xFFFFFFFFULL) + (lanes >> 32)) - 6 * 65536;
+  // sd in micro-messages = sqrt(mean / 1e6) * 1e6 = 1000 sqrt(mean), to a milli-message
+  const int64_t sd = static_cast<int64_t>(isqrt64(static_cast<uint64_t>(mean))) * 1000;
+  const int64_t a = mean + sd * z / 65536;
   return a > 0 ? a : 0;
 }
 
@@ -106,10 +99,10 @@ struct RateCursor {
   int32_t c;
 };
 
-// Expected arrivals (milli-messages) over [t0_ms, t1_ms): the rate integrated segment by
+// Expected arrivals (micro-messages) over [t0_ms, t1_ms): the rate integrated segment by
 // segment. Segment i covers [t_ms[i], t_ms[i+1]); the last one extends to infinity. Times only
 // grow, so the cursor never moves back.
-KSA_HD int64_t expected_arrivals_milli(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, RateCursor* k,
+KSA_HD int64_t expected_arrivals(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, RateCursor* k,
                                        int64_t t0_ms, int64_t t1_ms) {
   while (k->c + 1 < n && t_ms[k->c + 1] <= t0_ms) k->c++;
   int32_t i = k->c;
@@ -125,7 +118,8 @@ KSA_HD int64_t expected_arrivals_milli(const int64_t* t_ms, const int64_t* rate_
 }
 
 struct QueueState {
-  int64_t q_milli;       // backlog
+  int64_t q_micro;       // backlog
+  int64_t q_msgs;        // q_micro / 1e6, kept current (the depth SQS reports)
   int32_t ready, pending;
   int64_t pending_at_ms;  // when the pending pods start draining
   uint64_t draws;
@@ -139,13 +133,13 @@ KSA_HD void advance(QueueState* s, QueueResult* r, const QueueModel& m, const in
                     int32_t replicas) {
   if (t1_ms <= t0_ms) return;
   const int64_t dt = t1_ms - t0_ms;
-  const int64_t q0 = s->q_milli / 1000;
+  const int64_t q0 = s->q_msgs;
   r->pod_ms = sat_add(r->pod_ms, sat_mul(replicas, dt));
   r->backlog_msg_ms = sat_add(r->backlog_msg_ms, sat_mul(q0, dt));
   if (q0 > m.slo_backlog) r->violation_ms += dt;
-  const int64_t mean = expected_arrivals_milli(t_ms, rate_milli, n, cur, t0_ms, t1_ms);
-  const int64_t a = sample_arrivals_milli(mean, seed, s->draws++);
-  s->q_milli = sat_add(s->q_milli, a);
+  const int64_t mean = expected_arrivals(t_ms, rate_milli, n, cur, t0_ms, t1_ms);
+  const int64_t a = sample_arrivals(mean, seed, s->draws++);
+  s->q_micro = sat_add(s->q_micro, a);
   r->arrived = sat_add(r->arrived, a);
   // capacity: ready pods for the whole interval, pending ones from their ready time
   int64_t cap = sat_mul(s->ready, per_ms(m.service_milli, dt));
@@ -153,8 +147,9 @@ KSA_HD void advance(QueueState* s, QueueResult* r, const QueueModel& m, const in
     const int64_t from = s->pending_at_ms > t0_ms ? s->pending_at_ms : t0_ms;
     cap = sat_add(cap, sat_mul(s->pending, per_ms(m.service_milli, t1_ms - from)));
   }
-  const int64_t served = s->q_milli < cap ? s->q_milli : cap;
-  s->q_milli -= served;
+  const int64_t served = s->q_micro < cap ? s->q_micro : cap;
+  s->q_micro -= served;
+  s->q_msgs = s->q_micro / 1000000;
   r->served = sat_add(r->served, served);
   if (s->pending > 0 && s->pending_at_ms <= t1_ms) {
     s->ready += s->pending;
@@ -168,7 +163,8 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
   QueueResult res;
   const Rules k = make_rules(p);
   QueueState s;
-  s.q_milli = m.init_backlog * 1000;
+  s.q_micro = m.init_backlog * 1000000;
+  s.q_msgs = m.init_backlog;
   s.ready = init_replicas;
   s.pending = 0;
   s.pending_at_ms = 0;
@@ -189,7 +185,7 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
     now = t_poll;
     res.polls++;
     // depth the SQS call reports: every message not yet deleted (queued + in flight)
-    const int64_t d = s.q_milli / 1000;
+    const int64_t d = s.q_msgs;
     now += lat.sqs_ns;
     const int32_t before = replicas;
     int32_t gets = 0, writes = 0;
@@ -206,13 +202,13 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
       s.ready = s.ready > drop ? s.ready - drop : 0;
     }
     if (replicas > res.max_replicas) res.max_replicas = replicas;
-    if (s.q_milli / 1000 > res.peak_backlog) res.peak_backlog = s.q_milli / 1000;
+    if (s.q_msgs > res.peak_backlog) res.peak_backlog = s.q_msgs;
   }
   if (horizon_ms > prev_ms) advance(&s, &res, m, t_ms, rate_milli, n, &cur, seed, prev_ms, horizon_ms, replicas);
   res.final_replicas = replicas;
-  res.final_backlog = s.q_milli / 1000;
-  res.arrived /= 1000;
-  res.served /= 1000;
+  res.final_backlog = s.q_msgs;
+  res.arrived /= 1000000;
+  res.served /= 1000000;
   return res;
 }
 

@@ -212,13 +212,13 @@ def _mix64(z: int) -> int:
     return z ^ (z >> 31)
 
 
-def _sample_milli(mean: int, seed: int, k: int) -> int:
+def _sample(mean: int, seed: int, k: int) -> int:
     if mean <= 0:
         return 0
     base = (seed * 0xD1B54A32D192ED03 + k * 3) & _MASK64
     words = [_mix64((base + j) & _MASK64) for j in range(3)]
     z = sum((w >> (16 * i)) & 0xFFFF for w in words for i in range(4)) - 6 * 65536
-    sd = math.isqrt(mean * 1000) if mean < (1 << 52) else math.isqrt(mean) * 31623 // 1000
+    sd = math.isqrt(mean) * 1000  # micro-messages: 1000 sqrt(mean)
     prod = sd * z
     a = mean + (abs(prod) // 65536) * (1 if prod >= 0 else -1)  # C++ division truncates toward zero
     return max(a, 0)
@@ -249,7 +249,7 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
     up32, down32 = _i32(cfg["up_pods"]), _i32(cfg["down_pods"])
     r = dict(pod_ms=0, backlog_msg_ms=0, violation_ms=0, peak_backlog=0, arrived=0, served=0, final_backlog=0, ups=0,
              downs=0, final_replicas=0, max_replicas=init_replicas, polls=0)
-    st = {"q": model.init_backlog * 1000, "ready": init_replicas, "pending": 0, "pending_at": 0, "draws": 0}
+    st = {"q": model.init_backlog * 10**6, "ready": init_replicas, "pending": 0, "pending_at": 0, "draws": 0}
 
     def sat_add(a: int, b: int) -> int:  # the C++ accumulators saturate at 2^62
         return min(a + b, _SAT)
@@ -257,8 +257,8 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
     def sat_mul(a: int, b: int) -> int:
         return 0 if a <= 0 or b <= 0 else min(a * b, _SAT)
 
-    def per_ms(x_milli: int, dt: int) -> int:
-        return sat_add(sat_mul(x_milli // 1000, dt), sat_mul(x_milli % 1000, dt) // 1000)
+    def per_ms(x_milli: int, dt: int) -> int:  # milli-msgs/s x ms = micro-messages
+        return sat_mul(x_milli, dt)
 
     def expected(t0: int, t1: int) -> int:
         total = 0
@@ -273,12 +273,12 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
         if t1 <= t0:
             return
         dt = t1 - t0
-        q0 = st["q"] // 1000
+        q0 = st["q"] // 10**6
         r["pod_ms"] = sat_add(r["pod_ms"], sat_mul(replicas, dt))
         r["backlog_msg_ms"] = sat_add(r["backlog_msg_ms"], sat_mul(q0, dt))
         if q0 > model.slo_backlog:
             r["violation_ms"] += dt
-        a = _sample_milli(expected(t0, t1), seed, st["draws"])
+        a = _sample(expected(t0, t1), seed, st["draws"])
         st["draws"] += 1
         st["q"] = sat_add(st["q"], a)
         r["arrived"] = sat_add(r["arrived"], a)
@@ -303,7 +303,7 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
         prev_ms = t_poll // 1_000_000
         now = t_poll
         r["polls"] += 1
-        d = st["q"] // 1000
+        d = st["q"] // 10**6
         now += sqs
         before = replicas
         cont = False
@@ -335,10 +335,10 @@ def reference_lane(trace: ArrivalTrace, cfg: Dict[str, int], model: QueueModel, 
             st["pending"] -= take
             st["ready"] = max(st["ready"] - (drop - take), 0)
         r["max_replicas"] = max(r["max_replicas"], replicas)
-        r["peak_backlog"] = max(r["peak_backlog"], st["q"] // 1000)
+        r["peak_backlog"] = max(r["peak_backlog"], st["q"] // 10**6)
     horizon_ms = horizon_ns // 1_000_000
     if horizon_ms > prev_ms:
         advance(prev_ms, horizon_ms, replicas)
-    r.update(final_replicas=replicas, final_backlog=st["q"] // 1000, arrived=r["arrived"] // 1000,
-             served=r["served"] // 1000)
+    r.update(final_replicas=replicas, final_backlog=st["q"] // 10**6, arrived=r["arrived"] // 10**6,
+             served=r["served"] // 10**6)
     return r
