@@ -33,7 +33,7 @@ from typing import Dict, List
 import numpy as np
 
 from ..utils.goflag import parse_duration, parse_int
-from . import closedloop, sweep
+from . import closedloop, distributed, sweep
 
 FLAG_TO_FIELD = {
     "poll-period": ("poll_ns", parse_duration),
@@ -91,10 +91,12 @@ def main(argv=None) -> int:
                     help="open loop: pod_ms|backlog|ups|downs (default pod_ms); closed loop: a summary column "
                          "(default pod_hours_mean)")
     ap.add_argument("--max-backlog", type=float, default=None, help="keep configs with backlog <= this")
-    ap.add_argument("--top", type=int, default=10)
+    ap.add_argument("--top", type=int, default=10, help="rows to print (0: all)")
     ap.add_argument("--pareto", action="store_true", help="list the cost/pressure Pareto front instead of a ranking")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--json", action="store_true", help="print JSON lines instead of a table")
+    ap.add_argument("--distributed", action="store_true",
+                    help="shard the grid over the ranks of a torchrun launch (one GPU each); rank 0 prints")
     cl = ap.add_argument_group("closed loop (--arrivals)")
     cl.add_argument("--service-rate", type=float, default=None, help="msgs/s one ready pod drains (required)")
     cl.add_argument("--startup-delay", default="60s", help="scale-up write -> new pods taking work (Go duration)")
@@ -104,8 +106,19 @@ def main(argv=None) -> int:
     cl.add_argument("--seeds", type=int, default=32, help="random arrival sequences per configuration")
     cl.add_argument("--seed", type=int, default=1, help="first seed (the same seeds are used for every config)")
     a = ap.parse_args(argv)
-    if a.arrivals is not None:
-        return _closed_loop(ap, a)
+    group = distributed.Group(a.device) if a.distributed else None
+    try:
+        if a.arrivals is not None:
+            return _closed_loop(ap, a, group)
+        return _open_loop(ap, a, group)
+    finally:
+        if group is not None:
+            group.close()
+
+
+def _open_loop(ap: argparse.ArgumentParser, a, group) -> int:
+    if a.trace is None:
+        ap.error("one of --trace or --arrivals is required")
     if a.objective is None:
         a.objective = "pod_ms"
     if a.objective not in ("pod_ms", "backlog", "ups", "downs"):
@@ -119,8 +132,13 @@ def main(argv=None) -> int:
     params = sweep.grid(**values)
     horizon = parse_duration(a.horizon) if a.horizon else int(tr.t_ns[-1]) + int(params[0].max())
     t0 = time.perf_counter()
-    res = sweep.run(tr, params, a.init_replicas, horizon, lat, a.device)
+    if group is not None:
+        res = distributed.run_open_loop(group, tr, params, a.init_replicas, horizon, lat)
+    else:
+        res = sweep.run(tr, params, a.init_replicas, horizon, lat, a.device)
     wall = time.perf_counter() - t0
+    if group is not None and group.rank != 0:
+        return 0
     ok = np.ones(len(res), dtype=bool)
     if a.max_backlog is not None:
         ok &= res.out["backlog"] <= a.max_backlog
@@ -129,9 +147,11 @@ def main(argv=None) -> int:
         front = sweep.pareto_front(res.out["pod_ms"][idx], res.out["backlog"][idx])
         order = idx[front][: a.top] if a.top > 0 else idx[front]
     else:
-        order = idx[np.argsort(res.out[a.objective][idx], kind="stable")][: a.top]
+        order = idx[np.argsort(res.out[a.objective][idx], kind="stable")]
+        order = order[: a.top] if a.top > 0 else order
     baseline = sweep.run(tr, sweep.grid(), a.init_replicas, horizon, lat, "cpu").row(0)
     summary = {"configs": len(res), "feasible": int(ok.sum()), "device": res.device, "wall_s": round(wall, 4),
+               "ranks": group.world if group is not None else 1,
                "kernel_ms": round(res.kernel_ms, 3), "simulated_polls": int(res.out["polls"].sum()),
                "horizon_ns": horizon, "reference_defaults": baseline}
     if a.json:
@@ -157,7 +177,7 @@ CLOSED_COLS = ["poll_ns", "up_cool_ns", "down_cool_ns", "up_msgs", "down_msgs", 
                "downs_mean", "max_replicas_max"]
 
 
-def _closed_loop(ap: argparse.ArgumentParser, a) -> int:
+def _closed_loop(ap: argparse.ArgumentParser, a, group) -> int:
     if a.service_rate is None:
         ap.error("--arrivals needs --service-rate")
     objective = a.objective or "pod_hours_mean"
@@ -169,8 +189,13 @@ def _closed_loop(ap: argparse.ArgumentParser, a) -> int:
     params = sweep.grid(**parse_grid(a.grid))
     horizon = parse_duration(a.horizon) if a.horizon else int(tr.t_ms[-1]) * 1_000_000 + 3600 * closedloop.S
     t0 = time.perf_counter()
-    res = closedloop.run(tr, params, model, a.init_replicas, horizon, lat, a.seeds, a.seed, a.device)
+    if group is not None:
+        res = distributed.run_closed_loop(group, tr, params, model, a.init_replicas, horizon, lat, a.seeds, a.seed)
+    else:
+        res = closedloop.run(tr, params, model, a.init_replicas, horizon, lat, a.seeds, a.seed, a.device)
     wall = time.perf_counter() - t0
+    if group is not None and group.rank != 0:
+        return 0
     summ = res.summary()
     if objective not in summ:
         ap.error(f"closed-loop objective must be one of {sorted(summ)}, not {objective!r}")
@@ -184,9 +209,11 @@ def _closed_loop(ap: argparse.ArgumentParser, a) -> int:
         front = sweep.pareto_front(summ["pod_hours_mean"][idx], summ["violation_s_p95"][idx])
         order = idx[front][: a.top] if a.top > 0 else idx[front]
     else:
-        order = idx[np.argsort(summ[objective][idx], kind="stable")][: a.top]
+        order = idx[np.argsort(summ[objective][idx], kind="stable")]
+        order = order[: a.top] if a.top > 0 else order
     base = closedloop.run(tr, sweep.grid(), model, a.init_replicas, horizon, lat, a.seeds, a.seed, "cpu").row(0)
     info = {"configs": len(res), "feasible": int(ok.sum()), "seeds": a.seeds, "device": res.device,
+            "ranks": group.world if group is not None else 1,
             "wall_s": round(wall, 4), "kernel_ms": round(res.kernel_ms, 3),
             "simulated_polls": int(res.out["polls"].sum()), "horizon_ns": horizon, "reference_defaults": base}
     if a.json:

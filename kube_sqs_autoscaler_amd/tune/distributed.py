@@ -1,0 +1,126 @@
+"""Multi-GPU what-if sweeps: one process per GPU, configurations sharded by rank.
+
+Extension (an operator tool, like the rest of :mod:`kube_sqs_autoscaler_amd.tune`). Launch with
+``torchrun`` (``python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m
+kube_sqs_autoscaler_amd.tune --distributed ...``). Every rank:
+
+1. takes a contiguous slice of the configuration grid (near-equal sizes, so the ranks finish
+   together: every configuration of a grid simulates the same horizon);
+2. runs it on its own GPU (``LOCAL_RANK``) with the same kernel a single-GPU sweep uses, or on
+   CPU threads;
+3. all-gathers the per-configuration outputs over ``torch.distributed``. The backend is
+   ``nccl`` (RCCL over xGMI on an MI355X node) when the GPUs run the sweep, ``gloo`` on CPU.
+
+The outputs are a few dozen bytes per configuration, so the collective is one small
+all-gather per output field; the simulation dominates. Every rank ends with the full result,
+bit-identical to a single-process sweep of the whole grid (``tests/test_tune_distributed.py``).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Tuple
+
+import numpy as np
+
+from . import closedloop, sweep
+
+
+def shard_bounds(m: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous slice [lo, hi) of m configurations for `rank`; sizes differ by at most one."""
+    base, extra = divmod(m, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+class Group:
+    """The process group a sharded sweep runs in (initialised from the torchrun environment)."""
+
+    def __init__(self, device: str = "auto"):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if device == "auto":
+            device = "gpu" if sweep.gpu_available() else "cpu"
+        self.device = device
+        self.owned = False
+        use_gpu = device == "gpu"
+        if use_gpu:
+            torch.cuda.set_device(self.local_rank)
+            self.tensor_device = torch.device("cuda", self.local_rank)
+        else:
+            self.tensor_device = torch.device("cpu")
+        if self.world > 1 and not dist.is_initialized():
+            if use_gpu:
+                dist.init_process_group("nccl", device_id=self.tensor_device)
+            else:
+                dist.init_process_group("gloo")
+            self.owned = True
+
+    def close(self) -> None:
+        if self.owned:
+            self.dist.destroy_process_group()
+            self.owned = False
+
+    def all_gather_rows(self, shard: np.ndarray, counts: List[int]) -> np.ndarray:
+        """Concatenation over ranks of each rank's rows (axis 0), `counts[r]` rows from rank r."""
+        if self.world == 1:
+            return shard
+        torch = self.torch
+        longest = max(counts)
+        pad = np.zeros((longest,) + shard.shape[1:], dtype=shard.dtype)
+        pad[: shard.shape[0]] = shard
+        t = torch.from_numpy(pad).to(self.tensor_device)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return np.concatenate([p.cpu().numpy()[:n] for p, n in zip(parts, counts)], axis=0)
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.tensor_device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def _shards(g: Group, m: int) -> Tuple[Tuple[int, int], List[int]]:
+    bounds = [shard_bounds(m, r, g.world) for r in range(g.world)]
+    return bounds[g.rank], [hi - lo for lo, hi in bounds]
+
+
+def run_open_loop(g: Group, trace: sweep.Trace, params: np.ndarray, init_replicas: int, horizon_ns: int,
+                  latency_ns: Tuple[int, int, int]) -> sweep.SweepResult:
+    """:func:`sweep.run` over the whole grid, sharded over the group's ranks."""
+    params = np.ascontiguousarray(params, dtype=np.int64)
+    (lo, hi), counts = _shards(g, params.shape[1])
+    part = params[:, lo:hi]
+    if hi > lo:
+        res = sweep.run(trace, part, init_replicas, horizon_ns, latency_ns, g.device, gpu_index=g.local_rank)
+        out, kernel_ms = res.out, res.kernel_ms
+    else:  # more ranks than configurations
+        out = {k: np.zeros(0, dtype=np.int64 if k in sweep.OUT64 else np.int32) for k in sweep.OUT64 + sweep.OUT32}
+        kernel_ms = 0.0
+    full = {k: g.all_gather_rows(np.ascontiguousarray(v), counts) for k, v in out.items()}
+    return sweep.SweepResult(params, full, g.device, g.max(kernel_ms))
+
+
+def run_closed_loop(g: Group, trace: closedloop.ArrivalTrace, params: np.ndarray, model: closedloop.QueueModel,
+                    init_replicas: int, horizon_ns: int, latency_ns: Tuple[int, int, int], seeds: int,
+                    seed0: int) -> closedloop.ClosedLoopResult:
+    """:func:`closedloop.run` over the whole grid, sharded over the group's ranks. Seeds are
+    common to all configurations, so every shard draws the same arrival sequences."""
+    params = np.ascontiguousarray(params, dtype=np.int64)
+    (lo, hi), counts = _shards(g, params.shape[1])
+    if hi > lo:
+        res = closedloop.run(trace, params[:, lo:hi], model, init_replicas, horizon_ns, latency_ns, seeds, seed0,
+                             g.device, gpu_index=g.local_rank)
+        out, kernel_ms = res.out, res.kernel_ms
+    else:
+        out = {k: np.zeros((0, seeds), dtype=np.int64 if k in closedloop.OUT64 else np.int32)
+               for k in closedloop.OUT64 + closedloop.OUT32}
+        kernel_ms = 0.0
+    full = {k: g.all_gather_rows(np.ascontiguousarray(v), counts) for k, v in out.items()}
+    return closedloop.ClosedLoopResult(params, seeds, full, g.device, horizon_ns, g.max(kernel_ms))

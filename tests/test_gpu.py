@@ -151,3 +151,22 @@ def test_closed_loop_kernel_equals_cpu_at_extremes():
         c = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=4, device="cpu")
         for k in g.out:
             assert np.array_equal(g.out[k], c.out[k]), (rate, k)
+
+
+def test_sharded_sweep_single_rank_on_gpu():
+    """tune/distributed.py on the GPU (one rank: the device and gpu_index plumbing)."""
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import closedloop as cl
+    from kube_sqs_autoscaler_amd.tune import distributed, sweep
+
+    S = 1_000_000_000
+    g = distributed.Group("gpu")
+    assert g.world == 1 and g.device == "gpu"
+    tr = cl.ArrivalTrace.from_segments([(0, 1.0), (300, 25.0), (900, 1.0)])
+    grid = sweep.grid(up_cool_ns=[0, 60 * S], max_pods=[4, 8, 16])
+    model = cl.QueueModel(5.0, 60 * S, 100)
+    a = distributed.run_closed_loop(g, tr, grid, model, 1, 1800 * S, (1_000_000,) * 3, 8, 1)
+    b = cl.run(tr, grid, model, 1, 1800 * S, (1_000_000,) * 3, seeds=8, device="cpu")
+    assert a.device == "gpu" and all(np.array_equal(a.out[k], b.out[k]) for k in a.out)
+    g.close()
