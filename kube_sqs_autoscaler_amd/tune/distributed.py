@@ -36,6 +36,15 @@ class Group:
     """The process group a sharded sweep runs in (initialised from the torchrun environment)."""
 
     def __init__(self, device: str = "auto"):
+        import sys
+
+        from ..ops import gpu as _gpu
+
+        if "torch" not in sys.modules and _gpu._LIB is not None:
+            # Measured on the MI355X image: once libksa_gpu.so has initialised the ROCm runtime,
+            # a later `import torch` binds torch to that already-loaded runtime and
+            # torch.cuda.is_available() turns False. Import order is the only fix.
+            raise RuntimeError("create the sweep Group (it imports torch) before the first GPU sweep of the process")
         import torch
         import torch.distributed as dist
 

@@ -153,20 +153,34 @@ def test_closed_loop_kernel_equals_cpu_at_extremes():
             assert np.array_equal(g.out[k], c.out[k]), (rate, k)
 
 
-def test_sharded_sweep_single_rank_on_gpu():
-    """tune/distributed.py on the GPU (one rank: the device and gpu_index plumbing)."""
-    import numpy as np
+def test_sharded_sweep_cli_on_gpu(tmp_path):
+    """tune --distributed on the GPU under torchrun (one rank: the torch device / gpu_index
+    plumbing), in a fresh process -- torch must initialise its HIP runtime before this test
+    process's already-loaded kernels library could shadow it -- against the in-process CPU sweep."""
+    import json
+    import os
+    import subprocess
+    import sys
 
     from kube_sqs_autoscaler_amd.tune import closedloop as cl
-    from kube_sqs_autoscaler_amd.tune import distributed, sweep
+    from kube_sqs_autoscaler_amd.tune import sweep
 
     S = 1_000_000_000
-    g = distributed.Group("gpu")
-    assert g.world == 1 and g.device == "gpu"
-    tr = cl.ArrivalTrace.from_segments([(0, 1.0), (300, 25.0), (900, 1.0)])
+    csv = tmp_path / "rate.csv"
+    csv.write_text("0,1\n300,25\n900,1\n")
+    args = ["--arrivals", str(csv), "--horizon", "30m", "--service-rate", "5", "--seeds", "8", "--json", "--top", "0",
+            "--slo-backlog", "100", "--grid", "scale-up-cool-down=0s,1m", "--grid", "max-pods=4,8,16", "--latency",
+            "1ms,1ms,1ms"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", "--master-port=29517", "-m", "kube_sqs_autoscaler_amd.tune",
+                        "--distributed", "--device", "gpu", *args], cwd=root, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    info, rows = lines[0], lines[1:]
+    assert info["device"] == "gpu" and info["ranks"] == 1 and len(rows) == 6
+    tr = cl.ArrivalTrace.from_csv(str(csv))
     grid = sweep.grid(up_cool_ns=[0, 60 * S], max_pods=[4, 8, 16])
-    model = cl.QueueModel(5.0, 60 * S, 100)
-    a = distributed.run_closed_loop(g, tr, grid, model, 1, 1800 * S, (1_000_000,) * 3, 8, 1)
-    b = cl.run(tr, grid, model, 1, 1800 * S, (1_000_000,) * 3, seeds=8, device="cpu")
-    assert a.device == "gpu" and all(np.array_equal(a.out[k], b.out[k]) for k in a.out)
-    g.close()
+    c = cl.run(tr, grid, cl.QueueModel(5.0, 60 * S, 100), 1, 1800 * S, (1_000_000,) * 3, seeds=8, device="cpu")
+    want = sorted((c.row(i) for i in range(len(c))), key=lambda x: x["pod_hours_mean"])
+    assert sorted(rows, key=lambda x: x["pod_hours_mean"]) == want

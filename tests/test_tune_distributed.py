@@ -64,3 +64,15 @@ def test_closed_loop_two_ranks_equal_single_process(tmp_path):
     info2, rows2 = _run(args, world=2)
     assert info2["ranks"] == 2 and info1["configs"] == info2["configs"] == 15
     assert rows1 == rows2 and len(rows1) == 15
+
+
+def test_group_refuses_to_start_after_the_kernels_library(monkeypatch):
+    import sys
+
+    from kube_sqs_autoscaler_amd.ops import gpu
+    from kube_sqs_autoscaler_amd.tune import distributed
+
+    monkeypatch.setattr(gpu, "_LIB", object())
+    monkeypatch.delitem(sys.modules, "torch", raising=False)
+    with pytest.raises(RuntimeError, match="before the first GPU sweep"):
+        distributed.Group("cpu")
