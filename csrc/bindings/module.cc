@@ -607,6 +607,16 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<KubeRestDeployments, DeploymentApi, py::smart_holder>(m, "KubeRestDeployments")
       .def(py::init<KubeOptions>())
       .def("path_for", &KubeRestDeployments::path_for)
+      // the control loop's pipelined read (begin before the SQS call, finish after it)
+      .def("begin_get", &KubeRestDeployments::begin_get, py::call_guard<py::gil_scoped_release>())
+      .def("finish_get", [](KubeRestDeployments& k) {
+        Result<ScaleObject> r;
+        {
+          py::gil_scoped_release rel;
+          r = k.finish_get();
+        }
+        return unwrap(r);
+      })
       .def("stats", [](KubeRestDeployments& k) {
         auto s = k.stats();
         py::dict d;
@@ -617,6 +627,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["throttled"] = s.throttled;
         d["throttle_ns"] = s.throttle_ns;
         d["speculative_skipped"] = s.speculative_skipped;
+        d["retry_after"] = s.retry_after;
         d["http"] = http_stats_dict(s.http);
         return d;
       });
@@ -835,16 +846,17 @@ PYBIND11_MODULE(_ksa_native, m) {
 
   // ---- fakes ----
   py::class_<InjectedFault>(m, "InjectedFault")
-      .def(py::init([](int status, std::string body, std::string ct, bool drop) {
+      .def(py::init([](int status, std::string body, std::string ct, bool drop, std::string retry_after) {
              InjectedFault f;
              f.status = status;
              f.body = std::move(body);
              f.content_type = std::move(ct);
              f.drop_connection = drop;
+             f.retry_after = std::move(retry_after);
              return f;
            }),
            py::arg("status") = 500, py::arg("body") = "", py::arg("content_type") = "text/plain",
-           py::arg("drop_connection") = false);
+           py::arg("drop_connection") = false, py::arg("retry_after") = "");
 
   py::class_<FakeSqsServer, std::shared_ptr<FakeSqsServer>>(m, "FakeSqsServer")
       .def(py::init<>())

@@ -26,6 +26,7 @@ void apply_fault(const InjectedFault& f, HttpResponse* resp) {
   resp->status = f.status;
   resp->body = f.body;
   resp->headers.emplace_back("Content-Type", f.content_type);
+  if (!f.retry_after.empty()) resp->headers.emplace_back("Retry-After", f.retry_after);
 }
 
 std::string split_path_query(const std::string& target, std::string* query) {

@@ -29,6 +29,7 @@ struct InjectedFault {
   std::string body;
   std::string content_type = "text/plain";
   bool drop_connection = false;  // close the socket without responding
+  std::string retry_after;       // Retry-After header value ("" = none)
 };
 
 class FakeSqsServer {

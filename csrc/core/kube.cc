@@ -271,12 +271,55 @@ Status KubeRestDeployments::check_response(const std::string& verb_desc, const H
   return Status::OK();
 }
 
+// client-go rest.Request.request retries at most this many times (maxRetries).
+constexpr int kMaxRetryAfter = 10;
+
+int64_t KubeRestDeployments::retry_wait_s(const HttpRequest& req, const HttpResponse& resp,
+                                          const Status& transport) const {
+  if (!transport.ok()) {
+    // net.IsConnectionReset / net.IsProbableEOF: only GETs are replayed (writes are not idempotent)
+    if (req.method != "GET") return -1;
+    const std::string& m = transport.message();
+    const bool eof = m == "EOF" || m == "unexpected EOF" || (m.size() > 4 && m.compare(m.size() - 4, 4, ": EOF") == 0);
+    if (eof || m.find("connection reset by peer") != std::string::npos ||
+        m.find("use of closed network connection") != std::string::npos)
+      return 1;
+    return -1;
+  }
+  if (resp.status != 429 && resp.status < 500) return -1;
+  const std::string h = resp.header("Retry-After");
+  if (h.empty()) return -1;
+  auto v = go_atoi(h);  // strconv.Atoi: an HTTP-date is not retried
+  if (!v.ok()) return -1;
+  return v.value;
+}
+
+bool KubeRestDeployments::sleep_retry(int64_t seconds) {
+  // Go sleeps the (possibly negative: no wait) Duration; cap one wait at an hour so a bogus
+  // header cannot park the loop (stop still interrupts it).
+  const int64_t s = seconds < 0 ? 0 : (seconds > 3600 ? 3600 : seconds);
+  std::shared_ptr<Clock> clock = opts_.clock ? opts_.clock : std::make_shared<RealClock>();
+  if (s > 0 && !clock->sleep(s * kSecond, &cancel_)) return false;
+  return !cancel_.stopped();
+}
+
 Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest* req,
                                        HttpResponse* resp, const std::string& name) {
   Status a = add_auth(req);
   if (!a.ok()) return a;
   throttle();
-  return check_response(verb_desc, *req, *resp, name, http_->round_trip(*req, resp));
+  for (int retries = 1;; ++retries) {
+    Status t = http_->round_trip(*req, resp);
+    const int64_t wait = retry_wait_s(*req, *resp, t);
+    if (wait < 0 || retries > kMaxRetryAfter || !sleep_retry(wait))
+      return check_response(verb_desc, *req, *resp, name, t);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.retry_after++;
+    }
+    throttle();  // every retry also goes through the client-side rate limiter
+    *resp = HttpResponse();
+  }
 }
 
 Result<ScaleObject> KubeRestDeployments::parse_get(const Status& s, const HttpResponse& resp) {
@@ -316,6 +359,16 @@ Result<ScaleObject> KubeRestDeployments::finish_get() {
   if (!http_->in_flight()) return Result<ScaleObject>::Err(Status::Err("no pipelined GET in flight"));
   HttpResponse resp;
   Status t = http_->receive(&resp);
+  // A pipelined read that client-go would retry (Retry-After, reset connection) continues as
+  // the reference's own synchronous GET after the wait.
+  const int64_t wait = retry_wait_s(pending_req_, resp, t);
+  if (wait >= 0 && sleep_retry(wait)) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.retry_after++;
+    }
+    return get(pending_name_);
+  }
   return parse_get(check_response("get", pending_req_, resp, pending_name_, t), resp);
 }
 

@@ -142,6 +142,7 @@ struct KubeStats {
   uint64_t throttled = 0;     // requests that waited for the client-side throttle
   int64_t throttle_ns = 0;    // total time spent waiting
   uint64_t speculative_skipped = 0;  // pipelined GETs not sent: no throttle token free
+  uint64_t retry_after = 0;          // client-go style retries (Retry-After, or a reset GET)
   HttpClientStats http;
 };
 
@@ -157,6 +158,11 @@ class KubeRestDeployments final : public DeploymentApi {
   std::string path_for(const std::string& name) const;
 
  private:
+  // Seconds client-go would wait before retrying this outcome (rest.Request.request, checkWait):
+  // the integer Retry-After of a 429 / 5xx response, or 1 for a GET whose connection was reset
+  // or hit EOF; -1 = do not retry.
+  int64_t retry_wait_s(const HttpRequest& req, const HttpResponse& resp, const Status& transport) const;
+  bool sleep_retry(int64_t seconds);
   Status do_request(const std::string& verb_desc, HttpRequest* req, HttpResponse* resp,
                     const std::string& name);
   Status add_auth(HttpRequest* req);

@@ -177,6 +177,7 @@ void fuzz_kube(const std::string& in, ScaleMode mode) {
   o.mode = mode;
   o.timeout = 300 * kMillisecond;
   o.token = std::make_shared<StaticTokenProvider>("tok");
+  o.clock = std::make_shared<VirtualClock>();  // Retry-After / reset-GET retry waits: instant
   KubeRestDeployments api(o);
   auto g = api.get("workers");
   if (g.ok()) (void)api.update("workers", g.value, g.value.replicas + 1);

@@ -153,6 +153,8 @@ def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", time
     o.tls = tls_options(rc)
     o.timeout_ns = timeout_ns
     o.busy_poll_ns = busy_poll_ns
+    if clock is not None:
+        o.clock = clock  # throttle waits and Retry-After sleeps
     if qps > 0:
         o.qps, o.burst = float(qps), int(burst)
         o.clock = clock or nat.RealClock()

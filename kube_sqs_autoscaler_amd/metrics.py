@@ -48,6 +48,8 @@ _API_COUNTERS = [
     ("apiserver_throttle_seconds", "Time spent waiting for the client-side throttle", "kube_api", "throttle_ns"),
     ("speculative_reads_skipped", "Pipelined GETs not sent because no throttle token was free", "kube_api",
      "speculative_skipped"),
+    ("apiserver_retries", "kube-apiserver requests retried after Retry-After (429/5xx) or a reset GET", "kube_api",
+     "retry_after"),
 ]
 _NS_COUNTERS = {"throttle_ns"}  # exported in seconds
 
