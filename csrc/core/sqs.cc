@@ -119,8 +119,9 @@ Nanos HttpSqsApi::retry_delay(int retry_count, bool throttle) {
 
 Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
                                       const std::vector<std::string>& names, bool* retryable,
-                                      bool* throttle, bool* expired) {
+                                      bool* throttle, bool* expired, Nanos* retry_after) {
   *retryable = *throttle = *expired = false;
+  *retry_after = 0;
   auto cr = creds_.get(clock_->unix_nanos());
   if (!cr.ok()) return Result<AttrMap>::Err(cr.status);
 
@@ -233,6 +234,13 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
     for (const char* rc : retry_codes)
       if (code == rc) retry_code = true;
     *retryable = *throttle || *expired || retry_code || st == 500;
+    if (*throttle && (st == 429 || st == 503)) {  // canUseRetryAfterHeader
+      auto secs = go_atoi(resp.header("Retry-After"));
+      if (secs.ok()) {
+        const int64_t c = secs.value > 3600 ? 3600 : (secs.value < -3600 ? -3600 : secs.value);
+        *retry_after = c * kSecond;
+      }
+    }
     return Result<AttrMap>::Err(
         Status::Err(aws_request_failure(code, message, resp.status, rid), resp.status));
   }
@@ -266,7 +274,8 @@ Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
   Result<AttrMap> r;
   for (int attempt = 0;; ++attempt) {
     bool retryable, throttle, expired;
-    r = call_once(queue_url, names, &retryable, &throttle, &expired);
+    Nanos retry_after = 0;
+    r = call_once(queue_url, names, &retryable, &throttle, &expired, &retry_after);
     if (r.ok() || !retryable || attempt >= opts_.max_retries || cancel_.stopped()) break;
     if (expired) creds_.invalidate();
     {
@@ -274,7 +283,8 @@ Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
       stats_.retries++;
       if (throttle) stats_.throttle_retries++;
     }
-    if (!clock_->sleep(retry_delay(attempt, throttle), &cancel_)) break;  // cancelled mid back-off
+    const Nanos delay = retry_delay(attempt, throttle) + retry_after;  // a negative header shortens it
+    if (!clock_->sleep(delay > 0 ? delay : 0, &cancel_)) break;  // cancelled mid back-off
   }
   if (!r.ok()) {
     std::lock_guard<std::mutex> lk(mu_);

@@ -81,8 +81,10 @@ class HttpSqsApi final : public SqsApi {
   std::string endpoint() const { return endpoint_; }
 
  private:
+  // *retry_after: the extra initial delay of a throttle answered 429/503 with an integer
+  // Retry-After (DefaultRetryer.RetryRules, getRetryAfterDelay); 0 otherwise.
   Result<AttrMap> call_once(const std::string& queue_url, const std::vector<std::string>& names,
-                            bool* retryable, bool* throttle, bool* expired);
+                            bool* retryable, bool* throttle, bool* expired, Nanos* retry_after);
   Nanos retry_delay(int retry_count, bool throttle);
 
   SqsHttpOptions opts_;

@@ -358,3 +358,24 @@ def test_tls_reconnect_resumes_session(nat):
         assert st["connects"] == 4 and st["tls_resumptions"] == 3
     finally:
         k.stop()
+
+
+@pytest.mark.parametrize("status,header,extra_s", [(503, "2", 2), (429, "1", 1), (503, "", 0), (502, "5", 0),
+                                                     (503, "Fri, 31 Dec 1999 23:59:59 GMT", 0)])
+def test_sqs_throttle_honours_retry_after(nat, sqs_server, status, header, extra_s):
+    """aws-sdk-go v1.35 DefaultRetryer.RetryRules: a throttle answered 429 or 503 with an
+    integer Retry-After waits that many seconds on top of the back-off (getRetryAfterDelay);
+    other throttles (502) and non-integer values use the back-off alone."""
+    clock = nat.VirtualClock()
+    o = nat.SqsHttpOptions()
+    o.region, o.endpoint = REGION, sqs_server.url
+    o.min_retry_delay_ns = o.min_throttle_delay_ns = 1_000_000  # 1 ms: jitter in [1, 2) ms
+    api = nat.HttpSqsApi(o, static_provider(AKID, SECRET), clock)
+    url = f"{sqs_server.url}/123456789012/q"
+    sqs_server.set_attributes(url, ATTRS)
+    sqs_server.inject(1, nat.InjectedFault(status, "busy", retry_after=header))
+    t0 = clock.now()
+    assert nat.SqsClient(api, url, list(ATTRS)).num_messages() == sum(int(v) for v in ATTRS.values())
+    waited = clock.now() - t0
+    assert extra_s * 10**9 + 1_000_000 <= waited < extra_s * 10**9 + 2_000_000
+    assert api.stats()["throttle_retries"] == 1
