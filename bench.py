@@ -53,6 +53,10 @@ def main(argv=None) -> int:
     ap.add_argument("--no-sweep", action="store_true", help="skip the 1/2/4/8-queue sweep (single rank only)")
     ap.add_argument("--no-pipeline", action="store_true", help="strictly sequential SQS -> GET -> write")
     ap.add_argument("--busy-poll-us", type=int, default=25, help="adaptive client busy-poll window (CLI default --busy-poll=25us; 0: block)")
+    ap.add_argument("--servers", default="shared", choices=["shared", "per-queue"],
+                    help="fake SQS/apiserver: one pair for all of this rank's queues, or one pair per queue")
+    ap.add_argument("--loggers", default="shared", choices=["shared", "per-queue"],
+                    help="one logrus-style logger for the rank (as the reference's global logger) or one per queue")
     args = ap.parse_args(argv)
 
     import torch
@@ -83,7 +87,8 @@ def main(argv=None) -> int:
     native()  # build/load before timing
     pipeline = not args.no_pipeline
     bp = args.busy_poll_us * 1000
-    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp)
+    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp, servers=args.servers,
+                   loggers=args.loggers)
     try:
         if args.warmup:
             env.run(args.warmup)

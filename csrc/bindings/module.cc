@@ -302,11 +302,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_sink",
            [](Logger& l, py::object cb) {
              if (cb.is_none()) {
-               l.set_sink([](const std::string& line) {
-                 std::string s = line + "\n";
-                 ssize_t r = ::write(2, s.data(), s.size());
-                 (void)r;
-               });
+               l.set_sink_fd(2);
                return;
              }
              auto holder = std::make_shared<py::object>(cb);
@@ -322,11 +318,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_sink_fd",
            [](Logger& l, int fd) {
              // Native fd sink (no GIL): one write(2) per line, like logrus on os.Stderr.
-             l.set_sink([fd](const std::string& line) {
-               std::string s = line + "\n";
-               ssize_t r = ::write(fd, s.data(), s.size());
-               (void)r;
-             });
+             l.set_sink_fd(fd);
            })
       .def("set_time_source",
            [](Logger& l, std::shared_ptr<Clock> c) {

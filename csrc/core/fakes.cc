@@ -82,22 +82,26 @@ void FakeSqsServer::drop_connections() {
 }
 
 void FakeSqsServer::set_attributes(const std::string& queue_url, AttrMap attrs) {
+  auto p = std::make_shared<const AttrMap>(std::move(attrs));
   std::lock_guard<std::mutex> lk(mu_);
-  queues_[queue_url] = std::move(attrs);
+  queues_[queue_url] = std::move(p);
 }
 
 void FakeSqsServer::set_attribute_cycle(const std::string& queue_url, std::vector<AttrMap> cycle) {
+  Cycle c;
+  for (auto& m : cycle) c.maps.push_back(std::make_shared<const AttrMap>(std::move(m)));
   std::lock_guard<std::mutex> lk(mu_);
-  if (cycle.empty()) {
+  if (c.maps.empty()) {
     cycles_.erase(queue_url);
     return;
   }
-  cycles_[queue_url] = Cycle{std::move(cycle), 0};
+  cycles_[queue_url] = std::move(c);
 }
 
 void FakeSqsServer::set_default_attributes(AttrMap attrs) {
+  auto p = attrs.empty() ? nullptr : std::make_shared<const AttrMap>(std::move(attrs));
   std::lock_guard<std::mutex> lk(mu_);
-  default_attrs_ = std::move(attrs);
+  default_attrs_ = std::move(p);
 }
 
 void FakeSqsServer::inject(int count, InjectedFault fault) {
@@ -130,10 +134,14 @@ void FakeSqsServer::handle(const HttpRequest& req, HttpResponse* resp) {
   bool faulted;
   bool verify;
   std::string akid, secret, region;
+  // Copy outside the lock and swap inside it (the old values are freed after unlocking), so
+  // concurrent connections hold the shared mutex only for pointer swaps.
+  std::string body_copy = req.body;
+  auto headers_copy = req.headers;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    last_body_ = req.body;
-    last_headers_ = req.headers;
+    last_body_.swap(body_copy);
+    last_headers_.swap(headers_copy);
     latency = latency_;
     faulted = pop_fault(&faults_, &fault);
     verify = verify_;
@@ -205,7 +213,7 @@ void FakeSqsServer::handle(const HttpRequest& req, HttpResponse* resp) {
     }
     for (auto& kv : ordered) names.push_back(kv.second);
   }
-  AttrMap attrs;
+  AttrsPtr attrs;
   {
     std::lock_guard<std::mutex> lk(mu_);
     auto cy = cycles_.find(queue_url);
@@ -214,15 +222,15 @@ void FakeSqsServer::handle(const HttpRequest& req, HttpResponse* resp) {
       attrs = cy->second.maps[cy->second.next];
       cy->second.next = (cy->second.next + 1) % cy->second.maps.size();
     } else if (it != queues_.end()) attrs = it->second;
-    else if (!default_attrs_.empty()) attrs = default_attrs_;
-    else {
-      error(400, "AWS.SimpleQueueService.NonExistentQueue", "The specified queue does not exist for this wsdl version.");
-      return;
-    }
+    else attrs = default_attrs_;
+  }
+  if (!attrs) {
+    error(400, "AWS.SimpleQueueService.NonExistentQueue", "The specified queue does not exist for this wsdl version.");
+    return;
   }
   AttrMap out;
   bool all = std::find(names.begin(), names.end(), "All") != names.end();
-  for (auto& [k, v] : attrs)
+  for (auto& [k, v] : *attrs)
     if (all || std::find(names.begin(), names.end(), k) != names.end()) out[k] = v;
   resp->status = 200;
   resp->headers.emplace_back("x-amzn-RequestId", "fake-request-id");
@@ -535,11 +543,12 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   InjectedFault fault;
   bool faulted;
   std::string token;
+  std::string method_copy = req.method, body_copy = req.body, path_copy = path;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    last_method_ = req.method;
-    last_body_ = req.body;
-    last_path_ = path;
+    last_method_.swap(method_copy);
+    last_body_.swap(body_copy);
+    last_path_.swap(path_copy);
     latency = latency_;
     faulted = pop_fault(&faults_, &fault);
     token = token_;
@@ -605,10 +614,11 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   // Critical sections cover only the object state; rendering happens outside the lock so
   // concurrent workers are not serialised by the fake (a real apiserver serves them in parallel).
   Obj snapshot;
+  const std::string key = ns + "/" + name;
   if (req.method == "GET") {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      auto it = objs_.find(ns + "/" + name);
+      auto it = objs_.find(key);
       if (it == objs_.end()) {
         fail(404, "NotFound", "deployments.apps \"" + name + "\" not found");
         return;
@@ -647,7 +657,7 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   }
   {
     std::lock_guard<std::mutex> lk(mu_);
-    auto it = objs_.find(ns + "/" + name);
+    auto it = objs_.find(key);
     if (it == objs_.end()) {
       fail(404, "NotFound", "deployments.apps \"" + name + "\" not found");
       return;

@@ -67,13 +67,16 @@ class FakeSqsServer {
   bool tls_ = false;
   std::string cert_pem_, key_pem_;
   mutable std::mutex mu_;
-  std::map<std::string, AttrMap> queues_;
+  // Attribute maps are immutable once stored, so a request takes a reference under the lock
+  // and reads the map after releasing it.
+  using AttrsPtr = std::shared_ptr<const AttrMap>;
+  std::map<std::string, AttrsPtr> queues_;
   struct Cycle {
-    std::vector<AttrMap> maps;
+    std::vector<AttrsPtr> maps;
     size_t next = 0;
   };
   std::map<std::string, Cycle> cycles_;
-  AttrMap default_attrs_;
+  AttrsPtr default_attrs_;
   bool verify_ = false;
   std::string akid_, secret_, region_;
   std::vector<InjectedFault> faults_;

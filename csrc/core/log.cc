@@ -2,7 +2,9 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cerrno>
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <unistd.h>
 
@@ -50,22 +52,38 @@ bool logrus_needs_quoting(const std::string& s) {
   return false;
 }
 
-Logger::Logger()
-    : base_unix_ns_(std::chrono::duration_cast<std::chrono::nanoseconds>(
-                        std::chrono::system_clock::now().time_since_epoch())
-                        .count()),
-      shared_(std::make_shared<Shared>()) {
-  shared_->sink = [](const std::string& line) {
+namespace {
+
+int64_t wall_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+// One write(2) for the whole line; loops only on EINTR / a short write.
+void write_line(int fd, const std::string& l) {
+  size_t off = 0;
+  while (off < l.size()) {
+    ssize_t r = ::write(fd, l.data() + off, l.size() - off);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return;
+    off += static_cast<size_t>(r);
+  }
+}
+
+Logger::Sink fd_sink(int fd) {
+  return [fd](const std::string& line) {
     std::string l = line;
     l.push_back('\n');
-    ssize_t r = ::write(2, l.data(), l.size());
-    (void)r;
+    write_line(fd, l);
   };
-  shared_->time = [] {
-    return std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::system_clock::now().time_since_epoch())
-        .count();
-  };
+}
+
+}  // namespace
+
+Logger::Logger() : base_unix_ns_(wall_now_ns()), shared_(std::make_shared<Shared>()) {
+  shared_->sink = fd_sink(2);
+  shared_->time = wall_now_ns;
 }
 
 std::shared_ptr<Logger> Logger::default_logger() {
@@ -75,11 +93,19 @@ std::shared_ptr<Logger> Logger::default_logger() {
 
 void Logger::set_sink(Sink s) {
   std::lock_guard<std::mutex> lk(shared_->mu);
+  shared_->fd.store(-1, std::memory_order_release);
   shared_->sink = std::move(s);
+}
+
+void Logger::set_sink_fd(int fd) {
+  std::lock_guard<std::mutex> lk(shared_->mu);
+  shared_->sink = fd_sink(fd);
+  shared_->fd.store(fd, std::memory_order_release);
 }
 
 void Logger::set_time_source(TimeSource t) {
   std::lock_guard<std::mutex> lk(shared_->mu);
+  shared_->custom_time.store(true, std::memory_order_release);
   shared_->time = std::move(t);
 }
 
@@ -160,6 +186,18 @@ std::string Logger::format(Level l, const std::string& msg, const Fields& fields
 
 void Logger::log(Level l, const std::string& msg, const Fields& fields) {
   if (!enabled(l)) return;
+  const int fd = shared_->fd.load(std::memory_order_acquire);
+  if (fd >= 0 && !shared_->custom_time.load(std::memory_order_acquire)) {
+    std::string line = format(l, msg, fields, wall_now_ns());
+    line.push_back('\n');
+    if (line.size() <= PIPE_BUF) {  // atomic on pipes too: no lock needed
+      write_line(fd, line);
+      return;
+    }
+    std::lock_guard<std::mutex> lk(shared_->mu);
+    write_line(fd, line);
+    return;
+  }
   Sink sink;
   int64_t ts;
   {

@@ -15,6 +15,7 @@
 // offered as an extension.
 #pragma once
 
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -45,8 +46,14 @@ class Logger {
   Level level() const { return level_; }
   void set_format(LogFormat f) { format_ = f; }
   void set_base_time(int64_t unix_ns) { base_unix_ns_ = unix_ns; }
-  // Replaces the output (default: stderr). The sink receives the line without '\n'.
+  // Replaces the output (default: stderr). The sink receives the line without '\n'. Calls are
+  // serialised by the logger's mutex, so the sink need not be thread-safe.
   void set_sink(Sink s);
+  // Output to a file descriptor (the default is fd 2). Each line is one write(2), which the
+  // kernel keeps whole for pipes (up to PIPE_BUF), regular files and terminals, so a line on the
+  // wall clock is formatted and written without taking the logger's mutex: workers tracking
+  // different queues do not serialise on a shared lock per poll.
+  void set_sink_fd(int fd);
   void set_time_source(TimeSource t);
   // Fields appended to every entry of this logger (e.g. queue=... in multi-queue mode).
   void set_base_fields(Fields f) { base_ = std::move(f); }
@@ -68,6 +75,8 @@ class Logger {
     std::mutex mu;
     Sink sink;
     TimeSource time;
+    std::atomic<int> fd{2};                // >= 0: `sink` writes to this fd (lock-free path)
+    std::atomic<bool> custom_time{false};  // set_time_source was called
   };
   Level level_ = Level::Info;
   LogFormat format_ = LogFormat::Text;

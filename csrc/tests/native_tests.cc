@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -603,6 +604,47 @@ TEST(concurrent_logger_lines_are_whole) {
   for (auto& t : ts) t.join();
   CHECK_EQ(lines->size(), size_t(1600));
   for (auto& l : *lines) CHECK(l.rfind("time=\"", 0) == 0 && l.find(" queue=q") != std::string::npos);
+}
+
+TEST(concurrent_fd_sink_lines_are_whole) {
+  // The fd sink writes without the logger's mutex (one write(2) per line). 8 threads into one
+  // pipe: every line must arrive whole, including one longer than PIPE_BUF (locked path).
+  int p[2];
+  CHECK_EQ(::pipe(p), 0);
+  auto log = std::make_shared<Logger>();
+  log->set_sink_fd(p[1]);
+  std::string data;
+  std::thread reader([&] {
+    char buf[65536];
+    ssize_t r;
+    while ((r = ::read(p[0], buf, sizeof buf)) > 0) data.append(buf, static_cast<size_t>(r));
+  });
+  const std::string big(PIPE_BUF + 100, 'x');
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([log, t, &big] {
+      auto child = log->with_fields({{"queue", "q" + std::to_string(t)}});
+      for (int i = 0; i < 500; ++i) child->info("Found " + std::to_string(i) + " messages in the queue");
+      if (t == 0) child->error(big);
+    });
+  for (auto& t : ts) t.join();
+  ::close(p[1]);
+  reader.join();
+  ::close(p[0]);
+  size_t n = 0, bigs = 0, start = 0;
+  for (size_t nl; (nl = data.find('\n', start)) != std::string::npos; start = nl + 1, ++n) {
+    std::string l = data.substr(start, nl - start);
+    CHECK(l.rfind("time=\"", 0) == 0);
+    if (l.find(big) != std::string::npos) {
+      ++bigs;
+      continue;
+    }
+    CHECK(l.find(" level=info msg=\"Found ") != std::string::npos);
+    CHECK(l.size() > 8 && l.compare(l.size() - 8, 7, "queue=q") == 0);
+  }
+  CHECK_EQ(start, data.size());
+  CHECK_EQ(n, size_t(4001));
+  CHECK_EQ(bigs, size_t(1));
 }
 
 TEST(token_bucket_concurrent_reservations) {

@@ -81,52 +81,68 @@ class BenchEnv:
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
-                 busy_poll_ns: int = 0):
+                 busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared"):
         nat = native()
         self.nat = nat
         self.mode = mode
         self.pipeline = pipeline
-        self.sqs = nat.FakeSqsServer()
-        self.sqs.require_signature(AKID, SECRET, REGION)
-        self.sqs.start("127.0.0.1", 0, tls)
-        self.sqs.set_latency(sqs_latency_ns)
-        self.kube = nat.FakeKubeServer()
-        self.kube.require_token(TOKEN)
-        self.kube.start("127.0.0.1", 0, tls)
-        self.kube.set_latency(kube_latency_ns)
+        # servers="per-queue": every queue gets its own fake SQS endpoint and fake apiserver, as
+        # separate processes (one rank per GPU) have; "shared": one of each serves every queue.
+        n_servers = queues if servers == "per-queue" else 1
+        self.sqs_servers, self.kube_servers = [], []
+        for _ in range(n_servers):
+            sqs = nat.FakeSqsServer()
+            sqs.require_signature(AKID, SECRET, REGION)
+            sqs.start("127.0.0.1", 0, tls)
+            sqs.set_latency(sqs_latency_ns)
+            kube = nat.FakeKubeServer()
+            kube.require_token(TOKEN)
+            kube.start("127.0.0.1", 0, tls)
+            kube.set_latency(kube_latency_ns)
+            self.sqs_servers.append(sqs)
+            self.kube_servers.append(kube)
+        self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
         self.clock = nat.RealClock()
-        self.log = nat.Logger()
         self._devnull = None
         if log_fd is None:
             self._devnull = os.open(os.devnull, os.O_WRONLY)
             log_fd = self._devnull
-        self.log.set_sink_fd(log_fd)
+        self.loggers = []
+        for _ in range(queues if loggers == "per-queue" else 1):
+            lg = nat.Logger()
+            lg.set_sink_fd(log_fd)
+            self.loggers.append(lg)
+        self.log = self.loggers[0]
         high = {"ApproximateNumberOfMessages": "150", "ApproximateNumberOfMessagesDelayed": "20",
                 "ApproximateNumberOfMessagesNotVisible": "30"}
         low = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed": "0",
                "ApproximateNumberOfMessagesNotVisible": "0"}
-        rest = RestConfig(host=self.kube.url, bearer_token=TOKEN, insecure=tls)
-        sqs_tls = None
-        if tls:
-            sqs_tls = nat.TlsOptions()
-            sqs_tls.ca_pem = self.sqs.cert_pem
-            rest.insecure = False
-            rest.ca_pem = self.kube.cert_pem
         creds = static_provider(AKID, SECRET)
         self.runners = []
         self.kube_apis, self.sqs_apis = [], []
         self.targets = []
+        self.server_of = []  # queue -> index of the server pair that serves it
         for q in range(queues):
-            url = f"{self.sqs.url}/000000000000/bench-queue-{q}"
+            si = q % n_servers
+            sqs, kube, log = self.sqs_servers[si], self.kube_servers[si], self.loggers[q % len(self.loggers)]
+            rest = RestConfig(host=kube.url, bearer_token=TOKEN, insecure=tls)
+            sqs_tls = None
+            if tls:
+                sqs_tls = nat.TlsOptions()
+                sqs_tls.ca_pem = sqs.cert_pem
+                rest.insecure = False
+                rest.ca_pem = kube.cert_pem
+            url = f"{sqs.url}/000000000000/bench-queue-{q}"
             name = f"gpu-worker-{q}"
-            self.sqs.set_attribute_cycle(url, [high, low])
-            self.kube.add_deployment("bench", name, 1)
+            sqs.set_attribute_cycle(url, [high, low])
+            kube.add_deployment("bench", name, 1)
+            self.server_of.append(si)
             t = TargetConfig(queue_url=url, deployment=name, namespace="bench", poll_period_ns=0,
                              scale_up_cool_down_ns=0, scale_down_cool_down_ns=0, scale_up_messages=100,
                              scale_down_messages=10, max_pods=8, min_pods=1)
             kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=busy_poll_ns)
-            scaler = new_pod_autoscaler(t, kube_api, self.log, self.clock)
-            sqs_api = new_sqs_api(REGION, self.clock, endpoint=self.sqs.url, credentials=creds, tls=sqs_tls,
+            scaler = new_pod_autoscaler(t, kube_api, log, self.clock)
+            sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, credentials=creds, tls=sqs_tls,
                                   busy_poll_ns=busy_poll_ns)
             client = new_sqs_client(t, sqs_api)
             self.kube_apis.append(kube_api)
@@ -138,7 +154,7 @@ class BenchEnv:
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
-            self.runners.append(nat.Runner(cfg, client, scaler, self.clock, self.log))
+            self.runners.append(nat.Runner(cfg, client, scaler, self.clock, log))
             self.targets.append(t)
 
     def run(self, iterations: int) -> float:
@@ -155,12 +171,13 @@ class BenchEnv:
         res = LatencyResult(queues=len(self.runners), mode=self.mode, steps=steps, pipeline=self.pipeline, wall_s=wall)
         for r in self.runners:
             res.samples.extend(r.latencies())
-        res.sqs_requests = self.sqs.requests()
-        res.kube_requests = self.kube.requests()
-        res.sqs_connections = self.sqs.connections()
-        res.kube_connections = self.kube.connections()
-        res.signature_failures = self.sqs.signature_failures()
-        res.final_replicas = [self.kube.replicas("bench", t.deployment) for t in self.targets]
+        res.sqs_requests = sum(s.requests() for s in self.sqs_servers)
+        res.kube_requests = sum(k.requests() for k in self.kube_servers)
+        res.sqs_connections = sum(s.connections() for s in self.sqs_servers)
+        res.kube_connections = sum(k.connections() for k in self.kube_servers)
+        res.signature_failures = sum(s.signature_failures() for s in self.sqs_servers)
+        res.final_replicas = [self.kube_servers[si].replicas("bench", t.deployment)
+                              for si, t in zip(self.server_of, self.targets)]
         return res
 
     def clear(self) -> None:
@@ -168,8 +185,10 @@ class BenchEnv:
             r.clear_latencies()
 
     def close(self) -> None:
-        self.sqs.stop()
-        self.kube.stop()
+        for s in self.sqs_servers:
+            s.stop()
+        for k in self.kube_servers:
+            k.stop()
         if self._devnull is not None:
             os.close(self._devnull)
             self._devnull = None
