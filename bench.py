@@ -146,18 +146,23 @@ def main(argv=None) -> int:
             # Secondary rows: three interleaved rounds, median p50 per row, so one disturbed run
             # (CPU migration, a noisy neighbour) cannot invert the comparison.
             n, w = min(args.steps, 2000), min(args.warmup, 200)
-            rows = {f"q{q}": (q, args.mode, pipeline, bp, False) for q in (1, 2, 4, 8)}
-            rows["sequential"] = (1, args.mode, False, 0, False)
-            rows["reference"] = (1, "deployment", False, 0, False)
+            rows = {f"q{q}": (q, args.mode, pipeline, bp, False, "shared") for q in (1, 2, 4, 8)}
+            # 8 queues, each against its own fake SQS + apiserver pair (what 8 ranks see): the
+            # single-process fakes serialise on their own state lock, real endpoints do not.
+            rows["q8_per_queue_endpoints"] = (8, args.mode, pipeline, bp, False, "per-queue")
+            rows["sequential"] = (1, args.mode, False, 0, False, "shared")
+            rows["reference"] = (1, "deployment", False, 0, False, "shared")
             # Production endpoints are HTTPS: the same two paths over keep-alive TLS 1.3
-            rows["tls"] = (1, args.mode, pipeline, bp, True)
-            rows["reference_tls"] = (1, "deployment", False, 0, True)
+            rows["tls"] = (1, args.mode, pipeline, bp, True, "shared")
+            rows["reference_tls"] = (1, "deployment", False, 0, True, "shared")
             p50s = {k: [] for k in rows}
             for _ in range(3):
-                for k, (q, mode, pl, b, tls) in rows.items():
-                    p50s[k].append(measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls).summary()["p50_ms"])
+                for k, (q, mode, pl, b, tls, sv) in rows.items():
+                    p50s[k].append(measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls,
+                                           servers=sv).summary()["p50_ms"])
             med = {k: sorted(v)[1] for k, v in p50s.items()}
             extra["p50_ms_by_tracked_queues"] = {str(q): med[f"q{q}"] for q in (1, 2, 4, 8)}
+            extra["p50_ms_8_queues_per_queue_endpoints"] = med["q8_per_queue_endpoints"]
             extra["sequential_scale_p50_ms"] = med["sequential"]
             extra["reference_equivalent_p50_ms"] = med["reference"]
             extra["tls_p50_ms"] = {"default": med["tls"], "reference_equivalent": med["reference_tls"]}
