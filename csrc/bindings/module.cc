@@ -144,6 +144,8 @@ py::dict record_dict(const IterationRecord& r) {
   d["replicas_after"] = r.replicas_after;
   d["prefetched"] = r.prefetched;
   d["prefetch_used"] = r.prefetch_used;
+  d["prefetch_gated"] = r.prefetch_gated;
+  d["gets"] = r.gets;
   d["depth_ns"] = r.depth_ns;
   d["get_ns"] = r.get_ns;
   d["update_ns"] = r.update_ns;
@@ -645,6 +647,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readonly("before", &ScaleSpan::before)
       .def_readonly("used_prefetch", &ScaleSpan::used_prefetch)
       .def_readonly("refetched", &ScaleSpan::refetched)
+      .def_readonly("gets", &ScaleSpan::gets)
       .def_readonly("after", &ScaleSpan::after);
 
   py::class_<PodAutoScaler, std::shared_ptr<PodAutoScaler>>(m, "PodAutoScaler")
@@ -691,7 +694,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("scale_up_cool_down_ns", &LoopConfig::scale_up_cool_down)
       .def_readwrite("scale_up_messages", &LoopConfig::scale_up_messages)
       .def_readwrite("scale_down_messages", &LoopConfig::scale_down_messages)
-      .def_readwrite("prefetch", &LoopConfig::prefetch);
+      .def_readwrite("prefetch", &LoopConfig::prefetch)
+      .def_readwrite("prefetch_always", &LoopConfig::prefetch_always);
 
   py::class_<Runner, std::shared_ptr<Runner>>(m, "Runner")
       .def(py::init<LoopConfig, std::shared_ptr<SqsClient>, std::shared_ptr<PodAutoScaler>, std::shared_ptr<Clock>,
@@ -744,6 +748,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["failed_downs"] = s.failed_downs;
         d["speculative_reads"] = s.speculative_reads;
         d["speculative_reads_used"] = s.speculative_reads_used;
+        d["speculative_reads_gated"] = s.speculative_reads_gated;
+        d["apiserver_reads"] = s.apiserver_reads;
         d["last_depth"] = s.last_depth;
         d["last_replicas"] = s.last_replicas;
         d["latency_samples"] = s.latency_samples;

@@ -595,6 +595,7 @@ Result<ScaleObject> PodAutoScaler::read(ScaleSpan* span, bool* from_prefetch) {
     }
     // A failed speculative read is not reported: fall through to the reference's own GET.
   }
+  span->gets++;
   return api_->get(deployment_);
 }
 
@@ -647,6 +648,7 @@ Status PodAutoScaler::scale(bool up, ScaleSpan* span) {
       // The object changed after the pipelined read: re-read and decide again, which is the
       // reference's GET-after-poll. Only a conflict on this fresh read is reported.
       Nanos tg = clock_->now();
+      span->gets++;
       d = api_->get(deployment_);
       span->get_ns += clock_->now() - tg;
       span->refetched = true;

@@ -248,6 +248,7 @@ struct ScaleSpan {
   int32_t after = 0;
   bool used_prefetch = false;  // the decision used the pipelined GET
   bool refetched = false;      // the pipelined object was stale (409) and was re-read
+  int gets = 0;                // synchronous GETs this call sent (the pipelined one not counted)
 };
 
 class PodAutoScaler {

@@ -190,11 +190,12 @@ void Logger::log(Level l, const std::string& msg, const Fields& fields) {
   if (fd >= 0 && !shared_->custom_time.load(std::memory_order_acquire)) {
     std::string line = format(l, msg, fields, wall_now_ns());
     line.push_back('\n');
-    if (line.size() <= PIPE_BUF) {  // atomic on pipes too: no lock needed
+    if (line.size() <= PIPE_BUF) {  // one atomic write(2), on pipes too
+      std::shared_lock<std::shared_mutex> lk(shared_->fd_mu);
       write_line(fd, line);
       return;
     }
-    std::lock_guard<std::mutex> lk(shared_->mu);
+    std::unique_lock<std::shared_mutex> lk(shared_->fd_mu);
     write_line(fd, line);
     return;
   }

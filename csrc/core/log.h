@@ -19,6 +19,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -52,7 +53,8 @@ class Logger {
   // Output to a file descriptor (the default is fd 2). Each line is one write(2), which the
   // kernel keeps whole for pipes (up to PIPE_BUF), regular files and terminals, so a line on the
   // wall clock is formatted and written without taking the logger's mutex: workers tracking
-  // different queues do not serialise on a shared lock per poll.
+  // different queues only share a reader lock, which a line longer than PIPE_BUF (possibly
+  // several writes) takes exclusively so nothing interleaves with its pieces.
   void set_sink_fd(int fd);
   void set_time_source(TimeSource t);
   // Fields appended to every entry of this logger (e.g. queue=... in multi-queue mode).
@@ -73,6 +75,10 @@ class Logger {
   int64_t base_unix_ns_;  // logrus' baseTimestamp (package init) for the TTY layout
   struct Shared {
     std::mutex mu;
+    // fd sink: a line of at most PIPE_BUF bytes is one atomic write(2), so those writers share
+    // this lock; a longer line may take several writes and holds it exclusively, so no short
+    // line can land between its pieces.
+    std::shared_mutex fd_mu;
     Sink sink;
     TimeSource time;
     std::atomic<int> fd{2};                // >= 0: `sink` writes to this fd (lock-free path)

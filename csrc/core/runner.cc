@@ -51,6 +51,23 @@ void Runner::arm() {
   progress_ns_.store(clock_->now(), std::memory_order_release);
 }
 
+// Would this poll call ScaleUp/ScaleDown if the queue depth were still the last one read?
+// Evaluated at t0 + the last SQS round trip, which is when the gates of main.go:51-77 will run.
+// An exact replay of those gates on the previous depth: a depth at or above the up threshold
+// either passes the up cool-down (-> a GET) or `continue`s past the down check (main.go:54);
+// a depth in the dead band reads nothing. Before the first depth read either open cool-down
+// counts. A wrong guess costs nothing in decisions: an unsent prefetch means the reference's
+// own synchronous GET after the SQS response, an unused one is drained.
+bool Runner::action_likely(Nanos t0) const {
+  const Nanos at = t0 + last_depth_rtt_;
+  const bool up_open = sat_add(last_up_, cfg_.scale_up_cool_down) <= at;
+  const bool down_open = sat_add(last_down_, cfg_.scale_down_cool_down) <= at;
+  if (!have_depth_) return up_open || down_open;
+  if (last_depth_ >= cfg_.scale_up_messages) return up_open;
+  if (last_depth_ <= cfg_.scale_down_messages) return down_open;
+  return false;
+}
+
 IterationRecord Runner::step(StopFlag* stop) {
   // main.go:41 -- sleep BEFORE the poll.
   if (!clock_->sleep(cfg_.poll_period, stop)) {
@@ -66,13 +83,23 @@ IterationRecord Runner::poll_once() {
   rec.index = ++index_;
   const Nanos t0 = clock_->now();
   rec.t_poll = t0;
-  // Pipelined read: the Deployment GET goes out before the SQS call and overlaps it.
-  if (cfg_.prefetch) rec.prefetched = scaler_->prefetch();
+  // Pipelined read: the Deployment GET goes out before the SQS call and overlaps it -- only
+  // when this poll is likely to reach the apiserver at all (the reference reads the Deployment
+  // only past the threshold and cool-down gates, main.go:51-77).
+  if (cfg_.prefetch) {
+    if (cfg_.prefetch_always || action_likely(t0)) {
+      rec.prefetched = scaler_->prefetch();
+      if (rec.prefetched) rec.gets++;
+    } else {
+      rec.prefetch_gated = true;
+    }
+  }
 
   // main.go:43-47
   auto depth = sqs_->num_messages();
   Nanos t1 = clock_->now();
   rec.depth_ns = t1 - t0;
+  last_depth_rtt_ = rec.depth_ns;
   if (!depth.ok()) {
     rec.error = depth.status.message();
     log_->error("Failed to get SQS messages: " + depth.status.message());
@@ -84,6 +111,8 @@ IterationRecord Runner::poll_once() {
   const int64_t n = depth.value;
   rec.depth_ok = true;
   rec.depth = n;
+  have_depth_ = true;
+  last_depth_ = n;
   log_->info("Found " + std::to_string(n) + " messages in the queue");  // main.go:49
 
   auto finish = [&]() -> IterationRecord& {
@@ -105,6 +134,7 @@ IterationRecord Runner::poll_once() {
     rec.get_ns += span.get_ns;
     rec.update_ns += span.update_ns;
     rec.prefetch_used |= span.used_prefetch;
+    rec.gets += span.gets;
     if (span.read) {
       rec.replicas_before = span.before;
       rec.replicas_after = span.after;
@@ -132,6 +162,7 @@ IterationRecord Runner::poll_once() {
     rec.get_ns += span.get_ns;
     rec.update_ns += span.update_ns;
     rec.prefetch_used |= span.used_prefetch;
+    rec.gets += span.gets;
     if (span.read) {
       if (rec.replicas_before < 0) rec.replicas_before = span.before;
       rec.replicas_after = span.after;
@@ -156,6 +187,8 @@ void Runner::record(const IterationRecord& r) {
     stats_.polls++;
     if (r.prefetched) stats_.speculative_reads++;
     if (r.prefetch_used) stats_.speculative_reads_used++;
+    if (r.prefetch_gated) stats_.speculative_reads_gated++;
+    stats_.apiserver_reads += static_cast<uint64_t>(r.gets);
     if (!r.depth_ok) stats_.depth_errors++;
     else stats_.last_depth = r.depth;
     switch (r.up) {
@@ -197,6 +230,7 @@ std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std:
                   ",\"replicas_after\":" + std::to_string(r.replicas_after) +
                   ",\"prefetched\":" + (r.prefetched ? "true" : "false") +
                   ",\"prefetch_used\":" + (r.prefetch_used ? "true" : "false") +
+                  ",\"gets\":" + std::to_string(r.gets) +
                   ",\"depth_ns\":" + std::to_string(r.depth_ns) + ",\"get_ns\":" + std::to_string(r.get_ns) +
                   ",\"update_ns\":" + std::to_string(r.update_ns) + ",\"total_ns\":" + std::to_string(r.total_ns) +
                   ",\"patch_latency_ns\":" + std::to_string(r.patch_latency_ns);

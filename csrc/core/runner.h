@@ -44,6 +44,10 @@ struct LoopConfig {
   // Overlap the Deployment GET with the SQS poll (PodAutoScaler::prefetch). Decisions are the
   // reference's; only the read is issued earlier and validated by the write's resourceVersion.
   bool prefetch = false;                      // --pipeline-reads
+  // By default the speculative GET is only sent when a scale call is likely to follow the SQS
+  // response (Runner::action_likely), so an idle queue costs the apiserver what the reference
+  // costs it: nothing between cool-down expiries. true: send it with every poll.
+  bool prefetch_always = false;
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };
@@ -60,7 +64,9 @@ struct IterationRecord {
   int32_t replicas_before = -1;  // as read by the last GET of the iteration (-1: not read)
   int32_t replicas_after = -1;
   bool prefetched = false;     // a pipelined GET was issued with the poll
+  bool prefetch_gated = false; // --pipeline-reads, but the gate predicted no action: none sent
   bool prefetch_used = false;  // ... and a scale decision consumed it
+  int gets = 0;                // Deployment GETs this poll (speculative + synchronous)
   Nanos depth_ns = 0;          // SQS GetQueueAttributes round trip
   Nanos get_ns = 0;            // Deployment GET(s)
   Nanos update_ns = 0;         // Deployment PUT/PATCH(es)
@@ -82,6 +88,8 @@ struct RunnerStats {
   uint64_t failed_downs = 0;
   uint64_t speculative_reads = 0;       // pipelined GETs issued (one per poll with --pipeline-reads)
   uint64_t speculative_reads_used = 0;  // ... consumed by a scale decision (the rest are extra API load)
+  uint64_t speculative_reads_gated = 0; // polls where the gate predicted no action and sent none
+  uint64_t apiserver_reads = 0;         // Deployment GETs of any kind (speculative + synchronous)
   int64_t last_depth = 0;
   int32_t last_replicas = -1;
   uint64_t latency_samples = 0;
@@ -135,6 +143,11 @@ class Runner {
   std::shared_ptr<Logger> log_;
   Nanos last_up_ = 0, last_down_ = 0;
   uint64_t index_ = 0;
+  // Prefetch gate inputs: the last depth read (if any) and the last SQS round trip.
+  bool have_depth_ = false;
+  int64_t last_depth_ = 0;
+  Nanos last_depth_rtt_ = 0;
+  bool action_likely(Nanos t0) const;
   std::function<void(const IterationRecord&)> observer_;
   int trace_fd_ = -1;
   void write_trace(const IterationRecord& r);

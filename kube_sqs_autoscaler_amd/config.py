@@ -25,7 +25,9 @@ Extensions (all off or reference-equivalent by default):
   resourceVersion precondition).
 * ``--pipeline-reads`` (default on): overlap the Deployment GET with the SQS poll; the write's
   resourceVersion precondition validates the early read and a conflict re-reads once, so the
-  decisions are the reference's (``models/oracle.py`` ``prefetch``).
+  decisions are the reference's (``models/oracle.py`` ``prefetch``). The early GET is only sent
+  when the previous depth and the cool-downs say a scale call will follow (runner.h
+  ``action_likely``), so an idle queue reads the apiserver no more often than the reference.
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
   ``--log-format``, ``--metrics-addr``, ``--trace-file``, ``--gpu-aware-max``.
 * ``--leader-elect`` (+ lease name/namespace/identity/timings): Lease-based leader election so
@@ -107,11 +109,23 @@ class Config:
     leader_elect_retry_period_ns: int = 2 * SECOND
 
 
+# Go's unicode.IsSpace set, which strings.TrimSpace strips: ASCII \t \n \v \f \r and space,
+# U+0085 (NEL), U+00A0 (NBSP) and the other White_Space code points. Python's str.strip()
+# also strips U+001C..U+001F (and nothing Go keeps would survive it), so it is not used.
+GO_SPACE = ("\t\n\v\f\r \u0085\u00a0\u1680\u2000\u2001\u2002\u2003\u2004\u2005\u2006\u2007"
+            "\u2008\u2009\u200a\u2028\u2029\u202f\u205f\u3000")
+
+
+def go_trim_space(s: str) -> str:
+    """strings.TrimSpace."""
+    return s.strip(GO_SPACE)
+
+
 def parse_attribute_names(value: str) -> List[str]:
     """/root/reference/main.go:103-110 (string inequality with the default, then split+trim)."""
     if value == DEFAULT_ATTRIBUTE_NAMES:
         return DEFAULT_ATTRIBUTE_NAMES.split(",")
-    return [piece.strip() for piece in value.split(",")]
+    return [go_trim_space(piece) for piece in value.split(",")]
 
 
 def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
@@ -146,7 +160,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
     fs.int("worker-threads", 0, "Threads polling the tracked queues; 0 = one per queue (use fewer for hundreds of queues)")
     fs.bool("dry-run", False, "Shadow mode: poll and decide as usual, log the scaling that would happen, never write")
-    fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
+    fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap, on polls likely to scale (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.float64("kube-api-qps", 5.0, "Client-side limit on kube-apiserver requests per second for each tracked queue, as client-go's default rest client (0 disables)")
     fs.int("kube-api-burst", 10, "Requests allowed in a burst above -kube-api-qps (client-go default)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
@@ -190,13 +204,13 @@ def parse_queue_spec(spec: str, base: TargetConfig) -> TargetConfig:
     t = replace(base, attribute_names=list(base.attribute_names))
     seen_url = False
     for item in spec.split(","):
-        if not item.strip():
+        if not go_trim_space(item):
             continue
         if "=" not in item:
             raise FlagError(f'invalid value "{spec}" for flag -queue: expected key=value, got "{item}"')
         k, v = item.split("=", 1)
-        k = k.strip()
-        v = v.strip()
+        k = go_trim_space(k)
+        v = go_trim_space(v)
         try:
             if k in ("url", "sqs-queue-url"):
                 t.queue_url = v

@@ -31,6 +31,8 @@ _COUNTERS = [
     ("failed_downs", "Scale-downs that failed"),
     ("speculative_reads", "Deployment GETs sent with the SQS poll (--pipeline-reads)"),
     ("speculative_reads_used", "Speculative GETs consumed by a scale decision"),
+    ("speculative_reads_gated", "Polls that sent no speculative GET because no scale call was likely"),
+    ("apiserver_reads", "Deployment GETs of the control loop (speculative + synchronous)"),
 ]
 
 # Per-worker API client counters: (metric, help, client attribute, stats key)

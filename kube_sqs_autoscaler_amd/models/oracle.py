@@ -83,6 +83,8 @@ class Event:
     down: str = "none"
     replicas: int = 0  # Deployment replicas after the poll
     up_replicas: Optional[int] = None  # replicas right after a scale-up write
+    prefetched: bool = False  # a pipelined GET went out with this poll
+    gets: int = 0  # Deployment GETs sent during the poll (pipelined + synchronous)
 
     def key(self) -> Tuple:
         return (self.index, self.depth, self.up, self.down, self.replicas)
@@ -127,30 +129,46 @@ def simulate(
     lat: Latency = Latency(),
     faults: Optional[Faults] = None,
     prefetch: bool = False,
+    prefetch_always: bool = False,
 ) -> List[Event]:
     """Runs ``polls`` iterations of the reference loop on a virtual clock.
 
     ``prefetch`` models the pipelined read (``--pipeline-reads``): the Deployment GET is sent
     with the SQS call, so the first GET of a poll costs ``max(0, get - sqs)`` extra instead of
     ``get``, and an unused prefetch is drained at the end of the poll. The decision rules are
-    unchanged -- only when ``now`` is read moves.
+    unchanged -- only when ``now`` is read moves. The GET is only sent on polls whose gates
+    would open on the previous depth (``prefetch_always`` sends it on every poll): see
+    :func:`_likely`, restated from the rule in runner.h, not shared with it.
     """
     f = faults or Faults()
     st = {"now": 0, "last_up": 0, "last_down": 0, "replicas": int32(init_replicas)}  # main.go:37-38
     out: List[Event] = []
+    seen = {"depth": None, "rtt": 0}  # prefetch gate inputs: last depth read, last SQS latency
 
-    def read(k: int, pf: dict, fail_set: Set[int]) -> bool:
+    def _likely(t0: int) -> bool:
+        at = t0 + seen["rtt"]
+        up_open = st["last_up"] + p.up_cool_ns <= at
+        down_open = st["last_down"] + p.down_cool_ns <= at
+        d = seen["depth"]
+        if d is None:
+            return up_open or down_open
+        if d >= p.up_msgs:  # the up gate either reads or `continue`s past the down check
+            return up_open
+        return down_open if d <= p.down_msgs else False
+
+    def read(k: int, ev: Event, pf: dict, fail_set: Set[int]) -> bool:
         """One GET; returns False when it fails (injected fault)."""
         if pf["pending"]:
             pf["pending"] = False
             st["now"] = max(st["now"], pf["done"])
         else:
             st["now"] += lat.get_ns
+            ev.gets += 1
         return k not in fail_set
 
     def scale(k: int, ev: Event, up: bool, pf: dict) -> bool:
         """ScaleUp/ScaleDown + timer refresh; False means `continue` (failure)."""
-        if not read(k, pf, f.up_get if up else f.down_get):
+        if not read(k, ev, pf, f.up_get if up else f.down_get):
             setattr(ev, "up" if up else "down", "failed")
             return False
         r = st["replicas"]
@@ -186,6 +204,7 @@ def simulate(
     def poll(k: int, ev: Event, pf: dict) -> None:
         attrs = sample(trace, st["now"])
         st["now"] += lat.sqs_ns
+        seen["rtt"] = lat.sqs_ns
         if k in f.sqs:
             return
         try:
@@ -193,6 +212,7 @@ def simulate(
         except (ValueError, TypeError):
             return  # main.go:44-47
         ev.depth = n
+        seen["depth"] = n
         if n >= p.up_msgs:  # main.go:51
             if st["last_up"] + p.up_cool_ns > st["now"]:  # main.go:52
                 ev.up = "cooldown"
@@ -209,12 +229,21 @@ def simulate(
         st["now"] += max(p.poll_ns, 0)  # main.go:41 time.Sleep (<= 0: no sleep)
         ev = Event(index=k, t_poll_ns=st["now"], depth=None)
         out.append(ev)
-        pf = {"pending": prefetch, "done": st["now"] + lat.get_ns}
+        pf = {"pending": prefetch and (prefetch_always or _likely(st["now"])), "done": st["now"] + lat.get_ns}
+        ev.prefetched = pf["pending"]
+        ev.gets = int(ev.prefetched)
         poll(k, ev, pf)
         if pf["pending"]:  # drain an unused prefetch
             st["now"] = max(st["now"], pf["done"])
         ev.replicas = st["replicas"]
     return out
+
+
+def reference_gets(events: Sequence[Event]) -> int:
+    """Deployment GETs the reference sends on these polls: one per ScaleUp/ScaleDown call,
+    i.e. per direction that got past its threshold and cool-down gates (scale.go:55,82)."""
+    called = ("scaled", "noop", "failed")
+    return sum((e.up in called) + (e.down in called) for e in events)
 
 
 def scale_events(events: Sequence[Event]) -> List[Tuple[str, int, int]]:

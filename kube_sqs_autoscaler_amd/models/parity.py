@@ -29,6 +29,8 @@ def _records_to_events(recs: Sequence[dict], init_replicas: int) -> List[Event]:
             up=r["up"],
             down=r["down"],
             replicas=replicas,
+            prefetched=r["prefetched"],
+            gets=r["gets"],
         )
         out.append(ev)
     return out
@@ -97,6 +99,7 @@ def run_native(
     faults: Optional[Faults] = None,
     log_sink=None,
     prefetch: bool = False,
+    prefetch_always: bool = False,
 ) -> List[Event]:
     """Runs ``scenario`` through the native control loop and returns per-poll events."""
     nat = native()
@@ -135,6 +138,7 @@ def run_native(
     cfg.scale_up_messages = p.up_msgs
     cfg.scale_down_messages = p.down_msgs
     cfg.prefetch = prefetch
+    cfg.prefetch_always = prefetch_always
     runner = nat.Runner(cfg, sqs, scaler, clock, log)
     runner.arm()
     if counter is None:
@@ -173,15 +177,18 @@ class ParityResult:
         return self.agree == self.polls
 
 
-def compare(scenario: Scenario, faults: Optional[Faults] = None, prefetch: bool = False) -> ParityResult:
+def compare(scenario: Scenario, faults: Optional[Faults] = None, prefetch: bool = False,
+            prefetch_always: bool = False) -> ParityResult:
+    """Poll-by-poll agreement; with ``prefetch`` the gate's send/skip choice must agree too."""
     ref = simulate(
         scenario.params, scenario.trace, scenario.names, scenario.polls, scenario.init_replicas, scenario.latency, faults,
-        prefetch=prefetch,
+        prefetch=prefetch, prefetch_always=prefetch_always,
     )
-    got = run_native(scenario, faults, prefetch=prefetch)
+    got = run_native(scenario, faults, prefetch=prefetch, prefetch_always=prefetch_always)
     res = ParityResult(scenario=scenario.name, polls=len(ref), agree=0)
     for a, b in zip(ref, got):
-        if a.key() == b.key() and a.t_poll_ns == b.t_poll_ns:
+        if a.key() == b.key() and a.t_poll_ns == b.t_poll_ns and a.prefetched == b.prefetched \
+                and a.gets == b.gets:
             res.agree += 1
         else:
             res.mismatches.append((a, b))

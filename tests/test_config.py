@@ -61,6 +61,12 @@ def test_readme_example_flags():
     ("A,,B", ["A", "", "B"]),  # empty piece kept, like the reference (which then panics at sqs.go:58)
     ("", [""]),
     (DEFAULT_ATTRIBUTE_NAMES + " ", DEFAULT_ATTRIBUTE_NAMES.split(",")),  # differs as a string -> split+trim
+    # strings.TrimSpace is unicode.IsSpace: U+001C..U+001F are kept (Python's str.strip drops
+    # them), NEL / NBSP / U+3000 are trimmed
+    ("A,\x1cB\x1c, C ", ["A", "\x1cB\x1c", "C"]),
+    ("\x1f\x1eA", ["\x1f\x1eA"]),
+    ("\u0085A ,　B \t", ["A", "B"]),
+    ("​A", ["​A"]),  # ZERO WIDTH SPACE is not White_Space
 ])
 def test_attribute_names_rule(value, names):
     assert parse_attribute_names(value) == names

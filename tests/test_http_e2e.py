@@ -313,13 +313,42 @@ def test_full_loop_pipelined_over_the_wire(nat, sqs_server, kube_server):
     sqs_server.set_attributes(url, {n: "100" for n in NAMES})
     recs = r.steps(4)
     assert [x["up"] for x in recs] == ["scaled", "scaled", "noop", "noop"] and all(x["prefetched"] for x in recs)
-    sqs_server.set_attributes(url, {n: "50" for n in NAMES})  # dead band: prefetch drained
-    r.steps(3)
+    sqs_server.set_attributes(url, {n: "10" for n in NAMES})  # 30 messages: dead band
+    band = r.steps(3)
+    # the first dead-band poll still predicted an up (its prefetch is drained unused); the
+    # next two know the depth is in the dead band and send nothing, as the reference
+    assert [x["prefetched"] for x in band] == [True, False, False] and [x["gets"] for x in band] == [1, 0, 0]
     sqs_server.set_attributes(url, {n: "0" for n in NAMES})
     recs = r.steps(5)
     assert [x["down"] for x in recs] == ["scaled"] * 4 + ["noop"]
+    # the first drained poll reads synchronously (dead-band depth predicted nothing)
+    assert [x["prefetched"] for x in recs] == [False] + [True] * 4 and all(x["gets"] == 1 for x in recs)
     assert kube_server.replicas("ml", "worker") == 1 and kube_server.connections() == 1
-    assert kube_server.gets() == 12  # exactly one GET per poll
+    # the reference reads on the 4 + 5 polls that act; the gate adds the one mispredicted poll
+    assert kube_server.gets() == 10 and r.stats()["apiserver_reads"] == 10
+
+
+def test_idle_queue_sends_no_speculative_gets(nat, sqs_server, kube_server):
+    """C1-shaped idle queue (empty, replicas at min): with --pipeline-reads the apiserver sees
+    exactly the reference's reads -- one GET per scale-down cool-down expiry (the no-op at min,
+    /root/reference/scale/scale.go:82-92) -- and none on the polls in between."""
+    c, _, url = sqs_client(nat, sqs_server)
+    p, _ = scaler(nat, kube_server, "scale", max_=1, min_=1)
+    kube_server.set_replicas("ml", "worker", 1)
+    clock = nat.VirtualClock(0)
+    cfg = nat.LoopConfig()
+    cfg.poll_period_ns = 5 * 10**9
+    cfg.scale_up_cool_down_ns = 10 * 10**9
+    cfg.scale_down_cool_down_ns = 30 * 10**9
+    cfg.prefetch = True
+    r = nat.Runner(cfg, c, p, clock, capture_logger([]))
+    r.arm()
+    sqs_server.set_attributes(url, {n: "0" for n in NAMES})
+    gets0 = kube_server.gets()
+    recs = r.steps(60)
+    assert [i + 1 for i, x in enumerate(recs) if x["down"] == "noop"] == list(range(6, 61, 6))
+    assert [i + 1 for i, x in enumerate(recs) if x["prefetched"]] == list(range(6, 61, 6))
+    assert kube_server.gets() - gets0 == 10 and all(x["prefetch_used"] for x in recs if x["prefetched"])
 
 
 def test_adaptive_busy_poll_tracks_peer_rtt(nat, kube_server):

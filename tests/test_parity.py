@@ -72,3 +72,20 @@ def test_pipelined_reads_parity_and_goldens(sc):
     assert r.ok, r.mismatches[:3]
     ev = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True)
     assert traces.golden_from_events(ev, sc.params.poll_ns) == sc.golden
+
+
+@pytest.mark.parametrize("sc", traces.baseline_scenarios(), ids=lambda s: s.name)
+def test_gated_prefetch_reads_what_the_reference_reads(sc):
+    """--pipeline-reads on the Appendix C traces sends exactly the reference's Deployment GETs
+    (C1: 20 in 120 polls, one per down-no-op at min), where sending one with every poll would
+    read on every poll."""
+    r = parity.compare(sc, prefetch=True)
+    assert r.ok, r.mismatches[:3]
+    ref = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency)
+    ev = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True)
+    assert sum(e.gets for e in ev) == oracle.reference_gets(ref) == sum(e.gets for e in ref)
+    always = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True,
+                             prefetch_always=True)
+    assert sum(e.gets for e in always) == sc.polls
+    if sc.name.startswith("c1"):
+        assert oracle.reference_gets(ref) == 20 and sc.polls == 120

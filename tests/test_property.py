@@ -33,11 +33,46 @@ def scenarios(draw, with_faults=False):
 
 
 @settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
-@given(scenarios(), st.booleans())
+@given(scenarios(), st.sampled_from(["off", "gated", "always"]))
 def test_native_equals_oracle(case, prefetch):
+    """Poll-by-poll agreement, including (with --pipeline-reads) whether the gate sent the
+    speculative GET and how many GETs the poll made."""
     sc, _ = case
-    r = parity.compare(sc, prefetch=prefetch)
+    r = parity.compare(sc, prefetch=prefetch != "off", prefetch_always=prefetch == "always")
     assert r.ok, r.mismatches[:2]
+
+
+def _depth_class(d, p):
+    return "up" if d >= p.up_msgs else ("down" if d <= p.down_msgs else "band")
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(scenarios())
+def test_prefetch_gate_costs_the_reference_api_reads(case):
+    """The gated speculative GET goes out exactly on the polls that call ScaleUp/ScaleDown
+    whenever the depth stayed in the same threshold class as the previous read, so the
+    apiserver sees the reference's reads plus at most one per class change -- never one per
+    poll (120 GETs vs the reference's 20 on an idle queue)."""
+    sc, _ = case
+    p = sc.params
+    ref = oracle.simulate(p, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency)
+    ev = oracle.simulate(p, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True)
+    called = ("scaled", "noop", "failed")
+    prev = None
+    changes = 0
+    for e in ev:
+        if e.depth is None:
+            changes += 1  # a failed read: a prefetch sent with it is drained
+            continue
+        if prev is not None and _depth_class(e.depth, p) == _depth_class(prev, p):
+            assert e.prefetched == (e.up in called or e.down in called), e
+        elif prev is not None:
+            changes += 1
+        prev = e.depth
+    ref_gets = oracle.reference_gets(ref)
+    gated = sum(e.gets for e in ev)
+    if p.poll_ns >= 500 * MILLISECOND:  # same decisions as the reference (see below)
+        assert ref_gets <= gated <= ref_gets + changes + 1
 
 
 @settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])

@@ -89,10 +89,12 @@ def test_throttled_loop_keeps_reference_decisions(nat):
         env.close()
 
 
-def test_speculative_read_never_waits_for_the_throttle(nat):
-    """--pipeline-reads sends a GET with every poll, which the reference does not. Once the bucket
-    is empty the speculative GET is skipped rather than delayed, and only the reference's own
-    GET (when a decision needs one) waits."""
+@pytest.mark.parametrize("always", [True, False])
+def test_speculative_read_never_waits_for_the_throttle(nat, always):
+    """With prefetch_always a GET goes out with every poll, which the reference does not send.
+    Once the bucket is empty the speculative GET is skipped rather than delayed, and only the
+    reference's own GET (when a decision needs one) waits. The default gate sends none here:
+    no poll can get past its cool-down."""
     from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
 
     env = BenchEnv(1)
@@ -107,13 +109,17 @@ def test_speculative_read_never_waits_for_the_throttle(nat):
         cfg.scale_up_messages = 100
         cfg.scale_down_messages = 10
         cfg.prefetch = True
+        cfg.prefetch_always = always
         r = nat.Runner(cfg, env.runners[0].sqs, scaler, env.clock, env.log)
         r.arm()
         t0 = time.perf_counter()
         recs = [r.poll_once() for _ in range(20)]
         assert time.perf_counter() - t0 < 0.5  # no poll waited for a token
         st = api.stats()
-        assert sum(x["prefetched"] for x in recs) == 3 and st["speculative_skipped"] == 17
+        if always:
+            assert sum(x["prefetched"] for x in recs) == 3 and st["speculative_skipped"] == 17
+        else:
+            assert all(x["prefetch_gated"] and x["gets"] == 0 for x in recs) and st["gets"] == 0
         assert st["throttled"] == 0
     finally:
         env.close()
