@@ -574,7 +574,9 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("proxy", &KubeOptions::proxy)
       .def_readwrite("qps", &KubeOptions::qps)
       .def_readwrite("burst", &KubeOptions::burst)
-      .def_readwrite("clock", &KubeOptions::clock);
+      .def_readwrite("clock", &KubeOptions::clock)
+      .def_readwrite("rbac_fallback", &KubeOptions::rbac_fallback)
+      .def_readwrite("log", &KubeOptions::log);
   py::class_<TokenBucket>(m, "TokenBucket")
       .def(py::init<double, int, std::shared_ptr<Clock>>(), py::arg("qps"), py::arg("burst"), py::arg("clock"))
       .def("reserve", &TokenBucket::reserve)
@@ -601,6 +603,7 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<KubeRestDeployments, DeploymentApi, py::smart_holder>(m, "KubeRestDeployments")
       .def(py::init<KubeOptions>())
       .def("path_for", &KubeRestDeployments::path_for)
+      .def_property_readonly("mode", &KubeRestDeployments::mode)
       // the control loop's pipelined read (begin before the SQS call, finish after it)
       .def("begin_get", &KubeRestDeployments::begin_get, py::call_guard<py::gil_scoped_release>())
       .def("finish_get", [](KubeRestDeployments& k) {
@@ -622,6 +625,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["throttle_ns"] = s.throttle_ns;
         d["speculative_skipped"] = s.speculative_skipped;
         d["retry_after"] = s.retry_after;
+        d["scale_fallbacks"] = s.scale_fallbacks;
         d["http"] = http_stats_dict(s.http);
         return d;
       });
@@ -903,6 +907,8 @@ PYBIND11_MODULE(_ksa_native, m) {
            py::arg("gpus"), py::arg("unschedulable") = false)
       .def("inject", &FakeKubeServer::inject)
       .def("conflict_next", &FakeKubeServer::conflict_next)
+      .def("set_rbac", &FakeKubeServer::set_rbac)
+      .def("forbidden", &FakeKubeServer::forbidden)
       .def("set_latency", &FakeKubeServer::set_latency)
       .def("drop_connections", &FakeKubeServer::drop_connections)
       .def("requests", &FakeKubeServer::requests)

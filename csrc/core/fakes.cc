@@ -456,6 +456,11 @@ void FakeKubeServer::inject(int count, InjectedFault fault) {
   for (int i = 0; i < count; ++i) faults_.push_back(fault);
 }
 
+void FakeKubeServer::set_rbac(std::vector<std::string> rules) {
+  std::lock_guard<std::mutex> lk(mu_);
+  rbac_ = std::move(rules);
+}
+
 void FakeKubeServer::conflict_next(int n) {
   std::lock_guard<std::mutex> lk(mu_);
   conflict_ = n;
@@ -611,6 +616,26 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
   const std::string& ns = parts[0];
   const std::string& name = parts[2];
   const bool scale = parts.size() == 4;
+  {
+    // authorization runs before the handler: a forbidden request is 403 whether or not the
+    // object exists
+    const std::string verb = req.method == "GET" ? "get" : req.method == "PUT" ? "update" : req.method == "PATCH" ? "patch" : "";
+    const std::string resource = scale ? "deployments/scale" : "deployments";
+    bool allowed;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      allowed = std::find(rbac_.begin(), rbac_.end(), "*") != rbac_.end() ||
+                std::find(rbac_.begin(), rbac_.end(), resource + ":" + verb) != rbac_.end();
+    }
+    if (!verb.empty() && !allowed) {
+      forbidden_++;
+      fail(403, "Forbidden",
+           "deployments.apps \"" + name + "\" is forbidden: User \"system:serviceaccount:" + ns +
+               ":kube-sqs-autoscaler\" cannot " + verb + " resource \"" + resource +
+               "\" in API group \"apps\" in the namespace \"" + ns + "\"");
+      return;
+    }
+  }
   // Critical sections cover only the object state; rendering happens outside the lock so
   // concurrent workers are not serialised by the fake (a real apiserver serves them in parallel).
   Obj snapshot;

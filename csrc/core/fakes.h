@@ -107,6 +107,11 @@ class FakeKubeServer {
   void conflict_next(int n);
   void set_latency(Nanos per_request);
   void drop_connections();
+  // RBAC of the caller on Deployments: "resource:verb" rules, e.g. {"deployments:get",
+  // "deployments:update"} (a Role written for the reference) or "deployments/scale:patch";
+  // "*" allows everything (the default). A request outside them gets the apiserver's 403.
+  void set_rbac(std::vector<std::string> rules);
+  uint64_t forbidden() const { return forbidden_.load(); }
 
   // coordination.k8s.io/v1 Leases (leader election): raw JSON objects with resourceVersion
   // optimistic concurrency; POST creates (409 AlreadyExists), PUT replaces (409 Conflict).
@@ -158,12 +163,13 @@ class FakeKubeServer {
   void handle_nodes(const std::string& query, HttpResponse* resp);
   void handle_lease(const HttpRequest& req, const std::vector<std::string>& parts, HttpResponse* resp);
   std::string token_;
+  std::vector<std::string> rbac_{"*"};
   std::vector<InjectedFault> faults_;
   int conflict_ = 0;
   Nanos latency_ = 0;
   uint64_t rv_counter_ = 5000;
   std::string last_method_, last_body_, last_path_;
-  std::atomic<uint64_t> requests_{0}, gets_{0}, writes_{0}, conflicts_{0}, auth_failures_{0};
+  std::atomic<uint64_t> requests_{0}, gets_{0}, writes_{0}, conflicts_{0}, auth_failures_{0}, forbidden_{0};
 };
 
 }  // namespace ksa

@@ -129,7 +129,8 @@ Result<std::string> set_spec_replicas(const std::string& raw, int32_t replicas) 
 // ---------------------------------------------------------------------------------------
 // REST client
 
-KubeRestDeployments::KubeRestDeployments(KubeOptions opts) : opts_(std::move(opts)) {
+KubeRestDeployments::KubeRestDeployments(KubeOptions opts)
+    : mode_(static_cast<int>(opts.mode)), opts_(std::move(opts)) {
   auto u = parse_url(opts_.server);
   if (!u.ok()) {
     init_status_ = u.status;
@@ -168,12 +169,14 @@ KubeStats KubeRestDeployments::stats() const {
   return s;
 }
 
-std::string KubeRestDeployments::path_for(const std::string& name) const {
+std::string KubeRestDeployments::path_for(const std::string& name) const { return path_in(mode(), name); }
+
+std::string KubeRestDeployments::path_in(ScaleMode m, const std::string& name) const {
   std::string base = url_.path;
   while (!base.empty() && base.back() == '/') base.pop_back();
   std::string p = base + "/apis/apps/v1/namespaces/" + aws_uri_encode(opts_.namespace_, false) +
                   "/deployments/" + aws_uri_encode(name, false);
-  if (opts_.mode != ScaleMode::Deployment) p += "/scale";
+  if (m != ScaleMode::Deployment) p += "/scale";
   return p;
 }
 
@@ -322,20 +325,48 @@ Status KubeRestDeployments::do_request(const std::string& verb_desc, HttpRequest
   }
 }
 
-Result<ScaleObject> KubeRestDeployments::parse_get(const Status& s, const HttpResponse& resp) {
+Result<ScaleObject> KubeRestDeployments::parse_get(ScaleMode m, const Status& s, const HttpResponse& resp) {
   if (!s.ok()) {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.errors++;
     return Result<ScaleObject>::Err(s);
   }
-  return parse_scale_object(resp.body, opts_.mode != ScaleMode::Deployment);
+  return parse_scale_object(resp.body, m != ScaleMode::Deployment);
+}
+
+bool KubeRestDeployments::try_fallback(const Status& s, const std::string& name,
+                                       Result<ScaleObject>* deployment) {
+  if (!opts_.rbac_fallback || mode() == ScaleMode::Deployment) return false;
+  // 403: RBAC refuses deployments/scale. 404 only when it names no object -- the route is
+  // missing ("the server could not find the requested resource"), not the Deployment.
+  const bool missing_route =
+      s.code() == 404 && s.message().rfind("the server could not find the requested resource", 0) == 0;
+  if (s.code() != 403 && !missing_route) return false;
+  // Can the Deployment itself be read? If not, the /scale error stands and the mode is kept.
+  auto d = get_in(ScaleMode::Deployment, name);
+  if (!d.ok()) return false;
+  int expected = mode_.load(std::memory_order_acquire);
+  if (expected != static_cast<int>(ScaleMode::Deployment) &&
+      mode_.compare_exchange_strong(expected, static_cast<int>(ScaleMode::Deployment))) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.scale_fallbacks++;
+    }
+    if (opts_.log)
+      opts_.log->warn("The deployments/scale subresource is not usable (" + s.message() +
+                      "); scaling " + opts_.namespace_ + "/" + name +
+                      " with GET+PUT of the whole Deployment, as the reference does");
+  }
+  *deployment = std::move(d);
+  return true;
 }
 
 bool KubeRestDeployments::begin_get(const std::string& name) {
   if (!init_status_.ok() || name.empty() || http_->in_flight()) return false;
   HttpRequest req;
   req.method = "GET";
-  req.target = path_for(name);
+  const ScaleMode m = mode();
+  req.target = path_in(m, name);
   if (!add_auth(&req).ok()) return false;
   // A speculative read never waits for the throttle: without a free token it is skipped and
   // the decision (if any) does the reference's own throttled GET. So the extra reads of
@@ -351,6 +382,7 @@ bool KubeRestDeployments::begin_get(const std::string& name) {
     stats_.gets++;
   }
   pending_name_ = name;
+  pending_mode_ = m;
   pending_req_ = std::move(req);
   return true;
 }
@@ -369,21 +401,31 @@ Result<ScaleObject> KubeRestDeployments::finish_get() {
     }
     return get(pending_name_);
   }
-  return parse_get(check_response("get", pending_req_, resp, pending_name_, t), resp);
+  auto r = parse_get(pending_mode_, check_response("get", pending_req_, resp, pending_name_, t), resp);
+  Result<ScaleObject> d;
+  if (!r.ok() && try_fallback(r.status, pending_name_, &d)) return d;
+  return r;
 }
 
-Result<ScaleObject> KubeRestDeployments::get(const std::string& name) {
-  if (!init_status_.ok()) return Result<ScaleObject>::Err(init_status_);
-  if (name.empty()) return Result<ScaleObject>::Err(Status::Err("resource name may not be empty"));
+Result<ScaleObject> KubeRestDeployments::get_in(ScaleMode m, const std::string& name) {
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.gets++;
   }
   HttpRequest req;
   req.method = "GET";
-  req.target = path_for(name);
+  req.target = path_in(m, name);
   HttpResponse resp;
-  return parse_get(do_request("get", &req, &resp, name), resp);
+  return parse_get(m, do_request("get", &req, &resp, name), resp);
+}
+
+Result<ScaleObject> KubeRestDeployments::get(const std::string& name) {
+  if (!init_status_.ok()) return Result<ScaleObject>::Err(init_status_);
+  if (name.empty()) return Result<ScaleObject>::Err(Status::Err("resource name may not be empty"));
+  auto r = get_in(mode(), name);
+  Result<ScaleObject> d;
+  if (!r.ok() && try_fallback(r.status, name, &d)) return d;
+  return r;
 }
 
 Status KubeRestDeployments::update(const std::string& name, const ScaleObject& fetched,
@@ -394,9 +436,10 @@ Status KubeRestDeployments::update(const std::string& name, const ScaleObject& f
     std::lock_guard<std::mutex> lk(mu_);
     stats_.updates++;
   }
+  const ScaleMode m = mode();
   HttpRequest req;
-  req.target = path_for(name);
-  if (opts_.mode == ScaleMode::Patch) {
+  req.target = path_in(m, name);
+  if (m == ScaleMode::Patch) {
     req.method = "PATCH";
     req.headers.emplace_back("Content-Type", "application/merge-patch+json");
     req.body = "{\"metadata\":{\"resourceVersion\":" + json_quote(fetched.resource_version) +
@@ -411,8 +454,25 @@ Status KubeRestDeployments::update(const std::string& name, const ScaleObject& f
   HttpResponse resp;
   Status s = do_request("update", &req, &resp, name);
   if (!s.ok()) {
-    std::lock_guard<std::mutex> lk(mu_);
-    stats_.errors++;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.errors++;
+    }
+    // The Role may grant get on deployments/scale but not update: write through the Deployment
+    // instead, provided it is still the object that was read (the Scale carries the
+    // Deployment's resourceVersion), else report the conflict the write would have had.
+    Result<ScaleObject> d;
+    if (m != ScaleMode::Deployment && try_fallback(s, name, &d)) {
+      if (d.value.resource_version != fetched.resource_version) {
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.conflicts++;
+        return Status::Err("Operation cannot be fulfilled on deployments.apps \"" + name +
+                               "\": the object has been modified; please apply your changes to the latest "
+                               "version and try again",
+                           409);
+      }
+      return update(name, d.value, replicas);
+    }
   }
   return s;
 }

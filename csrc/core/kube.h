@@ -12,6 +12,8 @@
 //                            default, per BASELINE.json) uses the autoscaling/v1 /scale
 //                            subresource (smaller payloads, narrower RBAC); ScaleMode::Patch
 //                            sends a JSON merge patch with a resourceVersion precondition.
+//                            When RBAC refuses /scale (a Role written for the reference) the
+//                            client falls back to ScaleMode::Deployment once and for all.
 //   * FakeDeployments     -- in-memory object tracker (the fake clientset the reference tests
 //                            use, scale_test.go:85-115) with latency and fault injection.
 //   * PodAutoScaler       -- ScaleUp/ScaleDown with the reference's int32 clamp arithmetic and
@@ -132,6 +134,12 @@ struct KubeOptions {
   double qps = 0;
   int burst = 0;
   std::shared_ptr<Clock> clock;  // for the throttle's waits (null: RealClock)
+  // Scale/Patch modes: when the apiserver refuses the /scale subresource (403: a Role written
+  // for the reference grants only get/update on `deployments`, /root/reference/scale/scale.go:55,72;
+  // 404: no such subresource) but the Deployment itself can be read, switch this client to
+  // Mode::Deployment for good -- the reference's full-object GET+PUT -- and log one warning.
+  bool rbac_fallback = true;
+  std::shared_ptr<Logger> log;  // for that warning (null: none)
 };
 
 struct KubeStats {
@@ -143,6 +151,7 @@ struct KubeStats {
   int64_t throttle_ns = 0;    // total time spent waiting
   uint64_t speculative_skipped = 0;  // pipelined GETs not sent: no throttle token free
   uint64_t retry_after = 0;          // client-go style retries (Retry-After, or a reset GET)
+  uint64_t scale_fallbacks = 0;      // switches from /scale to the whole Deployment (0 or 1)
   HttpClientStats http;
 };
 
@@ -156,8 +165,15 @@ class KubeRestDeployments final : public DeploymentApi {
   KubeStats stats() const;
   void cancel() override;
   std::string path_for(const std::string& name) const;
+  ScaleMode mode() const { return static_cast<ScaleMode>(mode_.load(std::memory_order_acquire)); }
 
  private:
+  std::string path_in(ScaleMode m, const std::string& name) const;
+  Result<ScaleObject> get_in(ScaleMode m, const std::string& name);
+  // A /scale request failed with `s`: read the Deployment; when that works, switch to
+  // Mode::Deployment (once, with a warning) and return it, else return nothing.
+  bool try_fallback(const Status& s, const std::string& name, Result<ScaleObject>* deployment);
+  std::atomic<int> mode_;
   // Seconds client-go would wait before retrying this outcome (rest.Request.request, checkWait):
   // the integer Retry-After of a 429 / 5xx response, or 1 for a GET whose connection was reset
   // or hit EOF; -1 = do not retry.
@@ -168,8 +184,9 @@ class KubeRestDeployments final : public DeploymentApi {
   Status add_auth(HttpRequest* req);
   Status check_response(const std::string& verb_desc, const HttpRequest& req, const HttpResponse& resp,
                         const std::string& name, const Status& transport);
-  Result<ScaleObject> parse_get(const Status& s, const HttpResponse& resp);
+  Result<ScaleObject> parse_get(ScaleMode m, const Status& s, const HttpResponse& resp);
   std::string pending_name_;
+  ScaleMode pending_mode_ = ScaleMode::Scale;
   HttpRequest pending_req_;
   Status pending_status_;
 

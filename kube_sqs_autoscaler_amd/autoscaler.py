@@ -139,11 +139,13 @@ def new_http_client(rc: RestConfig, timeout_ns: int, environ: Optional[Mapping[s
 
 def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", timeout_ns: int = 30 * SECOND, clock=None,
                        busy_poll_ns: int = 0, environ: Optional[Mapping[str, str]] = None, qps: float = 0.0,
-                       burst: int = 0):
+                       burst: int = 0, logger=None, rbac_fallback: bool = True):
     """The ``DeploymentInterface`` seam over REST (/root/reference/scale/scale.go:44).
 
     ``qps``/``burst``: the client-side throttle of this client (client-go's clientset default is
-    5/10, which the CLI passes; 0 leaves it unthrottled)."""
+    5/10, which the CLI passes; 0 leaves it unthrottled). ``rbac_fallback``: in ``scale``/``patch``
+    mode, switch to the reference's whole-Deployment GET+PUT when the apiserver refuses the
+    ``/scale`` subresource (a Role written for the reference), warning once on ``logger``."""
     nat = native()
     o = nat.KubeOptions()
     o.server = rc.host
@@ -163,6 +165,9 @@ def new_deployment_api(rc: RestConfig, namespace: str, mode: str = "scale", time
         o.token = tp
     o.basic_user = rc.username
     o.basic_password = rc.password
+    o.rbac_fallback = rbac_fallback
+    if logger is not None:
+        o.log = logger
     return nat.KubeRestDeployments(o)
 
 
@@ -231,7 +236,7 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
         log = base_logger.with_fields([("deployment", target.name), ("queue", target.queue_url)])
     kube_api = new_deployment_api(rest, target.namespace, cfg.scale_mode, cfg.api_timeout_ns, clock,
                                   busy_poll_ns=cfg.busy_poll_ns, environ=environ, qps=cfg.kube_api_qps,
-                                  burst=cfg.kube_api_burst)
+                                  burst=cfg.kube_api_burst, logger=log)
     scaler = new_pod_autoscaler(target, kube_api, log, clock)
     scaler.dry_run = cfg.dry_run
     sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,

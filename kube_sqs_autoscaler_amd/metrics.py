@@ -52,6 +52,8 @@ _API_COUNTERS = [
      "speculative_skipped"),
     ("apiserver_retries", "kube-apiserver requests retried after Retry-After (429/5xx) or a reset GET", "kube_api",
      "retry_after"),
+    ("apiserver_scale_fallbacks", "Switches from the /scale subresource to whole-Deployment GET+PUT (RBAC refused /scale)",
+     "kube_api", "scale_fallbacks"),
 ]
 _NS_COUNTERS = {"throttle_ns"}  # exported in seconds
 

@@ -107,6 +107,35 @@ def test_deployment_mode_full_object_put(servers):
     assert kube.last_method() == "PUT" and kube.last_path().endswith("/deployments/workers")
 
 
+REFERENCE_ROLE = ["deployments:get", "deployments:update"]  # all /root/reference/scale/scale.go:55,72 needs
+
+
+@pytest.mark.parametrize("rules", [REFERENCE_ROLE, REFERENCE_ROLE + ["deployments/scale:get"]],
+                         ids=["reference-role", "scale-read-only"])
+def test_default_flags_scale_under_a_reference_role(servers, capfd, rules):
+    """A cluster whose Role was written for the reference (get/update on deployments only) is
+    scaled with default flags: the first /scale request is refused (403), the worker warns once
+    and continues with the reference's full-Deployment GET+PUT."""
+    from kube_sqs_autoscaler_amd.cli import main
+
+    sqs, kube, env = servers
+    kube.set_rbac(rules)
+    url = sqs.url + "/123/jobs"
+    sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500", "ApproximateNumberOfMessagesDelayed": "0",
+                             "ApproximateNumberOfMessagesNotVisible": "0"})
+    kube.add_deployment("gpu", "workers", 1)
+    rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=workers", "--kubernetes-namespace=gpu",
+               f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+               "--scale-down-cool-down=0s"], environ=env, max_iterations=10)
+    assert rc == 0
+    assert kube.replicas("gpu", "workers") == 8
+    err = capfd.readouterr().err
+    assert err.count("level=warning") >= 1 and err.count("deployments/scale subresource is not usable") == 1
+    assert "Failed scaling" not in err
+    assert 1 <= kube.forbidden() <= 2  # the refused /scale GET (or PUT) -- once, then never again
+    assert kube.last_path().endswith("/deployments/workers")  # no /scale request after the switch
+
+
 def test_sigterm_graceful_shutdown(servers):
     sqs, kube, env = servers
     url = sqs.url + "/123/jobs"

@@ -408,3 +408,53 @@ def test_sqs_throttle_honours_retry_after(nat, sqs_server, status, header, extra
     waited = clock.now() - t0
     assert extra_s * 10**9 + 1_000_000 <= waited < extra_s * 10**9 + 2_000_000
     assert api.stats()["throttle_retries"] == 1
+
+
+@pytest.mark.parametrize("mode", ["scale", "patch"])
+def test_scale_subresource_forbidden_falls_back_to_deployment(nat, kube_server, mode):
+    kube_server.set_rbac(["deployments:get", "deployments:update"])
+    lines = []
+    p, api = scaler(nat, kube_server, mode, lines=lines)
+    assert p.prefetch()  # the pipelined /scale GET is refused too
+    span = p.scale_up()
+    assert span.wrote and kube_server.replicas("ml", "worker") == 4
+    assert str(api.mode) == "ScaleMode.Deployment" and api.stats()["scale_fallbacks"] == 1
+    p.scale_up()
+    assert kube_server.replicas("ml", "worker") == 5 and api.stats()["scale_fallbacks"] == 1
+    assert kube_server.last_path().endswith("/deployments/worker") and kube_server.last_method() == "PUT"
+
+
+def test_scale_write_forbidden_writes_through_the_deployment(nat, kube_server):
+    """GET on deployments/scale allowed, update not: the write goes through the Deployment when
+    it is still the object that was read (same resourceVersion)."""
+    kube_server.set_rbac(["deployments:get", "deployments:update", "deployments/scale:get"])
+    p, api = scaler(nat, kube_server, "scale")
+    span = p.scale_up()
+    assert span.wrote and kube_server.replicas("ml", "worker") == 4 and kube_server.forbidden() == 1
+    assert api.stats()["scale_fallbacks"] == 1
+
+
+def test_missing_deployment_keeps_scale_mode(nat, kube_server):
+    """A 404 from /scale because the Deployment does not exist is an error, not a fallback."""
+    api = new_deployment_api(RestConfig(host=kube_server.url, bearer_token=TOKEN), "ml", "scale")
+    p = nat.PodAutoScaler(api, "ghost", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+    with pytest.raises(nat.NativeError, match='deployments.apps "ghost" not found'):
+        p.scale_up()
+    assert str(api.mode) == "ScaleMode.Scale" and api.stats()["scale_fallbacks"] == 0
+
+
+def test_fallback_can_be_disabled(nat, kube_server):
+    kube_server.set_rbac(["deployments:get", "deployments:update"])
+    api = new_deployment_api(RestConfig(host=kube_server.url, bearer_token=TOKEN), "ml", "scale", rbac_fallback=False)
+    p = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+    with pytest.raises(nat.NativeError, match='cannot get resource "deployments/scale"'):
+        p.scale_up()
+
+
+def test_missing_scale_route_falls_back(nat, kube_server):
+    """A 404 that names no object (no /scale route on this apiserver) switches to the
+    Deployment once the Deployment itself reads fine."""
+    p, api = scaler(nat, kube_server, "scale")
+    kube_server.inject(1, nat.InjectedFault(404, "404 page not found"))
+    assert p.scale_up().wrote and kube_server.replicas("ml", "worker") == 4
+    assert api.stats()["scale_fallbacks"] == 1

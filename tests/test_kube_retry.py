@@ -50,7 +50,7 @@ def test_retry_after_on_429_then_success(nat, kube):
     (503, "3", True), (500, "0", True), (429, "+2", True),
     (503, "", False),  # no header
     (500, "Wed, 21 Oct 2015 07:28:00 GMT", False),  # strconv.Atoi fails: not retried
-    (404, "1", False),  # only 429 and 5xx wait
+    (400, "1", False),  # only 429 and 5xx wait (a 404 on /scale may switch to the Deployment instead)
 ])
 def test_check_wait_rules(nat, kube, status, retry_after, retried):
     clock = nat.VirtualClock()
