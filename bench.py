@@ -8,7 +8,9 @@ number (BASELINE.json ``published: {}``), so ``vs_baseline`` is null.
 One rank per GPU (``torch.distributed``; backend ``nccl`` = RCCL on ROCm when a GPU is present,
 ``gloo`` otherwise). Each rank is one autoscaler process tracking ``--queues`` queues (default
 1) against its own localhost fake SQS + fake kube-apiserver, so the job tracks
-``N x queues`` queues in total (weak scaling). A "step" is one control-loop iteration on every
+``N x queues`` queues in total (weak scaling). The ranks share nothing while timed -- each is an
+independent control-plane process, as N reference deployments would be; the collective
+(``all_gather``) only pools the latency samples for the job-wide p50 afterwards. A "step" is one control-loop iteration on every
 tracked queue: SigV4-signed SQS GetQueueAttributes -> Deployment GET -> replica write (the trace
 alternates 200/0 messages, so every iteration scales). K timed steps are bracketed by a barrier
 + ``torch.cuda.synchronize()``; ``value`` is the p50 over every sample of every rank.
@@ -30,16 +32,33 @@ METRIC = "poll→scale-patch p50 latency (ms); decision parity vs ref on synthet
 
 
 def _parity_summary() -> dict:
-    from kube_sqs_autoscaler_amd.models import parity, traces
+    """Decision parity of the timed configuration: the five Appendix C scenarios through the
+    production wire path (SigV4 HttpSqsApi + KubeRestDeployments over HTTP to the fakes, VirtualClock),
+    poll by poll against the reference-semantics oracle -- for the default (pipelined /scale, the
+    timed row), strictly sequential /scale, the reference-equivalent full-Deployment GET+PUT, and
+    round 1's speculative GET on every poll (for its apiserver traffic)."""
+    from kube_sqs_autoscaler_amd.models import parity
 
-    out = {}
+    wire = parity.wire_summary()
     agree = total = 0
-    for sc in traces.baseline_scenarios():
-        r = parity.compare(sc)
-        out[sc.name] = f"{r.agree}/{r.polls}"
-        agree += r.agree
-        total += r.polls
-    out["fraction"] = agree / total if total else 1.0
+    for row in wire.values():
+        a, b = row["agree"].split("/")
+        agree, total = agree + int(a), total + int(b)
+    return {"path": "wire: HttpSqsApi + KubeRestDeployments -> FakeSqsServer/FakeKubeServer, VirtualClock, zero-latency oracle",
+            "fraction": agree / total if total else 1.0, "configs": wire}
+
+
+def _apiserver_requests_per_poll(wire: dict) -> dict:
+    """Per scenario, kube-apiserver requests per poll (GETs + writes) for each config, next to
+    the reference's own count on the same trace."""
+    out = {}
+    for key, row in wire["configs"].items():
+        for sc, r in row["scenarios"].items():
+            out.setdefault(sc, {})[key] = r["apiserver_requests_per_poll"]
+    for sc in out:
+        r = wire["configs"]["deployment"]["scenarios"][sc]
+        polls = int(r["agree"].split("/")[1])
+        out[sc]["reference"] = round((r["reference_gets"] + r["writes"]) / polls, 4)
     return out
 
 
@@ -57,6 +76,8 @@ def main(argv=None) -> int:
                     help="fake SQS/apiserver: one pair for all of this rank's queues, or one pair per queue")
     ap.add_argument("--loggers", default="shared", choices=["shared", "per-queue"],
                     help="one logrus-style logger for the rank (as the reference's global logger) or one per queue")
+    ap.add_argument("--secondary-samples", type=int, default=2000,
+                    help="samples per queue for every secondary row (independent of --steps)")
     args = ap.parse_args(argv)
 
     import torch
@@ -145,7 +166,7 @@ def main(argv=None) -> int:
         if world == 1 and not args.no_sweep:
             # Secondary rows: three interleaved rounds, median p50 per row, so one disturbed run
             # (CPU migration, a noisy neighbour) cannot invert the comparison.
-            n, w = min(args.steps, 2000), min(args.warmup, 200)
+            n, w = args.secondary_samples, 200
             rows = {f"q{q}": (q, args.mode, pipeline, bp, False, "shared") for q in (1, 2, 4, 8)}
             # 8 queues, each against its own fake SQS + apiserver pair (what 8 ranks see): the
             # single-process fakes serialise on their own state lock, real endpoints do not.
@@ -156,10 +177,12 @@ def main(argv=None) -> int:
             rows["tls"] = (1, args.mode, pipeline, bp, True, "shared")
             rows["reference_tls"] = (1, "deployment", False, 0, True, "shared")
             p50s = {k: [] for k in rows}
+            samples = {k: [] for k in rows}
             for _ in range(3):
                 for k, (q, mode, pl, b, tls, sv) in rows.items():
-                    p50s[k].append(measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls,
-                                           servers=sv).summary()["p50_ms"])
+                    sm = measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls, servers=sv).summary()
+                    p50s[k].append(sm["p50_ms"])
+                    samples[k].append(sm["samples"])
             med = {k: sorted(v)[1] for k, v in p50s.items()}
             extra["p50_ms_by_tracked_queues"] = {str(q): med[f"q{q}"] for q in (1, 2, 4, 8)}
             extra["p50_ms_8_queues_per_queue_endpoints"] = med["q8_per_queue_endpoints"]
@@ -167,6 +190,7 @@ def main(argv=None) -> int:
             extra["reference_equivalent_p50_ms"] = med["reference"]
             extra["tls_p50_ms"] = {"default": med["tls"], "reference_equivalent": med["reference_tls"]}
             extra["secondary_rows_p50_ms_all_rounds"] = p50s
+            extra["secondary_rows_samples_per_round"] = samples
             # Regional-RTT model: the fakes add 2 ms (SQS) / 1 ms (apiserver) per request, so the
             # structural round-trip savings show at production scale (200 polls each).
             wan = {}
@@ -174,6 +198,7 @@ def main(argv=None) -> int:
                 r = measure(1, 200, 5, mode, pipeline=pl, sqs_latency_ns=2_000_000, kube_latency_ns=1_000_000)
                 wan[name] = r.summary()["p50_ms"]
             extra["wan_model_sqs2ms_kube1ms_p50_ms"] = wan
+            extra["wan_model_samples"] = 200
             from kube_sqs_autoscaler_amd.bench.latency import phase_breakdown
 
             extra["phase_median_us"] = {
@@ -181,6 +206,7 @@ def main(argv=None) -> int:
                 "reference_equivalent": phase_breakdown(mode="deployment", pipeline=False),
             }
         extra["decision_parity"] = _parity_summary()
+        extra["apiserver_requests_per_poll"] = _apiserver_requests_per_poll(extra["decision_parity"])
         out = {
             "metric": METRIC,
             "value": round(p50, 4),
@@ -193,9 +219,12 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",  # control-plane service: no tensor compute (BASELINE.json north_star)
-            "data": "synthetic: 200/0 step trace served by localhost fake SQS + fake kube-apiserver (SigV4 + bearer auth verified)",
+            "data": "synthetic: every poll alternates 200 / 0 messages, served by localhost fake SQS + fake kube-apiserver (SigV4 + bearer auth verified)",
             "config": {
-                "model": "kube-sqs-autoscaler control loop (single queue step trace 0->200->0, scale-up-messages=100 / scale-down-messages=10, min 1 / max 8)",
+                "model": "kube-sqs-autoscaler control loop, scaling path: depth alternates 200/0 on every poll with "
+                         "poll-period=0 and both cool-downs 0, scale-up-messages=100 / scale-down-messages=10, "
+                         "min 1 / max 8, so every poll does SQS GetQueueAttributes + Deployment GET + /scale write "
+                         f"({args.mode} mode{', pipelined read' if pipeline else ''})",
                 "global_batch": args.queues * world,
                 "seq_len": 1,
                 "parallelism": f"dp{world}",
