@@ -161,6 +161,7 @@ py::dict http_stats_dict(const HttpClientStats& s) {
   d["connects"] = s.connects;
   d["tls_resumptions"] = s.tls_resumptions;
   d["reconnect_retries"] = s.reconnect_retries;
+  d["idle_closed"] = s.idle_closed;
   d["bytes_out"] = s.bytes_out;
   d["bytes_in"] = s.bytes_in;
   return d;

@@ -206,8 +206,15 @@ class Stream {
     }
   }
 
-  Status write_all(const std::string& data, int64_t deadline_ns) {
+  Status write_all(const std::string& data, int64_t deadline_ns, size_t* written = nullptr) {
     size_t off = 0;
+    struct Report {
+      size_t* w;
+      size_t& off;
+      ~Report() {
+        if (w) *w = off;
+      }
+    } report{written, off};
     while (off < data.size()) {
       if (ssl_) {
         int n = 0;
@@ -233,6 +240,29 @@ class Stream {
       return Status::Err(std::string("write: ") + std::strerror(errno));
     }
     return Status::OK();
+  }
+
+  // An idle keep-alive connection about to be reused: has the peer closed it (FIN, RST, a TLS
+  // close_notify) or sent something unsolicited? Go's transport learns this from the idle
+  // connection's read loop and dials a new one instead of writing into a dead socket; here the
+  // socket is peeked without blocking. TLS records that carry no application data (session
+  // tickets) are consumed by the peek and leave the connection usable.
+  bool peer_closed() {
+    if (ssl_) {
+      char c;
+      ERR_clear_error();
+      const int n = SSL_peek(ssl_, &c, 1);
+      if (n > 0) return true;  // unsolicited response bytes: the connection is out of sync
+      const int e = SSL_get_error(ssl_, n);
+      return !(e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE);
+    }
+    char c;
+    while (true) {
+      const ssize_t n = ::recv(fd_, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+      if (n >= 0) return true;  // 0: orderly close; > 0: unsolicited bytes
+      if (errno == EINTR) continue;
+      return !(errno == EAGAIN || errno == EWOULDBLOCK);
+    }
   }
 
   void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
@@ -1025,8 +1055,25 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   return Status::OK();
 }
 
+namespace {
+
+// Go's Request.isReplayable: a request the transport may send again after it was written
+// (net/http transport.go). Writes (PUT/PATCH/POST) are not: the first copy may have been
+// applied, and a second resourceVersion-checked PUT would then fail with 409.
+bool replayable(const HttpRequest& req) {
+  if (req.method == "GET" || req.method == "HEAD" || req.method == "OPTIONS" || req.method == "TRACE")
+    return true;
+  return has_header(req.headers, "Idempotency-Key") || has_header(req.headers, "X-Idempotency-Key");
+}
+
+}  // namespace
+
 Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable) {
   *retryable = false;
+  if (conn_ && conn_->uses > 0 && conn_->stream->peer_closed()) {
+    stats_.idle_closed++;
+    conn_.reset();  // closed while idle: dial a fresh one (the request was never sent)
+  }
   if (!conn_) {
     Status s = connect_locked(deadline_ns);
     if (!s.ok()) return s;
@@ -1053,9 +1100,12 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   wire += "\r\n";
   wire += req.body;
 
-  Status s = conn_->stream->write_all(wire, deadline_ns);
+  size_t written = 0;
+  Status s = conn_->stream->write_all(wire, deadline_ns, &written);
   if (!s.ok()) {
-    *retryable = reused && s.message() != "i/o timeout";
+    // Go's transport retries a request that never reached the wire (nothingWrittenError), and
+    // a partly written one only if it is replayable.
+    *retryable = reused && s.message() != "i/o timeout" && (written == 0 || replayable(req));
     conn_.reset();
     return s;
   }
@@ -1088,7 +1138,8 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   while (true) {
     s = rd.read_head(&head, deadline_ns, &got_any);
     if (!s.ok()) {
-      *retryable = reused && !got_any && s.message() != "i/o timeout";
+      // The whole request was written: only a replayable one may be sent again.
+      *retryable = reused && !got_any && s.message() != "i/o timeout" && replayable(req);
       conn_.reset();
       return s;
     }

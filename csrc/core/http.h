@@ -70,6 +70,7 @@ struct HttpClientStats {
   uint64_t connects = 0;
   uint64_t tls_resumptions = 0;  // reconnects that resumed the previous TLS session
   uint64_t reconnect_retries = 0;
+  uint64_t idle_closed = 0;  // reused connections found closed by the peer before a write
   uint64_t bytes_out = 0;
   uint64_t bytes_in = 0;
 };
@@ -84,9 +85,11 @@ class HttpClient {
   HttpClient& operator=(const HttpClient&) = delete;
 
   // Sends `req` (Host / Content-Length / User-Agent added when absent) and reads the full
-  // response. Reuses the connection; if a reused connection turns out to be dead before any
-  // response byte arrived, reconnects and retries once (what Go's transport does for
-  // requests that are safe to replay).
+  // response. Reuses the connection unless the peer closed it while idle (then dials anew).
+  // If a reused connection dies before any response byte arrived, reconnects and retries once
+  // -- as Go's transport does, only for a request that never reached the wire or is
+  // replayable (GET/HEAD/OPTIONS/TRACE or an Idempotency-Key): a PUT/PATCH/POST that was
+  // written is never sent twice.
   Status round_trip(const HttpRequest& req, HttpResponse* resp);
   // Pipelined use: send() writes the request and returns at once; receive() reads its
   // response. Between the two the caller is free to do other I/O -- the control loop sends the

@@ -101,3 +101,46 @@ def test_pipelined_read_falls_back_to_a_retried_get(nat, kube):
     assert api.begin_get("w")
     obj = api.finish_get()
     assert obj.replicas == 1 and api.stats()["retry_after"] == 1
+
+
+def test_written_put_on_a_reused_connection_is_never_replayed(nat, kube):
+    """a PUT fully written on a reused keep-alive connection that then closes without
+    a response byte must not be sent again (Go's transport replays only requests that never
+    reached the wire or are idempotent; client-go never retries a write on EOF). A replay could
+    apply the write twice, or 409 on its own first copy and skip the cool-down refresh."""
+    clock = nat.VirtualClock()
+    api, _, _ = scaler(nat, kube, clock)
+    obj = api.get("w")  # the connection is now reused
+    before = kube.requests()
+    kube.inject(1, nat.InjectedFault(0, "", "text/plain", True))  # the PUT's connection closes unanswered
+    with pytest.raises(nat.NativeError, match="EOF|closed|reset"):
+        api.update("w", obj, 4)
+    assert kube.requests() - before == 1  # exactly one write on the wire
+    assert api.stats()["http"]["reconnect_retries"] == 0 and api.stats()["retry_after"] == 0
+
+
+def test_reused_get_dropped_is_replayed_at_once(nat, kube):
+    clock = nat.VirtualClock()
+    api, _, _ = scaler(nat, kube, clock)
+    api.get("w")
+    kube.inject(1, nat.InjectedFault(0, "", "text/plain", True))
+    t0 = clock.now()
+    assert api.get("w").replicas == 1
+    st = api.stats()
+    assert st["http"]["reconnect_retries"] == 1 and st["retry_after"] == 0 and clock.now() == t0
+
+
+def test_idle_closed_connection_is_redialled_before_writing(nat, kube):
+    """The apiserver closed the idle keep-alive connection between polls: the next request --
+    a PUT included -- goes out on a fresh connection, never into the dead one."""
+    import time
+
+    clock = nat.VirtualClock()
+    api, _, _ = scaler(nat, kube, clock)
+    obj = api.get("w")
+    kube.drop_connections()
+    time.sleep(0.02)  # let the FIN arrive
+    api.update("w", obj, 3)
+    assert kube.replicas("ml", "w") == 3
+    st = api.stats()["http"]
+    assert st["idle_closed"] == 1 and st["reconnect_retries"] == 0 and st["connects"] == 2
