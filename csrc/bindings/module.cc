@@ -367,7 +367,7 @@ PYBIND11_MODULE(_ksa_native, m) {
            py::arg("origin"), py::arg("tls") = TlsOptions(), py::arg("timeout_ns") = 30 * kSecond)
       .def("request",
            [](HttpClient& c, const std::string& method, const std::string& target, py::object headers,
-              py::bytes body) {
+              py::bytes body, Nanos timeout) {
              HttpRequest req;
              req.method = method;
              req.target = target;
@@ -377,12 +377,13 @@ PYBIND11_MODULE(_ksa_native, m) {
              Status s;
              {
                py::gil_scoped_release rel;
-               s = c.round_trip(req, &resp);
+               s = c.round_trip(req, &resp, timeout);
              }
              if (!s.ok()) raise_status(s);
              return py::make_tuple(resp.status, resp.headers, py::bytes(resp.body));
            },
-           py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""))
+           py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""),
+           py::arg("timeout_ns") = -1)
       .def("set_busy_poll", &HttpClient::set_busy_poll)
       .def("set_proxy",
            [](HttpClient& c, const std::string& url) {
@@ -761,6 +762,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         return d;
       })
       .def("idle_ns", &Runner::idle_ns)
+      .def("cancel", &Runner::cancel)
       .def("set_trace_fd", &Runner::set_trace_fd)
       .def("latencies", &Runner::latencies)
       .def("clear_latencies", &Runner::clear_latencies)

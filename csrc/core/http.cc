@@ -1213,11 +1213,15 @@ Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t d
   return read_response(req, resp, deadline_ns, retryable);
 }
 
-Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) {
+Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp) { return round_trip(req, resp, -1); }
+
+Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp, Nanos timeout) {
   std::lock_guard<std::mutex> lk(mu_);
   if (in_flight_) return Status::Err("http: a pipelined request is still in flight");
   if (cancelled()) return Status::Err("request canceled");
-  const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
+  const Nanos t = timeout >= 0 ? timeout : timeout_;
+  if (timeout == 0) return Status::Err("i/o timeout");  // no time left at all
+  const int64_t deadline = t > 0 ? mono_ns() + t : 0;
   stats_.requests++;
   bool retryable = false;
   Status s = attempt(req, resp, deadline, &retryable);

@@ -91,6 +91,8 @@ class HttpClient {
   // replayable (GET/HEAD/OPTIONS/TRACE or an Idempotency-Key): a PUT/PATCH/POST that was
   // written is never sent twice.
   Status round_trip(const HttpRequest& req, HttpResponse* resp);
+  // The same with this call's own time limit (< 0: the client's timeout; 0: fails at once).
+  Status round_trip(const HttpRequest& req, HttpResponse* resp, Nanos timeout);
   // Pipelined use: send() writes the request and returns at once; receive() reads its
   // response. Between the two the caller is free to do other I/O -- the control loop sends the
   // Deployment GET, then makes the SQS call on another connection, so both round trips overlap.

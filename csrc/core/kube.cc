@@ -141,10 +141,8 @@ KubeRestDeployments::KubeRestDeployments(KubeOptions opts)
   http_->set_busy_poll(opts_.busy_poll);
   Status ps = http_->set_proxy(opts_.proxy);
   if (!ps.ok()) init_status_ = ps;
-  if (opts_.qps > 0) {
-    limiter_ = std::make_unique<TokenBucket>(opts_.qps, opts_.burst,
-                                             opts_.clock ? opts_.clock : std::make_shared<RealClock>());
-  }
+  wait_clock_ = opts_.clock ? opts_.clock : std::make_shared<RealClock>();
+  if (opts_.qps > 0) limiter_ = std::make_unique<TokenBucket>(opts_.qps, opts_.burst, wait_clock_);
 }
 
 void KubeRestDeployments::cancel() {
@@ -154,8 +152,10 @@ void KubeRestDeployments::cancel() {
 
 void KubeRestDeployments::throttle() {
   if (!limiter_) return;
-  const Nanos waited = limiter_->take(&cancel_);
+  const Nanos waited = limiter_->reserve();
   if (waited > 0) {
+    wait_until_.store(wait_clock_->now() + waited, std::memory_order_release);
+    wait_clock_->sleep(waited, &cancel_);
     std::lock_guard<std::mutex> lk(mu_);
     stats_.throttled++;
     stats_.throttle_ns += waited;
@@ -301,8 +301,10 @@ bool KubeRestDeployments::sleep_retry(int64_t seconds) {
   // Go sleeps the (possibly negative: no wait) Duration; cap one wait at an hour so a bogus
   // header cannot park the loop (stop still interrupts it).
   const int64_t s = seconds < 0 ? 0 : (seconds > 3600 ? 3600 : seconds);
-  std::shared_ptr<Clock> clock = opts_.clock ? opts_.clock : std::make_shared<RealClock>();
-  if (s > 0 && !clock->sleep(s * kSecond, &cancel_)) return false;
+  if (s > 0) {
+    wait_until_.store(wait_clock_->now() + s * kSecond, std::memory_order_release);
+    if (!wait_clock_->sleep(s * kSecond, &cancel_)) return false;
+  }
   return !cancel_.stopped();
 }
 

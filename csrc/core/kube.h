@@ -56,6 +56,9 @@ class DeploymentApi {
   }
   // Shutdown: abort the request in progress and any throttle wait (sticky). Default: nothing.
   virtual void cancel() {}
+  // Clock time at which the latest deliberate wait (client-side throttle, Retry-After) ends or
+  // ended; 0: none yet. The liveness check counts such a wait as progress.
+  virtual Nanos waiting_until() const { return 0; }
 };
 
 class TokenProvider {
@@ -166,8 +169,11 @@ class KubeRestDeployments final : public DeploymentApi {
   void cancel() override;
   std::string path_for(const std::string& name) const;
   ScaleMode mode() const { return static_cast<ScaleMode>(mode_.load(std::memory_order_acquire)); }
+  Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }
 
  private:
+  std::atomic<Nanos> wait_until_{0};
+  std::shared_ptr<Clock> wait_clock_;  // opts_.clock or a RealClock
   std::string path_in(ScaleMode m, const std::string& name) const;
   Result<ScaleObject> get_in(ScaleMode m, const std::string& name);
   // A /scale request failed with `s`: read the Deployment; when that works, switch to

@@ -258,6 +258,14 @@ void Runner::run(StopFlag* stop, int64_t max_iterations) {
   }
 }
 
+Nanos Runner::idle_ns() const {
+  const Nanos now = clock_->now();
+  Nanos last = progress_ns_.load(std::memory_order_acquire);
+  const Nanos waits = std::max(sqs_->api()->waiting_until(), scaler_->api()->waiting_until());
+  last = std::max(last, std::min(waits, now));
+  return now - last;
+}
+
 RunnerStats Runner::stats() const {
   std::lock_guard<std::mutex> lk(mu_);
   return stats_;

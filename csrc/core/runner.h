@@ -118,7 +118,9 @@ class Runner {
   RunnerStats stats() const;
   // Time since the loop last made progress (armed, or finished a poll) -- the liveness signal:
   // a worker wedged inside a call, or whose thread died, stops resetting it.
-  Nanos idle_ns() const { return clock_->now() - progress_ns_.load(std::memory_order_acquire); }
+  // A deliberate wait of its clients (Retry-After, back-off, throttle) counts as progress up
+  // to its end: a worker correctly waiting out a server's Retry-After is not wedged.
+  Nanos idle_ns() const;
   // Recent poll->patch latencies (ns), oldest first; bounded ring.
   std::vector<Nanos> latencies() const;
   void clear_latencies();

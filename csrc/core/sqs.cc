@@ -284,6 +284,7 @@ Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
       if (throttle) stats_.throttle_retries++;
     }
     const Nanos delay = retry_delay(attempt, throttle) + retry_after;  // a negative header shortens it
+    wait_until_.store(clock_->now() + (delay > 0 ? delay : 0), std::memory_order_release);
     if (!clock_->sleep(delay > 0 ? delay : 0, &cancel_)) break;  // cancelled mid back-off
   }
   if (!r.ok()) {

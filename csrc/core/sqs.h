@@ -11,6 +11,7 @@
 #pragma once
 
 #include <functional>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -41,6 +42,9 @@ class SqsApi {
                                                const std::vector<std::string>& names) = 0;
   // Shutdown: abort the call in progress and any retry back-off (sticky). Default: nothing.
   virtual void cancel() {}
+  // Clock time at which the latest deliberate wait (retry back-off, Retry-After) ends or ended;
+  // 0: none yet. The liveness check counts such a wait as progress.
+  virtual Nanos waiting_until() const { return 0; }
 };
 
 enum class SqsProtocol { Query, Json };
@@ -79,8 +83,10 @@ class HttpSqsApi final : public SqsApi {
   static std::string endpoint_for_region(const std::string& region);
   static std::string signing_region(const std::string& region);
   std::string endpoint() const { return endpoint_; }
+  Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }
 
  private:
+  std::atomic<Nanos> wait_until_{0};
   // *retry_after: the extra initial delay of a throttle answered 429/503 with an integer
   // Retry-After (DefaultRetryer.RetryRules, getRetryAfterDelay); 0 otherwise.
   Result<AttrMap> call_once(const std::string& queue_url, const std::vector<std::string>& names,

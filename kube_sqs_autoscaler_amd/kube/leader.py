@@ -88,6 +88,9 @@ class LeaseLock:
         self.name = name
         self.http = new_http_client(rest, int(timeout_s * 1e9))
         self._rv = ""
+        # Real-time (time.monotonic) instant by which every call must have returned; None: each
+        # call only has the client's own timeout. The elector sets it to the renew deadline.
+        self.deadline: Optional[float] = None
 
     def _headers(self, body: bool = False):
         from ..autoscaler import auth_headers
@@ -105,10 +108,16 @@ class LeaseLock:
         nat = native()
         from ..autoscaler import note_status
 
+        timeout_ns = -1
+        if self.deadline is not None:
+            left = self.deadline - time.monotonic()
+            if left <= 0:
+                raise LeaseError("renew deadline exceeded")
+            timeout_ns = max(1, int(left * 1e9))
         try:
             headers = self._headers(body is not None)
             status, _, raw = self.http.request(method, path, headers,
-                                               json.dumps(body).encode() if body is not None else b"")
+                                               json.dumps(body).encode() if body is not None else b"", timeout_ns)
         except nat.NativeError as e:
             raise LeaseError(str(e))
         note_status(self.rest, headers, status)
@@ -220,17 +229,55 @@ class LeaderElector:
         return False
 
     def renew_loop(self, stop: threading.Event, on_lost: Callable[[], None]) -> None:
-        """Renews every retry_period; calls ``on_lost`` if renew_deadline passes without success."""
-        last_ok = self.monotonic()
-        while not stop.wait(self.retry_period):
-            if self.try_acquire_or_renew():
-                last_ok = self.monotonic()
-                continue
-            if self.monotonic() - last_ok >= self.renew_deadline:
+        """Renews every retry_period. Leadership ends ``renew_deadline`` after the last successful
+        renewal, at that instant, even while a renewal is still in flight: a watchdog calls
+        ``on_lost`` when the deadline passes, and each attempt's lease calls only get the time
+        left before it (client-go bounds every renew with a RenewDeadline context). A standby
+        takes over ``lease_duration`` after it saw that last renewal, so the two never scale
+        together (lease_duration > renew_deadline)."""
+        mu = threading.Lock()
+        lost = threading.Event()
+        finished = threading.Event()
+        last_ok = [self.monotonic()]
+
+        def left() -> float:
+            with mu:
+                return last_ok[0] + self.renew_deadline - self.monotonic()
+
+        def lose() -> None:
+            with mu:
+                if lost.is_set():
+                    return
+                lost.set()
                 self._leader = False
-                self.log("error", f"failed to renew lease {self.lock.describe()}: timed out waiting for the condition")
-                on_lost()
-                return
+            self.log("error", f"failed to renew lease {self.lock.describe()}: timed out waiting for the condition")
+            on_lost()
+
+        def watchdog() -> None:
+            while not finished.is_set() and not stop.is_set():
+                remaining = left()
+                if remaining <= 0:
+                    lose()
+                    return
+                finished.wait(min(remaining, self.retry_period))
+
+        wd = threading.Thread(target=watchdog, name="ksa-lease-watchdog", daemon=True)
+        wd.start()
+        try:
+            while not lost.is_set() and not stop.wait(self.retry_period):
+                remaining = left()
+                if remaining <= 0:
+                    lose()
+                    break
+                self.lock.deadline = time.monotonic() + remaining
+                ok = self.try_acquire_or_renew()
+                with mu:
+                    if ok and not lost.is_set():  # a success after the deadline does not count
+                        last_ok[0] = self.monotonic()
+        finally:
+            self.lock.deadline = None
+            finished.set()
+            wd.join()
 
     def release(self) -> bool:
         """Gives the lease up (ReleaseOnCancel) so a standby can take over at once."""

@@ -103,9 +103,11 @@ class Health:
     * ``/healthz`` fails when the fleet is stopping, or when a running worker has made no
       progress for longer than its budget: ``poll period + 8 x api timeout + 60 s``. The
       budget covers an SQS call with 3 SDK retries, the GET, the write, and a 409 re-read, each
-      bounded by ``--api-timeout``. A worker stuck past all of them is wedged, and a restart
-      (Kubernetes' liveness probe) is the recovery. The reference has no probes and hangs on a
-      stalled call.
+      bounded by ``--api-timeout``. Deliberate waits are not: SQS back-off, a server's
+      ``Retry-After`` (up to an hour) and the client-side throttle count as progress up to
+      their end (``Runner.idle_ns``), so a worker correctly backing off is not restarted. A
+      worker stuck past all of them is wedged, and a restart (Kubernetes' liveness probe) is the
+      recovery. The reference has no probes and hangs on a stalled call.
     * ``/readyz`` is OK for a standby replica under ``--leader-elect``, since waiting for the
       lease is its healthy state. Otherwise it is OK once every worker has completed a poll.
       A standby that never became ready would stall every rolling update of a 2-replica

@@ -458,3 +458,30 @@ def test_missing_scale_route_falls_back(nat, kube_server):
     kube_server.inject(1, nat.InjectedFault(404, "404 page not found"))
     assert p.scale_up().wrote and kube_server.replicas("ml", "worker") == 4
     assert api.stats()["scale_fallbacks"] == 1
+
+
+def test_retry_after_wait_counts_as_liveness_progress(nat, sqs_server, kube_server):
+    """a worker waiting out an apiserver Retry-After (up to an hour) is backing off
+    correctly, not wedged -- /healthz must not get it restarted. Runner.idle_ns() stays ~0 for
+    the whole wait."""
+    import threading
+    import time
+
+    c, _, url = sqs_client(nat, sqs_server)
+    p, _ = scaler(nat, kube_server, "scale")
+    cfg = nat.LoopConfig()
+    cfg.poll_period_ns = cfg.scale_up_cool_down_ns = cfg.scale_down_cool_down_ns = 0
+    r = nat.Runner(cfg, c, p, nat.RealClock(), capture_logger([]))
+    r.arm()
+    sqs_server.set_attributes(url, {n: "100" for n in NAMES})
+    kube_server.inject(1, nat.InjectedFault(429, "", retry_after="3600"))
+    out = []
+    th = threading.Thread(target=lambda: out.append(r.poll_once()))
+    th.start()
+    try:
+        time.sleep(0.5)
+        assert th.is_alive() and r.idle_ns() < 100_000_000  # in the 1 h wait, counted as progress
+    finally:
+        r.cancel()
+        th.join(10)
+    assert not th.is_alive() and out[0]["up"] == "failed"

@@ -176,3 +176,32 @@ def test_two_processes_failover(nat, kube, tmp_path):
         assert kube.replicas("ml", "w") == 1
     finally:
         sqs.stop()
+
+
+def test_hanging_renewal_loses_leadership_at_the_deadline(nat, kube):
+    """a renewal that hangs must not stretch leadership past renew_deadline. The lease
+    calls get only the time left before the deadline, and a watchdog ends leadership when it
+    passes, long before the lease client's own 10 s timeout."""
+    a = LeaderElector(LeaseLock(RestConfig(host=kube.url, bearer_token=TOKEN), "ml", "ksa", timeout_s=10.0),
+                      "a", 1.2, 0.6, 0.1)
+    assert a.try_acquire_or_renew()
+    a._leader = True
+    lost_at = []
+    stop = threading.Event()
+    t0 = time.monotonic()
+    kube.set_latency(5_000_000_000)  # every apiserver call now hangs for 5 s
+    th = threading.Thread(target=a.renew_loop, args=(stop, lambda: lost_at.append(time.monotonic())))
+    th.start()
+    try:
+        deadline = time.monotonic() + 4
+        while not lost_at and time.monotonic() < deadline:
+            time.sleep(0.01)
+        assert lost_at, "leadership not given up"
+        assert lost_at[0] - t0 < 0.6 + 0.4  # renew_deadline (+ scheduling slack), not 10 s
+        assert not a.is_leader
+    finally:
+        stop.set()
+        kube.set_latency(0)
+        th.join(timeout=10)
+    assert not th.is_alive()
+    assert len(lost_at) == 1
