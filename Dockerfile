@@ -1,34 +1,48 @@
-# Two stages like the reference (/root/reference/Dockerfile): build the native runtime, then ship a
-# runtime image. Targets:
-#   runtime (default) -- ROCm base; includes libksa_gpu.so for --gpu-aware-max=local, which runs the
-#                        gfx950 HBM probe when the autoscaler is a sidecar on the MI355X node.
-#   slim              -- plain Ubuntu + Python + OpenSSL, no GPU code: the control loop alone needs
-#                        none (docker build --target slim).
+# Two stages like the reference (/root/reference/Dockerfile: build, then a small runtime image).
+# Targets (the LAST stage is what a plain `docker build .` produces):
+#   gpu   -- adds the HIP *runtime* (hip-runtime-amd from the ROCm apt repository, no compiler or
+#            dev packages) and libksa_gpu.so, for --gpu-aware-max=local: the gfx950 HBM probe of a
+#            sidecar on the MI355X node (docker build --target gpu).
+#   slim  -- (default) Ubuntu + Python + OpenSSL, no GPU code: the control loop needs none.
 # Both put the launcher at /kube-sqs-autoscaler, so the reference's manifests
-# (`command: [/kube-sqs-autoscaler, --flags...]`, README.md:37-39) work unchanged.
-FROM rocm/dev-ubuntu-22.04:7.2 AS builder
+# (`command: [/kube-sqs-autoscaler, --flags...]`, README.md:37-39) work unchanged, and with the
+# /scale -> Deployment fallback so does a Role written for the reference (get/update deployments).
+ARG ROCM_VERSION=7.2
+
+FROM rocm/dev-ubuntu-22.04:${ROCM_VERSION} AS builder
 RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-pip g++ libssl-dev \
  && rm -rf /var/lib/apt/lists/*
 WORKDIR /work
 COPY . /work
-RUN pip3 install --no-cache-dir pybind11 PyYAML prometheus-client \
- && PYTORCH_ROCM_ARCH=gfx950 python3 -m kube_sqs_autoscaler_amd.ops.build
+# pybind11 3 (smart_holder) is not in Ubuntu 22.04's archive: pinned from PyPI, build stage only.
+RUN pip3 install --no-cache-dir pybind11==3.0.4 \
+ && PYTORCH_ROCM_ARCH=gfx950 python3 -m kube_sqs_autoscaler_amd.ops.build \
+ && python3 -m kube_sqs_autoscaler_amd.ops.build --no-hip --sanitizers \
+ && ./build/native_tests
 
-FROM ubuntu:22.04 AS slim
-RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-pip ca-certificates libssl3 \
- && rm -rf /var/lib/apt/lists/* && pip3 install --no-cache-dir PyYAML prometheus-client
+FROM ubuntu:22.04 AS base
+# Runtime Python deps from the distribution archive (no pip at runtime).
+RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-yaml \
+      python3-prometheus-client ca-certificates libssl3 \
+ && rm -rf /var/lib/apt/lists/*
 COPY --from=builder /work/kube_sqs_autoscaler_amd /app/kube_sqs_autoscaler_amd
 COPY --from=builder /work/deploy/bin/kube-sqs-autoscaler /kube-sqs-autoscaler
-RUN rm -f /app/kube_sqs_autoscaler_amd/ops/libksa_gpu.so /app/kube_sqs_autoscaler_amd/ops/*.bin
 ENV PYTHONPATH=/app KSA_NO_AUTOBUILD=1
+
+FROM base AS gpu
+ARG ROCM_VERSION
+RUN apt-get update && apt-get install -y --no-install-recommends curl gnupg \
+ && mkdir -p /etc/apt/keyrings \
+ && curl -fsSL https://repo.radeon.com/rocm/rocm.gpg.key | gpg --dearmor -o /etc/apt/keyrings/rocm.gpg \
+ && echo "deb [arch=amd64 signed-by=/etc/apt/keyrings/rocm.gpg] https://repo.radeon.com/rocm/apt/${ROCM_VERSION} jammy main" \
+      > /etc/apt/sources.list.d/rocm.list \
+ && apt-get update && apt-get install -y --no-install-recommends hip-runtime-amd \
+ && apt-get purge -y curl gnupg && apt-get autoremove -y && rm -rf /var/lib/apt/lists/*
+ENV LD_LIBRARY_PATH=/opt/rocm/lib
 USER 65534
 ENTRYPOINT ["/kube-sqs-autoscaler"]
 
-FROM rocm/dev-ubuntu-22.04:7.2 AS runtime
-RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-pip ca-certificates libssl3 \
- && rm -rf /var/lib/apt/lists/* && pip3 install --no-cache-dir PyYAML prometheus-client
-COPY --from=builder /work/kube_sqs_autoscaler_amd /app/kube_sqs_autoscaler_amd
-COPY --from=builder /work/deploy/bin/kube-sqs-autoscaler /kube-sqs-autoscaler
-ENV PYTHONPATH=/app KSA_NO_AUTOBUILD=1
+FROM base AS slim
+RUN rm -f /app/kube_sqs_autoscaler_amd/ops/libksa_gpu.so /app/kube_sqs_autoscaler_amd/ops/*.bin
 USER 65534
 ENTRYPOINT ["/kube-sqs-autoscaler"]

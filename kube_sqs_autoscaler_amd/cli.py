@@ -16,7 +16,7 @@ import threading
 from typing import List, Mapping, Optional
 
 from . import autoscaler
-from .config import config_from_flags, new_flag_set
+from .config import MI355X_MAX_PODS, REFERENCE_MAX_PODS, config_from_flags, new_flag_set
 from .kube.config import KubeConfigError
 from .utils.goflag import FlagError
 from .utils.log import make_logger
@@ -72,6 +72,11 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     if w:
         log.log("warning", w)
 
+    if not fs.was_set("max-pods"):
+        # the one default that differs from the reference (main.go:90: 5)
+        log.log("warning", f"--max-pods not set: using {MI355X_MAX_PODS} (one GPU-worker pod per MI355X of an "
+                           f"8-GPU node); the reference defaults to {REFERENCE_MAX_PODS}")
+
     multi = len(cfg.targets) > 1
     workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
 
@@ -87,7 +92,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         else:
             capacity = ClusterGpuCapacity(rest, cfg.gpu_resource, cfg.gpu_node_selector, cfg.gpus_per_pod).pod_capacity
         capper = MaxPodsCapper([w.runner.scaler for w in workers], [t.max_pods for t in cfg.targets], capacity,
-                               cfg.gpu_refresh_period_ns / 1e9, log=lambda lvl, m: log.log(lvl, m))
+                               cfg.gpu_refresh_period_ns / 1e9, log=lambda lvl, m: log.log(lvl, m),
+                               min_pods=[t.min_pods for t in cfg.targets])
         capper.refresh()
         if cfg.gpu_aware_max == "cluster":
             capper.start()

@@ -10,9 +10,16 @@ effective max-pods:
   the AMD GPU device plugin advertises) over schedulable nodes matching ``--gpu-node-selector``,
   divided by ``--gpus-per-pod``, refreshed every ``--gpu-refresh-period``.
 
-The cap is ``min(--max-pods, capacity)`` and is applied through the native actuator's atomic
-``set_max``, so a refresh never races a running scale decision. A failed refresh keeps the last
-good cap (never scales to zero capacity by accident); no capacity read yet means no cap.
+The cap is ``min(--max-pods, capacity)``, never below ``--min-pods``, and is applied through
+the native actuator's atomic ``set_max``, so a refresh never races a running scale decision. A
+failed refresh keeps the last good cap; no capacity read yet means no cap. A capacity of 0 (no
+GPU visible, every GPU node cordoned) is treated as "unknown": it is logged as a warning and the
+configured ``--max-pods`` stays in force -- a cap of 0 would silently turn every scale-up into a
+no-op at max.
+
+``local`` only sees the GPUs allocated to the autoscaler's own pod: under the AMD GPU device
+plugin a pod that requests no ``amd.com/gpu`` sees none, so a ``local`` sidecar must request
+the GPUs it is meant to count (``cluster`` has no such constraint).
 """
 from __future__ import annotations
 
@@ -91,9 +98,11 @@ class MaxPodsCapper:
     """Applies ``min(configured max, capacity)`` to actuators, periodically."""
 
     def __init__(self, scalers: Sequence, configured_max: Sequence[int], capacity: Callable[[], int],
-                 refresh_s: float = 60.0, log: Optional[Callable[[str, str], None]] = None):
+                 refresh_s: float = 60.0, log: Optional[Callable[[str, str], None]] = None,
+                 min_pods: Optional[Sequence[int]] = None):
         self.scalers = list(scalers)
         self.configured = list(configured_max)
+        self.floor = list(min_pods) if min_pods is not None else [getattr(s, "min", 0) for s in self.scalers]
         self.capacity = capacity
         self.refresh_s = refresh_s
         self.log = log or (lambda lvl, m: None)
@@ -107,11 +116,20 @@ class MaxPodsCapper:
         except Exception as e:  # keep the last good cap
             self.log("warning", f"GPU capacity refresh failed, keeping max-pods cap {self.cap}: {e}")
             return self.cap
+        if cap <= 0:
+            if cap != self.cap:
+                self.log("warning", f"GPU capacity reads {cap} pods (no GPU visible to --gpu-aware-max?); "
+                                    f"keeping the configured max-pods {self.configured}")
+            self.cap = cap
+            for s, m in zip(self.scalers, self.configured):
+                s.max = m
+            return cap
+        eff = [max(min(m, cap), lo) for m, lo in zip(self.configured, self.floor)]
         if cap != self.cap:
-            self.log("info", f"GPU capacity: {cap} pods; effective max-pods {[min(m, cap) for m in self.configured]}")
+            self.log("info", f"GPU capacity: {cap} pods; effective max-pods {eff}")
         self.cap = cap
-        for s, m in zip(self.scalers, self.configured):
-            s.max = min(m, cap)
+        for s, e in zip(self.scalers, eff):
+            s.max = e
         return cap
 
     def start(self) -> None:

@@ -11,9 +11,8 @@ has no graceful shutdown, main.go:36).
 """
 from __future__ import annotations
 
-import signal
 import threading
-from typing import Callable, List, Optional, Sequence
+from typing import List, Sequence
 
 from ..ops import native
 
@@ -71,29 +70,3 @@ class Fleet:
             s["queue"] = w.target.queue_url
             out.append(s)
         return out
-
-    def run_until_signalled(self, signals=(signal.SIGTERM, signal.SIGINT),
-                            on_signal: Optional[Callable[[int], None]] = None, poll_s: float = 0.2) -> int:
-        """Starts the workers and blocks until a signal (or all workers finish); returns the signal."""
-        got: List[int] = []
-        prev = {}
-
-        def handler(signum, _frame):
-            got.append(signum)
-            if on_signal:
-                on_signal(signum)
-            self.stop()
-
-        if threading.current_thread() is threading.main_thread():
-            for s in signals:
-                prev[s] = signal.signal(s, handler)
-        try:
-            self.start()
-            while not self.wait(poll_s):
-                pass
-        finally:
-            self.stop()
-            self.join()
-            for s, h in prev.items():
-                signal.signal(s, h)
-        return got[0] if got else 0

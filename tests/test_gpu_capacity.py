@@ -71,3 +71,50 @@ def test_cli_cluster_cap(nat, kube, tmp_path, capfd):
         assert "GPU capacity: 4 pods" in capfd.readouterr().err
     finally:
         sqs.stop()
+
+
+def test_capper_floors_at_min_pods_and_ignores_zero_capacity(nat):
+    """a capacity of 0 (no GPU visible to a `local` probe, every GPU node cordoned)
+    must not freeze scale-up at 0; a capacity below --min-pods never caps below it."""
+    fake = nat.FakeDeployments("ns")
+    fake.add("w", 1)
+    s = nat.PodAutoScaler(fake, "w", "ns", 8, 3, 1, 1, nat.Logger(), nat.RealClock())
+    caps = [0, 2, 5, 0]
+    logs = []
+    m = MaxPodsCapper([s], [8], lambda: caps.pop(0), log=lambda lvl, msg: logs.append((lvl, msg)))
+    assert m.refresh() == 0 and s.max == 8  # unknown capacity: the configured max stays
+    assert logs[-1][0] == "warning" and "keeping the configured max-pods [8]" in logs[-1][1]
+    assert m.refresh() == 2 and s.max == 3  # floored at min-pods (3)
+    assert m.refresh() == 5 and s.max == 5
+    assert m.refresh() == 0 and s.max == 8
+
+
+def test_local_cap_with_no_gpu_still_scales_to_max(nat, tmp_path, capfd, monkeypatch):
+    """--gpu-aware-max=local on a pod that sees no GPU: a warning, and scale-up still reaches the
+    configured --max-pods."""
+    from kube_sqs_autoscaler_amd.cli import main
+    from kube_sqs_autoscaler_amd.ops import gpu
+
+    monkeypatch.setattr(gpu, "healthy_gpu_count", lambda: 0)
+    sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs.start()
+    kube.require_token(TOKEN)
+    kube.start()
+    try:
+        url = sqs.url + "/1/q"
+        sqs.set_attributes(url, {"ApproximateNumberOfMessages": "1000"})
+        kube.add_deployment("ml", "w", 1)
+        kc = tmp_path / "kc"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}], "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"AWS_ACCESS_KEY_ID": "a", "AWS_SECRET_ACCESS_KEY": "b", "KUBE_CONFIG_PATH": str(kc)}
+        rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=w", "--kubernetes-namespace=ml", "--aws-region=us-east-1",
+                   f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s", "--max-pods=6",
+                   "--attribute-names=ApproximateNumberOfMessages", "--gpu-aware-max=local"], environ=env, max_iterations=8)
+        assert rc == 0 and kube.replicas("ml", "w") == 6
+        err = capfd.readouterr().err
+        assert "level=warning" in err and "keeping the configured max-pods [6]" in err
+    finally:
+        sqs.stop()
+        kube.stop()
