@@ -141,6 +141,14 @@ def simulate(
     :func:`_likely`, restated from the rule in runner.h, not shared with it.
     """
     f = faults or Faults()
+    import bisect
+
+    starts = [start for start, _ in trace]
+
+    def sample_at(t: int) -> AttrMap:  # sample() in O(log n): long traces (GPU sweep checks)
+        i = bisect.bisect_right(starts, t) - 1
+        return trace[i][1] if i >= 0 else {}
+
     st = {"now": 0, "last_up": 0, "last_down": 0, "replicas": int32(init_replicas)}  # main.go:37-38
     out: List[Event] = []
     seen = {"depth": None, "rtt": 0}  # prefetch gate inputs: last depth read, last SQS latency
@@ -202,7 +210,7 @@ def simulate(
         return True
 
     def poll(k: int, ev: Event, pf: dict) -> None:
-        attrs = sample(trace, st["now"])
+        attrs = sample_at(st["now"])
         st["now"] += lat.sqs_ns
         seen["rtt"] = lat.sqs_ns
         if k in f.sqs:

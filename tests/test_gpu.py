@@ -184,3 +184,57 @@ def test_sharded_sweep_cli_on_gpu(tmp_path):
     c = cl.run(tr, grid, cl.QueueModel(5.0, 60 * S, 100), 1, 1800 * S, (1_000_000,) * 3, seeds=8, device="cpu")
     want = sorted((c.row(i) for i in range(len(c))), key=lambda x: x["pod_hours_mean"])
     assert sorted(rows, key=lambda x: x["pod_hours_mean"]) == want
+
+
+def test_sweep_kernel_random_lanes_equal_oracle():
+    """the gfx950 open-loop kernel against the independent Python oracle on 256 lanes
+    per dispatch (adversarial + random configurations), with the trace in LDS and in global
+    memory, plus GPU == CPU on every lane of the dispatch."""
+    import sys
+    import os
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from _lanes import MS, S, lanes_to_check, random_params, random_walk_trace
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    lat = (2 * MS, MS, MS)
+    params = random_params(16384, seed=21)  # >> 256 CUs x 64 lanes / 4: a full dispatch
+    for n, seed in ((400, 1), (2600, 2)):
+        tr = random_walk_trace(n, seed)
+        horizon = min(int(tr.t_ns[-1]) + 10 * S, 1800 * S)
+        g = sweep.run(tr, params, 2, horizon, lat, device="gpu")
+        c = sweep.run(tr, params, 2, horizon, lat, device="cpu")
+        assert g.device == "gpu"
+        for k in g.out:
+            assert np.array_equal(g.out[k], c.out[k]), k
+        for i in lanes_to_check(params.shape[1], 256, seed):
+            o = sweep.oracle_row(tr, g.config(i), 2, horizon, lat)
+            assert {k: g.row(i)[k] for k in o} == o, (i, g.config(i))
+
+
+def test_closed_loop_kernel_random_lanes_equal_reference_model():
+    import sys
+    import os
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from _lanes import MS, S, lanes_to_check, random_params
+    from kube_sqs_autoscaler_amd.tune import closedloop as cl
+
+    lat = (2 * MS, MS, MS)
+    params = random_params(4096, seed=31, min_poll_ms=2000)
+    tr = cl.ArrivalTrace.from_segments([(0, 0.5), (120, 30.0), (400, 2.0), (700, 45.0), (800, 0.0)])
+    model = cl.QueueModel(service_rate=4.0, startup_ns=45 * S, slo_backlog=150, init_backlog=20)
+    seeds = 8
+    g = cl.run(tr, params, model, 1, 1200 * S, lat, seeds=seeds, device="gpu")
+    c = cl.run(tr, params, model, 1, 1200 * S, lat, seeds=seeds, device="cpu")
+    for k in g.out:
+        assert np.array_equal(g.out[k], c.out[k]), k
+    rng = np.random.default_rng(9)
+    for i in lanes_to_check(params.shape[1], 256, 13):
+        s = int(rng.integers(0, seeds))
+        want = cl.reference_lane(tr, g.config(i), model, 1, 1200 * S, lat, 1 + s)
+        assert {k: int(v[i, s]) for k, v in g.out.items()} == want, (i, g.config(i))
