@@ -780,7 +780,18 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("wait", &Supervisor::wait, py::arg("timeout_ns"), py::call_guard<py::gil_scoped_release>())
       .def("join", &Supervisor::join, py::call_guard<py::gil_scoped_release>())
       .def("__len__", &Supervisor::size)
-      .def("runner", &Supervisor::runner);
+      .def("runner", &Supervisor::runner)
+      .def("thread_sched", [](Supervisor& s) {
+        auto t = s.thread_sched();
+        py::dict d;
+        d["threads"] = t.threads;
+        d["cpu_ns"] = t.cpu_ns;
+        d["runq_wait_ns"] = t.runq_wait_ns;
+        d["slices"] = t.slices;
+        d["vol_cs"] = t.vol_cs;
+        d["invol_cs"] = t.invol_cs;
+        return d;
+      });
 
   py::class_<Scheduler, std::shared_ptr<Scheduler>>(m, "Scheduler")
       .def(py::init([](size_t threads, bool stagger) {

@@ -16,6 +16,7 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <poll.h>
+#include <pthread.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -1316,7 +1317,10 @@ Status HttpServer::listen(const std::string& host, int port) {
   port_ = ss.ss_family == AF_INET6 ? ntohs(reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port)
                                    : ntohs(reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
   listen_fd_ = fd;
-  acceptor_ = std::thread([this] { accept_loop(); });
+  acceptor_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "ksa-accept");
+    accept_loop();
+  });
   return Status::OK();
 }
 
@@ -1348,6 +1352,7 @@ void HttpServer::accept_loop() {
       open_fds_.push_back(fd);
       auto done = std::make_shared<std::atomic<bool>>(false);
       workers_.push_back(Worker{std::thread([this, fd, done] {
+                                  pthread_setname_np(pthread_self(), "ksa-serve");
                                   serve(fd);
                                   done->store(true, std::memory_order_release);
                                 }),

@@ -1,8 +1,10 @@
 #include "runner.h"
 
+#include <pthread.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <functional>
 #include <cmath>
 #include <limits>
@@ -289,13 +291,42 @@ void Runner::clear_latencies() {
 
 // ---------------------------------------------------------------------------------------
 
+bool read_thread_sched(ThreadSched* out) {
+  *out = ThreadSched();
+  FILE* f = std::fopen("/proc/thread-self/schedstat", "r");
+  if (!f) return false;
+  long long cpu = 0, wait = 0, slices = 0;
+  const int n = std::fscanf(f, "%lld %lld %lld", &cpu, &wait, &slices);
+  std::fclose(f);
+  if (n != 3) return false;
+  out->threads = 1;
+  out->cpu_ns = cpu;
+  out->runq_wait_ns = wait;
+  out->slices = slices;
+  f = std::fopen("/proc/thread-self/status", "r");
+  if (f) {
+    char line[256];
+    while (std::fgets(line, sizeof line, f)) {
+      long long v = 0;
+      if (std::sscanf(line, "voluntary_ctxt_switches: %lld", &v) == 1) out->vol_cs = v;
+      else if (std::sscanf(line, "nonvoluntary_ctxt_switches: %lld", &v) == 1) out->invol_cs = v;
+    }
+    std::fclose(f);
+  }
+  return true;
+}
+
 void Supervisor::start(int64_t max_iterations) {
   std::lock_guard<std::mutex> lk(mu_);
   running_ = runners_.size();
   for (auto& r : runners_) {
     threads_.emplace_back([this, r, max_iterations] {
+      pthread_setname_np(pthread_self(), "ksa-worker");  // top -H / /proc/<pid>/task/*/comm
       r->run(&stop_, max_iterations);
+      ThreadSched ts;
+      const bool have = read_thread_sched(&ts);
       std::lock_guard<std::mutex> g(mu_);
+      if (have) sched_.add(ts);
       --running_;
       cv_.notify_all();
     });
@@ -355,7 +386,11 @@ void Scheduler::start(int64_t max_iterations) {
   std::make_heap(heap_.begin(), heap_.end(), std::greater<Item>());
   finished_ = 0;
   running_ = nthreads_;
-  for (size_t t = 0; t < nthreads_; ++t) threads_.emplace_back([this] { worker(); });
+  for (size_t t = 0; t < nthreads_; ++t)
+    threads_.emplace_back([this] {
+      pthread_setname_np(pthread_self(), "ksa-sched");
+      worker();
+    });
 }
 
 void Scheduler::worker() {

@@ -162,6 +162,27 @@ class Runner {
   static constexpr size_t kLatRing = 1 << 16;
 };
 
+// Scheduler accounting of one thread (/proc/thread-self/schedstat and status): time on CPU, time
+// runnable but waiting for a CPU, timeslices, voluntary / involuntary context switches.
+struct ThreadSched {
+  int64_t threads = 0;
+  int64_t cpu_ns = 0;
+  int64_t runq_wait_ns = 0;
+  int64_t slices = 0;
+  int64_t vol_cs = 0;
+  int64_t invol_cs = 0;
+  void add(const ThreadSched& o) {
+    threads += o.threads;
+    cpu_ns += o.cpu_ns;
+    runq_wait_ns += o.runq_wait_ns;
+    slices += o.slices;
+    vol_cs += o.vol_cs;
+    invol_cs += o.invol_cs;
+  }
+};
+// The calling thread's counters (false when /proc is unavailable).
+bool read_thread_sched(ThreadSched* out);
+
 class Supervisor {
  public:
   void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
@@ -180,15 +201,23 @@ class Supervisor {
   size_t size() const { return runners_.size(); }
   std::shared_ptr<Runner> runner(size_t i) const { return runners_.at(i); }
   StopFlag* stop_flag() { return &stop_; }
+  // Totals over the worker threads that have exited (each adds its counters on the way out):
+  // where a worker's wall time went besides its own work -- e.g. run-queue waits when more
+  // threads are runnable than the process's CPU share.
+  ThreadSched thread_sched() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return sched_;
+  }
   ~Supervisor();
 
  private:
   std::vector<std::shared_ptr<Runner>> runners_;
   std::vector<std::thread> threads_;
   StopFlag stop_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::condition_variable cv_;
   size_t running_ = 0;
+  ThreadSched sched_;
 };
 
 // JSON line of an iteration record (span trace format).

@@ -1,0 +1,55 @@
+"""The benchmark's fake SQS + kube-apiserver endpoints, in a process of their own.
+
+``python -m kube_sqs_autoscaler_amd.bench.fakeserve --queues Q --pairs N`` starts N fake SQS +
+apiserver pairs serving Q bench queues (latency.start_fake_endpoints), prints one JSON line
+with their URLs and certificates, then answers commands on stdin, one per line:
+``stats`` -> a JSON line of request / connection / signature counters and the replicas of every
+bench Deployment; ``quit`` -> stop the servers and exit (EOF on stdin does the same).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+from ..ops import native
+from .latency import deployment_name, start_fake_endpoints
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--queues", type=int, required=True)
+    ap.add_argument("--pairs", type=int, default=1)
+    ap.add_argument("--tls", type=int, default=0)
+    ap.add_argument("--sqs-latency-ns", type=int, default=0)
+    ap.add_argument("--kube-latency-ns", type=int, default=0)
+    a = ap.parse_args(argv)
+    nat = native()
+    sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns)
+    try:
+        info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],
+                "kube": [{"url": k.url, "cert_pem": k.cert_pem} for k in kube]}
+        print(json.dumps(info), flush=True)
+        for line in sys.stdin:
+            cmd = line.strip()
+            if cmd == "stats":
+                print(json.dumps({
+                    "sqs_requests": sum(s.requests() for s in sqs), "kube_requests": sum(k.requests() for k in kube),
+                    "sqs_connections": sum(s.connections() for s in sqs),
+                    "kube_connections": sum(k.connections() for k in kube),
+                    "signature_failures": sum(s.signature_failures() for s in sqs),
+                    "replicas": [kube[q % len(kube)].replicas("bench", deployment_name(q)) for q in range(a.queues)],
+                }), flush=True)
+            elif cmd == "quit":
+                break
+    finally:
+        for s in sqs:
+            s.stop()
+        for k in kube:
+            k.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

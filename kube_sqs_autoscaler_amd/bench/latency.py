@@ -76,8 +76,97 @@ class LatencyResult:
         }
 
 
+HIGH = {"ApproximateNumberOfMessages": "150", "ApproximateNumberOfMessagesDelayed": "20",
+        "ApproximateNumberOfMessagesNotVisible": "30"}
+LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed": "0",
+       "ApproximateNumberOfMessagesNotVisible": "0"}
+
+
+def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
+                         kube_latency_ns: int = 0):
+    """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues (queue q on pair
+    q % n_servers): the 200 <-> 0 attribute cycle per queue and one Deployment per queue."""
+    sqs_servers, kube_servers = [], []
+    for _ in range(n_servers):
+        sqs = nat.FakeSqsServer()
+        sqs.require_signature(AKID, SECRET, REGION)
+        sqs.start("127.0.0.1", 0, tls)
+        sqs.set_latency(sqs_latency_ns)
+        kube = nat.FakeKubeServer()
+        kube.require_token(TOKEN)
+        kube.start("127.0.0.1", 0, tls)
+        kube.set_latency(kube_latency_ns)
+        sqs_servers.append(sqs)
+        kube_servers.append(kube)
+    for q in range(queues):
+        si = q % n_servers
+        sqs_servers[si].set_attribute_cycle(queue_url(sqs_servers[si].url, q), [HIGH, LOW])
+        kube_servers[si].add_deployment("bench", deployment_name(q), 1)
+    return sqs_servers, kube_servers
+
+
+def queue_url(sqs_url: str, q: int) -> str:
+    return f"{sqs_url}/000000000000/bench-queue-{q}"
+
+
+def deployment_name(q: int) -> str:
+    return f"gpu-worker-{q}"
+
+
+class _Endpoint:
+    """Parent-side view of one fake server living in the endpoint process."""
+
+    def __init__(self, url: str, cert_pem: str):
+        self.url, self.cert_pem = url, cert_pem
+
+
+class RemoteEndpoints:
+    """The fake endpoints in a child process (``python -m kube_sqs_autoscaler_amd.bench.fakeserve``):
+    what an autoscaler sees in production, where SQS and the apiserver are other machines'
+    processes -- their threads do not share the autoscaler's process, allocator or CPU share."""
+
+    def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int):
+        import json
+        import subprocess
+        import sys
+
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        self.proc = subprocess.Popen(
+            [sys.executable, "-m", "kube_sqs_autoscaler_amd.bench.fakeserve", "--queues", str(queues), "--pairs",
+             str(n_servers), "--tls", str(int(tls)), "--sqs-latency-ns", str(sqs_latency_ns), "--kube-latency-ns",
+             str(kube_latency_ns)], cwd=root, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+        line = self.proc.stdout.readline()
+        if not line:
+            raise RuntimeError("fake endpoint process failed to start")
+        info = json.loads(line)
+        self.sqs = [_Endpoint(e["url"], e["cert_pem"]) for e in info["sqs"]]
+        self.kube = [_Endpoint(e["url"], e["cert_pem"]) for e in info["kube"]]
+        self.pid = info["pid"]
+
+    def stats(self) -> dict:
+        import json
+
+        self.proc.stdin.write("stats\n")
+        self.proc.stdin.flush()
+        return json.loads(self.proc.stdout.readline())
+
+    def close(self) -> None:
+        if self.proc.poll() is None:
+            try:
+                self.proc.stdin.write("quit\n")
+                self.proc.stdin.flush()
+                self.proc.wait(timeout=10)
+            except Exception:
+                self.proc.kill()
+                self.proc.wait()
+
+
 class BenchEnv:
-    """Fake servers + one worker per queue."""
+    """Fake servers + one worker per queue.
+
+    ``servers``: ``shared`` -- one fake SQS + apiserver pair in this process for every queue;
+    ``per-queue`` -- one pair per queue, in this process; ``process`` -- one pair per queue in a
+    separate endpoint process (as production's remote endpoints, and as separate ranks see it)."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
@@ -86,21 +175,16 @@ class BenchEnv:
         self.nat = nat
         self.mode = mode
         self.pipeline = pipeline
-        # servers="per-queue": every queue gets its own fake SQS endpoint and fake apiserver, as
-        # separate processes (one rank per GPU) have; "shared": one of each serves every queue.
-        n_servers = queues if servers == "per-queue" else 1
-        self.sqs_servers, self.kube_servers = [], []
-        for _ in range(n_servers):
-            sqs = nat.FakeSqsServer()
-            sqs.require_signature(AKID, SECRET, REGION)
-            sqs.start("127.0.0.1", 0, tls)
-            sqs.set_latency(sqs_latency_ns)
-            kube = nat.FakeKubeServer()
-            kube.require_token(TOKEN)
-            kube.start("127.0.0.1", 0, tls)
-            kube.set_latency(kube_latency_ns)
-            self.sqs_servers.append(sqs)
-            self.kube_servers.append(kube)
+        n_servers = 1 if servers == "shared" else queues
+        self.remote = None
+        if servers == "process":
+            self.remote = RemoteEndpoints(queues, n_servers, tls, sqs_latency_ns, kube_latency_ns)
+            self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
+        elif servers in ("shared", "per-queue"):
+            self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
+                                                                       kube_latency_ns)
+        else:
+            raise ValueError(f"servers must be shared, per-queue or process, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
         self.clock = nat.RealClock()
         self._devnull = None
@@ -113,10 +197,6 @@ class BenchEnv:
             lg.set_sink_fd(log_fd)
             self.loggers.append(lg)
         self.log = self.loggers[0]
-        high = {"ApproximateNumberOfMessages": "150", "ApproximateNumberOfMessagesDelayed": "20",
-                "ApproximateNumberOfMessagesNotVisible": "30"}
-        low = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed": "0",
-               "ApproximateNumberOfMessagesNotVisible": "0"}
         creds = static_provider(AKID, SECRET)
         self.runners = []
         self.kube_apis, self.sqs_apis = [], []
@@ -132,10 +212,8 @@ class BenchEnv:
                 sqs_tls.ca_pem = sqs.cert_pem
                 rest.insecure = False
                 rest.ca_pem = kube.cert_pem
-            url = f"{sqs.url}/000000000000/bench-queue-{q}"
-            name = f"gpu-worker-{q}"
-            sqs.set_attribute_cycle(url, [high, low])
-            kube.add_deployment("bench", name, 1)
+            url = queue_url(sqs.url, q)
+            name = deployment_name(q)
             self.server_of.append(si)
             t = TargetConfig(queue_url=url, deployment=name, namespace="bench", poll_period_ns=0,
                              scale_up_cool_down_ns=0, scale_down_cool_down_ns=0, scale_up_messages=100,
@@ -165,12 +243,21 @@ class BenchEnv:
         t0 = time.perf_counter()
         sup.start(iterations)
         sup.join()
-        return time.perf_counter() - t0
+        wall = time.perf_counter() - t0
+        self.last_thread_sched = dict(sup.thread_sched())  # the worker threads, as they exited
+        return wall
 
     def collect(self, steps: int, wall: float) -> LatencyResult:
         res = LatencyResult(queues=len(self.runners), mode=self.mode, steps=steps, pipeline=self.pipeline, wall_s=wall)
         for r in self.runners:
             res.samples.extend(r.latencies())
+        if self.remote is not None:
+            st = self.remote.stats()
+            res.sqs_requests, res.kube_requests = st["sqs_requests"], st["kube_requests"]
+            res.sqs_connections, res.kube_connections = st["sqs_connections"], st["kube_connections"]
+            res.signature_failures = st["signature_failures"]
+            res.final_replicas = st["replicas"]
+            return res
         res.sqs_requests = sum(s.requests() for s in self.sqs_servers)
         res.kube_requests = sum(k.requests() for k in self.kube_servers)
         res.sqs_connections = sum(s.connections() for s in self.sqs_servers)
@@ -185,10 +272,13 @@ class BenchEnv:
             r.clear_latencies()
 
     def close(self) -> None:
-        for s in self.sqs_servers:
-            s.stop()
-        for k in self.kube_servers:
-            k.stop()
+        if self.remote is not None:
+            self.remote.close()
+        else:
+            for s in self.sqs_servers:
+                s.stop()
+            for k in self.kube_servers:
+                k.stop()
         if self._devnull is not None:
             os.close(self._devnull)
             self._devnull = None
@@ -231,3 +321,133 @@ def measure(queues: int, steps: int, warmup: int, mode: str = "scale", **kw) -> 
         return env.collect(steps, wall)
     finally:
         env.close()
+
+
+# ---------------------------------------------------------------------------------------------
+# Where does multi-queue latency go? Scheduler and kernel evidence around a measurement.
+
+
+def _task_stats(pid: int) -> Dict[str, Dict[str, int]]:
+    """Per thread name (``ksa-worker``, ``ksa-serve``, ...): CPU time, run-queue wait and
+    timeslices from /proc/<pid>/task/*/schedstat, and context switches from .../status."""
+    out: Dict[str, Dict[str, int]] = {}
+    base = f"/proc/{pid}/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/comm") as f:
+                comm = f.read().strip()
+            with open(f"{base}/{tid}/schedstat") as f:
+                cpu, wait, slices = (int(x) for x in f.read().split()[:3])
+            vol = invol = 0
+            with open(f"{base}/{tid}/status") as f:
+                for line in f:
+                    if line.startswith("voluntary_ctxt_switches"):
+                        vol = int(line.split()[1])
+                    elif line.startswith("nonvoluntary_ctxt_switches"):
+                        invol = int(line.split()[1])
+        except (OSError, ValueError):
+            continue
+        d = out.setdefault(comm, {"threads": 0, "cpu_ns": 0, "runq_wait_ns": 0, "slices": 0, "vol_cs": 0,
+                                  "invol_cs": 0})
+        d["threads"] += 1
+        d["cpu_ns"] += cpu
+        d["runq_wait_ns"] += wait
+        d["slices"] += slices
+        d["vol_cs"] += vol
+        d["invol_cs"] += invol
+    return out
+
+
+def _system_stats() -> Dict[str, int]:
+    """cgroup v2 CPU throttling and the machine's TLB-shootdown IPIs (best effort)."""
+    out: Dict[str, int] = {}
+    for path in ("/sys/fs/cgroup/cpu.stat",):
+        try:
+            with open(path) as f:
+                for line in f:
+                    k, v = line.split()
+                    if k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec"):
+                        out[k] = int(v)
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/proc/interrupts") as f:
+            for line in f:
+                name = line.split(":", 1)[0].strip()
+                if name in ("TLB", "RES", "CAL"):
+                    out[f"irq_{name}"] = sum(int(x) for x in line.split(":", 1)[1].split() if x.isdigit())
+    except OSError:
+        pass
+    return out
+
+
+def _delta(after, before):
+    if isinstance(after, dict):
+        return {k: _delta(v, before.get(k, 0 if not isinstance(v, dict) else {})) for k, v in after.items()}
+    return after - before
+
+
+def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", **kw) -> Dict:
+    """``measure`` plus, for the timed run: per-phase medians over all queues' spans, and the
+    scheduler view of every thread group (this process and the endpoint process) per poll."""
+    import json
+    import statistics
+    import tempfile
+
+    env = BenchEnv(queues, mode, **kw)
+    try:
+        if warmup:
+            env.run(warmup)
+        env.clear()
+        pids = {"autoscaler": os.getpid()}
+        if env.remote is not None:
+            pids["endpoints"] = env.remote.pid
+        with tempfile.TemporaryFile() as f:
+            for r in env.runners:
+                r.set_trace_fd(f.fileno())
+            t_before = {k: _task_stats(p) for k, p in pids.items()}
+            s_before = _system_stats()
+            wall = env.run(steps)
+            s_after = _system_stats()
+            t_after = {k: _task_stats(p) for k, p in pids.items()}
+            for r in env.runners:
+                r.set_trace_fd(-1)
+            f.seek(0)
+            spans = [json.loads(line) for line in f.read().decode().splitlines()]
+        res = env.collect(steps, wall)
+    finally:
+        env.close()
+    polls = max(1, queues * steps)
+    med = lambda k: round(statistics.median(s[k] for s in spans) / 1e3, 2)
+    sched = {}
+    for proc, groups in t_after.items():
+        for comm, d in groups.items():
+            b = t_before[proc].get(comm, {})
+            dd = _delta(d, b)
+            sched[f"{proc}/{comm}"] = {
+                "threads": d["threads"],
+                "cpu_us_per_poll": round(dd["cpu_ns"] / polls / 1e3, 2),
+                "runq_wait_us_per_poll": round(dd["runq_wait_ns"] / polls / 1e3, 3),
+                "slices_per_poll": round(dd["slices"] / polls, 3),
+                "vol_cs_per_poll": round(dd["vol_cs"] / polls, 3),
+                "invol_cs_per_poll": round(dd["invol_cs"] / polls, 4),
+            }
+    w = env.last_thread_sched
+    sched["autoscaler/ksa-worker"] = {
+        "threads": w["threads"],
+        "cpu_us_per_poll": round(w["cpu_ns"] / polls / 1e3, 2),
+        "runq_wait_us_per_poll": round(w["runq_wait_ns"] / polls / 1e3, 3),
+        "slices_per_poll": round(w["slices"] / polls, 3),
+        "vol_cs_per_poll": round(w["vol_cs"] / polls, 3),
+        "invol_cs_per_poll": round(w["invol_cs"] / polls, 4),
+    }
+    sysd = _delta(s_after, s_before)
+    return {"queues": queues, "mode": mode, **{k: v for k, v in kw.items() if k in ("servers", "pipeline", "busy_poll_ns")},
+            "summary": res.summary(), "signature_failures": res.signature_failures,
+            "phases_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
+                                 "patch_us": med("patch_latency_ns")},
+            "sched": sched, "system": sysd, "wall_s": round(wall, 4)}
