@@ -762,6 +762,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         return d;
       })
       .def("idle_ns", &Runner::idle_ns)
+      .def_property("cpus", &Runner::cpus, &Runner::set_cpus)
       .def("cancel", &Runner::cancel)
       .def("set_trace_fd", &Runner::set_trace_fd)
       .def("latencies", &Runner::latencies)
@@ -892,6 +893,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_attribute_cycle", &FakeSqsServer::set_attribute_cycle)
       .def("inject", &FakeSqsServer::inject)
       .def("set_latency", &FakeSqsServer::set_latency)
+      .def("set_cpus", &FakeSqsServer::set_cpus)
       .def("drop_connections", &FakeSqsServer::drop_connections)
       .def("requests", &FakeSqsServer::requests)
       .def("signature_failures", &FakeSqsServer::signature_failures)
@@ -924,6 +926,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_rbac", &FakeKubeServer::set_rbac)
       .def("forbidden", &FakeKubeServer::forbidden)
       .def("set_latency", &FakeKubeServer::set_latency)
+      .def("set_cpus", &FakeKubeServer::set_cpus)
       .def("drop_connections", &FakeKubeServer::drop_connections)
       .def("requests", &FakeKubeServer::requests)
       .def("gets", &FakeKubeServer::gets)

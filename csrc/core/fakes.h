@@ -38,6 +38,9 @@ class FakeSqsServer {
   ~FakeSqsServer();
   // Requires valid SigV4 signatures for (access_key, secret, region).
   void require_signature(std::string access_key, std::string secret, std::string region);
+  // CPUs for the server's threads (call before start(); the benchmark keeps a queue's fake
+  // endpoints in its worker's L3 domain).
+  void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
   Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
   void stop();
   int port() const;
@@ -63,6 +66,7 @@ class FakeSqsServer {
   void handle(const HttpRequest& req, HttpResponse* resp);
 
   std::unique_ptr<HttpServer> server_;
+  std::vector<int> cpus_;
   StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;
@@ -92,6 +96,7 @@ class FakeKubeServer {
   FakeKubeServer();
   ~FakeKubeServer();
   void require_token(std::string token);
+  void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
   Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
   void stop();
   int port() const;
@@ -143,6 +148,7 @@ class FakeKubeServer {
   static std::string status_json(int code, const std::string& reason, const std::string& message);
 
   std::unique_ptr<HttpServer> server_;
+  std::vector<int> cpus_;
   StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;

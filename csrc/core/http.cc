@@ -1,5 +1,7 @@
 #include "http.h"
 
+#include "affinity.h"
+
 #include <csignal>
 #include <mutex>
 
@@ -1319,6 +1321,7 @@ Status HttpServer::listen(const std::string& host, int port) {
   listen_fd_ = fd;
   acceptor_ = std::thread([this] {
     pthread_setname_np(pthread_self(), "ksa-accept");
+    pin_current_thread(cpus_);
     accept_loop();
   });
   return Status::OK();
@@ -1353,6 +1356,7 @@ void HttpServer::accept_loop() {
       auto done = std::make_shared<std::atomic<bool>>(false);
       workers_.push_back(Worker{std::thread([this, fd, done] {
                                   pthread_setname_np(pthread_self(), "ksa-serve");
+                                  pin_current_thread(cpus_);
                                   serve(fd);
                                   done->store(true, std::memory_order_release);
                                 }),

@@ -189,6 +189,8 @@ class HttpServer {
   uint64_t connections_accepted() const { return accepted_.load(); }
   // Close every open client connection after its in-flight response (idle-close test).
   void drop_connections();
+  // CPUs for the acceptor and connection threads (call before listen(); empty: unpinned).
+  void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
 
  private:
   void accept_loop();
@@ -211,6 +213,7 @@ class HttpServer {
   std::vector<Worker> workers_;
   std::atomic<uint64_t> served_{0};
   std::atomic<uint64_t> accepted_{0};
+  std::vector<int> cpus_;
 };
 
 // Self-signed certificate for `host` (DNS name or IP literal) -- fakes only.

@@ -322,6 +322,7 @@ void Supervisor::start(int64_t max_iterations) {
   for (auto& r : runners_) {
     threads_.emplace_back([this, r, max_iterations] {
       pthread_setname_np(pthread_self(), "ksa-worker");  // top -H / /proc/<pid>/task/*/comm
+      pin_current_thread(r->cpus());
       r->run(&stop_, max_iterations);
       ThreadSched ts;
       const bool have = read_thread_sched(&ts);

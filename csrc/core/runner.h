@@ -28,6 +28,7 @@
 #include <thread>
 #include <vector>
 
+#include "affinity.h"
 #include "clock.h"
 #include "kube.h"
 #include "log.h"
@@ -134,9 +135,13 @@ class Runner {
   std::shared_ptr<PodAutoScaler> scaler() const { return scaler_; }
   Nanos last_scale_up() const { return last_up_; }
   Nanos last_scale_down() const { return last_down_; }
+  // CPUs the thread running this worker is pinned to (Supervisor; empty: no pinning).
+  void set_cpus(CpuList cpus) { cpus_ = std::move(cpus); }
+  const CpuList& cpus() const { return cpus_; }
 
  private:
   void record(const IterationRecord& r);
+  CpuList cpus_;
 
   LoopConfig cfg_;
   std::shared_ptr<SqsClient> sqs_;

@@ -24,9 +24,11 @@ def main(argv=None) -> int:
     ap.add_argument("--tls", type=int, default=0)
     ap.add_argument("--sqs-latency-ns", type=int, default=0)
     ap.add_argument("--kube-latency-ns", type=int, default=0)
+    ap.add_argument("--cpus", default="", help="JSON list: the CPU list of each pair's threads")
     a = ap.parse_args(argv)
     nat = native()
-    sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns)
+    cpus = json.loads(a.cpus) if a.cpus else None
+    sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus)
     try:
         info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],
                 "kube": [{"url": k.url, "cert_pem": k.cert_pem} for k in kube]}

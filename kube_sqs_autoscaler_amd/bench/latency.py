@@ -83,17 +83,21 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
 
 
 def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
-                         kube_latency_ns: int = 0):
+                         kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None):
     """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues (queue q on pair
-    q % n_servers): the 200 <-> 0 attribute cycle per queue and one Deployment per queue."""
+    q % n_servers): the 200 <-> 0 attribute cycle per queue and one Deployment per queue.
+    ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned)."""
     sqs_servers, kube_servers = [], []
-    for _ in range(n_servers):
+    for i in range(n_servers):
         sqs = nat.FakeSqsServer()
         sqs.require_signature(AKID, SECRET, REGION)
-        sqs.start("127.0.0.1", 0, tls)
-        sqs.set_latency(sqs_latency_ns)
         kube = nat.FakeKubeServer()
         kube.require_token(TOKEN)
+        if cpus is not None:
+            sqs.set_cpus(cpus[i])
+            kube.set_cpus(cpus[i])
+        sqs.start("127.0.0.1", 0, tls)
+        sqs.set_latency(sqs_latency_ns)
         kube.start("127.0.0.1", 0, tls)
         kube.set_latency(kube_latency_ns)
         sqs_servers.append(sqs)
@@ -125,16 +129,18 @@ class RemoteEndpoints:
     what an autoscaler sees in production, where SQS and the apiserver are other machines'
     processes -- their threads do not share the autoscaler's process, allocator or CPU share."""
 
-    def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int):
+    def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int,
+                 cpus: Optional[List[List[int]]] = None):
         import json
         import subprocess
         import sys
 
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        extra = ["--cpus", json.dumps(cpus)] if cpus is not None else []
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "kube_sqs_autoscaler_amd.bench.fakeserve", "--queues", str(queues), "--pairs",
              str(n_servers), "--tls", str(int(tls)), "--sqs-latency-ns", str(sqs_latency_ns), "--kube-latency-ns",
-             str(kube_latency_ns)], cwd=root, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+             str(kube_latency_ns), *extra], cwd=root, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
         line = self.proc.stdout.readline()
         if not line:
             raise RuntimeError("fake endpoint process failed to start")
@@ -166,23 +172,37 @@ class BenchEnv:
 
     ``servers``: ``shared`` -- one fake SQS + apiserver pair in this process for every queue;
     ``per-queue`` -- one pair per queue, in this process; ``process`` -- one pair per queue in a
-    separate endpoint process (as production's remote endpoints, and as separate ranks see it)."""
+    separate endpoint process (as production's remote endpoints, and as separate ranks see it).
+
+    ``affinity``: ``none`` -- threads float; ``llc`` -- queue q's worker thread and its fake
+    endpoint pair are pinned to L3 domain q mod D (utils/topology.py), so each queue's traffic
+    stays on one CCD, as a rank per queue would (needs per-queue or process servers)."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
-                 busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared"):
+                 busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared", affinity: str = "none"):
         nat = native()
         self.nat = nat
         self.mode = mode
         self.pipeline = pipeline
         n_servers = 1 if servers == "shared" else queues
         self.remote = None
+        cpus = None
+        if affinity == "llc":
+            from ..utils.topology import plan
+
+            cpus = plan(queues)
+            if servers == "shared" and queues > 1:
+                raise ValueError("affinity=llc needs per-queue or process servers")
+        elif affinity != "none":
+            raise ValueError(f"affinity must be none or llc, not {affinity!r}")
+        self.cpus = cpus
         if servers == "process":
-            self.remote = RemoteEndpoints(queues, n_servers, tls, sqs_latency_ns, kube_latency_ns)
+            self.remote = RemoteEndpoints(queues, n_servers, tls, sqs_latency_ns, kube_latency_ns, cpus)
             self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
         elif servers in ("shared", "per-queue"):
             self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
-                                                                       kube_latency_ns)
+                                                                       kube_latency_ns, cpus)
         else:
             raise ValueError(f"servers must be shared, per-queue or process, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
@@ -232,7 +252,10 @@ class BenchEnv:
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
-            self.runners.append(nat.Runner(cfg, client, scaler, self.clock, log))
+            runner = nat.Runner(cfg, client, scaler, self.clock, log)
+            if cpus is not None:
+                runner.cpus = cpus[q]
+            self.runners.append(runner)
             self.targets.append(t)
 
     def run(self, iterations: int) -> float:
@@ -446,7 +469,8 @@ def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", 
         "invol_cs_per_poll": round(w["invol_cs"] / polls, 4),
     }
     sysd = _delta(s_after, s_before)
-    return {"queues": queues, "mode": mode, **{k: v for k, v in kw.items() if k in ("servers", "pipeline", "busy_poll_ns")},
+    return {"queues": queues, "mode": mode,
+            **{k: v for k, v in kw.items() if k in ("servers", "pipeline", "busy_poll_ns", "affinity")},
             "summary": res.summary(), "signature_failures": res.signature_failures,
             "phases_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
                                  "patch_us": med("patch_latency_ns")},

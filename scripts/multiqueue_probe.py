@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--busy-poll-us", type=int, nargs="+", default=[25])
     ap.add_argument("--servers", nargs="+", default=["shared", "per-queue", "process"])
     ap.add_argument("--queues", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--affinity", nargs="+", default=["none"])
     a = ap.parse_args()
     env = {"cpus_visible": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
     try:
@@ -35,11 +36,15 @@ def main() -> int:
     print(json.dumps({"env": env}), flush=True)
     for rnd in range(a.rounds):
         for bp in a.busy_poll_us:
-            for sv in a.servers:
-                for q in a.queues:
-                    d = measure_detailed(q, a.samples, 200, "scale", pipeline=True, busy_poll_ns=bp * 1000, servers=sv)
-                    d["round"] = rnd
-                    print(json.dumps(d), flush=True)
+            for aff in a.affinity:
+                for sv in a.servers:
+                    if aff == "llc" and sv == "shared":
+                        continue
+                    for q in a.queues:
+                        d = measure_detailed(q, a.samples, 200, "scale", pipeline=True, busy_poll_ns=bp * 1000,
+                                             servers=sv, affinity=aff)
+                        d["round"] = rnd
+                        print(json.dumps(d), flush=True)
     return 0
 
 
