@@ -50,8 +50,11 @@ class StopFlag {
   bool stopped() const { return stopped_.load(std::memory_order_acquire); }
   // Waits up to `d`; returns true when the full duration elapsed, false if stopped.
   bool wait_for(Nanos d) {
-    std::unique_lock<std::mutex> lk(mu_);
+    // Every worker of a Supervisor shares one StopFlag, and a zero poll period calls this on
+    // every poll: no lock unless there is something to wait for, or the workers serialise on
+    // this mutex (a futex round trip per poll once they collide).
     if (d <= 0) return !stopped();
+    std::unique_lock<std::mutex> lk(mu_);
     return !cv_wait_for(cv_, lk, d, [&] { return stopped(); });
   }
 

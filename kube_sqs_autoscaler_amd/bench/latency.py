@@ -429,18 +429,25 @@ def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", 
         pids = {"autoscaler": os.getpid()}
         if env.remote is not None:
             pids["endpoints"] = env.remote.pid
-        with tempfile.TemporaryFile() as f:
-            for r in env.runners:
+        # one span file per worker: a shared one would serialise the workers on its file
+        # position lock and perturb what is measured
+        files = [tempfile.TemporaryFile() for _ in env.runners]
+        try:
+            for r, f in zip(env.runners, files):
                 r.set_trace_fd(f.fileno())
             t_before = {k: _task_stats(p) for k, p in pids.items()}
             s_before = _system_stats()
             wall = env.run(steps)
             s_after = _system_stats()
             t_after = {k: _task_stats(p) for k, p in pids.items()}
-            for r in env.runners:
+            spans = []
+            for r, f in zip(env.runners, files):
                 r.set_trace_fd(-1)
-            f.seek(0)
-            spans = [json.loads(line) for line in f.read().decode().splitlines()]
+                f.seek(0)
+                spans += [json.loads(line) for line in f.read().decode().splitlines()]
+        finally:
+            for f in files:
+                f.close()
         res = env.collect(steps, wall)
     finally:
         env.close()
