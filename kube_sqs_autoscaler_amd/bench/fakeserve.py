@@ -25,10 +25,12 @@ def main(argv=None) -> int:
     ap.add_argument("--sqs-latency-ns", type=int, default=0)
     ap.add_argument("--kube-latency-ns", type=int, default=0)
     ap.add_argument("--cpus", default="", help="JSON list: the CPU list of each pair's threads")
+    ap.add_argument("--queue-offset", type=int, default=0, help="number of the first bench queue served")
     a = ap.parse_args(argv)
     nat = native()
     cpus = json.loads(a.cpus) if a.cpus else None
-    sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus)
+    sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus,
+                                     a.queue_offset)
     try:
         info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],
                 "kube": [{"url": k.url, "cert_pem": k.cert_pem} for k in kube]}
@@ -41,7 +43,8 @@ def main(argv=None) -> int:
                     "sqs_connections": sum(s.connections() for s in sqs),
                     "kube_connections": sum(k.connections() for k in kube),
                     "signature_failures": sum(s.signature_failures() for s in sqs),
-                    "replicas": [kube[q % len(kube)].replicas("bench", deployment_name(q)) for q in range(a.queues)],
+                    "replicas": [kube[q % len(kube)].replicas("bench", deployment_name(a.queue_offset + q))
+                                 for q in range(a.queues)],
                 }), flush=True)
             elif cmd == "quit":
                 break

@@ -83,10 +83,10 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
 
 
 def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
-                         kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None):
-    """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues (queue q on pair
-    q % n_servers): the 200 <-> 0 attribute cycle per queue and one Deployment per queue.
-    ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned)."""
+                         kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None, offset: int = 0):
+    """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues numbered from
+    ``offset`` (queue offset+q on pair q % n_servers): the 200 <-> 0 attribute cycle per queue
+    and one Deployment per queue. ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned)."""
     sqs_servers, kube_servers = [], []
     for i in range(n_servers):
         sqs = nat.FakeSqsServer()
@@ -104,8 +104,8 @@ def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sq
         kube_servers.append(kube)
     for q in range(queues):
         si = q % n_servers
-        sqs_servers[si].set_attribute_cycle(queue_url(sqs_servers[si].url, q), [HIGH, LOW])
-        kube_servers[si].add_deployment("bench", deployment_name(q), 1)
+        sqs_servers[si].set_attribute_cycle(queue_url(sqs_servers[si].url, offset + q), [HIGH, LOW])
+        kube_servers[si].add_deployment("bench", deployment_name(offset + q), 1)
     return sqs_servers, kube_servers
 
 
@@ -130,7 +130,7 @@ class RemoteEndpoints:
     processes -- their threads do not share the autoscaler's process, allocator or CPU share."""
 
     def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int,
-                 cpus: Optional[List[List[int]]] = None):
+                 cpus: Optional[List[List[int]]] = None, offset: int = 0):
         import json
         import subprocess
         import sys
@@ -140,7 +140,8 @@ class RemoteEndpoints:
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "kube_sqs_autoscaler_amd.bench.fakeserve", "--queues", str(queues), "--pairs",
              str(n_servers), "--tls", str(int(tls)), "--sqs-latency-ns", str(sqs_latency_ns), "--kube-latency-ns",
-             str(kube_latency_ns), *extra], cwd=root, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+             str(kube_latency_ns), "--queue-offset", str(offset), *extra], cwd=root, stdin=subprocess.PIPE,
+            stdout=subprocess.PIPE, text=True)
         line = self.proc.stdout.readline()
         if not line:
             raise RuntimeError("fake endpoint process failed to start")
@@ -172,7 +173,8 @@ class BenchEnv:
 
     ``servers``: ``shared`` -- one fake SQS + apiserver pair in this process for every queue;
     ``per-queue`` -- one pair per queue, in this process; ``process`` -- one pair per queue in a
-    separate endpoint process (as production's remote endpoints, and as separate ranks see it).
+    separate endpoint process (as production's remote endpoints); ``processes`` -- one endpoint
+    process per queue (as separate ranks see it: no two queues' endpoint threads share a process).
 
     ``affinity``: ``none`` -- threads float; ``llc`` -- queue q's worker thread and its fake
     endpoint pair are pinned to L3 domain q mod D (utils/topology.py), so each queue's traffic
@@ -197,14 +199,22 @@ class BenchEnv:
         elif affinity != "none":
             raise ValueError(f"affinity must be none or llc, not {affinity!r}")
         self.cpus = cpus
+        self.remotes = []
         if servers == "process":
             self.remote = RemoteEndpoints(queues, n_servers, tls, sqs_latency_ns, kube_latency_ns, cpus)
+            self.remotes = [self.remote]
             self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
+        elif servers == "processes":
+            self.remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns,
+                                            [cpus[q]] if cpus is not None else None, offset=q) for q in range(queues)]
+            self.remote = self.remotes[0]
+            self.sqs_servers = [r.sqs[0] for r in self.remotes]
+            self.kube_servers = [r.kube[0] for r in self.remotes]
         elif servers in ("shared", "per-queue"):
             self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
                                                                        kube_latency_ns, cpus)
         else:
-            raise ValueError(f"servers must be shared, per-queue or process, not {servers!r}")
+            raise ValueError(f"servers must be shared, per-queue, process or processes, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
         self.clock = nat.RealClock()
         self._devnull = None
@@ -274,12 +284,15 @@ class BenchEnv:
         res = LatencyResult(queues=len(self.runners), mode=self.mode, steps=steps, pipeline=self.pipeline, wall_s=wall)
         for r in self.runners:
             res.samples.extend(r.latencies())
-        if self.remote is not None:
-            st = self.remote.stats()
-            res.sqs_requests, res.kube_requests = st["sqs_requests"], st["kube_requests"]
-            res.sqs_connections, res.kube_connections = st["sqs_connections"], st["kube_connections"]
-            res.signature_failures = st["signature_failures"]
-            res.final_replicas = st["replicas"]
+        if self.remotes:
+            for rem in self.remotes:
+                st = rem.stats()
+                res.sqs_requests += st["sqs_requests"]
+                res.kube_requests += st["kube_requests"]
+                res.sqs_connections += st["sqs_connections"]
+                res.kube_connections += st["kube_connections"]
+                res.signature_failures += st["signature_failures"]
+                res.final_replicas += st["replicas"]
             return res
         res.sqs_requests = sum(s.requests() for s in self.sqs_servers)
         res.kube_requests = sum(k.requests() for k in self.kube_servers)
@@ -295,8 +308,9 @@ class BenchEnv:
             r.clear_latencies()
 
     def close(self) -> None:
-        if self.remote is not None:
-            self.remote.close()
+        if self.remotes:
+            for rem in self.remotes:
+                rem.close()
         else:
             for s in self.sqs_servers:
                 s.stop()
@@ -427,8 +441,8 @@ def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", 
             env.run(warmup)
         env.clear()
         pids = {"autoscaler": os.getpid()}
-        if env.remote is not None:
-            pids["endpoints"] = env.remote.pid
+        for i, rem in enumerate(env.remotes):
+            pids[f"endpoints{i}" if len(env.remotes) > 1 else "endpoints"] = rem.pid
         # one span file per worker: a shared one would serialise the workers on its file
         # position lock and perturb what is measured
         files = [tempfile.TemporaryFile() for _ in env.runners]
