@@ -182,7 +182,8 @@ class BenchEnv:
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
-                 busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared", affinity: str = "none"):
+                 busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared", affinity: str = "none",
+                 log_level: str = "info"):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -217,14 +218,18 @@ class BenchEnv:
             raise ValueError(f"servers must be shared, per-queue, process or processes, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
         self.clock = nat.RealClock()
-        self._devnull = None
-        if log_fd is None:
-            self._devnull = os.open(os.devnull, os.O_WRONLY)
-            log_fd = self._devnull
+        # loggers="per-queue": a logger and an open file of its own per queue (as one process
+        # per queue has); "shared": one logger writing to one file, like the reference's global
+        self._devnulls = []
         self.loggers = []
         for _ in range(queues if loggers == "per-queue" else 1):
+            fd = log_fd
+            if fd is None:
+                fd = os.open(os.devnull, os.O_WRONLY)
+                self._devnulls.append(fd)
             lg = nat.Logger()
-            lg.set_sink_fd(log_fd)
+            lg.set_sink_fd(fd)
+            lg.set_level(log_level)
             self.loggers.append(lg)
         self.log = self.loggers[0]
         creds = static_provider(AKID, SECRET)
@@ -316,9 +321,9 @@ class BenchEnv:
                 s.stop()
             for k in self.kube_servers:
                 k.stop()
-        if self._devnull is not None:
-            os.close(self._devnull)
-            self._devnull = None
+        for fd in self._devnulls:
+            os.close(fd)
+        self._devnulls = []
 
 
 def phase_breakdown(steps: int = 2000, warmup: int = 200, **kw) -> Dict[str, float]:
@@ -491,7 +496,8 @@ def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", 
     }
     sysd = _delta(s_after, s_before)
     return {"queues": queues, "mode": mode,
-            **{k: v for k, v in kw.items() if k in ("servers", "pipeline", "busy_poll_ns", "affinity")},
+            **{k: v for k, v in kw.items() if k in ("servers", "pipeline", "busy_poll_ns", "affinity", "loggers",
+                                                    "log_level")},
             "summary": res.summary(), "signature_failures": res.signature_failures,
             "phases_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
                                  "patch_us": med("patch_latency_ns")},

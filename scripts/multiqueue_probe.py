@@ -28,6 +28,7 @@ def main() -> int:
     ap.add_argument("--queues", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--affinity", nargs="+", default=["none"])
     ap.add_argument("--loggers", nargs="+", default=["shared"])
+    ap.add_argument("--log-level", nargs="+", default=["info"])
     a = ap.parse_args()
     env = {"cpus_visible": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
     try:
@@ -42,12 +43,13 @@ def main() -> int:
                     if aff == "llc" and sv == "shared":
                         continue
                     for lg in a.loggers:
-                        for q in a.queues:
-                            d = measure_detailed(q, a.samples, 200, "scale", pipeline=True, busy_poll_ns=bp * 1000,
-                                                 servers=sv, affinity=aff, loggers=lg)
-                            d["round"] = rnd
-                            d["loggers"] = lg
-                            print(json.dumps(d), flush=True)
+                        for lv in a.log_level:
+                            for q in a.queues:
+                                d = measure_detailed(q, a.samples, 200, "scale", pipeline=True,
+                                                     busy_poll_ns=bp * 1000, servers=sv, affinity=aff, loggers=lg,
+                                                     log_level=lv)
+                                d["round"] = rnd
+                                print(json.dumps(d), flush=True)
     return 0
 
 
