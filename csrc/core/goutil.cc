@@ -144,14 +144,80 @@ std::string go_quote(const std::string& s) {
   return out;
 }
 
+namespace {
+
+// UTC calendar fields of a Unix time, by arithmetic (H. Hinnant's civil_from_days). Not
+// gmtime_r + strftime: glibc takes its process-wide tzset lock in both, and strftime also
+// re-runs tzset() -- with TZ unset that is a getenv, a free + strdup and a stat() of
+// /etc/localtime under the lock, on every call. Every SigV4 signature (X-Amz-Date) and every
+// log line formats a time, so workers tracking different queues serialised on that lock; one
+// process per queue never did.
+struct UtcFields {
+  int64_t year;
+  unsigned month, day, hour, minute, second;
+};
+
+UtcFields utc_fields(int64_t unix_nanos) {
+  int64_t secs = unix_nanos / 1000000000LL;
+  if (unix_nanos < 0 && unix_nanos % 1000000000LL) secs -= 1;  // floor
+  int64_t days = secs / 86400;
+  int64_t rem = secs % 86400;
+  if (rem < 0) {
+    rem += 86400;
+    days -= 1;
+  }
+  const int64_t z = days + 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const unsigned doe = static_cast<unsigned>(z - era * 146097);
+  const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const unsigned mp = (5 * doy + 2) / 153;
+  UtcFields f;
+  f.day = doy - (153 * mp + 2) / 5 + 1;
+  f.month = mp < 10 ? mp + 3 : mp - 9;
+  f.year = static_cast<int64_t>(yoe) + era * 400 + (f.month <= 2);
+  f.hour = static_cast<unsigned>(rem / 3600);
+  f.minute = static_cast<unsigned>(rem % 3600 / 60);
+  f.second = static_cast<unsigned>(rem % 60);
+  return f;
+}
+
+// Appends v as exactly `width` decimal digits (v < 10^width).
+char* put_digits(char* p, uint64_t v, int width) {
+  for (int i = width - 1; i >= 0; --i) {
+    p[i] = static_cast<char>('0' + v % 10);
+    v /= 10;
+  }
+  return p + width;
+}
+
+// "%Y" of strftime: the year in decimal, at least 4 digits here (int64 nanoseconds only span
+// the years 1677..2262, so this is always four).
+char* put_year(char* p, int64_t y) {
+  if (y >= 0 && y <= 9999) return put_digits(p, static_cast<uint64_t>(y), 4);
+  const std::string s = std::to_string(y);
+  for (char c : s) *p++ = c;
+  return p;
+}
+
+}  // namespace
+
 std::string rfc3339_utc(int64_t unix_nanos) {
-  time_t secs = static_cast<time_t>(unix_nanos / 1000000000LL);
-  if (unix_nanos < 0 && unix_nanos % 1000000000LL) secs -= 1;
-  struct tm tm;
-  gmtime_r(&secs, &tm);
-  char buf[32];
-  std::strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%SZ", &tm);
-  return buf;
+  const UtcFields f = utc_fields(unix_nanos);
+  char buf[48];
+  char* p = put_year(buf, f.year);
+  *p++ = '-';
+  p = put_digits(p, f.month, 2);
+  *p++ = '-';
+  p = put_digits(p, f.day, 2);
+  *p++ = 'T';
+  p = put_digits(p, f.hour, 2);
+  *p++ = ':';
+  p = put_digits(p, f.minute, 2);
+  *p++ = ':';
+  p = put_digits(p, f.second, 2);
+  *p++ = 'Z';
+  return std::string(buf, static_cast<size_t>(p - buf));
 }
 
 namespace {
@@ -232,12 +298,17 @@ bool parse_rfc3339(const std::string& s, int64_t* unix_nanos) {
 }
 
 std::string amz_date(int64_t unix_nanos) {
-  time_t secs = static_cast<time_t>(unix_nanos / 1000000000LL);
-  struct tm tm;
-  gmtime_r(&secs, &tm);
-  char buf[32];
-  std::strftime(buf, sizeof buf, "%Y%m%dT%H%M%SZ", &tm);
-  return buf;
+  const UtcFields f = utc_fields(unix_nanos);
+  char buf[48];
+  char* p = put_year(buf, f.year);
+  p = put_digits(p, f.month, 2);
+  p = put_digits(p, f.day, 2);
+  *p++ = 'T';
+  p = put_digits(p, f.hour, 2);
+  p = put_digits(p, f.minute, 2);
+  p = put_digits(p, f.second, 2);
+  *p++ = 'Z';
+  return std::string(buf, static_cast<size_t>(p - buf));
 }
 
 }  // namespace ksa

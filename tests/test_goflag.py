@@ -186,3 +186,20 @@ def test_float_flag_usage_and_errors():
         bad.parse(["-qps=x"])
     with pytest.raises(FlagError, match='invalid value "1e999" for flag -qps: value out of range'):
         bad.parse(["-qps=1e999"])
+
+
+def test_utc_formatting_matches_the_calendar(nat):
+    """rfc3339_utc / amz_date (X-Amz-Date) are formatted by arithmetic, not gmtime_r + strftime
+    (glibc's tzset lock, taken per call, serialised the workers): same text as a calendar
+    library over the whole int64-nanosecond range, negative times and leap days included."""
+    import datetime
+    import random
+
+    rng = random.Random(7)
+    cases = [0, -1, 1, 86399 * 10**9, -86400 * 10**9, 951782400 * 10**9, 4107542399 * 10**9 + 999_999_999,
+             -(2**63), 2**63 - 1, 1700000000 * 10**9] + [rng.randrange(-(2**63), 2**63) for _ in range(2000)]
+    epoch = datetime.datetime(1970, 1, 1)
+    for ns in cases:
+        dt = epoch + datetime.timedelta(microseconds=ns // 1000)  # floor, like time.Unix
+        assert nat.rfc3339_utc(ns) == dt.strftime("%Y-%m-%dT%H:%M:%SZ"), ns
+        assert nat.amz_date(ns) == dt.strftime("%Y%m%dT%H%M%SZ"), ns
