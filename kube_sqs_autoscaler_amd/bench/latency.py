@@ -190,15 +190,21 @@ class BenchEnv:
         self.pipeline = pipeline
         n_servers = 1 if servers == "shared" else queues
         self.remote = None
-        cpus = None
+        cpus = worker_cpus = None
         if affinity == "llc":
             from ..utils.topology import plan
 
-            cpus = plan(queues)
+            cpus = worker_cpus = plan(queues)
             if servers == "shared" and queues > 1:
                 raise ValueError("affinity=llc needs per-queue or process servers")
+        elif affinity.startswith("{"):
+            # explicit placement (probes): {"workers": [[cpu, ...] per queue], "servers": [...]}
+            import json
+
+            spec = json.loads(affinity)
+            worker_cpus, cpus = spec.get("workers"), spec.get("servers")
         elif affinity != "none":
-            raise ValueError(f"affinity must be none or llc, not {affinity!r}")
+            raise ValueError(f"affinity must be none, llc or a JSON placement, not {affinity!r}")
         self.cpus = cpus
         self.remotes = []
         if servers == "process":
@@ -268,8 +274,8 @@ class BenchEnv:
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
             runner = nat.Runner(cfg, client, scaler, self.clock, log)
-            if cpus is not None:
-                runner.cpus = cpus[q]
+            if worker_cpus is not None:
+                runner.cpus = worker_cpus[q]
             self.runners.append(runner)
             self.targets.append(t)
 
