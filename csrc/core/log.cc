@@ -81,6 +81,12 @@ Logger::Sink fd_sink(int fd) {
 
 }  // namespace
 
+size_t LineGate::slot_index() {
+  static std::atomic<size_t> next{0};
+  thread_local const size_t idx = next.fetch_add(1, std::memory_order_relaxed) % kSlots;
+  return idx;
+}
+
 Logger::Logger() : base_unix_ns_(wall_now_ns()), shared_(std::make_shared<Shared>()) {
   shared_->sink = fd_sink(2);
   shared_->time = wall_now_ns;
@@ -191,12 +197,10 @@ void Logger::log(Level l, const std::string& msg, const Fields& fields) {
     std::string line = format(l, msg, fields, wall_now_ns());
     line.push_back('\n');
     if (line.size() <= PIPE_BUF) {  // one atomic write(2), on pipes too
-      std::shared_lock<std::shared_mutex> lk(shared_->fd_mu);
-      write_line(fd, line);
+      shared_->gate.shared([&] { write_line(fd, line); });
       return;
     }
-    std::unique_lock<std::shared_mutex> lk(shared_->fd_mu);
-    write_line(fd, line);
+    shared_->gate.exclusive([&] { write_line(fd, line); });
     return;
   }
   Sink sink;

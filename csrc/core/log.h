@@ -19,12 +19,54 @@
 #include <functional>
 #include <memory>
 #include <mutex>
-#include <shared_mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
 namespace ksa {
+
+// Lets lines of at most PIPE_BUF bytes (one atomic write(2) each) go out concurrently while a
+// longer line -- possibly several writes -- goes out alone. A reader/writer lock would do, but
+// its lock word is written by every line of every worker: one cache line bouncing between the
+// cores (and sockets) of all tracked queues on every poll. Here each thread announces itself in
+// a slot of its own cache line; the rare long-line writer raises a flag and waits for the slots
+// to drain (Dekker-style: both sides store, then load, sequentially consistent).
+class LineGate {
+ public:
+  template <class F>
+  void shared(F&& write) {
+    Slot& s = slots_[slot_index()];
+    s.n.fetch_add(1, std::memory_order_seq_cst);
+    if (long_.load(std::memory_order_seq_cst) == 0) {
+      write();
+      s.n.fetch_sub(1, std::memory_order_release);
+      return;
+    }
+    s.n.fetch_sub(1, std::memory_order_release);
+    std::lock_guard<std::mutex> lk(mu_);  // behind the long line
+    write();
+  }
+  template <class F>
+  void exclusive(F&& write) {
+    std::lock_guard<std::mutex> lk(mu_);
+    long_.store(1, std::memory_order_seq_cst);
+    for (auto& s : slots_)
+      while (s.n.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    write();
+    long_.store(0, std::memory_order_release);
+  }
+
+ private:
+  static constexpr size_t kSlots = 64;
+  struct alignas(64) Slot {
+    std::atomic<int> n{0};
+  };
+  static size_t slot_index();
+  Slot slots_[kSlots];
+  alignas(64) std::atomic<int> long_{0};
+  std::mutex mu_;
+};
 
 enum class Level : int { Panic = 0, Fatal = 1, Error = 2, Warn = 3, Info = 4, Debug = 5, Trace = 6 };
 
@@ -52,9 +94,9 @@ class Logger {
   void set_sink(Sink s);
   // Output to a file descriptor (the default is fd 2). Each line is one write(2), which the
   // kernel keeps whole for pipes (up to PIPE_BUF), regular files and terminals, so a line on the
-  // wall clock is formatted and written without taking the logger's mutex: workers tracking
-  // different queues only share a reader lock, which a line longer than PIPE_BUF (possibly
-  // several writes) takes exclusively so nothing interleaves with its pieces.
+  // wall clock is formatted and written without taking the logger's mutex, and without
+  // writing any memory the workers of other queues write (LineGate); a line longer than
+  // PIPE_BUF (possibly several writes) goes out alone so nothing interleaves with its pieces.
   void set_sink_fd(int fd);
   void set_time_source(TimeSource t);
   // Fields appended to every entry of this logger (e.g. queue=... in multi-queue mode).
@@ -75,13 +117,13 @@ class Logger {
   int64_t base_unix_ns_;  // logrus' baseTimestamp (package init) for the TTY layout
   struct Shared {
     std::mutex mu;
-    // fd sink: a line of at most PIPE_BUF bytes is one atomic write(2), so those writers share
-    // this lock; a longer line may take several writes and holds it exclusively, so no short
-    // line can land between its pieces.
-    std::shared_mutex fd_mu;
+    // fd sink: a line of at most PIPE_BUF bytes is one atomic write(2), so those writers go
+    // concurrently; a longer line may take several writes and goes alone, so no short line can
+    // land between its pieces.
+    LineGate gate;
     Sink sink;
     TimeSource time;
-    std::atomic<int> fd{2};                // >= 0: `sink` writes to this fd (lock-free path)
+    alignas(64) std::atomic<int> fd{2};    // >= 0: `sink` writes to this fd (lock-free path)
     std::atomic<bool> custom_time{false};  // set_time_source was called
   };
   Level level_ = Level::Info;

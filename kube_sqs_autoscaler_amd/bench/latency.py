@@ -197,6 +197,12 @@ class BenchEnv:
             cpus = worker_cpus = plan(queues)
             if servers == "shared" and queues > 1:
                 raise ValueError("affinity=llc needs per-queue or process servers")
+        elif affinity == "ccd":
+            from ..utils.topology import plan_queue_ccds
+
+            if servers == "shared" and queues > 1:
+                raise ValueError("affinity=ccd needs per-queue or process servers")
+            worker_cpus, cpus = plan_queue_ccds(queues)
         elif affinity.startswith("{"):
             # explicit placement (probes): {"workers": [[cpu, ...] per queue], "servers": [...]}
             import json
@@ -204,7 +210,7 @@ class BenchEnv:
             spec = json.loads(affinity)
             worker_cpus, cpus = spec.get("workers"), spec.get("servers")
         elif affinity != "none":
-            raise ValueError(f"affinity must be none, llc or a JSON placement, not {affinity!r}")
+            raise ValueError(f"affinity must be none, llc, ccd or a JSON placement, not {affinity!r}")
         self.cpus = cpus
         self.remotes = []
         if servers == "process":

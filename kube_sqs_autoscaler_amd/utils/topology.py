@@ -59,3 +59,47 @@ def plan(n: int, domains: Optional[List[List[int]]] = None) -> List[List[int]]:
     if not doms:
         return [[] for _ in range(n)]
     return [doms[i % len(doms)] for i in range(n)]
+
+
+def physical_cores(domain: List[int], sys_cpu: str = SYS_CPU) -> List[List[int]]:
+    """The physical cores of one domain, each as its SMT sibling list (ordered by first CPU)."""
+    allowed = set(domain)
+    seen, cores = set(), []
+    for c in sorted(domain):
+        if c in seen:
+            continue
+        try:
+            with open(f"{sys_cpu}/cpu{c}/topology/thread_siblings_list") as f:
+                sib = sorted(allowed.intersection(parse_cpu_list(f.read())))
+        except OSError:
+            sib = [c]
+        seen.update(sib)
+        cores.append(sib)
+    return cores
+
+
+def plan_cores(n: int, domains: Optional[List[List[int]]] = None) -> List[List[int]]:
+    """One logical CPU on a distinct physical core for each of n busy-polling workers, filling
+    one L3 domain before the next (compact: whatever the workers share stays in one L3) and
+    never putting two workers on SMT siblings of one core. Wraps around when n exceeds the
+    cores available."""
+    doms = domains if domains is not None else llc_domains()
+    cores = [core for d in doms for core in physical_cores(d)]
+    if not cores:
+        return [[] for _ in range(n)]
+    return [[cores[i % len(cores)][0]] for i in range(n)]
+
+
+def plan_queue_ccds(n: int, endpoint_cores: int = 2,
+                    domains: Optional[List[List[int]]] = None) -> "tuple[List[List[int]], List[List[int]]]":
+    """Benchmark placement, one L3 domain per tracked queue (as one rank per queue gets):
+    queue i's worker on the first core of domain i, its fake endpoints on the next
+    ``endpoint_cores`` cores of that domain (SMT siblings included). Returns (workers, endpoints)."""
+    doms = domains if domains is not None else llc_domains()
+    workers, endpoints = [], []
+    for i in range(n):
+        cores = physical_cores(doms[i % len(doms)])
+        workers.append([cores[0][0]])
+        ep = [c for core in cores[1:1 + endpoint_cores] for c in core]
+        endpoints.append(ep or cores[0])
+    return workers, endpoints
