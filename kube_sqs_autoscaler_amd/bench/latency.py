@@ -445,9 +445,10 @@ def _delta(after, before):
     return after - before
 
 
-def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", **kw) -> Dict:
+def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", sync=None, **kw) -> Dict:
     """``measure`` plus, for the timed run: per-phase medians over all queues' spans, and the
-    scheduler view of every thread group (this process and the endpoint process) per poll."""
+    scheduler view of every thread group (this process and the endpoint process) per poll.
+    ``sync``: called after the warm-up, right before the timed run (a barrier across ranks)."""
     import json
     import statistics
     import tempfile
@@ -457,6 +458,8 @@ def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", 
         if warmup:
             env.run(warmup)
         env.clear()
+        if sync is not None:
+            sync()
         pids = {"autoscaler": os.getpid()}
         for i, rem in enumerate(env.remotes):
             pids[f"endpoints{i}" if len(env.remotes) > 1 else "endpoints"] = rem.pid
