@@ -791,6 +791,9 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["slices"] = t.slices;
         d["vol_cs"] = t.vol_cs;
         d["invol_cs"] = t.invol_cs;
+        d["utime_ns"] = t.utime_ns;
+        d["stime_ns"] = t.stime_ns;
+        d["minflt"] = t.minflt;
         return d;
       });
 

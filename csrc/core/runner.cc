@@ -1,6 +1,7 @@
 #include "runner.h"
 
 #include <pthread.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -300,6 +301,12 @@ bool read_thread_sched(ThreadSched* out) {
   std::fclose(f);
   if (n != 3) return false;
   out->threads = 1;
+  struct rusage ru;
+  if (getrusage(RUSAGE_THREAD, &ru) == 0) {
+    out->utime_ns = static_cast<int64_t>(ru.ru_utime.tv_sec) * 1000000000LL + ru.ru_utime.tv_usec * 1000LL;
+    out->stime_ns = static_cast<int64_t>(ru.ru_stime.tv_sec) * 1000000000LL + ru.ru_stime.tv_usec * 1000LL;
+    out->minflt = ru.ru_minflt;
+  }
   out->cpu_ns = cpu;
   out->runq_wait_ns = wait;
   out->slices = slices;

@@ -176,7 +176,13 @@ struct ThreadSched {
   int64_t slices = 0;
   int64_t vol_cs = 0;
   int64_t invol_cs = 0;
+  int64_t utime_ns = 0;  // getrusage(RUSAGE_THREAD): user / system CPU, minor page faults
+  int64_t stime_ns = 0;
+  int64_t minflt = 0;
   void add(const ThreadSched& o) {
+    utime_ns += o.utime_ns;
+    stime_ns += o.stime_ns;
+    minflt += o.minflt;
     threads += o.threads;
     cpu_ns += o.cpu_ns;
     runq_wait_ns += o.runq_wait_ns;

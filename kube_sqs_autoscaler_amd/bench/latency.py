@@ -508,6 +508,9 @@ def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", 
         "slices_per_poll": round(w["slices"] / polls, 3),
         "vol_cs_per_poll": round(w["vol_cs"] / polls, 3),
         "invol_cs_per_poll": round(w["invol_cs"] / polls, 4),
+        "user_us_per_poll": round(w["utime_ns"] / polls / 1e3, 2),
+        "sys_us_per_poll": round(w["stime_ns"] / polls / 1e3, 2),
+        "minflt_per_poll": round(w["minflt"] / polls, 4),
     }
     sysd = _delta(s_after, s_before)
     return {"queues": queues, "mode": mode,

@@ -19,20 +19,23 @@ def _rank(i, n, barrier, out, samples):
     aff = json.dumps({"workers": [w[i]], "servers": [e[i]]})
     d = measure_detailed(1, samples, 200, "scale", sync=barrier.wait, pipeline=True, busy_poll_ns=25000,
                          servers="processes", affinity=aff)
-    out.put((i, d["summary"]["p50_ms"], d["phases_median_us"]))
+    out.put((i, d["summary"]["p50_ms"], d["phases_median_us"], d["sched"]["autoscaler/ksa-worker"]))
 
 
 def main():
     from kube_sqs_autoscaler_amd.bench.latency import measure_detailed
 
+    print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith(("MALLOC", "GLIBC", "LD_", "OMP"))}}),
+          flush=True)
     samples = 2000
     ctx = mp.get_context("spawn")
     for rnd in range(3):
-        for n in (1, 2, 4, 8):
+        for n in (1, 8):
             d = measure_detailed(n, samples, 200, "scale", pipeline=True, busy_poll_ns=25000, servers="processes",
                                  affinity="ccd")
             print(json.dumps({"kind": "threads", "n": n, "round": rnd, "p50_ms": d["summary"]["p50_ms"],
-                              "phases": d["phases_median_us"]}), flush=True)
+                              "phases": d["phases_median_us"], "worker": d["sched"]["autoscaler/ksa-worker"]}),
+                  flush=True)
             barrier, out = ctx.Barrier(n), ctx.Queue()
             ps = [ctx.Process(target=_rank, args=(i, n, barrier, out, samples)) for i in range(n)]
             for p in ps:
@@ -41,7 +44,7 @@ def main():
             for p in ps:
                 p.join()
             print(json.dumps({"kind": "processes", "n": n, "round": rnd, "p50_ms_per_rank": [r[1] for r in res],
-                              "phases_rank0": res[0][2]}), flush=True)
+                              "phases_rank0": res[0][2], "workers": [r[3] for r in res]}), flush=True)
 
 
 if __name__ == "__main__":
