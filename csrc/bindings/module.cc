@@ -763,6 +763,9 @@ PYBIND11_MODULE(_ksa_native, m) {
       })
       .def("idle_ns", &Runner::idle_ns)
       .def_property("cpus", &Runner::cpus, &Runner::set_cpus)
+      .def("set_shared_state", [](Runner& r, uintptr_t addr) {
+        r.set_shared_state(addr ? reinterpret_cast<SharedWorkerState*>(addr) : nullptr);
+      })
       .def("cancel", &Runner::cancel)
       .def("set_trace_fd", &Runner::set_trace_fd)
       .def("latencies", &Runner::latencies)
@@ -771,6 +774,46 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_property_readonly("scaler", &Runner::scaler)
       .def_property_readonly("last_scale_up", &Runner::last_scale_up)
       .def_property_readonly("last_scale_down", &Runner::last_scale_down);
+
+  // ---- process-per-queue fleet: worker state in shared memory (procfleet.py) ----
+  auto ws = [](uintptr_t addr) { return reinterpret_cast<SharedWorkerState*>(addr); };
+  m.def("shared_worker_state_size", [] { return sizeof(SharedWorkerState); });
+  m.def("init_shared_worker_state", [](uintptr_t addr) { init_shared_worker_state(reinterpret_cast<void*>(addr)); });
+  m.def("read_shared_worker_state", [ws](uintptr_t addr) {
+    SharedWorkerState* s = ws(addr);
+    static const char* names[] = {"polls", "depth_errors", "scale_ups", "scale_downs", "noop_ups", "noop_downs",
+                                  "cooldown_skips_up", "cooldown_skips_down", "failed_ups", "failed_downs",
+                                  "speculative_reads", "speculative_reads_used", "speculative_reads_gated",
+                                  "apiserver_reads", "latency_samples"};
+    static_assert(sizeof(names) / sizeof(names[0]) == SharedWorkerState::kNumCounters, "counter names");
+    py::dict d;
+    for (int i = 0; i < SharedWorkerState::kNumCounters; ++i)
+      d[names[i]] = s->counters[i].load(std::memory_order_acquire);
+    d["progress_ns"] = s->progress_ns.load(std::memory_order_acquire);
+    d["last_depth"] = s->last_depth.load(std::memory_order_relaxed);
+    d["last_replicas"] = s->last_replicas.load(std::memory_order_relaxed);
+    d["latency_sum_ns"] = s->lat_sum_ns.load(std::memory_order_relaxed);
+    d["status"] = s->status.load(std::memory_order_acquire);
+    d["control"] = s->control.load(std::memory_order_acquire);
+    d["max_override"] = s->max_override.load(std::memory_order_relaxed);
+    d["iterations"] = s->iterations.load(std::memory_order_relaxed);
+    return d;
+  });
+  m.def("shared_worker_latencies", [ws](uintptr_t addr) {
+    SharedWorkerState* s = ws(addr);
+    const uint64_t n = s->counters[SharedWorkerState::kLatencySamples].load(std::memory_order_acquire);
+    const uint64_t keep = std::min<uint64_t>(n, SharedWorkerState::kRing);
+    std::vector<int64_t> out;
+    out.reserve(keep);
+    for (uint64_t i = n - keep; i < n; ++i)
+      out.push_back(s->lat_ring[i % SharedWorkerState::kRing].load(std::memory_order_relaxed));
+    return out;
+  });
+  m.def("set_shared_worker_control", [ws](uintptr_t addr, int32_t c) { ws(addr)->control.store(c, std::memory_order_release); });
+  m.def("set_shared_worker_status", [ws](uintptr_t addr, int32_t c) { ws(addr)->status.store(c, std::memory_order_release); });
+  m.def("set_shared_worker_max", [ws](uintptr_t addr, int64_t v) { ws(addr)->max_override.store(v, std::memory_order_relaxed); });
+  m.def("set_shared_worker_iterations", [ws](uintptr_t addr, int64_t v) { ws(addr)->iterations.store(v, std::memory_order_relaxed); });
+  m.def("set_shared_worker_progress", [ws](uintptr_t addr, int64_t v) { ws(addr)->progress_ns.store(v, std::memory_order_release); });
 
   py::class_<Supervisor, std::shared_ptr<Supervisor>>(m, "Supervisor")
       .def(py::init<>())

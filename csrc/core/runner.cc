@@ -9,6 +9,7 @@
 #include <functional>
 #include <cmath>
 #include <limits>
+#include <new>
 
 #include "json.h"
 
@@ -82,6 +83,10 @@ IterationRecord Runner::step(StopFlag* stop) {
 }
 
 IterationRecord Runner::poll_once() {
+  if (shared_) {  // the supervising process' GPU-capacity cap
+    const int64_t cap = shared_->max_override.load(std::memory_order_relaxed);
+    if (cap > 0 && cap != scaler_->max()) scaler_->set_max(cap);
+  }
   IterationRecord rec;
   rec.index = ++index_;
   const Nanos t0 = clock_->now();
@@ -219,8 +224,58 @@ void Runner::record(const IterationRecord& r) {
       }
     }
   }
+  if (shared_) mirror(r);
   if (trace_fd_ >= 0) write_trace(r);
   if (observer_) observer_(r);
+}
+
+SharedWorkerState* init_shared_worker_state(void* at) {
+  auto* s = new (at) SharedWorkerState;
+  for (auto& c : s->counters) c.store(0, std::memory_order_relaxed);
+  s->progress_ns.store(0, std::memory_order_relaxed);
+  s->last_depth.store(0, std::memory_order_relaxed);
+  s->last_replicas.store(-1, std::memory_order_relaxed);
+  s->lat_sum_ns.store(0, std::memory_order_relaxed);
+  s->status.store(SharedWorkerState::kStarting, std::memory_order_relaxed);
+  s->max_override.store(0, std::memory_order_relaxed);
+  s->iterations.store(-1, std::memory_order_relaxed);
+  s->control.store(SharedWorkerState::kWait, std::memory_order_relaxed);
+  for (auto& v : s->lat_ring) v.store(0, std::memory_order_relaxed);
+  std::atomic_thread_fence(std::memory_order_release);
+  return s;
+}
+
+void Runner::mirror(const IterationRecord& r) {
+  RunnerStats st;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    st = stats_;
+  }
+  using W = SharedWorkerState;
+  auto put = [&](int i, uint64_t v) { shared_->counters[i].store(v, std::memory_order_relaxed); };
+  put(W::kPolls, st.polls);
+  put(W::kDepthErrors, st.depth_errors);
+  put(W::kScaleUps, st.scale_ups);
+  put(W::kScaleDowns, st.scale_downs);
+  put(W::kNoopUps, st.noop_ups);
+  put(W::kNoopDowns, st.noop_downs);
+  put(W::kCooldownSkipsUp, st.cooldown_skips_up);
+  put(W::kCooldownSkipsDown, st.cooldown_skips_down);
+  put(W::kFailedUps, st.failed_ups);
+  put(W::kFailedDowns, st.failed_downs);
+  put(W::kSpeculativeReads, st.speculative_reads);
+  put(W::kSpeculativeReadsUsed, st.speculative_reads_used);
+  put(W::kSpeculativeReadsGated, st.speculative_reads_gated);
+  put(W::kApiserverReads, st.apiserver_reads);
+  shared_->last_depth.store(st.last_depth, std::memory_order_relaxed);
+  shared_->last_replicas.store(st.last_replicas, std::memory_order_relaxed);
+  if (r.patch_latency_ns >= 0) {
+    const uint64_t n = st.latency_samples;  // this sample is number n (1-based)
+    shared_->lat_ring[(n - 1) % SharedWorkerState::kRing].store(r.patch_latency_ns, std::memory_order_relaxed);
+    shared_->lat_sum_ns.fetch_add(r.patch_latency_ns, std::memory_order_relaxed);
+  }
+  // the count last, with release: a reader that sees it sees the ring entries before it
+  shared_->counters[W::kLatencySamples].store(st.latency_samples, std::memory_order_release);
 }
 
 std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std::string& queue,

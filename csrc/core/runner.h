@@ -96,6 +96,36 @@ struct RunnerStats {
   uint64_t latency_samples = 0;
 };
 
+// A worker's state mirrored into memory shared with a supervising process (the process-per-queue
+// fleet, kube_sqs_autoscaler_amd/parallel/procfleet.py): its counters, liveness and recent
+// poll->patch latencies for /metrics, /healthz and the benchmark, plus two words the parent
+// writes (a start/stop control and a max-pods override from the GPU-capacity cap). Lock-free
+// atomics only -- address-free on x86-64, so they work across processes -- and each word has one
+// writer: the worker for its state, the parent for the control words.
+struct SharedWorkerState {
+  enum Counter : int {
+    kPolls, kDepthErrors, kScaleUps, kScaleDowns, kNoopUps, kNoopDowns, kCooldownSkipsUp,
+    kCooldownSkipsDown, kFailedUps, kFailedDowns, kSpeculativeReads, kSpeculativeReadsUsed,
+    kSpeculativeReadsGated, kApiserverReads, kLatencySamples, kNumCounters
+  };
+  enum Control : int32_t { kWait = 0, kGo = 1, kStop = 2 };
+  enum Status : int32_t { kStarting = 0, kReady = 1, kRunning = 2, kExited = 3, kFailed = 4 };
+  static constexpr uint32_t kRing = 1 << 14;  // latency samples kept (the most recent)
+  alignas(64) std::atomic<uint64_t> counters[kNumCounters];
+  std::atomic<int64_t> progress_ns;  // CLOCK_MONOTONIC of the last progress (the worker process' heartbeat)
+  std::atomic<int64_t> last_depth;
+  std::atomic<int64_t> last_replicas;
+  std::atomic<int64_t> lat_sum_ns;
+  std::atomic<int32_t> status;
+  alignas(64) std::atomic<int64_t> max_override;  // parent -> worker: > 0 caps max-pods
+  std::atomic<int64_t> iterations;                // parent -> worker: polls to run (<= 0: until stopped)
+  std::atomic<int32_t> control;                   // parent -> worker
+  alignas(64) std::atomic<int64_t> lat_ring[kRing];
+};
+static_assert(std::atomic<int64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
+// Zero-initialises a SharedWorkerState in place (memory from a fresh shared mapping).
+SharedWorkerState* init_shared_worker_state(void* at);
+
 class Runner {
  public:
   Runner(LoopConfig cfg, std::shared_ptr<SqsClient> sqs, std::shared_ptr<PodAutoScaler> scaler,
@@ -137,11 +167,15 @@ class Runner {
   Nanos last_scale_down() const { return last_down_; }
   // CPUs the thread running this worker is pinned to (Supervisor; empty: no pinning).
   void set_cpus(CpuList cpus) { cpus_ = std::move(cpus); }
+  // Mirror the stats into `s` after every poll and follow its max-pods override (may be null).
+  void set_shared_state(SharedWorkerState* s) { shared_ = s; }
   const CpuList& cpus() const { return cpus_; }
 
  private:
   void record(const IterationRecord& r);
+  void mirror(const IterationRecord& r);
   CpuList cpus_;
+  SharedWorkerState* shared_ = nullptr;
 
   LoopConfig cfg_;
   std::shared_ptr<SqsClient> sqs_;

@@ -365,7 +365,96 @@ def phase_breakdown(steps: int = 2000, warmup: int = 200, **kw) -> Dict[str, flo
             "patch_us": med("patch_latency_ns")}
 
 
-def measure(queues: int, steps: int, warmup: int, mode: str = "scale", **kw) -> LatencyResult:
+def measure_processes(queues: int, steps: int, warmup: int, mode: str = "scale", tls: bool = False,
+                      pipeline: bool = True, busy_poll_ns: int = 0, sqs_latency_ns: int = 0, kube_latency_ns: int = 0,
+                      affinity: str = "none", log_level: str = "info", **_ignored) -> LatencyResult:
+    """``measure`` with every queue in a worker process of its own (``--worker-processes``,
+    parallel/procfleet.py) against one endpoint process per queue. Each worker runs
+    ``warmup + steps`` polls back to back and the last ``steps`` latencies of each are kept."""
+    from ..parallel.procfleet import ProcessFleet
+
+    nat = native()
+    worker_cpus = endpoint_cpus = None
+    if affinity == "ccd":
+        from ..utils.topology import plan_queue_ccds
+
+        worker_cpus, endpoint_cpus = plan_queue_ccds(queues)
+    remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns,
+                               [endpoint_cpus[q]] if endpoint_cpus is not None else None, offset=q)
+               for q in range(queues)]
+    creds = static_provider(AKID, SECRET)
+    targets = []
+    for q in range(queues):
+        targets.append(TargetConfig(queue_url=queue_url(remotes[q].sqs[0].url, q), deployment=deployment_name(q),
+                                    namespace="bench", poll_period_ns=0, scale_up_cool_down_ns=0,
+                                    scale_down_cool_down_ns=0, scale_up_messages=100, scale_down_messages=10,
+                                    max_pods=8, min_pods=1))
+
+    def build(q):
+        def make():
+            clock = nat.RealClock()
+            fd = os.open(os.devnull, os.O_WRONLY)
+            log = nat.Logger()
+            log.set_sink_fd(fd)
+            log.set_level(log_level)
+            sqs_ep, kube_ep = remotes[q].sqs[0], remotes[q].kube[0]
+            rest = RestConfig(host=kube_ep.url, bearer_token=TOKEN, insecure=tls)
+            sqs_tls = None
+            if tls:
+                sqs_tls = nat.TlsOptions()
+                sqs_tls.ca_pem = sqs_ep.cert_pem
+                rest.insecure = False
+                rest.ca_pem = kube_ep.cert_pem
+            t = targets[q]
+            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, clock, busy_poll_ns=busy_poll_ns)
+            scaler = new_pod_autoscaler(t, kube_api, log, clock)
+            sqs_api = new_sqs_api(REGION, clock, endpoint=sqs_ep.url, credentials=creds, tls=sqs_tls,
+                                  busy_poll_ns=busy_poll_ns)
+            cfg = nat.LoopConfig()
+            cfg.poll_period_ns = cfg.scale_up_cool_down_ns = cfg.scale_down_cool_down_ns = 0
+            cfg.scale_up_messages, cfg.scale_down_messages = 100, 10
+            cfg.prefetch = pipeline
+
+            class W:
+                runner = nat.Runner(cfg, new_sqs_client(t, sqs_api), scaler, clock, log)
+            return W
+        return make
+
+    fleet = None
+    try:
+        fleet = ProcessFleet([build(q) for q in range(queues)], targets, worker_cpus)
+        fleet.wait_ready()
+        t0 = time.perf_counter()
+        fleet.start(warmup + steps)
+        fleet.join()
+        wall = time.perf_counter() - t0
+        if any(c != 0 for c in fleet.exit_codes()):
+            raise RuntimeError(f"bench worker process failed: exit codes {fleet.exit_codes()}")
+        res = LatencyResult(queues=queues, mode=mode, steps=steps, pipeline=pipeline, wall_s=wall)
+        for w in fleet.workers:
+            res.samples.extend(w.runner.latencies()[-steps:])
+        for rem in remotes:
+            st = rem.stats()
+            res.sqs_requests += st["sqs_requests"]
+            res.kube_requests += st["kube_requests"]
+            res.sqs_connections += st["sqs_connections"]
+            res.kube_connections += st["kube_connections"]
+            res.signature_failures += st["signature_failures"]
+            res.final_replicas += st["replicas"]
+        return res
+    finally:
+        if fleet is not None:
+            fleet.close()
+        for rem in remotes:
+            rem.close()
+
+
+def measure(queues: int, steps: int, warmup: int, mode: str = "scale", workers: str = "threads",
+            **kw) -> LatencyResult:
+    """``workers``: ``threads`` (one process, a thread per queue) or ``processes`` (a worker
+    process per queue, ``measure_processes``)."""
+    if workers == "processes":
+        return measure_processes(queues, steps, warmup, mode, **kw)
     env = BenchEnv(queues, mode, **kw)
     try:
         if warmup:

@@ -78,7 +78,32 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
                            f"8-GPU node); the reference defaults to {REFERENCE_MAX_PODS}")
 
     multi = len(cfg.targets) > 1
-    workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
+    trace_fd = -1
+    if cfg.trace_file:
+        trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
+
+    if cfg.worker_processes:
+        # fork the workers first: before this process starts threads or touches the GPU
+        from .parallel.procfleet import ProcessFleet
+
+        def build(t):
+            def make():
+                w = autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi)
+                if trace_fd >= 0:
+                    w.runner.set_trace_fd(trace_fd)
+                return w
+            return make
+
+        fleet = ProcessFleet([build(t) for t in cfg.targets], cfg.targets)
+        workers = fleet.workers
+    else:
+        workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
+        if trace_fd >= 0:
+            for w in workers:
+                w.runner.set_trace_fd(trace_fd)
+        from .parallel.fleet import Fleet
+
+        fleet = Fleet(workers, cfg.worker_threads)
 
     capper = None
     if cfg.gpu_aware_max:
@@ -98,15 +123,6 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         if cfg.gpu_aware_max == "cluster":
             capper.start()
 
-    trace_fd = -1
-    if cfg.trace_file:
-        trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
-        for w in workers:
-            w.runner.set_trace_fd(trace_fd)
-
-    from .parallel.fleet import Fleet
-
-    fleet = Fleet(workers, cfg.worker_threads)
     metrics = None
     health = None
     if cfg.metrics_addr:
@@ -162,6 +178,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         while not fleet.wait(0.2):
             pass
         fleet.join()
+        if cfg.worker_processes and any(c not in (0, None) for c in fleet.exit_codes()):
+            log.log("error", f"worker process exit codes: {fleet.exit_codes()}")
         if lost.is_set():
             log.log("fatal", "leaderelection lost")
             return 1
@@ -179,6 +197,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
             capper.stop()
         if metrics is not None:
             metrics.stop()
+        if cfg.worker_processes:
+            fleet.close()
         if trace_fd >= 0:
             os.close(trace_fd)
     return 0

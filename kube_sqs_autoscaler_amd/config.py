@@ -28,6 +28,8 @@ Extensions (all off or reference-equivalent by default):
   decisions are the reference's (``models/oracle.py`` ``prefetch``). The early GET is only sent
   when the previous depth and the cool-downs say a scale call will follow (runner.h
   ``action_likely``), so an idle queue reads the apiserver no more often than the reference.
+* ``--worker-processes``: one worker process per tracked queue (parallel/procfleet.py) instead
+  of one thread per queue.
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
   ``--log-format``, ``--metrics-addr``, ``--trace-file``, ``--gpu-aware-max``.
 * ``--leader-elect`` (+ lease name/namespace/identity/timings): Lease-based leader election so
@@ -96,6 +98,7 @@ class Config:
     pipeline_reads: bool = True
     dry_run: bool = False
     worker_threads: int = 0
+    worker_processes: bool = False
     busy_poll_ns: int = 25_000
     kube_api_qps: float = 5.0
     kube_api_burst: int = 10
@@ -159,6 +162,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("sqs-protocol", "query", "SQS wire protocol: query (AWS Query/XML) or json (AWS JSON 1.0)")
     fs.duration("api-timeout", 30 * SECOND, "Per-request timeout for SQS and Kubernetes API calls")
     fs.int("worker-threads", 0, "Threads polling the tracked queues; 0 = one per queue (use fewer for hundreds of queues)")
+    fs.bool("worker-processes", False, "Run every tracked queue in a worker process of its own, like one reference process per queue (no per-poll cost shared between queues)")
     fs.bool("dry-run", False, "Shadow mode: poll and decide as usual, log the scaling that would happen, never write")
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap, on polls likely to scale (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.float64("kube-api-qps", 5.0, "Client-side limit on kube-apiserver requests per second for each tracked queue, as client-go's default rest client (0 disables)")
@@ -280,6 +284,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         pipeline_reads=fs["pipeline-reads"],
         dry_run=fs["dry-run"],
         worker_threads=fs["worker-threads"],
+        worker_processes=fs["worker-processes"],
         busy_poll_ns=fs["busy-poll"],
         kube_api_qps=fs["kube-api-qps"],
         kube_api_burst=fs["kube-api-burst"],
@@ -303,6 +308,8 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         raise FlagError("leader election needs lease-duration > renew-deadline > retry-period > 0")
     if cfg.gpu_aware_max not in ("", "local", "cluster"):
         raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty, local or cluster')
+    if cfg.worker_processes and cfg.worker_threads > 0:
+        raise FlagError("-worker-processes and -worker-threads cannot be combined")
     if cfg.gpus_per_pod < 1:
         raise FlagError(f'invalid value "{cfg.gpus_per_pod}" for flag -gpus-per-pod: must be >= 1')
     return cfg

@@ -1,0 +1,121 @@
+"""--worker-processes: one worker process per tracked queue (parallel/procfleet.py)."""
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+import yaml
+
+from kube_sqs_autoscaler_amd.config import TargetConfig
+from kube_sqs_autoscaler_amd.parallel.procfleet import ProcessFleet
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+AKID, SECRET, REGION, TOKEN = "AKIDPF", "pf/secret", "us-east-1", "pf-token"
+
+
+@pytest.fixture
+def servers(nat, tmp_path):
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, REGION)
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    kc = tmp_path / "kubeconfig"
+    kc.write_text(yaml.safe_dump({
+        "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+        "users": [{"name": "u", "user": {"token": TOKEN}}], "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+    env = {"AWS_ACCESS_KEY_ID": AKID, "AWS_SECRET_ACCESS_KEY": SECRET, "KUBE_CONFIG_PATH": str(kc)}
+    yield sqs, kube, env
+    sqs.stop()
+    kube.stop()
+
+
+def _specs(sqs, kube, depths):
+    specs = []
+    for i, depth in enumerate(depths):
+        url = f"{sqs.url}/123/q{i}"
+        sqs.set_attributes(url, {"ApproximateNumberOfMessages": depth})
+        kube.add_deployment("gpu", f"w{i}", 4)
+        specs += ["--queue", f"url={url},deployment=w{i},namespace=gpu,attribute-names=ApproximateNumberOfMessages"]
+    return specs
+
+
+def test_cli_worker_processes_scale_each_queue(servers, capfd):
+    from kube_sqs_autoscaler_amd.cli import main
+
+    sqs, kube, env = servers
+    specs = _specs(sqs, kube, ["500", "0", "50"])
+    rc = main([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+               "--scale-down-cool-down=0s", "--max-pods=6", "--worker-processes", *specs], environ=env, max_iterations=5)
+    assert rc == 0
+    assert [kube.replicas("gpu", f"w{i}") for i in range(3)] == [6, 1, 4]
+    err = capfd.readouterr().err
+    assert 'msg="Scale up successful. Replicas: 6" deployment=gpu/w0' in err
+    assert sqs.signature_failures() == 0
+
+
+def test_fleet_mirrors_stats_latencies_and_max_override(nat, servers):
+    """The supervisor sees each worker's counters and latencies through its shared slot, and a
+    max-pods override written there (the GPU-capacity cap) is applied by the worker."""
+    from kube_sqs_autoscaler_amd import autoscaler
+    from kube_sqs_autoscaler_amd.config import parse_args
+    from kube_sqs_autoscaler_amd.utils.log import make_logger
+
+    sqs, kube, env = servers
+    specs = _specs(sqs, kube, ["500", "500"])
+    cfg = parse_args([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=1ms",
+                      "--scale-up-cool-down=0s", "--max-pods=20", "--kube-api-qps=0", *specs], env)
+    rest = autoscaler.load_rest_config(cfg, env)
+    log = make_logger("error", "text")
+    clock = nat.RealClock()
+    builds = [lambda t=t: autoscaler.new_runner(t, cfg, rest, log, clock, environ=env) for t in cfg.targets]
+    fleet = ProcessFleet(builds, cfg.targets)
+    try:
+        fleet.workers[1].runner.scaler.max = 5  # the cap, before the first poll
+        fleet.start(8)
+        assert fleet.wait(30)
+        assert fleet.exit_codes() == [0, 0]
+        st = fleet.stats()
+        assert [s["polls"] for s in st] == [8, 8] and [s["scale_ups"] for s in st] == [8, 1]
+        assert kube.replicas("gpu", "w0") == 12 and kube.replicas("gpu", "w1") == 5
+        assert len(fleet.workers[0].runner.latencies()) == 8 and st[0]["latency_samples"] == 8
+        assert all(v > 0 for v in fleet.workers[0].runner.latencies())
+        assert st[0]["latency_sum_ns"] == sum(fleet.workers[0].runner.latencies())
+    finally:
+        fleet.close()
+
+
+def test_sigterm_stops_worker_processes(servers, tmp_path):
+    sqs, kube, env = servers
+    specs = _specs(sqs, kube, ["0", "0"])
+    e = dict(os.environ)
+    e.update(env)
+    p = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", f"--aws-region={REGION}",
+                          f"--sqs-endpoint={sqs.url}", "--poll-period=20ms", "--worker-processes", *specs],
+                         cwd=ROOT, env=e, stderr=subprocess.PIPE, text=True)
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and sqs.requests() < 4:
+            time.sleep(0.05)
+        assert sqs.requests() >= 4
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=20) == 0
+        err = p.stderr.read()
+        assert "Stopped kube-sqs-autoscaler" in err
+    finally:
+        if p.poll() is None:
+            p.kill()
+    n = sqs.requests()
+    time.sleep(0.2)
+    assert sqs.requests() == n  # no orphaned worker keeps polling
+
+
+def test_flag_conflict():
+    from kube_sqs_autoscaler_amd.config import parse_args
+    from kube_sqs_autoscaler_amd.utils.goflag import FlagError
+
+    with pytest.raises(FlagError):
+        parse_args(["--worker-processes", "--worker-threads=2"], {})
