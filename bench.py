@@ -15,6 +15,12 @@ tracked queue: SigV4-signed SQS GetQueueAttributes -> Deployment GET -> replica 
 alternates 200/0 messages, so every iteration scales). K timed steps are bracketed by a barrier
 + ``torch.cuda.synchronize()``; ``value`` is the p50 over every sample of every rank.
 
+Secondary rows (single rank; fixed ``--secondary-samples`` per queue, three interleaved rounds,
+median): p50 at 1/2/4/8 tracked queues with ``--worker-processes`` and with the default
+thread-per-queue fleet (each queue against its own fake endpoint process), the strictly
+sequential and reference-equivalent paths, TLS, a regional-RTT model, per-phase medians,
+wire-path decision parity and apiserver requests per poll on the Appendix C traces.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--queues Q] [--mode scale]
 """
 from __future__ import annotations
@@ -167,25 +173,33 @@ def main(argv=None) -> int:
             # Secondary rows: three interleaved rounds, median p50 per row, so one disturbed run
             # (CPU migration, a noisy neighbour) cannot invert the comparison.
             n, w = args.secondary_samples, 200
-            rows = {f"q{q}": (q, args.mode, pipeline, bp, False, "shared") for q in (1, 2, 4, 8)}
-            # 8 queues, each against its own fake SQS + apiserver pair (what 8 ranks see): the
-            # single-process fakes serialise on their own state lock, real endpoints do not.
-            rows["q8_per_queue_endpoints"] = (8, args.mode, pipeline, bp, False, "per-queue")
-            rows["sequential"] = (1, args.mode, False, 0, False, "shared")
-            rows["reference"] = (1, "deployment", False, 0, False, "shared")
+            # row: (queues, mode, pipelined, busy-poll ns, tls, servers, workers)
+            rows = {}
+            for q in (1, 2, 4, 8):
+                # --worker-processes: one worker process per queue, one endpoint process per queue
+                rows[f"q{q}"] = (q, args.mode, pipeline, bp, False, "processes", "processes")
+                # the default thread-per-queue fleet against the same endpoint processes
+                rows[f"q{q}_threads"] = (q, args.mode, pipeline, bp, False, "processes", "threads")
+            # round 1's row: 8 threads against one shared in-process fake pair
+            rows["q8_threads_shared_fakes"] = (8, args.mode, pipeline, bp, False, "shared", "threads")
+            rows["sequential"] = (1, args.mode, False, 0, False, "shared", "threads")
+            rows["reference"] = (1, "deployment", False, 0, False, "shared", "threads")
             # Production endpoints are HTTPS: the same two paths over keep-alive TLS 1.3
-            rows["tls"] = (1, args.mode, pipeline, bp, True, "shared")
-            rows["reference_tls"] = (1, "deployment", False, 0, True, "shared")
+            rows["tls"] = (1, args.mode, pipeline, bp, True, "shared", "threads")
+            rows["reference_tls"] = (1, "deployment", False, 0, True, "shared", "threads")
             p50s = {k: [] for k in rows}
             samples = {k: [] for k in rows}
             for _ in range(3):
-                for k, (q, mode, pl, b, tls, sv) in rows.items():
-                    sm = measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls, servers=sv).summary()
+                for k, (q, mode, pl, b, tls, sv, wk) in rows.items():
+                    sm = measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls, servers=sv, workers=wk).summary()
                     p50s[k].append(sm["p50_ms"])
                     samples[k].append(sm["samples"])
             med = {k: sorted(v)[1] for k, v in p50s.items()}
             extra["p50_ms_by_tracked_queues"] = {str(q): med[f"q{q}"] for q in (1, 2, 4, 8)}
-            extra["p50_ms_8_queues_per_queue_endpoints"] = med["q8_per_queue_endpoints"]
+            extra["tracked_queues_config"] = ("--worker-processes (one worker process per queue), each queue against "
+                                              "its own fake SQS + apiserver process")
+            extra["p50_ms_by_tracked_queues_threads"] = {str(q): med[f"q{q}_threads"] for q in (1, 2, 4, 8)}
+            extra["p50_ms_8_queues_threads_shared_fakes"] = med["q8_threads_shared_fakes"]
             extra["sequential_scale_p50_ms"] = med["sequential"]
             extra["reference_equivalent_p50_ms"] = med["reference"]
             extra["tls_p50_ms"] = {"default": med["tls"], "reference_equivalent": med["reference_tls"]}
@@ -195,10 +209,10 @@ def main(argv=None) -> int:
             # structural round-trip savings show at production scale (200 polls each).
             wan = {}
             for name, mode, pl in (("optimised", args.mode, pipeline), ("reference_equivalent", "deployment", False)):
-                r = measure(1, 200, 5, mode, pipeline=pl, sqs_latency_ns=2_000_000, kube_latency_ns=1_000_000)
+                r = measure(1, n, 5, mode, pipeline=pl, sqs_latency_ns=2_000_000, kube_latency_ns=1_000_000)
                 wan[name] = r.summary()["p50_ms"]
             extra["wan_model_sqs2ms_kube1ms_p50_ms"] = wan
-            extra["wan_model_samples"] = 200
+            extra["wan_model_samples"] = n
             from kube_sqs_autoscaler_amd.bench.latency import phase_breakdown
 
             extra["phase_median_us"] = {
