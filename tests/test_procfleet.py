@@ -119,3 +119,45 @@ def test_flag_conflict():
 
     with pytest.raises(FlagError):
         parse_args(["--worker-processes", "--worker-threads=2"], {})
+
+
+def test_metrics_and_health_over_worker_processes(nat, servers):
+    """/metrics and /healthz of a --worker-processes fleet come from the workers' shared slots."""
+    import urllib.request
+
+    from kube_sqs_autoscaler_amd import autoscaler
+    from kube_sqs_autoscaler_amd.config import parse_args
+    from kube_sqs_autoscaler_amd.metrics import Health, MetricsServer
+    from kube_sqs_autoscaler_amd.utils.log import make_logger
+
+    sqs, kube, env = servers
+    specs = _specs(sqs, kube, ["500", "0"])
+    cfg = parse_args([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=5ms",
+                      "--scale-up-cool-down=0s", "--scale-down-cool-down=0s", "--max-pods=7", *specs], env)
+    rest = autoscaler.load_rest_config(cfg, env)
+    log = make_logger("error", "text")
+    builds = [lambda t=t: autoscaler.new_runner(t, cfg, rest, log, nat.RealClock(), environ=env) for t in cfg.targets]
+    fleet = ProcessFleet(builds, cfg.targets)
+    health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets])
+    m = MetricsServer(fleet, "127.0.0.1:0", health)
+    m.start()
+    try:
+        fleet.start()
+        deadline = time.time() + 30
+        while time.time() < deadline and kube.replicas("gpu", "w0") < 7:
+            time.sleep(0.01)
+        base = f"http://127.0.0.1:{m.port}"
+        assert urllib.request.urlopen(base + "/healthz").read() == b"ok"
+        while time.time() < deadline and not all(s["polls"] > 0 for s in fleet.stats()):
+            time.sleep(0.01)
+        assert urllib.request.urlopen(base + "/readyz").read() == b"ok"
+        text = urllib.request.urlopen(base + "/metrics").read().decode()
+        assert 'ksa_scale_ups_total{deployment="gpu/w0"' in text
+        assert 'ksa_replicas{deployment="gpu/w0",queue="' in text and "} 7.0" in text
+        assert 'ksa_poll_to_patch_seconds_count{deployment="gpu/w0"' in text
+    finally:
+        fleet.stop()
+        fleet.join()
+        m.stop()
+        fleet.close()
+    assert kube.replicas("gpu", "w0") == 7 and kube.replicas("gpu", "w1") == 1
