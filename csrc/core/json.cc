@@ -261,6 +261,220 @@ class Parser {
 
 }  // namespace
 
+namespace {
+
+// Validating single-pass scanner for json_scan_scale. Accepts exactly the grammar Parser does
+// (RFC 8259, same depth limit); records only the spans it is asked about.
+class Scanner {
+ public:
+  explicit Scanner(const std::string& t) : t_(t.data()), n_(t.size()) {}
+
+  bool run(ScaleFields* f) {
+    f_ = f;
+    ws();
+    if (i_ >= n_ || t_[i_] != '{') return false;  // the actuator only handles objects
+    f->root_begin = i_;
+    if (!object(0, kRoot)) return false;
+    ws();
+    return i_ == n_;
+  }
+
+ private:
+  enum Ctx { kOther, kRoot, kMetadata, kSpec };
+
+  void ws() {
+    while (i_ < n_ && (t_[i_] == ' ' || t_[i_] == '\n' || t_[i_] == '\r' || t_[i_] == '\t')) ++i_;
+  }
+  static int hexval(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  // String at t_[i_] == '"'; sets [*b, *e) to the contents and *esc if escapes occur.
+  bool string(size_t* b, size_t* e, bool* esc) {
+    ++i_;
+    *b = i_;
+    *esc = false;
+    while (i_ < n_) {
+      const char c = t_[i_];
+      if (c == '"') {
+        *e = i_++;
+        return true;
+      }
+      if (static_cast<unsigned char>(c) < 0x20) return false;
+      if (c != '\\') {
+        ++i_;
+        continue;
+      }
+      *esc = true;
+      if (++i_ >= n_) return false;
+      const char x = t_[i_++];
+      if (x == 'u') {
+        if (i_ + 4 > n_) return false;
+        for (int k = 0; k < 4; ++k)
+          if (hexval(t_[i_ + k]) < 0) return false;
+        i_ += 4;
+      } else if (x != '"' && x != '\\' && x != '/' && x != 'b' && x != 'f' && x != 'n' && x != 'r' && x != 't') {
+        return false;
+      }
+    }
+    return false;
+  }
+  bool number() {
+    if (t_[i_] == '-') ++i_;
+    if (i_ >= n_) return false;
+    if (t_[i_] == '0') {
+      ++i_;
+    } else if (t_[i_] >= '1' && t_[i_] <= '9') {
+      while (i_ < n_ && t_[i_] >= '0' && t_[i_] <= '9') ++i_;
+    } else {
+      return false;
+    }
+    if (i_ < n_ && t_[i_] == '.') {
+      const size_t d = ++i_;
+      while (i_ < n_ && t_[i_] >= '0' && t_[i_] <= '9') ++i_;
+      if (d == i_) return false;
+    }
+    if (i_ < n_ && (t_[i_] == 'e' || t_[i_] == 'E')) {
+      ++i_;
+      if (i_ < n_ && (t_[i_] == '+' || t_[i_] == '-')) ++i_;
+      const size_t d = i_;
+      while (i_ < n_ && t_[i_] >= '0' && t_[i_] <= '9') ++i_;
+      if (d == i_) return false;
+    }
+    return true;
+  }
+  bool lit(const char* s, size_t len) {
+    if (i_ + len > n_ || std::char_traits<char>::compare(t_ + i_, s, len) != 0) return false;
+    i_ += len;
+    return true;
+  }
+  bool value(int depth, Ctx ctx) {
+    if (depth > 256 || i_ >= n_) return false;
+    const char c = t_[i_];
+    if (c == '{') return object(depth, ctx);
+    if (c == '[') return array(depth);
+    if (c == '"') {
+      size_t b, e;
+      bool esc;
+      return string(&b, &e, &esc);
+    }
+    if (c == 't') return lit("true", 4);
+    if (c == 'f') return lit("false", 5);
+    if (c == 'n') return lit("null", 4);
+    if (c == '-' || (c >= '0' && c <= '9')) return number();
+    return false;
+  }
+  bool key_is(size_t b, size_t e, const char* k, size_t len) const {
+    return e - b == len && std::char_traits<char>::compare(t_ + b, k, len) == 0;
+  }
+  bool object(int depth, Ctx ctx) {
+    const size_t open = i_++;
+    ws();
+    bool empty = i_ < n_ && t_[i_] == '}';
+    if (ctx == kRoot) f_->root_empty = empty;
+    if (ctx == kSpec) {
+      f_->spec_begin = open;
+      f_->spec_empty = empty;
+    }
+    if (empty) {
+      ++i_;
+      return true;
+    }
+    while (true) {
+      ws();
+      if (i_ >= n_ || t_[i_] != '"') return false;
+      size_t kb, ke;
+      bool kesc;
+      if (!string(&kb, &ke, &kesc)) return false;
+      ws();
+      if (i_ >= n_ || t_[i_] != ':') return false;
+      ++i_;
+      ws();
+      if (i_ >= n_) return false;
+      Ctx child = kOther;
+      if (ctx == kRoot || ctx == kMetadata || ctx == kSpec) {
+        if (kesc) return false;  // a key of interest could hide behind an escape: no fast path
+        if (ctx == kRoot && key_is(kb, ke, "metadata", 8)) {
+          if (seen_metadata_++) return false;
+          child = kMetadata;
+        } else if (ctx == kRoot && key_is(kb, ke, "spec", 4)) {
+          if (f_->has_spec) return false;
+          f_->has_spec = true;
+          f_->spec_is_object = t_[i_] == '{';
+          child = kSpec;
+        } else if (ctx == kMetadata && key_is(kb, ke, "resourceVersion", 15)) {
+          if (seen_rv_++) return false;
+          if (t_[i_] == '"') {
+            f_->has_rv = true;
+            if (!string(&f_->rv_begin, &f_->rv_end, &f_->rv_escaped)) return false;
+            goto next;
+          }
+        } else if (ctx == kSpec && key_is(kb, ke, "replicas", 8)) {
+          if (f_->has_replicas) return false;
+          f_->has_replicas = true;
+          f_->replicas_begin = i_;
+          f_->replicas_null = t_[i_] == 'n';
+          f_->replicas_number = t_[i_] == '-' || (t_[i_] >= '0' && t_[i_] <= '9');
+          if (!value(depth + 1, kOther)) return false;
+          f_->replicas_end = i_;
+          goto next;
+        }
+      }
+      if (!value(depth + 1, child)) return false;
+    next:
+      ws();
+      if (i_ < n_ && t_[i_] == ',') {
+        ++i_;
+        continue;
+      }
+      if (i_ < n_ && t_[i_] == '}') {
+        ++i_;
+        return true;
+      }
+      return false;
+    }
+  }
+  bool array(int depth) {
+    ++i_;
+    ws();
+    if (i_ < n_ && t_[i_] == ']') {
+      ++i_;
+      return true;
+    }
+    while (true) {
+      ws();
+      if (!value(depth + 1, kOther)) return false;
+      ws();
+      if (i_ < n_ && t_[i_] == ',') {
+        ++i_;
+        continue;
+      }
+      if (i_ < n_ && t_[i_] == ']') {
+        ++i_;
+        return true;
+      }
+      return false;
+    }
+  }
+
+  const char* t_;
+  size_t n_;
+  size_t i_ = 0;
+  ScaleFields* f_ = nullptr;
+  int seen_metadata_ = 0, seen_rv_ = 0;
+};
+
+}  // namespace
+
+ScaleFields json_scan_scale(const std::string& text) {
+  ScaleFields f;
+  Scanner s(text);
+  f.ok = s.run(&f);
+  return f;
+}
+
 const JsonValue* JsonValue::get(const std::string& key) const {
   if (type != Type::Object) return nullptr;
   // Last duplicate wins, like encoding/json.

@@ -47,6 +47,32 @@ Result<JsonValue> json_parse(const std::string& text);
 std::string json_serialize(const JsonValue& v);
 std::string json_quote(const std::string& s);
 
+// The fields the replica actuator needs from a Deployment or autoscaling/v1 Scale, located by
+// one validating pass over the text with no DOM and no allocation (json_parse builds a tree of
+// strings and vectors for every field of a ~3 KB Deployment on every poll). Offsets are into
+// the scanned text. `ok` is false -- and the caller must fall back to json_parse -- whenever
+// the text is not valid JSON or is anything but the plain case: keys of interest written with
+// escapes, duplicated `metadata` / `spec` / `resourceVersion` / `replicas` keys, nesting deeper
+// than json_parse allows. In the plain case the answer is exactly what json_parse + path()
+// would give.
+struct ScaleFields {
+  bool ok = false;
+  size_t root_begin = 0;         // offset of the root object's '{'
+  bool root_empty = false;
+  bool has_rv = false;           // metadata.resourceVersion is a string ...
+  bool rv_escaped = false;       // ... containing escapes (decode with json_parse)
+  size_t rv_begin = 0, rv_end = 0;  // its contents, without the quotes
+  bool has_spec = false;         // root key "spec" present
+  bool spec_is_object = false;
+  size_t spec_begin = 0;         // offset of spec's '{'
+  bool spec_empty = false;
+  bool has_replicas = false;     // spec.replicas present (any type)
+  bool replicas_null = false;
+  bool replicas_number = false;
+  size_t replicas_begin = 0, replicas_end = 0;
+};
+ScaleFields json_scan_scale(const std::string& text);
+
 // Replaces the bytes of `node` (located in `text`) with `replacement`.
 std::string json_splice(const std::string& text, const JsonValue& node,
                         const std::string& replacement);

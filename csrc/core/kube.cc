@@ -85,7 +85,55 @@ Nanos TokenBucket::take(StopFlag* stop) {
 // ---------------------------------------------------------------------------------------
 // Object helpers
 
+namespace {
+
+// JsonValue::as_int64 on a number literal in place.
+bool int_literal(const std::string& s, size_t b, size_t e, int64_t* out) {
+  if (b >= e) return false;
+  bool neg = false;
+  if (s[b] == '-') {
+    neg = true;
+    ++b;
+  }
+  uint64_t acc = 0;
+  for (size_t i = b; i < e; ++i) {
+    const char c = s[i];
+    if (c < '0' || c > '9') return false;  // fraction/exponent: not an integer literal
+    const uint64_t d = static_cast<uint64_t>(c - '0');
+    if (acc > (~uint64_t(0) - d) / 10) return false;
+    acc = acc * 10 + d;
+  }
+  const uint64_t cutoff = uint64_t(1) << 63;
+  if ((!neg && acc >= cutoff) || (neg && acc > cutoff)) return false;
+  *out = neg ? static_cast<int64_t>(0 - acc) : static_cast<int64_t>(acc);
+  return true;
+}
+
+}  // namespace
+
 Result<ScaleObject> parse_scale_object(const std::string& json, bool absent_is_zero) {
+  // Fast path: one scan, no DOM (every poll parses a Scale or a whole Deployment).
+  const ScaleFields f = json_scan_scale(json);
+  if (f.ok && !f.rv_escaped && (!f.has_replicas || f.replicas_null || f.replicas_number)) {
+    ScaleObject o;
+    o.raw = json;
+    if (f.has_rv) o.resource_version.assign(json, f.rv_begin, f.rv_end - f.rv_begin);
+    if (f.has_replicas && !f.replicas_null) {
+      int64_t v;
+      if (!int_literal(json, f.replicas_begin, f.replicas_end, &v))
+        return Result<ScaleObject>::Err(Status::Err("spec.replicas is not an integer"));
+      o.has_replicas = true;
+      o.replicas = go_int32(v);
+    } else if (absent_is_zero) {
+      o.has_replicas = true;
+      o.replicas = 0;
+    }
+    return Result<ScaleObject>::Ok(std::move(o));
+  }
+  return parse_scale_object_dom(json, absent_is_zero);
+}
+
+Result<ScaleObject> parse_scale_object_dom(const std::string& json, bool absent_is_zero) {
   auto j = json_parse(json);
   if (!j.ok()) return Result<ScaleObject>::Err(j.status);
   ScaleObject o;
@@ -106,10 +154,41 @@ Result<ScaleObject> parse_scale_object(const std::string& json, bool absent_is_z
 }
 
 Result<std::string> set_spec_replicas(const std::string& raw, int32_t replicas) {
+  const std::string num = std::to_string(replicas);
+  const ScaleFields f = json_scan_scale(raw);
+  if (f.ok) {
+    std::string out;
+    out.reserve(raw.size() + 32);
+    if (f.has_spec && f.spec_is_object) {
+      if (f.has_replicas) {  // splice the value in place
+        out.append(raw, 0, f.replicas_begin);
+        out += num;
+        out.append(raw, f.replicas_end, std::string::npos);
+      } else {  // insert as the first member of spec
+        out.append(raw, 0, f.spec_begin + 1);
+        out += "\"replicas\":";
+        out += num;
+        if (!f.spec_empty) out.push_back(',');
+        out.append(raw, f.spec_begin + 1, std::string::npos);
+      }
+    } else {
+      out.append(raw, 0, f.root_begin + 1);
+      out += "\"spec\":{\"replicas\":";
+      out += num;
+      out.push_back('}');
+      if (!f.root_empty) out.push_back(',');
+      out.append(raw, f.root_begin + 1, std::string::npos);
+    }
+    return Result<std::string>::Ok(std::move(out));
+  }
+  return set_spec_replicas_dom(raw, replicas);
+}
+
+Result<std::string> set_spec_replicas_dom(const std::string& raw, int32_t replicas) {
+  const std::string num = std::to_string(replicas);
   auto j = json_parse(raw);
   if (!j.ok()) return Result<std::string>::Err(j.status);
   if (!j.value.is_object()) return Result<std::string>::Err(Status::Err("object is not a JSON object"));
-  const std::string num = std::to_string(replicas);
   const JsonValue* spec = j.value.get("spec");
   if (spec && spec->is_object()) {
     const JsonValue* r = spec->get("replicas");

@@ -212,6 +212,10 @@ class KubeRestDeployments final : public DeploymentApi {
 Result<ScaleObject> parse_scale_object(const std::string& json, bool absent_is_zero);
 // Returns `raw` with spec.replicas set to `replicas` (inserted when absent).
 Result<std::string> set_spec_replicas(const std::string& raw, int32_t replicas);
+// The same two through the JSON DOM (json_parse): what the fast single-scan paths above fall
+// back to outside the plain case, and the reference the differential tests hold them to.
+Result<ScaleObject> parse_scale_object_dom(const std::string& json, bool absent_is_zero);
+Result<std::string> set_spec_replicas_dom(const std::string& raw, int32_t replicas);
 
 // In-memory object tracker (client-go fake clientset equivalent).
 class FakeDeployments final : public DeploymentApi {

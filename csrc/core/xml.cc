@@ -1,5 +1,6 @@
 #include "xml.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace ksa {
@@ -24,6 +25,14 @@ void put_utf8(std::string* s, unsigned long cp) {
   }
 }
 
+// Does doc[b, e) -- an element name, possibly namespace-prefixed -- have the local name `tag`?
+// Compared in place: no substring per tag scanned.
+bool local_name_is(const std::string& doc, size_t b, size_t e, const std::string& tag) {
+  for (size_t k = b; k < e; ++k)
+    if (doc[k] == ':') b = k + 1;  // the prefix ends at the (last) colon
+  return e - b == tag.size() && doc.compare(b, e - b, tag) == 0;
+}
+
 // Finds the next start tag whose local name equals `tag` at or after `pos` (before `to`).
 // Returns the offset just past '>' of the start tag, or npos. *self_closing set for <x/>.
 size_t find_start(const std::string& doc, const std::string& tag, size_t pos, size_t to,
@@ -41,12 +50,9 @@ size_t find_start(const std::string& doc, const std::string& tag, size_t pos, si
            doc[name_end] != '/' && doc[name_end] != '\t' && doc[name_end] != '\n' &&
            doc[name_end] != '\r')
       ++name_end;
-    std::string name = doc.substr(p, name_end - p);
-    size_t colon = name.find(':');
-    if (colon != std::string::npos) name = name.substr(colon + 1);
     size_t gt = doc.find('>', name_end);
     if (gt == std::string::npos) return std::string::npos;
-    if (name == tag) {
+    if (local_name_is(doc, p, name_end, tag)) {
       *self_closing = gt > 0 && doc[gt - 1] == '/';
       return gt + 1;
     }
@@ -61,11 +67,9 @@ size_t find_end(const std::string& doc, const std::string& tag, size_t pos, size
     size_t p = lt + 2;
     size_t gt = doc.find('>', p);
     if (gt == std::string::npos) return std::string::npos;
-    std::string name = doc.substr(p, gt - p);
-    while (!name.empty() && (name.back() == ' ' || name.back() == '\t')) name.pop_back();
-    size_t colon = name.find(':');
-    if (colon != std::string::npos) name = name.substr(colon + 1);
-    if (name == tag) return lt;
+    size_t e = gt;
+    while (e > p && (doc[e - 1] == ' ' || doc[e - 1] == '\t')) --e;
+    if (local_name_is(doc, p, e, tag)) return lt;
     pos = gt + 1;
   }
 }
@@ -73,6 +77,7 @@ size_t find_end(const std::string& doc, const std::string& tag, size_t pos, size
 }  // namespace
 
 std::string xml_unescape(const std::string& s) {
+  if (s.find('&') == std::string::npos) return s;
   std::string out;
   out.reserve(s.size());
   size_t i = 0;
@@ -134,12 +139,14 @@ std::string xml_first_text(const std::string& doc, const std::string& tag, bool*
   if (self_closing) return "";
   size_t end = find_end(doc, tag, start, to);
   if (end == std::string::npos) end = to;
-  std::string raw = doc.substr(start, end - start);
+  // [start, start + n): what doc.substr(start, end - start) keeps (the start tag can end past
+  // `to`, then end < start and the text runs to the end of doc).
+  const size_t n = std::min(end - start, doc.size() - start);
   // CDATA sections are passed through verbatim.
-  if (raw.compare(0, 9, "<![CDATA[") == 0 && raw.size() >= 12 &&
-      raw.compare(raw.size() - 3, 3, "]]>") == 0)
-    return raw.substr(9, raw.size() - 12);
-  return xml_unescape(raw);
+  if (n >= 12 && doc.compare(start, 9, "<![CDATA[") == 0 && doc.compare(start + n - 3, 3, "]]>") == 0)
+    return doc.substr(start + 9, n - 12);
+  if (std::char_traits<char>::find(doc.data() + start, n, '&') == nullptr) return doc.substr(start, n);
+  return xml_unescape(doc.substr(start, n));
 }
 
 std::vector<std::pair<std::string, std::string>> xml_sqs_attributes(const std::string& doc) {

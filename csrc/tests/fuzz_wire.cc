@@ -124,9 +124,17 @@ void fuzz_json(const std::string& in) {
     int64_t v;
     if (const JsonValue* r = j.value.path({"spec", "replicas"})) (void)r->as_int64(&v);
   }
-  (void)set_spec_replicas(in, 7);
-  (void)parse_scale_object(in, true);
-  (void)parse_scale_object(in, false);
+  // the single-scan fast paths give exactly what the DOM gives, errors included
+  auto a = set_spec_replicas(in, 7), b = set_spec_replicas_dom(in, 7);
+  if (a.ok() != b.ok() || (a.ok() ? a.value != b.value : a.status.message() != b.status.message())) __builtin_trap();
+  for (bool zero : {true, false}) {
+    auto p = parse_scale_object(in, zero), q = parse_scale_object_dom(in, zero);
+    if (p.ok() != q.ok()) __builtin_trap();
+    if (!p.ok() && p.status.message() != q.status.message()) __builtin_trap();
+    if (p.ok() && (p.value.has_replicas != q.value.has_replicas || p.value.replicas != q.value.replicas ||
+                   p.value.resource_version != q.value.resource_version || p.value.raw != q.value.raw))
+      __builtin_trap();
+  }
 }
 
 void fuzz_xml(const std::string& in) {
