@@ -277,6 +277,15 @@ PYBIND11_MODULE(_ksa_native, m) {
              d["signature"] = dbg.signature;
              return py::make_tuple(h, d);
            })
+      .def("sign_prepared_headers",
+           [](SigV4Signer& s, const Credentials& c, int64_t unix_ns, const std::string& method,
+              const std::string& path, const std::string& query, py::object headers, py::bytes body) {
+             // exactly what HttpSqsApi does per poll (no debug capture: the in-place fast path)
+             SigV4Prepared p = s.prepare(method, path, query, headers_from(headers), std::string(body));
+             Headers h;
+             s.sign_prepared(p, c, unix_ns, &h, nullptr);
+             return h;
+           })
       .def("signing_key_hex", [](SigV4Signer& s, const std::string& secret, const std::string& date) {
         return hex_encode(s.signing_key(secret, date));
       });

@@ -84,6 +84,29 @@ bool has_header(const Headers& hs, const std::string& name) {
   return false;
 }
 
+// Case-insensitive "does `hay` contain `needle`" (needle given in lower case), no copies.
+bool icontains(const std::string& hay, const char* needle) {
+  const size_t n = std::strlen(needle);
+  if (n > hay.size()) return false;
+  for (size_t i = 0; i + n <= hay.size(); ++i) {
+    size_t k = 0;
+    while (k < n && std::tolower(static_cast<unsigned char>(hay[i + k])) == needle[k]) ++k;
+    if (k == n) return true;
+  }
+  return false;
+}
+
+const std::string* header_ptr(const Headers& hs, const char* name, size_t len) {
+  for (auto& [k, v] : hs) {
+    if (k.size() != len) continue;
+    size_t i = 0;
+    while (i < len && std::tolower(static_cast<unsigned char>(k[i])) == std::tolower(static_cast<unsigned char>(name[i])))
+      ++i;
+    if (i == len) return &v;
+  }
+  return nullptr;
+}
+
 std::string ssl_error_string() {
   unsigned long e = ERR_get_error();
   if (!e) return "unknown TLS error";
@@ -462,26 +485,35 @@ class Reader {
 };
 
 void parse_header_lines(const std::string& head, size_t from, Headers* out) {
+  // Spans trimmed in place: one string per name and per value, nothing else allocated.
+  auto trimmed = [&](size_t b, size_t e) {
+    while (b < e && (head[b] == ' ' || head[b] == '\t')) ++b;
+    while (e > b && (head[e - 1] == ' ' || head[e - 1] == '\t' || head[e - 1] == '\r')) --e;
+    return std::string(head, b, e - b);
+  };
   size_t pos = from;
   while (pos < head.size()) {
     size_t e = head.find("\r\n", pos);
     if (e == std::string::npos) e = head.size();
-    std::string line = head.substr(pos, e - pos);
-    size_t colon = line.find(':');
-    if (colon != std::string::npos) out->emplace_back(trim(line.substr(0, colon)), trim(line.substr(colon + 1)));
+    const char* colon = static_cast<const char*>(std::memchr(head.data() + pos, ':', e - pos));
+    if (colon) {
+      const size_t c = static_cast<size_t>(colon - head.data());
+      out->emplace_back(trimmed(pos, c), trimmed(c + 1, e));
+    }
     pos = e + 2;
   }
 }
 
 bool wants_close(const Headers& hs, bool http10) {
-  std::string c = lower(header_of(hs, "Connection"));
-  if (c.find("close") != std::string::npos) return true;
-  if (http10 && c.find("keep-alive") == std::string::npos) return true;
+  const std::string* c = header_ptr(hs, "Connection", 10);
+  if (c && icontains(*c, "close")) return true;
+  if (http10 && !(c && icontains(*c, "keep-alive"))) return true;
   return false;
 }
 
 bool is_chunked(const Headers& hs) {
-  return lower(header_of(hs, "Transfer-Encoding")).find("chunked") != std::string::npos;
+  const std::string* t = header_ptr(hs, "Transfer-Encoding", 17);
+  return t && icontains(*t, "chunked");
 }
 
 struct SslInit {
@@ -1092,13 +1124,21 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   if (forward_proxy() && !origin_.tls()) wire += origin_.origin();
   wire += req.target.empty() ? "/" : req.target;
   wire += " HTTP/1.1\r\n";
-  if (!has_header(req.headers, "Host")) wire += "Host: " + origin_.host_header() + "\r\n";
-  if (forward_proxy() && !origin_.tls() && !proxy_auth_.empty()) wire += "Proxy-Authorization: " + proxy_auth_ + "\r\n";
+  auto line = [&wire](const std::string& k, const std::string& v) {
+    wire += k;
+    wire += ": ";
+    wire += v;
+    wire += "\r\n";
+  };
+  if (!has_header(req.headers, "Host")) line("Host", origin_.host_header());
+  if (forward_proxy() && !origin_.tls() && !proxy_auth_.empty()) line("Proxy-Authorization", proxy_auth_);
   if (!has_header(req.headers, "User-Agent")) wire += "User-Agent: kube-sqs-autoscaler-amd/1.0\r\n";
-  for (auto& [k, v] : req.headers) wire += k + ": " + v + "\r\n";
+  for (auto& [k, v] : req.headers) line(k, v);
   if (!req.body.empty() || req.method == "POST" || req.method == "PUT" || req.method == "PATCH") {
     if (!has_header(req.headers, "Content-Length"))
-      wire += "Content-Length: " + std::to_string(req.body.size()) + "\r\n";
+      wire += "Content-Length: ";
+      wire += std::to_string(req.body.size());
+      wire += "\r\n";
   }
   wire += "\r\n";
   wire += req.body;
@@ -1417,7 +1457,9 @@ void HttpServer::serve(int fd) {
                          (resp.reason.empty() ? http_reason(resp.status) : resp.reason) + "\r\n";
       for (auto& [k, v] : resp.headers) wire += k + ": " + v + "\r\n";
       if (!has_header(resp.headers, "Content-Length"))
-        wire += "Content-Length: " + std::to_string(resp.body.size()) + "\r\n";
+        wire += "Content-Length: ";
+        wire += std::to_string(resp.body.size());
+        wire += "\r\n";
       if (close_after) wire += "Connection: close\r\n";
       wire += "\r\n";
       wire += resp.body;

@@ -89,6 +89,16 @@ std::string HmacSha256Key::mac(const std::string& data) const {
   return std::string(reinterpret_cast<char*>(out), 32);
 }
 
+void HmacSha256Key::mac_parts(std::initializer_list<std::string_view> parts, unsigned char out[32]) const {
+  SHA256_CTX c = st_->inner;
+  unsigned char in[32];
+  for (auto p : parts) SHA256_Update(&c, p.data(), p.size());
+  SHA256_Final(in, &c);
+  c = st_->outer;
+  SHA256_Update(&c, in, 32);
+  SHA256_Final(out, &c);
+}
+
 std::string hmac_sha256(const std::string& key, const std::string& data) {
   return HmacSha256Key(key).mac(data);
 }
@@ -288,6 +298,18 @@ std::string SigV4Signer::signing_key(const std::string& secret, const std::strin
   return key_;
 }
 
+void SigV4Signer::mac_with_signing_key(const std::string& secret, const std::string& date,
+                                       std::initializer_list<std::string_view> parts, unsigned char out[32]) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (key_.empty() || key_secret_ != secret || key_date_ != date) {
+    key_ = derive_key(secret, date, region_, service_);
+    key_secret_ = secret;
+    key_date_ = date;
+    key_mac_ = HmacSha256Key(key_);
+  }
+  key_mac_.mac_parts(parts, out);
+}
+
 HmacSha256Key SigV4Signer::signing_mac(const std::string& secret, const std::string& date) {
   signing_key(secret, date);
   std::lock_guard<std::mutex> lk(mu_);
@@ -356,6 +378,30 @@ SigV4Prepared SigV4Signer::prepare(const std::string& method, const std::string&
     if (i) p.canonical_query.push_back('&');
     p.canonical_query += aws_uri_encode(params[i].first, false) + "=" + aws_uri_encode(params[i].second, false);
   }
+  // the canonical request around the date, for the no-session-token fast path
+  p.creq_prefix = p.method + "\n" + p.canonical_uri + "\n" + p.canonical_query + "\n";
+  std::string after;
+  bool date_done = false;
+  for (auto& [k, v] : p.canon) {
+    if (!date_done && std::string("x-amz-date") < k) {
+      date_done = true;
+      if (!p.signed_headers.empty()) p.signed_headers.push_back(';');
+      p.signed_headers += "x-amz-date";
+    }
+    std::string& dst = date_done ? after : p.creq_prefix;
+    dst += k;
+    dst.push_back(':');
+    dst += v;
+    dst.push_back('\n');
+    if (!p.signed_headers.empty()) p.signed_headers.push_back(';');
+    p.signed_headers += k;
+  }
+  if (!date_done) {
+    if (!p.signed_headers.empty()) p.signed_headers.push_back(';');
+    p.signed_headers += "x-amz-date";
+  }
+  p.creq_prefix += "x-amz-date:";
+  p.creq_suffix = "\n" + after + "\n" + p.signed_headers + "\n" + p.payload_hash;
   return p;
 }
 
@@ -363,6 +409,44 @@ void SigV4Signer::sign_prepared(const SigV4Prepared& p, const Credentials& creds
                                 SignDebug* debug) {
   const std::string amzdate = amz_date(unix_ns);
   const std::string date = amzdate.substr(0, 8);
+  if (creds.session_token.empty() && !debug && !p.creq_prefix.empty()) {
+    // hash the canonical request and MAC the string to sign in place: no request, string to
+    // sign or key copies (this runs on every SQS poll)
+    unsigned char md[32], mac[32];
+    SHA256_CTX c;
+    SHA256_Init(&c);
+    SHA256_Update(&c, p.creq_prefix.data(), p.creq_prefix.size());
+    SHA256_Update(&c, amzdate.data(), amzdate.size());
+    SHA256_Update(&c, p.creq_suffix.data(), p.creq_suffix.size());
+    SHA256_Final(md, &c);
+    const std::string creq_hash = hex32(md);
+    std::string scope;
+    scope.reserve(date.size() + region_.size() + service_.size() + 16);
+    scope += date;
+    scope.push_back('/');
+    scope += region_;
+    scope.push_back('/');
+    scope += service_;
+    scope += "/aws4_request";
+    mac_with_signing_key(creds.secret_access_key, date,
+                         {"AWS4-HMAC-SHA256\n", amzdate, "\n", scope, "\n", creq_hash}, mac);
+    out->clear();
+    out->reserve(p.headers.size() + 2);
+    *out = p.headers;
+    out->emplace_back("X-Amz-Date", amzdate);
+    std::string auth;
+    auth.reserve(64 + creds.access_key_id.size() + scope.size() + p.signed_headers.size() + 64);
+    auth += "AWS4-HMAC-SHA256 Credential=";
+    auth += creds.access_key_id;
+    auth.push_back('/');
+    auth += scope;
+    auth += ", SignedHeaders=";
+    auth += p.signed_headers;
+    auth += ", Signature=";
+    auth += hex32(mac);
+    out->emplace_back("Authorization", std::move(auth));
+    return;
+  }
   *out = p.headers;
   out->emplace_back("X-Amz-Date", amzdate);
   if (!creds.session_token.empty()) out->emplace_back("X-Amz-Security-Token", creds.session_token);

@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <utility>
 #include <vector>
 
@@ -38,6 +39,8 @@ class HmacSha256Key {
   HmacSha256Key& operator=(const HmacSha256Key&);
   ~HmacSha256Key();
   std::string mac(const std::string& data) const;  // raw 32 bytes
+  // The MAC of the concatenation of `parts`, without building it.
+  void mac_parts(std::initializer_list<std::string_view> parts, unsigned char out[32]) const;
 
  private:
   struct State;
@@ -111,6 +114,9 @@ struct SigV4Prepared {
   std::string payload_hash;   // hex SHA-256 of the body
   std::vector<std::pair<std::string, std::string>> canon;  // lower-case name, trimmed value; sorted
   std::string canonical_uri, canonical_query;
+  // Credentials without a session token (the common case): the canonical request is
+  // creq_prefix + X-Amz-Date + creq_suffix, so a signature hashes those three pieces in place.
+  std::string creq_prefix, creq_suffix, signed_headers;
 };
 
 class SigV4Signer {
@@ -135,6 +141,9 @@ class SigV4Signer {
   std::string signing_key(const std::string& secret, const std::string& date);
   // HMAC schedule of that key (what sign() uses).
   HmacSha256Key signing_mac(const std::string& secret, const std::string& date);
+  // MAC with that key of the concatenation of `parts` (no key or schedule copied).
+  void mac_with_signing_key(const std::string& secret, const std::string& date,
+                            std::initializer_list<std::string_view> parts, unsigned char out[32]);
 
   const std::string& region() const { return region_; }
   const std::string& service() const { return service_; }

@@ -247,7 +247,7 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
 
   AttrMap out;
   if (opts_.protocol == SqsProtocol::Query) {
-    for (auto& [k, v] : xml_sqs_attributes(resp.body)) out[k] = v;
+    for (auto& [k, v] : xml_sqs_attributes(resp.body)) out[std::move(k)] = std::move(v);
   } else {
     auto j = json_parse(resp.body);
     if (!j.ok())

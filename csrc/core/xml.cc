@@ -151,6 +151,7 @@ std::string xml_first_text(const std::string& doc, const std::string& tag, bool*
 
 std::vector<std::pair<std::string, std::string>> xml_sqs_attributes(const std::string& doc) {
   std::vector<std::pair<std::string, std::string>> out;
+  out.reserve(4);
   size_t pos = 0;
   while (true) {
     bool sc = false;
@@ -165,7 +166,7 @@ std::vector<std::pair<std::string, std::string>> xml_sqs_attributes(const std::s
     bool has_name = false, has_value = false;
     std::string name = xml_first_text(doc, "Name", &has_name, start, end);
     std::string value = xml_first_text(doc, "Value", &has_value, start, end);
-    if (has_name) out.emplace_back(name, value);
+    if (has_name) out.emplace_back(std::move(name), std::move(value));
     pos = end + 1;
   }
   return out;

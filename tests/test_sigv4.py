@@ -109,3 +109,6 @@ def test_prepared_signing_equals_generic(nat, headers, body, token, query, path,
     h2, d2 = s.sign_prepared(c, ts * 10**9, "POST", path, query, hs, body)
     assert d1["canonical_request"] == d2["canonical_request"]
     assert d1["signature"] == d2["signature"] and dict(h1)["Authorization"] == dict(h2)["Authorization"]
+    # the allocation-free path taken per poll (no debug capture; in place without a token)
+    h3 = s.sign_prepared_headers(c, ts * 10**9, "POST", path, query, hs, body)
+    assert h3 == h2
