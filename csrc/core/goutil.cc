@@ -101,6 +101,14 @@ std::string go_quote(const std::string& s) {
   out.push_back('"');
   size_t i = 0;
   while (i < s.size()) {
+    // Runs of printable ASCII other than '"' and '\\' are copied as they are, in one append.
+    size_t j = i;
+    while (j < s.size() && s[j] >= 0x20 && s[j] < 0x7F && s[j] != '"' && s[j] != '\\') ++j;
+    if (j > i) {
+      out.append(s, i, j - i);
+      i = j;
+      continue;
+    }
     size_t w = 1;
     int32_t r = decode_rune(s, i, &w);
     if (r < 0) {

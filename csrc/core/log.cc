@@ -79,7 +79,44 @@ Logger::Sink fd_sink(int fd) {
   };
 }
 
+// The calling thread's open batch (LogBatch): lines for one fd, through one gate.
+struct ThreadBatch {
+  int depth = 0;
+  int fd = -1;
+  LineGate* gate = nullptr;
+  std::shared_ptr<void> keep;  // keeps the gate's owner alive until the flush
+  std::string buf;
+
+  void flush() {
+    if (!buf.empty() && gate) {
+      if (buf.size() <= PIPE_BUF) gate->shared([&] { write_line(fd, buf); });
+      else gate->exclusive([&] { write_line(fd, buf); });
+    }
+    buf.clear();
+    if (buf.capacity() > 16 * PIPE_BUF) buf.shrink_to_fit();
+  }
+};
+
+ThreadBatch& thread_batch() {
+  thread_local ThreadBatch b;
+  return b;
+}
+
 }  // namespace
+
+LogBatch::LogBatch() { ++thread_batch().depth; }
+
+LogBatch::~LogBatch() {
+  ThreadBatch& b = thread_batch();
+  if (--b.depth == 0) {
+    b.flush();
+    b.keep.reset();
+    b.gate = nullptr;
+    b.fd = -1;
+  }
+}
+
+bool LogBatch::active() { return thread_batch().depth > 0; }
 
 size_t LineGate::slot_index() {
   static std::atomic<size_t> next{0};
@@ -118,15 +155,26 @@ void Logger::set_time_source(TimeSource t) {
 std::shared_ptr<Logger> Logger::with_fields(const Fields& extra) const {
   auto l = std::make_shared<Logger>(*this);  // shares sink/time (shared_ptr copy)
   for (auto& kv : extra) l->base_.push_back(kv);
+  l->sort_base();
   return l;
+}
+
+void Logger::sort_base() {
+  base_sorted_ = base_;
+  std::stable_sort(base_sorted_.begin(), base_sorted_.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
 }
 
 std::string Logger::format(Level l, const std::string& msg, const Fields& fields,
                            int64_t unix_ns) const {
-  Fields data = base_;
-  data.insert(data.end(), fields.begin(), fields.end());
-  std::stable_sort(data.begin(), data.end(),
-                   [](const auto& a, const auto& b) { return a.first < b.first; });
+  Fields merged;
+  if (!fields.empty()) {
+    merged = base_;
+    merged.insert(merged.end(), fields.begin(), fields.end());
+    std::stable_sort(merged.begin(), merged.end(),
+                     [](const auto& a, const auto& b) { return a.first < b.first; });
+  }
+  const Fields& data = fields.empty() ? base_sorted_ : merged;
   std::string out;
   if (format_ == LogFormat::Json) {
     // encoding/json marshals the map with sorted keys; time/level/msg sort among them.
@@ -177,16 +225,24 @@ std::string Logger::format(Level l, const std::string& msg, const Fields& fields
     }
     return out;
   }
-  auto append = [&](const std::string& k, const std::string& v) {
-    if (!out.empty()) out.push_back(' ');
-    out += k;
-    out.push_back('=');
-    out += logrus_needs_quoting(v) ? go_quote(v) : v;
+  out.reserve(64 + msg.size() + 32 * data.size());
+  auto value = [&](const std::string& v) {
+    if (logrus_needs_quoting(v)) out += go_quote(v);
+    else out += v;
   };
-  append("time", rfc3339_utc(unix_ns));
-  append("level", level_name(l));
-  append("msg", msg);
-  for (auto& kv : data) append(kv.first, kv.second);
+  // time= is an RFC 3339 UTC stamp: always quoted (':'), never escaped.
+  out += "time=\"";
+  out += rfc3339_utc(unix_ns);
+  out += "\" level=";
+  out += level_name(l);  // [a-z] only: never quoted
+  out += " msg=";
+  value(msg);
+  for (auto& kv : data) {
+    out.push_back(' ');
+    out += kv.first;
+    out.push_back('=');
+    value(kv.second);
+  }
   return out;
 }
 
@@ -196,6 +252,18 @@ void Logger::log(Level l, const std::string& msg, const Fields& fields) {
   if (fd >= 0 && !shared_->custom_time.load(std::memory_order_acquire)) {
     std::string line = format(l, msg, fields, wall_now_ns());
     line.push_back('\n');
+    ThreadBatch& b = thread_batch();
+    if (b.depth > 0 && l > Level::Fatal) {
+      if (b.fd != fd || b.gate != &shared_->gate) {
+        b.flush();
+        b.fd = fd;
+        b.gate = &shared_->gate;
+        b.keep = shared_;
+      }
+      b.buf += line;
+      return;
+    }
+    if (b.depth > 0) b.flush();  // keep the order ahead of a fatal line
     if (line.size() <= PIPE_BUF) {  // one atomic write(2), on pipes too
       shared_->gate.shared([&] { write_line(fd, line); });
       return;

@@ -68,6 +68,23 @@ class LineGate {
   std::mutex mu_;
 };
 
+// Holds back the fd-sink lines the calling thread logs while it lives and writes them with one
+// write(2) when it ends (nested batches join the outermost). The control loop opens one per
+// poll, so the poll's lines -- "Found N messages", the scale result -- cost one system call,
+// made after the replica write instead of between the SQS response and the PUT. Each line keeps
+// the timestamp of the moment it was logged and the order is unchanged; only the write moves
+// (by the length of the poll). A batch of at most PIPE_BUF bytes is one atomic write, like a
+// single line; a longer one goes out alone (LineGate::exclusive). Fatal and panic lines, custom
+// sinks and custom time sources are never held back.
+class LogBatch {
+ public:
+  LogBatch();
+  ~LogBatch();
+  LogBatch(const LogBatch&) = delete;
+  LogBatch& operator=(const LogBatch&) = delete;
+  static bool active();  // is the calling thread inside a batch?
+};
+
 enum class Level : int { Panic = 0, Fatal = 1, Error = 2, Warn = 3, Info = 4, Debug = 5, Trace = 6 };
 
 const char* level_name(Level l);  // "panic", ..., "warning", "info", ...
@@ -100,7 +117,10 @@ class Logger {
   void set_sink_fd(int fd);
   void set_time_source(TimeSource t);
   // Fields appended to every entry of this logger (e.g. queue=... in multi-queue mode).
-  void set_base_fields(Fields f) { base_ = std::move(f); }
+  void set_base_fields(Fields f) {
+    base_ = std::move(f);
+    sort_base();
+  }
   std::shared_ptr<Logger> with_fields(const Fields& extra) const;
 
   bool enabled(Level l) const { return static_cast<int>(l) <= static_cast<int>(level_); }
@@ -128,8 +148,11 @@ class Logger {
   };
   Level level_ = Level::Info;
   LogFormat format_ = LogFormat::Text;
+  void sort_base();
   Fields base_;
+  Fields base_sorted_;  // base_ stable-sorted by key: the layout of a line without extra fields
   std::shared_ptr<Shared> shared_;
+  friend class LogBatch;
 };
 
 // logrus TextFormatter.needsQuoting

@@ -83,6 +83,11 @@ IterationRecord Runner::step(StopFlag* stop) {
 }
 
 IterationRecord Runner::poll_once() {
+  LogBatch batch;  // the poll's log lines go out together once it is done (log.h)
+  return poll_body();
+}
+
+IterationRecord Runner::poll_body() {
   if (shared_) {  // the supervising process' GPU-capacity cap
     const int64_t cap = shared_->max_override.load(std::memory_order_relaxed);
     if (cap > 0 && cap != scaler_->max()) scaler_->set_max(cap);

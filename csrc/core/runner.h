@@ -172,6 +172,7 @@ class Runner {
   const CpuList& cpus() const { return cpus_; }
 
  private:
+  IterationRecord poll_body();
   void record(const IterationRecord& r);
   void mirror(const IterationRecord& r);
   CpuList cpus_;

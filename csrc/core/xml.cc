@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string_view>
 
 namespace ksa {
 
@@ -27,19 +28,24 @@ void put_utf8(std::string* s, unsigned long cp) {
 
 // Does doc[b, e) -- an element name, possibly namespace-prefixed -- have the local name `tag`?
 // Compared in place: no substring per tag scanned.
-bool local_name_is(const std::string& doc, size_t b, size_t e, const std::string& tag) {
+bool local_name_is(const std::string& doc, size_t b, size_t e, std::string_view tag) {
   for (size_t k = b; k < e; ++k)
     if (doc[k] == ':') b = k + 1;  // the prefix ends at the (last) colon
   return e - b == tag.size() && doc.compare(b, e - b, tag) == 0;
 }
 
-// Finds the next start tag whose local name equals `tag` at or after `pos` (before `to`).
-// Returns the offset just past '>' of the start tag, or npos. *self_closing set for <x/>.
-size_t find_start(const std::string& doc, const std::string& tag, size_t pos, size_t to,
-                  bool* self_closing) {
-  while (true) {
+// Walks the start tags at or after `pos` (their '<' before `to`) and records, for each of the
+// `n` tags, the first start tag with that local name: starts[i] = the offset just past its '>'
+// (npos if none), self_closing[i] for <x/>. Stops once all are found. The walk visits the same
+// positions whatever the tags are, so looking for several tags in one walk finds exactly what
+// one walk per tag would.
+void find_starts(const std::string& doc, const std::string_view* tags, size_t n, size_t pos,
+                 size_t to, size_t* starts, bool* self_closing) {
+  size_t left = n;
+  for (size_t i = 0; i < n; ++i) starts[i] = std::string::npos;
+  while (left > 0) {
     size_t lt = doc.find('<', pos);
-    if (lt == std::string::npos || lt >= to) return std::string::npos;
+    if (lt == std::string::npos || lt >= to) return;
     size_t p = lt + 1;
     if (p < doc.size() && (doc[p] == '/' || doc[p] == '?' || doc[p] == '!')) {
       pos = p;
@@ -51,16 +57,28 @@ size_t find_start(const std::string& doc, const std::string& tag, size_t pos, si
            doc[name_end] != '\r')
       ++name_end;
     size_t gt = doc.find('>', name_end);
-    if (gt == std::string::npos) return std::string::npos;
-    if (local_name_is(doc, p, name_end, tag)) {
-      *self_closing = gt > 0 && doc[gt - 1] == '/';
-      return gt + 1;
+    if (gt == std::string::npos) return;
+    for (size_t i = 0; i < n; ++i) {
+      if (starts[i] == std::string::npos && local_name_is(doc, p, name_end, tags[i])) {
+        starts[i] = gt + 1;
+        self_closing[i] = gt > 0 && doc[gt - 1] == '/';
+        --left;
+      }
     }
     pos = gt + 1;
   }
 }
 
-size_t find_end(const std::string& doc, const std::string& tag, size_t pos, size_t to) {
+// The next start tag whose local name equals `tag` at or after `pos` (before `to`): the offset
+// just past its '>', or npos. *self_closing set for <x/>.
+size_t find_start(const std::string& doc, std::string_view tag, size_t pos, size_t to,
+                  bool* self_closing) {
+  size_t start;
+  find_starts(doc, &tag, 1, pos, to, &start, self_closing);
+  return start;
+}
+
+size_t find_end(const std::string& doc, std::string_view tag, size_t pos, size_t to) {
   while (true) {
     size_t lt = doc.find("</", pos);
     if (lt == std::string::npos || lt >= to) return std::string::npos;
@@ -126,16 +144,11 @@ std::string xml_escape(const std::string& s) {
   return out;
 }
 
-std::string xml_first_text(const std::string& doc, const std::string& tag, bool* found,
-                           size_t from, size_t to) {
-  if (to > doc.size()) to = doc.size();
-  bool self_closing = false;
-  size_t start = find_start(doc, tag, from, to, &self_closing);
-  if (start == std::string::npos) {
-    if (found) *found = false;
-    return "";
-  }
-  if (found) *found = true;
+namespace {
+
+// The text of the element whose start tag ends at `start` (xml_first_text after the start tag).
+std::string text_from(const std::string& doc, std::string_view tag, size_t start, bool self_closing,
+                      size_t to) {
   if (self_closing) return "";
   size_t end = find_end(doc, tag, start, to);
   if (end == std::string::npos) end = to;
@@ -147,6 +160,18 @@ std::string xml_first_text(const std::string& doc, const std::string& tag, bool*
     return doc.substr(start + 9, n - 12);
   if (std::char_traits<char>::find(doc.data() + start, n, '&') == nullptr) return doc.substr(start, n);
   return xml_unescape(doc.substr(start, n));
+}
+
+}  // namespace
+
+std::string xml_first_text(const std::string& doc, const std::string& tag, bool* found,
+                           size_t from, size_t to) {
+  if (to > doc.size()) to = doc.size();
+  bool self_closing = false;
+  size_t start = find_start(doc, tag, from, to, &self_closing);
+  if (found) *found = start != std::string::npos;
+  if (start == std::string::npos) return "";
+  return text_from(doc, tag, start, self_closing, to);
 }
 
 std::vector<std::pair<std::string, std::string>> xml_sqs_attributes(const std::string& doc) {
@@ -163,10 +188,14 @@ std::vector<std::pair<std::string, std::string>> xml_sqs_attributes(const std::s
     }
     size_t end = find_end(doc, "Attribute", start, doc.size());
     if (end == std::string::npos) break;
-    bool has_name = false, has_value = false;
-    std::string name = xml_first_text(doc, "Name", &has_name, start, end);
-    std::string value = xml_first_text(doc, "Value", &has_value, start, end);
-    if (has_name) out.emplace_back(std::move(name), std::move(value));
+    // xml_first_text(Name) and xml_first_text(Value) over [start, end), in one walk.
+    static constexpr std::string_view kTags[2] = {"Name", "Value"};
+    size_t at[2];
+    bool sc2[2] = {false, false};
+    find_starts(doc, kTags, 2, start, end, at, sc2);
+    if (at[0] != std::string::npos)
+      out.emplace_back(text_from(doc, kTags[0], at[0], sc2[0], end),
+                       at[1] == std::string::npos ? std::string() : text_from(doc, kTags[1], at[1], sc2[1], end));
     pos = end + 1;
   }
   return out;

@@ -12,6 +12,7 @@
 #include <poll.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/ioctl.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -708,6 +709,75 @@ TEST(concurrent_fd_sink_lines_are_whole) {
   CHECK_EQ(start, data.size());
   CHECK_EQ(n, size_t(4001));
   CHECK_EQ(bigs, size_t(1));
+}
+
+TEST(log_batch_holds_lines_until_end) {
+  // Lines logged inside a LogBatch reach the fd only when the outermost batch ends, in order,
+  // with their own timestamps; a fatal line flushes what is held first; batches of several
+  // threads into one pipe (some over PIPE_BUF) arrive whole.
+  int p[2];
+  CHECK_EQ(::pipe(p), 0);
+  auto log = std::make_shared<Logger>();
+  log->set_sink_fd(p[1]);
+  auto pending = [&] {
+    int n = 0;
+    CHECK_EQ(::ioctl(p[0], FIONREAD, &n), 0);
+    return n;
+  };
+  {
+    LogBatch outer;
+    CHECK(LogBatch::active());
+    log->info("Found 200 messages in the queue");
+    {
+      LogBatch inner;
+      log->info("Scale up successful");
+    }
+    CHECK_EQ(pending(), 0);
+  }
+  CHECK(!LogBatch::active());
+  std::string got(static_cast<size_t>(pending()), '\0');
+  CHECK_EQ(::read(p[0], got.data(), got.size()), static_cast<ssize_t>(got.size()));
+  const size_t a = got.find("msg=\"Found 200 messages in the queue\"\n");
+  const size_t b = got.find("msg=\"Scale up successful\"\n");
+  CHECK(a != std::string::npos && b != std::string::npos && a < b);
+  CHECK(got.rfind("time=\"", 0) == 0 && got.back() == '\n');
+  {
+    LogBatch batch;
+    log->info("first");
+    log->log(Level::Fatal, "second");
+    CHECK(pending() > 0);
+    std::string now(static_cast<size_t>(pending()), '\0');
+    CHECK_EQ(::read(p[0], now.data(), now.size()), static_cast<ssize_t>(now.size()));
+    CHECK(now.find("msg=first") < now.find("msg=second"));
+  }
+  std::string data;
+  std::thread reader([&] {
+    char buf[65536];
+    ssize_t r;
+    while ((r = ::read(p[0], buf, sizeof buf)) > 0) data.append(buf, static_cast<size_t>(r));
+  });
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([log, t] {
+      auto child = log->with_fields({{"queue", "q" + std::to_string(t)}});
+      for (int i = 0; i < 200; ++i) {
+        LogBatch batch;  // 2 lines per batch; every 50th batch over PIPE_BUF
+        child->info("Found " + std::to_string(i) + " messages in the queue");
+        child->info(i % 50 == 0 ? std::string(PIPE_BUF, 'y') : std::string("Scale up successful"));
+      }
+    });
+  for (auto& t : ts) t.join();
+  ::close(p[1]);
+  reader.join();
+  ::close(p[0]);
+  size_t n = 0, start = 0;
+  for (size_t nl; (nl = data.find('\n', start)) != std::string::npos; start = nl + 1, ++n) {
+    std::string l = data.substr(start, nl - start);
+    CHECK(l.rfind("time=\"", 0) == 0);
+    CHECK(l.size() > 8 && l.compare(l.size() - 8, 7, "queue=q") == 0);
+  }
+  CHECK_EQ(start, data.size());
+  CHECK_EQ(n, size_t(3200));
 }
 
 TEST(token_bucket_concurrent_reservations) {
