@@ -14,6 +14,8 @@
 #include <mutex>
 #include <ctime>
 
+#include "log.h"
+
 namespace ksa {
 
 using Nanos = int64_t;
@@ -83,6 +85,7 @@ class RealClock final : public Clock {
         .count();
   }
   bool sleep(Nanos d, StopFlag* stop) override {
+    if (d > 0) log_flush_pending();  // nothing held back by a wait (log.h)
     if (stop) return stop->wait_for(d);
     if (d > 0) {
       struct timespec ts;

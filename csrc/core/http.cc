@@ -1,6 +1,7 @@
 #include "http.h"
 
 #include "affinity.h"
+#include "log.h"
 
 #include <csignal>
 #include <mutex>
@@ -1175,6 +1176,8 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   const bool reused = conn_->uses > 1;
   Status s;
   conn_->stream->set_spin_ns(spin_window());
+  // The request is on the wire: the poll's held log lines go out while the server works on it.
+  log_flush_pending();
   Reader rd(conn_->stream.get(), &conn_->rbuf);
   std::string head;
   bool got_any = false;

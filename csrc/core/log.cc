@@ -118,6 +118,11 @@ LogBatch::~LogBatch() {
 
 bool LogBatch::active() { return thread_batch().depth > 0; }
 
+void log_flush_pending() {
+  ThreadBatch& b = thread_batch();
+  if (b.depth > 0 && !b.buf.empty()) b.flush();
+}
+
 size_t LineGate::slot_index() {
   static std::atomic<size_t> next{0};
   thread_local const size_t idx = next.fetch_add(1, std::memory_order_relaxed) % kSlots;

@@ -73,7 +73,7 @@ class LineGate {
 // poll, so the poll's lines -- "Found N messages", the scale result -- cost one system call,
 // made after the replica write instead of between the SQS response and the PUT. Each line keeps
 // the timestamp of the moment it was logged and the order is unchanged; only the write moves
-// (by the length of the poll). A batch of at most PIPE_BUF bytes is one atomic write, like a
+// (by at most one round trip: see log_flush_pending). A batch of at most PIPE_BUF bytes is one atomic write, like a
 // single line; a longer one goes out alone (LineGate::exclusive). Fatal and panic lines, custom
 // sinks and custom time sources are never held back.
 class LogBatch {
@@ -84,6 +84,12 @@ class LogBatch {
   LogBatch& operator=(const LogBatch&) = delete;
   static bool active();  // is the calling thread inside a batch?
 };
+
+// Writes out what the calling thread's batch holds so far (the batch stays open). Called where
+// the thread is about to wait anyway -- a request is on the wire (HttpClient), or a deliberate
+// sleep (RealClock: back-off, Retry-After, throttle) -- so a line is never held back by a wait
+// longer than a round trip and its write overlaps the wait. No-op outside a batch.
+void log_flush_pending();
 
 enum class Level : int { Panic = 0, Fatal = 1, Error = 2, Warn = 3, Info = 4, Debug = 5, Trace = 6 };
 

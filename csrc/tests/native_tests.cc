@@ -733,6 +733,8 @@ TEST(log_batch_holds_lines_until_end) {
       log->info("Scale up successful");
     }
     CHECK_EQ(pending(), 0);
+    RealClock().sleep(0, nullptr);  // no wait: nothing flushed
+    CHECK_EQ(pending(), 0);
   }
   CHECK(!LogBatch::active());
   std::string got(static_cast<size_t>(pending()), '\0');
@@ -749,6 +751,13 @@ TEST(log_batch_holds_lines_until_end) {
     std::string now(static_cast<size_t>(pending()), '\0');
     CHECK_EQ(::read(p[0], now.data(), now.size()), static_cast<ssize_t>(now.size()));
     CHECK(now.find("msg=first") < now.find("msg=second"));
+    log->info("third");
+    CHECK_EQ(pending(), 0);
+    RealClock().sleep(1000, nullptr);  // a deliberate wait writes out what is held
+    CHECK(pending() > 0);
+    std::string third(static_cast<size_t>(pending()), '\0');
+    CHECK_EQ(::read(p[0], third.data(), third.size()), static_cast<ssize_t>(third.size()));
+    CHECK(third.find("msg=third\n") != std::string::npos);
   }
   std::string data;
   std::thread reader([&] {

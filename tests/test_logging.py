@@ -101,3 +101,32 @@ def test_make_logger_picks_colors_on_a_tty(nat):
     finally:
         for fd in (master, slave, r, w):
             os.close(fd)
+
+
+def test_poll_lines_batched_in_order_over_the_wire(nat, tmp_path):
+    """The production fd sink on a real clock: each poll's lines are held past the SQS answer
+    and written while the replica write is on the wire or when the poll ends (LogBatch,
+    csrc/core/log.h) -- same lines, same order as the reference (main.go:49,
+    scale/scale.go:79), each stamped when it was logged."""
+    import os
+
+    from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
+
+    path = tmp_path / "loop.log"
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o600)
+    env = BenchEnv(1, "scale", log_fd=fd)
+    try:
+        env.run(20)
+    finally:
+        env.close()
+        os.close(fd)
+    lines = path.read_text().splitlines()
+    msgs = [l.split('msg="', 1)[1].rsplit('"', 1)[0] for l in lines]
+    assert len(msgs) == 40
+    for i in range(0, 40, 4):  # the trace alternates 200 / 0 messages
+        assert msgs[i] == "Found 200 messages in the queue"
+        assert msgs[i + 1].startswith("Scale up successful. Replicas: ")
+        assert msgs[i + 2] == "Found 0 messages in the queue"
+        assert msgs[i + 3].startswith("Scale down successful. Replicas: ")
+    stamps = [l.split('time="', 1)[1].split('"', 1)[0] for l in lines]
+    assert stamps == sorted(stamps)
