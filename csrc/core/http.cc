@@ -1176,8 +1176,6 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   const bool reused = conn_->uses > 1;
   Status s;
   conn_->stream->set_spin_ns(spin_window());
-  // The request is on the wire: the poll's held log lines go out while the server works on it.
-  log_flush_pending();
   Reader rd(conn_->stream.get(), &conn_->rbuf);
   std::string head;
   bool got_any = false;
@@ -1256,6 +1254,10 @@ Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t d
                            bool* retryable) {
   Status s = write_request(req, deadline_ns, retryable);
   if (!s.ok()) return s;
+  // The request is on the wire: the poll's held log lines go out while the server works on it.
+  // (Not in receive(): a pipelined response has usually arrived already, and the write would
+  // sit between it and the next request.)
+  log_flush_pending();
   return read_response(req, resp, deadline_ns, retryable);
 }
 
