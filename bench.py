@@ -78,8 +78,11 @@ def main(argv=None) -> int:
     ap.add_argument("--no-sweep", action="store_true", help="skip the 1/2/4/8-queue sweep (single rank only)")
     ap.add_argument("--no-pipeline", action="store_true", help="strictly sequential SQS -> GET -> write")
     ap.add_argument("--busy-poll-us", type=int, default=25, help="adaptive client busy-poll window (CLI default --busy-poll=25us; 0: block)")
-    ap.add_argument("--servers", default="shared", choices=["shared", "per-queue"],
-                    help="fake SQS/apiserver: one pair for all of this rank's queues, or one pair per queue")
+    ap.add_argument("--servers", default="auto", choices=["auto", "shared", "per-queue", "processes"],
+                    help="fake SQS/apiserver: one in-process pair for all of this rank's queues (shared), one "
+                         "in-process pair per queue, or one endpoint process per queue (processes, so the "
+                         "fakes' threads do not share the autoscaler's process); auto: shared for one queue, "
+                         "processes for more")
     ap.add_argument("--loggers", default="shared", choices=["shared", "per-queue"],
                     help="one logrus-style logger for the rank (as the reference's global logger) or one per queue")
     ap.add_argument("--secondary-samples", type=int, default=2000,
@@ -114,7 +117,8 @@ def main(argv=None) -> int:
     native()  # build/load before timing
     pipeline = not args.no_pipeline
     bp = args.busy_poll_us * 1000
-    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp, servers=args.servers,
+    servers = args.servers if args.servers != "auto" else ("shared" if args.queues == 1 else "processes")
+    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp, servers=servers,
                    loggers=args.loggers)
     try:
         if args.warmup:
@@ -165,6 +169,7 @@ def main(argv=None) -> int:
             "scale_mode": args.mode,
             "pipeline_reads": pipeline,
             "busy_poll_us": args.busy_poll_us,
+            "fake_endpoints": servers,
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
