@@ -210,6 +210,7 @@ class Stream {
     }
     while (true) {
       ssize_t n = ::recv(fd_, tmp, sizeof tmp, 0);
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK) && spin_ns_ > 0) n = spin_recv(tmp, sizeof tmp);
       if (n > 0) {
         buf->append(tmp, static_cast<size_t>(n));
         return Status::OK();
@@ -220,7 +221,6 @@ class Stream {
       }
       if (errno == EINTR) continue;
       if (errno == EAGAIN || errno == EWOULDBLOCK) {
-        if (spin_ns_ > 0 && spin_for_data()) continue;
         Status s = wait_fd(fd_, POLLIN, deadline_ns, cancel_fd_);
         if (!s.ok()) return s;
         continue;
@@ -315,6 +315,25 @@ class Stream {
       if (n > 0 || n == 0) return true;  // data or orderly close: let the caller read it
       if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return true;  // surface the error
       if ((i & 15) == 15 && mono_ns() >= end) return false;
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
+
+  // Busy-poll on a plain socket: reads directly, so the bytes that end the spin are taken by
+  // the same system call that sees them (a peek would need a second one to read them).
+  // Returns recv's result; -1 with errno EAGAIN when the window passed without data.
+  ssize_t spin_recv(char* out, size_t cap) {
+    const int64_t end = mono_ns() + spin_ns_;
+    for (int i = 0;; ++i) {
+      const ssize_t n = ::recv(fd_, out, cap, 0);
+      if (n >= 0) return n;
+      if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return n;
+      if ((i & 15) == 15 && mono_ns() >= end) {
+        errno = EAGAIN;
+        return -1;
+      }
 #if defined(__x86_64__)
       __builtin_ia32_pause();
 #endif
