@@ -160,7 +160,9 @@ class Stream {
   // Drives an SSL_* call that may want read/write readiness.
   template <class F>
   Status ssl_op(F op, int64_t deadline_ns, int* out, const char* what) {
-    while (true) {
+    int64_t spin_end = 0;
+    bool spin_over = false;
+    for (int i = 0;; ++i) {
       ERR_clear_error();
       int r = op();
       if (r > 0) {
@@ -169,8 +171,19 @@ class Stream {
       }
       int e = SSL_get_error(ssl_, r);
       if (e == SSL_ERROR_WANT_READ) {
-        // Busy-poll applies to TLS too: the record's bytes land on the raw socket.
-        if (spin_ns_ > 0 && spin_for_data()) continue;
+        // Busy-poll applies to TLS too: retry the operation itself (a non-blocking read of the
+        // socket underneath) for up to spin_ns_, so the call that sees the record's bytes also
+        // decrypts them; then sleep in poll(2).
+        if (spin_ns_ > 0 && !spin_over) {
+          if (spin_end == 0) spin_end = mono_ns() + spin_ns_;
+          if ((i & 7) != 7 || mono_ns() < spin_end) {
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+            continue;
+          }
+          spin_over = true;
+        }
         Status s = wait_fd(fd_, POLLIN, deadline_ns, cancel_fd_);
         if (!s.ok()) return s;
       } else if (e == SSL_ERROR_WANT_WRITE) {
@@ -304,25 +317,10 @@ class Stream {
   }
 
  private:
-  // Busy-poll: peek the socket for up to spin_ns_ before sleeping in poll(2). A response that
-  // lands within the window is picked up without a scheduler wake-up (several microseconds on
-  // every round trip); past it the thread blocks as usual, so idle waits cost no CPU.
-  bool spin_for_data() {
-    const int64_t end = mono_ns() + spin_ns_;
-    char c;
-    for (int i = 0;; ++i) {
-      ssize_t n = ::recv(fd_, &c, 1, MSG_PEEK | MSG_DONTWAIT);
-      if (n > 0 || n == 0) return true;  // data or orderly close: let the caller read it
-      if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return true;  // surface the error
-      if ((i & 15) == 15 && mono_ns() >= end) return false;
-#if defined(__x86_64__)
-      __builtin_ia32_pause();
-#endif
-    }
-  }
-
-  // Busy-poll on a plain socket: reads directly, so the bytes that end the spin are taken by
-  // the same system call that sees them (a peek would need a second one to read them).
+  // Busy-poll on a plain socket: keep reading (non-blocking) for up to spin_ns_ before sleeping
+  // in poll(2). A response that lands within the window is picked up without a scheduler
+  // wake-up (several microseconds on every round trip), and by the same system call that sees
+  // it; past the window the thread blocks as usual, so idle waits cost no CPU.
   // Returns recv's result; -1 with errno EAGAIN when the window passed without data.
   ssize_t spin_recv(char* out, size_t cap) {
     const int64_t end = mono_ns() + spin_ns_;
