@@ -16,7 +16,11 @@ v1.35.35's resolution order (go.mod:6):
    allowed);
 4. remote: ECS task role (``AWS_CONTAINER_CREDENTIALS_RELATIVE_URI`` /
    ``AWS_CONTAINER_CREDENTIALS_FULL_URI`` + ``AWS_CONTAINER_AUTHORIZATION_TOKEN``), otherwise
-   the EC2 instance role through IMDSv2 (token PUT, falling back to IMDSv1).
+   the EC2 instance role through IMDSv2 (token PUT, falling back to IMDSv1). A plain-http
+   ``FULL_URI`` must name a loopback host, as in the SDK; as an extension (what later SDKs
+   added for EKS Pod Identity) the Pod Identity Agent's addresses 169.254.170.23 /
+   fd00:ec2::23 are accepted too, and ``AWS_CONTAINER_AUTHORIZATION_TOKEN_FILE`` (re-read on
+   every fetch: the agent's token rotates) takes precedence over the inline token.
 
 Resolution is lazy: nothing is fetched until the first poll (like the SDK), and the native
 ``CachedCredentials`` (csrc/core/sigv4.h) only calls :meth:`ChainProvider.retrieve` again
@@ -266,6 +270,33 @@ class WebIdentityProvider(_Provider):
         return _make(akid, secret, tok or "", parse_expiration(exp) if exp else 0, self.name)
 
 
+# EKS Pod Identity Agent endpoints (link-local; served by the node's agent).
+_POD_IDENTITY_HOSTS = ("169.254.170.23", "fd00:ec2::23")
+
+
+def _full_uri_error(url: str) -> str:
+    """Why ``AWS_CONTAINER_CREDENTIALS_FULL_URI`` may not be used ("" if it may)."""
+    import ipaddress
+
+    try:
+        u = urllib.parse.urlsplit(url)
+        host = u.hostname or ""
+    except ValueError as e:
+        return f"invalid URL, {e}"
+    if not host:
+        return "unable to parse host from local HTTP cred provider URL"
+    if u.scheme == "https" or host in _POD_IDENTITY_HOSTS:
+        return ""
+    if host == "localhost":
+        return ""
+    try:
+        if ipaddress.ip_address(host).is_loopback:
+            return ""
+    except ValueError:
+        pass
+    return f"invalid endpoint host, {host!r}, only loopback hosts are allowed."
+
+
 class RemoteProvider(_Provider):
     """ECS container credentials when configured, otherwise EC2 IMDS (v2 with v1 fallback)."""
 
@@ -287,9 +318,23 @@ class RemoteProvider(_Provider):
     def fetch(self):
         url = self._ecs_url()
         if url:
+            if not self.env.get("AWS_CONTAINER_CREDENTIALS_RELATIVE_URI"):
+                err = _full_uri_error(url)
+                if err:
+                    raise CredentialsError(f"CredentialsEndpointError: {err}")
             headers = {}
-            if self.env.get("AWS_CONTAINER_AUTHORIZATION_TOKEN"):
-                headers["Authorization"] = self.env["AWS_CONTAINER_AUTHORIZATION_TOKEN"]
+            token = self.env.get("AWS_CONTAINER_AUTHORIZATION_TOKEN", "")
+            token_file = self.env.get("AWS_CONTAINER_AUTHORIZATION_TOKEN_FILE", "")
+            if token_file:
+                try:
+                    with open(token_file) as f:
+                        token = f.read().rstrip("\r\n")
+                except OSError as e:
+                    raise CredentialsError(f"CredentialsEndpointError: failed to read authorization token file: {e}")
+            if "\r" in token or "\n" in token:
+                raise CredentialsError("CredentialsEndpointError: authorization token contains invalid characters")
+            if token:
+                headers["Authorization"] = token
             status, body = self.http("GET", url, headers, b"", 5.0)
             if status != 200:
                 raise CredentialsError(f"CredentialsEndpointError: failed to load credentials (HTTP {status})")

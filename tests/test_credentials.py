@@ -226,3 +226,51 @@ def test_malformed_remote_credentials_are_credential_errors(nat, body):
     p = cr.RemoteProvider({"AWS_CONTAINER_CREDENTIALS_FULL_URI": "http://169.254.170.2/creds"}, fetch)
     with pytest.raises(cr.CredentialsError):
         p.fetch()
+
+
+@pytest.mark.parametrize("url,ok", [
+    ("http://127.0.0.1:51679/creds", True), ("http://localhost/creds", True), ("http://[::1]/creds", True),
+    ("http://169.254.170.23/v1/credentials", True), ("http://[fd00:ec2::23]/v1/credentials", True),
+    ("https://creds.example.com/role", True), ("http://10.0.0.8/creds", False), ("http://169.254.170.2/creds", False),
+])
+def test_full_uri_host_rules(nat, url, ok):
+    """A plain-http FULL_URI must be loopback (or the EKS Pod Identity Agent); anything else is
+    refused before a request is sent."""
+    sent = []
+
+    def fetch(method, u, headers, body, timeout):
+        sent.append(u)
+        return 200, json.dumps({"AccessKeyId": "F", "SecretAccessKey": "S", "Token": "T",
+                                "Expiration": "2030-01-01T00:00:00Z"}).encode()
+
+    p = cr.RemoteProvider({"AWS_CONTAINER_CREDENTIALS_FULL_URI": url}, fetch)
+    if ok:
+        assert p.fetch().access_key_id == "F" and sent == [url]
+    else:
+        with pytest.raises(cr.CredentialsError, match="only loopback hosts are allowed"):
+            p.fetch()
+        assert sent == []
+
+
+def test_eks_pod_identity_token_file_is_reread(nat, tmp_path):
+    """EKS Pod Identity: the agent's token is read from AWS_CONTAINER_AUTHORIZATION_TOKEN_FILE on
+    every fetch (it rotates) and wins over AWS_CONTAINER_AUTHORIZATION_TOKEN."""
+    tok = tmp_path / "eks-pod-identity-token"
+    tok.write_text("token-1")
+    seen = []
+
+    def fetch(method, url, headers, body, timeout):
+        seen.append(headers.get("Authorization"))
+        return 200, json.dumps({"AccessKeyId": "POD", "SecretAccessKey": "S", "Token": "T",
+                                "Expiration": "2030-01-01T00:00:00Z"}).encode()
+
+    env = {"AWS_CONTAINER_CREDENTIALS_FULL_URI": "http://169.254.170.23/v1/credentials",
+           "AWS_CONTAINER_AUTHORIZATION_TOKEN_FILE": str(tok), "AWS_CONTAINER_AUTHORIZATION_TOKEN": "inline"}
+    c = chain(env, fetch).retrieve()
+    assert c.access_key_id == "POD" and c.provider_name == "ECSCredentialsProvider"
+    tok.write_text("token-2\n")
+    cr.RemoteProvider(env, fetch).fetch()
+    assert seen == ["token-1", "token-2"]
+    tok.unlink()
+    with pytest.raises(cr.CredentialsError, match="token file"):
+        cr.RemoteProvider(env, fetch).fetch()
