@@ -175,11 +175,21 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
         log.log("info", "Starting kube-sqs-autoscaler")  # main.go:114
         fleet.start(max_iterations)
+        worker_died = False
         while not fleet.wait(0.2):
-            pass
+            if cfg.worker_processes and not worker_died and fleet.failed():
+                # One queue's worker died (a crash, an OOM kill): stop the rest and exit non-zero
+                # so the pod restarts with every queue polled, as when a thread crash takes the
+                # whole process down.
+                worker_died = True
+                log.log("error", f"worker process(es) {fleet.failed()} died (exit codes {fleet.exit_codes()}); "
+                                 "stopping the other workers")
+                fleet.stop()
         fleet.join()
         if cfg.worker_processes and any(c not in (0, None) for c in fleet.exit_codes()):
             log.log("error", f"worker process exit codes: {fleet.exit_codes()}")
+            if not got:
+                return 1
         if lost.is_set():
             log.log("fatal", "leaderelection lost")
             return 1

@@ -259,6 +259,16 @@ class ProcessFleet:
         while not self.wait(1.0):
             pass
 
+    def failed(self) -> List[int]:
+        """Indices of workers that exited with an error or were killed (an OOM kill, a crash).
+
+        Threads of one process die together and the pod restarts; a worker process can die alone,
+        so the supervisor asks this and brings the whole fleet down instead of letting one queue
+        go unpolled while the others carry on."""
+        self._reap()
+        return [i for i, w in enumerate(self.workers)
+                if w.pid in self._reaped and os.waitstatus_to_exitcode(self._reaped[w.pid]) != 0]
+
     def exit_codes(self) -> List[int]:
         self._reap()
         return [os.waitstatus_to_exitcode(self._reaped[w.pid]) if w.pid in self._reaped else None for w in self.workers]

@@ -161,3 +161,33 @@ def test_metrics_and_health_over_worker_processes(nat, servers):
         m.stop()
         fleet.close()
     assert kube.replicas("gpu", "w0") == 7 and kube.replicas("gpu", "w1") == 1
+
+
+def test_a_dead_worker_process_brings_the_fleet_down(servers):
+    """A worker process killed on its own (the OOM killer, a crash) must not leave its queue
+    unpolled while the others carry on: the supervisor stops the rest and exits non-zero, so the
+    pod restarts -- what a crashing thread does to the single-process fleet."""
+    sqs, kube, env = servers
+    specs = _specs(sqs, kube, ["0", "0", "0"])
+    e = dict(os.environ)
+    e.update(env)
+    p = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", f"--aws-region={REGION}",
+                          f"--sqs-endpoint={sqs.url}", "--poll-period=20ms", "--worker-processes", *specs],
+                         cwd=ROOT, env=e, stderr=subprocess.PIPE, text=True)
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline and sqs.requests() < 6:
+            time.sleep(0.05)
+        with open(f"/proc/{p.pid}/task/{p.pid}/children") as f:
+            kids = [int(x) for x in f.read().split()]
+        assert len(kids) == 3
+        os.kill(kids[1], signal.SIGKILL)
+        assert p.wait(timeout=20) == 1
+        err = p.stderr.read()
+        assert "worker process(es) [1] died" in err and "-9" in err
+    finally:
+        if p.poll() is None:
+            p.kill()
+    n = sqs.requests()
+    time.sleep(0.2)
+    assert sqs.requests() == n  # the surviving workers were stopped too
