@@ -164,6 +164,8 @@ py::dict http_stats_dict(const HttpClientStats& s) {
   d["idle_closed"] = s.idle_closed;
   d["bytes_out"] = s.bytes_out;
   d["bytes_in"] = s.bytes_in;
+  d["tls_version"] = s.tls_version;
+  d["tls_cipher"] = s.tls_cipher;
   return d;
 }
 

@@ -861,6 +861,9 @@ Status HttpClient::init_tls_ctx() {
   if (!ctx_) return Status::Err("SSL_CTX_new: " + ssl_error_string());
   Status st;
   SSL_CTX_set_min_proto_version(ctx_, TLS1_2_VERSION);
+  // TLS 1.3 suites in crypto/tls's client order on AES-capable CPUs (AES-128-GCM first; OpenSSL's
+  // own default leads with AES-256-GCM): the reference's clients offer this order.
+  SSL_CTX_set_ciphersuites(ctx_, "TLS_AES_128_GCM_SHA256:TLS_CHACHA20_POLY1305_SHA256:TLS_AES_256_GCM_SHA384");
   if (tls_.insecure_skip_verify) {
     SSL_CTX_set_verify(ctx_, SSL_VERIFY_NONE, nullptr);
   } else {
@@ -1100,6 +1103,8 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
       return h;
     }
     if (SSL_session_reused(ssl)) stats_.tls_resumptions++;
+    stats_.tls_version = SSL_get_version(ssl);
+    stats_.tls_cipher = SSL_get_cipher_name(ssl);
   }
   conn_ = std::make_unique<Conn>();
   conn_->stream = std::move(stream);

@@ -73,6 +73,8 @@ struct HttpClientStats {
   uint64_t idle_closed = 0;  // reused connections found closed by the peer before a write
   uint64_t bytes_out = 0;
   uint64_t bytes_in = 0;
+  std::string tls_version;  // of the last TLS connection ("" before one), e.g. "TLSv1.3"
+  std::string tls_cipher;   // its cipher suite, e.g. "TLS_AES_128_GCM_SHA256"
 };
 
 // One persistent connection to one origin. Thread-safe (requests are serialised), but each

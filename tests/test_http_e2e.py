@@ -385,6 +385,8 @@ def test_tls_reconnect_resumes_session(nat):
             time.sleep(0.02)
         st = c.stats()
         assert st["connects"] == 4 and st["tls_resumptions"] == 3
+        # TLS 1.3 with crypto/tls's suite order (AES-128-GCM first), as the reference's clients
+        assert (st["tls_version"], st["tls_cipher"]) == ("TLSv1.3", "TLS_AES_128_GCM_SHA256")
     finally:
         k.stop()
 
