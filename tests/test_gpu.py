@@ -71,6 +71,62 @@ def test_cli_gpu_aware_max_local(tmp_path, capfd):
         kube.stop()
 
 
+def test_cli_gpu_aware_max_local_with_worker_processes(tmp_path):
+    """--gpu-aware-max=local with --worker-processes, in a fresh process as in production: the
+    workers are forked first, then the supervisor runs the gfx950 probe and forwards the cap to
+    every worker through its shared slot. Two queues, both capped at the healthy GPU count."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    import yaml
+
+    from kube_sqs_autoscaler_amd.ops import gpu, native
+
+    nat = native()
+    n_gpus = gpu.device_count()
+    sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs.start()
+    kube.start()
+    p = None
+    try:
+        specs = []
+        for i in range(2):
+            url = f"{sqs.url}/1/q{i}"
+            sqs.set_attributes(url, {"ApproximateNumberOfMessages": "1000"})
+            kube.add_deployment("ml", f"w{i}", 1)
+            specs += ["--queue", f"url={url},deployment=w{i},namespace=ml,attribute-names=ApproximateNumberOfMessages"]
+        kc = tmp_path / "kc"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": "x"}}], "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = dict(os.environ, AWS_ACCESS_KEY_ID="a", AWS_SECRET_ACCESS_KEY="b", KUBE_CONFIG_PATH=str(kc))
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        p = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", "--aws-region=us-east-1",
+                              f"--sqs-endpoint={sqs.url}", "--poll-period=5ms", "--scale-up-cool-down=0s", "--max-pods=64",
+                              "--gpu-aware-max=local", "--kube-api-qps=0", "--worker-processes", *specs],
+                             cwd=root, env=env, stderr=subprocess.PIPE, text=True)
+        want = min(64, n_gpus)
+        deadline = time.time() + 90
+        while time.time() < deadline and p.poll() is None and \
+                [kube.replicas("ml", f"w{i}") for i in range(2)] != [want, want]:
+            time.sleep(0.05)
+        polled = sqs.requests()
+        time.sleep(0.3)  # more polls: the cap holds
+        assert sqs.requests() >= polled + 20
+        assert [kube.replicas("ml", f"w{i}") for i in range(2)] == [want, want]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=30) == 0
+        assert f"GPU capacity: {n_gpus} pods" in p.stderr.read()
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        sqs.stop()
+        kube.stop()
+
+
 def _random_walk_trace(n, seed):
     import numpy as np
 
