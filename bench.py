@@ -192,11 +192,16 @@ def main(argv=None) -> int:
             # Production endpoints are HTTPS: the same two paths over keep-alive TLS 1.3
             rows["tls"] = (1, args.mode, pipeline, bp, True, "shared", "threads")
             rows["reference_tls"] = (1, "deployment", False, 0, True, "shared", "threads")
+            # --sqs-protocol=json (AWS JSON 1.0, what current SDKs speak to SQS) instead of the
+            # reference's Query/XML
+            rows["sqs_json"] = (1, args.mode, pipeline, bp, False, "shared", "threads", "json")
             p50s = {k: [] for k in rows}
             samples = {k: [] for k in rows}
             for _ in range(3):
-                for k, (q, mode, pl, b, tls, sv, wk) in rows.items():
-                    sm = measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls, servers=sv, workers=wk).summary()
+                for k, (q, mode, pl, b, tls, sv, wk, *proto) in rows.items():
+                    extra_kw = {"sqs_protocol": proto[0]} if proto else {}
+                    sm = measure(q, n, w, mode, pipeline=pl, busy_poll_ns=b, tls=tls, servers=sv, workers=wk,
+                                 **extra_kw).summary()
                     p50s[k].append(sm["p50_ms"])
                     samples[k].append(sm["samples"])
             med = {k: sorted(v)[1] for k, v in p50s.items()}
@@ -208,6 +213,7 @@ def main(argv=None) -> int:
             extra["sequential_scale_p50_ms"] = med["sequential"]
             extra["reference_equivalent_p50_ms"] = med["reference"]
             extra["tls_p50_ms"] = {"default": med["tls"], "reference_equivalent": med["reference_tls"]}
+            extra["sqs_json_protocol_p50_ms"] = med["sqs_json"]
             extra["secondary_rows_p50_ms_all_rounds"] = p50s
             extra["secondary_rows_samples_per_round"] = samples
             # Regional-RTT model: the fakes add 2 ms (SQS) / 1 ms (apiserver) per request, so the

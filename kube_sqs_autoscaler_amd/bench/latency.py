@@ -183,7 +183,7 @@ class BenchEnv:
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared", affinity: str = "none",
-                 log_level: str = "info"):
+                 log_level: str = "info", sqs_protocol: str = "query"):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -267,7 +267,7 @@ class BenchEnv:
                              scale_down_messages=10, max_pods=8, min_pods=1)
             kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=busy_poll_ns)
             scaler = new_pod_autoscaler(t, kube_api, log, self.clock)
-            sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, credentials=creds, tls=sqs_tls,
+            sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds, tls=sqs_tls,
                                   busy_poll_ns=busy_poll_ns)
             client = new_sqs_client(t, sqs_api)
             self.kube_apis.append(kube_api)
