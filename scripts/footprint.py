@@ -1,6 +1,6 @@
 """Process footprint vs the reference pod budget (100m CPU, 200Mi; README.md:60-66): RSS, threads and
 steady CPU of the CLI tracking 1 and 64 queues at 1 s polls against localhost fakes."""
-import os, subprocess, sys, time, yaml, resource
+import os, subprocess, sys, time, yaml
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from kube_sqs_autoscaler_amd.ops import native
 nat = native()

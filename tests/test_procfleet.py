@@ -8,7 +8,6 @@ import time
 import pytest
 import yaml
 
-from kube_sqs_autoscaler_amd.config import TargetConfig
 from kube_sqs_autoscaler_amd.parallel.procfleet import ProcessFleet
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
