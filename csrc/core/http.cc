@@ -502,24 +502,45 @@ class Reader {
   std::string* buf_;
 };
 
-void parse_header_lines(const std::string& head, size_t from, Headers* out) {
-  // Spans trimmed in place: one string per name and per value, nothing else allocated.
+// Header lines as Go's textproto.Reader.ReadMIMEHeader reads them (net/http, client and server):
+// "Name: value", a line starting with a space or tab continues the previous value (obs-fold),
+// and a line without a colon -- or a continuation with nothing to continue -- is a protocol error
+// ("malformed MIME header line"); *bad gets the line. Spans are trimmed in place: one string per
+// name and per value, nothing else allocated.
+bool parse_header_lines(const std::string& head, size_t from, Headers* out, std::string* bad) {
   auto trimmed = [&](size_t b, size_t e) {
     while (b < e && (head[b] == ' ' || head[b] == '\t')) ++b;
     while (e > b && (head[e - 1] == ' ' || head[e - 1] == '\t' || head[e - 1] == '\r')) --e;
     return std::string(head, b, e - b);
   };
   size_t pos = from;
+  const size_t first = out->size();
   while (pos < head.size()) {
     size_t e = head.find("\r\n", pos);
     if (e == std::string::npos) e = head.size();
-    const char* colon = static_cast<const char*>(std::memchr(head.data() + pos, ':', e - pos));
-    if (colon) {
+    if (e > pos && (head[pos] == ' ' || head[pos] == '\t')) {
+      if (out->size() == first) {  // "malformed MIME header initial line"
+        *bad = head.substr(pos, e - pos);
+        return false;
+      }
+      std::string more = trimmed(pos, e);
+      if (!more.empty()) {
+        std::string& v = out->back().second;
+        if (!v.empty()) v.push_back(' ');
+        v += more;
+      }
+    } else if (e > pos) {
+      const char* colon = static_cast<const char*>(std::memchr(head.data() + pos, ':', e - pos));
+      if (!colon) {
+        *bad = head.substr(pos, e - pos);
+        return false;
+      }
       const size_t c = static_cast<size_t>(colon - head.data());
       out->emplace_back(trimmed(pos, c), trimmed(c + 1, e));
     }
     pos = e + 2;
   }
+  return true;
 }
 
 bool wants_close(const Headers& hs, bool http10) {
@@ -1158,10 +1179,11 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   if (!has_header(req.headers, "User-Agent")) wire += "User-Agent: kube-sqs-autoscaler-amd/1.0\r\n";
   for (auto& [k, v] : req.headers) line(k, v);
   if (!req.body.empty() || req.method == "POST" || req.method == "PUT" || req.method == "PATCH") {
-    if (!has_header(req.headers, "Content-Length"))
+    if (!has_header(req.headers, "Content-Length")) {
       wire += "Content-Length: ";
       wire += std::to_string(req.body.size());
       wire += "\r\n";
+    }
   }
   wire += "\r\n";
   wire += req.body;
@@ -1225,7 +1247,11 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
     size_t sp2 = status_line.find(' ', sp1 + 1);
     resp->reason = sp2 == std::string::npos ? "" : status_line.substr(sp2 + 1);
     resp->headers.clear();
-    if (eol != std::string::npos) parse_header_lines(head, eol + 2, &resp->headers);
+    std::string bad;
+    if (eol != std::string::npos && !parse_header_lines(head, eol + 2, &resp->headers, &bad)) {
+      conn_.reset();
+      return Status::Err("net/http: malformed MIME header line: " + bad);
+    }
     if (resp->status >= 100 && resp->status < 200 && resp->status != 101) continue;  // interim
     break;
   }
@@ -1465,7 +1491,15 @@ void HttpServer::serve(int fd) {
         if (req.target[0] == '?') req.target = "/" + req.target;
       }
       const bool http10 = line.compare(b + 1, 8, "HTTP/1.0") == 0;
-      if (eol != std::string::npos) parse_header_lines(head, eol + 2, &req.headers);
+      std::string bad;
+      if (eol != std::string::npos && !parse_header_lines(head, eol + 2, &req.headers, &bad)) {
+        // net/http's server answers a malformed header with 400 and closes the connection
+        const std::string msg = "400 Bad Request: malformed MIME header line: " + bad;
+        stream.write_all("HTTP/1.1 400 Bad Request\r\nContent-Type: text/plain; charset=utf-8\r\n"
+                         "Connection: close\r\nContent-Length: " + std::to_string(msg.size()) + "\r\n\r\n" + msg,
+                         mono_ns() + kSecond);
+        break;
+      }
       Status s;
       if (is_chunked(req.headers)) {
         s = rd.read_chunked(&req.body, 0);
@@ -1483,10 +1517,11 @@ void HttpServer::serve(int fd) {
       std::string wire = "HTTP/1.1 " + std::to_string(resp.status) + " " +
                          (resp.reason.empty() ? http_reason(resp.status) : resp.reason) + "\r\n";
       for (auto& [k, v] : resp.headers) wire += k + ": " + v + "\r\n";
-      if (!has_header(resp.headers, "Content-Length"))
+      if (!has_header(resp.headers, "Content-Length")) {
         wire += "Content-Length: ";
         wire += std::to_string(resp.body.size());
         wire += "\r\n";
+      }
       if (close_after) wire += "Connection: close\r\n";
       wire += "\r\n";
       wire += resp.body;

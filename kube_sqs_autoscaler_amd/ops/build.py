@@ -39,7 +39,8 @@ CXX = os.environ.get("CXX", "g++")
 CLANGXX = os.environ.get("FUZZ_CXX", "/opt/rocm/llvm/bin/clang++")
 GPU_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
-CXXFLAGS = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread"]
+CXXFLAGS = ["-std=c++17", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Werror=misleading-indentation",
+            "-Werror=return-type", "-pthread"]
 LIBS = ["-lssl", "-lcrypto", "-pthread"]
 
 

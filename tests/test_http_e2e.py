@@ -487,3 +487,95 @@ def test_retry_after_wait_counts_as_liveness_progress(nat, sqs_server, kube_serv
         r.cancel()
         th.join(10)
     assert not th.is_alive() and out[0]["up"] == "failed"
+
+
+def test_explicit_content_length_header_keeps_framing(nat):
+    """A request that carries its own Content-Length is sent with that header once and the body
+    right after it, so the keep-alive connection stays in sync for the next request."""
+    import json
+
+    k = nat.FakeKubeServer()
+    k.require_token(TOKEN)
+    k.start()
+    try:
+        k.add_deployment("ml", "w", 2)
+        c = nat.HttpClient(k.url)
+        auth = [("Authorization", f"Bearer {TOKEN}")]
+        path = "/apis/apps/v1/namespaces/ml/deployments/w/scale"
+        status, _, body = c.request("GET", path, auth)
+        assert status == 200
+        obj = json.loads(body)
+        obj["spec"]["replicas"] = 5
+        payload = json.dumps(obj).encode()
+        status, _, _ = c.request("PUT", path, auth + [("Content-Type", "application/json"),
+                                                     ("Content-Length", str(len(payload)))], payload)
+        assert status == 200
+        status, _, body = c.request("GET", path, auth)  # same connection: still framed correctly
+        assert status == 200 and json.loads(body)["spec"]["replicas"] == 5
+        assert c.stats()["connects"] == 1 and k.replicas("ml", "w") == 5
+    finally:
+        k.stop()
+
+
+def _raw_exchange(url, data):
+    import socket
+    import urllib.parse
+
+    u = urllib.parse.urlsplit(url)
+    with socket.create_connection((u.hostname, u.port), timeout=10) as s:
+        s.sendall(data)
+        out = b""
+        while True:
+            chunk = s.recv(65536)
+            if not chunk:
+                return out
+            out += chunk
+
+
+def test_server_rejects_malformed_header_line_like_net_http(nat):
+    """Go's net/http server answers a header line without a colon with 400 and closes; an
+    obs-fold continuation line joins the previous value (textproto.ReadMIMEHeader)."""
+    k = nat.FakeKubeServer()
+    k.start()
+    try:
+        bad = _raw_exchange(k.url, b"GET /healthz HTTP/1.1\r\nHost: x\r\nno colon here\r\n\r\n")
+        assert bad.startswith(b"HTTP/1.1 400 ") and b"malformed MIME header line: no colon here" in bad
+        folded = _raw_exchange(k.url, b"GET /apis/apps/v1/namespaces/ml/deployments/none/scale HTTP/1.1\r\n"
+                                      b"Host: x\r\nX-Long: a\r\n b\r\nConnection: close\r\n\r\n")
+        assert folded.startswith(b"HTTP/1.1 404 ")
+    finally:
+        k.stop()
+
+
+def test_client_rejects_malformed_response_header_line(nat):
+    """The client reads response headers as Go's transport does: a line without a colon is
+    "net/http: malformed MIME header line", an obs-fold line continues the previous value."""
+    import socket
+    import threading
+
+    replies = [b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\nX-Folded: a\r\n  b\r\n\r\nok",
+               b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\nbogus\r\n\r\nok"]
+    ls = socket.socket()
+    ls.bind(("127.0.0.1", 0))
+    ls.listen(4)
+    port = ls.getsockname()[1]
+
+    def serve():
+        for r in replies:
+            c, _ = ls.accept()
+            c.recv(65536)
+            c.sendall(r)
+            c.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    try:
+        c = nat.HttpClient(f"http://127.0.0.1:{port}")
+        status, headers, body = c.request("GET", "/")
+        assert status == 200 and body == b"ok" and ("X-Folded", "a b") in list(headers)
+        c2 = nat.HttpClient(f"http://127.0.0.1:{port}")
+        with pytest.raises(nat.NativeError, match="malformed MIME header line: bogus"):
+            c2.request("GET", "/")
+    finally:
+        t.join(timeout=10)
+        ls.close()
