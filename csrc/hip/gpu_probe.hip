@@ -221,23 +221,23 @@ int ksa_gpu_health_check_ex(int dev, uint64_t bytes, int reps, ksa_gpu_health* o
     for (int r = 0; r <= reps && ok; ++r) {  // r == 0 is the untimed warm-up
       ok = check(hipMemset(counters, 0, 3 * sizeof(unsigned long long)), "hipMemset");
       if (!ok) break;
-      hipEventRecord(e0, nullptr);
+      if (!(ok = check(hipEventRecord(e0, nullptr), "hipEventRecord"))) break;
       hipLaunchKernelGGL(fill_kernel, dim3(grid), dim3(kBlock), 0, nullptr, buf, n_vec, seed, counters);
       ok = check(hipGetLastError(), "fill_kernel launch");
-      hipEventRecord(e1, nullptr);
+      ok = ok && check(hipEventRecord(e1, nullptr), "hipEventRecord");
       ok = ok && check(hipEventSynchronize(e1), "hipEventSynchronize");
       float ms = 0;
-      hipEventElapsedTime(&ms, e0, e1);
-      if (r > 0 && ms < best_fill) best_fill = ms;
+      ok = ok && check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
       if (!ok) break;
-      hipEventRecord(e0, nullptr);
+      if (r > 0 && ms < best_fill) best_fill = ms;
+      if (!(ok = check(hipEventRecord(e0, nullptr), "hipEventRecord"))) break;
       hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kBlock), 0, nullptr, buf, n_vec, seed, counters + 1,
                          counters + 2);
       ok = check(hipGetLastError(), "verify_kernel launch");
-      hipEventRecord(e1, nullptr);
+      ok = ok && check(hipEventRecord(e1, nullptr), "hipEventRecord");
       ok = ok && check(hipEventSynchronize(e1), "hipEventSynchronize");
-      hipEventElapsedTime(&ms, e0, e1);
-      if (r > 0 && ms < best_verify) best_verify = ms;
+      ok = ok && check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+      if (ok && r > 0 && ms < best_verify) best_verify = ms;
     }
     if (!ok) break;
     unsigned long long host[3] = {0, 0, 0};
@@ -253,10 +253,10 @@ int ksa_gpu_health_check_ex(int dev, uint64_t bytes, int reps, ksa_gpu_health* o
     rc = (host[2] == 0 && host[0] == host[1]) ? 0 : 1;
     if (rc) g_last_error = "device memory verification failed";
   } while (false);
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
-  if (buf) hipFree(buf);
-  if (counters) hipFree(counters);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (buf) (void)hipFree(buf);
+  if (counters) (void)hipFree(counters);
   return rc;
 }
 

@@ -150,27 +150,27 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
     }
     const int grid = static_cast<int>(want < cap ? want : cap);
     const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
-    hipEventRecord(e0, nullptr);
+    if (!ok(hipEventRecord(e0, nullptr), "hipEventRecord")) break;
     hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), lds, nullptr, d_p, m, lat, d_t, d_d, n, init_replicas,
                        horizon_ns, d_o64, d_o32);
     if (!ok(hipGetLastError(), "sweep_kernel launch")) break;
-    hipEventRecord(e1, nullptr);
+    if (!ok(hipEventRecord(e1, nullptr), "hipEventRecord")) break;
     if (!ok(hipEventSynchronize(e1), "hipEventSynchronize")) break;
     float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
+    if (!ok(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime")) break;
     if (kernel_ms) *kernel_ms = ms;
     if (!ok(hipMemcpy(out64, d_o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy") ||
         !ok(hipMemcpy(out32, d_o32, kNumOut32 * m * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
       break;
     rc = 0;
   } while (false);
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
-  hipFree(d_t);
-  hipFree(d_d);
-  hipFree(d_p);
-  hipFree(d_o64);
-  hipFree(d_o32);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(d_t);
+  (void)hipFree(d_d);
+  (void)hipFree(d_p);
+  (void)hipFree(d_o64);
+  (void)hipFree(d_o32);
   return rc;
 }
 
