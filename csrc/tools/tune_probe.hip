@@ -5,6 +5,17 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+
+// A failed HIP call ends the probe with its error (a tuning run must not print made-up numbers).
+#define CHECK(call)                                                                   \
+  do {                                                                                \
+    const hipError_t e_ = (call);                                                     \
+    if (e_ != hipSuccess) {                                                           \
+      std::fprintf(stderr, "%s failed: %s\n", #call, hipGetErrorString(e_));          \
+      std::exit(1);                                                                   \
+    }                                                                                 \
+  } while (0)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -67,20 +78,21 @@ __global__ __launch_bounds__(256) void verify(const u32x4* __restrict__ buf, uin
 template <class K>
 float best_ms(K launch, int reps) {
   hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
   float best = 1e30f;
   for (int r = 0; r <= reps; ++r) {
-    hipEventRecord(a, nullptr);
+    CHECK(hipEventRecord(a, nullptr));
     launch();
-    hipEventRecord(b, nullptr);
-    hipEventSynchronize(b);
+    CHECK(hipGetLastError());
+    CHECK(hipEventRecord(b, nullptr));
+    CHECK(hipEventSynchronize(b));
     float ms;
-    hipEventElapsedTime(&ms, a, b);
+    CHECK(hipEventElapsedTime(&ms, a, b));
     if (r > 0 && ms < best) best = ms;
   }
-  hipEventDestroy(a);
-  hipEventDestroy(b);
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
   return best;
 }
 
@@ -91,21 +103,21 @@ void run(u32x4* buf, uint64_t n, unsigned long long* ctr, int cus, int bpc) {
   float f = best_ms([&] { hipLaunchKernelGGL((fill<U, NT>), dim3(grid), dim3(256), 0, nullptr, buf, n, ctr); }, 5);
   float v = best_ms([&] { hipLaunchKernelGGL((verify<U, NT, SUM>), dim3(grid), dim3(256), 0, nullptr, buf, n, ctr + 1); }, 5);
   unsigned long long h[3];
-  hipMemcpy(h, ctr, sizeof h, hipMemcpyDeviceToHost);
+  CHECK(hipMemcpy(h, ctr, sizeof h, hipMemcpyDeviceToHost));
   std::printf("{\"unroll\":%d,\"nontemporal\":%s,\"checksum\":%s,\"blocks_per_cu\":%d,\"write_GBps\":%.1f,\"read_verify_GBps\":%.1f,\"mismatches\":%llu}\n",
               U, NT ? "true" : "false", SUM ? "true" : "false", bpc, bytes / (f * 1e6), bytes / (v * 1e6), h[1]);
 }
 
 int main() {
   hipDeviceProp_t p;
-  hipGetDeviceProperties(&p, 0);
+  CHECK(hipGetDeviceProperties(&p, 0));
   const uint64_t bytes = 2ull << 30;
   const uint64_t n = bytes / 16;
   u32x4* buf;
   unsigned long long* ctr;
-  hipMalloc(&buf, bytes);
-  hipMalloc(&ctr, 32);
-  hipMemset(ctr, 0, 32);
+  CHECK(hipMalloc(&buf, bytes));
+  CHECK(hipMalloc(&ctr, 32));
+  CHECK(hipMemset(ctr, 0, 32));
   for (int bpc : {2, 4, 8}) {
     run<4, true>(buf, n, ctr, p.multiProcessorCount, bpc);
     run<8, true>(buf, n, ctr, p.multiProcessorCount, bpc);
@@ -113,7 +125,7 @@ int main() {
     run<8, true, true>(buf, n, ctr, p.multiProcessorCount, bpc);
     run<16, true, true>(buf, n, ctr, p.multiProcessorCount, bpc);
   }
-  hipFree(buf);
-  hipFree(ctr);
+  CHECK(hipFree(buf));
+  CHECK(hipFree(ctr));
   return 0;
 }

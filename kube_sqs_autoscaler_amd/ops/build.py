@@ -114,7 +114,8 @@ def build_gpu_probe(verbose: bool = True) -> Path | None:
     hipcc = HIPCC if Path(HIPCC).exists() else "hipcc"
     if _stale(GPU_SO, deps, 0.0):
         tmp = GPU_SO.with_suffix(".tmp.so")
-        _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", *map(str, srcs), "-o", str(tmp)])
+        _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-Wall", "-Werror=unused-value",
+              "-Werror=unused-result", "-shared", "-fPIC", *map(str, srcs), "-o", str(tmp)])
         os.replace(tmp, GPU_SO)
         if verbose:
             print(f"[build] hipcc --offload-arch={GPU_ARCH} -> {GPU_SO.relative_to(ROOT)}")
@@ -141,7 +142,7 @@ def build_tools(verbose: bool = True) -> list[Path]:
     for src in sorted((CSRC / "tools").glob("*.hip")):
         exe = OPS / (src.stem + ".bin")
         if _stale(exe, [src], 0.0):
-            _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-w", str(src), "-o", str(exe)])
+            _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-Wall", "-Werror=unused-value", str(src), "-o", str(exe)])
             if verbose:
                 print(f"[build] hipcc --offload-arch={GPU_ARCH} -> {exe.relative_to(ROOT)}")
         out.append(exe)
