@@ -829,6 +829,7 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<Supervisor, std::shared_ptr<Supervisor>>(m, "Supervisor")
       .def(py::init<>())
       .def("add", &Supervisor::add)
+      .def_property("private_files", &Supervisor::private_files, &Supervisor::set_private_files)
       .def("start", &Supervisor::start, py::arg("max_iterations") = -1)
       .def("stop", &Supervisor::stop)
       .def("stopped", &Supervisor::stopped)

@@ -922,6 +922,7 @@ HttpClient::~HttpClient() {
 void HttpClient::close() {
   std::lock_guard<std::mutex> lk(mu_);
   conn_.reset();
+  in_flight_ = false;  // a pipelined response that was never read goes with the connection
 }
 
 void HttpClient::cancel() {

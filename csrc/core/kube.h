@@ -56,6 +56,8 @@ class DeploymentApi {
   }
   // Shutdown: abort the request in progress and any throttle wait (sticky). Default: nothing.
   virtual void cancel() {}
+  // Closes the keep-alive connection (and drops a pipelined GET in flight); see SqsApi.
+  virtual void close_connections() {}
   // Clock time at which the latest deliberate wait (client-side throttle, Retry-After) ends or
   // ended; 0: none yet. The liveness check counts such a wait as progress.
   virtual Nanos waiting_until() const { return 0; }
@@ -167,6 +169,9 @@ class KubeRestDeployments final : public DeploymentApi {
   Result<ScaleObject> finish_get() override;
   KubeStats stats() const;
   void cancel() override;
+  void close_connections() override {
+    if (http_) http_->close();
+  }
   std::string path_for(const std::string& name) const;
   ScaleMode mode() const { return static_cast<ScaleMode>(mode_.load(std::memory_order_acquire)); }
   Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }

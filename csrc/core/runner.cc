@@ -1,11 +1,14 @@
 #include "runner.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <cmath>
 #include <limits>
@@ -383,14 +386,31 @@ bool read_thread_sched(ThreadSched* out) {
   return true;
 }
 
+Supervisor::Supervisor() {
+  const char* e = std::getenv("KSA_WORKER_FD_TABLE");
+  private_files_ = !(e && std::strcmp(e, "shared") == 0);
+#if defined(__SANITIZE_THREAD__)
+  // ThreadSanitizer keys its file-descriptor sync objects by number, process-wide: the same
+  // number in two tables reads as a race on one descriptor. Its builds keep one table.
+  private_files_ = false;
+#endif
+}
+
 void Supervisor::start(int64_t max_iterations) {
   std::lock_guard<std::mutex> lk(mu_);
   running_ = runners_.size();
+  const bool private_files = private_files_;
   for (auto& r : runners_) {
-    threads_.emplace_back([this, r, max_iterations] {
+    threads_.emplace_back([this, r, max_iterations, private_files] {
       pthread_setname_np(pthread_self(), "ksa-worker");  // top -H / /proc/<pid>/task/*/comm
       pin_current_thread(r->cpus());
+      bool own_table = false;
+      if (private_files) {
+        r->release_connections();  // sockets opened so far belong to the shared table
+        own_table = ::unshare(CLONE_FILES) == 0;
+      }
       r->run(&stop_, max_iterations);
+      if (own_table) r->release_connections();  // this table's sockets, closed on this thread
       ThreadSched ts;
       const bool have = read_thread_sched(&ts);
       std::lock_guard<std::mutex> g(mu_);

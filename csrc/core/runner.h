@@ -143,6 +143,11 @@ class Runner {
     sqs_->cancel();
     scaler_->cancel();
   }
+  // Closes the clients' keep-alive connections (on the calling thread's file table).
+  void release_connections() {
+    sqs_->api()->close_connections();
+    scaler_->api()->close_connections();
+  }
   // The reference's Run(): arm(), then step() until stopped (or max_iterations > 0 reached).
   void run(StopFlag* stop, int64_t max_iterations = -1);
 
@@ -231,7 +236,19 @@ bool read_thread_sched(ThreadSched* out);
 
 class Supervisor {
  public:
+  Supervisor();
   void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
+  // Each worker thread runs on a file table of its own (unshare(CLONE_FILES)), as a process
+  // would. On a table shared by several threads every socket call takes and drops a reference
+  // on the socket's file (an atomic read-modify-write per call, and a busy-polled receive is
+  // many calls); on a private table the kernel skips that, as it does for a single-threaded
+  // process. Measured with a bare TCP echo (csrc/tools/loopback_probe.cc, profiles/README.md):
+  // it closes the gap between N queues as threads and as processes. The worker owns its
+  // clients' connections for the run: they are closed on the shared table before it unshares
+  // and on its own table before it exits, so no socket number outlives the table it belongs
+  // to. Default on; KSA_WORKER_FD_TABLE=shared turns it off.
+  void set_private_files(bool on) { private_files_ = on; }
+  bool private_files() const { return private_files_; }
   // Starts one thread per runner; each arms its timers then loops.
   void start(int64_t max_iterations = -1);
   // Stop request: interrupts poll sleeps and cancels every worker's in-flight API call, so a
@@ -264,6 +281,7 @@ class Supervisor {
   std::condition_variable cv_;
   size_t running_ = 0;
   ThreadSched sched_;
+  bool private_files_ = true;
 };
 
 // JSON line of an iteration record (span trace format).

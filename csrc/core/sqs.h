@@ -42,6 +42,9 @@ class SqsApi {
                                                const std::vector<std::string>& names) = 0;
   // Shutdown: abort the call in progress and any retry back-off (sticky). Default: nothing.
   virtual void cancel() {}
+  // Closes the keep-alive connection(s); the next call dials again. Called by the thread that
+  // owns the client (Supervisor: before and after a worker runs on a private file table).
+  virtual void close_connections() {}
   // Clock time at which the latest deliberate wait (retry back-off, Retry-After) ends or ended;
   // 0: none yet. The liveness check counts such a wait as progress.
   virtual Nanos waiting_until() const { return 0; }
@@ -79,6 +82,9 @@ class HttpSqsApi final : public SqsApi {
                                        const std::vector<std::string>& names) override;
   SqsApiStats stats() const;
   void cancel() override;
+  void close_connections() override {
+    if (http_) http_->close();
+  }
   // Regional endpoint aws-sdk-go would resolve for `region` ("" if region is empty).
   static std::string endpoint_for_region(const std::string& region);
   static std::string signing_region(const std::string& region);

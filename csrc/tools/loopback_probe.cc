@@ -3,7 +3,9 @@
 // does differently for threads of one process (shared mm, files, signal struct) from anything in
 // the autoscaler's own code. Used to attribute the multi-queue latency rise (profiles/README.md).
 //
-//   loopback_probe <threads|procs> <n> <iterations> <cpu-spec>
+//   loopback_probe <threads|threads-unshare|procs> <n> <iterations> <cpu-spec>
+// threads-unshare: each client thread first takes a private file table (unshare(CLONE_FILES)),
+// to test whether the shared fd table is what threads pay for.
 // cpu-spec: "client0:server0,client1:server1,..." (CPU numbers; "-" = unpinned)
 // Prints one JSON line per client: {"client":i,"p50_ns":...,"p90_ns":...}.
 #include <arpa/inet.h>
@@ -69,8 +71,9 @@ void echo_server(int cpu, int port_fd) {
 
 // One client: connect, then `iters` 64-byte request/response round trips with a busy-polled
 // receive (the autoscaler's --busy-poll path); returns sorted RTTs.
-std::vector<int64_t> client(int cpu, int port, int iters) {
+std::vector<int64_t> client(int cpu, int port, int iters, bool unshare_files = false) {
   pin(cpu);
+  if (unshare_files && ::unshare(CLONE_FILES) != 0) return {};
   int s = socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in a{};
   a.sin_family = AF_INET;
@@ -117,7 +120,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s threads|procs n iterations cpu-spec\n", argv[0]);
     return 2;
   }
-  const bool threads = std::strcmp(argv[1], "threads") == 0;
+  const bool unshare_files = std::strcmp(argv[1], "threads-unshare") == 0;
+  const bool threads = std::strcmp(argv[1], "threads") == 0 || unshare_files;
   const int n = std::atoi(argv[2]);
   const int iters = std::atoi(argv[3]);
   std::vector<int> ccpu(static_cast<size_t>(n), -1), scpu(static_cast<size_t>(n), -1);
@@ -156,7 +160,8 @@ int main(int argc, char** argv) {
     std::vector<std::thread> ts;
     for (int i = 0; i < n; ++i)
       ts.emplace_back([&, i] {
-        res[static_cast<size_t>(i)] = client(ccpu[static_cast<size_t>(i)], ports[static_cast<size_t>(i)], iters);
+        res[static_cast<size_t>(i)] =
+            client(ccpu[static_cast<size_t>(i)], ports[static_cast<size_t>(i)], iters, unshare_files);
       });
     for (auto& t : ts) t.join();
     for (int i = 0; i < n; ++i) report(i, res[static_cast<size_t>(i)]);

@@ -1,0 +1,45 @@
+"""Supervisor workers run on a private file table (unshare(CLONE_FILES), csrc/core/runner.h):
+their sockets never appear in, leak into, or get closed through the process' shared table, and
+the clients keep working across runs and from other threads afterwards."""
+import os
+
+from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
+
+
+def _sockets(path="/proc/self/fd"):
+    n = 0
+    for fd in os.listdir(path):
+        try:
+            if os.readlink(f"{path}/{fd}").startswith("socket:"):
+                n += 1
+        except OSError:
+            pass
+    return n
+
+
+def test_worker_sockets_stay_off_the_shared_table(nat):
+    env = BenchEnv(4, "scale", servers="processes")  # endpoints in another process: only client sockets here
+    try:
+        assert nat.Supervisor().private_files
+        before = _sockets()
+        for _ in range(3):  # three runs, three supervisors, reconnecting each time
+            env.run(50)
+            assert _sockets() == before
+        res = env.collect(50, 1.0)
+        assert len(res.samples) > 0 and res.signature_failures == 0
+        # the same clients from this (main) thread: they dial on this table, and work
+        assert env.sqs_apis[0] is not None
+        r = env.runners[0]
+        assert r.sqs.num_messages() in (0, 200)
+        assert _sockets() == before + 1
+    finally:
+        env.close()
+
+
+def test_shared_table_opt_out(nat, monkeypatch):
+    monkeypatch.setenv("KSA_WORKER_FD_TABLE", "shared")
+    assert not nat.Supervisor().private_files
+    monkeypatch.delenv("KSA_WORKER_FD_TABLE")
+    s = nat.Supervisor()
+    s.private_files = False
+    assert not s.private_files
