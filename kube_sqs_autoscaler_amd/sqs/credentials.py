@@ -79,7 +79,12 @@ def urllib_fetch(method: str, url: str, headers: Dict[str, str], body: bytes, ti
         with opener.open(req, timeout=timeout) as r:
             return r.status, r.read()
     except urllib.error.HTTPError as e:
-        return e.code, e.read()
+        # closed here, on the calling thread: it may be a control-loop worker on a file table
+        # of its own (Supervisor), where a socket must not be left for another thread to close
+        try:
+            return e.code, e.read()
+        finally:
+            e.close()
 
 
 def _make(akid: str, secret: str, token: str, expires_ns: int, name: str):
