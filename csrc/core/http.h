@@ -79,7 +79,7 @@ struct HttpClientStats {
 
 // One persistent connection to one origin. Thread-safe (requests are serialised), but each
 // control-loop worker owns its clients, so there is no contention in practice.
-class HttpClient {
+class alignas(kCacheLine) HttpClient {
  public:
   HttpClient(const Url& origin, TlsOptions tls, Nanos timeout);
   ~HttpClient();

@@ -104,7 +104,7 @@ class FileTokenProvider final : public TokenProvider {
 // flowcontrol.NewTokenBucketRateLimiter, whose Accept() reserves a token from a
 // golang.org/x/time/rate limiter and sleeps until it is due. The bucket starts full; a reservation
 // takes its token at once (the count may go negative), so waiters are served in order.
-class TokenBucket {
+class alignas(kCacheLine) TokenBucket {
  public:
   TokenBucket(double qps, int burst, std::shared_ptr<Clock> clock);
   // Reserves one token; returns how long the caller must wait before using it.
@@ -160,7 +160,7 @@ struct KubeStats {
   HttpClientStats http;
 };
 
-class KubeRestDeployments final : public DeploymentApi {
+class alignas(kCacheLine) KubeRestDeployments final : public DeploymentApi {
  public:
   explicit KubeRestDeployments(KubeOptions opts);
   Result<ScaleObject> get(const std::string& name) override;
@@ -283,7 +283,7 @@ struct ScaleSpan {
   int gets = 0;                // synchronous GETs this call sent (the pipelined one not counted)
 };
 
-class PodAutoScaler {
+class alignas(kCacheLine) PodAutoScaler {
  public:
   PodAutoScaler(std::shared_ptr<DeploymentApi> api, std::string deployment, std::string ns,
                 int64_t max, int64_t min, int64_t scale_up_pods, int64_t scale_down_pods,

@@ -126,7 +126,7 @@ static_assert(std::atomic<int64_t>::is_always_lock_free, "shared-memory atomics 
 // Zero-initialises a SharedWorkerState in place (memory from a fresh shared mapping).
 SharedWorkerState* init_shared_worker_state(void* at);
 
-class Runner {
+class alignas(kCacheLine) Runner {
  public:
   Runner(LoopConfig cfg, std::shared_ptr<SqsClient> sqs, std::shared_ptr<PodAutoScaler> scaler,
          std::shared_ptr<Clock> clock, std::shared_ptr<Logger> log);

@@ -82,7 +82,7 @@ class StaticCredentialsProvider final : public CredentialsProvider {
 
 // aws.Credentials-style cache: retrieve() again only when the cached value is within
 // `expiry_window_ns` of its expiry (or was invalidated after a 403).
-class CachedCredentials {
+class alignas(kCacheLine) CachedCredentials {
  public:
   CachedCredentials(std::shared_ptr<CredentialsProvider> p, int64_t expiry_window_ns)
       : provider_(std::move(p)), window_(expiry_window_ns) {}

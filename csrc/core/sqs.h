@@ -74,7 +74,7 @@ struct SqsApiStats {
   HttpClientStats http;
 };
 
-class HttpSqsApi final : public SqsApi {
+class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
  public:
   HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider> creds,
              std::shared_ptr<Clock> clock);
@@ -159,7 +159,7 @@ class TraceSqsApi final : public SqsApi {
   Nanos latency_;
 };
 
-class SqsClient {
+class alignas(kCacheLine) SqsClient {
  public:
   SqsClient(std::shared_ptr<SqsApi> api, std::string queue_url,
             std::vector<std::string> attribute_names);

@@ -6,11 +6,18 @@
 // log lines ("Failed scaling up: Failed to scale up: <cause>") match byte for byte.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 #include <string>
 #include <utility>
 
 namespace ksa {
+
+// Cache-line size for the objects each worker writes on every poll (Runner, its clients and
+// their connections). They are built one queue after another on one thread, so without the
+// alignment the end of one queue's object and the start of the next share a line, and two
+// workers on different cores write it every poll.
+constexpr std::size_t kCacheLine = 64;
 
 class Status {
  public:
