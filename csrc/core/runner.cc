@@ -388,7 +388,7 @@ bool read_thread_sched(ThreadSched* out) {
 
 Supervisor::Supervisor() {
   const char* e = std::getenv("KSA_WORKER_FD_TABLE");
-  private_files_ = !(e && std::strcmp(e, "shared") == 0);
+  private_files_ = e && std::strcmp(e, "private") == 0;
 #if defined(__SANITIZE_THREAD__)
   // ThreadSanitizer keys its file-descriptor sync objects by number, process-wide: the same
   // number in two tables reads as a race on one descriptor. Its builds keep one table.

@@ -238,15 +238,16 @@ class Supervisor {
  public:
   Supervisor();
   void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
-  // Each worker thread runs on a file table of its own (unshare(CLONE_FILES)), as a process
-  // would. On a table shared by several threads every socket call takes and drops a reference
-  // on the socket's file (an atomic read-modify-write per call, and a busy-polled receive is
-  // many calls); on a private table the kernel skips that, as it does for a single-threaded
-  // process. Measured with a bare TCP echo (csrc/tools/loopback_probe.cc, profiles/README.md):
-  // it closes the gap between N queues as threads and as processes. The worker owns its
-  // clients' connections for the run: they are closed on the shared table before it unshares
-  // and on its own table before it exits, so no socket number outlives the table it belongs
-  // to. Default on; KSA_WORKER_FD_TABLE=shared turns it off.
+  // Opt-in (KSA_WORKER_FD_TABLE=private): each worker thread runs on a file table of its own
+  // (unshare(CLONE_FILES)), as a process would. On a table shared by several threads every
+  // socket call takes and drops a reference on the socket's file (an atomic read-modify-write
+  // per call, and a busy-polled receive is many calls); on a private table the kernel skips
+  // that, as for a single-threaded process. A bare TCP echo (csrc/tools/loopback_probe.cc)
+  // loses its thread penalty this way; the autoscaler's 8-queue thread fleet gains 3-6 %
+  // (profiles/README.md, r02j), which --worker-processes beats, so it stays off by default:
+  // it makes every descriptor a worker opens invisible to the other threads. The worker owns
+  // its clients' connections for the run: they are closed on the shared table before it
+  // unshares and on its own table before it exits, so no socket number outlives its table.
   void set_private_files(bool on) { private_files_ = on; }
   bool private_files() const { return private_files_; }
   // Starts one thread per runner; each arms its timers then loops.
@@ -281,7 +282,7 @@ class Supervisor {
   std::condition_variable cv_;
   size_t running_ = 0;
   ThreadSched sched_;
-  bool private_files_ = true;
+  bool private_files_ = false;
 };
 
 // JSON line of an iteration record (span trace format).

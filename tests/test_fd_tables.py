@@ -1,6 +1,7 @@
-"""Supervisor workers run on a private file table (unshare(CLONE_FILES), csrc/core/runner.h):
-their sockets never appear in, leak into, or get closed through the process' shared table, and
-the clients keep working across runs and from other threads afterwards."""
+"""Opt-in private file tables for Supervisor workers (KSA_WORKER_FD_TABLE=private,
+unshare(CLONE_FILES), csrc/core/runner.h): their sockets never appear in, leak into, or get
+closed through the process' shared table, and the clients keep working across runs and from
+other threads afterwards."""
 import os
 
 from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
@@ -17,7 +18,8 @@ def _sockets(path="/proc/self/fd"):
     return n
 
 
-def test_worker_sockets_stay_off_the_shared_table(nat):
+def test_worker_sockets_stay_off_the_shared_table(nat, monkeypatch):
+    monkeypatch.setenv("KSA_WORKER_FD_TABLE", "private")  # read by every Supervisor env.run() builds
     env = BenchEnv(4, "scale", servers="processes")  # endpoints in another process: only client sockets here
     try:
         assert nat.Supervisor().private_files
@@ -36,10 +38,11 @@ def test_worker_sockets_stay_off_the_shared_table(nat):
         env.close()
 
 
-def test_shared_table_opt_out(nat, monkeypatch):
+def test_private_tables_are_opt_in(nat, monkeypatch):
+    monkeypatch.delenv("KSA_WORKER_FD_TABLE", raising=False)
+    assert not nat.Supervisor().private_files
     monkeypatch.setenv("KSA_WORKER_FD_TABLE", "shared")
     assert not nat.Supervisor().private_files
-    monkeypatch.delenv("KSA_WORKER_FD_TABLE")
     s = nat.Supervisor()
-    s.private_files = False
-    assert not s.private_files
+    s.private_files = True
+    assert s.private_files
