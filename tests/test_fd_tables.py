@@ -46,3 +46,44 @@ def test_private_tables_are_opt_in(nat, monkeypatch):
     s = nat.Supervisor()
     s.private_files = True
     assert s.private_files
+
+
+def test_private_tables_under_dropped_connections(nat):
+    """Workers on private tables reconnect on their own table when the servers drop every
+    connection mid-run; no socket is left behind and the replicas stay in bounds."""
+    import threading
+    import time
+
+    env = BenchEnv(4, "scale", servers="per-queue")  # in-process fakes: they can drop connections
+    try:
+        time.sleep(0.1)
+        before = _sockets()
+        sup = nat.Supervisor()
+        sup.private_files = True
+        for r in env.runners:
+            sup.add(r)
+        stop = threading.Event()
+
+        def chaos():
+            while not stop.is_set():
+                for s in env.sqs_servers + env.kube_servers:
+                    s.drop_connections()
+                time.sleep(0.005)
+
+        t = threading.Thread(target=chaos)
+        t.start()
+        try:
+            sup.start(400)
+            sup.join()
+        finally:
+            stop.set()
+            t.join()
+        assert sum(r.stats()["polls"] for r in env.runners) == 4 * 400
+        deadline = time.time() + 5  # the servers close their side once they see the clients' EOF
+        while _sockets() > before and time.time() < deadline:
+            time.sleep(0.05)
+        assert _sockets() <= before
+        res = env.collect(400, 1.0)
+        assert all(1 <= x <= 8 for x in res.final_replicas)
+    finally:
+        env.close()
