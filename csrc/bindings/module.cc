@@ -770,6 +770,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["last_depth"] = s.last_depth;
         d["last_replicas"] = s.last_replicas;
         d["latency_samples"] = s.latency_samples;
+        d["latency_sum_ns"] = s.latency_sum_ns;
+        d["latency_buckets"] = std::vector<uint64_t>(s.latency_buckets, s.latency_buckets + kLatBuckets);
         return d;
       })
       .def("idle_ns", &Runner::idle_ns)
@@ -785,6 +787,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_property_readonly("scaler", &Runner::scaler)
       .def_property_readonly("last_scale_up", &Runner::last_scale_up)
       .def_property_readonly("last_scale_down", &Runner::last_scale_down);
+
+  m.attr("latency_bucket_le_ns") = std::vector<int64_t>(kLatBucketLeNs, kLatBucketLeNs + kLatBuckets - 1);
 
   // ---- process-per-queue fleet: worker state in shared memory (procfleet.py) ----
   auto ws = [](uintptr_t addr) { return reinterpret_cast<SharedWorkerState*>(addr); };
@@ -804,6 +808,9 @@ PYBIND11_MODULE(_ksa_native, m) {
     d["last_depth"] = s->last_depth.load(std::memory_order_relaxed);
     d["last_replicas"] = s->last_replicas.load(std::memory_order_relaxed);
     d["latency_sum_ns"] = s->lat_sum_ns.load(std::memory_order_relaxed);
+    std::vector<uint64_t> hist(kLatBuckets);
+    for (int i = 0; i < kLatBuckets; ++i) hist[i] = s->lat_hist[i].load(std::memory_order_relaxed);
+    d["latency_buckets"] = hist;
     d["status"] = s->status.load(std::memory_order_acquire);
     d["control"] = s->control.load(std::memory_order_acquire);
     d["max_override"] = s->max_override.load(std::memory_order_relaxed);

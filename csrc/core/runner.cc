@@ -224,6 +224,8 @@ void Runner::record(const IterationRecord& r) {
     if (r.replicas_after >= 0) stats_.last_replicas = r.replicas_after;
     if (r.patch_latency_ns >= 0) {
       stats_.latency_samples++;
+      stats_.latency_sum_ns += r.patch_latency_ns;
+      stats_.latency_buckets[latency_bucket(r.patch_latency_ns)]++;
       if (lat_ring_.size() < kLatRing) {
         lat_ring_.push_back(r.patch_latency_ns);
       } else {
@@ -248,6 +250,7 @@ SharedWorkerState* init_shared_worker_state(void* at) {
   s->max_override.store(0, std::memory_order_relaxed);
   s->iterations.store(-1, std::memory_order_relaxed);
   s->control.store(SharedWorkerState::kWait, std::memory_order_relaxed);
+  for (auto& v : s->lat_hist) v.store(0, std::memory_order_relaxed);
   for (auto& v : s->lat_ring) v.store(0, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   return s;
@@ -280,7 +283,9 @@ void Runner::mirror(const IterationRecord& r) {
   if (r.patch_latency_ns >= 0) {
     const uint64_t n = st.latency_samples;  // this sample is number n (1-based)
     shared_->lat_ring[(n - 1) % SharedWorkerState::kRing].store(r.patch_latency_ns, std::memory_order_relaxed);
-    shared_->lat_sum_ns.fetch_add(r.patch_latency_ns, std::memory_order_relaxed);
+    shared_->lat_sum_ns.store(st.latency_sum_ns, std::memory_order_relaxed);
+    const int b = latency_bucket(r.patch_latency_ns);
+    shared_->lat_hist[b].store(st.latency_buckets[b], std::memory_order_relaxed);
   }
   // the count last, with release: a reader that sees it sees the ring entries before it
   shared_->counters[W::kLatencySamples].store(st.latency_samples, std::memory_order_release);

@@ -76,6 +76,20 @@ struct IterationRecord {
   std::string error;
 };
 
+// Poll->patch latency histogram: bucket i counts samples <= kLatBucketLeNs[i] (and above the
+// previous bound); the last bucket is everything above 10 s. Prometheus-style bounds from 10 µs
+// (a localhost poll) to 10 s (a throttled apiserver).
+constexpr int kLatBuckets = 20;
+constexpr int64_t kLatBucketLeNs[kLatBuckets - 1] = {
+    10000,     25000,     50000,      100000,     250000,     500000,     1000000,
+    2500000,   5000000,   10000000,   25000000,   50000000,   100000000,  250000000,
+    500000000, 1000000000, 2500000000, 5000000000, 10000000000};
+inline int latency_bucket(int64_t ns) {
+  int i = 0;
+  while (i < kLatBuckets - 1 && ns > kLatBucketLeNs[i]) ++i;
+  return i;
+}
+
 struct RunnerStats {
   uint64_t polls = 0;
   uint64_t depth_errors = 0;
@@ -94,6 +108,8 @@ struct RunnerStats {
   int64_t last_depth = 0;
   int32_t last_replicas = -1;
   uint64_t latency_samples = 0;
+  int64_t latency_sum_ns = 0;                 // over every sample (the ring keeps the latest)
+  uint64_t latency_buckets[kLatBuckets] = {};  // per bucket, not cumulative
 };
 
 // A worker's state mirrored into memory shared with a supervising process (the process-per-queue
@@ -120,6 +136,7 @@ struct SharedWorkerState {
   alignas(64) std::atomic<int64_t> max_override;  // parent -> worker: > 0 caps max-pods
   std::atomic<int64_t> iterations;                // parent -> worker: polls to run (<= 0: until stopped)
   std::atomic<int32_t> control;                   // parent -> worker
+  alignas(64) std::atomic<uint64_t> lat_hist[kLatBuckets];  // per bucket (RunnerStats::latency_buckets)
   alignas(64) std::atomic<int64_t> lat_ring[kRing];
 };
 static_assert(std::atomic<int64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");

@@ -14,8 +14,9 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Optional, Sequence, Tuple
 
 from prometheus_client import CollectorRegistry, generate_latest
-from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, SummaryMetricFamily
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily, SummaryMetricFamily
 
+from .ops import native
 from .parallel.fleet import Fleet
 
 _COUNTERS = [
@@ -75,7 +76,10 @@ class FleetCollector:
         fams = {k: CounterMetricFamily(f"ksa_{k}", h, labels=labels) for k, h in _COUNTERS}
         depth = GaugeMetricFamily("ksa_queue_depth", "Last observed queue depth (sum of attributes)", labels=labels)
         reps = GaugeMetricFamily("ksa_replicas", "Last observed Deployment replicas", labels=labels)
-        lat = SummaryMetricFamily("ksa_poll_to_patch_seconds", "Poll end -> replica write latency", labels=labels)
+        lat = SummaryMetricFamily("ksa_poll_to_patch_seconds", "Poll start -> replica write acknowledged", labels=labels)
+        hist = HistogramMetricFamily("ksa_poll_to_patch_latency_seconds",
+                                     "Poll start -> replica write acknowledged, per scaling poll", labels=labels)
+        bounds = [b / 1e9 for b in native().latency_bucket_le_ns]
         api = {k: CounterMetricFamily(f"ksa_{k}", h, labels=labels) for k, h, _, _ in _API_COUNTERS}
         for w, s in zip(self.fleet.workers, stats):
             lv = [s["deployment"], s["queue"]]
@@ -88,13 +92,19 @@ class FleetCollector:
                     api[k].add_metric(lv, v / 1e9 if key in _NS_COUNTERS else v)
             depth.add_metric(lv, s["last_depth"])
             reps.add_metric(lv, s["last_replicas"])
-            samples = w.runner.latencies()
-            lat.add_metric(lv, count_value=s["latency_samples"], sum_value=sum(samples) / 1e9)
+            # every sample since start (the latency ring only keeps the latest)
+            lat.add_metric(lv, count_value=s["latency_samples"], sum_value=s["latency_sum_ns"] / 1e9)
+            cum, buckets = 0, []
+            for le, n in zip(bounds + [float("inf")], s["latency_buckets"]):
+                cum += n
+                buckets.append(("+Inf" if le == float("inf") else repr(le), cum))
+            hist.add_metric(lv, buckets, sum_value=s["latency_sum_ns"] / 1e9)
         yield from fams.values()
         yield from (f for f in api.values() if f.samples)
         yield depth
         yield reps
         yield lat
+        yield hist
 
 
 class Health:

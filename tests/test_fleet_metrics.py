@@ -77,6 +77,15 @@ def test_metrics_endpoints(nat):
             assert metric["ksa_apiserver_gets_total"] == 10 and metric["ksa_apiserver_conflicts_total"] == 0
             assert metric["ksa_apiserver_throttled_total"] == 0 and metric["ksa_apiserver_throttle_seconds_total"] == 0
             assert metric["ksa_sqs_throttle_retries_total"] == 0 and metric["ksa_speculative_reads_skipped_total"] == 0
+            # latency histogram: cumulative buckets ending at +Inf == count, same sum as the summary
+            buckets = [(line.split('le="')[1].split('"')[0], float(line.rsplit(" ", 1)[1]))
+                       for line in body.splitlines()
+                       if line.startswith("ksa_poll_to_patch_latency_seconds_bucket")
+                       and 'deployment="bench/gpu-worker-0"' in line]
+            assert len(buckets) == 20 and buckets[-1] == ("+Inf", 10.0)
+            assert all(a[1] <= b[1] for a, b in zip(buckets, buckets[1:]))
+            assert metric["ksa_poll_to_patch_latency_seconds_count"] == 10
+            assert metric["ksa_poll_to_patch_latency_seconds_sum"] == metric["ksa_poll_to_patch_seconds_sum"] > 0
             assert urllib.request.urlopen(base + "/readyz").read() == b"ok"
             assert urllib.request.urlopen(base + "/healthz").status == 200
         finally:
@@ -218,5 +227,21 @@ def test_stop_cancels_in_flight_calls(nat, pooled):
         fleet.join()
         assert time.perf_counter() - t0 < 2.0
         assert all(s["depth_errors"] >= 1 for s in fleet.stats()[: 1 if pooled else 2])
+    finally:
+        env.close()
+
+
+def test_latency_sum_and_buckets_cover_every_sample(nat):
+    """The summary's sum and the histogram count every sample since start, not only the ones
+    the latency ring still holds (the ring keeps the latest 65536)."""
+    env = BenchEnv(1)
+    try:
+        env.run(50)
+        env.clear()  # empties the ring; the cumulative sum and buckets stay
+        env.run(50)
+        st = env.runners[0].stats()
+        assert st["latency_samples"] == 100 == sum(st["latency_buckets"])
+        assert st["latency_sum_ns"] > sum(env.runners[0].latencies()) > 0
+        assert len(nat.latency_bucket_le_ns) == len(st["latency_buckets"]) - 1
     finally:
         env.close()

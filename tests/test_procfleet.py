@@ -154,6 +154,7 @@ def test_metrics_and_health_over_worker_processes(nat, servers):
         assert 'ksa_scale_ups_total{deployment="gpu/w0"' in text
         assert 'ksa_replicas{deployment="gpu/w0",queue="' in text and "} 7.0" in text
         assert 'ksa_poll_to_patch_seconds_count{deployment="gpu/w0"' in text
+        assert 'ksa_poll_to_patch_latency_seconds_bucket{deployment="gpu/w0",le="+Inf"' in text
     finally:
         fleet.stop()
         fleet.join()
