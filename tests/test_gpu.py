@@ -110,9 +110,11 @@ def test_cli_gpu_aware_max_local_with_worker_processes(tmp_path):
                              cwd=root, env=env, stderr=subprocess.PIPE, text=True)
         want = min(64, n_gpus)
         deadline = time.time() + 90
-        while time.time() < deadline and p.poll() is None and \
-                [kube.replicas("ml", f"w{i}") for i in range(2)] != [want, want]:
+        # both workers polling (the CLI imports and forks first), each far past the cap's reach
+        while time.time() < deadline and p.poll() is None and sqs.requests() < 100:
             time.sleep(0.05)
+        assert sqs.requests() >= 100, "the workers did not start polling"
+        assert [kube.replicas("ml", f"w{i}") for i in range(2)] == [want, want]
         polled = sqs.requests()
         time.sleep(0.3)  # more polls: the cap holds
         assert sqs.requests() >= polled + 20
