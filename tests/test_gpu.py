@@ -104,10 +104,13 @@ def test_cli_gpu_aware_max_local_with_worker_processes(tmp_path):
             "users": [{"name": "u", "user": {"token": "x"}}], "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
         env = dict(os.environ, AWS_ACCESS_KEY_ID="a", AWS_SECRET_ACCESS_KEY="b", KUBE_CONFIG_PATH=str(kc))
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        err_path = tmp_path / "stderr.log"  # a file, not a pipe: nobody drains a pipe while it runs
+        err = open(err_path, "w")
         p = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", "--aws-region=us-east-1",
                               f"--sqs-endpoint={sqs.url}", "--poll-period=5ms", "--scale-up-cool-down=0s", "--max-pods=64",
                               "--gpu-aware-max=local", "--kube-api-qps=0", "--worker-processes", *specs],
-                             cwd=root, env=env, stderr=subprocess.PIPE, text=True)
+                             cwd=root, env=env, stderr=err, text=True)
+        err.close()
         want = min(64, n_gpus)
         deadline = time.time() + 90
         # both workers polling (the CLI imports and forks first), each far past the cap's reach
@@ -121,7 +124,7 @@ def test_cli_gpu_aware_max_local_with_worker_processes(tmp_path):
         assert [kube.replicas("ml", f"w{i}") for i in range(2)] == [want, want]
         p.send_signal(signal.SIGTERM)
         assert p.wait(timeout=30) == 0
-        assert f"GPU capacity: {n_gpus} pods" in p.stderr.read()
+        assert f"GPU capacity: {n_gpus} pods" in err_path.read_text()
     finally:
         if p is not None and p.poll() is None:
             p.kill()

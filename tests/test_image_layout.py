@@ -57,17 +57,20 @@ def test_slim_image_layout_scales_with_only_its_runtime_packages(nat, image_root
            "AWS_ACCESS_KEY_ID": AKID, "AWS_SECRET_ACCESS_KEY": SECRET, "KUBE_CONFIG_PATH": str(kc),
            "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
     # -S: no site-packages, so only the image's packages (PYTHONPATH) can be imported
-    p = subprocess.Popen([sys.executable, "-S", str(launcher), f"--sqs-queue-url={url}", "--kubernetes-deployment=workers",
-                          "--kubernetes-namespace=gpu", f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}",
-                          "--poll-period=1ms", "--scale-up-cool-down=0s", "--scale-down-cool-down=0s"],
-                         cwd=str(tmp), env=env, stderr=subprocess.PIPE, text=True)
+    err_path = tmp / "stderr.log"  # a file, not a pipe: nobody drains a pipe while it runs
+    with open(err_path, "w") as err_file:
+        p = subprocess.Popen([sys.executable, "-S", str(launcher), f"--sqs-queue-url={url}",
+                              "--kubernetes-deployment=workers", "--kubernetes-namespace=gpu", f"--aws-region={REGION}",
+                              f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
+                              "--scale-down-cool-down=0s"],
+                             cwd=str(tmp), env=env, stderr=err_file, text=True)
     try:
         deadline = time.time() + 60
         while kube.replicas("gpu", "workers") < 8 and p.poll() is None and time.time() < deadline:
             time.sleep(0.01)
         p.send_signal(signal.SIGTERM)
         rc = p.wait(timeout=30)
-        err = p.stderr.read()
+        err = err_path.read_text()
         assert rc == 0, err[-2000:]
         assert kube.replicas("gpu", "workers") == 8
         assert 'msg="Starting kube-sqs-autoscaler"' in err and 'msg="Found 500 messages in the queue"' in err
