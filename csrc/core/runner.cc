@@ -401,25 +401,108 @@ Supervisor::Supervisor() {
 #endif
 }
 
+HomeThread::HomeThread() {
+  thread_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "ksa-worker");  // top -H / /proc/<pid>/task/*/comm
+    cpu_set_t set;
+    if (pthread_getaffinity_np(pthread_self(), sizeof set, &set) == 0) {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &set)) start_mask_.push_back(c);
+    }
+    loop();
+  });
+}
+
+void HomeThread::loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] { return quit_ || task_ != nullptr; });
+    if (!task_) return;  // quit with nothing left to run
+    std::function<void()> task = std::move(task_);
+    task_ = nullptr;
+    lk.unlock();
+    task();
+    task = nullptr;  // the task's captures go before the thread reports idle
+    lk.lock();
+    busy_ = false;
+    cv_.notify_all();
+  }
+}
+
+void HomeThread::post(std::function<void()> task) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return !busy_; });
+  task_ = std::move(task);
+  busy_ = true;
+  cv_.notify_all();
+}
+
+void HomeThread::wait_idle() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return !busy_; });
+}
+
+void HomeThread::unpin() {
+  CpuList mask;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    mask = start_mask_;
+  }
+  pin_current_thread(mask);
+}
+
+HomeThread::~HomeThread() {
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return !busy_; });
+    quit_ = true;
+  }
+  cv_.notify_all();
+  if (thread_.get_id() == std::this_thread::get_id()) thread_.detach();  // never from its own task
+  else if (thread_.joinable()) thread_.join();
+}
+
+HomeThread* Runner::home_thread(bool private_files) {
+  if (home_ && home_->private_files && !private_files) home_.reset();  // cannot rejoin the shared table
+  if (!home_) home_ = std::make_unique<HomeThread>();
+  return home_.get();
+}
+
 void Supervisor::start(int64_t max_iterations) {
-  std::lock_guard<std::mutex> lk(mu_);
-  running_ = runners_.size();
-  const bool private_files = private_files_;
+  bool private_files;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    running_ += runners_.size();
+    private_files = private_files_;
+  }
+  // Posting waits for a task a runner's thread still runs, and that task's last step takes
+  // mu_: so no lock is held from here on.
   for (auto& r : runners_) {
-    threads_.emplace_back([this, r, max_iterations, private_files] {
-      pthread_setname_np(pthread_self(), "ksa-worker");  // top -H / /proc/<pid>/task/*/comm
-      pin_current_thread(r->cpus());
-      bool own_table = false;
-      if (private_files) {
-        r->release_connections();  // sockets opened so far belong to the shared table
-        own_table = ::unshare(CLONE_FILES) == 0;
+    Runner* rp = r.get();  // runners_ keeps it alive until join()
+    HomeThread* h = rp->home_thread(private_files);
+    // Between runs a runner's connections live on the shared table: a worker on a table of its
+    // own closes its sockets before its run ends, and the caller may have dialled since. Those
+    // are closed here, on a thread of the shared table, before a private worker runs.
+    if (private_files && h->private_files) rp->release_connections();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      started_.push_back(h);
+    }
+    h->post([this, rp, h, max_iterations, private_files] {
+      if (rp->cpus().empty()) h->unpin();
+      else pin_current_thread(rp->cpus());
+      if (private_files && !h->private_files) {
+        rp->release_connections();  // sockets opened so far belong to the shared table
+        h->private_files = ::unshare(CLONE_FILES) == 0;
       }
-      r->run(&stop_, max_iterations);
-      if (own_table) r->release_connections();  // this table's sockets, closed on this thread
-      ThreadSched ts;
-      const bool have = read_thread_sched(&ts);
+      ThreadSched before, after;
+      const bool have = read_thread_sched(&before);
+      rp->run(&stop_, max_iterations);
+      if (h->private_files) rp->release_connections();  // this table's sockets, closed on this thread
+      const bool have_after = have && read_thread_sched(&after);
       std::lock_guard<std::mutex> g(mu_);
-      if (have) sched_.add(ts);
+      if (have_after) sched_.add(after.since(before));
       --running_;
       cv_.notify_all();
     });
@@ -436,9 +519,12 @@ bool Supervisor::wait(Nanos timeout) {
 }
 
 void Supervisor::join() {
-  for (auto& t : threads_)
-    if (t.joinable()) t.join();
-  threads_.clear();
+  std::vector<HomeThread*> started;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    started.swap(started_);
+  }
+  for (HomeThread* h : started) h->wait_idle();
 }
 
 Supervisor::~Supervisor() {

@@ -143,6 +143,40 @@ static_assert(std::atomic<int64_t>::is_always_lock_free, "shared-memory atomics 
 // Zero-initialises a SharedWorkerState in place (memory from a fresh shared mapping).
 SharedWorkerState* init_shared_worker_state(void* at);
 
+// The OS thread a Runner's loop runs on, kept for the Runner's lifetime across Supervisor runs
+// (named ksa-worker). glibc gives every thread a malloc arena of its own and hands the arena of
+// an exited thread to the next thread created. When a fleet's threads are replaced -- a
+// warm-up run, a leadership hand-over -- queue i's new thread inherits the arena in which
+// queue j's old thread allocated j's lazily-built buffers, and i's per-poll temporaries land on
+// the cache lines of buffers j's thread writes every poll. Measured on the 8-queue thread fleet
+// (profiles/README.md, r02l): the same instructions per poll, +70 % user cycles and ~80 more
+// cache misses per poll, +30 % p50; with the threads kept, the fleet polls like one queue.
+class HomeThread {
+ public:
+  HomeThread();
+  ~HomeThread();  // lets the task in progress finish, then ends the thread
+  HomeThread(const HomeThread&) = delete;
+  HomeThread& operator=(const HomeThread&) = delete;
+  // Runs `task` on the thread (after the previous task, if one is still running).
+  void post(std::function<void()> task);
+  void wait_idle();
+  // Whether the thread has taken a file table of its own (unshare(CLONE_FILES)); set by the
+  // task that did it. Such a thread is never handed to a run that wants the shared table.
+  bool private_files = false;
+  // Restores the CPU mask the thread started with (a run without explicit CPUs after a pinned one).
+  void unpin();
+
+ private:
+  void loop();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::function<void()> task_;
+  bool busy_ = false;
+  bool quit_ = false;
+  CpuList start_mask_;
+  std::thread thread_;
+};
+
 class alignas(kCacheLine) Runner {
  public:
   Runner(LoopConfig cfg, std::shared_ptr<SqsClient> sqs, std::shared_ptr<PodAutoScaler> scaler,
@@ -192,6 +226,10 @@ class alignas(kCacheLine) Runner {
   // Mirror the stats into `s` after every poll and follow its max-pods override (may be null).
   void set_shared_state(SharedWorkerState* s) { shared_ = s; }
   const CpuList& cpus() const { return cpus_; }
+  // This runner's HomeThread (created on first use). A thread that unshared its file table is
+  // retired when a run wants the shared one (`private_files` false), and vice versa the new
+  // thread unshares on its first private run.
+  HomeThread* home_thread(bool private_files);
 
  private:
   IterationRecord poll_body();
@@ -222,6 +260,7 @@ class alignas(kCacheLine) Runner {
   std::vector<Nanos> lat_ring_;
   size_t lat_pos_ = 0;
   static constexpr size_t kLatRing = 1 << 16;
+  std::unique_ptr<HomeThread> home_;  // last: ends (after its task) before the state it runs on
 };
 
 // Scheduler accounting of one thread (/proc/thread-self/schedstat and status): time on CPU, time
@@ -247,6 +286,19 @@ struct ThreadSched {
     vol_cs += o.vol_cs;
     invol_cs += o.invol_cs;
   }
+  // What the same thread accumulated since `o` was read (a HomeThread serves many runs).
+  ThreadSched since(const ThreadSched& o) const {
+    ThreadSched d = *this;
+    d.utime_ns -= o.utime_ns;
+    d.stime_ns -= o.stime_ns;
+    d.minflt -= o.minflt;
+    d.cpu_ns -= o.cpu_ns;
+    d.runq_wait_ns -= o.runq_wait_ns;
+    d.slices -= o.slices;
+    d.vol_cs -= o.vol_cs;
+    d.invol_cs -= o.invol_cs;
+    return d;
+  }
 };
 // The calling thread's counters (false when /proc is unavailable).
 bool read_thread_sched(ThreadSched* out);
@@ -267,7 +319,8 @@ class Supervisor {
   // unshares and on its own table before it exits, so no socket number outlives its table.
   void set_private_files(bool on) { private_files_ = on; }
   bool private_files() const { return private_files_; }
-  // Starts one thread per runner; each arms its timers then loops.
+  // Runs every runner on its HomeThread (one thread per runner, kept across runs); each arms
+  // its timers then loops.
   void start(int64_t max_iterations = -1);
   // Stop request: interrupts poll sleeps and cancels every worker's in-flight API call, so a
   // SIGTERM does not wait for a slow or hung endpoint (the call's own timeout can be 30 s).
@@ -293,7 +346,7 @@ class Supervisor {
 
  private:
   std::vector<std::shared_ptr<Runner>> runners_;
-  std::vector<std::thread> threads_;
+  std::vector<HomeThread*> started_;  // the runners' threads this supervisor posted to
   StopFlag stop_;
   mutable std::mutex mu_;
   std::condition_variable cv_;

@@ -249,9 +249,13 @@ class BenchEnv:
         self.kube_apis, self.sqs_apis = [], []
         self.targets = []
         self.server_of = []  # queue -> index of the server pair that serves it
-        for q in range(queues):
+        built = [None] * queues
+
+        def build(q):
             si = q % n_servers
             sqs, kube, log = self.sqs_servers[si], self.kube_servers[si], self.loggers[q % len(self.loggers)]
+            # probe: KSA_BENCH_CLOCK=per-queue gives each queue a clock object of its own
+            clock = nat.RealClock() if os.environ.get("KSA_BENCH_CLOCK") == "per-queue" else self.clock
             rest = RestConfig(host=kube.url, bearer_token=TOKEN, insecure=tls)
             sqs_tls = None
             if tls:
@@ -261,17 +265,14 @@ class BenchEnv:
                 rest.ca_pem = kube.cert_pem
             url = queue_url(sqs.url, q)
             name = deployment_name(q)
-            self.server_of.append(si)
             t = TargetConfig(queue_url=url, deployment=name, namespace="bench", poll_period_ns=0,
                              scale_up_cool_down_ns=0, scale_down_cool_down_ns=0, scale_up_messages=100,
                              scale_down_messages=10, max_pods=8, min_pods=1)
-            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=busy_poll_ns)
-            scaler = new_pod_autoscaler(t, kube_api, log, self.clock)
-            sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds, tls=sqs_tls,
+            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, clock, busy_poll_ns=busy_poll_ns)
+            scaler = new_pod_autoscaler(t, kube_api, log, clock)
+            sqs_api = new_sqs_api(REGION, clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds, tls=sqs_tls,
                                   busy_poll_ns=busy_poll_ns)
             client = new_sqs_client(t, sqs_api)
-            self.kube_apis.append(kube_api)
-            self.sqs_apis.append(sqs_api)
             cfg = nat.LoopConfig()
             cfg.poll_period_ns = 0
             cfg.scale_up_cool_down_ns = 0
@@ -279,9 +280,34 @@ class BenchEnv:
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
-            runner = nat.Runner(cfg, client, scaler, self.clock, log)
+            runner = nat.Runner(cfg, client, scaler, clock, log)
             if worker_cpus is not None:
                 runner.cpus = worker_cpus[q]
+            built[q] = (si, kube_api, sqs_api, runner, t)
+
+        if os.environ.get("KSA_BENCH_BUILD") == "threads" and queues > 1:
+            # probe: each queue's objects built on a thread of its own, all alive together, so
+            # every queue's heap allocations come from a separate malloc arena
+            import threading
+
+            done = threading.Barrier(queues)
+
+            def build_on_thread(q):
+                build(q)
+                done.wait()
+
+            ts = [threading.Thread(target=build_on_thread, args=(q,)) for q in range(queues)]
+            for th in ts:
+                th.start()
+            for th in ts:
+                th.join()
+        else:
+            for q in range(queues):
+                build(q)
+        for si, kube_api, sqs_api, runner, t in built:
+            self.server_of.append(si)
+            self.kube_apis.append(kube_api)
+            self.sqs_apis.append(sqs_api)
             self.runners.append(runner)
             self.targets.append(t)
 

@@ -1,0 +1,76 @@
+"""Each Runner polls on one OS thread for its whole life (HomeThread, csrc/core/runner.h), across
+Supervisor runs: a replaced thread would hand its malloc arena to another queue's new thread
+and interleave two queues' hot buffers (profiles/README.md, r02l). A thread that took a private
+file table is retired when a run wants the shared one."""
+import os
+
+from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
+
+
+def _workers():
+    out = set()
+    for t in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{t}/comm") as f:
+                if f.read().strip() == "ksa-worker":
+                    out.add(int(t))
+        except OSError:
+            pass
+    return out
+
+
+def test_runner_keeps_its_thread_across_runs(nat):
+    env = BenchEnv(3, "scale", servers="per-queue")
+    try:
+        env.run(20)
+        first = _workers()
+        assert len(first) == 3
+        env.run(20)  # a new Supervisor, the same runners
+        assert _workers() == first
+        sched = env.last_thread_sched
+        assert sched["threads"] == 3 and sched["cpu_ns"] > 0  # this run's share only
+        res = env.collect(20, 1.0)
+        assert len(res.samples) == 3 * 40 and res.signature_failures == 0
+    finally:
+        env.close()
+
+
+def test_private_table_thread_is_retired_for_a_shared_run(nat):
+    env = BenchEnv(2, "scale", servers="per-queue")
+    try:
+        sup = nat.Supervisor()
+        sup.private_files = True
+        for r in env.runners:
+            sup.add(r)
+        sup.start(10)
+        sup.join()
+        private = _workers()
+        assert len(private) == 2
+        sup2 = nat.Supervisor()
+        sup2.private_files = True
+        for r in env.runners:
+            sup2.add(r)
+        sup2.start(10)
+        sup2.join()
+        assert _workers() == private  # still private: kept
+        env.run(10)  # shared table: new threads
+        shared = _workers()
+        assert len(shared) == 2 and not (shared & private)
+        assert sum(r.stats()["polls"] for r in env.runners) == 2 * 30
+    finally:
+        env.close()
+
+
+def test_threads_end_with_their_runners(nat):
+    import gc
+
+    env = BenchEnv(2, "scale", servers="per-queue")
+    try:
+        before = len(_workers())
+        env.run(5)
+        assert len(_workers()) == before + 2
+        env.runners.clear()
+        gc.collect()
+        assert len(_workers()) == before
+    finally:
+        env.close()
