@@ -146,7 +146,7 @@ SharedWorkerState* init_shared_worker_state(void* at);
 // The OS thread a Runner's loop runs on, kept for the Runner's lifetime across Supervisor runs
 // (named ksa-worker). glibc gives every thread a malloc arena of its own and hands the arena of
 // an exited thread to the next thread created. When a fleet's threads are replaced -- a
-// warm-up run, a leadership hand-over -- queue i's new thread inherits the arena in which
+// warm-up run, any restart of a Supervisor -- queue i's new thread inherits the arena in which
 // queue j's old thread allocated j's lazily-built buffers, and i's per-poll temporaries land on
 // the cache lines of buffers j's thread writes every poll. Measured on the 8-queue thread fleet
 // (profiles/README.md, r02l): the same instructions per poll, +70 % user cycles and ~80 more
