@@ -1,14 +1,13 @@
 """Process-per-queue fleet: every tracked queue runs in a worker process of its own.
 
 The reference is one process per queue (/root/reference/main.go:95-97, one URL and one
-Deployment). :class:`~.fleet.Fleet` runs N queues as N threads of one process; that is cheap, but
-on the MI355X hosts the threads of one process pay for what the kernel shares between them
-(address space, file table) on every socket call -- measured, not guessed: the same N queues
-with the same CPU placement poll ~25 % slower as threads than as processes
-(``profiles/README.md``, r02 multi-queue study; ``csrc/tools/loopback_probe.cc`` shows it on a
-bare TCP echo). ``--worker-processes`` keeps the reference's isolation and this build's single
-pod: the supervisor forks one worker per queue, each with its own native clients, connections,
-logger and ``Runner``, and nothing mutable is shared except one
+Deployment). :class:`~.fleet.Fleet` runs N queues as N threads of one process, and since each
+runner keeps one thread for its life (``HomeThread``, csrc/core/runner.h; ``profiles/README.md``
+r02l) 8 thread queues poll as fast as 8 processes. ``--worker-processes`` keeps the
+reference's isolation inside this build's single pod: separate address spaces, file tables
+and allocators per queue, and per-process CPU and memory accounting. The supervisor forks one
+worker per queue, each with its own native clients, connections, logger and ``Runner``, and
+nothing mutable is shared except one
 ``SharedWorkerState`` slot per worker (csrc/core/runner.h) in an anonymous shared mapping:
 
 * the worker mirrors its counters, latency ring and a heartbeat into its slot (lock-free);
