@@ -837,7 +837,9 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def(py::init<>())
       .def("add", &Supervisor::add)
       .def_property("private_files", &Supervisor::private_files, &Supervisor::set_private_files)
-      .def("start", &Supervisor::start, py::arg("max_iterations") = -1)
+      // start may wait for a runner's HomeThread to finish a previous run (whose observer may
+      // need the GIL)
+      .def("start", &Supervisor::start, py::arg("max_iterations") = -1, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Supervisor::stop)
       .def("stopped", &Supervisor::stopped)
       .def("wait", &Supervisor::wait, py::arg("timeout_ns"), py::call_guard<py::gil_scoped_release>())

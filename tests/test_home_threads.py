@@ -20,13 +20,14 @@ def _workers():
 
 
 def test_runner_keeps_its_thread_across_runs(nat):
+    earlier = _workers()  # other tests' runners may still be alive in this process
     env = BenchEnv(3, "scale", servers="per-queue")
     try:
         env.run(20)
-        first = _workers()
+        first = _workers() - earlier
         assert len(first) == 3
         env.run(20)  # a new Supervisor, the same runners
-        assert _workers() == first
+        assert _workers() - earlier == first
         sched = env.last_thread_sched
         assert sched["threads"] == 3 and sched["cpu_ns"] > 0  # this run's share only
         res = env.collect(20, 1.0)
@@ -36,6 +37,7 @@ def test_runner_keeps_its_thread_across_runs(nat):
 
 
 def test_private_table_thread_is_retired_for_a_shared_run(nat):
+    earlier = _workers()
     env = BenchEnv(2, "scale", servers="per-queue")
     try:
         sup = nat.Supervisor()
@@ -44,7 +46,7 @@ def test_private_table_thread_is_retired_for_a_shared_run(nat):
             sup.add(r)
         sup.start(10)
         sup.join()
-        private = _workers()
+        private = _workers() - earlier
         assert len(private) == 2
         sup2 = nat.Supervisor()
         sup2.private_files = True
@@ -52,9 +54,9 @@ def test_private_table_thread_is_retired_for_a_shared_run(nat):
             sup2.add(r)
         sup2.start(10)
         sup2.join()
-        assert _workers() == private  # still private: kept
+        assert _workers() - earlier == private  # still private: kept
         env.run(10)  # shared table: new threads
-        shared = _workers()
+        shared = _workers() - earlier
         assert len(shared) == 2 and not (shared & private)
         assert sum(r.stats()["polls"] for r in env.runners) == 2 * 30
     finally:
@@ -66,11 +68,12 @@ def test_threads_end_with_their_runners(nat):
 
     env = BenchEnv(2, "scale", servers="per-queue")
     try:
-        before = len(_workers())
+        earlier = _workers()
         env.run(5)
-        assert len(_workers()) == before + 2
+        mine = _workers() - earlier
+        assert len(mine) == 2
         env.runners.clear()
         gc.collect()
-        assert len(_workers()) == before
+        assert not (_workers() & mine)
     finally:
         env.close()
