@@ -583,6 +583,53 @@ TEST(supervisor_stop_interrupts_sleep) {
   CHECK_EQ(api->calls(), uint64_t(0));
 }
 
+// Runners outlive their supervisors and keep their HomeThread: three supervisors in a row over
+// the same runners (the last one stopped mid-run), a second start() on a busy runner waiting for
+// the first run, then the runners dropped -- the threads end with them (TSan target).
+TEST(supervisor_runs_reuse_home_threads) {
+  auto clock = std::make_shared<RealClock>();
+  auto log = quiet_logger();
+  auto fake = std::make_shared<FakeDeployments>("ns");
+  std::vector<std::shared_ptr<Runner>> runners;
+  LoopConfig lc;
+  lc.poll_period = 0;
+  lc.scale_up_cool_down = 0;
+  lc.scale_down_cool_down = 0;
+  for (int i = 0; i < 4; ++i) {
+    fake->add("w" + std::to_string(i), 1);
+    auto api = std::make_shared<MockSqsApi>(attrs(150));
+    runners.push_back(std::make_shared<Runner>(
+        lc, std::make_shared<SqsClient>(api, "q", default_attribute_names()),
+        std::make_shared<PodAutoScaler>(fake, "w" + std::to_string(i), "ns", 8, 1, 1, 1, log, clock), clock, log));
+  }
+  for (int round = 0; round < 2; ++round) {
+    Supervisor sup;
+    for (auto& r : runners) sup.add(r);
+    sup.start(25);
+    CHECK(sup.wait(10 * kSecond));
+    sup.join();
+    CHECK_EQ(sup.thread_sched().threads, int64_t(4));
+  }
+  for (auto& r : runners) CHECK_EQ(r->stats().polls, uint64_t(50));
+  {
+    Supervisor sup;
+    for (auto& r : runners) sup.add(r);
+    sup.start(100);
+    sup.start(10);  // waits for each runner's first run, then runs again
+    CHECK(sup.wait(10 * kSecond));
+    sup.join();
+  }
+  for (auto& r : runners) CHECK_EQ(r->stats().polls, uint64_t(160));
+  {
+    Supervisor sup;
+    for (auto& r : runners) sup.add(r);
+    sup.start();  // until stopped
+    sup.stop();
+    CHECK(sup.wait(5 * kSecond));
+  }  // ~Supervisor joins
+  runners.clear();  // ~Runner ends each HomeThread
+}
+
 // 32 queues on 3 workers against the threaded fakes (TSan target for the scheduler heap).
 TEST(scheduler_many_queues_few_threads) {
   FakeSqsServer sqs;
