@@ -30,6 +30,9 @@ std::string amz_date(int64_t unix_nanos);
 
 // Wrapping int32 arithmetic, matching Go's defined overflow for int32(x) conversions and
 // `*currentReplicas + int32(p.ScaleUpPods)` (/root/reference/scale/scale.go:62-69).
+// ASCII-only lower case, as Go's textproto/strings.ToLower for header names and SigV4 (C's
+// tolower follows the process locale, which Python sets from the environment, and is a call).
+inline char ascii_lower(char c) { return (c >= 'A' && c <= 'Z') ? static_cast<char>(c + ('a' - 'A')) : c; }
 inline int32_t go_int32(int64_t v) { return static_cast<int32_t>(static_cast<uint32_t>(static_cast<uint64_t>(v))); }
 inline int32_t wrap_add32(int32_t a, int32_t b) {
   return static_cast<int32_t>(static_cast<uint32_t>(a) + static_cast<uint32_t>(b));

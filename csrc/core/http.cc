@@ -1,6 +1,7 @@
 #include "http.h"
 
 #include "affinity.h"
+#include "goutil.h"
 #include "log.h"
 
 #include <csignal>
@@ -54,15 +55,14 @@ int64_t mono_ns() {
 }
 
 std::string lower(std::string s) {
-  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  for (auto& c : s) c = ascii_lower(c);
   return s;
 }
 
 bool iequals(const std::string& a, const std::string& b) {
   if (a.size() != b.size()) return false;
   for (size_t i = 0; i < a.size(); ++i)
-    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i])))
-      return false;
+    if (ascii_lower(a[i]) != ascii_lower(b[i])) return false;
   return true;
 }
 
@@ -91,7 +91,7 @@ bool icontains(const std::string& hay, const char* needle) {
   if (n > hay.size()) return false;
   for (size_t i = 0; i + n <= hay.size(); ++i) {
     size_t k = 0;
-    while (k < n && std::tolower(static_cast<unsigned char>(hay[i + k])) == needle[k]) ++k;
+    while (k < n && ascii_lower(hay[i + k]) == needle[k]) ++k;
     if (k == n) return true;
   }
   return false;
@@ -101,8 +101,7 @@ const std::string* header_ptr(const Headers& hs, const char* name, size_t len) {
   for (auto& [k, v] : hs) {
     if (k.size() != len) continue;
     size_t i = 0;
-    while (i < len && std::tolower(static_cast<unsigned char>(k[i])) == std::tolower(static_cast<unsigned char>(name[i])))
-      ++i;
+    while (i < len && ascii_lower(k[i]) == ascii_lower(name[i])) ++i;
     if (i == len) return &v;
   }
   return nullptr;

@@ -198,7 +198,7 @@ void CachedCredentials::invalidate() {
 namespace {
 
 std::string lower(std::string s) {
-  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  for (auto& c : s) c = ascii_lower(c);
   return s;
 }
 
