@@ -178,12 +178,17 @@ class BenchEnv:
 
     ``affinity``: ``none`` -- threads float; ``llc`` -- queue q's worker thread and its fake
     endpoint pair are pinned to L3 domain q mod D (utils/topology.py), so each queue's traffic
-    stays on one CCD, as a rank per queue would (needs per-queue or process servers)."""
+    stays on one CCD, as a rank per queue would (needs per-queue or process servers).
+
+    Layout probes (profiles/README.md r02l): ``build_on_threads`` builds each queue's objects on a
+    thread of its own (separate malloc arenas); ``clock_per_queue`` gives each queue its own
+    clock object instead of one shared ``RealClock``."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared", affinity: str = "none",
-                 log_level: str = "info", sqs_protocol: str = "query"):
+                 log_level: str = "info", sqs_protocol: str = "query", build_on_threads: bool = False,
+                 clock_per_queue: bool = False):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -254,8 +259,7 @@ class BenchEnv:
         def build(q):
             si = q % n_servers
             sqs, kube, log = self.sqs_servers[si], self.kube_servers[si], self.loggers[q % len(self.loggers)]
-            # probe: KSA_BENCH_CLOCK=per-queue gives each queue a clock object of its own
-            clock = nat.RealClock() if os.environ.get("KSA_BENCH_CLOCK") == "per-queue" else self.clock
+            clock = nat.RealClock() if clock_per_queue else self.clock
             rest = RestConfig(host=kube.url, bearer_token=TOKEN, insecure=tls)
             sqs_tls = None
             if tls:
@@ -285,9 +289,9 @@ class BenchEnv:
                 runner.cpus = worker_cpus[q]
             built[q] = (si, kube_api, sqs_api, runner, t)
 
-        if os.environ.get("KSA_BENCH_BUILD") == "threads" and queues > 1:
-            # probe: each queue's objects built on a thread of its own, all alive together, so
-            # every queue's heap allocations come from a separate malloc arena
+        if build_on_threads and queues > 1:
+            # each queue's objects built on a thread of its own, all alive together, so every
+            # queue's heap allocations come from a separate malloc arena (scripts/arena_probe.py)
             import threading
 
             done = threading.Barrier(queues)

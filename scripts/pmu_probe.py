@@ -44,7 +44,7 @@ def read_counter(fd: int) -> int:
     return struct.unpack("Q", os.read(fd, 8))[0]
 
 
-VARIANTS = {"shared": {}, "isolated": {"KSA_BENCH_BUILD": "threads", "KSA_BENCH_CLOCK": "per-queue"},
+VARIANTS = {"shared": {}, "isolated": {"build_on_threads": True, "clock_per_queue": True, "loggers": "per-queue"},
             "one_run": {}}
 print(json.dumps({"perf_event_paranoid": open("/proc/sys/kernel/perf_event_paranoid").read().strip()}), flush=True)
 quick = "--quick" in sys.argv  # 1 and 8 queues in the CLI layout only (for GLIBC_TUNABLES A/B runs)
@@ -52,11 +52,8 @@ configs = ((1, "shared"), (8, "shared")) if quick else ((1, "shared"), (8, "shar
 tunables = os.environ.get("GLIBC_TUNABLES", "")
 for rnd in range(2 if quick else 3):
     for q, variant in configs:
-        for k in ("KSA_BENCH_BUILD", "KSA_BENCH_CLOCK"):
-            os.environ.pop(k, None)
-        os.environ.update(VARIANTS[variant])
         env = BenchEnv(q, "scale", busy_poll_ns=25_000, servers="process" if q == 1 else "processes",
-                       loggers="per-queue" if variant == "isolated" else "shared")
+                       **VARIANTS[variant])
         try:
             # Counters open before the first run: a fleet's threads (HomeThread, one per runner,
             # kept across runs) are created by it, and only threads created after an inherited
