@@ -863,7 +863,19 @@ struct HttpClient::Conn {
   std::string rbuf;
   uint64_t uses = 0;
   bool session_saved = false;
+  int64_t last_response_ns = 0;  // mono time a response was last read in full (0: none yet)
 };
+
+namespace {
+// A connection that delivered a complete keep-alive response this recently is reused without
+// the idle-close peek (one system call per request). Go's transport makes the same call
+// without any system call: its per-connection read loop flags a connection the peer closed, and
+// the flag is checked at reuse. A peer closes an idle keep-alive connection after seconds
+// (AWS, the apiserver), not milliseconds. At production poll periods the peek therefore still
+// runs for a poll's first request on each connection, and is skipped for the replica write
+// that follows the Deployment GET.
+constexpr int64_t kFreshConnNs = 20 * 1000 * 1000;
+}  // namespace
 
 HttpClient::HttpClient(const Url& origin, TlsOptions tls, Nanos timeout)
     : origin_(origin), tls_(std::move(tls)), timeout_(timeout) {
@@ -1149,7 +1161,8 @@ bool replayable(const HttpRequest& req) {
 
 Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable) {
   *retryable = false;
-  if (conn_ && conn_->uses > 0 && conn_->stream->peer_closed()) {
+  if (conn_ && conn_->uses > 0 && !(conn_->last_response_ns > 0 && mono_ns() - conn_->last_response_ns < kFreshConnNs) &&
+      conn_->stream->peer_closed()) {
     stats_.idle_closed++;
     conn_.reset();  // closed while idle: dial a fresh one (the request was never sent)
   }
@@ -1160,7 +1173,9 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   const bool reused = conn_->uses > 0;
   conn_->uses++;
 
-  std::string wire;
+  std::string& wire = wire_;  // kept across requests: no allocation per request
+  if (wire.capacity() > 64 * 1024) std::string().swap(wire);
+  wire.clear();
   wire.reserve(256 + req.body.size());
   wire += req.method;
   wire.push_back(' ');
@@ -1221,7 +1236,9 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   Status s;
   conn_->stream->set_spin_ns(spin_window());
   Reader rd(conn_->stream.get(), &conn_->rbuf);
-  std::string head;
+  std::string& head = head_;  // kept across responses: no allocation per response
+  if (head.capacity() > 64 * 1024) std::string().swap(head);
+  head.clear();
   bool got_any = false;
   while (true) {
     s = rd.read_head(&head, deadline_ns, &got_any);
@@ -1276,8 +1293,10 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   }
   stats_.bytes_in += head.size() + resp->body.size();
   {
-    const Nanos rtt = mono_ns() - sent_at_;
+    const int64_t now = mono_ns();
+    const Nanos rtt = now - sent_at_;
     ewma_ns_ = ewma_ns_ < 0 ? rtt : (ewma_ns_ * 7 + rtt) / 8;
+    conn_->last_response_ns = now;
   }
   // TLS 1.3 tickets arrive after the handshake (with the first response): keep the session of
   // each new connection once, for resumption on the next reconnect.

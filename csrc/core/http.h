@@ -172,6 +172,8 @@ class alignas(kCacheLine) HttpClient {
   std::atomic<bool> cancelled_{false};
   HttpRequest pending_;
   int64_t pending_deadline_ = 0;
+  std::string wire_;  // request serialisation buffer (write_request)
+  std::string head_;  // response head buffer (read_response)
 };
 
 // Threaded HTTP/1.1 server (accept thread + one thread per connection). Used by the fake

@@ -139,7 +139,9 @@ def test_idle_closed_connection_is_redialled_before_writing(nat, kube):
     api, _, _ = scaler(nat, kube, clock)
     obj = api.get("w")
     kube.drop_connections()
-    time.sleep(0.02)  # let the FIN arrive
+    # let the FIN arrive, and leave the 20 ms after a response in which a connection is reused
+    # without the idle-close peek (http.cc kFreshConnNs)
+    time.sleep(0.05)
     api.update("w", obj, 3)
     assert kube.replicas("ml", "w") == 3
     st = api.stats()["http"]
