@@ -1317,10 +1317,30 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   return Status::OK();
 }
 
+namespace {
+struct OnWire {
+  void (*fn)(void*) = nullptr;
+  void* arg = nullptr;
+};
+thread_local OnWire t_on_wire;
+void run_on_wire() {
+  OnWire w = t_on_wire;
+  if (!w.fn) return;
+  t_on_wire = OnWire{};  // one-shot, and not re-entered by a request `fn` makes
+  w.fn(w.arg);
+}
+}  // namespace
+
+void set_on_wire(void (*fn)(void*), void* arg) { t_on_wire = OnWire{fn, arg}; }
+bool on_wire_pending() { return t_on_wire.fn != nullptr; }
+void clear_on_wire() { t_on_wire = OnWire{}; }
+
 Status HttpClient::attempt(const HttpRequest& req, HttpResponse* resp, int64_t deadline_ns,
                            bool* retryable) {
   Status s = write_request(req, deadline_ns, retryable);
   if (!s.ok()) return s;
+  // Work that waits for this request to be on the wire (set_on_wire): the pipelined GET.
+  run_on_wire();
   // The request is on the wire: the poll's held log lines go out while the server works on it.
   // (Not in receive(): a pipelined response has usually arrived already, and the write would
   // sit between it and the next request.)

@@ -77,6 +77,15 @@ struct HttpClientStats {
   std::string tls_cipher;   // its cipher suite, e.g. "TLS_AES_128_GCM_SHA256"
 };
 
+// One-shot work for the calling thread to run as soon as its next HTTP request is on the wire
+// (HttpClient::attempt, after the write and before the wait for the response). The control loop
+// sends its pipelined Deployment GET from here: the SQS request goes out first and the GET
+// overlaps the SQS round trip, instead of its write delaying the SQS request. Setting replaces
+// a pending one; taking it clears it, so a request made by `fn` itself does not run it again.
+void set_on_wire(void (*fn)(void*), void* arg);
+bool on_wire_pending();
+void clear_on_wire();
+
 // One persistent connection to one origin. Thread-safe (requests are serialised), but each
 // control-loop worker owns its clients, so there is no contention in practice.
 class alignas(kCacheLine) HttpClient {

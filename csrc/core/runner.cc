@@ -99,13 +99,32 @@ IterationRecord Runner::poll_body() {
   rec.index = ++index_;
   const Nanos t0 = clock_->now();
   rec.t_poll = t0;
-  // Pipelined read: the Deployment GET goes out before the SQS call and overlaps it -- only
-  // when this poll is likely to reach the apiserver at all (the reference reads the Deployment
-  // only past the threshold and cool-down gates, main.go:51-77).
+  // Pipelined read: the Deployment GET overlaps the SQS call -- only when this poll is likely to
+  // reach the apiserver at all (the reference reads the Deployment only past the threshold and
+  // cool-down gates, main.go:51-77). Over HTTP the GET is sent as soon as the SQS request is on the wire (set_on_wire): sending
+  // it first would put its write (the loopback/TCP send path, ~2 µs) ahead of the SQS request on
+  // the critical path, while the GET's own round trip is shorter than the SQS call it overlaps.
+  // If the SQS write fails before that point, the GET goes out after the call (when it
+  // succeeded on a retry). In-memory clients (tests, the parity harness) get it first, as
+  // the virtual-time model of the overlap expects.
+  struct Prefetch {
+    Runner* self;
+    IterationRecord* rec;
+    static void send(void* p) {
+      auto* f = static_cast<Prefetch*>(p);
+      f->rec->prefetched = f->self->scaler_->prefetch();
+      if (f->rec->prefetched) f->rec->gets++;
+    }
+  } pf{this, &rec};
+  bool on_wire = false;
   if (cfg_.prefetch) {
     if (cfg_.prefetch_always || action_likely(t0)) {
-      rec.prefetched = scaler_->prefetch();
-      if (rec.prefetched) rec.gets++;
+      if (sqs_->api()->runs_on_wire_work()) {
+        on_wire = true;
+        set_on_wire(&Prefetch::send, &pf);
+      } else {
+        Prefetch::send(&pf);
+      }
     } else {
       rec.prefetch_gated = true;
     }
@@ -114,6 +133,10 @@ IterationRecord Runner::poll_body() {
   // main.go:43-47
   auto depth = sqs_->num_messages();
   Nanos t1 = clock_->now();
+  if (on_wire && on_wire_pending()) {
+    clear_on_wire();
+    if (depth.ok()) Prefetch::send(&pf);  // the SQS request never reached the wire first
+  }
   rec.depth_ns = t1 - t0;
   last_depth_rtt_ = rec.depth_ns;
   if (!depth.ok()) {

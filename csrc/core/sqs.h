@@ -48,6 +48,9 @@ class SqsApi {
   // Clock time at which the latest deliberate wait (retry back-off, Retry-After) ends or ended;
   // 0: none yet. The liveness check counts such a wait as progress.
   virtual Nanos waiting_until() const { return 0; }
+  // True when a call writes an HTTP request through HttpClient, so work handed to set_on_wire
+  // (http.h) runs while the call is in flight.
+  virtual bool runs_on_wire_work() const { return false; }
 };
 
 enum class SqsProtocol { Query, Json };
@@ -90,6 +93,7 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   static std::string signing_region(const std::string& region);
   std::string endpoint() const { return endpoint_; }
   Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }
+  bool runs_on_wire_work() const override { return true; }
 
  private:
   std::atomic<Nanos> wait_until_{0};
