@@ -279,6 +279,56 @@ TEST(http_keepalive_roundtrips) {
   srv.stop();
 }
 
+// set_on_wire: the work runs once, after the request is written (the server may already hold
+// it) and before the response is read; a request the work makes itself does not run it again;
+// a request that never reaches the wire leaves it pending; clear_on_wire drops it.
+TEST(http_on_wire_hook) {
+  HttpServer srv([](const HttpRequest& req, HttpResponse* resp) {
+    resp->status = 200;
+    resp->body = req.target;
+  });
+  CHECK(srv.listen("127.0.0.1", 0).ok());
+  auto u = parse_url("http://127.0.0.1:" + std::to_string(srv.port()));
+  HttpClient a(u.value, TlsOptions{}, 5 * kSecond), b(u.value, TlsOptions{}, 5 * kSecond);
+  struct Ctx {
+    HttpClient* other;
+    int runs = 0;
+    bool inner_ok = false;
+  } ctx{&b};
+  auto work = [](void* p) {
+    auto* c = static_cast<Ctx*>(p);
+    c->runs++;
+    HttpRequest r;
+    r.target = "/inner";
+    c->inner_ok = c->other->send(r).ok();  // an HTTP request from inside the hook
+  };
+  set_on_wire(work, &ctx);
+  CHECK(on_wire_pending());
+  HttpRequest req;
+  req.target = "/outer";
+  HttpResponse resp;
+  CHECK(a.round_trip(req, &resp).ok());
+  CHECK_EQ(resp.body, std::string("/outer"));
+  CHECK_EQ(ctx.runs, 1);
+  CHECK(ctx.inner_ok);
+  CHECK(!on_wire_pending());
+  HttpResponse inner;
+  CHECK(b.receive(&inner).ok());
+  CHECK_EQ(inner.body, std::string("/inner"));
+  CHECK(a.round_trip(req, &resp).ok());  // one-shot
+  CHECK_EQ(ctx.runs, 1);
+  // nothing listens there: the request never reaches the wire, the work stays pending
+  auto dead = parse_url("http://127.0.0.1:1");
+  HttpClient c(dead.value, TlsOptions{}, 200 * kMillisecond);
+  set_on_wire(work, &ctx);
+  CHECK(!c.round_trip(req, &resp).ok());
+  CHECK_EQ(ctx.runs, 1);
+  CHECK(on_wire_pending());
+  clear_on_wire();
+  CHECK(!on_wire_pending());
+  srv.stop();
+}
+
 TEST(http_tls_roundtrip) {
   std::string cert, key;
   CHECK(generate_self_signed("127.0.0.1", &cert, &key).ok());
