@@ -161,8 +161,13 @@ class Stream {
   Status ssl_op(F op, int64_t deadline_ns, int* out, const char* what) {
     int64_t spin_end = 0;
     bool spin_over = false;
+    // SSL_get_error reads the thread's error queue, so it must start empty. A WANT_READ /
+    // WANT_WRITE result queues nothing: the busy-poll retries skip the clear (OpenSSL 3 resets
+    // all 16 queue slots per call, the largest cost of a TLS spin iteration in the r02q
+    // profile) unless something is queued after all.
+    ERR_clear_error();
     for (int i = 0;; ++i) {
-      ERR_clear_error();
+      if (i > 0 && ERR_peek_error() != 0) ERR_clear_error();
       int r = op();
       if (r > 0) {
         *out = r;

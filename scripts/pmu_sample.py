@@ -76,10 +76,11 @@ def drain(ring: mmap.mmap, pages: int) -> tuple:
 
 
 os.makedirs("gpurun_out/pmu_sample", exist_ok=True)
-for q in (1, 8):
+TLS = "--tls" in sys.argv  # one queue over keep-alive TLS 1.3 instead of 1 and 8 plain queues
+for q in ((1,) if TLS else (1, 8)):
     pages = DATA_PAGES // q  # the rings of all workers together stay within the mlock limit
     for event, (typ, cfg, period) in EVENTS.items():
-        env = BenchEnv(q, "scale", busy_poll_ns=25_000, servers="process" if q == 1 else "processes")
+        env = BenchEnv(q, "scale", busy_poll_ns=25_000, servers="process" if q == 1 else "processes", tls=TLS)
         try:
             env.run(200)
             env.clear()
@@ -114,10 +115,10 @@ for q in (1, 8):
                 maps_text = f.read()
         finally:
             env.close()
-        out = {"queues": q, "event": event, "period": period * q, "polls": q * steps, "p50_ms": res.summary()["p50_ms"],
+        out = {"queues": q, "tls": TLS, "event": event, "period": period * q, "polls": q * steps, "p50_ms": res.summary()["p50_ms"],
                "threads_sampled": len(rings), "samples": sum(hist.values()), "lost": lost,
                "hist": {hex(k): v for k, v in hist.most_common()}, "maps": maps_text}
-        with open(f"gpurun_out/pmu_sample/q{q}_{event}.json", "w") as f:
+        with open(f"gpurun_out/pmu_sample/q{q}{'_tls' if TLS else ''}_{event}.json", "w") as f:
             json.dump(out, f)
         print(json.dumps({k: out[k] for k in ("queues", "event", "polls", "p50_ms", "threads_sampled", "samples", "lost")}),
               flush=True)

@@ -111,7 +111,7 @@ def main():
     for f in sorted(os.listdir(root)):
         if f.endswith(".json"):
             d, by_fn = profile(os.path.join(root, f))
-            profiles[(d["event"], d["queues"])] = (d, by_fn)
+            profiles[(d["event"], f'{d["queues"]}{"tls" if d.get("tls") else ""}')] = (d, by_fn)
     for event in sorted({e for e, _ in profiles}):
         qs = sorted(q for e, q in profiles if e == event)
         print(f"== {event}: samples x period per poll, by function ({', '.join(f'q{q}' for q in qs)}) ==")
