@@ -87,6 +87,11 @@ def main(argv=None) -> int:
                     help="one logrus-style logger for the rank (as the reference's global logger) or one per queue")
     ap.add_argument("--secondary-samples", type=int, default=2000,
                     help="samples per queue for every secondary row (independent of --steps)")
+    ap.add_argument("--placement", default="kernel", choices=["rank-l3", "kernel"],
+                    help="kernel: the scheduler places the threads; rank-l3: this rank's worker thread and fake "
+                         "endpoints on a block of physical cores of their own in L3 domain LOCAL_RANK mod D "
+                         "(utils/topology.plan_rank; one tracked queue per rank only). Rehearsed at 1/2/4/8 ranks "
+                         "on the box, rank-l3 was slower (profiles/README.md r02s), so kernel is the default")
     args = ap.parse_args(argv)
 
     import torch
@@ -118,8 +123,18 @@ def main(argv=None) -> int:
     pipeline = not args.no_pipeline
     bp = args.busy_poll_us * 1000
     servers = args.servers if args.servers != "auto" else ("shared" if args.queues == 1 else "processes")
+    placement = None
+    if args.placement == "rank-l3" and args.queues == 1 and servers in ("shared", "per-queue"):
+        from kube_sqs_autoscaler_amd.utils.topology import plan_rank
+
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        try:
+            placement = plan_rank(local_rank, max(local_world, 1))
+        except OSError:
+            placement = None
+    affinity = json.dumps({"workers": [placement[0]], "servers": [placement[1]]}) if placement else "none"
     env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp, servers=servers,
-                   loggers=args.loggers)
+                   loggers=args.loggers, affinity=affinity)
     try:
         if args.warmup:
             env.run(args.warmup)
@@ -170,6 +185,9 @@ def main(argv=None) -> int:
             "pipeline_reads": pipeline,
             "busy_poll_us": args.busy_poll_us,
             "fake_endpoints": servers,
+            "placement": ({"rank0_worker_cpus": placement[0], "rank0_endpoint_cpus": placement[1],
+                           "rule": "rank r: L3 domain r mod D, a block of 3 physical cores of its own"}
+                          if placement else "kernel"),
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},

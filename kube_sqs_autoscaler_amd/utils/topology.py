@@ -103,3 +103,26 @@ def plan_queue_ccds(n: int, endpoint_cores: int = 2,
         ep = [c for core in cores[1:1 + endpoint_cores] for c in core]
         endpoints.append(ep or cores[0])
     return workers, endpoints
+
+
+def plan_rank(rank: int, nranks: int, endpoint_cores: int = 2,
+              domains: Optional[List[List[int]]] = None) -> Optional["tuple[List[int], List[int]]"]:
+    """Placement of one bench rank (one autoscaler process per GPU, its fake endpoints in the same
+    process): rank r gets L3 domain r mod D, and within it a block of 1 + ``endpoint_cores``
+    physical cores of its own -- the worker on the first core's first CPU, the fake servers on
+    the rest (SMT siblings included) -- so ranks never share a core and each rank's round trips
+    stay inside one L3. None when the domains cannot give every rank its own block (then the
+    kernel places the threads)."""
+    doms = domains if domains is not None else llc_domains()
+    if not doms or rank < 0 or rank >= nranks:
+        return None
+    per = 1 + endpoint_cores
+    d = rank % len(doms)
+    slot = rank // len(doms)
+    ranks_here = (nranks - d + len(doms) - 1) // len(doms)  # ranks that land on domain d
+    cores = physical_cores(doms[d])
+    if len(cores) < ranks_here * per:
+        return None
+    skip = 1 if len(cores) > ranks_here * per else 0  # leave a domain's first core (CPU 0's housekeeping) when it can
+    block = cores[skip + slot * per:skip + (slot + 1) * per]
+    return [block[0][0]], [c for core in block[1:] for c in core]
