@@ -1,3 +1,4 @@
+# TLS vs plain per-phase probe (scripts/tls_detail.py), twice, on the GPU box.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
