@@ -126,12 +126,7 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
   if (!cr.ok()) return Result<AttrMap>::Err(cr.status);
 
   std::unique_lock<std::mutex> prep_lock(prep_mu_);
-  std::string key = queue_url;
-  for (auto& n : names) {
-    key.push_back('\x1f');
-    key += n;
-  }
-  if (key != prepared_key_) {
+  if (!prepared_valid_ || queue_url != prepared_url_ || names != prepared_names_) {
     HttpRequest proto;
     proto.method = "POST";
     proto.target = url_.path.empty() ? "/" : url_.path;
@@ -170,13 +165,26 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
     }
     prepared_ = signer_.prepare("POST", path, query, proto.headers, proto.body);
     prepared_body_ = std::move(proto.body);
-    prepared_key_ = std::move(key);
+    prepared_url_ = queue_url;
+    prepared_names_ = names;
+    prepared_valid_ = true;
+    signed_valid_ = false;
   }
   HttpRequest req;
   req.method = "POST";
   req.target = url_.path.empty() ? "/" : url_.path;
   req.body = prepared_body_;
-  signer_.sign_prepared(prepared_, cr.value, clock_->unix_nanos(), &req.headers);
+  const int64_t now_ns = clock_->unix_nanos();
+  const int64_t sec = now_ns / 1000000000 - (now_ns % 1000000000 < 0 ? 1 : 0);  // floor: amz_date's second
+  const Credentials& c = cr.value;
+  if (!signed_valid_ || sec != signed_sec_ || c.access_key_id != signed_creds_.access_key_id ||
+      c.secret_access_key != signed_creds_.secret_access_key || c.session_token != signed_creds_.session_token) {
+    signer_.sign_prepared(prepared_, c, now_ns, &signed_headers_);
+    signed_sec_ = sec;
+    signed_creds_ = c;
+    signed_valid_ = true;
+  }
+  req.headers = signed_headers_;
   prep_lock.unlock();
 
   HttpResponse resp;

@@ -114,9 +114,18 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   // Prepared request for the last (queue, attribute names): the body and every fixed signing
   // input are built once per queue instead of once per poll.
   std::mutex prep_mu_;  // guards the prepared request (an HttpSqsApi may be shared by workers)
-  std::string prepared_key_;
+  bool prepared_valid_ = false;
+  std::string prepared_url_;
+  std::vector<std::string> prepared_names_;
   SigV4Prepared prepared_;
   std::string prepared_body_;
+  // Signed headers of the prepared request, kept for the second they were signed in: X-Amz-Date
+  // has one-second resolution, so within that second (and for the same credentials) the
+  // signature is the same bytes and is not recomputed.
+  int64_t signed_sec_ = 0;
+  bool signed_valid_ = false;
+  Credentials signed_creds_;
+  Headers signed_headers_;
   mutable std::mutex mu_;
   SqsApiStats stats_;
   uint64_t rng_ = 0x9E3779B97F4A7C15ULL;

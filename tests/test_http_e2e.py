@@ -579,3 +579,32 @@ def test_client_rejects_malformed_response_header_line(nat):
     finally:
         t.join(timeout=10)
         ls.close()
+
+
+def test_signature_reused_only_within_its_second_and_credentials(nat, sqs_server):
+    """The prepared SQS request's signed headers are reused while X-Amz-Date (one-second
+    resolution) and the credentials are unchanged -- the same bytes a fresh signature gives --
+    and re-signed at the next second or after a credential rotation."""
+    token = ["t1"]
+
+    class Rotating(nat.CredentialsProvider):
+        def retrieve(self):  # expired at once: fetched again for every call
+            return nat.Credentials(AKID, SECRET, token[0], 1, "Rotating")
+
+    clock = nat.VirtualClock()  # starts on a whole second of unix time
+    api = new_sqs_api(REGION, clock, endpoint=sqs_server.url, credentials=Rotating())
+    url = f"{sqs_server.url}/123456789012/jobs"
+    c = nat.SqsClient(api, url, NAMES)
+    sqs_server.set_attributes(url, ATTRS)
+    seen = []
+    for i, step_ms in enumerate((0, 400, 599, 1, 0)):
+        clock.advance(step_ms * 1_000_000)
+        if i == 4:
+            token[0] = "t2"
+        assert c.num_messages() == 18
+        h = dict(sqs_server.last_headers())
+        seen.append((h["X-Amz-Date"], h["Authorization"], h.get("X-Amz-Security-Token")))
+    assert sqs_server.signature_failures() == 0
+    assert seen[0] == seen[1] == seen[2]  # same second, same credentials
+    assert seen[3][0] != seen[2][0] and seen[3][1] != seen[2][1]  # next second: signed again
+    assert seen[4][0] == seen[3][0] and seen[4][2] == "t2" and seen[4][1] != seen[3][1]  # rotated token
