@@ -5,8 +5,9 @@
 // (integer-only, bit-identical to the CPU path). Lane l simulates configuration l / seeds with
 // seed l % seeds, so a wave holds consecutive seeds of one configuration. Layout as the open-loop
 // kernel (policy_sweep.hip): parameters [9][m] int64 (structure of arrays, read once per lane),
-// outputs [field][m * seeds]; the arrival-rate trace is read from global memory (all lanes walk
-// it nearly in lockstep, so L2 serves it). The grid is one resident wave of workgroups
+// outputs [field][m * seeds]; the arrival-rate trace is read from global memory through a
+// register-resident cursor (queue_sim.h RateCursor), one segment ahead, so a poll inside a segment
+// makes no trace load. The grid is one resident wave of workgroups
 // (occupancy API x CUs) with a grid-stride loop; every lane's loop is bounded by the horizon
 // and ksa_sim::kMaxPolls.
 #include <hip/hip_runtime.h>
@@ -24,6 +25,8 @@ constexpr int kBlock = 256;
 // Minimum resident waves per SIMD the register allocator must allow (0: compiler's choice).
 // Measured on an MI355X (768k lanes x 24 h, same box): compiler's choice 107 VGPRs / 4 waves
 // 182.7 ms; 5 waves (96 VGPRs, 24 B scratch) 171.1 ms; 6 waves (80 VGPRs, 92 B scratch) 188.5 ms.
+// Round 2 (register rate cursor + sqrt memo, 24000 x 32 lanes x 24 h): 5 waves 125.6 ms vs 4 waves
+// 131.3 ms (profiles/r02u_queue_ab).
 #ifndef KSA_QUEUE_WAVES_PER_EU
 #define KSA_QUEUE_WAVES_PER_EU 5
 #endif
