@@ -148,3 +148,22 @@ def test_cpu_path_equals_python_model_at_extremes(nat, rate, service, poll_s, in
         for s in range(2):
             want = cl.reference_lane(tr, res.config(i), model, 1, horizon, (0, 0, 0), 5 + s)
             assert {k: int(v[i, s]) for k, v in res.out.items()} == want, (res.config(i), s)
+
+
+def test_cpu_path_equals_python_model_on_fine_segments(nat):
+    """Segments shorter than a poll interval, boundaries on whole poll times, a zero-rate run and
+    a rate held to the horizon: the register-resident rate cursor (queue_sim.h RateCursor) must
+    integrate exactly what the Python model does."""
+    segs = [(0.0, 3.0), (2.0, 0.0), (2.5, 7.25), (5.0, 40.0), (10.0, 0.5), (10.001, 12.0), (35.0, 0.0),
+            (70.0, 0.0), (71.0, 90.0), (71.5, 1.0)]
+    tr = cl.ArrivalTrace.from_segments(segs)
+    grid = sweep.grid(poll_ns=[1 * S, 5 * S], up_cool_ns=[0, 3 * S], down_cool_ns=[0], up_msgs=[10, 50],
+                      down_msgs=[2], max_pods=[6], min_pods=[1])
+    model = cl.QueueModel(service_rate=3.0, startup_ns=2 * S, slo_backlog=50, init_backlog=5)
+    horizon = 120 * S
+    res = cl.run(tr, grid, model, 1, horizon, (0, 1_000_000, 1_000_000), seeds=4, seed0=3, device="cpu")
+    for i in range(len(res)):
+        for s in range(4):
+            want = cl.reference_lane(tr, res.config(i), model, 1, horizon, (0, 1_000_000, 1_000_000), 3 + s)
+            got = {k: int(v[i, s]) for k, v in res.out.items()}
+            assert got == want, (res.config(i), s)
