@@ -66,6 +66,8 @@ void queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
                      int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, int threads) {
   const int64_t lanes = m * seeds;
   if (lanes <= 0 || n < 1) return;
+  for (int k = 0; k < 3; ++k)
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return;  // closedloop.py validates first
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
   const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
   auto work = [&](int64_t lo, int64_t hi) {

@@ -107,6 +107,11 @@ int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli,
     g_queue_error = "seeds must be >= 1";
     return -1;
   }
+  for (int k = 0; k < 3; ++k)
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) {
+      g_queue_error = "latencies must be within [0, 1 h]";
+      return -1;
+    }
   const int64_t lanes = m * seeds;
   if (lanes <= 0) return 0;
   if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;

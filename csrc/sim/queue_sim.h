@@ -72,6 +72,9 @@ KSA_HD int64_t sat_mul(int64_t a, int64_t b) {
   int64_t r;
   return __builtin_mul_overflow(a, b, &r) || r > kSat ? kSat : r;
 }
+// x / 10^6 for x >= 0 (backlogs, virtual times): as an unsigned division by a constant it drops
+// the signed form's rounding correction (21 fewer VALU instructions in the gfx950 kernel).
+KSA_HD int64_t udiv_1e6(int64_t x) { return static_cast<int64_t>(static_cast<uint64_t>(x) / 1000000u); }
 KSA_HD int64_t sat_add(int64_t a, int64_t b) { return a > kSat - b ? kSat : a + b; }
 // Messages (micro-messages) a rate of x_milli milli-msgs/s delivers in dt_ms: the product,
 // saturating.
@@ -180,7 +183,7 @@ KSA_HD void advance(QueueState* s, QueueResult* r, const QueueModel& m, const in
   }
   const int64_t served = s->q_micro < cap ? s->q_micro : cap;
   s->q_micro -= served;
-  s->q_msgs = s->q_micro / 1000000;
+  s->q_msgs = udiv_1e6(s->q_micro);
   r->served = sat_add(r->served, served);
   if (s->pending > 0 && s->pending_at_ms <= t1_ms) {
     s->ready += s->pending;
@@ -194,8 +197,11 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
   QueueResult res;
   const Rules k = make_rules(p);
   QueueState s;
-  s.q_micro = m.init_backlog * 1000000;
-  s.q_msgs = m.init_backlog;
+  // backlog and virtual time never go negative (arrivals and latencies are >= 0; a negative
+  // initial backlog is clamped), so the per-poll divisions by 10^6 can be unsigned
+  const int64_t init_backlog = m.init_backlog > 0 ? m.init_backlog : 0;
+  s.q_micro = init_backlog * 1000000;
+  s.q_msgs = init_backlog;
   s.ready = init_replicas;
   s.pending = 0;
   s.pending_at_ms = 0;
@@ -212,7 +218,7 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
   while (advances && res.polls < kMaxPolls) {
     const int64_t t_poll = now + k.period;  // main.go:41 sleep, then poll
     if (t_poll > horizon_ns) break;
-    const int64_t t_poll_ms = t_poll / 1000000;
+    const int64_t t_poll_ms = udiv_1e6(t_poll);
     advance(&s, &res, m, t_ms, rate_milli, n, &cur, seed, prev_ms, t_poll_ms, replicas);
     prev_ms = t_poll_ms;
     now = t_poll;
