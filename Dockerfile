@@ -22,8 +22,7 @@ RUN pip3 install --no-cache-dir pybind11==3.0.4 \
 
 FROM ubuntu:22.04 AS base
 # Runtime Python deps from the distribution archive (no pip at runtime).
-RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-yaml \
-      python3-prometheus-client ca-certificates libssl3 \
+RUN apt-get update && apt-get install -y --no-install-recommends python3 python3-yaml ca-certificates libssl3 \
  && rm -rf /var/lib/apt/lists/*
 COPY --from=builder /work/kube_sqs_autoscaler_amd /app/kube_sqs_autoscaler_amd
 COPY --from=builder /work/deploy/bin/kube-sqs-autoscaler /kube-sqs-autoscaler

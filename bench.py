@@ -68,6 +68,30 @@ def _apiserver_requests_per_poll(wire: dict) -> dict:
     return out
 
 
+def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
+    """Poll->patch latency at production poll periods (250 ms and 1 s; the reference's default
+    is 5 s, /root/reference/main.go:83): ``--cadence-queues`` queues, one thread each, staggered
+    over the period, against one endpoint process serving them all (bench/latency.py
+    ``measure_cadenced``). Default path and reference-equivalent path, plain and TLS, with
+    per-phase medians. Each row keeps >= 400 samples."""
+    from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced
+
+    ms = 1_000_000
+    p50, rows = {}, {}
+    for label, period in (("250ms", 250 * ms), ("1s", 1000 * ms)):
+        for name, mode, pl, b in (("default", args.mode, pipeline, bp), ("reference_equivalent", "deployment", False, 0)):
+            for tls in (False, True):
+                key = name + ("_tls" if tls else "")
+                r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls)
+                rows.setdefault(label, {})[key] = r
+                p50.setdefault(label, {})[key] = r["p50_ms"]
+    return {
+        "cadenced_p50_ms": p50,
+        "cadenced_rows": rows,
+        "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()},
+    }
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,7 +99,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--queues", type=int, default=1, help="tracked queues per rank")
     ap.add_argument("--mode", default="scale", choices=["scale", "deployment", "patch"])
-    ap.add_argument("--no-sweep", action="store_true", help="skip the 1/2/4/8-queue sweep (single rank only)")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip every secondary row: the 1/2/4/8-queue sweep, the production-cadence rows, ...")
     ap.add_argument("--no-pipeline", action="store_true", help="strictly sequential SQS -> GET -> write")
     ap.add_argument("--busy-poll-us", type=int, default=25, help="adaptive client busy-poll window (CLI default --busy-poll=25us; 0: block)")
     ap.add_argument("--servers", default="auto", choices=["auto", "shared", "per-queue", "processes"],
@@ -83,15 +108,13 @@ def main(argv=None) -> int:
                          "in-process pair per queue, or one endpoint process per queue (processes, so the "
                          "fakes' threads do not share the autoscaler's process); auto: shared for one queue, "
                          "processes for more")
-    ap.add_argument("--loggers", default="shared", choices=["shared", "per-queue"],
-                    help="one logrus-style logger for the rank (as the reference's global logger) or one per queue")
     ap.add_argument("--secondary-samples", type=int, default=2000,
                     help="samples per queue for every secondary row (independent of --steps)")
-    ap.add_argument("--placement", default="kernel", choices=["rank-l3", "kernel"],
-                    help="kernel: the scheduler places the threads; rank-l3: this rank's worker thread and fake "
-                         "endpoints on a block of physical cores of their own in L3 domain LOCAL_RANK mod D "
-                         "(utils/topology.plan_rank; one tracked queue per rank only). Rehearsed at 1/2/4/8 ranks "
-                         "on the box, rank-l3 was slower (profiles/README.md r02s), so kernel is the default")
+    ap.add_argument("--cadence-queues", type=int, default=16,
+                    help="queues (one thread each, staggered) per production-cadence row")
+    ap.add_argument("--cadence-polls", type=int, default=27,
+                    help="polls per queue per production-cadence row (the first 2 of each queue are dropped)")
+    ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
     args = ap.parse_args(argv)
 
     import torch
@@ -123,18 +146,7 @@ def main(argv=None) -> int:
     pipeline = not args.no_pipeline
     bp = args.busy_poll_us * 1000
     servers = args.servers if args.servers != "auto" else ("shared" if args.queues == 1 else "processes")
-    placement = None
-    if args.placement == "rank-l3" and args.queues == 1 and servers in ("shared", "per-queue"):
-        from kube_sqs_autoscaler_amd.utils.topology import plan_rank
-
-        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-        try:
-            placement = plan_rank(local_rank, max(local_world, 1))
-        except OSError:
-            placement = None
-    affinity = json.dumps({"workers": [placement[0]], "servers": [placement[1]]}) if placement else "none"
-    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp, servers=servers,
-                   loggers=args.loggers, affinity=affinity)
+    env = BenchEnv(args.queues, args.mode, pipeline=pipeline, busy_poll_ns=bp, servers=servers)
     try:
         if args.warmup:
             env.run(args.warmup)
@@ -185,9 +197,6 @@ def main(argv=None) -> int:
             "pipeline_reads": pipeline,
             "busy_poll_us": args.busy_poll_us,
             "fake_endpoints": servers,
-            "placement": ({"rank0_worker_cpus": placement[0], "rank0_endpoint_cpus": placement[1],
-                           "rule": "rank r: L3 domain r mod D, a block of 3 physical cores of its own"}
-                          if placement else "kernel"),
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
@@ -249,6 +258,8 @@ def main(argv=None) -> int:
                 "default": phase_breakdown(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp),
                 "reference_equivalent": phase_breakdown(mode="deployment", pipeline=False),
             }
+        if world == 1 and not args.no_sweep and not args.no_cadence:
+            extra.update(_cadence_rows(args, pipeline, bp, p50))
         extra["decision_parity"] = _parity_summary()
         extra["apiserver_requests_per_poll"] = _apiserver_requests_per_poll(extra["decision_parity"])
         out = {

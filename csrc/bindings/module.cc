@@ -772,9 +772,12 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["latency_samples"] = s.latency_samples;
         d["latency_sum_ns"] = s.latency_sum_ns;
         d["latency_buckets"] = std::vector<uint64_t>(s.latency_buckets, s.latency_buckets + kLatBuckets);
+        d["consecutive_failed_polls"] = s.consecutive_failed_polls;
         return d;
       })
       .def("idle_ns", &Runner::idle_ns)
+      .def("failing_ns", &Runner::failing_ns)
+      .def("last_error", &Runner::last_error)
       .def_property("cpus", &Runner::cpus, &Runner::set_cpus)
       .def("set_shared_state", [](Runner& r, uintptr_t addr) {
         r.set_shared_state(addr ? reinterpret_cast<SharedWorkerState*>(addr) : nullptr);
@@ -799,12 +802,13 @@ PYBIND11_MODULE(_ksa_native, m) {
     static const char* names[] = {"polls", "depth_errors", "scale_ups", "scale_downs", "noop_ups", "noop_downs",
                                   "cooldown_skips_up", "cooldown_skips_down", "failed_ups", "failed_downs",
                                   "speculative_reads", "speculative_reads_used", "speculative_reads_gated",
-                                  "apiserver_reads", "latency_samples"};
+                                  "apiserver_reads", "latency_samples", "consecutive_failed_polls"};
     static_assert(sizeof(names) / sizeof(names[0]) == SharedWorkerState::kNumCounters, "counter names");
     py::dict d;
     for (int i = 0; i < SharedWorkerState::kNumCounters; ++i)
       d[names[i]] = s->counters[i].load(std::memory_order_acquire);
     d["progress_ns"] = s->progress_ns.load(std::memory_order_acquire);
+    d["last_good_ns"] = s->last_good_ns.load(std::memory_order_relaxed);
     d["last_depth"] = s->last_depth.load(std::memory_order_relaxed);
     d["last_replicas"] = s->last_replicas.load(std::memory_order_relaxed);
     d["latency_sum_ns"] = s->lat_sum_ns.load(std::memory_order_relaxed);
@@ -836,7 +840,7 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<Supervisor, std::shared_ptr<Supervisor>>(m, "Supervisor")
       .def(py::init<>())
       .def("add", &Supervisor::add)
-      .def_property("private_files", &Supervisor::private_files, &Supervisor::set_private_files)
+      .def_property("stagger", &Supervisor::stagger, &Supervisor::set_stagger)
       // start may wait for a runner's HomeThread to finish a previous run (whose observer may
       // need the GIL)
       .def("start", &Supervisor::start, py::arg("max_iterations") = -1, py::call_guard<py::gil_scoped_release>())

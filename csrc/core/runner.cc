@@ -56,6 +56,11 @@ void Runner::arm() {
   last_up_ = clock_->now();
   last_down_ = clock_->now();
   progress_ns_.store(clock_->now(), std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.last_good_ns = clock_->now();  // a failing streak is timed from Run() entry at the earliest
+  }
+  if (shared_) shared_->last_good_ns.store(clock_->now(), std::memory_order_relaxed);
 }
 
 // Would this poll call ScaleUp/ScaleDown if the queue depth were still the last one read?
@@ -220,10 +225,19 @@ IterationRecord Runner::poll_body() {
 }
 
 void Runner::record(const IterationRecord& r) {
-  progress_ns_.store(clock_->now(), std::memory_order_release);
+  const Nanos now = clock_->now();
+  progress_ns_.store(now, std::memory_order_release);
+  const bool good = r.depth_ok && r.up != Action::Failed && r.down != Action::Failed;
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.polls++;
+    if (good) {
+      stats_.consecutive_failed_polls = 0;
+      stats_.last_good_ns = now;
+    } else {
+      stats_.consecutive_failed_polls++;
+      last_error_ = r.error;
+    }
     if (r.prefetched) stats_.speculative_reads++;
     if (r.prefetch_used) stats_.speculative_reads_used++;
     if (r.prefetch_gated) stats_.speculative_reads_gated++;
@@ -266,6 +280,7 @@ SharedWorkerState* init_shared_worker_state(void* at) {
   auto* s = new (at) SharedWorkerState;
   for (auto& c : s->counters) c.store(0, std::memory_order_relaxed);
   s->progress_ns.store(0, std::memory_order_relaxed);
+  s->last_good_ns.store(0, std::memory_order_relaxed);
   s->last_depth.store(0, std::memory_order_relaxed);
   s->last_replicas.store(-1, std::memory_order_relaxed);
   s->lat_sum_ns.store(0, std::memory_order_relaxed);
@@ -301,6 +316,8 @@ void Runner::mirror(const IterationRecord& r) {
   put(W::kSpeculativeReadsUsed, st.speculative_reads_used);
   put(W::kSpeculativeReadsGated, st.speculative_reads_gated);
   put(W::kApiserverReads, st.apiserver_reads);
+  put(W::kConsecutiveFailedPolls, st.consecutive_failed_polls);
+  shared_->last_good_ns.store(st.last_good_ns, std::memory_order_relaxed);
   shared_->last_depth.store(st.last_depth, std::memory_order_relaxed);
   shared_->last_replicas.store(st.last_replicas, std::memory_order_relaxed);
   if (r.patch_latency_ns >= 0) {
@@ -341,7 +358,8 @@ void Runner::write_trace(const IterationRecord& r) {
   (void)n;
 }
 
-void Runner::run(StopFlag* stop, int64_t max_iterations) {
+void Runner::run(StopFlag* stop, int64_t max_iterations, Nanos start_delay) {
+  if (start_delay > 0 && !clock_->sleep(start_delay, stop)) return;
   arm();
   int64_t done = 0;
   while (!(stop && stop->stopped())) {
@@ -358,6 +376,17 @@ Nanos Runner::idle_ns() const {
   const Nanos waits = std::max(sqs_->api()->waiting_until(), scaler_->api()->waiting_until());
   last = std::max(last, std::min(waits, now));
   return now - last;
+}
+
+Nanos Runner::failing_ns() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (stats_.consecutive_failed_polls == 0) return 0;
+  return std::max<Nanos>(clock_->now() - stats_.last_good_ns, 0);
+}
+
+std::string Runner::last_error() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return last_error_;
 }
 
 RunnerStats Runner::stats() const {
@@ -414,15 +443,7 @@ bool read_thread_sched(ThreadSched* out) {
   return true;
 }
 
-Supervisor::Supervisor() {
-  const char* e = std::getenv("KSA_WORKER_FD_TABLE");
-  private_files_ = e && std::strcmp(e, "private") == 0;
-#if defined(__SANITIZE_THREAD__)
-  // ThreadSanitizer keys its file-descriptor sync objects by number, process-wide: the same
-  // number in two tables reads as a race on one descriptor. Its builds keep one table.
-  private_files_ = false;
-#endif
-}
+Supervisor::Supervisor() = default;
 
 HomeThread::HomeThread() {
   thread_ = std::thread([this] {
@@ -486,43 +507,34 @@ HomeThread::~HomeThread() {
   else if (thread_.joinable()) thread_.join();
 }
 
-HomeThread* Runner::home_thread(bool private_files) {
-  if (home_ && home_->private_files && !private_files) home_.reset();  // cannot rejoin the shared table
+HomeThread* Runner::home_thread() {
   if (!home_) home_ = std::make_unique<HomeThread>();
   return home_.get();
 }
 
 void Supervisor::start(int64_t max_iterations) {
-  bool private_files;
   {
     std::lock_guard<std::mutex> lk(mu_);
     running_ += runners_.size();
-    private_files = private_files_;
   }
+  const size_t n = runners_.size();
   // Posting waits for a task a runner's thread still runs, and that task's last step takes
   // mu_: so no lock is held from here on.
-  for (auto& r : runners_) {
-    Runner* rp = r.get();  // runners_ keeps it alive until join()
-    HomeThread* h = rp->home_thread(private_files);
-    // Between runs a runner's connections live on the shared table: a worker on a table of its
-    // own closes its sockets before its run ends, and the caller may have dialled since. Those
-    // are closed here, on a thread of the shared table, before a private worker runs.
-    if (private_files && h->private_files) rp->release_connections();
+  for (size_t i = 0; i < n; ++i) {
+    Runner* rp = runners_[i].get();  // runners_ keeps it alive until join()
+    HomeThread* h = rp->home_thread();
+    const Nanos period = std::max<Nanos>(rp->config().poll_period, 0);
+    const Nanos delay = stagger_ && n > 1 ? static_cast<Nanos>(static_cast<double>(period) * i / n) : 0;
     {
       std::lock_guard<std::mutex> lk(mu_);
       started_.push_back(h);
     }
-    h->post([this, rp, h, max_iterations, private_files] {
+    h->post([this, rp, h, max_iterations, delay] {
       if (rp->cpus().empty()) h->unpin();
       else pin_current_thread(rp->cpus());
-      if (private_files && !h->private_files) {
-        rp->release_connections();  // sockets opened so far belong to the shared table
-        h->private_files = ::unshare(CLONE_FILES) == 0;
-      }
       ThreadSched before, after;
       const bool have = read_thread_sched(&before);
-      rp->run(&stop_, max_iterations);
-      if (h->private_files) rp->release_connections();  // this table's sockets, closed on this thread
+      rp->run(&stop_, max_iterations, delay);
       const bool have_after = have && read_thread_sched(&after);
       std::lock_guard<std::mutex> g(mu_);
       if (have_after) sched_.add(after.since(before));

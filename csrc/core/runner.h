@@ -109,6 +109,10 @@ struct RunnerStats {
   int32_t last_replicas = -1;
   uint64_t latency_samples = 0;
   int64_t latency_sum_ns = 0;                 // over every sample (the ring keeps the latest)
+  // Readiness: polls in a row that failed to read the depth or to write the Deployment, and
+  // when the last poll that did neither ended (clock time; Run() entry before any poll).
+  uint64_t consecutive_failed_polls = 0;
+  Nanos last_good_ns = 0;
   uint64_t latency_buckets[kLatBuckets] = {};  // per bucket, not cumulative
 };
 
@@ -122,13 +126,14 @@ struct SharedWorkerState {
   enum Counter : int {
     kPolls, kDepthErrors, kScaleUps, kScaleDowns, kNoopUps, kNoopDowns, kCooldownSkipsUp,
     kCooldownSkipsDown, kFailedUps, kFailedDowns, kSpeculativeReads, kSpeculativeReadsUsed,
-    kSpeculativeReadsGated, kApiserverReads, kLatencySamples, kNumCounters
+    kSpeculativeReadsGated, kApiserverReads, kLatencySamples, kConsecutiveFailedPolls, kNumCounters
   };
   enum Control : int32_t { kWait = 0, kGo = 1, kStop = 2 };
   enum Status : int32_t { kStarting = 0, kReady = 1, kRunning = 2, kExited = 3, kFailed = 4 };
   static constexpr uint32_t kRing = 1 << 14;  // latency samples kept (the most recent)
   alignas(64) std::atomic<uint64_t> counters[kNumCounters];
   std::atomic<int64_t> progress_ns;  // CLOCK_MONOTONIC of the last progress (the worker process' heartbeat)
+  std::atomic<int64_t> last_good_ns;  // CLOCK_MONOTONIC of the last poll that did not fail
   std::atomic<int64_t> last_depth;
   std::atomic<int64_t> last_replicas;
   std::atomic<int64_t> lat_sum_ns;
@@ -160,9 +165,6 @@ class HomeThread {
   // Runs `task` on the thread (after the previous task, if one is still running).
   void post(std::function<void()> task);
   void wait_idle();
-  // Whether the thread has taken a file table of its own (unshare(CLONE_FILES)); set by the
-  // task that did it. Such a thread is never handed to a run that wants the shared table.
-  bool private_files = false;
   // Restores the CPU mask the thread started with (a run without explicit CPUs after a pinned one).
   void unpin();
 
@@ -200,7 +202,9 @@ class alignas(kCacheLine) Runner {
     scaler_->api()->close_connections();
   }
   // The reference's Run(): arm(), then step() until stopped (or max_iterations > 0 reached).
-  void run(StopFlag* stop, int64_t max_iterations = -1);
+  // start_delay > 0: wait that long first (interruptible by `stop`), then arm -- a staggered
+  // start, as if this queue's reference process had been launched that much later.
+  void run(StopFlag* stop, int64_t max_iterations = -1, Nanos start_delay = 0);
 
   RunnerStats stats() const;
   // Time since the loop last made progress (armed, or finished a poll) -- the liveness signal:
@@ -208,6 +212,12 @@ class alignas(kCacheLine) Runner {
   // A deliberate wait of its clients (Retry-After, back-off, throttle) counts as progress up
   // to its end: a worker correctly waiting out a server's Retry-After is not wedged.
   Nanos idle_ns() const;
+  // How long every poll has been failing (0 while the last poll succeeded): the time since the
+  // last poll that read the depth and wrote what it decided, or since Run() entry. The
+  // reference retries such a poll forever (main.go:44-47,57-60,71-74), so this is a readiness
+  // signal (/readyz), not a liveness one.
+  Nanos failing_ns() const;
+  std::string last_error() const;
   // Recent poll->patch latencies (ns), oldest first; bounded ring.
   std::vector<Nanos> latencies() const;
   void clear_latencies();
@@ -226,10 +236,8 @@ class alignas(kCacheLine) Runner {
   // Mirror the stats into `s` after every poll and follow its max-pods override (may be null).
   void set_shared_state(SharedWorkerState* s) { shared_ = s; }
   const CpuList& cpus() const { return cpus_; }
-  // This runner's HomeThread (created on first use). A thread that unshared its file table is
-  // retired when a run wants the shared one (`private_files` false), and vice versa the new
-  // thread unshares on its first private run.
-  HomeThread* home_thread(bool private_files);
+  // This runner's HomeThread (created on first use, kept for the runner's lifetime).
+  HomeThread* home_thread();
 
  private:
   IterationRecord poll_body();
@@ -257,6 +265,7 @@ class alignas(kCacheLine) Runner {
   mutable std::mutex mu_;
   std::atomic<Nanos> progress_ns_{0};
   RunnerStats stats_;
+  std::string last_error_;
   std::vector<Nanos> lat_ring_;
   size_t lat_pos_ = 0;
   static constexpr size_t kLatRing = 1 << 16;
@@ -307,18 +316,13 @@ class Supervisor {
  public:
   Supervisor();
   void add(std::shared_ptr<Runner> r) { runners_.push_back(std::move(r)); }
-  // Opt-in (KSA_WORKER_FD_TABLE=private): each worker thread runs on a file table of its own
-  // (unshare(CLONE_FILES)), as a process would. On a table shared by several threads every
-  // socket call takes and drops a reference on the socket's file (an atomic read-modify-write
-  // per call, and a busy-polled receive is many calls); on a private table the kernel skips
-  // that, as for a single-threaded process. A bare TCP echo (csrc/tools/loopback_probe.cc)
-  // loses its thread penalty this way; the autoscaler's 8-queue thread fleet gains 3-6 %
-  // (profiles/README.md, r02j), which --worker-processes beats, so it stays off by default:
-  // it makes every descriptor a worker opens invisible to the other threads. The worker owns
-  // its clients' connections for the run: they are closed on the shared table before it
-  // unshares and on its own table before it exits, so no socket number outlives its table.
-  void set_private_files(bool on) { private_files_ = on; }
-  bool private_files() const { return private_files_; }
+  // Staggered start (the Scheduler's default too): runner i of N arms its timers and starts its
+  // sleep-then-poll loop i/N of its poll period after start(), so N queues with one poll period
+  // do not poll in one burst every period -- as N reference processes launched a little apart
+  // would not. Per-queue decisions are unchanged: each queue's timers start at its own Run()
+  // entry (main.go:37-38), exactly as the reference's.
+  void set_stagger(bool on) { stagger_ = on; }
+  bool stagger() const { return stagger_; }
   // Runs every runner on its HomeThread (one thread per runner, kept across runs); each arms
   // its timers then loops.
   void start(int64_t max_iterations = -1);
@@ -352,7 +356,7 @@ class Supervisor {
   std::condition_variable cv_;
   size_t running_ = 0;
   ThreadSched sched_;
-  bool private_files_ = false;
+  bool stagger_ = false;
 };
 
 // JSON line of an iteration record (span trace format).

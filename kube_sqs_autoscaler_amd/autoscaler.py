@@ -21,6 +21,7 @@ from .config import Config, TargetConfig
 from .kube.config import RestConfig, build_config_from_flags
 from .ops import native
 from .sqs.credentials import make_chain_provider
+from .sqs.session import custom_ca_bundle
 from .utils import proxy
 from .utils.goflag import SECOND
 
@@ -196,9 +197,9 @@ def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query",
     o.proxy = proxy.select(endpoint or nat.HttpSqsApi.endpoint_for_region(region), env)
     if tls is not None:
         o.tls = tls
-    elif env.get("AWS_CA_BUNDLE"):  # aws-sdk-go v1 session: custom CA bundle for AWS endpoints
+    elif custom_ca_bundle(env):  # aws-sdk-go v1 session: custom CA bundle for AWS endpoints
         t = nat.TlsOptions()
-        t.ca_file = env["AWS_CA_BUNDLE"]
+        t.ca_file = custom_ca_bundle(env)
         o.tls = t
     creds = credentials if credentials is not None else make_chain_provider(environ=environ, region=region)
     return nat.HttpSqsApi(o, creds, clock)

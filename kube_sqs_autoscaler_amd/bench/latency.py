@@ -3,8 +3,8 @@
 BASELINE.json's metric is the p50 of the time from the end of the poll sleep to the end of the
 replica write (``Runner`` records it per iteration, csrc/core/runner.cc), at 1/2/4/8
 concurrently tracked queues. Every tracked queue gets its own native worker thread, its own
-persistent connections and its own Deployment; all of them share one fake SQS endpoint and one
-fake apiserver (as production shares AWS and the apiserver).
+persistent connections and its own Deployment (``BenchEnv`` documents where the fake endpoints
+run).
 
 The wire path is the production one: SigV4-signed ``GetQueueAttributes`` (verified by the
 fake), bearer-token kube REST calls with resourceVersion preconditions, real attribute summing
@@ -15,9 +15,10 @@ Deployment GET overlaps the SQS call) and the reference-equivalent one (full-obj
 strictly sequential -- what /root/reference/scale/scale.go:54-107 does after sqs.go:51).
 
 Trace: the fake serves the BASELINE.json "step trace" 200 -> 0 -> 200 ... one value per poll,
-with scale-up-messages=100 / scale-down-messages=10, min 1 / max 8 and zero poll period and
-cool-downs, so *every* iteration performs SQS + GET + write (the 3-round-trip scaling path of
-SURVEY.md §3.2) -- the path whose latency the metric names.
+with scale-up-messages=100 / scale-down-messages=10, min 1 / max 8 and zero cool-downs, so
+*every* iteration performs SQS + GET + write (the 3-round-trip scaling path of SURVEY.md §3.2)
+-- the path whose latency the metric names. ``measure`` polls back to back (the hot loop);
+``measure_cadenced`` polls at a production ``--poll-period``.
 """
 from __future__ import annotations
 
@@ -172,94 +173,61 @@ class BenchEnv:
     """Fake servers + one worker per queue.
 
     ``servers``: ``shared`` -- one fake SQS + apiserver pair in this process for every queue;
-    ``per-queue`` -- one pair per queue, in this process; ``process`` -- one pair per queue in a
-    separate endpoint process (as production's remote endpoints); ``processes`` -- one endpoint
-    process per queue (as separate ranks see it: no two queues' endpoint threads share a process).
+    ``per-queue`` -- one pair per queue, in this process; ``process`` -- one pair serving every
+    queue, in an endpoint process of its own (production's shape: every queue talks to the same
+    SQS endpoint and apiserver, which are other machines' processes); ``processes`` -- one
+    endpoint process per queue (as separate ranks see it: no two queues' endpoint threads share
+    a process).
 
-    ``affinity``: ``none`` -- threads float; ``llc`` -- queue q's worker thread and its fake
-    endpoint pair are pinned to L3 domain q mod D (utils/topology.py), so each queue's traffic
-    stays on one CCD, as a rank per queue would (needs per-queue or process servers).
-
-    Layout probes (profiles/README.md r02l): ``build_on_threads`` builds each queue's objects on a
-    thread of its own (separate malloc arenas); ``clock_per_queue`` gives each queue its own
-    clock object instead of one shared ``RealClock``."""
+    ``poll_period_ns``: every queue's ``--poll-period`` (0: back to back, the hot loop);
+    ``stagger``: queue i of N starts i/N of a poll period late (Supervisor.stagger), so N
+    queues at one cadence do not poll in one burst."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
-                 busy_poll_ns: int = 0, servers: str = "shared", loggers: str = "shared", affinity: str = "none",
-                 log_level: str = "info", sqs_protocol: str = "query", build_on_threads: bool = False,
-                 clock_per_queue: bool = False):
+                 busy_poll_ns: int = 0, servers: str = "shared", log_level: str = "info", sqs_protocol: str = "query",
+                 poll_period_ns: int = 0, stagger: bool = False):
         nat = native()
         self.nat = nat
         self.mode = mode
         self.pipeline = pipeline
-        n_servers = 1 if servers == "shared" else queues
+        self.stagger = stagger
+        n_servers = queues if servers in ("per-queue", "processes") else 1
         self.remote = None
-        cpus = worker_cpus = None
-        if affinity == "llc":
-            from ..utils.topology import plan
-
-            cpus = worker_cpus = plan(queues)
-            if servers == "shared" and queues > 1:
-                raise ValueError("affinity=llc needs per-queue or process servers")
-        elif affinity == "ccd":
-            from ..utils.topology import plan_queue_ccds
-
-            if servers == "shared" and queues > 1:
-                raise ValueError("affinity=ccd needs per-queue or process servers")
-            worker_cpus, cpus = plan_queue_ccds(queues)
-        elif affinity.startswith("{"):
-            # explicit placement (probes): {"workers": [[cpu, ...] per queue], "servers": [...]}
-            import json
-
-            spec = json.loads(affinity)
-            worker_cpus, cpus = spec.get("workers"), spec.get("servers")
-        elif affinity != "none":
-            raise ValueError(f"affinity must be none, llc, ccd or a JSON placement, not {affinity!r}")
-        self.cpus = cpus
         self.remotes = []
         if servers == "process":
-            self.remote = RemoteEndpoints(queues, n_servers, tls, sqs_latency_ns, kube_latency_ns, cpus)
+            self.remote = RemoteEndpoints(queues, 1, tls, sqs_latency_ns, kube_latency_ns)
             self.remotes = [self.remote]
             self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
         elif servers == "processes":
-            self.remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns,
-                                            [cpus[q]] if cpus is not None else None, offset=q) for q in range(queues)]
+            self.remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns, offset=q) for q in range(queues)]
             self.remote = self.remotes[0]
             self.sqs_servers = [r.sqs[0] for r in self.remotes]
             self.kube_servers = [r.kube[0] for r in self.remotes]
         elif servers in ("shared", "per-queue"):
             self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
-                                                                       kube_latency_ns, cpus)
+                                                                       kube_latency_ns)
         else:
             raise ValueError(f"servers must be shared, per-queue, process or processes, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
         self.clock = nat.RealClock()
-        # loggers="per-queue": a logger and an open file of its own per queue (as one process
-        # per queue has); "shared": one logger writing to one file, like the reference's global
+        # one logger writing to one file, like the reference's global logrus logger
         self._devnulls = []
-        self.loggers = []
-        for _ in range(queues if loggers == "per-queue" else 1):
-            fd = log_fd
-            if fd is None:
-                fd = os.open(os.devnull, os.O_WRONLY)
-                self._devnulls.append(fd)
-            lg = nat.Logger()
-            lg.set_sink_fd(fd)
-            lg.set_level(log_level)
-            self.loggers.append(lg)
-        self.log = self.loggers[0]
+        fd = log_fd
+        if fd is None:
+            fd = os.open(os.devnull, os.O_WRONLY)
+            self._devnulls.append(fd)
+        self.log = nat.Logger()
+        self.log.set_sink_fd(fd)
+        self.log.set_level(log_level)
         creds = static_provider(AKID, SECRET)
         self.runners = []
         self.kube_apis, self.sqs_apis = [], []
         self.targets = []
         self.server_of = []  # queue -> index of the server pair that serves it
-        built = [None] * queues
-
-        def build(q):
+        for q in range(queues):
             si = q % n_servers
-            sqs, kube, log = self.sqs_servers[si], self.kube_servers[si], self.loggers[q % len(self.loggers)]
-            clock = nat.RealClock() if clock_per_queue else self.clock
+            sqs, kube = self.sqs_servers[si], self.kube_servers[si]
             rest = RestConfig(host=kube.url, bearer_token=TOKEN, insecure=tls)
             sqs_tls = None
             if tls:
@@ -267,57 +235,30 @@ class BenchEnv:
                 sqs_tls.ca_pem = sqs.cert_pem
                 rest.insecure = False
                 rest.ca_pem = kube.cert_pem
-            url = queue_url(sqs.url, q)
-            name = deployment_name(q)
-            t = TargetConfig(queue_url=url, deployment=name, namespace="bench", poll_period_ns=0,
-                             scale_up_cool_down_ns=0, scale_down_cool_down_ns=0, scale_up_messages=100,
-                             scale_down_messages=10, max_pods=8, min_pods=1)
-            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, clock, busy_poll_ns=busy_poll_ns)
-            scaler = new_pod_autoscaler(t, kube_api, log, clock)
-            sqs_api = new_sqs_api(REGION, clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds, tls=sqs_tls,
-                                  busy_poll_ns=busy_poll_ns)
-            client = new_sqs_client(t, sqs_api)
+            t = TargetConfig(queue_url=queue_url(sqs.url, q), deployment=deployment_name(q), namespace="bench",
+                             poll_period_ns=poll_period_ns, scale_up_cool_down_ns=0, scale_down_cool_down_ns=0,
+                             scale_up_messages=100, scale_down_messages=10, max_pods=8, min_pods=1)
+            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=busy_poll_ns)
+            scaler = new_pod_autoscaler(t, kube_api, self.log, self.clock)
+            sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds,
+                                  tls=sqs_tls, busy_poll_ns=busy_poll_ns)
             cfg = nat.LoopConfig()
-            cfg.poll_period_ns = 0
+            cfg.poll_period_ns = poll_period_ns
             cfg.scale_up_cool_down_ns = 0
             cfg.scale_down_cool_down_ns = 0
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
-            runner = nat.Runner(cfg, client, scaler, clock, log)
-            if worker_cpus is not None:
-                runner.cpus = worker_cpus[q]
-            built[q] = (si, kube_api, sqs_api, runner, t)
-
-        if build_on_threads and queues > 1:
-            # each queue's objects built on a thread of its own, all alive together, so every
-            # queue's heap allocations come from a separate malloc arena (scripts/arena_probe.py)
-            import threading
-
-            done = threading.Barrier(queues)
-
-            def build_on_thread(q):
-                build(q)
-                done.wait()
-
-            ts = [threading.Thread(target=build_on_thread, args=(q,)) for q in range(queues)]
-            for th in ts:
-                th.start()
-            for th in ts:
-                th.join()
-        else:
-            for q in range(queues):
-                build(q)
-        for si, kube_api, sqs_api, runner, t in built:
             self.server_of.append(si)
             self.kube_apis.append(kube_api)
             self.sqs_apis.append(sqs_api)
-            self.runners.append(runner)
+            self.runners.append(nat.Runner(cfg, new_sqs_client(t, sqs_api), scaler, self.clock, self.log))
             self.targets.append(t)
 
     def run(self, iterations: int) -> float:
         """All workers run ``iterations`` polls concurrently; returns wall seconds."""
         sup = self.nat.Supervisor()
+        sup.stagger = self.stagger
         for r in self.runners:
             sup.add(r)
         t0 = time.perf_counter()
@@ -397,21 +338,14 @@ def phase_breakdown(steps: int = 2000, warmup: int = 200, **kw) -> Dict[str, flo
 
 def measure_processes(queues: int, steps: int, warmup: int, mode: str = "scale", tls: bool = False,
                       pipeline: bool = True, busy_poll_ns: int = 0, sqs_latency_ns: int = 0, kube_latency_ns: int = 0,
-                      affinity: str = "none", log_level: str = "info", **_ignored) -> LatencyResult:
+                      log_level: str = "info", **_ignored) -> LatencyResult:
     """``measure`` with every queue in a worker process of its own (``--worker-processes``,
     parallel/procfleet.py) against one endpoint process per queue. Each worker runs
     ``warmup + steps`` polls back to back and the last ``steps`` latencies of each are kept."""
     from ..parallel.procfleet import ProcessFleet
 
     nat = native()
-    worker_cpus = endpoint_cpus = None
-    if affinity == "ccd":
-        from ..utils.topology import plan_queue_ccds
-
-        worker_cpus, endpoint_cpus = plan_queue_ccds(queues)
-    remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns,
-                               [endpoint_cpus[q]] if endpoint_cpus is not None else None, offset=q)
-               for q in range(queues)]
+    remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns, offset=q) for q in range(queues)]
     creds = static_provider(AKID, SECRET)
     targets = []
     for q in range(queues):
@@ -452,7 +386,7 @@ def measure_processes(queues: int, steps: int, warmup: int, mode: str = "scale",
 
     fleet = None
     try:
-        fleet = ProcessFleet([build(q) for q in range(queues)], targets, worker_cpus)
+        fleet = ProcessFleet([build(q) for q in range(queues)], targets)
         fleet.wait_ready()
         t0 = time.perf_counter()
         fleet.start(warmup + steps)
@@ -496,146 +430,66 @@ def measure(queues: int, steps: int, warmup: int, mode: str = "scale", workers: 
         env.close()
 
 
-# ---------------------------------------------------------------------------------------------
-# Where does multi-queue latency go? Scheduler and kernel evidence around a measurement.
+def _pct_ns(v: List[int], p: float) -> int:
+    import math
+
+    v = sorted(v)
+    k = max(1, math.ceil(p / 100.0 * len(v)))
+    return v[min(k, len(v)) - 1]
 
 
-def _task_stats(pid: int) -> Dict[str, Dict[str, int]]:
-    """Per thread name (``ksa-worker``, ``ksa-serve``, ...): CPU time, run-queue wait and
-    timeslices from /proc/<pid>/task/*/schedstat, and context switches from .../status."""
-    out: Dict[str, Dict[str, int]] = {}
-    base = f"/proc/{pid}/task"
-    try:
-        tids = os.listdir(base)
-    except OSError:
-        return out
-    for tid in tids:
-        try:
-            with open(f"{base}/{tid}/comm") as f:
-                comm = f.read().strip()
-            with open(f"{base}/{tid}/schedstat") as f:
-                cpu, wait, slices = (int(x) for x in f.read().split()[:3])
-            vol = invol = 0
-            with open(f"{base}/{tid}/status") as f:
-                for line in f:
-                    if line.startswith("voluntary_ctxt_switches"):
-                        vol = int(line.split()[1])
-                    elif line.startswith("nonvoluntary_ctxt_switches"):
-                        invol = int(line.split()[1])
-        except (OSError, ValueError):
-            continue
-        d = out.setdefault(comm, {"threads": 0, "cpu_ns": 0, "runq_wait_ns": 0, "slices": 0, "vol_cs": 0,
-                                  "invol_cs": 0})
-        d["threads"] += 1
-        d["cpu_ns"] += cpu
-        d["runq_wait_ns"] += wait
-        d["slices"] += slices
-        d["vol_cs"] += vol
-        d["invol_cs"] += invol
-    return out
+def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: str = "scale", pipeline: bool = True,
+                     busy_poll_ns: int = 0, tls: bool = False, skip: int = 2, servers: str = "process") -> Dict:
+    """Poll -> patch latency at a production poll cadence, not back to back.
 
-
-def _system_stats() -> Dict[str, int]:
-    """cgroup v2 CPU throttling and the machine's TLB-shootdown IPIs (best effort)."""
-    out: Dict[str, int] = {}
-    for path in ("/sys/fs/cgroup/cpu.stat",):
-        try:
-            with open(path) as f:
-                for line in f:
-                    k, v = line.split()
-                    if k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec"):
-                        out[k] = int(v)
-        except (OSError, ValueError):
-            pass
-    try:
-        with open("/proc/interrupts") as f:
-            for line in f:
-                name = line.split(":", 1)[0].strip()
-                if name in ("TLB", "RES", "CAL"):
-                    out[f"irq_{name}"] = sum(int(x) for x in line.split(":", 1)[1].split() if x.isdigit())
-    except OSError:
-        pass
-    return out
-
-
-def _delta(after, before):
-    if isinstance(after, dict):
-        return {k: _delta(v, before.get(k, 0 if not isinstance(v, dict) else {})) for k, v in after.items()}
-    return after - before
-
-
-def measure_detailed(queues: int, steps: int, warmup: int, mode: str = "scale", sync=None, **kw) -> Dict:
-    """``measure`` plus, for the timed run: per-phase medians over all queues' spans, and the
-    scheduler view of every thread group (this process and the endpoint process) per poll.
-    ``sync``: called after the warm-up, right before the timed run (a barrier across ranks)."""
+    The reference sleeps ``--poll-period`` (5 s by default) before every poll
+    (/root/reference/main.go:41,83). Between polls the worker thread is asleep, its caches and
+    branch predictors are cold, the CPU may sit in a deep idle state, and a keep-alive
+    connection unused for longer than ``kFreshConnNs`` gets the idle-close check again. The
+    hot-loop rows measure none of that. Here ``queues`` queues (the default fleet: a thread
+    each, staggered over the period) each run ``polls`` polls at ``poll_period_ns`` against
+    one endpoint process that serves them all; every poll scales (the 200/0 trace, zero
+    cool-downs). The first ``skip`` polls of each queue (dial, TLS handshake, first
+    allocations) are dropped. Phases come from the per-poll spans (``--trace-file`` format).
+    """
     import json
     import statistics
     import tempfile
 
-    env = BenchEnv(queues, mode, **kw)
+    env = BenchEnv(queues, mode, tls=tls, pipeline=pipeline, busy_poll_ns=busy_poll_ns, servers=servers,
+                   poll_period_ns=poll_period_ns, stagger=True)
+    files = [tempfile.TemporaryFile() for _ in env.runners]
+    spans: List[dict] = []
     try:
-        if warmup:
-            env.run(warmup)
-        env.clear()
-        if sync is not None:
-            sync()
-        pids = {"autoscaler": os.getpid()}
-        for i, rem in enumerate(env.remotes):
-            pids[f"endpoints{i}" if len(env.remotes) > 1 else "endpoints"] = rem.pid
-        # one span file per worker: a shared one would serialise the workers on its file
-        # position lock and perturb what is measured
-        files = [tempfile.TemporaryFile() for _ in env.runners]
-        try:
-            for r, f in zip(env.runners, files):
-                r.set_trace_fd(f.fileno())
-            t_before = {k: _task_stats(p) for k, p in pids.items()}
-            s_before = _system_stats()
-            wall = env.run(steps)
-            s_after = _system_stats()
-            t_after = {k: _task_stats(p) for k, p in pids.items()}
-            spans = []
-            for r, f in zip(env.runners, files):
-                r.set_trace_fd(-1)
-                f.seek(0)
-                spans += [json.loads(line) for line in f.read().decode().splitlines()]
-        finally:
-            for f in files:
-                f.close()
-        res = env.collect(steps, wall)
+        for r, f in zip(env.runners, files):
+            r.set_trace_fd(f.fileno())
+        wall = env.run(polls)
+        for r, f in zip(env.runners, files):
+            r.set_trace_fd(-1)
+            f.seek(0)
+            spans += [json.loads(line) for line in f.read().decode().splitlines()][skip:]
+        res = env.collect(polls, wall)
     finally:
+        for f in files:
+            f.close()
         env.close()
-    polls = max(1, queues * steps)
-    med = lambda k: round(statistics.median(s[k] for s in spans) / 1e3, 2)
-    sched = {}
-    for proc, groups in t_after.items():
-        for comm, d in groups.items():
-            b = t_before[proc].get(comm, {})
-            dd = _delta(d, b)
-            sched[f"{proc}/{comm}"] = {
-                "threads": d["threads"],
-                "cpu_us_per_poll": round(dd["cpu_ns"] / polls / 1e3, 2),
-                "runq_wait_us_per_poll": round(dd["runq_wait_ns"] / polls / 1e3, 3),
-                "slices_per_poll": round(dd["slices"] / polls, 3),
-                "vol_cs_per_poll": round(dd["vol_cs"] / polls, 3),
-                "invol_cs_per_poll": round(dd["invol_cs"] / polls, 4),
-            }
-    w = env.last_thread_sched
-    sched["autoscaler/ksa-worker"] = {
-        "threads": w["threads"],
-        "cpu_us_per_poll": round(w["cpu_ns"] / polls / 1e3, 2),
-        "runq_wait_us_per_poll": round(w["runq_wait_ns"] / polls / 1e3, 3),
-        "slices_per_poll": round(w["slices"] / polls, 3),
-        "vol_cs_per_poll": round(w["vol_cs"] / polls, 3),
-        "invol_cs_per_poll": round(w["invol_cs"] / polls, 4),
-        "user_us_per_poll": round(w["utime_ns"] / polls / 1e3, 2),
-        "sys_us_per_poll": round(w["stime_ns"] / polls / 1e3, 2),
-        "minflt_per_poll": round(w["minflt"] / polls, 4),
+    lat = [s["patch_latency_ns"] for s in spans if s["patch_latency_ns"] >= 0]
+    scaled = [s for s in spans if s["patch_latency_ns"] >= 0]
+    med = (lambda k: round(statistics.median(s[k] for s in scaled) / 1e3, 2)) if scaled else (lambda k: None)
+    return {
+        "poll_period_ms": poll_period_ns / 1e6,
+        "queues": queues,
+        "mode": mode,
+        "pipeline_reads": pipeline,
+        "tls": tls,
+        "p50_ms": round(_pct_ns(lat, 50) / 1e6, 4) if lat else None,
+        "p90_ms": round(_pct_ns(lat, 90) / 1e6, 4) if lat else None,
+        "p99_ms": round(_pct_ns(lat, 99) / 1e6, 4) if lat else None,
+        "samples": len(lat),
+        "polls": len(spans),
+        "errors": sum(1 for s in spans if "error" in s),
+        "signature_failures": res.signature_failures,
+        "phase_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
+                            "patch_us": med("patch_latency_ns")},
+        "wall_s": round(wall, 2),
     }
-    sysd = _delta(s_after, s_before)
-    return {"queues": queues, "mode": mode,
-            **{k: v for k, v in kw.items() if k in ("servers", "pipeline", "busy_poll_ns", "affinity", "loggers",
-                                                    "log_level")},
-            "summary": res.summary(), "signature_failures": res.signature_failures,
-            "phases_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
-                                 "patch_us": med("patch_latency_ns")},
-            "sched": sched, "system": sysd, "wall_s": round(wall, 4)}

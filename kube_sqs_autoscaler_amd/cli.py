@@ -1,7 +1,8 @@
 """Process entry point: ``python -m kube_sqs_autoscaler_amd [flags]`` (the reference's ``main``).
 
 /root/reference/main.go:82-116: parse flags -> ``NewPodAutoScaler`` (panics when no kube config
-can be built, scale.go:35) -> attribute list -> ``NewSqsClient`` -> log
+can be built, scale.go:35) -> attribute list -> ``NewSqsClient`` (panics when the AWS session's
+configuration is invalid, ``session.Must``, sqs.go:36; sqs/session.py) -> log
 ``Starting kube-sqs-autoscaler`` -> ``Run`` forever. Exit codes follow Go: 2 for a flag error
 (after printing the message and usage), 0 for ``-h``/``-help``, 2 for a start-up panic.
 Extensions: several ``--queue`` targets, SIGTERM/SIGINT graceful stop (exit 0), optional
@@ -18,6 +19,7 @@ from typing import List, Mapping, Optional
 from . import autoscaler
 from .config import MI355X_MAX_PODS, REFERENCE_MAX_PODS, config_from_flags, new_flag_set
 from .kube.config import KubeConfigError
+from .sqs.session import SessionError, validate_session
 from .utils.goflag import FlagError
 from .utils.log import make_logger
 
@@ -71,6 +73,12 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         return _panic("Failed to configure client", str(e))
     if w:
         log.log("warning", w)
+    # kubesqs.NewSqsClient -> sqs.New(session.Must(session.NewSession()), ...) (sqs/sqs.go:36):
+    # the session's configuration is checked now; credentials are still fetched on first use.
+    try:
+        validate_session(env)
+    except SessionError as e:
+        return _panic(str(e))
 
     if not fs.was_set("max-pods"):
         # the one default that differs from the reference (main.go:90: 5)
@@ -129,7 +137,7 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         from .metrics import Health, MetricsServer
 
         health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets],
-                        leader_elect=cfg.leader_elect)
+                        leader_elect=cfg.leader_elect, failure_window_ns=cfg.readiness_failure_window_ns)
         metrics = MetricsServer(fleet, cfg.metrics_addr, health)
         metrics.start()
         log.log("info", f"Serving metrics on {cfg.metrics_addr}")

@@ -31,7 +31,8 @@ Extensions (all off or reference-equivalent by default):
 * ``--worker-processes``: one worker process per tracked queue (parallel/procfleet.py) instead
   of one thread per queue.
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
-  ``--log-format``, ``--metrics-addr``, ``--trace-file``, ``--gpu-aware-max``.
+  ``--log-format``, ``--metrics-addr`` (+ ``--readiness-failure-window``), ``--trace-file``,
+  ``--gpu-aware-max``.
 * ``--leader-elect`` (+ lease name/namespace/identity/timings): Lease-based leader election so
   several replicas can run (the reference must run exactly one, README.md:27).
 """
@@ -110,6 +111,7 @@ class Config:
     leader_elect_lease_duration_ns: int = 15 * SECOND
     leader_elect_renew_deadline_ns: int = 10 * SECOND
     leader_elect_retry_period_ns: int = 2 * SECOND
+    readiness_failure_window_ns: int = 300 * SECOND
 
 
 # Go's unicode.IsSpace set, which strings.TrimSpace strips: ASCII \t \n \v \f \r and space,
@@ -172,6 +174,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
     fs.string("trace-file", "", "Append one JSON span per poll (depth, decisions, per-call latencies) to this file; empty disables")
     fs.string("metrics-addr", "", "Serve Prometheus metrics and /healthz on host:port (disabled when empty)")
+    fs.duration("readiness-failure-window", 300 * SECOND, "/readyz fails while every poll of a tracked queue has failed (to read the queue depth or to write the Deployment) for this long; 0s disables")
     fs.bool("leader-elect", False, "Run several replicas safely: only the holder of a coordination.k8s.io Lease scales")
     fs.string("leader-elect-lease-name", "kube-sqs-autoscaler", "Name of the leader-election Lease")
     fs.string("leader-elect-namespace", "", "Namespace of the leader-election Lease (default: --kubernetes-namespace)")
@@ -296,6 +299,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         leader_elect_lease_duration_ns=fs["leader-elect-lease-duration"],
         leader_elect_renew_deadline_ns=fs["leader-elect-renew-deadline"],
         leader_elect_retry_period_ns=fs["leader-elect-retry-period"],
+        readiness_failure_window_ns=fs["readiness-failure-window"],
     )
     if cfg.scale_mode not in SCALE_MODES:
         raise FlagError(f'invalid value "{cfg.scale_mode}" for flag -scale-mode: must be one of {", ".join(SCALE_MODES)}')

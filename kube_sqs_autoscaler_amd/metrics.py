@@ -1,20 +1,19 @@
 """Prometheus metrics + health endpoints (extension; the reference has none).
 
 Pull model: nothing runs per poll on the Python side. On each scrape the collector reads the
-native per-worker counters (``Runner.stats()``) and the latency ring (``Runner.latencies()``),
-so the control loop never takes the GIL for observability.
+native per-worker counters (``Runner.stats()``), so the control loop never takes the GIL for
+observability. The text exposition format (0.0.4) is written here with the standard library
+only: the slim image ships Python, PyYAML and nothing else (Dockerfile).
 
 Endpoints on ``--metrics-addr``: ``/metrics`` (Prometheus text format), ``/healthz`` and
 ``/readyz`` (see :class:`Health`).
 """
 from __future__ import annotations
 
+import math
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Optional, Sequence, Tuple
-
-from prometheus_client import CollectorRegistry, generate_latest
-from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily, SummaryMetricFamily
+from typing import List, Optional, Sequence, Tuple
 
 from .ops import native
 from .parallel.fleet import Fleet
@@ -66,45 +65,86 @@ def _client_stats(client) -> dict:
         return {}
 
 
-class FleetCollector:
-    def __init__(self, fleet: Fleet) -> None:
-        self.fleet = fleet
+def _num(v: float) -> str:
+    """Sample values and ``le`` bounds as the Prometheus client libraries write them."""
+    v = float(v)
+    if math.isinf(v):
+        return "+Inf" if v > 0 else "-Inf"
+    if math.isnan(v):
+        return "NaN"
+    return repr(v)
 
-    def collect(self):
-        labels = ["deployment", "queue"]
+
+def _label(v: str) -> str:
+    return str(v).replace("\\", "\\\\").replace("\n", "\\n").replace('"', '\\"')
+
+
+class _Family:
+    """One metric family of the text exposition: HELP, TYPE, then its samples."""
+
+    def __init__(self, name: str, kind: str, help_text: str) -> None:
+        self.name, self.kind, self.help = name, kind, help_text
+        self.samples: List[Tuple[str, List[Tuple[str, str]], float]] = []
+
+    def add(self, suffix: str, labels: List[Tuple[str, str]], value: float) -> None:
+        self.samples.append((suffix, labels, value))
+
+    def render(self, out: List[str]) -> None:
+        out.append(f"# HELP {self.name} {self.help.replace(chr(92), chr(92) * 2).replace(chr(10), chr(92) + 'n')}")
+        out.append(f"# TYPE {self.name} {self.kind}")
+        for suffix, labels, value in self.samples:
+            lv = ",".join(f'{k}="{_label(v)}"' for k, v in sorted(labels))
+            out.append(f"{self.name}{suffix}{{{lv}}} {_num(value)}" if lv else f"{self.name}{suffix} {_num(value)}")
+
+
+class FleetCollector:
+    def __init__(self, fleet: Fleet, health: Optional["Health"] = None) -> None:
+        self.fleet = fleet
+        self.health = health
+
+    def families(self) -> List[_Family]:
         stats = self.fleet.stats()
-        fams = {k: CounterMetricFamily(f"ksa_{k}", h, labels=labels) for k, h in _COUNTERS}
-        depth = GaugeMetricFamily("ksa_queue_depth", "Last observed queue depth (sum of attributes)", labels=labels)
-        reps = GaugeMetricFamily("ksa_replicas", "Last observed Deployment replicas", labels=labels)
-        lat = SummaryMetricFamily("ksa_poll_to_patch_seconds", "Poll start -> replica write acknowledged", labels=labels)
-        hist = HistogramMetricFamily("ksa_poll_to_patch_latency_seconds",
-                                     "Poll start -> replica write acknowledged, per scaling poll", labels=labels)
-        bounds = [b / 1e9 for b in native().latency_bucket_le_ns]
-        api = {k: CounterMetricFamily(f"ksa_{k}", h, labels=labels) for k, h, _, _ in _API_COUNTERS}
+        fams = {k: _Family(f"ksa_{k}_total", "counter", h) for k, h in _COUNTERS}
+        api = {k: _Family(f"ksa_{k}_total", "counter", h) for k, h, _, _ in _API_COUNTERS}
+        depth = _Family("ksa_queue_depth", "gauge", "Last observed queue depth (sum of attributes)")
+        reps = _Family("ksa_replicas", "gauge", "Last observed Deployment replicas")
+        failing = _Family("ksa_consecutive_failed_polls", "gauge",
+                          "Polls in a row that failed to read the queue depth or to write the Deployment")
+        failing_s = _Family("ksa_failing_seconds", "gauge",
+                            "How long every poll has been failing (0 after a successful poll)")
+        lat = _Family("ksa_poll_to_patch_seconds", "summary", "Poll start -> replica write acknowledged")
+        hist = _Family("ksa_poll_to_patch_latency_seconds", "histogram",
+                       "Poll start -> replica write acknowledged, per scaling poll")
+        bounds = [b / 1e9 for b in native().latency_bucket_le_ns] + [math.inf]
         for w, s in zip(self.fleet.workers, stats):
-            lv = [s["deployment"], s["queue"]]
+            lv = [("deployment", s["deployment"]), ("queue", s["queue"])]
             for k, _ in _COUNTERS:
-                fams[k].add_metric(lv, s[k])
+                fams[k].add("", lv, s[k])
             clients = {a: _client_stats(getattr(w, a, None)) for a in ("kube_api", "sqs_api")}
             for k, _, attr, key in _API_COUNTERS:
                 if key in clients[attr]:
                     v = clients[attr][key]
-                    api[k].add_metric(lv, v / 1e9 if key in _NS_COUNTERS else v)
-            depth.add_metric(lv, s["last_depth"])
-            reps.add_metric(lv, s["last_replicas"])
+                    api[k].add("", lv, v / 1e9 if key in _NS_COUNTERS else v)
+            depth.add("", lv, s["last_depth"])
+            reps.add("", lv, s["last_replicas"])
+            failing.add("", lv, s.get("consecutive_failed_polls", 0))
+            failing_s.add("", lv, w.runner.failing_ns() / 1e9)
             # every sample since start (the latency ring only keeps the latest)
-            lat.add_metric(lv, count_value=s["latency_samples"], sum_value=s["latency_sum_ns"] / 1e9)
-            cum, buckets = 0, []
-            for le, n in zip(bounds + [float("inf")], s["latency_buckets"]):
+            lat.add("_count", lv, s["latency_samples"])
+            lat.add("_sum", lv, s["latency_sum_ns"] / 1e9)
+            cum = 0
+            for le, n in zip(bounds, s["latency_buckets"]):
                 cum += n
-                buckets.append(("+Inf" if le == float("inf") else repr(le), cum))
-            hist.add_metric(lv, buckets, sum_value=s["latency_sum_ns"] / 1e9)
-        yield from fams.values()
-        yield from (f for f in api.values() if f.samples)
-        yield depth
-        yield reps
-        yield lat
-        yield hist
+                hist.add("_bucket", lv + [("le", _num(le))], cum)
+            hist.add("_count", lv, cum)
+            hist.add("_sum", lv, s["latency_sum_ns"] / 1e9)
+        return [*fams.values(), *(f for f in api.values() if f.samples), depth, reps, failing, failing_s, lat, hist]
+
+    def exposition(self) -> bytes:
+        out: List[str] = []
+        for f in self.families():
+            f.render(out)
+        return ("\n".join(out) + "\n").encode()
 
 
 class Health:
@@ -119,15 +159,23 @@ class Health:
       worker stuck past all of them is wedged, and a restart (Kubernetes' liveness probe) is the
       recovery. The reference has no probes and hangs on a stalled call.
     * ``/readyz`` is OK for a standby replica under ``--leader-elect``, since waiting for the
-      lease is its healthy state. Otherwise it is OK once every worker has completed a poll.
-      A standby that never became ready would stall every rolling update of a 2-replica
-      Deployment.
+      lease is its healthy state. Otherwise it is OK once every worker has completed a poll,
+      and fails again while a worker's every poll has failed -- to read the queue depth or to
+      write the Deployment -- for ``failure_window_ns`` (``--readiness-failure-window``, 5 min;
+      0 disables). A pod that can never read its queue or write its Deployment (a wrong IAM
+      role, a Role without ``update``) then shows NotReady instead of healthy forever; one
+      good poll makes it ready again. Liveness stays as it is: like the reference, the loop
+      retries such a poll forever (main.go:44-47,57-60,71-74), and a restart would not fix a
+      permission. A standby that never became ready would stall every rolling update of a
+      2-replica Deployment.
     """
 
-    def __init__(self, fleet: Fleet, stale_after_ns: Optional[Sequence[int]] = None, leader_elect: bool = False) -> None:
+    def __init__(self, fleet: Fleet, stale_after_ns: Optional[Sequence[int]] = None, leader_elect: bool = False,
+                 failure_window_ns: int = 300 * 10**9) -> None:
         self.fleet = fleet
         self.stale_after_ns = list(stale_after_ns) if stale_after_ns is not None else None
         self.role = "standby" if leader_elect else "active"
+        self.failure_window_ns = failure_window_ns
 
     @staticmethod
     def budget_ns(poll_period_ns: int, api_timeout_ns: int) -> int:
@@ -155,6 +203,14 @@ class Health:
             return False, why
         if not all(s["polls"] > 0 for s in self.fleet.stats()):
             return False, "waiting for first poll"
+        if self.failure_window_ns > 0:
+            for w in self.fleet.workers:
+                failing = w.runner.failing_ns()
+                if failing >= self.failure_window_ns:
+                    n = w.runner.stats().get("consecutive_failed_polls", 0)
+                    err = w.runner.last_error()
+                    return False, (f"worker {w.target.name}: every poll failed for {failing / 1e9:.0f}s ({n} polls)"
+                                   + (f"; last error: {err}" if err else ""))
         return True, "ok"
 
 
@@ -168,14 +224,13 @@ class MetricsServer:
         self.fleet = fleet
         self.health = health or Health(fleet)
         hl = self.health
-        self.registry = CollectorRegistry()
-        self.registry.register(FleetCollector(fleet))
-        reg = self.registry
+        self.collector = FleetCollector(fleet)
+        coll = self.collector
 
         class Handler(BaseHTTPRequestHandler):
             def do_GET(self):  # noqa: N802
                 if self.path == "/metrics":
-                    body, code, ctype = generate_latest(reg), 200, "text/plain; version=0.0.4; charset=utf-8"
+                    body, code, ctype = coll.exposition(), 200, "text/plain; version=0.0.4; charset=utf-8"
                 elif self.path in ("/healthz", "/readyz"):
                     ok, why = hl.live() if self.path == "/healthz" else hl.ready()
                     body, code, ctype = why.encode(), (200 if ok else 503), "text/plain"

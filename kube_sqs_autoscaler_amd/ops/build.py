@@ -122,33 +122,6 @@ def build_gpu_probe(verbose: bool = True) -> Path | None:
     return GPU_SO
 
 
-def build_host_tools(verbose: bool = True) -> list[Path]:
-    """Host diagnostic tools (csrc/tools/*.cc) -> kube_sqs_autoscaler_amd/ops/<name>.bin."""
-    out = []
-    for src in sorted((CSRC / "tools").glob("*.cc")):
-        exe = OPS / (src.stem + ".bin")
-        if _stale(exe, [src], 0.0):
-            _run([CXX, "-std=c++17", "-O2", "-Wall", "-pthread", str(src), "-o", str(exe)])
-            if verbose:
-                print(f"[build] {CXX} -> {exe.relative_to(ROOT)}")
-        out.append(exe)
-    return out
-
-
-def build_tools(verbose: bool = True) -> list[Path]:
-    """HIP tuning tools (csrc/tools/*.hip) -> kube_sqs_autoscaler_amd/ops/<name>.bin."""
-    hipcc = HIPCC if Path(HIPCC).exists() else "hipcc"
-    out = []
-    for src in sorted((CSRC / "tools").glob("*.hip")):
-        exe = OPS / (src.stem + ".bin")
-        if _stale(exe, [src], 0.0):
-            _run([hipcc, f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-Wall", "-Werror=unused-value", str(src), "-o", str(exe)])
-            if verbose:
-                print(f"[build] hipcc --offload-arch={GPU_ARCH} -> {exe.relative_to(ROOT)}")
-        out.append(exe)
-    return out
-
-
 def build_native_tests(sanitizer: str | None = None, jobs: int = 8) -> Path:
     """Host-only C++ unit-test binary; `sanitizer` in {None, 'asan', 'tsan'}."""
     flags = {
@@ -185,10 +158,9 @@ def build_fuzzer(jobs: int = 8) -> Path:
 
 
 def build_all(hip: bool = True, jobs: int = 8) -> dict:
-    out = {"native": str(build_native(jobs=jobs)), "host_tools": [str(p) for p in build_host_tools()]}
+    out = {"native": str(build_native(jobs=jobs))}
     if hip:
         out["gpu_probe"] = str(build_gpu_probe())
-        out["tools"] = [str(p) for p in build_tools()]
     return out
 
 

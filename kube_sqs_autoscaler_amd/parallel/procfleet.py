@@ -74,6 +74,15 @@ class SlotRunner:
         p = self.state()["progress_ns"]
         return max(0, time.monotonic_ns() - p) if p else 0
 
+    def failing_ns(self) -> int:
+        st = self.state()
+        if not st["consecutive_failed_polls"] or not st["last_good_ns"]:
+            return 0
+        return max(0, time.monotonic_ns() - st["last_good_ns"])
+
+    def last_error(self) -> str:
+        return ""  # the text stays in the worker process (its log has it)
+
 
 class ProcWorker:
     def __init__(self, target, runner: SlotRunner, pid: int):

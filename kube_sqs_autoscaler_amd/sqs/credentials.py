@@ -221,6 +221,9 @@ def resolve_sts_endpoint(region: str, environ: Mapping[str, str]) -> Tuple[str, 
             mode = (load_profiles(environ).get(prof) or {}).get("sts_regional_endpoints", "").lower()
         except CredentialsError:
             mode = ""
+    if mode and mode not in ("legacy", "regional"):
+        # the CLI refuses this at start-up (sqs/session.py), as session.NewSession does
+        raise CredentialsError(f"unable to resolve the value of STSRegionalEndpoint for {mode}")
     if not region or (mode != "regional" and region in LEGACY_GLOBAL_STS_REGIONS):
         return "https://sts.amazonaws.com", "us-east-1"
     return f"https://sts.{region}.{native().aws_dns_suffix(region)}", region
@@ -382,7 +385,10 @@ class RemoteProvider(_Provider):
 
 
 def _truthy(v: Optional[str]) -> bool:
-    return bool(v) and v.lower() not in ("0", "false", "no")
+    """``AWS_SDK_LOAD_CONFIG``: Go's strconv.ParseBool (aws-sdk-go v1 loadEnvConfig)."""
+    from .session import go_parse_bool
+
+    return go_parse_bool(v)
 
 
 def load_profiles(environ: Mapping[str, str]) -> Dict[str, Dict[str, str]]:

@@ -40,7 +40,7 @@ setup(
     description="SQS queue-depth autoscaler for Kubernetes GPU-worker Deployments on AMD Instinct MI355X nodes",
     license="MIT",
     python_requires=">=3.10",
-    install_requires=["PyYAML>=5.4", "prometheus-client>=0.16"],
+    install_requires=["PyYAML>=5.4"],  # /metrics writes the Prometheus text format itself
     extras_require={"test": ["pytest>=7", "pytest-timeout", "hypothesis"], "bench": ["torch", "numpy"],
                     "tune": ["numpy"]},
     entry_points={"console_scripts": ["kube-sqs-autoscaler = kube_sqs_autoscaler_amd.cli:main_entry"]},

@@ -245,3 +245,88 @@ def test_latency_sum_and_buckets_cover_every_sample(nat):
         assert len(nat.latency_bucket_le_ns) == len(st["latency_buckets"]) - 1
     finally:
         env.close()
+
+
+def _readiness_env(nat, fail):
+    env = BenchEnv(1)
+    fail(env)
+    fleet = Fleet([W(*a) for a in zip(env.runners, env.targets, env.kube_apis, env.sqs_apis)])
+    from kube_sqs_autoscaler_amd.metrics import Health
+
+    h = Health(fleet, [Health.budget_ns(0, 30 * nat.SECOND)], failure_window_ns=150_000_000)
+    m = MetricsServer(fleet, "127.0.0.1:0", h)
+    m.start()
+    return env, fleet, m
+
+
+def _get(url):
+    try:
+        r = urllib.request.urlopen(url)
+        return r.status, r.read().decode()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode()
+
+
+@pytest.mark.parametrize("kind", ["sqs", "apiserver"])
+def test_readyz_fails_while_every_poll_fails(nat, kind):
+    """--readiness-failure-window: a queue that can never be read (SQS refuses the role) or a
+    Deployment that can never be written (RBAC refuses /scale and the Deployment fallback too)
+    turns /readyz to 503 after the window, while /healthz stays 200 (the loop is alive and
+    retrying, as the reference's does); one good poll makes it ready again."""
+    import time
+
+    def fail(env):
+        if kind == "sqs":
+            env.sqs.inject(50000, nat.InjectedFault(403, "<ErrorResponse><Error><Type>Sender</Type><Code>AccessDenied</Code>"
+                                                         "<Message>not authorized</Message></Error></ErrorResponse>",
+                                                    "text/xml"))
+        else:
+            env.kube.set_rbac([])
+
+    env, fleet, m = _readiness_env(nat, fail)
+    base = f"http://127.0.0.1:{m.port}"
+    try:
+        fleet.start()
+        deadline = time.time() + 10
+        while "every poll failed" not in _get(base + "/readyz")[1]:
+            assert time.time() < deadline, _get(base + "/readyz")
+            time.sleep(0.02)
+        code, why = _get(base + "/readyz")
+        assert code == 503 and "every poll failed for" in why and "gpu-worker-0" in why
+        assert ("AccessDenied" in why) if kind == "sqs" else ("forbidden" in why)
+        assert _get(base + "/healthz") == (200, "ok")
+        text = _get(base + "/metrics")[1]
+        streak = [l for l in text.splitlines() if l.startswith("ksa_consecutive_failed_polls{")]
+        assert streak and float(streak[0].rsplit(" ", 1)[1]) > 1
+        assert any(l.startswith("ksa_failing_seconds{") and float(l.rsplit(" ", 1)[1]) >= 0.15 for l in text.splitlines())
+        if kind == "apiserver":  # recovery: the next good poll makes the pod ready again
+            env.kube.set_rbac(["*"])
+            deadline = time.time() + 10
+            while _get(base + "/readyz")[0] != 200:
+                assert time.time() < deadline
+                time.sleep(0.02)
+            assert fleet.stats()[0]["consecutive_failed_polls"] == 0
+    finally:
+        fleet.stop()
+        fleet.join()
+        m.stop()
+        env.close()
+
+
+def test_readiness_window_zero_disables(nat):
+    import time
+
+    from kube_sqs_autoscaler_amd.metrics import Health
+
+    env = BenchEnv(1)
+    env.kube.set_rbac([])
+    try:
+        fleet = Fleet([W(*a) for a in zip(env.runners, env.targets, env.kube_apis, env.sqs_apis)])
+        h = Health(fleet, [Health.budget_ns(0, 30 * nat.SECOND)], failure_window_ns=0)
+        fleet.start(50)
+        fleet.join()
+        time.sleep(0.01)
+        assert env.runners[0].failing_ns() > 0
+        assert h.ready() == (True, "ok")
+    finally:
+        env.close()

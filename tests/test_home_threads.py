@@ -1,7 +1,6 @@
 """Each Runner polls on one OS thread for its whole life (HomeThread, csrc/core/runner.h), across
 Supervisor runs: a replaced thread would hand its malloc arena to another queue's new thread
-and interleave two queues' hot buffers (profiles/README.md, r02l). A thread that took a private
-file table is retired when a run wants the shared one."""
+and interleave two queues' hot buffers (profiles/README.md, r02l)."""
 import os
 
 from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
@@ -32,33 +31,6 @@ def test_runner_keeps_its_thread_across_runs(nat):
         assert sched["threads"] == 3 and sched["cpu_ns"] > 0  # this run's share only
         res = env.collect(20, 1.0)
         assert len(res.samples) == 3 * 40 and res.signature_failures == 0
-    finally:
-        env.close()
-
-
-def test_private_table_thread_is_retired_for_a_shared_run(nat):
-    earlier = _workers()
-    env = BenchEnv(2, "scale", servers="per-queue")
-    try:
-        sup = nat.Supervisor()
-        sup.private_files = True
-        for r in env.runners:
-            sup.add(r)
-        sup.start(10)
-        sup.join()
-        private = _workers() - earlier
-        assert len(private) == 2
-        sup2 = nat.Supervisor()
-        sup2.private_files = True
-        for r in env.runners:
-            sup2.add(r)
-        sup2.start(10)
-        sup2.join()
-        assert _workers() - earlier == private  # still private: kept
-        env.run(10)  # shared table: new threads
-        shared = _workers() - earlier
-        assert len(shared) == 2 and not (shared & private)
-        assert sum(r.stats()["polls"] for r in env.runners) == 2 * 30
     finally:
         env.close()
 

@@ -1,11 +1,12 @@
 """The slim image's file system, assembled the way the Dockerfile's `base` + `slim` stages do
 (Dockerfile: the package under /app, the launcher at /kube-sqs-autoscaler, PYTHONPATH=/app,
 KSA_NO_AUTOBUILD=1, libksa_gpu.so and host tools removed), run with nothing importable but the
-standard library, PyYAML and prometheus_client (the image's only runtime Python packages,
-python3-yaml and python3-prometheus-client). The reference's manifest command
-(`/kube-sqs-autoscaler --flags...`, /root/reference/README.md:37-39) must scale a Deployment
-and stop cleanly on SIGTERM. No image is built here (no container runtime in CI's CPU tier);
-this checks what the image would contain."""
+standard library and PyYAML (the image's only runtime Python package, Ubuntu 22.04's
+python3-yaml 5.4.1; the metrics endpoint writes the Prometheus text format itself). The
+reference's manifest command (`/kube-sqs-autoscaler --flags...`, /root/reference/README.md:37-39)
+must scale a Deployment, serve /metrics and /readyz, and stop cleanly on SIGTERM. No image is
+built here (no container runtime in CI's CPU tier); this checks what the image would contain,
+and which modules the process actually loaded."""
 import os
 import shutil
 import signal
@@ -22,16 +23,13 @@ AKID, SECRET, REGION, TOKEN = "AKIDIMAGE", "image/secret", "us-east-1", "image-t
 
 @pytest.fixture
 def image_root(nat, tmp_path):
-    import prometheus_client
-
     app = tmp_path / "app"
     shutil.copytree(os.path.join(ROOT, "kube_sqs_autoscaler_amd"), app / "kube_sqs_autoscaler_amd",
                     ignore=shutil.ignore_patterns("__pycache__", "libksa_gpu.so", "*.bin"))
     deps = tmp_path / "dist-packages"
     deps.mkdir()
-    for mod in (yaml, prometheus_client):
-        d = os.path.dirname(mod.__file__)
-        os.symlink(d, deps / os.path.basename(d))
+    d = os.path.dirname(yaml.__file__)
+    os.symlink(d, deps / os.path.basename(d))
     launcher = tmp_path / "kube-sqs-autoscaler"
     shutil.copy(os.path.join(ROOT, "deploy", "bin", "kube-sqs-autoscaler"), launcher)
     return tmp_path, launcher, f"{app}:{deps}"
@@ -56,18 +54,35 @@ def test_slim_image_layout_scales_with_only_its_runtime_packages(nat, image_root
     env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), "PYTHONPATH": pythonpath, "KSA_NO_AUTOBUILD": "1",
            "AWS_ACCESS_KEY_ID": AKID, "AWS_SECRET_ACCESS_KEY": SECRET, "KUBE_CONFIG_PATH": str(kc),
            "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    import socket
+
+    with socket.socket() as sk:  # a free port for --metrics-addr
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
     # -S: no site-packages, so only the image's packages (PYTHONPATH) can be imported
     err_path = tmp / "stderr.log"  # a file, not a pipe: nobody drains a pipe while it runs
+    modules_path = tmp / "modules.txt"
+    # the launcher runs under a wrapper that records every module loaded when the process exits
+    wrapper = tmp / "run.py"
+    wrapper.write_text("import atexit, runpy, sys\n"
+                       f"atexit.register(lambda: open({str(modules_path)!r}, 'w').write('\\n'.join(sorted(sys.modules))))\n"
+                       f"sys.argv = [{str(launcher)!r}] + sys.argv[1:]\n"
+                       f"runpy.run_path({str(launcher)!r}, run_name='__main__')\n")
     with open(err_path, "w") as err_file:
-        p = subprocess.Popen([sys.executable, "-S", str(launcher), f"--sqs-queue-url={url}",
+        p = subprocess.Popen([sys.executable, "-S", str(wrapper), f"--sqs-queue-url={url}",
                               "--kubernetes-deployment=workers", "--kubernetes-namespace=gpu", f"--aws-region={REGION}",
                               f"--sqs-endpoint={sqs.url}", "--poll-period=1ms", "--scale-up-cool-down=0s",
-                              "--scale-down-cool-down=0s"],
+                              "--scale-down-cool-down=0s", f"--metrics-addr=127.0.0.1:{port}"],
                              cwd=str(tmp), env=env, stderr=err_file, text=True)
     try:
         deadline = time.time() + 60
         while kube.replicas("gpu", "workers") < 8 and p.poll() is None and time.time() < deadline:
             time.sleep(0.01)
+        import urllib.request
+
+        metrics = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=10).read().decode()
+        assert 'ksa_polls_total{deployment="gpu/workers"' in metrics and "# TYPE ksa_poll_to_patch_latency_seconds histogram" in metrics
+        assert urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=10).read() == b"ok"
         p.send_signal(signal.SIGTERM)
         rc = p.wait(timeout=30)
         err = err_path.read_text()
@@ -76,6 +91,24 @@ def test_slim_image_layout_scales_with_only_its_runtime_packages(nat, image_root
         assert 'msg="Starting kube-sqs-autoscaler"' in err and 'msg="Found 500 messages in the queue"' in err
         assert "Stopped kube-sqs-autoscaler" in err
         assert sqs.signature_failures() == 0
+        # nothing outside the standard library, PyYAML and the package itself was imported
+        import sysconfig
+
+        stdlib = sysconfig.get_paths()["stdlib"]
+        loaded = modules_path.read_text().split()
+        outside = []
+        for name in loaded:
+            top = name.split(".")[0]
+            if top in ("kube_sqs_autoscaler_amd", "yaml", "_yaml", "__main__") or top in sys.builtin_module_names:
+                continue
+            if top == "cython_runtime" or top.startswith("_cython_"):  # PyYAML's compiled _yaml module
+                continue
+            spec_file = getattr(sys.modules.get(top), "__file__", None) or ""
+            if top in sys.stdlib_module_names or spec_file.startswith(stdlib):
+                continue
+            outside.append(name)
+        assert not outside, outside
+        assert "prometheus_client" not in loaded and "torch" not in loaded
     finally:
         if p.poll() is None:
             p.kill()
