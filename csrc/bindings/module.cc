@@ -446,6 +446,7 @@ PYBIND11_MODULE(_ksa_native, m) {
   py::class_<HttpSqsApi, SqsApi, py::smart_holder>(m, "HttpSqsApi")
       .def(py::init<SqsHttpOptions, std::shared_ptr<CredentialsProvider>, std::shared_ptr<Clock>>(),
            py::arg("options"), py::arg("credentials"), py::arg("clock"))
+      .def("set_timing", &HttpSqsApi::set_timing)
       .def_static("endpoint_for_region", &HttpSqsApi::endpoint_for_region)
       .def_static("signing_region", &HttpSqsApi::signing_region)
       .def("endpoint", &HttpSqsApi::endpoint)
@@ -618,7 +619,9 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("path_for", &KubeRestDeployments::path_for)
       .def_property_readonly("mode", &KubeRestDeployments::mode)
       // the control loop's pipelined read (begin before the SQS call, finish after it)
-      .def("begin_get", &KubeRestDeployments::begin_get, py::call_guard<py::gil_scoped_release>())
+      .def("set_timing", &KubeRestDeployments::set_timing)
+      .def("begin_get", &KubeRestDeployments::begin_get, py::arg("name"), py::arg("may_dial") = true,
+           py::call_guard<py::gil_scoped_release>())
       .def("finish_get", [](KubeRestDeployments& k) {
         Result<ScaleObject> r;
         {
@@ -683,7 +686,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         return span;
       })
       .def_property("dry_run", &PodAutoScaler::dry_run, &PodAutoScaler::set_dry_run)
-      .def("prefetch", &PodAutoScaler::prefetch)
+      .def("prefetch", &PodAutoScaler::prefetch, py::arg("may_dial") = true)
+      .def("warm", &PodAutoScaler::warm, py::call_guard<py::gil_scoped_release>())
       .def("discard_prefetch", &PodAutoScaler::discard_prefetch)
       .def("scale_down", [](PodAutoScaler& p) {
         ScaleSpan span;
@@ -712,7 +716,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("scale_up_messages", &LoopConfig::scale_up_messages)
       .def_readwrite("scale_down_messages", &LoopConfig::scale_down_messages)
       .def_readwrite("prefetch", &LoopConfig::prefetch)
-      .def_readwrite("prefetch_always", &LoopConfig::prefetch_always);
+      .def_readwrite("prefetch_always", &LoopConfig::prefetch_always)
+      .def_readwrite("prewarm_ns", &LoopConfig::prewarm);
 
   py::class_<Runner, std::shared_ptr<Runner>>(m, "Runner")
       .def(py::init<LoopConfig, std::shared_ptr<SqsClient>, std::shared_ptr<PodAutoScaler>, std::shared_ptr<Clock>,
@@ -965,10 +970,17 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("inject", &FakeSqsServer::inject)
       .def("set_latency", &FakeSqsServer::set_latency)
       .def("set_cpus", &FakeSqsServer::set_cpus)
+      .def("set_hot", &FakeSqsServer::set_hot)
       .def("drop_connections", &FakeSqsServer::drop_connections)
       .def("requests", &FakeSqsServer::requests)
       .def("signature_failures", &FakeSqsServer::signature_failures)
       .def("connections", &FakeSqsServer::connections)
+      .def("timings", [](const FakeSqsServer& s) {
+        std::vector<std::pair<int64_t, int64_t>> out;
+        for (auto& t : s.timings()) out.emplace_back(t.wake_ns, t.service_ns);
+        return out;
+      })
+      .def("clear_timings", &FakeSqsServer::clear_timings)
       .def("last_body", &FakeSqsServer::last_body)
       .def("last_headers", &FakeSqsServer::last_headers);
 
@@ -998,6 +1010,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("forbidden", &FakeKubeServer::forbidden)
       .def("set_latency", &FakeKubeServer::set_latency)
       .def("set_cpus", &FakeKubeServer::set_cpus)
+      .def("set_hot", &FakeKubeServer::set_hot)
       .def("drop_connections", &FakeKubeServer::drop_connections)
       .def("requests", &FakeKubeServer::requests)
       .def("gets", &FakeKubeServer::gets)
@@ -1005,6 +1018,12 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("conflicts", &FakeKubeServer::conflicts)
       .def("auth_failures", &FakeKubeServer::auth_failures)
       .def("connections", &FakeKubeServer::connections)
+      .def("timings", [](const FakeKubeServer& s) {
+        std::vector<std::pair<int64_t, int64_t>> out;
+        for (auto& t : s.timings()) out.emplace_back(t.wake_ns, t.service_ns);
+        return out;
+      })
+      .def("clear_timings", &FakeKubeServer::clear_timings)
       .def("last_method", &FakeKubeServer::last_method)
       .def("last_body", &FakeKubeServer::last_body)
       .def("last_path", &FakeKubeServer::last_path);

@@ -33,6 +33,12 @@ bool cv_wait_for(std::condition_variable& cv, Lock& lk, int64_t ns, Pred pred) {
   return cv.wait_for(lk, std::chrono::nanoseconds(ns), pred);
 #endif
 }
+// CLOCK_MONOTONIC nanoseconds (what RealClock::now() reads): deadlines and diagnostics.
+inline int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 constexpr Nanos kMicrosecond = 1000;
 constexpr Nanos kMillisecond = 1000 * kMicrosecond;
 constexpr Nanos kSecond = 1000 * kMillisecond;
@@ -75,6 +81,9 @@ class Clock {
   virtual bool sleep(Nanos d, StopFlag* stop) = 0;
   // Unix wall-clock nanoseconds (for log timestamps and SigV4 dates).
   virtual int64_t unix_nanos() = 0;
+  // Waits until now() >= deadline, busy-waiting on a real clock (for a short final stretch
+  // that must end on time with the core awake). Returns false if `stop` fired.
+  virtual bool spin_until(Nanos deadline, StopFlag* stop) { return sleep(deadline - now(), stop); }
 };
 
 class RealClock final : public Clock {
@@ -100,6 +109,15 @@ class RealClock final : public Clock {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::system_clock::now().time_since_epoch())
         .count();
+  }
+  bool spin_until(Nanos deadline, StopFlag* stop) override {
+    for (unsigned i = 0;; ++i) {
+      if (now() >= deadline) return true;
+      if ((i & 63) == 63 && stop && stop->stopped()) return false;
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
   }
 };
 

@@ -58,6 +58,7 @@ void FakeSqsServer::require_signature(std::string access_key, std::string secret
 Status FakeSqsServer::start(const std::string& host, int port, bool tls) {
   server_ = std::make_unique<HttpServer>([this](const HttpRequest& q, HttpResponse* r) { handle(q, r); });
   server_->set_cpus(cpus_);
+  server_->set_hot(hot_);
   tls_ = tls;
   if (tls) {
     Status s = generate_self_signed(host, &cert_pem_, &key_pem_);
@@ -266,6 +267,7 @@ void FakeKubeServer::require_token(std::string token) {
 Status FakeKubeServer::start(const std::string& host, int port, bool tls) {
   server_ = std::make_unique<HttpServer>([this](const HttpRequest& q, HttpResponse* r) { handle(q, r); });
   server_->set_cpus(cpus_);
+  server_->set_hot(hot_);
   tls_ = tls;
   if (tls) {
     Status s = generate_self_signed(host, &cert_pem_, &key_pem_);

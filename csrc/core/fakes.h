@@ -41,6 +41,8 @@ class FakeSqsServer {
   // CPUs for the server's threads (call before start(); the benchmark keeps a queue's fake
   // endpoints in its worker's L3 domain).
   void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
+  // HttpServer::set_hot: one busy-polling thread serves every connection (call before start()).
+  void set_hot(bool on) { hot_ = on; }
   Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
   void stop();
   int port() const;
@@ -59,6 +61,9 @@ class FakeSqsServer {
   uint64_t requests() const { return requests_.load(); }
   uint64_t signature_failures() const { return sig_failures_.load(); }
   uint64_t connections() const;
+  // HttpServer::timings(): per request, the server's wake-up delay and service time.
+  std::vector<HttpServer::ServeTiming> timings() const { return server_ ? server_->timings() : std::vector<HttpServer::ServeTiming>{}; }
+  void clear_timings() { if (server_) server_->clear_timings(); }
   std::string last_body() const;
   Headers last_headers() const;
 
@@ -67,6 +72,7 @@ class FakeSqsServer {
 
   std::unique_ptr<HttpServer> server_;
   std::vector<int> cpus_;
+  bool hot_ = false;
   StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;
@@ -97,6 +103,7 @@ class FakeKubeServer {
   ~FakeKubeServer();
   void require_token(std::string token);
   void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
+  void set_hot(bool on) { hot_ = on; }
   Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
   void stop();
   int port() const;
@@ -132,6 +139,8 @@ class FakeKubeServer {
   uint64_t conflicts() const { return conflicts_.load(); }
   uint64_t auth_failures() const { return auth_failures_.load(); }
   uint64_t connections() const;
+  std::vector<HttpServer::ServeTiming> timings() const { return server_ ? server_->timings() : std::vector<HttpServer::ServeTiming>{}; }
+  void clear_timings() { if (server_) server_->clear_timings(); }
   std::string last_method() const;
   std::string last_body() const;
   std::string last_path() const;
@@ -149,6 +158,7 @@ class FakeKubeServer {
 
   std::unique_ptr<HttpServer> server_;
   std::vector<int> cpus_;
+  bool hot_ = false;
   StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;

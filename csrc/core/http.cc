@@ -5,6 +5,7 @@
 #include "log.h"
 
 #include <csignal>
+#include <map>
 #include <mutex>
 
 #include <arpa/inet.h>
@@ -21,6 +22,7 @@
 #include <openssl/x509v3.h>
 #include <poll.h>
 #include <pthread.h>
+#include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -47,12 +49,6 @@ void ignore_sigpipe_once() {
 
 
 namespace {
-
-int64_t mono_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(
-             std::chrono::steady_clock::now().time_since_epoch())
-      .count();
-}
 
 std::string lower(std::string s) {
   for (auto& c : s) c = ascii_lower(c);
@@ -223,12 +219,24 @@ class Stream {
       if (!s.ok()) return s;
       if (n == 0) *eof = true;
       else buf->append(tmp, static_cast<size_t>(n));
+      if (n > 0 && first_.armed) {
+        first_.armed = false;
+        first_.seen = mono_ns();
+      }
       return Status::OK();
     }
     while (true) {
-      ssize_t n = ::recv(fd_, tmp, sizeof tmp, 0);
-      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK) && spin_ns_ > 0) n = spin_recv(tmp, sizeof tmp);
+      ssize_t n = recv_some(tmp, sizeof tmp);
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK) && spin_ns_ > 0) {
+        n = spin_recv(tmp, sizeof tmp);
+        if (n > 0 && first_.armed) first_.spun = true;
+      }
       if (n > 0) {
+        if (first_.armed) {
+          first_.armed = false;
+          first_.seen = mono_ns();
+          first_.rx_real = pending_rx_real_;
+        }
         buf->append(tmp, static_cast<size_t>(n));
         return Status::OK();
       }
@@ -311,6 +319,21 @@ class Stream {
 
   void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
   void set_cancel_fd(int fd) { cancel_fd_ = fd; }
+  // First-bytes timing of the next response (HttpClient::set_timing): arm before reading it;
+  // the first read that gets data stamps when this thread saw it and, on a plain socket with
+  // receive timestamps on, the kernel's receive time (CLOCK_REALTIME) of those bytes.
+  struct FirstBytes {
+    bool armed = false;
+    bool spun = false;
+    int64_t seen = 0;
+    int64_t rx_real = 0;
+  };
+  void enable_rx_timestamps() {
+    int on = 1;
+    ts_ = setsockopt(fd_, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
+  }
+  void arm_first_bytes() { first_ = FirstBytes{true, false, 0, 0}; }
+  const FirstBytes& first_bytes() const { return first_; }
   SSL* ssl() const { return ssl_; }
   void attach_ssl(SSL* ssl) { ssl_ = ssl; }  // TLS inside an established CONNECT tunnel
   // TLS inside TLS (an https origin behind an https proxy): `inner` becomes the session the
@@ -329,7 +352,7 @@ class Stream {
   ssize_t spin_recv(char* out, size_t cap) {
     const int64_t end = mono_ns() + spin_ns_;
     for (int i = 0;; ++i) {
-      const ssize_t n = ::recv(fd_, out, cap, 0);
+      const ssize_t n = recv_some(out, cap);
       if (n >= 0) return n;
       if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return n;
       if ((i & 15) == 15 && mono_ns() >= end) {
@@ -342,11 +365,38 @@ class Stream {
     }
   }
 
+  // recv(2), or recvmsg(2) with the receive timestamp while first-bytes timing is armed.
+  ssize_t recv_some(char* out, size_t cap) {
+    if (!(ts_ && first_.armed)) return ::recv(fd_, out, cap, 0);
+    struct iovec iov = {out, cap};
+    alignas(struct cmsghdr) char ctrl[CMSG_SPACE(sizeof(struct timespec))];
+    struct msghdr msg = {};
+    msg.msg_iov = &iov;
+    msg.msg_iovlen = 1;
+    msg.msg_control = ctrl;
+    msg.msg_controllen = sizeof ctrl;
+    const ssize_t n = ::recvmsg(fd_, &msg, 0);
+    if (n > 0) {
+      pending_rx_real_ = 0;
+      for (struct cmsghdr* cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
+        if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_TIMESTAMPNS) {
+          struct timespec ts;
+          std::memcpy(&ts, CMSG_DATA(cm), sizeof ts);
+          pending_rx_real_ = static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+        }
+      }
+    }
+    return n;
+  }
+
   int fd_;
   SSL* ssl_;
   SSL* outer_ = nullptr;  // the proxy's TLS session when ssl_ runs inside it
   int64_t spin_ns_ = 0;
   int cancel_fd_ = -1;
+  bool ts_ = false;
+  FirstBytes first_;
+  int64_t pending_rx_real_ = 0;
 };
 
 // BIO carrying one TLS session's records inside another (the https-proxy tunnel). Non-blocking
@@ -869,6 +919,7 @@ struct HttpClient::Conn {
   uint64_t uses = 0;
   bool session_saved = false;
   int64_t last_response_ns = 0;  // mono time a response was last read in full (0: none yet)
+  int64_t last_checked_ns = 0;   // mono time the idle-close peek last passed (HttpClient::warm)
 };
 
 namespace {
@@ -949,6 +1000,21 @@ void HttpClient::cancel() {
     ssize_t r = ::write(cancel_fd_, &one, sizeof one);
     (void)r;
   }
+}
+
+HttpTiming HttpClient::last_timing() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return timing_last_;
+}
+
+std::string http_timing_json(const HttpTiming& t) {
+  if (t.done == 0) return "";
+  auto d = [](int64_t a, int64_t b) { return std::to_string(a > 0 && b > 0 ? b - a : -1); };
+  // the wait ends when the kernel received the first response bytes (seen, without a stamp)
+  const int64_t arrival = t.rx > 0 ? t.rx : t.seen;
+  return "{\"pre\":" + d(t.start, t.write_begin) + ",\"write\":" + d(t.write_begin, t.written) +
+         ",\"wait\":" + d(t.written, arrival) + ",\"wake\":" + (t.rx > 0 ? d(t.rx, t.seen) : std::string("-1")) +
+         ",\"read\":" + d(t.seen, t.done) + ",\"spun\":" + (t.spun ? "true" : "false") + "}";
 }
 
 HttpClientStats HttpClient::stats() const {
@@ -1147,6 +1213,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   conn_ = std::make_unique<Conn>();
   conn_->stream = std::move(stream);
   conn_->rbuf = std::move(rbuf);
+  if (timing_) conn_->stream->enable_rx_timestamps();
   stats_.connects++;
   return Status::OK();
 }
@@ -1164,9 +1231,43 @@ bool replayable(const HttpRequest& req) {
 
 }  // namespace
 
+bool HttpClient::fresh_locked() const {
+  const int64_t now = mono_ns();
+  return conn_ && ((conn_->last_response_ns > 0 && now - conn_->last_response_ns < kFreshConnNs) ||
+                   (conn_->last_checked_ns > 0 && now - conn_->last_checked_ns < kFreshConnNs));
+}
+
+bool HttpClient::warm() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (in_flight_ || cancelled()) return false;
+  if (fresh_locked()) return true;
+  if (conn_ && conn_->uses > 0 && conn_->stream->peer_closed()) {
+    stats_.idle_closed++;
+    conn_.reset();
+  }
+  if (!conn_ && !connect_locked(timeout_ > 0 ? mono_ns() + timeout_ : 0).ok()) return false;
+  conn_->last_checked_ns = mono_ns();
+  return true;
+}
+
+bool HttpClient::ready_without_dial() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (in_flight_ || !conn_) return false;
+  if (fresh_locked() || conn_->uses == 0) return true;
+  if (conn_->stream->peer_closed()) {
+    stats_.idle_closed++;
+    conn_.reset();
+    return false;
+  }
+  conn_->last_checked_ns = mono_ns();
+  return true;
+}
+
 Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable) {
   *retryable = false;
-  if (conn_ && conn_->uses > 0 && !(conn_->last_response_ns > 0 && mono_ns() - conn_->last_response_ns < kFreshConnNs) &&
+  // The idle-close peek may be skipped on a connection used or checked this recently -- unless
+  // the request must not be replayed and nobody above retries it (a Deployment write).
+  if (conn_ && conn_->uses > 0 && !(fresh_locked() && (caller_retries_ || replayable(req))) &&
       conn_->stream->peer_closed()) {
     stats_.idle_closed++;
     conn_.reset();  // closed while idle: dial a fresh one (the request was never sent)
@@ -1177,6 +1278,7 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   }
   const bool reused = conn_->uses > 0;
   conn_->uses++;
+  if (timing_) timing_cur_.write_begin = mono_ns();
 
   std::string& wire = wire_;  // kept across requests: no allocation per request
   if (wire.capacity() > 64 * 1024) std::string().swap(wire);
@@ -1219,6 +1321,7 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   }
   stats_.bytes_out += wire.size();
   sent_at_ = mono_ns();
+  if (timing_) timing_cur_.written = sent_at_;
   return Status::OK();
 }
 
@@ -1240,6 +1343,7 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   const bool reused = conn_->uses > 1;
   Status s;
   conn_->stream->set_spin_ns(spin_window());
+  if (timing_) conn_->stream->arm_first_bytes();
   Reader rd(conn_->stream.get(), &conn_->rbuf);
   std::string& head = head_;  // kept across responses: no allocation per response
   if (head.capacity() > 64 * 1024) std::string().swap(head);
@@ -1302,6 +1406,20 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
     const Nanos rtt = now - sent_at_;
     ewma_ns_ = ewma_ns_ < 0 ? rtt : (ewma_ns_ * 7 + rtt) / 8;
     conn_->last_response_ns = now;
+    if (timing_) {
+      const auto& fb = conn_->stream->first_bytes();
+      timing_cur_.seen = fb.seen;
+      timing_cur_.spun = fb.spun;
+      timing_cur_.rx = 0;
+      if (fb.rx_real > 0) {  // CLOCK_REALTIME -> CLOCK_MONOTONIC
+        struct timespec rt;
+        clock_gettime(CLOCK_REALTIME, &rt);
+        const int64_t real_now = static_cast<int64_t>(rt.tv_sec) * 1000000000LL + rt.tv_nsec;
+        timing_cur_.rx = fb.rx_real - (real_now - mono_ns());
+      }
+      timing_cur_.done = now;
+      timing_last_ = timing_cur_;
+    }
   }
   // TLS 1.3 tickets arrive after the handshake (with the first response): keep the session of
   // each new connection once, for resumption on the next reconnect.
@@ -1363,6 +1481,7 @@ Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp, Nanos 
   if (timeout == 0) return Status::Err("i/o timeout");  // no time left at all
   const int64_t deadline = t > 0 ? mono_ns() + t : 0;
   stats_.requests++;
+  if (timing_) timing_cur_ = HttpTiming{mono_ns()};
   bool retryable = false;
   Status s = attempt(req, resp, deadline, &retryable);
   if (!s.ok() && retryable && !cancelled()) {
@@ -1378,6 +1497,7 @@ Status HttpClient::send(const HttpRequest& req) {
   if (cancelled()) return Status::Err("request canceled");
   const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
   stats_.requests++;
+  if (timing_) timing_cur_ = HttpTiming{mono_ns()};
   bool retryable = false;
   Status s = write_request(req, deadline, &retryable);
   if (!s.ok() && retryable && !cancelled()) {
@@ -1457,9 +1577,10 @@ Status HttpServer::listen(const std::string& host, int port) {
                                    : ntohs(reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
   listen_fd_ = fd;
   acceptor_ = std::thread([this] {
-    pthread_setname_np(pthread_self(), "ksa-accept");
+    pthread_setname_np(pthread_self(), hot_ ? "ksa-serve-hot" : "ksa-accept");
     pin_current_thread(cpus_);
-    accept_loop();
+    if (hot_) hot_loop();
+    else accept_loop();
   });
   return Status::OK();
 }
@@ -1503,6 +1624,61 @@ void HttpServer::accept_loop() {
   }
 }
 
+namespace {
+int64_t realtime_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+// Blocks until `fd` is readable; returns the kernel receive time (CLOCK_REALTIME ns) of the
+// first queued byte, 0 when the socket reports none (closed, or timestamps unavailable).
+int64_t wait_rx_timestamp(int fd) {
+  struct pollfd p = {fd, POLLIN, 0};
+  while (::poll(&p, 1, -1) < 0 && errno == EINTR) {
+  }
+  char c;
+  struct iovec iov = {&c, 1};
+  alignas(struct cmsghdr) char ctrl[CMSG_SPACE(sizeof(struct timespec))];
+  struct msghdr msg = {};
+  msg.msg_iov = &iov;
+  msg.msg_iovlen = 1;
+  msg.msg_control = ctrl;
+  msg.msg_controllen = sizeof ctrl;
+  if (::recvmsg(fd, &msg, MSG_PEEK | MSG_DONTWAIT) <= 0) return 0;
+  for (struct cmsghdr* cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
+    if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_TIMESTAMPNS) {
+      struct timespec ts;
+      std::memcpy(&ts, CMSG_DATA(cm), sizeof ts);
+      return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+    }
+  }
+  return 0;
+}
+}  // namespace
+
+void HttpServer::record_timing(ServeTiming t) {
+  std::lock_guard<std::mutex> lk(timing_mu_);
+  constexpr size_t kKeep = 1 << 16;
+  if (timings_.size() < kKeep) {
+    timings_.push_back(t);
+  } else {
+    timings_[timing_pos_] = t;
+    timing_pos_ = (timing_pos_ + 1) % kKeep;
+  }
+}
+
+std::vector<HttpServer::ServeTiming> HttpServer::timings() const {
+  std::lock_guard<std::mutex> lk(timing_mu_);
+  return timings_;
+}
+
+void HttpServer::clear_timings() {
+  std::lock_guard<std::mutex> lk(timing_mu_);
+  timings_.clear();
+  timing_pos_ = 0;
+}
+
 void HttpServer::serve(int fd) {
   SSL* ssl = nullptr;
   if (ctx_) {
@@ -1517,7 +1693,13 @@ void HttpServer::serve(int fd) {
     if (ssl) ok = stream.handshake(true, mono_ns() + 10 * kSecond).ok();
     std::string rbuf;
     Reader rd(&stream, &rbuf);
+    int on = 1;
+    const bool stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
     while (ok && !stopping_.load()) {
+      // The next request's arrival: its kernel receive time and when this thread got to it.
+      int64_t rx = 0;
+      if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd);
+      const int64_t t_read = realtime_ns();
       std::string head;
       bool got_any = false;
       if (!rd.read_head(&head, 0, &got_any).ok()) break;
@@ -1571,11 +1753,207 @@ void HttpServer::serve(int fd) {
       wire += resp.body;
       if (!stream.write_all(wire, mono_ns() + 10 * kSecond).ok()) break;
       served_++;
+      if (rx > 0) record_timing(ServeTiming{std::max<int64_t>(t_read - rx, 0), realtime_ns() - t_read});
       if (close_after) break;
     }
     std::lock_guard<std::mutex> lk(mu_);
     open_fds_.erase(std::remove(open_fds_.begin(), open_fds_.end(), fd), open_fds_.end());
   }  // Stream dtor closes fd (after removal from open_fds_, so no fd-reuse race)
+}
+
+namespace {
+
+// One complete request at the front of `buf`: parses it into *req and returns the bytes it
+// took; 0 while incomplete; -1 for a request this server cannot take (malformed, chunked).
+long take_request(const std::string& buf, HttpRequest* req, bool* http10) {
+  const size_t end = buf.find("\r\n\r\n");
+  if (end == std::string::npos) return buf.size() > (64u << 10) ? -1 : 0;
+  const size_t eol = buf.find("\r\n");
+  const std::string line = buf.substr(0, eol);
+  const size_t a = line.find(' '), b = line.rfind(' ');
+  if (a == std::string::npos || b == a) return -1;
+  req->method = line.substr(0, a);
+  req->target = line.substr(a + 1, b - a - 1);
+  *http10 = line.compare(b + 1, 8, "HTTP/1.0") == 0;
+  req->headers.clear();
+  std::string bad;
+  const std::string head = buf.substr(0, end + 4);
+  if (!parse_header_lines(head, eol + 2, &req->headers, &bad)) return -1;
+  if (is_chunked(req->headers)) return -1;
+  size_t n = 0;
+  if (!req->header("Content-Length").empty()) {
+    const long long cl = std::atoll(req->header("Content-Length").c_str());
+    if (cl < 0 || cl > (64LL << 20)) return -1;
+    n = static_cast<size_t>(cl);
+  }
+  if (buf.size() < end + 4 + n) return 0;
+  req->body.assign(buf, end + 4, n);
+  return static_cast<long>(end + 4 + n);
+}
+
+std::string response_wire(const HttpResponse& resp, bool close_after) {
+  std::string wire = "HTTP/1.1 " + std::to_string(resp.status) + " " +
+                     (resp.reason.empty() ? http_reason(resp.status) : resp.reason) + "\r\n";
+  for (auto& [k, v] : resp.headers) wire += k + ": " + v + "\r\n";
+  if (!has_header(resp.headers, "Content-Length")) {
+    wire += "Content-Length: ";
+    wire += std::to_string(resp.body.size());
+    wire += "\r\n";
+  }
+  if (close_after) wire += "Connection: close\r\n";
+  wire += "\r\n";
+  wire += resp.body;
+  return wire;
+}
+
+}  // namespace
+
+void HttpServer::hot_loop() {
+  struct Conn {
+    int fd = -1;
+    SSL* ssl = nullptr;
+    bool handshaken = false;
+    std::string rbuf;
+  };
+  const int ep = epoll_create1(EPOLL_CLOEXEC);
+  if (ep < 0) return;
+  fcntl(listen_fd_, F_SETFL, fcntl(listen_fd_, F_GETFL, 0) | O_NONBLOCK);
+  struct epoll_event lev = {};
+  lev.events = EPOLLIN;
+  lev.data.fd = listen_fd_;
+  epoll_ctl(ep, EPOLL_CTL_ADD, listen_fd_, &lev);
+  std::map<int, Conn> conns;
+  auto drop = [&](int fd) {
+    auto it = conns.find(fd);
+    if (it == conns.end()) return;
+    epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
+    if (it->second.ssl) SSL_free(it->second.ssl);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      open_fds_.erase(std::remove(open_fds_.begin(), open_fds_.end(), fd), open_fds_.end());
+    }
+    ::close(fd);
+    conns.erase(it);
+  };
+  struct epoll_event evs[64];
+  while (!stopping_.load(std::memory_order_relaxed)) {
+    const int n = epoll_wait(ep, evs, 64, 0);  // busy-polled: this thread never sleeps
+    for (int i = 0; i < n; ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == listen_fd_) {
+        for (;;) {
+          const int c = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
+          if (c < 0) break;
+          int one = 1;
+          setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          setsockopt(c, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
+          accepted_++;
+          Conn cn;
+          cn.fd = c;
+          if (ctx_) {
+            cn.ssl = SSL_new(ctx_);
+            SSL_set_fd(cn.ssl, c);
+          } else {
+            cn.handshaken = true;
+          }
+          conns[c] = std::move(cn);
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            open_fds_.push_back(c);
+          }
+          struct epoll_event ev = {};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.fd = c;
+          epoll_ctl(ep, EPOLL_CTL_ADD, c, &ev);
+        }
+        continue;
+      }
+      auto it = conns.find(fd);
+      if (it == conns.end()) continue;
+      Conn& cn = it->second;
+      if (!cn.handshaken) {
+        const int r = SSL_accept(cn.ssl);
+        if (r == 1) {
+          cn.handshaken = true;
+        } else {
+          const int e = SSL_get_error(cn.ssl, r);
+          if (e != SSL_ERROR_WANT_READ && e != SSL_ERROR_WANT_WRITE) drop(fd);
+          continue;
+        }
+      }
+      // the kernel's receive time of the oldest unread byte, when nothing is buffered yet
+      int64_t rx = 0;
+      if (cn.rbuf.empty() && !(cn.ssl && SSL_pending(cn.ssl) > 0)) rx = wait_rx_timestamp(fd);
+      const int64_t t_read = realtime_ns();
+      bool closed = false;
+      char tmp[16384];
+      for (;;) {
+        int got;
+        if (cn.ssl) {
+          got = SSL_read(cn.ssl, tmp, sizeof tmp);
+          if (got <= 0) {
+            const int e = SSL_get_error(cn.ssl, got);
+            if (e != SSL_ERROR_WANT_READ && e != SSL_ERROR_WANT_WRITE) closed = true;
+            break;
+          }
+        } else {
+          got = static_cast<int>(::recv(fd, tmp, sizeof tmp, 0));
+          if (got == 0) closed = true;
+          if (got <= 0) break;
+        }
+        cn.rbuf.append(tmp, static_cast<size_t>(got));
+      }
+      bool close_after = false;
+      for (;;) {
+        HttpRequest req;
+        bool http10 = false;
+        const long used = take_request(cn.rbuf, &req, &http10);
+        if (used == 0) break;
+        if (used < 0) {
+          close_after = true;
+          break;
+        }
+        cn.rbuf.erase(0, static_cast<size_t>(used));
+        HttpResponse resp;
+        resp.status = 200;
+        handler_(req, &resp);
+        if (resp.status < 0) {
+          close_after = true;
+          break;
+        }
+        close_after = wants_close(req.headers, http10);
+        const std::string wire = response_wire(resp, close_after);
+        size_t off = 0;
+        while (off < wire.size()) {  // small responses: spin until written
+          int w;
+          if (cn.ssl) {
+            w = SSL_write(cn.ssl, wire.data() + off, static_cast<int>(wire.size() - off));
+            if (w <= 0) {
+              const int e = SSL_get_error(cn.ssl, w);
+              if (e == SSL_ERROR_WANT_WRITE || e == SSL_ERROR_WANT_READ) continue;
+              close_after = true;
+              break;
+            }
+          } else {
+            w = static_cast<int>(::send(fd, wire.data() + off, wire.size() - off, MSG_NOSIGNAL));
+            if (w < 0) {
+              if (errno == EAGAIN || errno == EINTR) continue;
+              close_after = true;
+              break;
+            }
+          }
+          off += static_cast<size_t>(w);
+        }
+        served_++;
+        if (rx > 0) record_timing(ServeTiming{std::max<int64_t>(t_read - rx, 0), realtime_ns() - t_read});
+        rx = 0;
+        if (close_after) break;
+      }
+      if (closed || close_after) drop(fd);
+    }
+  }
+  while (!conns.empty()) drop(conns.begin()->first);
+  ::close(ep);
 }
 
 void HttpServer::drop_connections() {

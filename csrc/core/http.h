@@ -77,6 +77,21 @@ struct HttpClientStats {
   std::string tls_cipher;   // its cipher suite, e.g. "TLS_AES_128_GCM_SHA256"
 };
 
+// Where one request's time went (HttpClient::set_timing), CLOCK_MONOTONIC ns; 0 = not known.
+// rx is the kernel's receive time of the response's first bytes (SO_TIMESTAMPNS; plain sockets
+// only), so seen - rx is how long those bytes waited for this thread: its wake-up.
+struct HttpTiming {
+  int64_t start = 0;        // the request call began
+  int64_t write_begin = 0;  // connection ready (peek / dial done), request serialised
+  int64_t written = 0;      // request fully written
+  int64_t rx = 0;           // kernel receive time of the first response bytes
+  int64_t seen = 0;         // this thread read the first response bytes
+  int64_t done = 0;         // response fully read
+  bool spun = false;        // the first bytes came while busy-polling (no sleep)
+};
+// {"pre":..,"write":..,"wait":..,"wake":..,"read":..,"spun":..} in ns (empty when not timed).
+std::string http_timing_json(const HttpTiming& t);
+
 // One-shot work for the calling thread to run as soon as its next HTTP request is on the wire
 // (HttpClient::attempt, after the write and before the wait for the response). The control loop
 // sends its pipelined Deployment GET from here: the SQS request goes out first and the GET
@@ -113,6 +128,26 @@ class alignas(kCacheLine) HttpClient {
   Status receive(HttpResponse* resp);
   bool in_flight() const;
   void close();
+  // Pre-poll warm-up (Runner prewarm): checks the idle keep-alive connection now -- the
+  // idle-close peek the next request would make -- and dials (with TLS) when there is none or
+  // the peer closed it, so the request itself finds a live, freshly checked connection. Dial
+  // errors are left for the request to report. Returns whether a connection is ready.
+  bool warm();
+  // Whether a request could go out now without dialing: a connection exists and is either
+  // fresh (a response or a check within kFreshConnNs) or passes the idle-close peek. The
+  // pipelined GET, sent from inside the SQS call, goes out only then (a dial there would run
+  // on the SQS call's deadline).
+  bool ready_without_dial();
+  // The caller retries a failed request itself (the SQS client's SDK-style retryer): a request
+  // that is not replayable may then skip the idle-close peek on a fresh connection. Without it
+  // (the apiserver client) a PUT/PATCH is always preceded by the peek, so a connection the
+  // peer half-closed is redialled instead of failing the write.
+  void set_caller_retries(bool on) { caller_retries_ = on; }
+  // Per-request timing breakdown (diagnostics: a benchmark's attribution rows); adds a
+  // timestamp read per phase and a recvmsg for the first response bytes. Off by default.
+  void set_timing(bool on) { timing_ = on; }
+  bool timing() const { return timing_; }
+  HttpTiming last_timing() const;
   // Aborts any request in progress ("request canceled") and every later one: graceful shutdown
   // must not wait for a slow or hung peer (the in-flight call's timeout can be 30 s). Sticky.
   void cancel();
@@ -177,6 +212,10 @@ class alignas(kCacheLine) HttpClient {
   std::string proxy_user_, proxy_pass_;  // socks5 credentials
   std::string proxy_auth_;  // "Basic ..." or empty
   bool in_flight_ = false;
+  bool caller_retries_ = false;
+  bool timing_ = false;
+  HttpTiming timing_cur_, timing_last_;
+  bool fresh_locked() const;
   int cancel_fd_ = -1;  // eventfd signalled by cancel(); polled next to the socket
   std::atomic<bool> cancelled_{false};
   HttpRequest pending_;
@@ -204,10 +243,29 @@ class HttpServer {
   void drop_connections();
   // CPUs for the acceptor and connection threads (call before listen(); empty: unpinned).
   void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
+  // Per request served (the latest 64K): the wake-up delay -- the kernel's receive timestamp
+  // of the request's first segment (SO_TIMESTAMPNS) to the connection thread running -- and
+  // the service time, from then to the response written. A benchmark subtracts the first from
+  // a client's round trip: it is what a fake endpoint idle between polls adds by sleeping,
+  // which a production endpoint does not.
+  struct ServeTiming {
+    int64_t wake_ns;
+    int64_t service_ns;
+  };
+  std::vector<ServeTiming> timings() const;
+  void clear_timings();
+  // Hot mode (call before listen()): one thread serves every connection from a busy-polled
+  // epoll set and never sleeps -- a model of a loaded production endpoint (AWS, a busy
+  // apiserver), which is awake when a request arrives. The default thread-per-connection
+  // server sleeps between requests, so a client polling every second pays the endpoint's
+  // wake-up from a deep idle state on top of its own round trip. Costs one CPU per server.
+  void set_hot(bool on) { hot_ = on; }
 
  private:
   void accept_loop();
   void serve(int fd);
+  void hot_loop();
+  bool hot_ = false;
 
   Handler handler_;
   SSL_CTX* ctx_ = nullptr;
@@ -227,6 +285,10 @@ class HttpServer {
   std::atomic<uint64_t> served_{0};
   std::atomic<uint64_t> accepted_{0};
   std::vector<int> cpus_;
+  mutable std::mutex timing_mu_;
+  std::vector<ServeTiming> timings_;
+  size_t timing_pos_ = 0;
+  void record_timing(ServeTiming t);
 };
 
 // Self-signed certificate for `host` (DNS name or IP literal) -- fakes only.

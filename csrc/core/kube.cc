@@ -442,8 +442,15 @@ bool KubeRestDeployments::try_fallback(const Status& s, const std::string& name,
   return true;
 }
 
-bool KubeRestDeployments::begin_get(const std::string& name) {
+void KubeRestDeployments::warm() {
+  if (!init_status_.ok() || cancel_.stopped()) return;
+  if (opts_.token) (void)opts_.token->token();  // a token file due for a re-read is read now
+  http_->warm();
+}
+
+bool KubeRestDeployments::begin_get(const std::string& name, bool may_dial) {
   if (!init_status_.ok() || name.empty() || http_->in_flight()) return false;
+  if (!may_dial && !http_->ready_without_dial()) return false;
   HttpRequest req;
   req.method = "GET";
   const ScaleMode m = mode();
@@ -610,7 +617,7 @@ void FakeDeployments::enable_pipelining(bool on) {
   pipelining_ = on;
 }
 
-bool FakeDeployments::begin_get(const std::string& name) {
+bool FakeDeployments::begin_get(const std::string& name, bool) {
   std::lock_guard<std::mutex> lk(mu_);
   if (!pipelining_ || pending_) return false;
   pending_result_ = get_locked(name);  // the server reads the object when the request arrives
@@ -713,9 +720,9 @@ PodAutoScaler::PodAutoScaler(std::shared_ptr<DeploymentApi> api, std::string dep
       log_(std::move(log)),
       clock_(std::move(clock)) {}
 
-bool PodAutoScaler::prefetch() {
+bool PodAutoScaler::prefetch(bool may_dial) {
   if (prefetch_pending_) return true;
-  prefetch_pending_ = api_->begin_get(deployment_);
+  prefetch_pending_ = api_->begin_get(deployment_, may_dial);
   return prefetch_pending_;
 }
 

@@ -50,7 +50,13 @@ class DeploymentApi {
   // Pipelined read: begin_get() starts a GET and returns without waiting (false: not
   // supported, nothing started); finish_get() returns its result. Implementations that
   // cannot overlap I/O keep the defaults and the control loop reads synchronously.
-  virtual bool begin_get(const std::string& name) { return false; }
+  // may_dial false: start it only on a connection that needs no dial (the caller is inside
+  // another request's deadline); otherwise return false and let the synchronous GET run.
+  virtual bool begin_get(const std::string& name, bool may_dial = true) {
+    (void)name;
+    (void)may_dial;
+    return false;
+  }
   virtual Result<ScaleObject> finish_get() {
     return Result<ScaleObject>::Err(Status::Err("no pipelined GET in flight"));
   }
@@ -61,6 +67,11 @@ class DeploymentApi {
   // Clock time at which the latest deliberate wait (client-side throttle, Retry-After) ends or
   // ended; 0: none yet. The liveness check counts such a wait as progress.
   virtual Nanos waiting_until() const { return 0; }
+  // Pre-poll warm-up (Runner prewarm): the bearer token and the connection check or dial, done
+  // before the poll is due. Sends nothing. Default: nothing.
+  virtual void warm() {}
+  // The last request's time breakdown as a JSON object ("" when not timed).
+  virtual std::string timing_json() const { return ""; }
 };
 
 class TokenProvider {
@@ -165,8 +176,15 @@ class alignas(kCacheLine) KubeRestDeployments final : public DeploymentApi {
   explicit KubeRestDeployments(KubeOptions opts);
   Result<ScaleObject> get(const std::string& name) override;
   Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override;
-  bool begin_get(const std::string& name) override;
+  bool begin_get(const std::string& name, bool may_dial = true) override;
   Result<ScaleObject> finish_get() override;
+  void warm() override;
+  void set_timing(bool on) {
+    if (http_) http_->set_timing(on);
+  }
+  std::string timing_json() const override {
+    return http_ && http_->timing() ? http_timing_json(http_->last_timing()) : "";
+  }
   KubeStats stats() const;
   void cancel() override;
   void close_connections() override {
@@ -233,7 +251,7 @@ class FakeDeployments final : public DeploymentApi {
   // Pipelined read in virtual time: the snapshot is taken when the GET starts, and
   // finish_get() only advances a VirtualClock to start + latency (the GET ran concurrently with
   // whatever the caller did in between). Disabled unless enable_pipelining(true).
-  bool begin_get(const std::string& name) override;
+  bool begin_get(const std::string& name, bool may_dial = true) override;
   Result<ScaleObject> finish_get() override;
   void enable_pipelining(bool on);
 
@@ -296,8 +314,10 @@ class alignas(kCacheLine) PodAutoScaler {
   // it instead of issuing its own GET. If the write then fails with 409 (the object changed
   // after the prefetch) the call re-reads and retries once -- exactly the GET-then-write the
   // reference would have done at that point. discard_prefetch() drains an unused prefetch.
-  bool prefetch();
+  // may_dial: see DeploymentApi::begin_get.
+  bool prefetch(bool may_dial = true);
   void discard_prefetch();
+  void warm() { api_->warm(); }
   bool prefetch_pending() const { return prefetch_pending_; }
 
   std::shared_ptr<DeploymentApi> api() const { return api_; }

@@ -82,12 +82,35 @@ bool Runner::action_likely(Nanos t0) const {
 
 IterationRecord Runner::step(StopFlag* stop) {
   // main.go:41 -- sleep BEFORE the poll.
-  if (!clock_->sleep(cfg_.poll_period, stop)) {
+  const Nanos period = cfg_.poll_period, w = cfg_.prewarm;
+  bool slept;
+  if (w > 0 && period > 2 * w) {
+    const Nanos due = clock_->now() + period;
+    slept = clock_->sleep(period - w, stop);
+    if (slept) {
+      warm(due);
+      slept = clock_->spin_until(due, stop);
+    }
+  } else {
+    slept = clock_->sleep(period, stop);
+    // a period too short to wake early in: the same preparation, at the due time (cheap on
+    // connections used within the last few milliseconds, which at such a period they were)
+    if (slept && w > 0) warm(clock_->now());
+  }
+  if (!slept) {
     IterationRecord rec;
     rec.stopped = true;
     return rec;
   }
   return poll_once();
+}
+
+void Runner::warm(Nanos due) {
+  sqs_->warm(clock_->unix_nanos() + (due - clock_->now()));
+  // the Deployment read and write only follow on polls the gates may let through (or every
+  // poll, with a GET sent on every poll)
+  if ((cfg_.prefetch && cfg_.prefetch_always) || action_likely(due)) scaler_->warm();
+  log_flush_pending();  // nothing held back past the due time
 }
 
 IterationRecord Runner::poll_once() {
@@ -112,15 +135,19 @@ IterationRecord Runner::poll_body() {
   // If the SQS write fails before that point, the GET goes out after the call (when it
   // succeeded on a retry). In-memory clients (tests, the parity harness) get it first, as
   // the virtual-time model of the overlap expects.
+  // From the on-wire hook the GET must not dial: that would run on the SQS call's deadline, so
+  // an unreachable apiserver would fail the SQS read. Without a ready connection the poll does
+  // the reference's synchronous GET after the SQS answer instead.
   struct Prefetch {
     Runner* self;
     IterationRecord* rec;
+    bool may_dial;
     static void send(void* p) {
       auto* f = static_cast<Prefetch*>(p);
-      f->rec->prefetched = f->self->scaler_->prefetch();
+      f->rec->prefetched = f->self->scaler_->prefetch(f->may_dial);
       if (f->rec->prefetched) f->rec->gets++;
     }
-  } pf{this, &rec};
+  } pf{this, &rec, false};
   bool on_wire = false;
   if (cfg_.prefetch) {
     if (cfg_.prefetch_always || action_likely(t0)) {
@@ -128,6 +155,7 @@ IterationRecord Runner::poll_body() {
         on_wire = true;
         set_on_wire(&Prefetch::send, &pf);
       } else {
+        pf.may_dial = true;
         Prefetch::send(&pf);
       }
     } else {
@@ -140,6 +168,7 @@ IterationRecord Runner::poll_body() {
   Nanos t1 = clock_->now();
   if (on_wire && on_wire_pending()) {
     clear_on_wire();
+    pf.may_dial = true;  // outside the SQS call now
     if (depth.ok()) Prefetch::send(&pf);  // the SQS request never reached the wire first
   }
   rec.depth_ns = t1 - t0;
@@ -162,6 +191,13 @@ IterationRecord Runner::poll_body() {
   auto finish = [&]() -> IterationRecord& {
     scaler_->discard_prefetch();  // unused (no action this poll): drain it
     rec.total_ns = clock_->now() - t0;
+    if (trace_fd_ >= 0) {  // per-call breakdowns of timed clients (bench attribution rows)
+      const std::string sq = sqs_->api()->timing_json();
+      const std::string wr = rec.patch_latency_ns >= 0 ? scaler_->api()->timing_json() : std::string();
+      if (!sq.empty() || !wr.empty())
+        rec.detail = "{\"sqs\":" + (sq.empty() ? std::string("null") : sq) +
+                     ",\"write\":" + (wr.empty() ? std::string("null") : wr) + "}";
+    }
     record(rec);
     return rec;
   };
@@ -346,6 +382,7 @@ std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std:
                   ",\"update_ns\":" + std::to_string(r.update_ns) + ",\"total_ns\":" + std::to_string(r.total_ns) +
                   ",\"patch_latency_ns\":" + std::to_string(r.patch_latency_ns);
   if (!r.error.empty()) j += ",\"error\":" + json_quote(r.error);
+  if (!r.detail.empty()) j += ",\"detail\":" + r.detail;
   j += "}";
   return j;
 }

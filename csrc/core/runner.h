@@ -49,6 +49,14 @@ struct LoopConfig {
   // response (Runner::action_likely), so an idle queue costs the apiserver what the reference
   // costs it: nothing between cool-down expiries. true: send it with every poll.
   bool prefetch_always = false;
+  // Pre-poll warm-up (--poll-prewarm): wake this long before a poll is due, do what the poll
+  // would do first without sending anything -- credentials, the signed SQS request for that
+  // second, the bearer token, both connections checked (or dialled) -- then spin until the due
+  // time, so the poll starts on time on an awake core with its code and data in cache. The
+  // poll itself, and so every decision, is unchanged (sleep-then-poll, main.go:41); the cost is
+  // up to `prewarm` of CPU per poll. 0 disables. With a poll period under 2x `prewarm` the
+  // preparation runs at the due time instead, without the early wake-up.
+  Nanos prewarm = 0;
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };
@@ -74,6 +82,7 @@ struct IterationRecord {
   Nanos total_ns = 0;          // end of sleep -> end of iteration
   Nanos patch_latency_ns = -1; // end of sleep -> end of last successful write (-1: no write)
   std::string error;
+  std::string detail;  // traced polls with timed clients: {"sqs":{...},"write":{...}} (HttpTiming)
 };
 
 // Poll->patch latency histogram: bucket i counts samples <= kLatBucketLeNs[i] (and above the
@@ -241,6 +250,7 @@ class alignas(kCacheLine) Runner {
 
  private:
   IterationRecord poll_body();
+  void warm(Nanos due);
   void record(const IterationRecord& r);
   void mirror(const IterationRecord& r);
   CpuList cpus_;

@@ -81,6 +81,7 @@ HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider>
   url_ = u.value;
   http_ = std::make_unique<HttpClient>(url_, opts_.tls, opts_.timeout);
   http_->set_busy_poll(opts_.busy_poll);
+  http_->set_caller_retries(true);  // DefaultRetryer: a failed send is retried above the client
   Status ps = http_->set_proxy(opts_.proxy);
   if (!ps.ok()) endpoint_status_ = ps;
 }
@@ -117,15 +118,8 @@ Nanos HttpSqsApi::retry_delay(int retry_count, bool throttle) {
   return d > max_delay ? jitter(max_delay / 2) : d;
 }
 
-Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
-                                      const std::vector<std::string>& names, bool* retryable,
-                                      bool* throttle, bool* expired, Nanos* retry_after) {
-  *retryable = *throttle = *expired = false;
-  *retry_after = 0;
-  auto cr = creds_.get(clock_->unix_nanos());
-  if (!cr.ok()) return Result<AttrMap>::Err(cr.status);
-
-  std::unique_lock<std::mutex> prep_lock(prep_mu_);
+void HttpSqsApi::sign_locked(const std::string& queue_url, const std::vector<std::string>& names,
+                             const Credentials& c, int64_t unix_ns) {
   if (!prepared_valid_ || queue_url != prepared_url_ || names != prepared_names_) {
     HttpRequest proto;
     proto.method = "POST";
@@ -170,13 +164,8 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
     prepared_valid_ = true;
     signed_valid_ = false;
   }
-  HttpRequest req;
-  req.method = "POST";
-  req.target = url_.path.empty() ? "/" : url_.path;
-  req.body = prepared_body_;
-  const int64_t now_ns = clock_->unix_nanos();
+  const int64_t now_ns = unix_ns;
   const int64_t sec = now_ns / 1000000000 - (now_ns % 1000000000 < 0 ? 1 : 0);  // floor: amz_date's second
-  const Credentials& c = cr.value;
   if (!signed_valid_ || sec != signed_sec_ || c.access_key_id != signed_creds_.access_key_id ||
       c.secret_access_key != signed_creds_.secret_access_key || c.session_token != signed_creds_.session_token) {
     signer_.sign_prepared(prepared_, c, now_ns, &signed_headers_);
@@ -184,6 +173,37 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
     signed_creds_ = c;
     signed_valid_ = true;
   }
+}
+
+void HttpSqsApi::warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) {
+  if (!endpoint_status_.ok() || cancel_.stopped()) return;
+  // Credentials first: a refresh (IMDS, STS, a credential process) happens here, not inside
+  // the poll. Then the request signed for the second the poll is due in, and the connection.
+  auto cr = creds_.get(at_unix_ns);
+  if (cr.ok()) {
+    std::lock_guard<std::mutex> lk(prep_mu_);
+    sign_locked(queue_url, names, cr.value, at_unix_ns);
+  }
+  http_->warm();
+}
+
+Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
+                                      const std::vector<std::string>& names, bool* retryable,
+                                      bool* throttle, bool* expired, Nanos* retry_after) {
+  *retryable = *throttle = *expired = false;
+  *retry_after = 0;
+  const bool timed = http_->timing();
+  const int64_t t_sign = timed ? mono_ns() : 0;
+  auto cr = creds_.get(clock_->unix_nanos());
+  if (!cr.ok()) return Result<AttrMap>::Err(cr.status);
+
+  std::unique_lock<std::mutex> prep_lock(prep_mu_);
+  sign_locked(queue_url, names, cr.value, clock_->unix_nanos());
+  if (timed) sign_ns_.store(mono_ns() - t_sign, std::memory_order_relaxed);
+  HttpRequest req;
+  req.method = "POST";
+  req.target = url_.path.empty() ? "/" : url_.path;
+  req.body = prepared_body_;
   req.headers = signed_headers_;
   prep_lock.unlock();
 
@@ -254,6 +274,14 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
   }
 
   AttrMap out;
+  struct ParseTimer {
+    bool on;
+    std::atomic<int64_t>* out;
+    int64_t t0;
+    ~ParseTimer() {
+      if (on) out->store(mono_ns() - t0, std::memory_order_relaxed);
+    }
+  } parse_timer{timed, &parse_ns_, timed ? mono_ns() : 0};
   if (opts_.protocol == SqsProtocol::Query) {
     for (auto& [k, v] : xml_sqs_attributes(resp.body)) out[std::move(k)] = std::move(v);
   } else {
@@ -266,6 +294,14 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
       for (auto& [k, v] : attrs->obj) out[k] = v.is_string() ? v.str : json_serialize(v);
   }
   return Result<AttrMap>::Ok(std::move(out));
+}
+
+std::string HttpSqsApi::timing_json() const {
+  if (!http_ || !http_->timing()) return "";
+  std::string h = http_timing_json(http_->last_timing());
+  if (h.empty()) return "";
+  return "{\"sign\":" + std::to_string(sign_ns_.load(std::memory_order_relaxed)) + "," + h.substr(1, h.size() - 2) +
+         ",\"parse\":" + std::to_string(parse_ns_.load(std::memory_order_relaxed)) + "}";
 }
 
 Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,

@@ -51,6 +51,16 @@ class SqsApi {
   // True when a call writes an HTTP request through HttpClient, so work handed to set_on_wire
   // (http.h) runs while the call is in flight.
   virtual bool runs_on_wire_work() const { return false; }
+  // The last call's time breakdown as a JSON object ("" when not timed): set_timing below.
+  virtual std::string timing_json() const { return ""; }
+  // Pre-poll warm-up (Runner prewarm), just before a call due at unix time `at_unix_ns`: do
+  // now what the call would otherwise do first -- credentials, the request and its signature
+  // for that second, the connection check or dial. Sends nothing. Default: nothing.
+  virtual void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) {
+    (void)queue_url;
+    (void)names;
+    (void)at_unix_ns;
+  }
 };
 
 enum class SqsProtocol { Query, Json };
@@ -94,9 +104,21 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   std::string endpoint() const { return endpoint_; }
   Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }
   bool runs_on_wire_work() const override { return true; }
+  void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) override;
+  // Diagnostics: time each call -- credentials + signing, the HTTP phases (HttpTiming), the
+  // response parse -- for timing_json().
+  void set_timing(bool on) {
+    if (http_) http_->set_timing(on);
+  }
+  std::string timing_json() const override;
 
  private:
+  std::atomic<int64_t> sign_ns_{0}, parse_ns_{0};
   std::atomic<Nanos> wait_until_{0};
+  // The prepared request for (queue_url, names), signed for the second of `unix_ns` with `c`
+  // (cached per second); leaves the signed headers in signed_headers_. Needs prep_mu_.
+  void sign_locked(const std::string& queue_url, const std::vector<std::string>& names, const Credentials& c,
+                   int64_t unix_ns);
   // *retry_after: the extra initial delay of a throttle answered 429/503 with an integer
   // Retry-After (DefaultRetryer.RetryRules, getRetryAfterDelay); 0 otherwise.
   Result<AttrMap> call_once(const std::string& queue_url, const std::vector<std::string>& names,
@@ -182,6 +204,7 @@ class alignas(kCacheLine) SqsClient {
   const std::vector<std::string>& attribute_names() const { return names_; }
   std::shared_ptr<SqsApi> api() const { return api_; }
   void cancel() { api_->cancel(); }
+  void warm(int64_t at_unix_ns) { api_->warm(queue_url_, names_, at_unix_ns); }
 
  private:
   std::shared_ptr<SqsApi> api_;

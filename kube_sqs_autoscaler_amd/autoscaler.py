@@ -209,9 +209,10 @@ def new_sqs_client(target: TargetConfig, api):
     return native().SqsClient(api, target.queue_url, list(target.attribute_names))
 
 
-def loop_config(target: TargetConfig, pipeline_reads: bool = False):
+def loop_config(target: TargetConfig, pipeline_reads: bool = False, prewarm_ns: int = 0):
     c = native().LoopConfig()
     c.prefetch = pipeline_reads
+    c.prewarm_ns = prewarm_ns
     c.poll_period_ns = target.poll_period_ns
     c.scale_down_cool_down_ns = target.scale_down_cool_down_ns
     c.scale_up_cool_down_ns = target.scale_up_cool_down_ns
@@ -243,7 +244,7 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
                           credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
-    runner = nat.Runner(loop_config(target, cfg.pipeline_reads), sqs, scaler, clock, log)
+    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns), sqs, scaler, clock, log)
     return Worker(target, runner, sqs_api, kube_api, log)
 
 

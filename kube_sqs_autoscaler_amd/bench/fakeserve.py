@@ -4,7 +4,9 @@
 apiserver pairs serving Q bench queues (latency.start_fake_endpoints), prints one JSON line
 with their URLs and certificates, then answers commands on stdin, one per line:
 ``stats`` -> a JSON line of request / connection / signature counters and the replicas of every
-bench Deployment; ``quit`` -> stop the servers and exit (EOF on stdin does the same).
+bench Deployment; ``timings`` -> a JSON line with every served request's (wake-up delay, service
+time) in ns, per endpoint kind (HttpServer::timings), and clears them; ``quit`` -> stop the
+servers and exit (EOF on stdin does the same).
 """
 from __future__ import annotations
 
@@ -26,11 +28,12 @@ def main(argv=None) -> int:
     ap.add_argument("--kube-latency-ns", type=int, default=0)
     ap.add_argument("--cpus", default="", help="JSON list: the CPU list of each pair's threads")
     ap.add_argument("--queue-offset", type=int, default=0, help="number of the first bench queue served")
+    ap.add_argument("--hot", action="store_true", help="busy-polling servers that never sleep (HttpServer::set_hot)")
     a = ap.parse_args(argv)
     nat = native()
     cpus = json.loads(a.cpus) if a.cpus else None
     sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus,
-                                     a.queue_offset)
+                                     a.queue_offset, hot=a.hot)
     try:
         info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],
                 "kube": [{"url": k.url, "cert_pem": k.cert_pem} for k in kube]}
@@ -46,6 +49,11 @@ def main(argv=None) -> int:
                     "replicas": [kube[q % len(kube)].replicas("bench", deployment_name(a.queue_offset + q))
                                  for q in range(a.queues)],
                 }), flush=True)
+            elif cmd == "timings":
+                out = {"sqs": [t for s in sqs for t in s.timings()], "kube": [t for k in kube for t in k.timings()]}
+                for s in (*sqs, *kube):
+                    s.clear_timings()
+                print(json.dumps(out), flush=True)
             elif cmd == "quit":
                 break
     finally:

@@ -84,10 +84,12 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
 
 
 def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
-                         kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None, offset: int = 0):
+                         kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None, offset: int = 0,
+                         hot: bool = False):
     """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues numbered from
     ``offset`` (queue offset+q on pair q % n_servers): the 200 <-> 0 attribute cycle per queue
-    and one Deployment per queue. ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned)."""
+    and one Deployment per queue. ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned).
+    ``hot``: each server is one busy-polling thread that never sleeps (HttpServer::set_hot)."""
     sqs_servers, kube_servers = [], []
     for i in range(n_servers):
         sqs = nat.FakeSqsServer()
@@ -97,6 +99,8 @@ def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sq
         if cpus is not None:
             sqs.set_cpus(cpus[i])
             kube.set_cpus(cpus[i])
+        sqs.set_hot(hot)
+        kube.set_hot(hot)
         sqs.start("127.0.0.1", 0, tls)
         sqs.set_latency(sqs_latency_ns)
         kube.start("127.0.0.1", 0, tls)
@@ -131,13 +135,13 @@ class RemoteEndpoints:
     processes -- their threads do not share the autoscaler's process, allocator or CPU share."""
 
     def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int,
-                 cpus: Optional[List[List[int]]] = None, offset: int = 0):
+                 cpus: Optional[List[List[int]]] = None, offset: int = 0, hot: bool = False):
         import json
         import subprocess
         import sys
 
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        extra = ["--cpus", json.dumps(cpus)] if cpus is not None else []
+        extra = (["--cpus", json.dumps(cpus)] if cpus is not None else []) + (["--hot"] if hot else [])
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "kube_sqs_autoscaler_amd.bench.fakeserve", "--queues", str(queues), "--pairs",
              str(n_servers), "--tls", str(int(tls)), "--sqs-latency-ns", str(sqs_latency_ns), "--kube-latency-ns",
@@ -155,6 +159,14 @@ class RemoteEndpoints:
         import json
 
         self.proc.stdin.write("stats\n")
+        self.proc.stdin.flush()
+        return json.loads(self.proc.stdout.readline())
+
+    def timings(self) -> dict:
+        """{"sqs": [(wake_ns, service_ns), ...], "kube": [...]}, then cleared (fakeserve)."""
+        import json
+
+        self.proc.stdin.write("timings\n")
         self.proc.stdin.flush()
         return json.loads(self.proc.stdout.readline())
 
@@ -181,12 +193,18 @@ class BenchEnv:
 
     ``poll_period_ns``: every queue's ``--poll-period`` (0: back to back, the hot loop);
     ``stagger``: queue i of N starts i/N of a poll period late (Supervisor.stagger), so N
-    queues at one cadence do not poll in one burst."""
+    queues at one cadence do not poll in one burst. ``hot_endpoints``: every fake server is one
+    busy-polling thread (HttpServer::set_hot), awake whenever a request arrives, as a loaded
+    production endpoint is (supported with ``shared`` and ``process``). ``prewarm_ns``: the
+    loop's pre-poll warm-up (``--poll-prewarm``); it and ``busy_poll_ns`` may be lists, one
+    value per queue, cycled (paired comparisons within one run). ``timing``: the clients time every request's
+    phases (HttpTiming) and traced polls carry the breakdown (``detail``)."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", log_level: str = "info", sqs_protocol: str = "query",
-                 poll_period_ns: int = 0, stagger: bool = False):
+                 poll_period_ns: int = 0, stagger: bool = False, hot_endpoints: bool = False, prewarm_ns: int = 0,
+                 timing: bool = False):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -196,7 +214,7 @@ class BenchEnv:
         self.remote = None
         self.remotes = []
         if servers == "process":
-            self.remote = RemoteEndpoints(queues, 1, tls, sqs_latency_ns, kube_latency_ns)
+            self.remote = RemoteEndpoints(queues, 1, tls, sqs_latency_ns, kube_latency_ns, hot=hot_endpoints)
             self.remotes = [self.remote]
             self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
         elif servers == "processes":
@@ -206,7 +224,7 @@ class BenchEnv:
             self.kube_servers = [r.kube[0] for r in self.remotes]
         elif servers in ("shared", "per-queue"):
             self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
-                                                                       kube_latency_ns)
+                                                                       kube_latency_ns, hot=hot_endpoints)
         else:
             raise ValueError(f"servers must be shared, per-queue, process or processes, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
@@ -225,9 +243,11 @@ class BenchEnv:
         self.kube_apis, self.sqs_apis = [], []
         self.targets = []
         self.server_of = []  # queue -> index of the server pair that serves it
+        per_queue = lambda v, q: v[q % len(v)] if isinstance(v, (list, tuple)) else v  # noqa: E731
         for q in range(queues):
             si = q % n_servers
             sqs, kube = self.sqs_servers[si], self.kube_servers[si]
+            bp_q, pw_q = per_queue(busy_poll_ns, q), per_queue(prewarm_ns, q)
             rest = RestConfig(host=kube.url, bearer_token=TOKEN, insecure=tls)
             sqs_tls = None
             if tls:
@@ -238,10 +258,13 @@ class BenchEnv:
             t = TargetConfig(queue_url=queue_url(sqs.url, q), deployment=deployment_name(q), namespace="bench",
                              poll_period_ns=poll_period_ns, scale_up_cool_down_ns=0, scale_down_cool_down_ns=0,
                              scale_up_messages=100, scale_down_messages=10, max_pods=8, min_pods=1)
-            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=busy_poll_ns)
+            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=bp_q)
             scaler = new_pod_autoscaler(t, kube_api, self.log, self.clock)
             sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds,
-                                  tls=sqs_tls, busy_poll_ns=busy_poll_ns)
+                                  tls=sqs_tls, busy_poll_ns=bp_q)
+            if timing:
+                sqs_api.set_timing(True)
+                kube_api.set_timing(True)
             cfg = nat.LoopConfig()
             cfg.poll_period_ns = poll_period_ns
             cfg.scale_up_cool_down_ns = 0
@@ -249,6 +272,9 @@ class BenchEnv:
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
+            cfg.prewarm_ns = pw_q
+            if pipeline:
+                scaler.warm()  # connect the apiserver client, as --poll-prewarm does before a poll
             self.server_of.append(si)
             self.kube_apis.append(kube_api)
             self.sqs_apis.append(sqs_api)
@@ -294,6 +320,21 @@ class BenchEnv:
     def clear(self) -> None:
         for r in self.runners:
             r.clear_latencies()
+
+    def server_timings(self) -> dict:
+        """Every fake endpoint's per-request (wake-up delay, service time), then cleared."""
+        if self.remotes:
+            out = {"sqs": [], "kube": []}
+            for rem in self.remotes:
+                t = rem.timings()
+                out["sqs"] += t["sqs"]
+                out["kube"] += t["kube"]
+            return out
+        out = {"sqs": [t for x in self.sqs_servers for t in x.timings()],
+               "kube": [t for x in self.kube_servers for t in x.timings()]}
+        for x in (*self.sqs_servers, *self.kube_servers):
+            x.clear_timings()
+        return out
 
     def close(self) -> None:
         if self.remotes:
@@ -439,7 +480,8 @@ def _pct_ns(v: List[int], p: float) -> int:
 
 
 def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: str = "scale", pipeline: bool = True,
-                     busy_poll_ns: int = 0, tls: bool = False, skip: int = 2, servers: str = "process") -> Dict:
+                     busy_poll_ns: int = 0, tls: bool = False, skip: int = 2, servers: str = "process",
+                     hot_endpoints: bool = False, prewarm_ns: int = 0, timing: bool = False) -> Dict:
     """Poll -> patch latency at a production poll cadence, not back to back.
 
     The reference sleeps ``--poll-period`` (5 s by default) before every poll
@@ -457,7 +499,8 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
     import tempfile
 
     env = BenchEnv(queues, mode, tls=tls, pipeline=pipeline, busy_poll_ns=busy_poll_ns, servers=servers,
-                   poll_period_ns=poll_period_ns, stagger=True)
+                   poll_period_ns=poll_period_ns, stagger=True, hot_endpoints=hot_endpoints, prewarm_ns=prewarm_ns,
+                   timing=timing)
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: List[dict] = []
     try:
@@ -469,6 +512,7 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
             f.seek(0)
             spans += [json.loads(line) for line in f.read().decode().splitlines()][skip:]
         res = env.collect(polls, wall)
+        served = env.server_timings()
     finally:
         for f in files:
             f.close()
@@ -482,6 +526,8 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
         "mode": mode,
         "pipeline_reads": pipeline,
         "tls": tls,
+        "hot_endpoints": hot_endpoints,
+        "prewarm_us": prewarm_ns / 1e3,
         "p50_ms": round(_pct_ns(lat, 50) / 1e6, 4) if lat else None,
         "p90_ms": round(_pct_ns(lat, 90) / 1e6, 4) if lat else None,
         "p99_ms": round(_pct_ns(lat, 99) / 1e6, 4) if lat else None,
@@ -491,5 +537,33 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
         "signature_failures": res.signature_failures,
         "phase_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
                             "patch_us": med("patch_latency_ns")},
+        # The fake endpoints' side of each request (HttpServer::timings): how long the endpoint's
+        # thread took to wake up for it after the kernel received it, and to answer it.
+        "endpoint_median_us": {k: {"wake": _median_us([w for w, _ in v]), "service": _median_us([sv for _, sv in v])}
+                               for k, v in served.items()},
         "wall_s": round(wall, 2),
+        **({"call_phase_median_us": _detail_medians(scaled)} if timing else {}),
     }
+
+
+def _detail_medians(spans: List[dict]) -> Dict:
+    """Medians (us) of the per-call phases in the spans' ``detail`` (HttpTiming): for the SQS
+    call sign / pre (connection check, serialisation) / write / wait (until the kernel received
+    the answer) / wake (until this thread read it) / read / parse, and the same HTTP phases for
+    the replica write; ``spun``: the share of calls whose answer came while busy-polling."""
+    out: Dict[str, Dict] = {}
+    for call in ("sqs", "write"):
+        rows = [s["detail"][call] for s in spans if s.get("detail") and s["detail"].get(call)]
+        if not rows:
+            continue
+        d = {k: _median_us([r[k] for r in rows if r.get(k, -1) >= 0])
+             for k in ("sign", "pre", "write", "wait", "wake", "read", "parse") if k in rows[0]}
+        d["spun_share"] = round(sum(1 for r in rows if r.get("spun")) / len(rows), 3)
+        out[call] = d
+    return out
+
+
+def _median_us(v: List[int]):
+    import statistics
+
+    return round(statistics.median(v) / 1e3, 2) if v else None

@@ -30,6 +30,10 @@ Extensions (all off or reference-equivalent by default):
   ``action_likely``), so an idle queue reads the apiserver no more often than the reference.
 * ``--worker-processes``: one worker process per tracked queue (parallel/procfleet.py) instead
   of one thread per queue.
+* ``--poll-prewarm`` (default 1ms): the pre-poll warm-up (runner.h ``LoopConfig::prewarm``):
+  the signed SQS request, the bearer token and both connections are ready, and the core awake,
+  when the poll is due. The pipelined GET never dials inside the SQS call, so this is also what
+  connects the apiserver client before the first pipelined poll.
 * ``--sqs-endpoint`` / ``--sqs-protocol``, ``--api-timeout``, ``--log-level`` /
   ``--log-format``, ``--metrics-addr`` (+ ``--readiness-failure-window``), ``--trace-file``,
   ``--gpu-aware-max``.
@@ -49,6 +53,7 @@ DEFAULT_ATTRIBUTE_NAMES = (
 )  # /root/reference/main.go:28
 
 REFERENCE_MAX_PODS = 5  # /root/reference/main.go:90
+DEFAULT_POLL_PREWARM_NS = 1_000_000  # --poll-prewarm (runner.h LoopConfig::prewarm)
 MI355X_MAX_PODS = 8  # one GPU-worker pod per MI355X of an 8-GPU node
 
 SCALE_MODES = ("scale", "deployment", "patch")
@@ -101,6 +106,7 @@ class Config:
     worker_threads: int = 0
     worker_processes: bool = False
     busy_poll_ns: int = 25_000
+    poll_prewarm_ns: int = DEFAULT_POLL_PREWARM_NS
     kube_api_qps: float = 5.0
     kube_api_burst: int = 10
     trace_file: str = ""
@@ -170,6 +176,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.float64("kube-api-qps", 5.0, "Client-side limit on kube-apiserver requests per second for each tracked queue, as client-go's default rest client (0 disables)")
     fs.int("kube-api-burst", 10, "Requests allowed in a burst above -kube-api-qps (client-go default)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
+    fs.duration("poll-prewarm", DEFAULT_POLL_PREWARM_NS, "Before each poll, wake this long early to sign the SQS request, read the token and check (or dial) both connections, then start the poll on time; decisions are unchanged (0s disables)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
     fs.string("trace-file", "", "Append one JSON span per poll (depth, decisions, per-call latencies) to this file; empty disables")
@@ -289,6 +296,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         worker_threads=fs["worker-threads"],
         worker_processes=fs["worker-processes"],
         busy_poll_ns=fs["busy-poll"],
+        poll_prewarm_ns=fs["poll-prewarm"],
         kube_api_qps=fs["kube-api-qps"],
         kube_api_burst=fs["kube-api-burst"],
         trace_file=fs["trace-file"],
@@ -314,6 +322,8 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty, local or cluster')
     if cfg.worker_processes and cfg.worker_threads > 0:
         raise FlagError("-worker-processes and -worker-threads cannot be combined")
+    if cfg.poll_prewarm_ns < 0:
+        raise FlagError(f'invalid value "{cfg.poll_prewarm_ns}ns" for flag -poll-prewarm: must not be negative')
     if cfg.gpus_per_pod < 1:
         raise FlagError(f'invalid value "{cfg.gpus_per_pod}" for flag -gpus-per-pod: must be >= 1')
     return cfg

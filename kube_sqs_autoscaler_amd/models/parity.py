@@ -236,6 +236,7 @@ def run_wire(scenario: Scenario, mode: str = "scale", prefetch: bool = True, ser
     apiserver's own request counters must add up to the same GETs and writes.
     """
     from ..autoscaler import new_deployment_api, new_sqs_api
+    from ..config import DEFAULT_POLL_PREWARM_NS
     from ..kube.config import RestConfig
     from ..sqs.credentials import static_provider
     from .oracle import reference_gets, sample
@@ -275,6 +276,7 @@ def run_wire(scenario: Scenario, mode: str = "scale", prefetch: bool = True, ser
         cfg.scale_down_messages = p.down_msgs
         cfg.prefetch = prefetch
         cfg.prefetch_always = prefetch_always
+        cfg.prewarm_ns = DEFAULT_POLL_PREWARM_NS  # the CLI's pre-poll warm-up (dials before the pipelined GET)
         runner = nat.Runner(cfg, sqs, scaler, clock, log)
         trace = sorted(scenario.trace, key=lambda s: s[0])
         gets0, writes0, sqs0, sig0 = kube_srv.gets(), kube_srv.writes(), sqs_srv.requests(), sqs_srv.signature_failures()

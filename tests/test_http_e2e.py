@@ -310,6 +310,7 @@ def test_full_loop_pipelined_over_the_wire(nat, sqs_server, kube_server):
     cfg.prefetch = True
     r = nat.Runner(cfg, c, p, nat.RealClock(), capture_logger([]))
     r.arm()
+    p.warm()  # what --poll-prewarm does before a poll: the pipelined GET itself never dials
     sqs_server.set_attributes(url, {n: "100" for n in NAMES})
     recs = r.steps(4)
     assert [x["up"] for x in recs] == ["scaled", "scaled", "noop", "noop"] and all(x["prefetched"] for x in recs)
@@ -341,6 +342,7 @@ def test_idle_queue_sends_no_speculative_gets(nat, sqs_server, kube_server):
     cfg.scale_up_cool_down_ns = 10 * 10**9
     cfg.scale_down_cool_down_ns = 30 * 10**9
     cfg.prefetch = True
+    cfg.prewarm_ns = 10**6  # the CLI default: connections are checked (or dialled) before a poll
     r = nat.Runner(cfg, c, p, clock, capture_logger([]))
     r.arm()
     sqs_server.set_attributes(url, {n: "0" for n in NAMES})

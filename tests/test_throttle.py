@@ -112,6 +112,7 @@ def test_speculative_read_never_waits_for_the_throttle(nat, always):
         cfg.prefetch_always = always
         r = nat.Runner(cfg, env.runners[0].sqs, scaler, env.clock, env.log)
         r.arm()
+        scaler.warm()  # connected, as --poll-prewarm leaves it (the pipelined GET never dials)
         t0 = time.perf_counter()
         recs = [r.poll_once() for _ in range(20)]
         assert time.perf_counter() - t0 < 0.5  # no poll waited for a token
