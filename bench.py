@@ -72,21 +72,33 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
     """Poll->patch latency at production poll periods (250 ms and 1 s; the reference's default
     is 5 s, /root/reference/main.go:83): ``--cadence-queues`` queues, one thread each, staggered
     over the period, against one endpoint process serving them all (bench/latency.py
-    ``measure_cadenced``). Default path and reference-equivalent path, plain and TLS, with
-    per-phase medians. Each row keeps >= 400 samples."""
+    ``measure_cadenced``). Default path (with the CLI's --poll-prewarm) and reference-equivalent
+    path, plain and TLS, with per-phase medians; the plain rows also break every call down
+    (HttpTiming) and report the fake endpoints' own wake-up and service times. The ``_hot_endpoints``
+    rows at 1 s serve the same polls from endpoints that never sleep (a loaded production
+    endpoint): the difference is what the fakes' own idle wake-ups add. Each row keeps >= 400
+    samples."""
     from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced
+    from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS
 
     ms = 1_000_000
     p50, rows = {}, {}
+    # (row, mode, pipelined, busy-poll, pre-poll warm-up): the CLI default, and the reference's path
+    paths = (("default", args.mode, pipeline, bp, DEFAULT_POLL_PREWARM_NS), ("reference_equivalent", "deployment", False, 0, 0))
     for label, period in (("250ms", 250 * ms), ("1s", 1000 * ms)):
-        for name, mode, pl, b in (("default", args.mode, pipeline, bp), ("reference_equivalent", "deployment", False, 0)):
-            for tls in (False, True):
-                key = name + ("_tls" if tls else "")
-                r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls)
+        for name, mode, pl, b, pw in paths:
+            for tls, hot in ((False, False), (True, False), (False, True)):
+                if hot and label != "1s":
+                    continue
+                key = name + ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
+                # timing: every call's phases (HttpTiming) in the spans, for the attribution
+                r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls,
+                                     hot_endpoints=hot, prewarm_ns=pw, timing=not tls)
                 rows.setdefault(label, {})[key] = r
                 p50.setdefault(label, {})[key] = r["p50_ms"]
     return {
         "cadenced_p50_ms": p50,
+        "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
         "cadenced_rows": rows,
         "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()},
     }

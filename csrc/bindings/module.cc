@@ -939,17 +939,19 @@ PYBIND11_MODULE(_ksa_native, m) {
 
   // ---- fakes ----
   py::class_<InjectedFault>(m, "InjectedFault")
-      .def(py::init([](int status, std::string body, std::string ct, bool drop, std::string retry_after) {
+      .def(py::init([](int status, std::string body, std::string ct, bool drop, std::string retry_after,
+                       std::string method) {
              InjectedFault f;
              f.status = status;
              f.body = std::move(body);
              f.content_type = std::move(ct);
              f.drop_connection = drop;
              f.retry_after = std::move(retry_after);
+             f.method = std::move(method);
              return f;
            }),
            py::arg("status") = 500, py::arg("body") = "", py::arg("content_type") = "text/plain",
-           py::arg("drop_connection") = false, py::arg("retry_after") = "");
+           py::arg("drop_connection") = false, py::arg("retry_after") = "", py::arg("method") = "");
 
   py::class_<FakeSqsServer, std::shared_ptr<FakeSqsServer>>(m, "FakeSqsServer")
       .def(py::init<>())

@@ -11,11 +11,15 @@ namespace ksa {
 
 namespace {
 
-bool pop_fault(std::vector<InjectedFault>* faults, InjectedFault* out) {
-  if (faults->empty()) return false;
-  *out = faults->front();
-  faults->erase(faults->begin());
-  return true;
+// The first queued fault for a request with `method` (a fault may name one).
+bool pop_fault(std::vector<InjectedFault>* faults, const std::string& method, InjectedFault* out) {
+  for (auto it = faults->begin(); it != faults->end(); ++it) {
+    if (!it->method.empty() && it->method != method) continue;
+    *out = std::move(*it);
+    faults->erase(it);
+    return true;
+  }
+  return false;
 }
 
 void apply_fault(const InjectedFault& f, HttpResponse* resp) {
@@ -145,7 +149,7 @@ void FakeSqsServer::handle(const HttpRequest& req, HttpResponse* resp) {
     last_body_.swap(body_copy);
     last_headers_.swap(headers_copy);
     latency = latency_;
-    faulted = pop_fault(&faults_, &fault);
+    faulted = pop_fault(&faults_, req.method, &fault);
     verify = verify_;
     akid = akid_;
     secret = secret_;
@@ -559,7 +563,7 @@ void FakeKubeServer::handle(const HttpRequest& req, HttpResponse* resp) {
     last_body_.swap(body_copy);
     last_path_.swap(path_copy);
     latency = latency_;
-    faulted = pop_fault(&faults_, &fault);
+    faulted = pop_fault(&faults_, req.method, &fault);
     token = token_;
   }
   if (latency > 0) shutdown_.wait_for(latency);

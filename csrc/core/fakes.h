@@ -30,6 +30,7 @@ struct InjectedFault {
   std::string content_type = "text/plain";
   bool drop_connection = false;  // close the socket without responding
   std::string retry_after;       // Retry-After header value ("" = none)
+  std::string method;            // only requests with this method ("" = any)
 };
 
 class FakeSqsServer {

@@ -418,11 +418,19 @@ Result<ScaleObject> KubeRestDeployments::parse_get(ScaleMode m, const Status& s,
 bool KubeRestDeployments::try_fallback(const Status& s, const std::string& name,
                                        Result<ScaleObject>* deployment) {
   if (!opts_.rbac_fallback || mode() == ScaleMode::Deployment) return false;
-  // 403: RBAC refuses deployments/scale. 404 only when it names no object -- the route is
-  // missing ("the server could not find the requested resource"), not the Deployment.
+  // 403 only when RBAC refuses the subresource itself: its message names it ("User ... cannot
+  // get resource \"deployments/scale\" in API group \"apps\" ..."). An admission webhook
+  // (Gatekeeper, Kyverno) or a quota also answers 403, but it judged this write: sending the
+  // same write to the whole Deployment would step around a policy that only matches
+  // deployments/scale. 404 only when it names no object -- the route is missing ("the server
+  // could not find the requested resource"), not the Deployment.
+  const std::string& m = s.message();
+  const bool rbac_refusal = s.code() == 403 && m.find(" cannot ") != std::string::npos &&
+                            m.find("resource \"deployments/scale\"") != std::string::npos &&
+                            m.find("admission webhook") == std::string::npos;
   const bool missing_route =
-      s.code() == 404 && s.message().rfind("the server could not find the requested resource", 0) == 0;
-  if (s.code() != 403 && !missing_route) return false;
+      s.code() == 404 && m.rfind("the server could not find the requested resource", 0) == 0;
+  if (!rbac_refusal && !missing_route) return false;
   // Can the Deployment itself be read? If not, the /scale error stands and the mode is kept.
   auto d = get_in(ScaleMode::Deployment, name);
   if (!d.ok()) return false;

@@ -248,5 +248,5 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     return Worker(target, runner, sqs_api, kube_api, log)
 
 
-def load_rest_config(cfg: Config, environ: Optional[Mapping[str, str]] = None) -> RestConfig:
-    return build_config_from_flags(cfg.kube_config_path, environ)
+def load_rest_config(cfg: Config, environ: Optional[Mapping[str, str]] = None, klog=None) -> RestConfig:
+    return build_config_from_flags(cfg.kube_config_path, environ, klog=klog)

@@ -60,13 +60,14 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     clock = nat.RealClock()
     log = make_logger(cfg.log_level, cfg.log_format, clock=None)
 
-    # scale.NewPodAutoScaler -> clientcmd.BuildConfigFromFlags("", KUBE_CONFIG_PATH)
+    # scale.NewPodAutoScaler -> clientcmd.BuildConfigFromFlags("", KUBE_CONFIG_PATH); client-go's
+    # own warnings there are klog lines, as the reference's are (utils/klog.py)
+    from .utils.klog import Klog
+
     try:
-        rest = autoscaler.load_rest_config(cfg, env)
+        rest = autoscaler.load_rest_config(cfg, env, klog=Klog())
     except KubeConfigError as e:
         return _panic("Failed to configure incluster or local config", str(e))
-    for w in rest.warnings:
-        log.log("warning", w)
     try:
         w = autoscaler.prepare_kube_auth(rest, clock, cfg.api_timeout_ns)
     except autoscaler.KubeClientError as e:

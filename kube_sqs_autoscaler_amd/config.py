@@ -30,7 +30,7 @@ Extensions (all off or reference-equivalent by default):
   ``action_likely``), so an idle queue reads the apiserver no more often than the reference.
 * ``--worker-processes``: one worker process per tracked queue (parallel/procfleet.py) instead
   of one thread per queue.
-* ``--poll-prewarm`` (default 1ms): the pre-poll warm-up (runner.h ``LoopConfig::prewarm``):
+* ``--poll-prewarm`` (default 200us): the pre-poll warm-up (runner.h ``LoopConfig::prewarm``):
   the signed SQS request, the bearer token and both connections are ready, and the core awake,
   when the poll is due. The pipelined GET never dials inside the SQS call, so this is also what
   connects the apiserver client before the first pipelined poll.
@@ -53,7 +53,7 @@ DEFAULT_ATTRIBUTE_NAMES = (
 )  # /root/reference/main.go:28
 
 REFERENCE_MAX_PODS = 5  # /root/reference/main.go:90
-DEFAULT_POLL_PREWARM_NS = 1_000_000  # --poll-prewarm (runner.h LoopConfig::prewarm)
+DEFAULT_POLL_PREWARM_NS = 200_000  # --poll-prewarm (runner.h LoopConfig::prewarm)
 MI355X_MAX_PODS = 8  # one GPU-worker pod per MI355X of an 8-GPU node
 
 SCALE_MODES = ("scale", "deployment", "patch")

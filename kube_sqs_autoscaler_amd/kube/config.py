@@ -52,7 +52,6 @@ class RestConfig:
     exec_plugin: Optional["ExecPlugin"] = None
     auth_provider: str = ""  # kubeconfig auth-provider name (unsupported, like the reference)
     source: str = ""
-    warnings: list = field(default_factory=list)
     # shared per-config state (the exec authenticator), like client-go's authenticator cache
     shared: dict = field(default_factory=dict, repr=False, compare=False)
 
@@ -191,16 +190,25 @@ def load_kubeconfig(path: str, context: str = "") -> RestConfig:
 
 
 def build_config_from_flags(kube_config_path: str, environ: Optional[Mapping[str, str]] = None,
-                            sa_dir: str = SA_DIR) -> RestConfig:
-    """clientcmd.BuildConfigFromFlags("", kube_config_path)."""
+                            sa_dir: str = SA_DIR, klog=None) -> RestConfig:
+    """clientcmd.BuildConfigFromFlags("", kube_config_path).
+
+    Without a path client-go warns through klog before trying the in-cluster config, and again
+    when that fails and it falls back to the default loading rules, which -- with no explicit
+    path -- find nothing ("no configuration has been provided"). ``klog``: a utils/klog.Klog
+    for those two lines (None: not written)."""
+    from ..utils import klog as k
+
     if not kube_config_path:
-        warnings = ["Neither --kubeconfig nor --master was specified.  Using the inClusterConfig.  This might not work."]
+        if klog is not None:
+            klog.warning("Neither --kubeconfig nor --master was specified.  Using the inClusterConfig.  This might not work.",
+                         k.CLIENT_CONFIG_GO, k.NEITHER_LINE)
         try:
-            rc = in_cluster_config(environ, sa_dir)
-            rc.warnings = warnings
-            return rc
+            return in_cluster_config(environ, sa_dir)
         except KubeConfigError as e:
+            if klog is not None:
+                klog.warning(f"error creating inClusterConfig, falling back to default config: {e}",
+                             k.CLIENT_CONFIG_GO, k.FALLBACK_LINE)
             raise KubeConfigError(
-                f"error creating inClusterConfig, falling back to default config: {e}; "
                 "invalid configuration: no configuration has been provided, try setting KUBERNETES_MASTER environment variable")
     return load_kubeconfig(kube_config_path)

@@ -88,9 +88,11 @@ class LeaseLock:
         self.name = name
         self.http = new_http_client(rest, int(timeout_s * 1e9))
         self._rv = ""
-        # Real-time (time.monotonic) instant by which every call must have returned; None: each
-        # call only has the client's own timeout. The elector sets it to the renew deadline.
+        # Instant by which every call must have returned, on ``self.monotonic`` (the elector's
+        # clock: LeaderElector points it at its own, so the renew deadline and the per-call limit
+        # share one time base); None: each call only has the client's own timeout.
         self.deadline: Optional[float] = None
+        self.monotonic: Callable[[], float] = time.monotonic
 
     def _headers(self, body: bool = False):
         from ..autoscaler import auth_headers
@@ -110,7 +112,7 @@ class LeaseLock:
 
         timeout_ns = -1
         if self.deadline is not None:
-            left = self.deadline - time.monotonic()
+            left = self.deadline - self.monotonic()
             if left <= 0:
                 raise LeaseError("renew deadline exceeded")
             timeout_ns = max(1, int(left * 1e9))
@@ -168,6 +170,7 @@ class LeaderElector:
         self.renew_deadline = renew_deadline_s
         self.retry_period = retry_period_s
         self.monotonic = monotonic
+        lock.monotonic = monotonic  # the lock's per-call deadline is set on this clock
         self.wall = wall
         self.log = log or (lambda level, msg: None)
         self.observed: Optional[LeaderElectionRecord] = None
@@ -269,7 +272,7 @@ class LeaderElector:
                 if remaining <= 0:
                     lose()
                     break
-                self.lock.deadline = time.monotonic() + remaining
+                self.lock.deadline = self.monotonic() + remaining
                 ok = self.try_acquire_or_renew()
                 with mu:
                     if ok and not lost.is_set():  # a success after the deadline does not count

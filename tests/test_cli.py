@@ -34,7 +34,8 @@ def test_bad_flag_exits_two():
 
 def test_no_kube_config_panics_like_reference():
     r = run_cli("--sqs-queue-url=x", env={"KUBERNETES_SERVICE_HOST": ""})
-    assert r.returncode == 2 and r.stderr.startswith("panic: Failed to configure incluster or local config")
+    # after client-go's two klog warnings (tests/test_klog.py)
+    assert r.returncode == 2 and r.stderr.splitlines()[2] == "panic: Failed to configure incluster or local config"
 
 
 @pytest.fixture

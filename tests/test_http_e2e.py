@@ -342,7 +342,7 @@ def test_idle_queue_sends_no_speculative_gets(nat, sqs_server, kube_server):
     cfg.scale_up_cool_down_ns = 10 * 10**9
     cfg.scale_down_cool_down_ns = 30 * 10**9
     cfg.prefetch = True
-    cfg.prewarm_ns = 10**6  # the CLI default: connections are checked (or dialled) before a poll
+    cfg.prewarm_ns = 200_000  # the CLI default: connections are checked (or dialled) before a poll
     r = nat.Runner(cfg, c, p, clock, capture_logger([]))
     r.arm()
     sqs_server.set_attributes(url, {n: "0" for n in NAMES})
@@ -610,3 +610,57 @@ def test_signature_reused_only_within_its_second_and_credentials(nat, sqs_server
     assert seen[0] == seen[1] == seen[2]  # same second, same credentials
     assert seen[3][0] != seen[2][0] and seen[3][1] != seen[2][1]  # next second: signed again
     assert seen[4][0] == seen[3][0] and seen[4][2] == "t2" and seen[4][1] != seen[3][1]  # rotated token
+
+
+def test_webhook_denial_is_not_retried_through_the_deployment(nat, kube_server):
+    """A 403 from an admission webhook (Gatekeeper, Kyverno) judged the write itself: the /scale
+    -> Deployment fallback is for RBAC refusing the subresource only, or the same write would
+    step around a policy that matches deployments/scale."""
+    import json
+
+    lines = []
+    p, api = scaler(nat, kube_server, "scale", lines=lines)
+    status = {"kind": "Status", "apiVersion": "v1", "status": "Failure", "reason": "Forbidden", "code": 403,
+              "message": 'admission webhook "validate.kyverno.svc-fail" denied the request: resource Deployment/ml/worker '
+                         'was blocked: replicas must stay under policy'}
+    kube_server.inject(1, nat.InjectedFault(403, json.dumps(status), "application/json", method="PUT"))
+    with pytest.raises(nat.NativeError, match="admission webhook"):
+        p.scale_up()
+    assert kube_server.replicas("ml", "worker") == 3  # nothing was written through the Deployment
+    assert str(api.mode) == "ScaleMode.Scale" and api.stats()["scale_fallbacks"] == 0
+    assert not any("not usable" in l for l in lines)
+    assert kube_server.last_method() == "PUT" and kube_server.last_path().endswith("/scale")
+    assert p.scale_up().wrote and kube_server.replicas("ml", "worker") == 4  # still /scale afterwards
+
+
+def test_pipelined_get_never_dials_inside_the_sqs_call(nat, sqs_server):
+    """An apiserver that accepts TCP but never completes the TLS handshake: the pipelined GET is
+    not sent from inside the SQS call (it would dial on the SQS call's deadline), so the depth
+    read succeeds at once; the synchronous GET then times out on its own deadline."""
+    import socket
+    import time
+
+    tarpit = socket.socket()
+    tarpit.bind(("127.0.0.1", 0))
+    tarpit.listen(8)
+    try:
+        host = f"https://127.0.0.1:{tarpit.getsockname()[1]}"
+        api = new_deployment_api(RestConfig(host=host, bearer_token=TOKEN, insecure=True), "ml", "scale",
+                                 timeout_ns=1_500_000_000)
+        p = nat.PodAutoScaler(api, "worker", "ml", 5, 1, 1, 1, capture_logger([]), nat.RealClock())
+        c, _, url = sqs_client(nat, sqs_server)
+        sqs_server.set_attributes(url, {n: "100" for n in NAMES})
+        cfg = nat.LoopConfig()
+        cfg.poll_period_ns = 0
+        cfg.scale_up_cool_down_ns = 0
+        cfg.prefetch = True
+        r = nat.Runner(cfg, c, p, nat.RealClock(), capture_logger([]))
+        r.arm()
+        t0 = time.perf_counter()
+        rec = r.steps(1)[0]
+        assert rec["depth"] == 300 and not rec["prefetched"]
+        assert rec["depth_ns"] < 500_000_000  # the SQS call did not wait for the apiserver
+        assert rec["up"] == "failed" and "timeout" in rec["error"]
+        assert time.perf_counter() - t0 < 10
+    finally:
+        tarpit.close()

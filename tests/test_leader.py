@@ -205,3 +205,41 @@ def test_hanging_renewal_loses_leadership_at_the_deadline(nat, kube):
         th.join(timeout=10)
     assert not th.is_alive()
     assert len(lost_at) == 1
+
+
+def test_lock_deadline_uses_the_electors_clock():
+    """The renew deadline handed to the lock and the lock's per-call limit share one time base
+    (an injected clock far from time.monotonic must not expire every call)."""
+    from kube_sqs_autoscaler_amd.kube.leader import LeaderElector
+
+    class Lock:
+        deadline = None
+        monotonic = None
+        calls = []
+
+        def describe(self):
+            return "ns/lease"
+
+        def get(self):
+            # the time left before the deadline, on the lock's clock, as _call computes it
+            self.calls.append(self.deadline - self.monotonic() if self.deadline is not None else None)
+            return None
+
+        def create(self, rec):
+            pass
+
+    clock = [1e9]  # nowhere near time.monotonic()
+    lock = Lock()
+    el = LeaderElector(lock, "me", 15, 10, 0.01, monotonic=lambda: clock[0], wall=lambda: 0.0)
+    assert lock.monotonic() == 1e9
+    import threading
+
+    stop = threading.Event()
+    t = threading.Thread(target=el.renew_loop, args=(stop, lambda: None))
+    t.start()
+    import time
+
+    time.sleep(0.1)
+    stop.set()
+    t.join()
+    assert lock.calls and all(c is not None and 0 < c <= 10 for c in lock.calls)
