@@ -18,7 +18,8 @@ from ..ops import native
 
 
 class Fleet:
-    """``threads`` <= 0 or >= len(workers): one native thread per queue (``Supervisor``);
+    """``threads`` <= 0 or >= len(workers): one native thread per queue (``Supervisor``, with a
+    staggered start: each queue's Run() entry, main.go:37-38, is spread over its first period);
     otherwise ``threads`` workers share the queues through the native ``Scheduler`` (a timer
     heap that keeps every queue's sleep-then-poll cadence), for processes tracking hundreds of
     queues."""
@@ -27,7 +28,13 @@ class Fleet:
         self.workers = list(workers)
         nat = native()
         self.pooled = 0 < threads < len(self.workers)
-        self._sup = nat.Scheduler(threads) if self.pooled else nat.Supervisor()
+        if self.pooled:
+            self._sup = nat.Scheduler(threads)  # staggered by default
+        else:
+            # queue i of N starts i/N of its poll period late (as the pooled Scheduler does), so N
+            # queues at one cadence do not all poll in the same instant every period
+            self._sup = nat.Supervisor()
+            self._sup.stagger = True
         for w in self.workers:
             self._sup.add(w.runner)
         self._started = False

@@ -11,14 +11,15 @@ kube_sqs_autoscaler_amd.tune --distributed ...``). Every rank:
 3. all-gathers the per-configuration outputs over ``torch.distributed``. The backend is
    ``nccl`` (RCCL over xGMI on an MI355X node) when the GPUs run the sweep, ``gloo`` on CPU.
 
-The outputs are a few dozen bytes per configuration, so the collective is one small
-all-gather per output field; the simulation dominates. Every rank ends with the full result,
+The outputs are a few dozen bytes per configuration: every field is packed into one int64
+row per configuration, so a sweep makes one all-gather (plus one all-reduce of the kernel
+time), not one per field; the simulation dominates. Every rank ends with the full result,
 bit-identical to a single-process sweep of the whole grid (``tests/test_tune_distributed.py``).
 """
 from __future__ import annotations
 
 import os
-from typing import List, Tuple
+from typing import Dict, List, Tuple
 
 import numpy as np
 
@@ -87,6 +88,25 @@ class Group:
         self.dist.all_gather(parts, t)
         return np.concatenate([p.cpu().numpy()[:n] for p, n in zip(parts, counts)], axis=0)
 
+    def all_gather_fields(self, out: Dict[str, np.ndarray], counts: List[int]) -> Dict[str, np.ndarray]:
+        """:meth:`all_gather_rows` of every output field at once: the fields (int32 / int64,
+        one row per configuration) are packed side by side into one int64 array -- exact for
+        both -- gathered in one collective, and split back to their own dtypes and shapes."""
+        keys = sorted(out)  # the same order on every rank
+        widths = [int(np.prod(out[k].shape[1:], dtype=np.int64)) for k in keys]
+        rows = out[keys[0]].shape[0] if keys else 0
+        packed = np.empty((rows, sum(widths)), dtype=np.int64)
+        off = 0
+        for k, w in zip(keys, widths):
+            packed[:, off:off + w] = out[k].reshape(rows, w)
+            off += w
+        full = self.all_gather_rows(packed, counts)
+        res, off = {}, 0
+        for k, w in zip(keys, widths):
+            res[k] = full[:, off:off + w].astype(out[k].dtype).reshape((full.shape[0],) + out[k].shape[1:])
+            off += w
+        return res
+
     def max(self, x: float) -> float:
         if self.world == 1:
             return x
@@ -112,7 +132,7 @@ def run_open_loop(g: Group, trace: sweep.Trace, params: np.ndarray, init_replica
     else:  # more ranks than configurations
         out = {k: np.zeros(0, dtype=np.int64 if k in sweep.OUT64 else np.int32) for k in sweep.OUT64 + sweep.OUT32}
         kernel_ms = 0.0
-    full = {k: g.all_gather_rows(np.ascontiguousarray(v), counts) for k, v in out.items()}
+    full = g.all_gather_fields(out, counts)
     return sweep.SweepResult(params, full, g.device, g.max(kernel_ms))
 
 
@@ -131,5 +151,5 @@ def run_closed_loop(g: Group, trace: closedloop.ArrivalTrace, params: np.ndarray
         out = {k: np.zeros((0, seeds), dtype=np.int64 if k in closedloop.OUT64 else np.int32)
                for k in closedloop.OUT64 + closedloop.OUT32}
         kernel_ms = 0.0
-    full = {k: g.all_gather_rows(np.ascontiguousarray(v), counts) for k, v in out.items()}
+    full = g.all_gather_fields(out, counts)
     return closedloop.ClosedLoopResult(params, seeds, full, g.device, horizon_ns, g.max(kernel_ms))

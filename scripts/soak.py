@@ -1,81 +1,286 @@
-"""Soak: the headline configuration (one queue, /scale, pipelined read, busy-poll) polling back to
-back for --minutes against the localhost fakes, one JSON line per --window seconds: polls, p50 /
-p99 / max latency of the window, errors, RSS of this process. A leak shows as RSS growth, a
-slowdown as p50 drift, a stall as a window with few polls. Ends with a summary line.
+"""Soak: the CLI at a production cadence against failing endpoints, then a replay of its spans.
 
-    python scripts/soak.py --minutes 5 --window 10 > gpurun_out/soak.jsonl
+Starts TLS fake SQS and kube-apiserver endpoints in this process and runs the real CLI
+(``python -m kube_sqs_autoscaler_amd``) as a child tracking ``--queues`` queues at
+``--poll-period`` with short cool-downs, so it scales up and down all the time (each queue's
+depth is a square wave of its own period). While it runs, a fault schedule hits it:
+
+* apiserver 503 with ``Retry-After: 1`` (client-go retries after the wait), plain 500s,
+  409 conflicts (a concurrent write after the GET) and dropped connections;
+* SQS throttles (503 ``RequestThrottled`` with ``Retry-After: 1``; the SDK retryer backs off)
+  and dropped connections;
+* a bearer-token rotation half-way: the token file is rewritten and the apiserver accepts only
+  the new token, so the next apiserver call gets a 401 and the client re-reads the file.
+
+Every ``--window`` seconds it prints one JSON line: the child's open fds, threads and RSS, the
+poll and failure counters from its ``/metrics``, and the faults injected so far. At the end the
+child is stopped with SIGTERM and every queue's ``--trace-file`` spans are replayed through
+models/replay.py: each cool-down gate, no-op and clamp the loop decided must be the reference's
+(/root/reference/main.go:40-78, scale/scale.go:54-107) given the inputs the spans recorded. The
+summary line has the mismatch count (must be 0) and whether fds / threads / RSS stayed flat.
+
+    python scripts/soak.py --minutes 10 --queues 8 --poll-period 1s > gpurun_out/soak.jsonl
+
+``--hot``: the old back-to-back soak of one queue (no faults), p50/p99 per window.
 """
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import tempfile
+import threading
 import time
+import urllib.request
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
-from kube_sqs_autoscaler_amd.bench.latency import BenchEnv  # noqa: E402
+AKID, SECRET, REGION = "AKIDSOAK", "soak/secret", "us-east-1"
+S = 1_000_000_000
+THROTTLE = ('<?xml version="1.0"?><ErrorResponse><Error><Type>Sender</Type><Code>RequestThrottled</Code>'
+            '<Message>Rate exceeded</Message></Error><RequestId>soak</RequestId></ErrorResponse>')
+HIGH = {"ApproximateNumberOfMessages": "400", "ApproximateNumberOfMessagesDelayed": "50",
+        "ApproximateNumberOfMessagesNotVisible": "50"}
+LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed": "0",
+       "ApproximateNumberOfMessagesNotVisible": "0"}
 
 
-def rss_kb() -> int:
-    with open("/proc/self/status") as f:
+def proc_stats(pid: int) -> dict:
+    out = {"fds": len(os.listdir(f"/proc/{pid}/fd"))}
+    with open(f"/proc/{pid}/status") as f:
         for line in f:
             if line.startswith("VmRSS:"):
-                return int(line.split()[1])
-    return 0
+                out["rss_kb"] = int(line.split()[1])
+            elif line.startswith("Threads:"):
+                out["threads"] = int(line.split()[1])
+    return out
 
 
-def pct(v, p):
-    return v[min(len(v) - 1, max(0, int(p / 100.0 * len(v) + 0.5) - 1))] if v else 0
+def scrape(port: int) -> dict:
+    text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    tot = {}
+    for line in text.splitlines():
+        if line.startswith("#") or "{" not in line:
+            continue
+        name = line.split("{", 1)[0]
+        if name.endswith("_total"):
+            tot[name[4:-6]] = tot.get(name[4:-6], 0) + float(line.rsplit(" ", 1)[1])
+    return {k: int(v) for k, v in tot.items() if k in (
+        "polls", "scale_ups", "scale_downs", "depth_errors", "failed_ups", "failed_downs", "sqs_retries",
+        "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors")}
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--minutes", type=float, default=5.0)
-    ap.add_argument("--window", type=float, default=10.0)
-    ap.add_argument("--busy-poll-us", type=int, default=25)
-    a = ap.parse_args()
-    env = BenchEnv(1, "scale", pipeline=True, busy_poll_ns=a.busy_poll_us * 1000)
-    runner = env.runners[0]
-    out = []
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def cadenced(a) -> int:
+    import yaml
+
+    from kube_sqs_autoscaler_amd.models.oracle import Params
+    from kube_sqs_autoscaler_amd.models.replay import group_spans, replay_queue
+    from kube_sqs_autoscaler_amd.ops import native
+    from kube_sqs_autoscaler_amd.utils.goflag import parse_duration
+
+    nat = native()
+    period = parse_duration(a.poll_period)
+    up_cool, down_cool = parse_duration(a.up_cool_down), parse_duration(a.down_cool_down)
+    tmp = tempfile.mkdtemp(prefix="ksa-soak-")
+    tokens = ["soak-token-1", "soak-token-2"]
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, REGION)
+    sqs.start("127.0.0.1", 0, True)
+    kube = nat.FakeKubeServer()
+    kube.require_token(tokens[0])
+    kube.start("127.0.0.1", 0, True)
+    token_file = os.path.join(tmp, "token")
+    with open(token_file, "w") as f:
+        f.write(tokens[0])
+    ca = os.path.join(tmp, "sqs-ca.pem")
+    with open(ca, "w") as f:
+        f.write(sqs.cert_pem)
+    import base64
+
+    kc = os.path.join(tmp, "kubeconfig")
+    with open(kc, "w") as f:
+        yaml.safe_dump({"current-context": "s", "contexts": [{"name": "s", "context": {"cluster": "c", "user": "u"}}],
+                        "clusters": [{"name": "c", "cluster": {"server": kube.url, "certificate-authority-data":
+                                                               base64.b64encode(kube.cert_pem.encode()).decode()}}],
+                        "users": [{"name": "u", "user": {"tokenFile": token_file}}]}, f)
+    urls = [f"{sqs.url}/000000000000/soak-{q}" for q in range(a.queues)]
+    for q in range(a.queues):
+        kube.add_deployment("soak", f"workers-{q}", 1)
+    waves = [(20 + 7 * q) * S for q in range(a.queues)]  # each queue's square-wave period
+
+    def set_depths(t_ns: int) -> None:
+        for q, url in enumerate(urls):
+            sqs.set_attributes(url, HIGH if (t_ns % waves[q]) < waves[q] // 2 else LOW)
+
+    set_depths(0)
+    trace = os.path.join(tmp, "spans.jsonl")
+    port = free_port()
+    args = [sys.executable, "-m", "kube_sqs_autoscaler_amd", f"--poll-period={a.poll_period}",
+            f"--scale-up-cool-down={a.up_cool_down}", f"--scale-down-cool-down={a.down_cool_down}", "--max-pods=8",
+            f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", f"--trace-file={trace}",
+            f"--metrics-addr=127.0.0.1:{port}", "--log-level=error", "--api-timeout=10s"]
+    args += [f"--queue=url={u},deployment=workers-{q},namespace=soak" for q, u in enumerate(urls)]
+    env = dict(os.environ, AWS_ACCESS_KEY_ID=AKID, AWS_SECRET_ACCESS_KEY=SECRET, KUBE_CONFIG_PATH=kc,
+               AWS_CA_BUNDLE=ca, HOME=tmp)
+    err = open(os.path.join(tmp, "stderr.log"), "w")
+    child = subprocess.Popen(args, cwd=ROOT, env=env, stderr=err, stdout=subprocess.DEVNULL)
+    injected = {"kube_503_retry_after": 0, "kube_500": 0, "kube_409": 0, "kube_drop": 0, "sqs_throttle": 0,
+                "sqs_drop": 0, "token_rotations": 0}
+    stop = threading.Event()
+    t_start = time.monotonic()
+
+    def driver() -> None:
+        step = 0
+        next_fault = t_start + a.fault_every
+        rotated = False
+        while not stop.wait(0.05):
+            now = time.monotonic()
+            set_depths(int((now - t_start) * S))
+            if not rotated and now - t_start >= a.minutes * 30:
+                with open(token_file + ".new", "w") as f:
+                    f.write(tokens[1])
+                os.replace(token_file + ".new", token_file)
+                kube.require_token(tokens[1])
+                injected["token_rotations"] += 1
+                rotated = True
+            if now >= next_fault:
+                next_fault = now + a.fault_every
+                kind = step % 6
+                step += 1
+                if kind == 0:
+                    kube.inject(2, nat.InjectedFault(503, '{"kind":"Status","code":503,"message":"overloaded"}',
+                                                     "application/json", retry_after="1"))
+                    injected["kube_503_retry_after"] += 2
+                elif kind == 1:
+                    kube.inject(1, nat.InjectedFault(500, '{"kind":"Status","code":500,"message":"etcd"}',
+                                                     "application/json"))
+                    injected["kube_500"] += 1
+                elif kind == 2:
+                    kube.conflict_next(2)
+                    injected["kube_409"] += 2
+                elif kind == 3:
+                    kube.drop_connections()
+                    injected["kube_drop"] += 1
+                elif kind == 4:
+                    sqs.inject(2, nat.InjectedFault(503, THROTTLE, "text/xml", retry_after="1"))
+                    injected["sqs_throttle"] += 2
+                else:
+                    sqs.drop_connections()
+                    injected["sqs_drop"] += 1
+
+    th = threading.Thread(target=driver, daemon=True)
+    th.start()
+    rows = []
     try:
-        env.run(2000)  # warm-up
+        end = t_start + a.minutes * 60
+        k = 0
+        while time.monotonic() < end and child.poll() is None:
+            time.sleep(min(a.window, max(0.0, end - time.monotonic())))
+            if child.poll() is not None:
+                break
+            try:
+                m = scrape(port)
+            except OSError as e:
+                m = {"scrape_error": str(e)}
+            row = {"window": k, "t_s": round(time.monotonic() - t_start, 1), **proc_stats(child.pid), **m,
+                   "injected": dict(injected)}
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+            k += 1
+    finally:
+        stop.set()
+        th.join()
+        if child.poll() is None:
+            child.send_signal(signal.SIGTERM)
+        rc = child.wait(timeout=60)
+        err.close()
+        sqs.stop()
+        kube.stop()
+    with open(trace) as f:
+        spans = [json.loads(line) for line in f if line.strip()]
+    p = Params(poll_ns=period, up_cool_ns=up_cool, down_cool_ns=down_cool, up_msgs=100, down_msgs=10, max_pods=8,
+               min_pods=1)
+    replays = [replay_queue(p, ss, boundary_ns=a.boundary_us * 1000, queue=q) for q, ss in group_spans(spans).items()]
+    steady = rows[1:] if len(rows) > 2 else rows  # the first window includes start-up allocations
+    flat = {}
+    for key, tol in (("fds", 2), ("threads", 0), ("rss_kb", 8 * 1024)):
+        vals = [r[key] for r in steady if key in r]
+        flat[key] = {"min": min(vals), "max": max(vals), "flat": max(vals) - min(vals) <= tol} if vals else None
+    with open(os.path.join(tmp, "stderr.log")) as f:
+        stderr_tail = f.read()[-2000:]
+    summary = {
+        "summary": True, "minutes": a.minutes, "queues": a.queues, "poll_period": a.poll_period,
+        "cool_downs": [a.up_cool_down, a.down_cool_down], "exit_code": rc, "windows": len(rows),
+        "spans": len(spans), "injected": injected, "last_metrics": {k: v for k, v in rows[-1].items() if k not in
+                                                                   ("window", "injected")} if rows else {},
+        "replay": {"polls": sum(r.polls for r in replays), "judged": sum(r.checked for r in replays),
+                   "boundary": sum(r.boundary for r in replays), "depth_errors": sum(r.depth_errors for r in replays),
+                   "failed_calls": sum(r.failed_calls for r in replays),
+                   "scale_writes": sum(r.scale_writes for r in replays),
+                   "mismatches": sum(len(r.mismatches) for r in replays),
+                   "first_mismatches": [m for r in replays for m in r.mismatches][:5]},
+        "resources": flat,
+        "signature_failures": sqs.signature_failures(), "kube_auth_failures": kube.auth_failures(),
+        "ok": rc == 0 and all(r.ok for r in replays) and all(v and v["flat"] for v in flat.values()),
+    }
+    if not summary["ok"]:
+        summary["stderr_tail"] = stderr_tail
+    print(json.dumps(summary), flush=True)
+    return 0 if summary["ok"] else 1
+
+
+def hot(a) -> int:
+    from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
+
+    def pct(v, q):
+        return v[min(len(v) - 1, max(0, int(q / 100.0 * len(v) + 0.5) - 1))] if v else 0
+
+    env = BenchEnv(1, "scale", pipeline=True, busy_poll_ns=25_000)
+    runner = env.runners[0]
+    try:
+        env.run(2000)
         env.clear()
         end = time.monotonic() + a.minutes * 60
         k = 0
         while time.monotonic() < end:
-            st0 = runner.stats()
-            t0 = time.monotonic()
-            polls = 0
-            samples = []
+            t0, polls, samples = time.monotonic(), 0, []
             while time.monotonic() - t0 < a.window:
-                env.run(2000)  # a batch of polls, then drain the latency ring
+                env.run(2000)
                 samples += runner.latencies()
                 env.clear()
                 polls += 2000
-            st1 = runner.stats()
             samples.sort()
-            row = {"window": k, "t_s": round(time.monotonic() - (end - a.minutes * 60), 1), "polls": polls,
-                   "polls_per_s": round(polls / (time.monotonic() - t0), 1),
-                   "p50_us": round(pct(samples, 50) / 1e3, 2), "p99_us": round(pct(samples, 99) / 1e3, 2),
-                   "max_us": round(samples[-1] / 1e3, 1) if samples else 0,
-                   "errors": (st1["depth_errors"] - st0["depth_errors"]) + (st1["failed_ups"] - st0["failed_ups"]) +
-                             (st1["failed_downs"] - st0["failed_downs"]),
-                   "rss_kb": rss_kb()}
-            out.append(row)
-            print(json.dumps(row), flush=True)
+            print(json.dumps({"window": k, "polls": polls, "p50_us": round(pct(samples, 50) / 1e3, 2),
+                              "p99_us": round(pct(samples, 99) / 1e3, 2), **proc_stats(os.getpid())}), flush=True)
             k += 1
     finally:
         env.close()
-    if out:
-        first, last = out[0], out[-1]
-        print(json.dumps({"summary": True, "windows": len(out), "polls": sum(r["polls"] for r in out),
-                          "errors": sum(r["errors"] for r in out),
-                          "p50_us_first_last": [first["p50_us"], last["p50_us"]],
-                          "p50_us_range": [min(r["p50_us"] for r in out), max(r["p50_us"] for r in out)],
-                          "p99_us_max": max(r["p99_us"] for r in out),
-                          "rss_kb_first_last": [first["rss_kb"], last["rss_kb"]],
-                          "signature_failures": env.sqs.signature_failures()}), flush=True)
     return 0
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--minutes", type=float, default=10.0)
+    ap.add_argument("--window", type=float, default=30.0, help="seconds between resource samples")
+    ap.add_argument("--queues", type=int, default=8)
+    ap.add_argument("--poll-period", default="1s")
+    ap.add_argument("--up-cool-down", default="3s")
+    ap.add_argument("--down-cool-down", default="5s")
+    ap.add_argument("--fault-every", type=float, default=7.0, help="seconds between injected faults")
+    ap.add_argument("--boundary-us", type=int, default=250,
+                    help="cool-down comparisons this close to the edge are not judged by the replay")
+    ap.add_argument("--hot", action="store_true", help="back-to-back single-queue soak without faults")
+    a = ap.parse_args()
+    return hot(a) if a.hot else cadenced(a)
 
 
 if __name__ == "__main__":

@@ -330,3 +330,29 @@ def test_readiness_window_zero_disables(nat):
         assert h.ready() == (True, "ok")
     finally:
         env.close()
+
+
+def test_fleet_staggers_queue_starts(nat, tmp_path):
+    """Four queues at one poll period start a quarter period apart (Supervisor.stagger): their
+    polls do not arrive together every period. Each queue still polls one period after its own
+    start (main.go:37-41)."""
+    import json
+    import os
+
+    env = BenchEnv(4, poll_period_ns=200_000_000)
+    try:
+        trace = tmp_path / "t.jsonl"
+        fd = os.open(trace, os.O_WRONLY | os.O_CREAT | os.O_APPEND)
+        for r in env.runners:
+            r.set_trace_fd(fd)
+        fleet = Fleet([W(r, t) for r, t in zip(env.runners, env.targets)])
+        fleet.start(2)
+        assert fleet.wait(10)
+        fleet.join()
+        os.close(fd)
+        spans = [json.loads(l) for l in trace.read_text().splitlines()]
+    finally:
+        env.close()
+    first = sorted((s["ts"] - s["total_ns"]) for s in spans if s["poll"] == 1)
+    gaps = [(b - a) / 1e6 for a, b in zip(first, first[1:])]
+    assert len(first) == 4 and all(35 < g < 65 for g in gaps), gaps  # 50 ms apart
