@@ -68,6 +68,12 @@ def _apiserver_requests_per_poll(wire: dict) -> dict:
     return out
 
 
+def _progress(msg: str) -> None:
+    """One line per finished row on stderr (stdout carries only the result line): a run of
+    several minutes shows that it is alive."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
     """Poll->patch latency at production poll periods (250 ms and 1 s; the reference's default
     is 5 s, /root/reference/main.go:83): ``--cadence-queues`` queues, one thread each, staggered
@@ -96,6 +102,7 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
                                      hot_endpoints=hot, prewarm_ns=pw, timing=not tls)
                 rows.setdefault(label, {})[key] = r
                 p50.setdefault(label, {})[key] = r["p50_ms"]
+                _progress(f"cadence {label} {key}: p50 {r['p50_ms']} ms over {r['samples']} samples")
     return {
         "cadenced_p50_ms": p50,
         "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
@@ -169,6 +176,8 @@ def main(argv=None) -> int:
         barrier_sync()
         wall = time.perf_counter() - t0
         res = env.collect(args.steps, wall)
+        if rank == 0:
+            _progress(f"timed run: {args.steps} steps in {wall:.3f} s")
     finally:
         env.close()
 
@@ -243,6 +252,7 @@ def main(argv=None) -> int:
                                  **extra_kw).summary()
                     p50s[k].append(sm["p50_ms"])
                     samples[k].append(sm["samples"])
+                _progress(f"secondary rows, round {len(p50s['sequential'])}/3 done")
             med = {k: sorted(v)[1] for k, v in p50s.items()}
             # the CLI's default fleet (a thread per queue) is the primary row
             extra["p50_ms_by_tracked_queues"] = {str(q): med[f"q{q}_threads"] for q in (1, 2, 4, 8)}
@@ -263,12 +273,15 @@ def main(argv=None) -> int:
                 r = measure(1, n, 5, mode, pipeline=pl, sqs_latency_ns=2_000_000, kube_latency_ns=1_000_000)
                 wan[name] = r.summary()["p50_ms"]
             extra["wan_model_sqs2ms_kube1ms_p50_ms"] = wan
+            _progress(f"regional-RTT model rows: {wan}")
             extra["wan_model_samples"] = n
             from kube_sqs_autoscaler_amd.bench.latency import phase_breakdown
 
             extra["phase_median_us"] = {
                 "default": phase_breakdown(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp),
                 "reference_equivalent": phase_breakdown(mode="deployment", pipeline=False),
+                # the same hot loop with every call timed (HttpTiming), next to the cadence rows' breakdown
+                "default_timed": phase_breakdown(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp, timing=True),
             }
         if world == 1 and not args.no_sweep and not args.no_cadence:
             extra.update(_cadence_rows(args, pipeline, bp, p50))

@@ -8,8 +8,9 @@
 //     an image and load a model first); a scale-down removes pending pods before ready ones;
 //   * the decisions are the reference's rules -- KSA_DECIDE, the same code policy_sim.h
 //     runs -- on the same virtual clock with the same API latency model.
-// Arrivals per poll interval are random: a normal approximation of Poisson built from a CLT of
-// 12 uniform 16-bit draws, integer-only, so the gfx950 kernel and the CPU path agree bit for bit.
+// Arrivals per poll interval are random: a normal approximation of Poisson, its standard normal
+// the Irwin-Hall sum of four uniform 16-bit draws (one 64-bit hash) scaled to unit variance,
+// integer-only, so the gfx950 kernel and the CPU path agree bit for bit.
 // The stream is counter-based on (seed, interval index) and the same seeds are used for every
 // configuration (common random numbers), so configurations are compared on the same arrival
 // sequences. The backlog is kept in micro-messages: a rate in milli-msgs/s times an interval in ms
@@ -75,25 +76,34 @@ KSA_HD int64_t sat_mul(int64_t a, int64_t b) {
 // x / 10^6 for x >= 0 (backlogs, virtual times): as an unsigned division by a constant it drops
 // the signed form's rounding correction (21 fewer VALU instructions in the gfx950 kernel).
 KSA_HD int64_t udiv_1e6(int64_t x) { return static_cast<int64_t>(static_cast<uint64_t>(x) / 1000000u); }
-KSA_HD int64_t sat_add(int64_t a, int64_t b) { return a > kSat - b ? kSat : a + b; }
+// min(a + b, kSat) for 0 <= a, b < 2^63: the unsigned sum cannot wrap, so the add comes first
+// and one compare clamps it (the form `a > kSat - b` needs a subtraction and an add on the GPU).
+KSA_HD int64_t sat_add(int64_t a, int64_t b) {
+  const uint64_t s = static_cast<uint64_t>(a) + static_cast<uint64_t>(b);
+  return s > static_cast<uint64_t>(kSat) ? kSat : static_cast<int64_t>(s);
+}
 // Messages (micro-messages) a rate of x_milli milli-msgs/s delivers in dt_ms: the product,
 // saturating.
 KSA_HD int64_t per_ms(int64_t x_milli, int64_t dt_ms) { return sat_mul(x_milli, dt_ms); }
 
-// Random arrivals (micro-messages) with mean `mean`: mean + sqrt(mean) * Z, where Z is the CLT
-// of 12 uniform 16-bit integers (standard deviation 2^16 in fixed point). sqrt(mean) is kept for
-// the last mean (*memo_mean, *memo_sd): polls of one interval length inside one rate segment --
-// most of them -- ask for the same mean, and the isqrt is the longest sequence of the poll on the
-// GPU (gfx950, 768k lanes x 24 h: 132.4 -> 125.6 ms).
+// Random arrivals (micro-messages) with mean `mean`: mean + sqrt(mean) * Z. Z is the sum of the
+// four 16-bit fields of one splitmix64 draw (Irwin-Hall, n = 4: mean 131070, standard deviation
+// 65536/sqrt(3)), centred and scaled by sqrt(3) to a standard deviation of 2^16 in fixed point;
+// |Z| < 3.47. Round 2 drew twelve fields from three hashes (the CLT of 12): on gfx950 the three
+// 64-bit hashes and their field sums were a third of the VALU work of a simulated poll, and four
+// fields already give a normal approximation far finer than the Poisson noise it stands for.
+// sqrt(mean) is kept for the last mean (*memo_mean, *memo_sd): polls of one interval length inside
+// one rate segment -- most of them -- ask for the same mean, and the isqrt is the longest sequence
+// of the poll on the GPU.
+constexpr int64_t kSqrt3Q16 = 113512;  // round(sqrt(3) * 2^16)
 KSA_HD int64_t sample_arrivals(int64_t mean, uint64_t seed, uint64_t k, int64_t* memo_mean, int64_t* memo_sd) {
   if (mean <= 0) return 0;
-  const uint64_t base = seed * 0xD1B54A32D192ED03ULL + k * 3;
-  const uint64_t w0 = mix64(base), w1 = mix64(base + 1), w2 = mix64(base + 2);
-  // Sum of the twelve 16-bit fields, SWAR: the even and odd fields of each word are added in
-  // 32-bit lanes (6 x 65535 fits), then the two lanes are folded.
+  const uint64_t w = mix64(seed * 0xD1B54A32D192ED03ULL + k);
+  // the four 16-bit fields, summed in two 32-bit lanes (2 x 65535 fits), then folded
   constexpr uint64_t kM = 0x0000FFFF0000FFFFULL;
-  const uint64_t lanes = (w0 & kM) + ((w0 >> 16) & kM) + (w1 & kM) + ((w1 >> 16) & kM) + (w2 & kM) + ((w2 >> 16) & kM);
-  const int64_t z = static_cast<int64_t>((lanes & 0xFFFFFFFFULL) + (lanes >> 32)) - 6 * 65536;
+  const uint64_t lanes = (w & kM) + ((w >> 16) & kM);
+  const int64_t u = static_cast<int64_t>((lanes & 0xFFFFFFFFULL) + (lanes >> 32)) - 131070;  // 2 x centred
+  const int64_t z = (u * kSqrt3Q16) >> 16;  // arithmetic shift: floor, as Python's >>
   // sd in micro-messages = sqrt(mean / 1e6) * 1e6 = 1000 sqrt(mean), to a milli-message
   if (mean != *memo_mean) {
     *memo_mean = mean;
@@ -215,10 +225,30 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
   int64_t prev_ms = 0;
   const int64_t horizon_ms = horizon_ns / 1000000;
   const bool advances = k.period > 0 || lat.sqs_ns > 0;
+  // `now` is also kept as whole milliseconds + the nanoseconds past them, advanced by the same
+  // increments (the period, the SQS call, each GET and write), each split once here: the poll's
+  // millisecond then needs no 64-bit division per poll. Exact: now == now_ms * 10^6 + now_sub.
+  const int64_t period_ms = udiv_1e6(k.period), sqs_ms = udiv_1e6(lat.sqs_ns);
+  const int64_t get_ms = udiv_1e6(lat.get_ns), upd_ms = udiv_1e6(lat.update_ns);
+  const uint32_t period_sub = static_cast<uint32_t>(k.period - period_ms * 1000000);
+  const uint32_t sqs_sub = static_cast<uint32_t>(lat.sqs_ns - sqs_ms * 1000000);
+  const uint32_t get_sub = static_cast<uint32_t>(lat.get_ns - get_ms * 1000000);
+  const uint32_t upd_sub = static_cast<uint32_t>(lat.update_ns - upd_ms * 1000000);
+  int64_t now_ms = 0;
+  uint32_t now_sub = 0;
+  // adds (ms, sub) with sub < 6 * 10^6 (now_sub, the SQS call's and up to four more latencies'
+  // remainders): the sum stays far below 2^32
+  auto carry = [&](int64_t add_ms, uint32_t add_sub) {
+    const uint32_t t = now_sub + add_sub;
+    const uint32_t c = t / 1000000u;  // 32-bit division by a constant: a multiply-high
+    now_sub = t - c * 1000000u;
+    now_ms += add_ms + c;
+  };
   while (advances && res.polls < kMaxPolls) {
     const int64_t t_poll = now + k.period;  // main.go:41 sleep, then poll
     if (t_poll > horizon_ns) break;
-    const int64_t t_poll_ms = udiv_1e6(t_poll);
+    carry(period_ms, period_sub);
+    const int64_t t_poll_ms = now_ms;
     advance(&s, &res, m, t_ms, rate_milli, n, &cur, seed, prev_ms, t_poll_ms, replicas);
     prev_ms = t_poll_ms;
     now = t_poll;
@@ -229,6 +259,8 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
     const int32_t before = replicas;
     int32_t gets = 0, writes = 0;
     KSA_DECIDE(k, lat, d, now, last_up, last_down, replicas, gets, writes, res.ups++, (void)0, res.downs++, (void)0);
+    carry(sqs_ms + gets * get_ms + writes * upd_ms,
+          sqs_sub + static_cast<uint32_t>(gets) * get_sub + static_cast<uint32_t>(writes) * upd_sub);
     const int32_t delta = sub_i32(replicas, before);
     if (delta > 0) {  // new pods: billed now, draining after the start-up delay
       s.pending += delta;

@@ -350,18 +350,19 @@ class BenchEnv:
         self._devnulls = []
 
 
-def phase_breakdown(steps: int = 2000, warmup: int = 200, **kw) -> Dict[str, float]:
+def phase_breakdown(steps: int = 2000, warmup: int = 200, timing: bool = False, **kw) -> Dict[str, float]:
     """Median per-phase times (us) of the scaling iteration, from the native span trace.
 
     ``depth_us`` is the SQS call (the pipelined GET is in flight during it), ``get_wait_us`` the
     extra wait for the GET response afterwards (0 when it arrived during the SQS call),
     ``write_us`` the replica write, ``patch_us`` the poll->patch span the metric reports.
+    ``timing``: also every call's phases (HttpTiming), under ``calls``.
     """
     import json
     import statistics
     import tempfile
 
-    env = BenchEnv(1, **kw)
+    env = BenchEnv(1, timing=timing, **kw)
     try:
         env.run(warmup)
         with tempfile.TemporaryFile() as f:
@@ -373,8 +374,11 @@ def phase_breakdown(steps: int = 2000, warmup: int = 200, **kw) -> Dict[str, flo
     finally:
         env.close()
     med = lambda k: round(statistics.median(s[k] for s in spans) / 1e3, 2)
-    return {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
-            "patch_us": med("patch_latency_ns")}
+    out = {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
+           "patch_us": med("patch_latency_ns")}
+    if timing:
+        out["calls"] = _detail_medians([s for s in spans if s["patch_latency_ns"] >= 0])
+    return out
 
 
 def measure_processes(queues: int, steps: int, warmup: int, mode: str = "scale", tls: bool = False,

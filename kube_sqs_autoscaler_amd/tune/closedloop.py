@@ -6,7 +6,8 @@ workers that take minutes to start needs the feedback loop: more replicas drain 
 changes the next decision. ``csrc/sim/queue_sim.h`` models it:
 
 * arrivals at a piecewise-constant rate (msgs/s), random per poll interval (integer normal
-  approximation of Poisson, counter-based per seed, the same seeds for every configuration);
+  approximation of Poisson -- an Irwin-Hall sum of four 16-bit draws -- counter-based per seed,
+  the same seeds for every configuration);
 * each ready pod drains ``service_rate`` msgs/s; a scale-up's pods take work only
   ``startup`` after the write returned; a scale-down removes starting pods first;
 * the decisions are the reference's rules (``KSA_DECIDE`` in ``policy_sim.h``, shared with the open-loop
@@ -215,9 +216,9 @@ def _mix64(z: int) -> int:
 def _sample(mean: int, seed: int, k: int) -> int:
     if mean <= 0:
         return 0
-    base = (seed * 0xD1B54A32D192ED03 + k * 3) & _MASK64
-    words = [_mix64((base + j) & _MASK64) for j in range(3)]
-    z = sum((w >> (16 * i)) & 0xFFFF for w in words for i in range(4)) - 6 * 65536
+    w = _mix64((seed * 0xD1B54A32D192ED03 + k) & _MASK64)
+    u = sum((w >> (16 * i)) & 0xFFFF for i in range(4)) - 131070  # Irwin-Hall(4), centred
+    z = (u * 113512) >> 16  # x sqrt(3): standard deviation 2^16; >> floors, as the C++ shift
     sd = math.isqrt(mean) * 1000  # micro-messages: 1000 sqrt(mean)
     prod = sd * z
     a = mean + (abs(prod) // 65536) * (1 if prod >= 0 else -1)  # C++ division truncates toward zero
