@@ -61,15 +61,18 @@ void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
   for (auto& th : pool) th.join();
 }
 
-void queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
+bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
                      int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params, int64_t m,
-                     int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, int threads) {
+                     int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, int threads, int arith) {
   const int64_t lanes = m * seeds;
-  if (lanes <= 0 || n < 1) return;
+  if (lanes <= 0 || n < 1) return false;
   for (int k = 0; k < 3; ++k)
-    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return;  // closedloop.py validates first
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return false;  // closedloop.py validates first
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
   const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
+  const bool fast = arith == 0 && ksa_sim::fast_path_ok(t_ms, rate_milli, n, qm, init_replicas, horizon_ns, params, m);
+  std::vector<uint32_t> t32(fast ? n : 0), r32(fast ? n : 0);
+  if (fast) ksa_sim::narrow_trace(t_ms, rate_milli, n, t32.data(), r32.data());
   auto work = [&](int64_t lo, int64_t hi) {
     for (int64_t l = lo; l < hi; ++l) {
       const int64_t i = l / seeds;
@@ -84,8 +87,12 @@ void queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
       p.down_pods = params[6 * m + i];
       p.max_pods = params[7 * m + i];
       p.min_pods = params[8 * m + i];
-      const ksa_sim::QueueResult r = ksa_sim::simulate_queue(p, lat, qm, t_ms, rate_milli, n, init_replicas, horizon_ns,
-                                                             seed0 + static_cast<uint64_t>(s));
+      const uint64_t seed = seed0 + static_cast<uint64_t>(s);
+      const ksa_sim::QueueResult r =
+          fast ? ksa_sim::simulate_queue<ksa_sim::FastArith>(p, lat, qm, t32.data(), r32.data(), n, init_replicas,
+                                                             horizon_ns, seed)
+               : ksa_sim::simulate_queue<ksa_sim::SatArith>(p, lat, qm, t_ms, rate_milli, n, init_replicas, horizon_ns,
+                                                            seed);
       const int64_t o64[7] = {r.pod_ms, r.backlog_msg_ms, r.violation_ms, r.peak_backlog, r.arrived, r.served,
                               r.final_backlog};
       const int32_t o32[5] = {r.ups, r.downs, r.final_replicas, r.max_replicas, r.polls};
@@ -97,7 +104,7 @@ void queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
   if (t > lanes) t = static_cast<int>(lanes);
   if (t == 1) {
     work(0, lanes);
-    return;
+    return fast;
   }
   std::vector<std::thread> pool;
   const int64_t chunk = 256;
@@ -111,6 +118,7 @@ void queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
       }
     });
   for (auto& th : pool) th.join();
+  return fast;
 }
 
 }  // namespace ksa

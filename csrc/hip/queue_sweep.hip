@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../sim/queue_sim.h"
 
@@ -26,7 +27,9 @@ constexpr int kBlock = 256;
 // Measured on an MI355X (768k lanes x 24 h, same box): compiler's choice 107 VGPRs / 4 waves
 // 182.7 ms; 5 waves (96 VGPRs, 24 B scratch) 171.1 ms; 6 waves (80 VGPRs, 92 B scratch) 188.5 ms.
 // Round 2 (register rate cursor + sqrt memo, 24000 x 32 lanes x 24 h): 5 waves 125.6 ms vs 4 waves
-// 131.3 ms (profiles/r02u_queue_ab).
+// 131.3 ms. Round 3 (one-hash sampler, SatArith): 5 waves 109.1 ms (84 B scratch) vs 4 waves
+// 111.2 ms (122 VGPRs, none); FastArith fits 96 VGPRs at 5 waves with no scratch (68.2 ms,
+// profiles/r03h_queue).
 #ifndef KSA_QUEUE_WAVES_PER_EU
 #define KSA_QUEUE_WAVES_PER_EU 5
 #endif
@@ -36,18 +39,17 @@ enum : int { kUps = 0, kDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
 
 thread_local std::string g_queue_error;
 
+// A: ksa_sim::FastArith (T = uint32_t, the host proved the sweep's bounds: fast_path_ok) or
+// ksa_sim::SatArith (T = int64_t).
+template <class A, class T>
 __global__ __launch_bounds__(kBlock)
 #if KSA_QUEUE_WAVES_PER_EU > 0
 __attribute__((amdgpu_waves_per_eu(KSA_QUEUE_WAVES_PER_EU)))
 #endif
-void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m,
-                                                             int32_t seeds, uint64_t seed0, ksa_sim::Latency lat,
-                                                             ksa_sim::QueueModel model,
-                                                             const int64_t* __restrict__ t_ms,
-                                                             const int64_t* __restrict__ rate_milli, int32_t n,
-                                                             int32_t init, int64_t horizon,
-                                                             int64_t* __restrict__ out64,
-                                                             int32_t* __restrict__ out32) {
+void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m, int32_t seeds, uint64_t seed0,
+                        ksa_sim::Latency lat, ksa_sim::QueueModel model, const T* __restrict__ t_ms,
+                        const T* __restrict__ rate_milli, int32_t n, int32_t init, int64_t horizon,
+                        int64_t* __restrict__ out64, int32_t* __restrict__ out32) {
   const int64_t lanes = m * seeds;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t l = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; l < lanes; l += stride) {
@@ -64,7 +66,7 @@ void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m,
     p.max_pods = params[kMaxPods * m + i];
     p.min_pods = params[kMinPods * m + i];
     const ksa_sim::QueueResult r =
-        ksa_sim::simulate_queue(p, lat, model, t_ms, rate_milli, n, init, horizon, seed0 + static_cast<uint64_t>(s));
+        ksa_sim::simulate_queue<A>(p, lat, model, t_ms, rate_milli, n, init, horizon, seed0 + static_cast<uint64_t>(s));
     out64[kPodMs * lanes + l] = r.pod_ms;
     out64[kBacklogMsgMs * lanes + l] = r.backlog_msg_ms;
     out64[kViolationMs * lanes + l] = r.violation_ms;
@@ -86,6 +88,24 @@ bool ok(hipError_t e, const char* what) {
   return false;
 }
 
+// Launches one arithmetic's kernel on device buffers; the grid is one resident wave of workgroups.
+template <class A, class T>
+bool launch(const hipDeviceProp_t& prop, const int64_t* d_p, int64_t m, int32_t seeds, uint64_t seed0,
+            const ksa_sim::Latency& lat, const ksa_sim::QueueModel& qm, const T* d_t, const T* d_r, int32_t n,
+            int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
+  const int64_t lanes = m * seeds;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_sweep_kernel<A, T>, kBlock, 0) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int64_t cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  const int64_t want = (lanes + kBlock - 1) / kBlock;
+  const int grid = static_cast<int>(std::min<int64_t>(want, cus * per_cu));
+  hipLaunchKernelGGL((queue_sweep_kernel<A, T>), dim3(grid), dim3(kBlock), 0, nullptr, d_p, m, seeds, seed0, lat, qm,
+                     d_t, d_r, n, init, horizon_ns, d_o64, d_o32);
+  return ok(hipGetLastError(), "queue_sweep_kernel launch");
+}
+
 }  // namespace
 
 extern "C" {
@@ -95,10 +115,13 @@ const char* ksa_queue_sweep_last_error() { return g_queue_error.c_str(); }
 // trace: n segments (t_ms ascending from 0, rate in msgs/s x1000); model: {service_milli,
 // startup_ns, slo_backlog, init_backlog}; latency {sqs, get, update} ns; params [9][m];
 // out64 [7][m*seeds] (pod_ms, backlog_msg_ms, violation_ms, peak_backlog, arrived, served,
-// final_backlog); out32 [5][m*seeds] (ups, downs, final, max_replicas, polls). 0 on success.
+// final_backlog); out32 [5][m*seeds] (ups, downs, final, max_replicas, polls). arith: 0 picks
+// FastArith when ksa_sim::fast_path_ok holds, 1 forces SatArith; *fast_used reports the choice.
+// 0 on success.
 int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
                         int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params,
-                        int64_t m, int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, double* kernel_ms) {
+                        int64_t m, int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, double* kernel_ms,
+                        int32_t arith, int32_t* fast_used) {
   if (n < 1 || t_ms[0] != 0) {
     g_queue_error = "arrival trace must have at least one segment starting at t=0";
     return -1;
@@ -114,36 +137,48 @@ int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli,
     }
   const int64_t lanes = m * seeds;
   if (lanes <= 0) return 0;
+  const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
+  const bool fast = arith == 0 && ksa_sim::fast_path_ok(t_ms, rate_milli, n, qm, init_replicas, horizon_ns, params, m);
+  if (fast_used) *fast_used = fast ? 1 : 0;
+  // the trace in the chosen arithmetic's element type
+  std::vector<uint32_t> t32, r32;
+  const size_t elem = fast ? sizeof(uint32_t) : sizeof(int64_t);
+  const void* h_t = t_ms;
+  const void* h_r = rate_milli;
+  if (fast) {
+    t32.resize(n);
+    r32.resize(n);
+    ksa_sim::narrow_trace(t_ms, rate_milli, n, t32.data(), r32.data());
+    h_t = t32.data();
+    h_r = r32.data();
+  }
   if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
   hipDeviceProp_t prop;
   if (!ok(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties")) return -1;
-  int64_t *d_t = nullptr, *d_r = nullptr, *d_p = nullptr, *d_o64 = nullptr;
+  void *d_t = nullptr, *d_r = nullptr;
+  int64_t *d_p = nullptr, *d_o64 = nullptr;
   int32_t* d_o32 = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = -1;
   do {
-    if (!ok(hipMalloc(&d_t, n * sizeof(int64_t)), "hipMalloc") || !ok(hipMalloc(&d_r, n * sizeof(int64_t)), "hipMalloc") ||
+    if (!ok(hipMalloc(&d_t, n * elem), "hipMalloc") || !ok(hipMalloc(&d_r, n * elem), "hipMalloc") ||
         !ok(hipMalloc(&d_p, kNumParams * m * sizeof(int64_t)), "hipMalloc") ||
         !ok(hipMalloc(&d_o64, kNumOut64 * lanes * sizeof(int64_t)), "hipMalloc") ||
         !ok(hipMalloc(&d_o32, kNumOut32 * lanes * sizeof(int32_t)), "hipMalloc"))
       break;
-    if (!ok(hipMemcpy(d_t, t_ms, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
-        !ok(hipMemcpy(d_r, rate_milli, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
+    if (!ok(hipMemcpy(d_t, h_t, n * elem, hipMemcpyHostToDevice), "hipMemcpy") ||
+        !ok(hipMemcpy(d_r, h_r, n * elem, hipMemcpyHostToDevice), "hipMemcpy") ||
         !ok(hipMemcpy(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy"))
       break;
     if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_sweep_kernel, kBlock, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    const int64_t cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    const int64_t want = (lanes + kBlock - 1) / kBlock;
-    const int grid = static_cast<int>(std::min<int64_t>(want, cus * per_cu));
     const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
-    const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
     if (!ok(hipEventRecord(e0, nullptr), "hipEventRecord")) break;
-    hipLaunchKernelGGL(queue_sweep_kernel, dim3(grid), dim3(kBlock), 0, nullptr, d_p, m, seeds, seed0, lat, qm, d_t, d_r,
-                       n, init_replicas, horizon_ns, d_o64, d_o32);
-    if (!ok(hipGetLastError(), "queue_sweep_kernel launch")) break;
+    const bool launched =
+        fast ? launch<ksa_sim::FastArith>(prop, d_p, m, seeds, seed0, lat, qm, static_cast<const uint32_t*>(d_t),
+                                          static_cast<const uint32_t*>(d_r), n, init_replicas, horizon_ns, d_o64, d_o32)
+             : launch<ksa_sim::SatArith>(prop, d_p, m, seeds, seed0, lat, qm, static_cast<const int64_t*>(d_t),
+                                         static_cast<const int64_t*>(d_r), n, init_replicas, horizon_ns, d_o64, d_o32);
+    if (!launched) break;
     if (!ok(hipEventRecord(e1, nullptr), "hipEventRecord")) break;
     if (!ok(hipEventSynchronize(e1), "hipEventSynchronize")) break;
     float ms = 0;

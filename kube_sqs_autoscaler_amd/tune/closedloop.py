@@ -108,6 +108,7 @@ class ClosedLoopResult:
     device: str
     horizon_ns: int
     kernel_ms: float = 0.0
+    fast_arith: bool = False  # the native path ran queue_sim.h's FastArith (bounds proven)
 
     def __len__(self) -> int:
         return self.params.shape[1]
@@ -145,7 +146,8 @@ def _queue_lib():
         lib.ksa_queue_sweep_gpu.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_void_p,
-                                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+                                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_int32)]
         lib.ksa_queue_sweep_last_error.restype = ctypes.c_char_p
         lib._queue_ready = True
     return lib
@@ -153,7 +155,14 @@ def _queue_lib():
 
 def run(trace: ArrivalTrace, params: np.ndarray, model: QueueModel, init_replicas: int = 1,
         horizon_ns: int = 3600 * S, latency_ns: Tuple[int, int, int] = (1_000_000, 1_000_000, 1_000_000),
-        seeds: int = 32, seed0: int = 1, device: str = "auto", threads: int = 0, gpu_index: int = 0) -> ClosedLoopResult:
+        seeds: int = 32, seed0: int = 1, device: str = "auto", threads: int = 0, gpu_index: int = 0,
+        arith: str = "auto") -> ClosedLoopResult:
+    """Runs the sweep. ``arith``: ``"auto"`` runs queue_sim.h's FastArith (plain integer ops,
+    32-bit times) when ``fast_path_ok`` proves that no quantity can saturate -- identical results --
+    and the saturating arithmetic otherwise; ``"saturating"`` always runs the latter."""
+    if arith not in ("auto", "saturating"):
+        raise ValueError(f"arith must be auto or saturating, not {arith!r}")
+    saturating = arith == "saturating"
     params = np.ascontiguousarray(params, dtype=np.int64)
     if params.ndim != 2 or params.shape[0] != len(PARAM_FIELDS):
         raise ValueError("params must have shape (9, m); build it with sweep.grid()")
@@ -180,23 +189,27 @@ def run(trace: ArrivalTrace, params: np.ndarray, model: QueueModel, init_replica
         out64 = np.zeros((len(OUT64), lanes), dtype=np.int64)
         out32 = np.zeros((len(OUT32), lanes), dtype=np.int32)
         ms = ctypes.c_double(0)
+        used = ctypes.c_int32(0)
         rc = lib.ksa_queue_sweep_gpu(gpu_index, trace.t_ms.ctypes.data, trace.rate_milli.ctypes.data, len(trace.t_ms),
                                      init_replicas, horizon_ns, lat.ctypes.data, packed.ctypes.data, params.ctypes.data,
-                                     m, seeds, seed0, out64.ctypes.data, out32.ctypes.data, ctypes.byref(ms))
+                                     m, seeds, seed0, out64.ctypes.data, out32.ctypes.data, ctypes.byref(ms),
+                                     1 if saturating else 0, ctypes.byref(used))
         if rc != 0:
             raise RuntimeError("GPU closed-loop sweep failed: " + (lib.ksa_queue_sweep_last_error() or b"").decode())
         kernel_ms = ms.value
+        fast = bool(used.value)
     elif device == "cpu":
         from ..ops import native
 
-        out64, out32 = native().queue_sweep_cpu(trace.t_ms, trace.rate_milli, init_replicas, horizon_ns, lat, packed,
-                                                params, seeds, seed0, threads or (os.cpu_count() or 8))
+        out64, out32, fast = native().queue_sweep_cpu(trace.t_ms, trace.rate_milli, init_replicas, horizon_ns, lat,
+                                                      packed, params, seeds, seed0, threads or (os.cpu_count() or 8),
+                                                      saturating)
         kernel_ms = 0.0
     else:
         raise ValueError(f"device must be auto, gpu or cpu, not {device!r}")
     out = {k: out64[i].reshape(m, seeds) for i, k in enumerate(OUT64)}
     out.update({k: out32[i].reshape(m, seeds) for i, k in enumerate(OUT32)})
-    return ClosedLoopResult(params, seeds, out, device, horizon_ns, kernel_ms)
+    return ClosedLoopResult(params, seeds, out, device, horizon_ns, kernel_ms, fast)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -220,8 +233,7 @@ def _sample(mean: int, seed: int, k: int) -> int:
     u = sum((w >> (16 * i)) & 0xFFFF for i in range(4)) - 131070  # Irwin-Hall(4), centred
     z = (u * 113512) >> 16  # x sqrt(3): standard deviation 2^16; >> floors, as the C++ shift
     sd = math.isqrt(mean) * 1000  # micro-messages: 1000 sqrt(mean)
-    prod = sd * z
-    a = mean + (abs(prod) // 65536) * (1 if prod >= 0 else -1)  # C++ division truncates toward zero
+    a = mean + ((sd * z) >> 16)  # floors, as the C++ arithmetic shift
     return max(a, 0)
 
 

@@ -1,5 +1,10 @@
 """Closed-loop what-if sweep throughput: configurations x seeds over a synthetic 24 h arrival
-pattern, gfx950 kernel vs the CPU path (same header, bit-identical). One JSON line per device."""
+pattern, gfx950 kernel vs the CPU path (same header, bit-identical). One JSON line per device.
+
+``--arith saturating`` forces queue_sim.h's saturating arithmetic on the GPU (default: auto, which
+runs FastArith when its bounds hold -- they do here). The CPU slice always runs the saturating
+arithmetic, so the equality line checks the GPU's arithmetic against it."""
+import argparse
 import json
 import os
 import sys
@@ -12,6 +17,9 @@ import numpy as np  # noqa: E402
 from kube_sqs_autoscaler_amd.tune import closedloop as cl  # noqa: E402
 from kube_sqs_autoscaler_amd.tune import sweep  # noqa: E402
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--arith", choices=("auto", "saturating"), default="auto")
+args = ap.parse_args()
 S = 1_000_000_000
 minutes = np.arange(1440)
 rate = 20 + 15 * np.sin(minutes / 1440 * 2 * np.pi * 2) + (np.random.default_rng(3).random(1440) < 0.02) * 120
@@ -26,16 +34,17 @@ for device in ("gpu", "cpu"):
     if device == "gpu" and not sweep.gpu_available():
         continue
     sub = grid if device == "gpu" else grid[:, : max(1, m // 100)]  # CPU on a 1 % slice
-    cl.run(trace, sub[:, :64], model, 1, horizon, lat, seeds=seeds, device=device)  # warm-up
+    arith = args.arith if device == "gpu" else "saturating"
+    cl.run(trace, sub[:, :64], model, 1, horizon, lat, seeds=seeds, device=device, arith=arith)  # warm-up
     t0 = time.perf_counter()
-    r = cl.run(trace, sub, model, 1, horizon, lat, seeds=seeds, device=device, threads=16)
+    r = cl.run(trace, sub, model, 1, horizon, lat, seeds=seeds, device=device, threads=16, arith=arith)
     wall = time.perf_counter() - t0
     polls = int(r.out["polls"].sum())
     results[device] = r
     summ = r.summary()
     feasible = summ["violation_s_p95"] <= 600
     best = int(np.argmin(np.where(feasible, summ["pod_hours_mean"], np.inf))) if feasible.any() else None
-    print(json.dumps({"device": device, "configs": sub.shape[1], "seeds": seeds, "lane_polls": polls,
+    print(json.dumps({"device": device, "arith": "fast" if r.fast_arith else "saturating", "configs": sub.shape[1], "seeds": seeds, "lane_polls": polls,
                       "wall_s": round(wall, 4), "kernel_ms": round(r.kernel_ms, 3),
                       "lane_polls_per_s": round(polls / wall, 1),
                       "feasible": int(feasible.sum()),

@@ -144,6 +144,7 @@ def test_cpu_path_equals_python_model_at_extremes(nat, rate, service, poll_s, in
     model = cl.QueueModel(service_rate=service, startup_ns=86400 * S, slo_backlog=0, init_backlog=init)
     horizon = (30 * 86400 if poll_s > 86400 else 400) * S
     res = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=2, seed0=5, device="cpu")
+    assert not res.fast_arith  # 2^31 - 1 pods: queue_sim.h's fast_path_ok refuses
     for i in range(len(res)):
         for s in range(2):
             want = cl.reference_lane(tr, res.config(i), model, 1, horizon, (0, 0, 0), 5 + s)
@@ -162,8 +163,47 @@ def test_cpu_path_equals_python_model_on_fine_segments(nat):
     model = cl.QueueModel(service_rate=3.0, startup_ns=2 * S, slo_backlog=50, init_backlog=5)
     horizon = 120 * S
     res = cl.run(tr, grid, model, 1, horizon, (0, 1_000_000, 1_000_000), seeds=4, seed0=3, device="cpu")
+    assert res.fast_arith
     for i in range(len(res)):
         for s in range(4):
             want = cl.reference_lane(tr, res.config(i), model, 1, horizon, (0, 1_000_000, 1_000_000), 3 + s)
             got = {k: int(v[i, s]) for k, v in res.out.items()}
             assert got == want, (res.config(i), s)
+
+
+@pytest.mark.parametrize("tweak,fast", [
+    ({}, True),
+    ({"min_pods": [-1]}, False),             # a negative replica bound: counts could go negative
+    ({"max_pods": [2**31 - 2], "up_pods": [2]}, False),  # max + up wraps int32
+    ({"down_pods": [-3]}, False),
+])
+def test_fast_arithmetic_selection_is_exact(nat, tweak, fast):
+    """queue_sim.h runs FastArith (plain integer ops, 32-bit times) only when fast_path_ok proves
+    that nothing can saturate or wrap; then it computes exactly what the saturating arithmetic
+    (and the Python model) does."""
+    tr = burst_trace()
+    axes = dict(poll_ns=[5 * S], up_cool_ns=[0, 60 * S], down_cool_ns=[0, 120 * S], up_msgs=[20, 100], down_msgs=[5],
+                max_pods=[4, 8], min_pods=[1])
+    axes.update(tweak)
+    grid = sweep.grid(**axes)
+    model = cl.QueueModel(service_rate=5.0, startup_ns=45 * S, slo_backlog=100, init_backlog=15)
+    auto = cl.run(tr, grid, model, 1, 2400 * S, LAT, seeds=4, seed0=2, device="cpu")
+    sat = cl.run(tr, grid, model, 1, 2400 * S, LAT, seeds=4, seed0=2, device="cpu", arith="saturating")
+    assert auto.fast_arith is fast and not sat.fast_arith
+    for k in auto.out:
+        assert np.array_equal(auto.out[k], sat.out[k]), k
+    for i in range(len(auto)):
+        want = cl.reference_lane(tr, auto.config(i), model, 1, 2400 * S, LAT, 3)
+        assert {k: int(v[i, 1]) for k, v in auto.out.items()} == want
+    with pytest.raises(ValueError, match="arith"):
+        cl.run(tr, grid, model, device="cpu", arith="fast")
+
+
+def test_fast_arithmetic_refuses_unbounded_backlogs(nat):
+    """A 1e12-message initial backlog times a 30-day horizon could overflow the backlog
+    integral: fast_path_ok must fall back to the saturating arithmetic."""
+    tr = cl.ArrivalTrace.from_segments([(0, 1.0)])
+    grid = sweep.grid(poll_ns=[3600 * S], max_pods=[4])
+    big = cl.run(tr, grid, cl.QueueModel(1.0, 0, 10, init_backlog=10**12), 1, 30 * 86400 * S, LAT, seeds=1, device="cpu")
+    small = cl.run(tr, grid, cl.QueueModel(1.0, 0, 10, init_backlog=10**6), 1, 30 * 86400 * S, LAT, seeds=1, device="cpu")
+    assert not big.fast_arith and small.fast_arith

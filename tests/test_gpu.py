@@ -184,10 +184,14 @@ def test_closed_loop_kernel_equals_cpu_and_python_model():
     model = cl.QueueModel(service_rate=5.0, startup_ns=60 * S, slo_backlog=200, init_backlog=10)
     lat = (2_000_000, 1_000_000, 1_000_000)
     g = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="gpu")
-    c = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="cpu")
+    gs = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="gpu", arith="saturating")
+    c = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="cpu", arith="saturating")
     assert g.device == "gpu" and g.kernel_ms > 0
+    # the bounds hold, so the GPU ran FastArith -- and matches the saturating arithmetic exactly
+    assert g.fast_arith and not gs.fast_arith and not c.fast_arith
     for k in g.out:
         assert np.array_equal(g.out[k], c.out[k]), k
+        assert np.array_equal(gs.out[k], c.out[k]), k
     for i in range(0, len(g), 37):
         want = cl.reference_lane(tr, g.config(i), model, 1, 2400 * S, lat, 1 + 5)
         assert {k: int(v[i, 5]) for k, v in g.out.items()} == want
@@ -210,6 +214,7 @@ def test_closed_loop_kernel_equals_cpu_at_extremes():
         horizon = (30 * 86400 if poll_s > 86400 else 400) * S
         g = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=4, device="gpu")
         c = cl.run(tr, grid, model, 1, horizon, (0, 0, 0), seeds=4, device="cpu")
+        assert not g.fast_arith  # 2^31 - 1 pods: only the saturating arithmetic is safe
         for k in g.out:
             assert np.array_equal(g.out[k], c.out[k]), (rate, k)
 
