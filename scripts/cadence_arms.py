@@ -1,0 +1,73 @@
+"""Paired A/B of the poll-path knobs at a production cadence.
+
+The cadence rows of ``bench.py`` compare whole configurations in separate runs, so run-to-run
+noise (loopback send cost, scheduler placement) lands between them. Here the arms share one run:
+queue q gets arm q % 4 of ``--poll-prewarm`` {0, 1 ms} x ``--busy-poll`` {25 us, 300 us}, all
+queues against the same endpoint process, starts staggered over the period. One JSON line per
+arm and endpoint kind (fakes that sleep / never sleep): poll->patch p50/p90 and the per-call
+phase medians (``HttpTiming``, see ``bench/latency.py``).
+
+    python scripts/cadence_arms.py --period-ms 1000 --polls 27 --queues 16
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, _detail_medians  # noqa: E402
+
+MS = 1_000_000
+ARMS = [(0, 25_000), (1_000_000, 25_000), (0, 300_000), (1_000_000, 300_000)]  # (prewarm ns, busy-poll ns)
+
+
+def run(period_ms: int, polls: int, queues: int, skip: int = 2) -> None:
+    for hot in (False, True):
+        env = BenchEnv(queues, "scale", pipeline=True, busy_poll_ns=[a[1] for a in ARMS], servers="process",
+                       poll_period_ns=period_ms * MS, stagger=True, hot_endpoints=hot,
+                       prewarm_ns=[a[0] for a in ARMS], timing=True)
+        files = [tempfile.TemporaryFile() for _ in env.runners]
+        try:
+            for r, f in zip(env.runners, files):
+                r.set_trace_fd(f.fileno())
+            env.run(polls)
+            per_arm = {i: [] for i in range(len(ARMS))}
+            for q, (r, f) in enumerate(zip(env.runners, files)):
+                r.set_trace_fd(-1)
+                f.seek(0)
+                per_arm[q % len(ARMS)] += [json.loads(x) for x in f.read().decode().splitlines()][skip:]
+        finally:
+            for f in files:
+                f.close()
+            env.close()
+        for i, (prewarm, busy) in enumerate(ARMS):
+            spans = [s for s in per_arm[i] if s["patch_latency_ns"] >= 0]
+            lat = sorted(s["patch_latency_ns"] for s in spans)
+            if not lat:
+                continue
+            print(json.dumps({"period_ms": period_ms, "hot_endpoints": hot, "prewarm_us": prewarm / 1e3,
+                              "busy_poll_us": busy / 1e3, "samples": len(lat),
+                              "p50_us": round(lat[len(lat) // 2] / 1e3, 1),
+                              "p90_us": round(lat[int(len(lat) * 0.9)] / 1e3, 1),
+                              "depth_us": round(statistics.median(s["depth_ns"] for s in spans) / 1e3, 1),
+                              "write_us": round(statistics.median(s["update_ns"] for s in spans) / 1e3, 1),
+                              "calls": _detail_medians(spans)}), flush=True)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--period-ms", type=int, default=1000)
+    ap.add_argument("--polls", type=int, default=27, help="polls per queue (the first two are dropped)")
+    ap.add_argument("--queues", type=int, default=16, help="a multiple of 4: each arm gets queues / 4")
+    a = ap.parse_args()
+    if a.queues % len(ARMS):
+        ap.error("--queues must be a multiple of 4")
+    run(a.period_ms, a.polls, a.queues)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
