@@ -26,9 +26,11 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../sim/policy_sim.h"
+#include "device_arena.h"
 
 namespace {
 
@@ -120,58 +122,47 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
     }
   }
   if (m <= 0) return 0;
+  ksa_gpu::DeviceArena* ar = ksa_gpu::device_arena(dev, &g_sweep_error);
+  if (!ar) return -1;
+  std::lock_guard<std::mutex> lock(ar->mu);
   if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
-  hipDeviceProp_t prop;
-  if (!ok(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties")) return -1;
-  int64_t *d_t = nullptr, *d_d = nullptr, *d_p = nullptr, *d_o64 = nullptr;
-  int32_t* d_o32 = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  int rc = -1;
-  do {
-    if (!ok(hipMalloc(&d_t, n * sizeof(int64_t)), "hipMalloc") || !ok(hipMalloc(&d_d, n * sizeof(int64_t)), "hipMalloc") ||
-        !ok(hipMalloc(&d_p, kNumParams * m * sizeof(int64_t)), "hipMalloc") ||
-        !ok(hipMalloc(&d_o64, kNumOut64 * m * sizeof(int64_t)), "hipMalloc") ||
-        !ok(hipMalloc(&d_o32, kNumOut32 * m * sizeof(int32_t)), "hipMalloc"))
-      break;
-    if (!ok(hipMemcpy(d_t, trace_t, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
-        !ok(hipMemcpy(d_d, trace_d, n * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy") ||
-        !ok(hipMemcpy(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy"))
-      break;
-    if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
-    const int64_t want = (m + kBlock - 1) / kBlock;
-    const size_t lds = n <= kLdsTraceMax ? 2 * static_cast<size_t>(n) * sizeof(int64_t) : 0;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel, kBlock, lds) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    const int64_t cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    int64_t cap = cus * per_cu;  // one wave of resident workgroups
-    if (const char* g = std::getenv("KSA_SWEEP_GRID")) {  // tuning knob: "tiles" or N x resident
-      cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
-    }
-    const int grid = static_cast<int>(want < cap ? want : cap);
-    const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
-    if (!ok(hipEventRecord(e0, nullptr), "hipEventRecord")) break;
-    hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), lds, nullptr, d_p, m, lat, d_t, d_d, n, init_replicas,
-                       horizon_ns, d_o64, d_o32);
-    if (!ok(hipGetLastError(), "sweep_kernel launch")) break;
-    if (!ok(hipEventRecord(e1, nullptr), "hipEventRecord")) break;
-    if (!ok(hipEventSynchronize(e1), "hipEventSynchronize")) break;
-    float ms = 0;
-    if (!ok(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime")) break;
-    if (kernel_ms) *kernel_ms = ms;
-    if (!ok(hipMemcpy(out64, d_o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy") ||
-        !ok(hipMemcpy(out32, d_o32, kNumOut32 * m * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
-      break;
-    rc = 0;
-  } while (false);
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  (void)hipFree(d_t);
-  (void)hipFree(d_d);
-  (void)hipFree(d_p);
-  (void)hipFree(d_o64);
-  (void)hipFree(d_o32);
-  return rc;
+  void *d_t = nullptr, *d_d = nullptr, *d_p = nullptr, *d_o64 = nullptr, *d_o32 = nullptr;
+  if (!ok(ar->get(0, n * sizeof(int64_t), &d_t), "hipMalloc") || !ok(ar->get(1, n * sizeof(int64_t), &d_d), "hipMalloc") ||
+      !ok(ar->get(2, kNumParams * m * sizeof(int64_t), &d_p), "hipMalloc") ||
+      !ok(ar->get(3, kNumOut64 * m * sizeof(int64_t), &d_o64), "hipMalloc") ||
+      !ok(ar->get(4, kNumOut32 * m * sizeof(int32_t), &d_o32), "hipMalloc"))
+    return -1;
+  hipStream_t st = ar->stream;
+  const ksa_gpu::StreamDrain drain{st};
+  if (!ok(hipMemcpyAsync(d_t, trace_t, n * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(d_d, trace_d, n * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync"))
+    return -1;
+  const int64_t want = (m + kBlock - 1) / kBlock;
+  const size_t lds = n <= kLdsTraceMax ? 2 * static_cast<size_t>(n) * sizeof(int64_t) : 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel, kBlock, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  int64_t cap = static_cast<int64_t>(ar->cus) * per_cu;  // one wave of resident workgroups
+  if (const char* g = std::getenv("KSA_SWEEP_GRID")) {  // tuning knob: "tiles" or N x resident
+    cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
+  }
+  const int grid = static_cast<int>(want < cap ? want : cap);
+  const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+  if (!ok(hipEventRecord(ar->e0, st), "hipEventRecord")) return -1;
+  hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), lds, st, static_cast<const int64_t*>(d_p), m, lat,
+                     static_cast<const int64_t*>(d_t), static_cast<const int64_t*>(d_d), n, init_replicas, horizon_ns,
+                     static_cast<int64_t*>(d_o64), static_cast<int32_t*>(d_o32));
+  if (!ok(hipGetLastError(), "sweep_kernel launch")) return -1;
+  if (!ok(hipEventRecord(ar->e1, st), "hipEventRecord")) return -1;
+  if (!ok(hipMemcpyAsync(out64, d_o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(out32, d_o32, kNumOut32 * m * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync"))
+    return -1;
+  if (!ok(hipStreamSynchronize(st), "hipStreamSynchronize")) return -1;
+  float ms = 0;
+  if (!ok(hipEventElapsedTime(&ms, ar->e0, ar->e1), "hipEventElapsedTime")) return -1;
+  if (kernel_ms) *kernel_ms = ms;
+  return 0;
 }
 
 }  // extern "C"

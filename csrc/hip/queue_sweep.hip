@@ -14,10 +14,12 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../sim/queue_sim.h"
+#include "device_arena.h"
 
 namespace {
 
@@ -88,9 +90,10 @@ bool ok(hipError_t e, const char* what) {
   return false;
 }
 
-// Launches one arithmetic's kernel on device buffers; the grid is one resident wave of workgroups.
+// Launches one arithmetic's kernel on the arena's stream; the grid is one resident wave of
+// workgroups.
 template <class A, class T>
-bool launch(const hipDeviceProp_t& prop, const int64_t* d_p, int64_t m, int32_t seeds, uint64_t seed0,
+bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, int32_t seeds, uint64_t seed0,
             const ksa_sim::Latency& lat, const ksa_sim::QueueModel& qm, const T* d_t, const T* d_r, int32_t n,
             int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
   const int64_t lanes = m * seeds;
@@ -98,10 +101,9 @@ bool launch(const hipDeviceProp_t& prop, const int64_t* d_p, int64_t m, int32_t 
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_sweep_kernel<A, T>, kBlock, 0) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
-  const int64_t cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   const int64_t want = (lanes + kBlock - 1) / kBlock;
-  const int grid = static_cast<int>(std::min<int64_t>(want, cus * per_cu));
-  hipLaunchKernelGGL((queue_sweep_kernel<A, T>), dim3(grid), dim3(kBlock), 0, nullptr, d_p, m, seeds, seed0, lat, qm,
+  const int grid = static_cast<int>(std::min<int64_t>(want, static_cast<int64_t>(ar.cus) * per_cu));
+  hipLaunchKernelGGL((queue_sweep_kernel<A, T>), dim3(grid), dim3(kBlock), 0, ar.stream, d_p, m, seeds, seed0, lat, qm,
                      d_t, d_r, n, init, horizon_ns, d_o64, d_o32);
   return ok(hipGetLastError(), "queue_sweep_kernel launch");
 }
@@ -152,51 +154,44 @@ int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli,
     h_t = t32.data();
     h_r = r32.data();
   }
+  ksa_gpu::DeviceArena* ar = ksa_gpu::device_arena(dev, &g_queue_error);
+  if (!ar) return -1;
+  std::lock_guard<std::mutex> lock(ar->mu);
   if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
-  hipDeviceProp_t prop;
-  if (!ok(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties")) return -1;
-  void *d_t = nullptr, *d_r = nullptr;
-  int64_t *d_p = nullptr, *d_o64 = nullptr;
-  int32_t* d_o32 = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  int rc = -1;
-  do {
-    if (!ok(hipMalloc(&d_t, n * elem), "hipMalloc") || !ok(hipMalloc(&d_r, n * elem), "hipMalloc") ||
-        !ok(hipMalloc(&d_p, kNumParams * m * sizeof(int64_t)), "hipMalloc") ||
-        !ok(hipMalloc(&d_o64, kNumOut64 * lanes * sizeof(int64_t)), "hipMalloc") ||
-        !ok(hipMalloc(&d_o32, kNumOut32 * lanes * sizeof(int32_t)), "hipMalloc"))
-      break;
-    if (!ok(hipMemcpy(d_t, h_t, n * elem, hipMemcpyHostToDevice), "hipMemcpy") ||
-        !ok(hipMemcpy(d_r, h_r, n * elem, hipMemcpyHostToDevice), "hipMemcpy") ||
-        !ok(hipMemcpy(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice), "hipMemcpy"))
-      break;
-    if (!ok(hipEventCreate(&e0), "hipEventCreate") || !ok(hipEventCreate(&e1), "hipEventCreate")) break;
-    const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
-    if (!ok(hipEventRecord(e0, nullptr), "hipEventRecord")) break;
-    const bool launched =
-        fast ? launch<ksa_sim::FastArith>(prop, d_p, m, seeds, seed0, lat, qm, static_cast<const uint32_t*>(d_t),
-                                          static_cast<const uint32_t*>(d_r), n, init_replicas, horizon_ns, d_o64, d_o32)
-             : launch<ksa_sim::SatArith>(prop, d_p, m, seeds, seed0, lat, qm, static_cast<const int64_t*>(d_t),
-                                         static_cast<const int64_t*>(d_r), n, init_replicas, horizon_ns, d_o64, d_o32);
-    if (!launched) break;
-    if (!ok(hipEventRecord(e1, nullptr), "hipEventRecord")) break;
-    if (!ok(hipEventSynchronize(e1), "hipEventSynchronize")) break;
-    float ms = 0;
-    if (!ok(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime")) break;
-    if (kernel_ms) *kernel_ms = ms;
-    if (!ok(hipMemcpy(out64, d_o64, kNumOut64 * lanes * sizeof(int64_t), hipMemcpyDeviceToHost), "hipMemcpy") ||
-        !ok(hipMemcpy(out32, d_o32, kNumOut32 * lanes * sizeof(int32_t), hipMemcpyDeviceToHost), "hipMemcpy"))
-      break;
-    rc = 0;
-  } while (false);
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
-  (void)hipFree(d_t);
-  (void)hipFree(d_r);
-  (void)hipFree(d_p);
-  (void)hipFree(d_o64);
-  (void)hipFree(d_o32);
-  return rc;
+  void *d_t = nullptr, *d_r = nullptr, *d_p = nullptr, *d_o64 = nullptr, *d_o32 = nullptr;
+  if (!ok(ar->get(0, n * elem, &d_t), "hipMalloc") || !ok(ar->get(1, n * elem, &d_r), "hipMalloc") ||
+      !ok(ar->get(2, kNumParams * m * sizeof(int64_t), &d_p), "hipMalloc") ||
+      !ok(ar->get(3, kNumOut64 * lanes * sizeof(int64_t), &d_o64), "hipMalloc") ||
+      !ok(ar->get(4, kNumOut32 * lanes * sizeof(int32_t), &d_o32), "hipMalloc"))
+    return -1;
+  hipStream_t st = ar->stream;
+  const ksa_gpu::StreamDrain drain{st};
+  if (!ok(hipMemcpyAsync(d_t, h_t, n * elem, hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(d_r, h_r, n * elem, hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync"))
+    return -1;
+  const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+  const int64_t* p = static_cast<const int64_t*>(d_p);
+  int64_t* o64 = static_cast<int64_t*>(d_o64);
+  int32_t* o32 = static_cast<int32_t*>(d_o32);
+  if (!ok(hipEventRecord(ar->e0, st), "hipEventRecord")) return -1;
+  const bool launched =
+      fast ? launch<ksa_sim::FastArith>(*ar, p, m, seeds, seed0, lat, qm, static_cast<const uint32_t*>(d_t),
+                                        static_cast<const uint32_t*>(d_r), n, init_replicas, horizon_ns, o64, o32)
+           : launch<ksa_sim::SatArith>(*ar, p, m, seeds, seed0, lat, qm, static_cast<const int64_t*>(d_t),
+                                       static_cast<const int64_t*>(d_r), n, init_replicas, horizon_ns, o64, o32);
+  if (!launched) return -1;
+  if (!ok(hipEventRecord(ar->e1, st), "hipEventRecord")) return -1;
+  if (!ok(hipMemcpyAsync(out64, o64, kNumOut64 * lanes * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(out32, o32, kNumOut32 * lanes * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync"))
+    return -1;
+  // (`drain` also synchronizes on the error paths: the host trace copies t32 / r32 die with
+  // this frame)
+  if (!ok(hipStreamSynchronize(st), "hipStreamSynchronize")) return -1;
+  float ms = 0;
+  if (!ok(hipEventElapsedTime(&ms, ar->e0, ar->e1), "hipEventElapsedTime")) return -1;
+  if (kernel_ms) *kernel_ms = ms;
+  return 0;
 }
 
 }  // extern "C"

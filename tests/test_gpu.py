@@ -304,3 +304,30 @@ def test_closed_loop_kernel_random_lanes_equal_reference_model():
         s = int(rng.integers(0, seeds))
         want = cl.reference_lane(tr, g.config(i), model, 1, 1200 * S, lat, 1 + s)
         assert {k: int(v[i, s]) for k, v in g.out.items()} == want, (i, g.config(i))
+
+
+def test_sweeps_reuse_device_buffers_across_sizes():
+    """The sweep launchers keep grow-only device buffers and a stream per device
+    (csrc/hip/device_arena.h): calls that shrink, grow and alternate kernels must still give
+    exactly the CPU path's results (no stale tail of a larger earlier call leaks in)."""
+    import numpy as np
+
+    from kube_sqs_autoscaler_amd.tune import closedloop as cl
+    from kube_sqs_autoscaler_amd.tune import sweep
+
+    S = 1_000_000_000
+    lat = (2_000_000, 1_000_000, 1_000_000)
+    tr = cl.ArrivalTrace.from_segments([(0, 1.0), (200, 30.0), (500, 2.0)])
+    model = cl.QueueModel(service_rate=4.0, startup_ns=30 * S, slo_backlog=100)
+    big = sweep.grid(up_cool_ns=list(range(0, 240 * S, 30 * S)), max_pods=[4, 8, 16])
+    small = big[:, :5]
+    dtr = sweep.Trace.from_segments([(0, 0), (60 * S, 300), (400 * S, 5)])
+    for grid, seeds in ((big, 16), (small, 3), (big, 16), (small, 40)):
+        g = cl.run(tr, grid, model, 1, 900 * S, lat, seeds=seeds, device="gpu")
+        c = cl.run(tr, grid, model, 1, 900 * S, lat, seeds=seeds, device="cpu")
+        for k in g.out:
+            assert np.array_equal(g.out[k], c.out[k]), (grid.shape, seeds, k)
+        go = sweep.run(dtr, grid, 1, 900 * S, lat, device="gpu")
+        co = sweep.run(dtr, grid, 1, 900 * S, lat, device="cpu")
+        for k in go.out:
+            assert np.array_equal(go.out[k], co.out[k]), (grid.shape, k)
