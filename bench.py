@@ -243,12 +243,6 @@ def main(argv=None) -> int:
             # --sqs-protocol=json (AWS JSON 1.0, what current SDKs speak to SQS) instead of the
             # reference's Query/XML
             rows["sqs_json"] = (1, args.mode, pipeline, bp, False, "shared", "threads", {"sqs_protocol": "json"})
-            # the same two paths against fakes that never sleep (one busy-polled thread each), as a
-            # loaded production endpoint is awake: what is left is the client's own work and the
-            # loopback TCP path
-            rows["hot_endpoints"] = (1, args.mode, pipeline, bp, False, "shared", "threads", {"hot_endpoints": True})
-            rows["reference_hot_endpoints"] = (1, "deployment", False, 0, False, "shared", "threads",
-                                               {"hot_endpoints": True})
             p50s = {k: [] for k in rows}
             samples = {k: [] for k in rows}
             for _ in range(3):
@@ -270,8 +264,6 @@ def main(argv=None) -> int:
             extra["reference_equivalent_p50_ms"] = med["reference"]
             extra["tls_p50_ms"] = {"default": med["tls"], "reference_equivalent": med["reference_tls"]}
             extra["sqs_json_protocol_p50_ms"] = med["sqs_json"]
-            extra["hot_endpoints_p50_ms"] = {"default": med["hot_endpoints"],
-                                             "reference_equivalent": med["reference_hot_endpoints"]}
             extra["secondary_rows_p50_ms_all_rounds"] = p50s
             extra["secondary_rows_samples_per_round"] = samples
             # Regional-RTT model: the fakes add 2 ms (SQS) / 1 ms (apiserver) per request, so the
