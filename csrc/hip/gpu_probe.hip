@@ -33,7 +33,7 @@ constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
 constexpr int kUnrollFill = 4;    // 16-byte stores per lane per iteration
 constexpr int kUnrollVerify = 8;  // 16-byte loads in flight per lane per iteration
-constexpr int kBlocksPerCu = 2;   // measured best (csrc/tools/tune_probe.hip, profiles/r01_tune_probe.jsonl)
+constexpr int kBlocksPerCu = 2;   // measured best in round 1 (variant sweep; git history: r01_tune_probe.jsonl)
 
 thread_local std::string g_last_error;
 
