@@ -207,3 +207,33 @@ def test_fast_arithmetic_refuses_unbounded_backlogs(nat):
     big = cl.run(tr, grid, cl.QueueModel(1.0, 0, 10, init_backlog=10**12), 1, 30 * 86400 * S, LAT, seeds=1, device="cpu")
     small = cl.run(tr, grid, cl.QueueModel(1.0, 0, 10, init_backlog=10**6), 1, 30 * 86400 * S, LAT, seeds=1, device="cpu")
     assert not big.fast_arith and small.fast_arith
+
+
+def test_fast_arithmetic_matches_saturating_on_random_extremes(nat):
+    """Randomised inputs near the bounds fast_path_ok reasons about (rates up to 1e6 msgs/s,
+    service up to 1e6, backlogs up to 1e12, horizons up to 30 days, pods up to 2^31 - 1): whenever
+    the host picks FastArith it must compute exactly what the saturating arithmetic does."""
+    rng = np.random.default_rng(20261017)
+    picked = {True: 0, False: 0}
+    for _ in range(40):
+        horizon_s = int(rng.choice([600, 86400, 10 * 86400, 30 * 86400]))
+        n_seg = int(rng.integers(1, 5))
+        starts = sorted({0, *[int(x) for x in rng.integers(1, horizon_s, n_seg - 1)]})
+        rates = [float(rng.choice([0.0, 0.001, 3.5, 1e3, 1e6])) for _ in starts]
+        tr = cl.ArrivalTrace.from_segments(list(zip(starts, rates)))
+        grid = sweep.grid(poll_ns=[max(horizon_s // 500, 1) * S], up_cool_ns=[0, 60 * S], down_cool_ns=[0],
+                          up_msgs=[int(rng.choice([1, 100, 10**9]))], down_msgs=[0],
+                          up_pods=[int(rng.choice([1, 1000, 2**30]))],
+                          max_pods=[int(rng.choice([8, 10**4, 2**31 - 1]))], min_pods=[0, 1])
+        model = cl.QueueModel(service_rate=float(rng.choice([0.0, 0.5, 40.0, 1e6])),
+                              startup_ns=int(rng.choice([0, 60, 86400])) * S, slo_backlog=100,
+                              init_backlog=int(rng.choice([0, 10**6, 10**12])))
+        lat = (int(rng.integers(0, 5_000_000)), 1_500_000, 700_000)
+        init = int(rng.choice([0, 3]))
+        args = (tr, grid, model, init, horizon_s * S, lat)
+        auto = cl.run(*args, seeds=2, seed0=9, device="cpu")
+        sat = cl.run(*args, seeds=2, seed0=9, device="cpu", arith="saturating")
+        for k in auto.out:
+            assert np.array_equal(auto.out[k], sat.out[k]), (k, horizon_s, rates, model, auto.fast_arith)
+        picked[auto.fast_arith] += 1
+    assert picked[True] and picked[False]
