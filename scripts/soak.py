@@ -210,6 +210,12 @@ def cadenced(a) -> int:
     p = Params(poll_ns=period, up_cool_ns=up_cool, down_cool_ns=down_cool, up_msgs=100, down_msgs=10, max_pods=8,
                min_pods=1)
     replays = [replay_queue(p, ss, boundary_ns=a.boundary_us * 1000, queue=q) for q, ss in group_spans(spans).items()]
+    # poll->patch latency of the polls that wrote (the CLI at its cadence, over TLS, faults included)
+    lat = sorted(sp["patch_latency_ns"] for sp in spans if sp.get("patch_latency_ns", -1) >= 0)
+
+    def pct_us(q):
+        return round(lat[min(len(lat) - 1, max(0, int(q / 100.0 * len(lat) + 0.5) - 1))] / 1e3, 1) if lat else None
+
     steady = rows[1:] if len(rows) > 2 else rows  # the first window includes start-up allocations
     flat = {}
     for key, tol in (("fds", 2), ("threads", 0), ("rss_kb", 8 * 1024)):
@@ -229,6 +235,7 @@ def cadenced(a) -> int:
                    "mismatches": sum(len(r.mismatches) for r in replays),
                    "first_mismatches": [m for r in replays for m in r.mismatches][:5]},
         "resources": flat,
+        "poll_to_patch_us": {"samples": len(lat), "p50": pct_us(50), "p90": pct_us(90), "p99": pct_us(99)},
         "signature_failures": sqs.signature_failures(), "kube_auth_failures": kube.auth_failures(),
         "ok": rc == 0 and all(r.ok for r in replays) and all(v and v["flat"] for v in flat.values()),
     }
