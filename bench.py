@@ -79,11 +79,12 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
     is 5 s, /root/reference/main.go:83): ``--cadence-queues`` queues, one thread each, staggered
     over the period, against one endpoint process serving them all (bench/latency.py
     ``measure_cadenced``). Default path (with the CLI's --poll-prewarm) and reference-equivalent
-    path, plain and TLS, with per-phase medians; the plain rows also break every call down
-    (HttpTiming) and report the fake endpoints' own wake-up and service times. The ``_hot_endpoints``
-    rows at 1 s serve the same polls from endpoints that never sleep (a loaded production
-    endpoint): the difference is what the fakes' own idle wake-ups add. Each row keeps >= 400
-    samples."""
+    path, plain and TLS, with per-phase medians. The ``_hot_endpoints`` rows at 1 s serve the same
+    polls from endpoints that never sleep (a loaded production endpoint): the difference is what
+    the fakes' own idle wake-ups add. These rows run uninstrumented; the two ``_timed`` rows at 1 s
+    repeat the default path with every call broken down (HttpTiming on the client, per-request
+    wake-up and service times on the fakes) for the attribution -- the instrumentation adds a few
+    syscalls per request, so their p50 is not the row's number. Each row keeps >= 400 samples."""
     from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced
     from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS
 
@@ -91,18 +92,25 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
     p50, rows = {}, {}
     # (row, mode, pipelined, busy-poll, pre-poll warm-up): the CLI default, and the reference's path
     paths = (("default", args.mode, pipeline, bp, DEFAULT_POLL_PREWARM_NS), ("reference_equivalent", "deployment", False, 0, 0))
+    plan = []
     for label, period in (("250ms", 250 * ms), ("1s", 1000 * ms)):
         for name, mode, pl, b, pw in paths:
             for tls, hot in ((False, False), (True, False), (False, True)):
                 if hot and label != "1s":
                     continue
                 key = name + ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
-                # timing: every call's phases (HttpTiming) in the spans, for the attribution
-                r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls,
-                                     hot_endpoints=hot, prewarm_ns=pw, timing=not tls)
-                rows.setdefault(label, {})[key] = r
-                p50.setdefault(label, {})[key] = r["p50_ms"]
-                _progress(f"cadence {label} {key}: p50 {r['p50_ms']} ms over {r['samples']} samples")
+                plan.append((label, period, key, mode, pl, b, pw, tls, hot, False))
+    name, mode, pl, b, pw = paths[0]
+    for hot in (False, True):
+        plan.append(("1s", 1000 * ms, name + ("_hot_endpoints" if hot else "") + "_timed", mode, pl, b, pw, False, hot,
+                     True))
+    for label, period, key, mode, pl, b, pw, tls, hot, timing in plan:
+        r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls, hot_endpoints=hot,
+                             prewarm_ns=pw, timing=timing)
+        rows.setdefault(label, {})[key] = r
+        if not timing:
+            p50.setdefault(label, {})[key] = r["p50_ms"]
+        _progress(f"cadence {label} {key}: p50 {r['p50_ms']} ms over {r['samples']} samples")
     return {
         "cadenced_p50_ms": p50,
         "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},

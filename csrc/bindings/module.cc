@@ -975,6 +975,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_latency", &FakeSqsServer::set_latency)
       .def("set_cpus", &FakeSqsServer::set_cpus)
       .def("set_hot", &FakeSqsServer::set_hot)
+      .def("set_timing", &FakeSqsServer::set_timing)
       .def("drop_connections", &FakeSqsServer::drop_connections)
       .def("requests", &FakeSqsServer::requests)
       .def("signature_failures", &FakeSqsServer::signature_failures)
@@ -1015,6 +1016,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_latency", &FakeKubeServer::set_latency)
       .def("set_cpus", &FakeKubeServer::set_cpus)
       .def("set_hot", &FakeKubeServer::set_hot)
+      .def("set_timing", &FakeKubeServer::set_timing)
       .def("drop_connections", &FakeKubeServer::drop_connections)
       .def("requests", &FakeKubeServer::requests)
       .def("gets", &FakeKubeServer::gets)

@@ -63,6 +63,7 @@ Status FakeSqsServer::start(const std::string& host, int port, bool tls) {
   server_ = std::make_unique<HttpServer>([this](const HttpRequest& q, HttpResponse* r) { handle(q, r); });
   server_->set_cpus(cpus_);
   server_->set_hot(hot_);
+  server_->set_timing(timing_);
   tls_ = tls;
   if (tls) {
     Status s = generate_self_signed(host, &cert_pem_, &key_pem_);
@@ -272,6 +273,7 @@ Status FakeKubeServer::start(const std::string& host, int port, bool tls) {
   server_ = std::make_unique<HttpServer>([this](const HttpRequest& q, HttpResponse* r) { handle(q, r); });
   server_->set_cpus(cpus_);
   server_->set_hot(hot_);
+  server_->set_timing(timing_);
   tls_ = tls;
   if (tls) {
     Status s = generate_self_signed(host, &cert_pem_, &key_pem_);

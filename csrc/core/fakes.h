@@ -44,6 +44,11 @@ class FakeSqsServer {
   void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
   // HttpServer::set_hot: one busy-polling thread serves every connection (call before start()).
   void set_hot(bool on) { hot_ = on; }
+  // HttpServer::set_timing: record timings() (off by default; any time).
+  void set_timing(bool on) {
+    timing_ = on;
+    if (server_) server_->set_timing(on);
+  }
   Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
   void stop();
   int port() const;
@@ -74,6 +79,7 @@ class FakeSqsServer {
   std::unique_ptr<HttpServer> server_;
   std::vector<int> cpus_;
   bool hot_ = false;
+  bool timing_ = false;
   StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;
@@ -105,6 +111,11 @@ class FakeKubeServer {
   void require_token(std::string token);
   void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
   void set_hot(bool on) { hot_ = on; }
+  // HttpServer::set_timing: record timings() (off by default; any time).
+  void set_timing(bool on) {
+    timing_ = on;
+    if (server_) server_->set_timing(on);
+  }
   Status start(const std::string& host = "127.0.0.1", int port = 0, bool tls = false);
   void stop();
   int port() const;
@@ -160,6 +171,7 @@ class FakeKubeServer {
   std::unique_ptr<HttpServer> server_;
   std::vector<int> cpus_;
   bool hot_ = false;
+  bool timing_ = false;
   StopFlag shutdown_;  // stop() cuts injected-latency sleeps short
   bool tls_ = false;
   std::string cert_pem_, key_pem_;

@@ -1693,13 +1693,20 @@ void HttpServer::serve(int fd) {
     if (ssl) ok = stream.handshake(true, mono_ns() + 10 * kSecond).ok();
     std::string rbuf;
     Reader rd(&stream, &rbuf);
-    int on = 1;
-    const bool stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
+    bool stamps = false, stamps_tried = false;
     while (ok && !stopping_.load()) {
-      // The next request's arrival: its kernel receive time and when this thread got to it.
-      int64_t rx = 0;
-      if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd);
-      const int64_t t_read = realtime_ns();
+      // With timing on: the next request's arrival, its kernel receive time and when this
+      // thread got to it.
+      int64_t rx = 0, t_read = 0;
+      if (timing_.load(std::memory_order_relaxed)) {
+        if (!stamps_tried) {
+          int on = 1;
+          stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
+          stamps_tried = true;
+        }
+        if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd);
+        t_read = realtime_ns();
+      }
       std::string head;
       bool got_any = false;
       if (!rd.read_head(&head, 0, &got_any).ok()) break;
@@ -1813,6 +1820,7 @@ void HttpServer::hot_loop() {
     int fd = -1;
     SSL* ssl = nullptr;
     bool handshaken = false;
+    bool stamps = false, stamps_tried = false;
     std::string rbuf;
   };
   const int ep = epoll_create1(EPOLL_CLOEXEC);
@@ -1846,7 +1854,6 @@ void HttpServer::hot_loop() {
           if (c < 0) break;
           int one = 1;
           setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-          setsockopt(c, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
           accepted_++;
           Conn cn;
           cn.fd = c;
@@ -1881,10 +1888,18 @@ void HttpServer::hot_loop() {
           continue;
         }
       }
-      // the kernel's receive time of the oldest unread byte, when nothing is buffered yet
-      int64_t rx = 0;
-      if (cn.rbuf.empty() && !(cn.ssl && SSL_pending(cn.ssl) > 0)) rx = wait_rx_timestamp(fd);
-      const int64_t t_read = realtime_ns();
+      // with timing on: the kernel's receive time of the oldest unread byte, when nothing is
+      // buffered yet
+      int64_t rx = 0, t_read = 0;
+      if (timing_.load(std::memory_order_relaxed)) {
+        if (!cn.stamps_tried) {
+          int on = 1;
+          cn.stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
+          cn.stamps_tried = true;
+        }
+        if (cn.stamps && cn.rbuf.empty() && !(cn.ssl && SSL_pending(cn.ssl) > 0)) rx = wait_rx_timestamp(fd);
+        t_read = realtime_ns();
+      }
       bool closed = false;
       char tmp[16384];
       for (;;) {

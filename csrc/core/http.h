@@ -243,11 +243,14 @@ class HttpServer {
   void drop_connections();
   // CPUs for the acceptor and connection threads (call before listen(); empty: unpinned).
   void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
-  // Per request served (the latest 64K): the wake-up delay -- the kernel's receive timestamp
-  // of the request's first segment (SO_TIMESTAMPNS) to the connection thread running -- and
-  // the service time, from then to the response written. A benchmark subtracts the first from
-  // a client's round trip: it is what a fake endpoint idle between polls adds by sleeping,
-  // which a production endpoint does not.
+  // Per request served (the latest 64K) while set_timing(true): the wake-up delay -- the
+  // kernel's receive timestamp of the request's first segment (SO_TIMESTAMPNS) to the
+  // connection thread running -- and the service time, from then to the response written. A
+  // benchmark subtracts the first from a client's round trip: it is what a fake endpoint idle
+  // between polls adds by sleeping, which a production endpoint does not. Off by default: the
+  // receive timestamp costs a poll(2) and a peeking recvmsg(2) per request on the endpoint's
+  // side of every round trip (any time; applies from each connection's next request).
+  void set_timing(bool on) { timing_.store(on, std::memory_order_relaxed); }
   struct ServeTiming {
     int64_t wake_ns;
     int64_t service_ns;
@@ -285,6 +288,7 @@ class HttpServer {
   std::atomic<uint64_t> served_{0};
   std::atomic<uint64_t> accepted_{0};
   std::vector<int> cpus_;
+  std::atomic<bool> timing_{false};
   mutable std::mutex timing_mu_;
   std::vector<ServeTiming> timings_;
   size_t timing_pos_ = 0;

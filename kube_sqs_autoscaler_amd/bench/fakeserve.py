@@ -29,11 +29,12 @@ def main(argv=None) -> int:
     ap.add_argument("--cpus", default="", help="JSON list: the CPU list of each pair's threads")
     ap.add_argument("--queue-offset", type=int, default=0, help="number of the first bench queue served")
     ap.add_argument("--hot", action="store_true", help="busy-polling servers that never sleep (HttpServer::set_hot)")
+    ap.add_argument("--timing", action="store_true", help="record per-request timings (HttpServer::set_timing)")
     a = ap.parse_args(argv)
     nat = native()
     cpus = json.loads(a.cpus) if a.cpus else None
     sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus,
-                                     a.queue_offset, hot=a.hot)
+                                     a.queue_offset, hot=a.hot, timing=a.timing)
     try:
         info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],
                 "kube": [{"url": k.url, "cert_pem": k.cert_pem} for k in kube]}

@@ -85,11 +85,13 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
 
 def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
                          kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None, offset: int = 0,
-                         hot: bool = False):
+                         hot: bool = False, timing: bool = False):
     """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues numbered from
     ``offset`` (queue offset+q on pair q % n_servers): the 200 <-> 0 attribute cycle per queue
     and one Deployment per queue. ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned).
-    ``hot``: each server is one busy-polling thread that never sleeps (HttpServer::set_hot)."""
+    ``hot``: each server is one busy-polling thread that never sleeps (HttpServer::set_hot).
+    ``timing``: the servers record each request's wake-up delay and service time
+    (HttpServer::set_timing; off by default, it adds two syscalls per request)."""
     sqs_servers, kube_servers = [], []
     for i in range(n_servers):
         sqs = nat.FakeSqsServer()
@@ -101,6 +103,8 @@ def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sq
             kube.set_cpus(cpus[i])
         sqs.set_hot(hot)
         kube.set_hot(hot)
+        sqs.set_timing(timing)
+        kube.set_timing(timing)
         sqs.start("127.0.0.1", 0, tls)
         sqs.set_latency(sqs_latency_ns)
         kube.start("127.0.0.1", 0, tls)
@@ -135,13 +139,15 @@ class RemoteEndpoints:
     processes -- their threads do not share the autoscaler's process, allocator or CPU share."""
 
     def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int,
-                 cpus: Optional[List[List[int]]] = None, offset: int = 0, hot: bool = False):
+                 cpus: Optional[List[List[int]]] = None, offset: int = 0, hot: bool = False,
+                 timing: bool = False):
         import json
         import subprocess
         import sys
 
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        extra = (["--cpus", json.dumps(cpus)] if cpus is not None else []) + (["--hot"] if hot else [])
+        extra = ((["--cpus", json.dumps(cpus)] if cpus is not None else []) + (["--hot"] if hot else [])
+                 + (["--timing"] if timing else []))
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "kube_sqs_autoscaler_amd.bench.fakeserve", "--queues", str(queues), "--pairs",
              str(n_servers), "--tls", str(int(tls)), "--sqs-latency-ns", str(sqs_latency_ns), "--kube-latency-ns",
@@ -198,7 +204,8 @@ class BenchEnv:
     production endpoint is (supported with ``shared`` and ``process``). ``prewarm_ns``: the
     loop's pre-poll warm-up (``--poll-prewarm``); it and ``busy_poll_ns`` may be lists, one
     value per queue, cycled (paired comparisons within one run). ``timing``: the clients time every request's
-    phases (HttpTiming) and traced polls carry the breakdown (``detail``)."""
+    phases (HttpTiming), traced polls carry the breakdown (``detail``), and the fakes record each
+    request's wake-up delay and service time (HttpServer::set_timing)."""
 
     def __init__(self, queues: int, mode: str = "scale", tls: bool = False, sqs_latency_ns: int = 0,
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
@@ -214,17 +221,20 @@ class BenchEnv:
         self.remote = None
         self.remotes = []
         if servers == "process":
-            self.remote = RemoteEndpoints(queues, 1, tls, sqs_latency_ns, kube_latency_ns, hot=hot_endpoints)
+            self.remote = RemoteEndpoints(queues, 1, tls, sqs_latency_ns, kube_latency_ns, hot=hot_endpoints,
+                                          timing=timing)
             self.remotes = [self.remote]
             self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
         elif servers == "processes":
-            self.remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns, offset=q) for q in range(queues)]
+            self.remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns, offset=q, timing=timing)
+                            for q in range(queues)]
             self.remote = self.remotes[0]
             self.sqs_servers = [r.sqs[0] for r in self.remotes]
             self.kube_servers = [r.kube[0] for r in self.remotes]
         elif servers in ("shared", "per-queue"):
             self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
-                                                                       kube_latency_ns, hot=hot_endpoints)
+                                                                       kube_latency_ns, hot=hot_endpoints,
+                                                                       timing=timing)
         else:
             raise ValueError(f"servers must be shared, per-queue, process or processes, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
@@ -541,12 +551,13 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
         "signature_failures": res.signature_failures,
         "phase_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
                             "patch_us": med("patch_latency_ns")},
-        # The fake endpoints' side of each request (HttpServer::timings): how long the endpoint's
-        # thread took to wake up for it after the kernel received it, and to answer it.
-        "endpoint_median_us": {k: {"wake": _median_us([w for w, _ in v]), "service": _median_us([sv for _, sv in v])}
-                               for k, v in served.items()},
         "wall_s": round(wall, 2),
-        **({"call_phase_median_us": _detail_medians(scaled)} if timing else {}),
+        # With timing: the fake endpoints' side of each request (HttpServer::timings) -- how long
+        # the endpoint's thread took to wake up for it after the kernel received it, and to answer
+        # it -- and every client call's phases.
+        **({"endpoint_median_us": {k: {"wake": _median_us([w for w, _ in v]),
+                                       "service": _median_us([sv for _, sv in v])} for k, v in served.items()},
+            "call_phase_median_us": _detail_medians(scaled)} if timing else {}),
     }
 
 

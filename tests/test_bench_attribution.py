@@ -1,0 +1,37 @@
+"""The bench's attribution instrumentation (bench/latency.py): client HttpTiming and the fakes'
+per-request wake-up/service times are recorded only when asked for -- the fake's receive-time
+stamp costs syscalls on every round trip, so the latency rows run without it."""
+import pytest
+
+from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, measure_cadenced
+
+
+@pytest.mark.parametrize("timing", [False, True])
+def test_fake_server_timings_only_when_enabled(nat, timing):
+    env = BenchEnv(1, timing=timing)
+    try:
+        env.run(20)
+        served = env.server_timings()
+    finally:
+        env.close()
+    if not timing:
+        assert served == {"sqs": [], "kube": []}
+        return
+    assert len(served["sqs"]) >= 20 and len(served["kube"]) >= 20
+    assert all(wake >= 0 and service > 0 for wake, service in served["sqs"] + served["kube"])
+
+
+@pytest.mark.parametrize("servers", ["shared", "process"])
+def test_cadenced_rows_attribute_only_the_timed_runs(nat, servers):
+    plain = measure_cadenced(20_000_000, 6, queues=4, busy_poll_ns=25_000, servers=servers, prewarm_ns=200_000)
+    timed = measure_cadenced(20_000_000, 6, queues=4, busy_poll_ns=25_000, servers=servers, prewarm_ns=200_000,
+                             timing=True)
+    for r in (plain, timed):
+        assert r["samples"] >= 12 and r["errors"] == 0 and r["signature_failures"] == 0
+        assert r["p50_ms"] > 0
+    assert "call_phase_median_us" not in plain and "endpoint_median_us" not in plain
+    calls = timed["call_phase_median_us"]
+    assert {"sign", "write", "wait", "read", "parse"} <= set(calls["sqs"])
+    assert {"write", "wait"} <= set(calls["write"])
+    assert timed["endpoint_median_us"]["sqs"]["service"] > 0
+    assert timed["endpoint_median_us"]["kube"]["service"] > 0

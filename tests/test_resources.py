@@ -68,11 +68,11 @@ def test_fits_the_reference_pod_resources(endpoints, queues, procs):
             pids = [p.pid] + [int(x) for x in f.read().split()]
         assert len(pids) == (1 + queues if procs else 1)
         before, t0, r0 = _cpu_ticks(pids), time.monotonic(), sqs.requests()
-        time.sleep(2.0)
+        time.sleep(5.0)  # long enough that per-process tick rounding (8 processes) stays small
         ticks, wall, polls = _cpu_ticks(pids) - before, time.monotonic() - t0, sqs.requests() - r0
         pss = sum(_pss_kb(x) for x in pids)
         hz = os.sysconf("SC_CLK_TCK")
-        assert polls >= queues * 5  # it was polling all along (200 ms period)
+        assert polls >= queues * 15  # it was polling all along (200 ms period)
         assert pss < LIMIT_KB / 2, pss
         assert ticks / hz / wall < 0.05, (ticks, wall)  # < 50m of the reference's 100m
     finally:
