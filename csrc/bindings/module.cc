@@ -717,7 +717,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("scale_down_messages", &LoopConfig::scale_down_messages)
       .def_readwrite("prefetch", &LoopConfig::prefetch)
       .def_readwrite("prefetch_always", &LoopConfig::prefetch_always)
-      .def_readwrite("prewarm_ns", &LoopConfig::prewarm);
+      .def_readwrite("prewarm_ns", &LoopConfig::prewarm)
+      .def_readwrite("connect_at_start", &LoopConfig::connect_at_start);
 
   py::class_<Runner, std::shared_ptr<Runner>>(m, "Runner")
       .def(py::init<LoopConfig, std::shared_ptr<SqsClient>, std::shared_ptr<PodAutoScaler>, std::shared_ptr<Clock>,

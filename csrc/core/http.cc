@@ -135,8 +135,10 @@ Status wait_fd(int fd, short events, int64_t deadline_ns, int cancel_fd = -1) {
   }
 }
 
-// A non-blocking socket, optionally wrapped in TLS, with deadline-bounded I/O.
-class Stream {
+// A non-blocking socket, optionally wrapped in TLS, with deadline-bounded I/O. Cache-line
+// aligned, as Conn: the streams of different workers' clients never share a line, whichever
+// thread dialled them.
+class alignas(kCacheLine) Stream {
  public:
   Stream(int fd, SSL* ssl) : fd_(fd), ssl_(ssl) {}
   ~Stream() {
@@ -913,7 +915,11 @@ Status socks5_connect(Stream* stream, std::string* rbuf, const Url& proxy, const
 
 }  // namespace
 
-struct HttpClient::Conn {
+// Cache-line aligned: a connection's per-request fields (uses, last_response_ns, the read
+// buffer's pointers) are written on every request by the worker that owns it; connections of
+// several workers dialled from one thread would otherwise sit next to each other in that
+// thread's allocator arena and share cache lines.
+struct alignas(kCacheLine) HttpClient::Conn {
   std::unique_ptr<Stream> stream;
   std::string rbuf;
   uint64_t uses = 0;
@@ -1693,17 +1699,21 @@ void HttpServer::serve(int fd) {
     if (ssl) ok = stream.handshake(true, mono_ns() + 10 * kSecond).ok();
     std::string rbuf;
     Reader rd(&stream, &rbuf);
+    // receive stamps from the first request on when timing is already on (a socket stamps only
+    // the segments queued after the option is set); else from the first request after it is
     bool stamps = false, stamps_tried = false;
+    auto arm_stamps = [&] {
+      int on = 1;
+      stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
+      stamps_tried = true;
+    };
+    if (timing_.load(std::memory_order_relaxed)) arm_stamps();
     while (ok && !stopping_.load()) {
       // With timing on: the next request's arrival, its kernel receive time and when this
       // thread got to it.
       int64_t rx = 0, t_read = 0;
       if (timing_.load(std::memory_order_relaxed)) {
-        if (!stamps_tried) {
-          int on = 1;
-          stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
-          stamps_tried = true;
-        }
+        if (!stamps_tried) arm_stamps();
         if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd);
         t_read = realtime_ns();
       }
@@ -1857,6 +1867,10 @@ void HttpServer::hot_loop() {
           accepted_++;
           Conn cn;
           cn.fd = c;
+          if (timing_.load(std::memory_order_relaxed)) {
+            cn.stamps = setsockopt(c, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one) == 0;
+            cn.stamps_tried = true;
+          }
           if (ctx_) {
             cn.ssl = SSL_new(ctx_);
             SSL_set_fd(cn.ssl, c);

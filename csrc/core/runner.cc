@@ -397,6 +397,10 @@ void Runner::write_trace(const IterationRecord& r) {
 
 void Runner::run(StopFlag* stop, int64_t max_iterations, Nanos start_delay) {
   if (start_delay > 0 && !clock_->sleep(start_delay, stop)) return;
+  if (cfg_.connect_at_start) {
+    sqs_->warm(clock_->unix_nanos());
+    if (cfg_.prefetch) scaler_->warm();
+  }
   arm();
   int64_t done = 0;
   while (!(stop && stop->stopped())) {

@@ -57,6 +57,12 @@ struct LoopConfig {
   // up to `prewarm` of CPU per poll. 0 disables. With a poll period under 2x `prewarm` the
   // preparation runs at the due time instead, without the early wake-up.
   Nanos prewarm = 0;
+  // Dial both clients at Run() entry, on the worker's own thread, before the timers are armed
+  // (decisions unchanged). A harness that would otherwise connect them from its main thread
+  // (the bench) gets each connection's TLS state and buffers from the worker's allocator arena
+  // instead of one shared arena. The CLI needs none: its first poll, or its first warm-up, dials
+  // on the worker thread.
+  bool connect_at_start = false;
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };

@@ -283,8 +283,10 @@ class BenchEnv:
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
             cfg.prewarm_ns = pw_q
-            if pipeline:
-                scaler.warm()  # connect the apiserver client, as --poll-prewarm does before a poll
+            # connect both clients when the worker starts, on its own thread (as --poll-prewarm
+            # does before a poll): the on-wire GET never dials, and a dial from this thread would
+            # put every worker's connection state in this thread's allocator arena, side by side
+            cfg.connect_at_start = True
             self.server_of.append(si)
             self.kube_apis.append(kube_api)
             self.sqs_apis.append(sqs_api)
