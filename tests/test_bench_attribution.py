@@ -35,3 +35,19 @@ def test_cadenced_rows_attribute_only_the_timed_runs(nat, servers):
     assert {"write", "wait"} <= set(calls["write"])
     assert timed["endpoint_median_us"]["sqs"]["service"] > 0
     assert timed["endpoint_median_us"]["kube"]["service"] > 0
+
+
+def test_bench_workers_dial_their_own_connections(nat):
+    """LoopConfig.connect_at_start: nothing is dialled while the bench environment is built (on
+    the harness's thread); each worker connects both clients when it starts, so even its first
+    poll sends the Deployment GET with the SQS request."""
+    env = BenchEnv(2)
+    try:
+        assert env.kube_servers[0].connections() == 0 and env.sqs_servers[0].connections() == 0
+        env.run(3)
+        assert env.kube_servers[0].connections() == 2 and env.sqs_servers[0].connections() == 2
+        for r in env.runners:
+            st = r.stats()
+            assert st["polls"] == 3 and st["speculative_reads"] == 3 and st["speculative_reads_used"] == 3
+    finally:
+        env.close()
