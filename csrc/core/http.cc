@@ -1569,6 +1569,9 @@ Status HttpServer::listen(const std::string& host, int port) {
   }
   int one = 1;
   setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  // with timing on from the start, accepted sockets inherit receive stamps from the listener:
+  // a client's first request can arrive before its connection thread runs
+  if (timing_.load(std::memory_order_relaxed)) setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
   if (::bind(fd, res->ai_addr, res->ai_addrlen) != 0 || ::listen(fd, 128) != 0) {
     std::string e = std::strerror(errno);
     ::close(fd);

@@ -8,10 +8,19 @@ from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, measure_cadenced
 
 @pytest.mark.parametrize("timing", [False, True])
 def test_fake_server_timings_only_when_enabled(nat, timing):
+    import time
+
     env = BenchEnv(1, timing=timing)
     try:
         env.run(20)
-        served = env.server_timings()
+        served = {"sqs": [], "kube": []}
+        deadline = time.monotonic() + 2
+        while True:  # a request is recorded after its response is written: the last may lag
+            for k, v in env.server_timings().items():
+                served[k] += v
+            if not timing or (len(served["sqs"]) >= 20 and len(served["kube"]) >= 20) or time.monotonic() > deadline:
+                break
+            time.sleep(0.01)
     finally:
         env.close()
     if not timing:
