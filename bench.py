@@ -142,7 +142,11 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence-polls", type=int, default=27,
                     help="polls per queue per production-cadence row (the first 2 of each queue are dropped)")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
+    ap.add_argument("--extras-budget-s", type=float, default=450.0,
+                    help="seconds after start past which the remaining secondary sections are skipped "
+                         "(recorded under extra.skipped_sections); the headline line is always printed")
     args = ap.parse_args(argv)
+    t_start = time.monotonic()
 
     import torch
     import torch.distributed as dist
@@ -230,7 +234,20 @@ def main(argv=None) -> int:
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
         }
-        if world == 1 and not args.no_sweep:
+        def guarded(name, fn, budgeted=True):
+            """One secondary section: its failure or the time budget costs that section only --
+            the headline line is printed whatever happens here."""
+            if budgeted and time.monotonic() - t_start > args.extras_budget_s:
+                extra.setdefault("skipped_sections", []).append(name)
+                _progress(f"{name}: skipped (past --extras-budget-s)")
+                return
+            try:
+                fn()
+            except Exception as e:  # noqa: BLE001 -- recorded, never fatal to the headline
+                extra.setdefault("section_errors", {})[name] = f"{type(e).__name__}: {e}"
+                _progress(f"{name} failed: {type(e).__name__}: {e}")
+
+        def secondary():
             # Secondary rows: three interleaved rounds, median p50 per row, so one disturbed run
             # (CPU migration, a noisy neighbour) cannot invert the comparison.
             n, w = args.secondary_samples, 200
@@ -291,10 +308,16 @@ def main(argv=None) -> int:
                 # the same hot loop with every call timed (HttpTiming), next to the cadence rows' breakdown
                 "default_timed": phase_breakdown(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp, timing=True),
             }
+
+        def parity():
+            extra["decision_parity"] = _parity_summary()
+            extra["apiserver_requests_per_poll"] = _apiserver_requests_per_poll(extra["decision_parity"])
+
+        if world == 1 and not args.no_sweep:
+            guarded("secondary_rows", secondary)
         if world == 1 and not args.no_sweep and not args.no_cadence:
-            extra.update(_cadence_rows(args, pipeline, bp, p50))
-        extra["decision_parity"] = _parity_summary()
-        extra["apiserver_requests_per_poll"] = _apiserver_requests_per_poll(extra["decision_parity"])
+            guarded("cadence_rows", lambda: extra.update(_cadence_rows(args, pipeline, bp, p50)))
+        guarded("decision_parity", parity, budgeted=False)  # seconds; part of the metric's name
         out = {
             "metric": METRIC,
             "value": round(p50, 4),

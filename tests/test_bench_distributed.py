@@ -42,3 +42,15 @@ def test_bench_two_ranks_gloo():
     out = _json_line(r.stdout)
     _check(out, 2, 150, 10)
     assert out["extra"]["tracked_queues"] == 2
+
+
+def test_bench_prints_its_line_when_secondary_sections_run_out_of_time():
+    """--extras-budget-s: sections past the budget are skipped and named; the headline line and
+    the decision parity (part of the metric) are still there."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "50", "--warmup", "5", "--extras-budget-s", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = _json_line(r.stdout)
+    _check(out, 1, 50, 5)
+    assert out["extra"]["skipped_sections"] == ["secondary_rows", "cadence_rows"]
+    assert "section_errors" not in out["extra"] and "cadenced_p50_ms" not in out["extra"]
