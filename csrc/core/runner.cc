@@ -635,7 +635,7 @@ void Scheduler::start(int64_t max_iterations) {
       heap_.push_back(Item{t0 + static_cast<Nanos>(static_cast<double>(period) * i / n), i, true});
     } else {
       runners_[i]->arm();
-      heap_.push_back(Item{t0 + period, i, false});
+      push_poll(i, t0, false);  // heapified below
     }
   }
   std::make_heap(heap_.begin(), heap_.end(), std::greater<Item>());
@@ -646,6 +646,17 @@ void Scheduler::start(int64_t max_iterations) {
       pthread_setname_np(pthread_self(), "ksa-sched");
       worker();
     });
+}
+
+void Scheduler::push_poll(size_t idx, Nanos from, bool heapify) {
+  const LoopConfig& c = runners_[idx]->config();
+  const Nanos period = std::max<Nanos>(c.poll_period, 0), w = c.prewarm;
+  const Nanos due = from + period;  // sleep-then-poll (main.go:41)
+  if (w > 0 && period > 2 * w)
+    heap_.push_back(Item{due - w, idx, false, due});
+  else
+    heap_.push_back(Item{due, idx, false});
+  if (heapify) std::push_heap(heap_.begin(), heap_.end(), std::greater<Item>());
 }
 
 void Scheduler::worker() {
@@ -668,7 +679,16 @@ void Scheduler::worker() {
     heap_.pop_back();
     if (top.arm) {  // staggered start: Run() entry for this queue
       runners_[top.idx]->arm();
-      heap_.push_back(Item{clock_->now() + std::max<Nanos>(runners_[top.idx]->config().poll_period, 0), top.idx, false});
+      push_poll(top.idx, clock_->now());
+      cv_.notify_all();
+      continue;
+    }
+    if (top.poll_at > 0) {  // --poll-prewarm: prepare now, poll at its due time (no spinning here:
+                            // the thread serves other queues meanwhile)
+      lk.unlock();
+      runners_[top.idx]->prepare(top.poll_at);
+      lk.lock();
+      heap_.push_back(Item{top.poll_at, top.idx, false});
       std::push_heap(heap_.begin(), heap_.end(), std::greater<Item>());
       cv_.notify_all();
       continue;
@@ -683,8 +703,7 @@ void Scheduler::worker() {
     if (max_iter_ > 0 && ++done_[top.idx] >= max_iter_) {
       ++finished_;
     } else {
-      heap_.push_back(Item{clock_->now() + std::max<Nanos>(runners_[top.idx]->config().poll_period, 0), top.idx});
-      std::push_heap(heap_.begin(), heap_.end(), std::greater<Item>());
+      push_poll(top.idx, clock_->now());
     }
     cv_.notify_all();
   }

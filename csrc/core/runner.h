@@ -206,6 +206,9 @@ class alignas(kCacheLine) Runner {
   // The iteration without the leading sleep (main.go:43-77); used by Scheduler, which owns
   // the waiting between polls.
   IterationRecord poll_once();
+  // The pre-poll warm-up (LoopConfig::prewarm) for a poll due at `due`, without waiting: the
+  // Scheduler runs it as its own event `prewarm` before the poll's.
+  void prepare(Nanos due) { warm(due); }
   // Shutdown: aborts this worker's API call in progress and its back-off/throttle waits.
   void cancel() {
     sqs_->cancel();
@@ -414,8 +417,12 @@ class Scheduler {
     Nanos due;
     size_t idx;
     bool arm = false;  // start event: arm the runner, first poll one period later
+    Nanos poll_at = 0;  // > 0: a warm-up event (Runner::prepare) for the poll due then
     bool operator>(const Item& o) const { return due != o.due ? due > o.due : idx > o.idx; }
   };
+  // Queues runner idx's next poll one period after `from`: preceded by a warm-up event when its
+  // LoopConfig::prewarm fits the period (the same rule as Runner::step).
+  void push_poll(size_t idx, Nanos from, bool heapify = true);
   void worker();
 
   size_t nthreads_;

@@ -15,9 +15,15 @@ from ..ops import native
 from .latency import BenchEnv
 
 
-def run_capacity(queues: int, period_s: float, threads: int, duration_s: float = 5.0) -> Dict[str, float]:
+def run_capacity(queues: int, period_s: float, threads: int, duration_s: float = 5.0,
+                 prewarm_ns: int = -1) -> Dict[str, float]:
     """Steady-state numbers are taken after a warm-up of two poll periods (connections set up,
-    staggered starts done)."""
+    staggered starts done). ``prewarm_ns``: each queue's --poll-prewarm (-1: the CLI default),
+    which the scheduler runs as a separate event before each poll."""
+    from ..config import DEFAULT_POLL_PREWARM_NS
+
+    if prewarm_ns < 0:
+        prewarm_ns = DEFAULT_POLL_PREWARM_NS
     nat = native()
     env = BenchEnv(queues)
     try:
@@ -29,6 +35,7 @@ def run_capacity(queues: int, period_s: float, threads: int, duration_s: float =
             cfg.scale_up_cool_down_ns = 0
             cfg.scale_down_cool_down_ns = 0
             cfg.prefetch = True
+            cfg.prewarm_ns = prewarm_ns
             rr = nat.Runner(cfg, r.sqs, r.scaler, nat.RealClock(), env.log)
             runners.append(rr)
             sched.add(rr)
@@ -47,6 +54,7 @@ def run_capacity(queues: int, period_s: float, threads: int, duration_s: float =
             "queues": queues,
             "threads": threads,
             "poll_period_s": period_s,
+            "prewarm_us": prewarm_ns / 1e3,
             "polls_per_s": round(polls / wall, 1),
             "ideal_polls_per_s": round(queues / period_s, 1),
             "late_poll_fraction": round(late / max(polls, 1), 4),

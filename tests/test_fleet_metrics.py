@@ -151,6 +151,35 @@ def test_pooled_scheduler_keeps_cadence(nat, tmp_path):
         env.close()
 
 
+@pytest.mark.parametrize("prewarm_ns", [0, 2_000_000])
+def test_pooled_scheduler_runs_the_pre_poll_warm_up(nat, prewarm_ns):
+    """--poll-prewarm under the pooled scheduler: a warm-up event of its own before each poll
+    (no spinning on a shared thread). It dials the apiserver client before the first poll, so
+    even that poll pipelines its GET; without it the first GET is synchronous (the on-wire GET
+    never dials). Decisions are the same either way."""
+    env = BenchEnv(8)
+    try:
+        cfg = nat.LoopConfig()
+        cfg.poll_period_ns = 20_000_000
+        cfg.scale_up_cool_down_ns = 0
+        cfg.scale_down_cool_down_ns = 0
+        cfg.prefetch = True
+        cfg.prewarm_ns = prewarm_ns
+        runners = [nat.Runner(cfg, r.sqs, r.scaler, nat.RealClock(), env.log) for r in env.runners]
+        fleet = Fleet([W(r, t) for r, t in zip(runners, env.targets)], threads=2)
+        assert fleet.pooled
+        fleet.start(4)
+        assert fleet.wait(60)
+        fleet.join()
+        stats = fleet.stats()
+        assert all(s["polls"] == 4 and s["scale_ups"] == 2 and s["scale_downs"] == 2 for s in stats)
+        want = 4 if prewarm_ns else 3
+        assert all(s["speculative_reads_used"] == want for s in stats), [s["speculative_reads_used"] for s in stats]
+        assert env.sqs.signature_failures() == 0
+    finally:
+        env.close()
+
+
 def test_liveness_detects_a_wedged_worker(nat):
     """/healthz fails once a running worker makes no progress for longer than its budget
     (here an SQS call that takes 1.5 s against a 0.2 s budget)."""
