@@ -74,7 +74,7 @@ def _progress(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
+def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: float = float("inf")) -> dict:
     """Poll->patch latency at production poll periods (250 ms and 1 s; the reference's default
     is 5 s, /root/reference/main.go:83): ``--cadence-queues`` queues, one thread each, staggered
     over the period, against one endpoint process serving them all (bench/latency.py
@@ -84,7 +84,8 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
     the fakes' own idle wake-ups add. These rows run uninstrumented; the two ``_timed`` rows at 1 s
     repeat the default path with every call broken down (HttpTiming on the client, per-request
     wake-up and service times on the fakes) for the attribution -- the instrumentation adds a few
-    syscalls per request, so their p50 is not the row's number. Each row keeps >= 400 samples."""
+    syscalls per request, so their p50 is not the row's number. Each row keeps >= 400 samples.
+    Rows that would start past ``deadline`` (time.monotonic) are skipped and listed."""
     from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced
     from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS
 
@@ -104,18 +105,26 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float) -> dict:
     for hot in (False, True):
         plan.append(("1s", 1000 * ms, name + ("_hot_endpoints" if hot else "") + "_timed", mode, pl, b, pw, False, hot,
                      True))
+    skipped = []
     for label, period, key, mode, pl, b, pw, tls, hot, timing in plan:
+        if time.monotonic() > deadline:
+            skipped.append(f"{label}/{key}")
+            continue
         r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls, hot_endpoints=hot,
                              prewarm_ns=pw, timing=timing)
         rows.setdefault(label, {})[key] = r
         if not timing:
             p50.setdefault(label, {})[key] = r["p50_ms"]
         _progress(f"cadence {label} {key}: p50 {r['p50_ms']} ms over {r['samples']} samples")
+    if skipped:
+        _progress(f"cadence rows skipped (past --extras-budget-s): {skipped}")
     return {
+        **({"cadenced_rows_skipped": skipped} if skipped else {}),
         "cadenced_p50_ms": p50,
         "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
         "cadenced_rows": rows,
-        "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()},
+        "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()
+                                               if "default" in v},
     }
 
 
@@ -142,8 +151,8 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence-polls", type=int, default=27,
                     help="polls per queue per production-cadence row (the first 2 of each queue are dropped)")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
-    ap.add_argument("--extras-budget-s", type=float, default=450.0,
-                    help="seconds after start past which the remaining secondary sections are skipped "
+    ap.add_argument("--extras-budget-s", type=float, default=400.0,
+                    help="seconds after start past which the remaining secondary sections and cadence rows are skipped "
                          "(recorded under extra.skipped_sections); the headline line is always printed")
     args = ap.parse_args(argv)
     t_start = time.monotonic()
@@ -316,7 +325,8 @@ def main(argv=None) -> int:
         if world == 1 and not args.no_sweep:
             guarded("secondary_rows", secondary)
         if world == 1 and not args.no_sweep and not args.no_cadence:
-            guarded("cadence_rows", lambda: extra.update(_cadence_rows(args, pipeline, bp, p50)))
+            guarded("cadence_rows", lambda: extra.update(
+                _cadence_rows(args, pipeline, bp, p50, deadline=t_start + args.extras_budget_s)))
         guarded("decision_parity", parity, budgeted=False)  # seconds; part of the metric's name
         out = {
             "metric": METRIC,

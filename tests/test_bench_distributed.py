@@ -54,3 +54,17 @@ def test_bench_prints_its_line_when_secondary_sections_run_out_of_time():
     _check(out, 1, 50, 5)
     assert out["extra"]["skipped_sections"] == ["secondary_rows", "cadence_rows"]
     assert "section_errors" not in out["extra"] and "cadenced_p50_ms" not in out["extra"]
+
+
+def test_cadence_rows_past_their_deadline_are_skipped_and_named():
+    """The cadence section checks the budget before every row (12 rows of up to ~27 s each), so a
+    slow box cannot run the whole section past --extras-budget-s."""
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=1)
+    out = bench._cadence_rows(args, True, 0, 0.02, deadline=0.0)
+    assert len(out["cadenced_rows_skipped"]) == 12 and "250ms/default" in out["cadenced_rows_skipped"]
+    assert out["cadenced_p50_ms"] == {} and out["cadenced_vs_hot_loop_default_plain"] == {}
