@@ -313,6 +313,10 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         raise FlagError(f'invalid value "{cfg.scale_mode}" for flag -scale-mode: must be one of {", ".join(SCALE_MODES)}')
     if cfg.sqs_protocol not in SQS_PROTOCOLS:
         raise FlagError(f'invalid value "{cfg.sqs_protocol}" for flag -sqs-protocol: must be query or json')
+    if cfg.metrics_addr:
+        host, sep, port = cfg.metrics_addr.rpartition(":")
+        if not sep or not port.isdigit() or int(port) > 65535 or (":" in host and not host.startswith("[")):
+            raise FlagError(f'invalid value "{cfg.metrics_addr}" for flag -metrics-addr: want host:port, :port or [ipv6]:port')
     if cfg.log_format not in ("text", "json"):
         raise FlagError(f'invalid value "{cfg.log_format}" for flag -log-format: must be text or json')
     if cfg.leader_elect and not (cfg.leader_elect_lease_duration_ns > cfg.leader_elect_renew_deadline_ns

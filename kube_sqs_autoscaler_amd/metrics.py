@@ -11,6 +11,7 @@ Endpoints on ``--metrics-addr``: ``/metrics`` (Prometheus text format), ``/healt
 from __future__ import annotations
 
 import math
+import socket
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import List, Optional, Sequence, Tuple
@@ -215,8 +216,40 @@ class Health:
 
 
 def parse_addr(addr: str) -> Tuple[str, int]:
-    host, _, port = addr.rpartition(":")
-    return (host or "0.0.0.0"), int(port)
+    """Go's ``host:port`` listen address: ``:9090`` (every interface), ``0.0.0.0:9090``,
+    ``[::]:9090`` (an IPv6 literal in brackets). Returns ("", port) for every interface."""
+    host, sep, port = addr.rpartition(":")
+    if not sep:
+        raise ValueError(f"address {addr}: missing port in address")
+    if host.startswith("[") and host.endswith("]"):
+        host = host[1:-1]
+    return host, int(port)
+
+
+class _Server(ThreadingHTTPServer):
+    daemon_threads = True
+    dual_stack = False
+
+    def server_bind(self) -> None:
+        if self.dual_stack:  # "[::]" taking IPv4 too, as Go's ":port" listener does
+            self.socket.setsockopt(socket.IPPROTO_IPV6, socket.IPV6_V6ONLY, 0)
+        super().server_bind()
+
+
+def _listen(host: str, port: int, handler) -> ThreadingHTTPServer:
+    if host:
+        cls = type("_Server6" if ":" in host else "_Server4", (_Server,),
+                   {"address_family": socket.AF_INET6 if ":" in host else socket.AF_INET})
+        return cls((host, port), handler)
+    # every interface: dual-stack IPv6 where the host has it (an IPv6-only cluster reaches the
+    # pod on its IPv6 address), plain IPv4 otherwise
+    if socket.has_ipv6:
+        try:
+            cls = type("_ServerDual", (_Server,), {"address_family": socket.AF_INET6, "dual_stack": True})
+            return cls(("::", port), handler)
+        except OSError:
+            pass
+    return type("_Server4", (_Server,), {"address_family": socket.AF_INET})(("0.0.0.0", port), handler)
 
 
 class MetricsServer:
@@ -246,7 +279,7 @@ class MetricsServer:
                 pass
 
         host, port = parse_addr(addr)
-        self.httpd = ThreadingHTTPServer((host, port), Handler)
+        self.httpd = _listen(host, port, Handler)
         self.port = self.httpd.server_address[1]
         self._thread: Optional[threading.Thread] = None
 

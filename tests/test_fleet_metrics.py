@@ -385,3 +385,42 @@ def test_fleet_staggers_queue_starts(nat, tmp_path):
     first = sorted((s["ts"] - s["total_ns"]) for s in spans if s["poll"] == 1)
     gaps = [(b - a) / 1e6 for a, b in zip(first, first[1:])]
     assert len(first) == 4 and all(35 < g < 65 for g in gaps), gaps  # 50 ms apart
+
+
+def test_metrics_listen_addresses():
+    """Go-style listen addresses: ``:port`` listens on every interface (dual-stack where the host
+    has IPv6, so an IPv6-only cluster reaches it), ``[::1]:port`` an IPv6 literal; a bad
+    --metrics-addr is a flag error, not a traceback at start-up."""
+    import socket
+
+    from kube_sqs_autoscaler_amd.config import config_from_flags, new_flag_set
+    from kube_sqs_autoscaler_amd.metrics import parse_addr
+    from kube_sqs_autoscaler_amd.utils.goflag import FlagError
+
+    assert parse_addr(":9090") == ("", 9090) and parse_addr("[::1]:80") == ("::1", 80)
+    assert parse_addr("127.0.0.1:0") == ("127.0.0.1", 0)
+    for bad in ("9090", "host:port", "::1:80", ":70000"):
+        fs = new_flag_set("kube-sqs-autoscaler")
+        fs.parse([f"--metrics-addr={bad}"])
+        with pytest.raises(FlagError, match="metrics-addr"):
+            config_from_flags(fs, {})
+
+    class _Fleet:
+        workers, stopped, started = [], False, False
+
+        def stats(self):
+            return []
+
+    addrs = [":0", "127.0.0.1:0"] + (["[::1]:0"] if socket.has_ipv6 else [])
+    for addr in addrs:
+        try:
+            m = MetricsServer(_Fleet(), addr)
+        except OSError:  # no IPv6 loopback in this sandbox
+            assert addr.startswith("[")
+            continue
+        m.start()
+        try:
+            host = "[::1]" if addr.startswith("[") else "127.0.0.1"  # ":0" takes IPv4 too
+            assert urllib.request.urlopen(f"http://{host}:{m.port}/healthz", timeout=5).status == 200
+        finally:
+            m.stop()
