@@ -727,6 +727,76 @@ TEST(scheduler_many_queues_few_threads) {
   kube.stop();
 }
 
+// --poll-prewarm over the wire (TSan target): dedicated threads wake early, sign, check both
+// connections and spin to the due time; pooled threads run the warm-up as an event of its own
+// before each poll. Decisions and poll counts are those without it; a period under 2x the
+// warm-up takes the at-due-time branch.
+TEST(prewarm_over_wire_dedicated_and_pooled) {
+  FakeSqsServer sqs;
+  sqs.require_signature("AKID", "SECRET", "us-east-1");
+  CHECK(sqs.start().ok());
+  FakeKubeServer kube;
+  kube.require_token("tok");
+  CHECK(kube.start().ok());
+  auto clock = std::make_shared<RealClock>();
+  auto log = quiet_logger();
+  Credentials cr;
+  cr.access_key_id = "AKID";
+  cr.secret_access_key = "SECRET";
+  auto creds = std::make_shared<StaticCredentialsProvider>(cr);
+  const int kQueues = 6, kIters = 12;
+  auto make = [&](const std::string& tag, int q) {
+    std::string url = sqs.url() + "/1/" + tag + std::to_string(q);
+    sqs.set_attribute_cycle(url, {attrs(150), attrs(0)});
+    kube.add_deployment("ns", tag + std::to_string(q), 1);
+    SqsHttpOptions so;
+    so.region = "us-east-1";
+    so.endpoint = sqs.url();
+    auto api = std::make_shared<HttpSqsApi>(so, creds, clock);
+    KubeOptions ko;
+    ko.server = kube.url();
+    ko.namespace_ = "ns";
+    ko.token = std::make_shared<StaticTokenProvider>("tok");
+    auto dep = std::make_shared<KubeRestDeployments>(ko);
+    auto scaler = std::make_shared<PodAutoScaler>(dep, tag + std::to_string(q), "ns", 8, 1, 1, 1, log, clock);
+    LoopConfig lc;
+    lc.poll_period = (q % 3 == 2) ? 300 * kMicrosecond : 2 * kMillisecond;  // the last: under 2x prewarm
+    lc.prewarm = 250 * kMicrosecond;
+    lc.scale_up_cool_down = 0;
+    lc.scale_down_cool_down = 0;
+    lc.prefetch = (q % 2) == 0;
+    return std::make_shared<Runner>(lc, std::make_shared<SqsClient>(api, url, default_attribute_names()), scaler,
+                                    clock, log);
+  };
+  Supervisor sup;
+  sup.set_stagger(true);
+  Scheduler sched(2, clock);
+  for (int q = 0; q < kQueues; ++q) {
+    sup.add(make("d", q));
+    sched.add(make("p", q));
+  }
+  sup.start(kIters);
+  sched.start(kIters);
+  CHECK(sup.wait(60 * kSecond));
+  CHECK(sched.wait(60 * kSecond));
+  sup.join();
+  sched.join();
+  for (int q = 0; q < kQueues; ++q) {
+    for (const auto& r : {sup.runner(q), sched.runner(q)}) {
+      auto st = r->stats();
+      CHECK_EQ(st.polls, uint64_t(kIters));
+      CHECK_EQ(st.scale_ups, uint64_t(kIters / 2));
+      CHECK_EQ(st.scale_downs, uint64_t(kIters / 2));
+      CHECK_EQ(st.depth_errors, uint64_t(0));
+    }
+    CHECK_EQ(kube.replicas("ns", "d" + std::to_string(q)), 1);
+    CHECK_EQ(kube.replicas("ns", "p" + std::to_string(q)), 1);
+  }
+  CHECK_EQ(sqs.signature_failures(), uint64_t(0));
+  sqs.stop();
+  kube.stop();
+}
+
 TEST(scheduler_stop) {
   auto clock = std::make_shared<RealClock>();
   auto log = quiet_logger();
