@@ -9,12 +9,17 @@
 
 namespace ksa {
 
-void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
-               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads) {
-  if (m <= 0 || n < 1) return;
+bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads,
+               int arith) {
+  if (m <= 0 || n < 1) return false;
   for (int k = 0; k < 3; ++k)
-    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return;  // sweep.py validates first
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return false;  // sweep.py validates first
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+  const bool ms = arith == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
+  std::vector<int32_t> t32(ms ? n : 0), d32(ms ? n : 0);
+  if (ms) ksa_sim::narrow_policy_trace(trace_t, trace_d, n, t32.data(), d32.data());
+  const ksa_sim::MsLatency lat_ms = ksa_sim::ms_latency(lat);
   auto work = [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
       ksa_sim::Params p;
@@ -27,7 +32,9 @@ void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
       p.down_pods = params[6 * m + i];
       p.max_pods = params[7 * m + i];
       p.min_pods = params[8 * m + i];
-      const ksa_sim::Result r = ksa_sim::simulate(p, lat, trace_t, trace_d, n, init_replicas, horizon_ns);
+      const ksa_sim::Result r =
+          ms ? ksa_sim::simulate_ms(p, lat_ms, t32.data(), d32.data(), n, init_replicas, horizon_ns)
+             : ksa_sim::simulate(p, lat, trace_t, trace_d, n, init_replicas, horizon_ns);
       out64[0 * m + i] = r.pod_ms;
       out64[1 * m + i] = r.backlog;
       out64[2 * m + i] = r.first_up_ns;
@@ -44,7 +51,7 @@ void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
   if (t > m) t = static_cast<int>(m);
   if (t == 1) {
     work(0, m);
-    return;
+    return ms;
   }
   // Interleaved chunks balance the (period-dependent) cost across threads.
   std::vector<std::thread> pool;
@@ -59,6 +66,7 @@ void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
       }
     });
   for (auto& th : pool) th.join();
+  return ms;
 }
 
 bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,

@@ -10,9 +10,11 @@
 namespace ksa {
 
 // Layouts as in ksa_sweep_gpu (csrc/hip/policy_sweep.hip): params [9][m], out64 [3][m],
-// out32 [7][m], latency {sqs, get, update} ns.
-void sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
-               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads);
+// out32 [7][m], latency {sqs, get, update} ns. arith: 0 runs ksa_sim::simulate_ms when
+// ms_path_ok holds, 1 forces simulate (nanosecond clock). Returns true if the ms clock ran.
+bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads,
+               int arith = 0);
 
 // Closed-loop sweep (csrc/sim/queue_sim.h), CPU path; layouts as ksa_queue_sweep_gpu
 // (csrc/hip/queue_sweep.hip): params [9][m], model {service_milli, startup_ns, slo_backlog,

@@ -7,12 +7,16 @@
 //   * parameters and results are structure-of-arrays ([field][config]), so the 64 lanes of a
 //     wave load and store each field as one contiguous 512-byte (int64) segment;
 //   * the trace (segment start times + depths) is staged once per workgroup into dynamically
-//     sized LDS when it fits (kLdsTraceMax segments = 32 KiB), so the per-poll depth lookups --
+//     sized LDS when it fits (kLdsTraceBytes = 32 KiB: 2048 int64 segments), so the per-poll depth lookups --
 //     every lane walks its own forward-only cursor -- hit LDS; longer traces are read from
 //     global memory (lanes advance through it nearly in lockstep, so L1/L2 serve them) and then
 //     no LDS is allocated at all, leaving occupancy to the VGPR budget;
 //   * no 64-bit integer division per poll: the backlog metric divides once per replica run, and
 //     the poll-to-poll interval in ms is picked from six precomputed floors (policy_sim.h);
+//   * sweeps whose periods and latencies are whole milliseconds (ksa_sim::ms_path_ok: the grids
+//     and latency models one writes by hand) run ksa_sim::simulate_ms, on 32-bit millisecond
+//     clocks with a 32-bit trace (8 B per segment, so 4096 segments fit the same 32 KiB of LDS);
+//     the same results, without the per-poll 64-bit compares, adds and products;
 //   * the host orders configurations with the poll period outermost, so neighbouring lanes share
 //     trip counts and a wave's lanes retire together (less divergence at the loop exit);
 //   * grid-stride loop over configurations; the grid is one resident wave of workgroups
@@ -28,6 +32,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../sim/policy_sim.h"
 #include "device_arena.h"
@@ -35,7 +40,7 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kLdsTraceMax = 2048;  // segments staged in LDS (2 x 8 B x 2048 = 32 KiB -> 5 WG/CU)
+constexpr int kLdsTraceBytes = 32 * 1024;  // trace staged in LDS up to this size (-> 5 WG/CU)
 
 thread_local std::string g_sweep_error;
 
@@ -43,30 +48,21 @@ enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPo
 enum : int { kPodMs = 0, kBacklog, kFirstUp, kNumOut64 };
 enum : int { kUps = 0, kDowns, kNoopUps, kNoopDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
 
+#ifndef KSA_SWEEP_FLAT
+#define KSA_SWEEP_FLAT 0
+#endif
 #ifndef KSA_SWEEP_WAVES_PER_EU
 #define KSA_SWEEP_WAVES_PER_EU 6
 #endif
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEEP_WAVES_PER_EU))) void sweep_kernel(const int64_t* __restrict__ params, int64_t m,
-                                                       ksa_sim::Latency lat, const int64_t* __restrict__ g_t,
-                                                       const int64_t* __restrict__ g_d, int32_t n, int32_t init,
-                                                       int64_t horizon, int64_t* __restrict__ out64,
-                                                       int32_t* __restrict__ out32) {
-  // Dynamic LDS: 16 B per segment when the trace is staged, none otherwise -- a static
-  // allocation would cap occupancy even for traces that are read from global memory.
-  extern __shared__ int64_t s_lds[];
-  int64_t* s_t = s_lds;
-  int64_t* s_d = s_lds + (n <= kLdsTraceMax ? n : 0);
-  const bool in_lds = n <= kLdsTraceMax;
-  if (in_lds) {
-    for (int i = threadIdx.x; i < n; i += kBlock) {
-      s_t[i] = g_t[i];
-      s_d[i] = g_d[i];
-    }
-    __syncthreads();
-  }
-  const int64_t* t = in_lds ? s_t : g_t;
-  const int64_t* d = in_lds ? s_d : g_d;
+// The grid-stride loop over configurations. Called with the LDS copy or the global trace, in
+// separate branches, so each inlined copy addresses one memory (ds_read / global_load) instead of
+// flat loads that wait on both counters.
+template <bool kMs, class T>
+__device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, int64_t m, const ksa_sim::Latency& lat,
+                                            const T* __restrict__ t, const T* __restrict__ d, int32_t n, int32_t init,
+                                            int64_t horizon, int64_t* __restrict__ out64, int32_t* __restrict__ out32) {
+  const ksa_sim::MsLatency lat_ms = ksa_sim::ms_latency(lat);
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += stride) {
     ksa_sim::Params p;
@@ -79,7 +75,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEE
     p.down_pods = params[kDownPods * m + i];
     p.max_pods = params[kMaxPods * m + i];
     p.min_pods = params[kMinPods * m + i];
-    const ksa_sim::Result r = ksa_sim::simulate(p, lat, t, d, n, init, horizon);
+    ksa_sim::Result r;
+    if constexpr (kMs)
+      r = ksa_sim::simulate_ms(p, lat_ms, t, d, n, init, horizon);
+    else
+      r = ksa_sim::simulate(p, lat, t, d, n, init, horizon);
     out64[kPodMs * m + i] = r.pod_ms;
     out64[kBacklog * m + i] = r.backlog;
     out64[kFirstUp * m + i] = r.first_up_ns;
@@ -93,10 +93,71 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEE
   }
 }
 
+// kMs: ksa_sim::simulate_ms over a 32-bit trace (T = int32_t; the host checked ms_path_ok), else
+// ksa_sim::simulate over the int64 trace.
+template <bool kMs, class T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEEP_WAVES_PER_EU))) void sweep_kernel(
+    const int64_t* __restrict__ params, int64_t m, ksa_sim::Latency lat, const T* __restrict__ g_t,
+    const T* __restrict__ g_d, int32_t n, int32_t init, int64_t horizon, int64_t* __restrict__ out64,
+    int32_t* __restrict__ out32) {
+  // Dynamic LDS: 2 x sizeof(T) per segment when the trace is staged, none otherwise -- a static
+  // allocation would cap occupancy even for traces that are read from global memory.
+  constexpr int kMaxSeg = kLdsTraceBytes / (2 * static_cast<int>(sizeof(T)));
+  extern __shared__ int64_t s_lds[];
+#if KSA_SWEEP_FLAT
+  const bool in_lds = n <= kMaxSeg;
+  T* s_t = reinterpret_cast<T*>(s_lds);
+  T* s_d = s_t + (in_lds ? n : 0);
+  if (in_lds) {
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+      s_t[i] = g_t[i];
+      s_d[i] = g_d[i];
+    }
+    __syncthreads();
+  }
+  sweep_lanes<kMs>(params, m, lat, in_lds ? static_cast<const T*>(s_t) : g_t, in_lds ? static_cast<const T*>(s_d) : g_d, n,
+                   init, horizon, out64, out32);
+#else
+  if (n <= kMaxSeg) {
+    T* s_t = reinterpret_cast<T*>(s_lds);
+    T* s_d = s_t + n;
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+      s_t[i] = g_t[i];
+      s_d[i] = g_d[i];
+    }
+    __syncthreads();
+    sweep_lanes<kMs>(params, m, lat, static_cast<const T*>(s_t), static_cast<const T*>(s_d), n, init, horizon, out64,
+                     out32);
+  } else {
+    sweep_lanes<kMs>(params, m, lat, g_t, g_d, n, init, horizon, out64, out32);
+  }
+#endif
+}
+
 bool ok(hipError_t e, const char* what) {
   if (e == hipSuccess) return true;
   g_sweep_error = std::string(what) + ": " + hipGetErrorString(e);
   return false;
+}
+
+// Launches one path's kernel on the arena's stream. The grid is one resident wave of workgroups
+// (KSA_SWEEP_GRID: "tiles" = one workgroup per 256 configurations, or N x resident).
+template <bool kMs, class T>
+bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const ksa_sim::Latency& lat, const T* d_t,
+            const T* d_d, int32_t n, int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
+  const int64_t want = (m + kBlock - 1) / kBlock;
+  const size_t trace_bytes = 2 * static_cast<size_t>(n) * sizeof(T);
+  const size_t lds = trace_bytes <= static_cast<size_t>(kLdsTraceBytes) ? trace_bytes : 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<kMs, T>, kBlock, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  int64_t cap = static_cast<int64_t>(ar.cus) * per_cu;
+  if (const char* g = std::getenv("KSA_SWEEP_GRID")) cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
+  const int grid = static_cast<int>(want < cap ? want : cap);
+  hipLaunchKernelGGL((sweep_kernel<kMs, T>), dim3(grid), dim3(kBlock), lds, ar.stream, d_p, m, lat, d_t, d_d, n, init,
+                     horizon_ns, d_o64, d_o32);
+  return ok(hipGetLastError(), "sweep_kernel launch");
 }
 
 }  // namespace
@@ -107,10 +168,12 @@ const char* ksa_sweep_last_error() { return g_sweep_error.c_str(); }
 
 // params: [9][m] int64 (poll, up_cool, down_cool, up_msgs, down_msgs, up_pods, down_pods, max, min)
 // out64:  [3][m] int64 (pod_ms, backlog, first_up_ns); out32: [7][m] int32 (ups, downs, noop_ups,
-// noop_downs, final, max_replicas, polls). latency: {sqs, get, update} ns. Returns 0 on success.
+// noop_downs, final, max_replicas, polls). latency: {sqs, get, update} ns. arith: 0 runs the
+// millisecond clock when ksa_sim::ms_path_ok holds, 1 forces the nanosecond one; *ms_used reports
+// the choice. Returns 0 on success.
 int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas,
                   int64_t horizon_ns, const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64,
-                  int32_t* out32, double* kernel_ms) {
+                  int32_t* out32, double* kernel_ms, int32_t arith, int32_t* ms_used) {
   if (n < 1 || trace_t[0] != 0) {
     g_sweep_error = "trace must have at least one segment starting at t=0";
     return -1;
@@ -122,46 +185,55 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
     }
   }
   if (m <= 0) return 0;
+  const bool ms = arith == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
+  if (ms_used) *ms_used = ms ? 1 : 0;
+  // the trace in the chosen path's element type
+  std::vector<int32_t> t32, d32;
+  const size_t elem = ms ? sizeof(int32_t) : sizeof(int64_t);
+  const void* h_t = trace_t;
+  const void* h_d = trace_d;
+  if (ms) {
+    t32.resize(n);
+    d32.resize(n);
+    ksa_sim::narrow_policy_trace(trace_t, trace_d, n, t32.data(), d32.data());
+    h_t = t32.data();
+    h_d = d32.data();
+  }
   ksa_gpu::DeviceArena* ar = ksa_gpu::device_arena(dev, &g_sweep_error);
   if (!ar) return -1;
   std::lock_guard<std::mutex> lock(ar->mu);
   if (!ok(hipSetDevice(dev), "hipSetDevice")) return -1;
   void *d_t = nullptr, *d_d = nullptr, *d_p = nullptr, *d_o64 = nullptr, *d_o32 = nullptr;
-  if (!ok(ar->get(0, n * sizeof(int64_t), &d_t), "hipMalloc") || !ok(ar->get(1, n * sizeof(int64_t), &d_d), "hipMalloc") ||
+  if (!ok(ar->get(0, n * elem, &d_t), "hipMalloc") || !ok(ar->get(1, n * elem, &d_d), "hipMalloc") ||
       !ok(ar->get(2, kNumParams * m * sizeof(int64_t), &d_p), "hipMalloc") ||
       !ok(ar->get(3, kNumOut64 * m * sizeof(int64_t), &d_o64), "hipMalloc") ||
       !ok(ar->get(4, kNumOut32 * m * sizeof(int32_t), &d_o32), "hipMalloc"))
     return -1;
   hipStream_t st = ar->stream;
-  const ksa_gpu::StreamDrain drain{st};
-  if (!ok(hipMemcpyAsync(d_t, trace_t, n * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
-      !ok(hipMemcpyAsync(d_d, trace_d, n * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
+  const ksa_gpu::StreamDrain drain{st};  // also on the error paths: t32 / d32 die with this frame
+  if (!ok(hipMemcpyAsync(d_t, h_t, n * elem, hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(d_d, h_d, n * elem, hipMemcpyHostToDevice, st), "hipMemcpyAsync") ||
       !ok(hipMemcpyAsync(d_p, params, kNumParams * m * sizeof(int64_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync"))
     return -1;
-  const int64_t want = (m + kBlock - 1) / kBlock;
-  const size_t lds = n <= kLdsTraceMax ? 2 * static_cast<size_t>(n) * sizeof(int64_t) : 0;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel, kBlock, lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  int64_t cap = static_cast<int64_t>(ar->cus) * per_cu;  // one wave of resident workgroups
-  if (const char* g = std::getenv("KSA_SWEEP_GRID")) {  // tuning knob: "tiles" or N x resident
-    cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
-  }
-  const int grid = static_cast<int>(want < cap ? want : cap);
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
+  const int64_t* p = static_cast<const int64_t*>(d_p);
+  int64_t* o64 = static_cast<int64_t*>(d_o64);
+  int32_t* o32 = static_cast<int32_t*>(d_o32);
   if (!ok(hipEventRecord(ar->e0, st), "hipEventRecord")) return -1;
-  hipLaunchKernelGGL(sweep_kernel, dim3(grid), dim3(kBlock), lds, st, static_cast<const int64_t*>(d_p), m, lat,
-                     static_cast<const int64_t*>(d_t), static_cast<const int64_t*>(d_d), n, init_replicas, horizon_ns,
-                     static_cast<int64_t*>(d_o64), static_cast<int32_t*>(d_o32));
-  if (!ok(hipGetLastError(), "sweep_kernel launch")) return -1;
+  const bool launched =
+      ms ? launch<true>(*ar, p, m, lat, static_cast<const int32_t*>(d_t), static_cast<const int32_t*>(d_d), n,
+                        init_replicas, horizon_ns, o64, o32)
+         : launch<false>(*ar, p, m, lat, static_cast<const int64_t*>(d_t), static_cast<const int64_t*>(d_d), n,
+                         init_replicas, horizon_ns, o64, o32);
+  if (!launched) return -1;
   if (!ok(hipEventRecord(ar->e1, st), "hipEventRecord")) return -1;
-  if (!ok(hipMemcpyAsync(out64, d_o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync") ||
-      !ok(hipMemcpyAsync(out32, d_o32, kNumOut32 * m * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync"))
+  if (!ok(hipMemcpyAsync(out64, o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync") ||
+      !ok(hipMemcpyAsync(out32, o32, kNumOut32 * m * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync"))
     return -1;
   if (!ok(hipStreamSynchronize(st), "hipStreamSynchronize")) return -1;
-  float ms = 0;
-  if (!ok(hipEventElapsedTime(&ms, ar->e0, ar->e1), "hipEventElapsedTime")) return -1;
-  if (kernel_ms) *kernel_ms = ms;
+  float ms_elapsed = 0;
+  if (!ok(hipEventElapsedTime(&ms_elapsed, ar->e0, ar->e1), "hipEventElapsedTime")) return -1;
+  if (kernel_ms) *kernel_ms = ms_elapsed;
   return 0;
 }
 

@@ -280,4 +280,231 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
   return res;
 }
 
+// ---- Millisecond clock (the usual sweep: periods and latencies in whole milliseconds) --------
+//
+// When every poll period that can fire and every call latency is a whole number of
+// milliseconds, every time the simulation produces is one too (sums of periods and latencies),
+// so it can run on 32-bit millisecond clocks with the same decisions and metrics:
+//   * a cool-down c enters as ceil(c / 1 ms): for whole-ms `last` and `now`,
+//     last + c > now  <=>  c > (now - last)  <=>  ceil(c / 1 ms) > (now - last) / 1 ms;
+//   * a trace boundary T as ceil(T / 1 ms): a whole-ms poll time t reaches it iff t >= that;
+//   * the horizon H as floor(H / 1 ms): a whole-ms poll time t <= H iff t <= that, and the last
+//     interval's floor((H - t) / 1 ms) is floor(H / 1 ms) - t;
+//   * every time a lane holds stays within B = H + sqs + 2 (get + update) (ms); cool-downs and
+//     periods beyond +-(B + 1) compare and end the loop as the clamped values do, and the host
+//     (ms_path_ok) requires 2B + 1 < 2^31, so no 32-bit sum can wrap;
+//   * depths are in [0, 2^31 - 2] (checked by the host), so thresholds clamp to 32 bits.
+// On gfx950 this drops the per-poll 64-bit compares, adds and 64 x 64 products (each several
+// VALU instructions) and halves the trace's LDS footprint. The CPU path runs the same function
+// for the same sweeps, and tests pin it equal to simulate() on randomised inputs.
+constexpr int32_t kMsNever = INT32_MAX;
+
+struct MsRules {
+  int32_t up_msgs, down_msgs, up_cool, down_cool, period;
+  int32_t max32, min32, up32, down32;
+};
+
+// Latencies in milliseconds (the field names are KSA_DECIDE's).
+struct MsLatency {
+  int32_t sqs_ns, get_ns, update_ns;
+};
+
+KSA_HD int64_t ceil_div_1e6(int64_t v) {
+  const int64_t q = v / 1000000;  // truncates toward zero: already the ceiling for v < 0
+  return q * 1000000 < v ? q + 1 : q;
+}
+
+KSA_HD int32_t clamp_i32(int64_t v, int64_t lo, int64_t hi) {
+  return static_cast<int32_t>(v < lo ? lo : (v > hi ? hi : v));
+}
+
+KSA_HD MsLatency ms_latency(const Latency& lat) {
+  return MsLatency{static_cast<int32_t>(lat.sqs_ns / 1000000), static_cast<int32_t>(lat.get_ns / 1000000),
+                   static_cast<int32_t>(lat.update_ns / 1000000)};
+}
+
+// B: the bound on every time value of a lane (see above).
+KSA_HD int32_t ms_bound(int32_t horizon_ms, const MsLatency& lat) {
+  return horizon_ms + lat.sqs_ns + 2 * (lat.get_ns + lat.update_ns);
+}
+
+KSA_HD MsRules make_ms_rules(const Params& p, int64_t horizon_ns, int32_t bound) {
+  MsRules k;
+  const int64_t b1 = static_cast<int64_t>(bound) + 1;
+  k.up_msgs = clamp_i32(p.up_msgs, 0, INT32_MAX);     // d >= up_msgs, d in [0, 2^31 - 2]
+  k.down_msgs = clamp_i32(p.down_msgs, -1, INT32_MAX);  // d <= down_msgs
+  k.up_cool = clamp_i32(ceil_div_1e6(p.up_cool_ns), -b1, b1);
+  k.down_cool = clamp_i32(ceil_div_1e6(p.down_cool_ns), -b1, b1);
+  // a period past the horizon never fires (its first poll is past it); others are whole ms
+  k.period = p.poll_ns <= 0 ? 0 : (p.poll_ns > horizon_ns ? static_cast<int32_t>(b1) : clamp_i32(p.poll_ns / 1000000, 0, b1));
+  k.max32 = go_i32(p.max_pods);
+  k.min32 = go_i32(p.min_pods);
+  k.up32 = go_i32(p.up_pods);
+  k.down32 = go_i32(p.down_pods);
+  return k;
+}
+
+struct MsCursor {
+  int32_t c;
+  int32_t cur_d, next_t, next_d;
+};
+
+KSA_HD MsCursor ms_cursor_init(const int32_t* t_ms, const int32_t* depth, int32_t n) {
+  MsCursor k;
+  k.c = 0;
+  k.cur_d = depth[0];
+  k.next_t = n > 1 ? t_ms[1] : kMsNever;
+  k.next_d = n > 1 ? depth[1] : 0;
+  return k;
+}
+
+KSA_HD int32_t ms_depth_at(const int32_t* t_ms, const int32_t* depth, int32_t n, MsCursor* k, int32_t t) {
+  while (t >= k->next_t) {
+    k->c++;
+    k->cur_d = k->next_d;
+    if (k->c + 1 < n) {
+      k->next_t = t_ms[k->c + 1];
+      k->next_d = depth[k->c + 1];
+    } else {
+      k->next_t = kMsNever;
+    }
+  }
+  return k->cur_d;
+}
+KSA_HD void accumulate_ms32(Result* r, Accum* a, int32_t dt_ms, int32_t replicas, int32_t depth) {
+  r->pod_ms += static_cast<int64_t>(replicas) * dt_ms;
+  if (replicas != a->run_r) {
+    flush(r, a);
+    a->run_r = replicas;
+  }
+  a->run += static_cast<int64_t>(depth) * dt_ms;
+}
+
+#ifndef KSA_MS_SELECT
+#define KSA_MS_SELECT 1
+#endif
+
+// KSA_DECIDE written with selects instead of branches: every lane evaluates both gates and both
+// actions and keeps what its own branch would have produced. In a 64-lane wave whose lanes take
+// different branches (different thresholds, cool-downs, bounds) the branchy form executes every
+// taken branch anyway, plus the exec-mask bookkeeping of each. Same semantics, term by term: the
+// scale-down check is skipped only when the scale-up gate passed but its cool-down had not
+// elapsed (main.go:52-53 `continue`); `now` advances by a GET per call and an update per write,
+// in order, so the scale-down cool-down compares against the time after the scale-up's calls.
+// K / L: rules and latencies in T's unit (MsRules + MsLatency with int32 ms, or Rules + Latency
+// with int64 ns); D: the depth's type.
+struct Decision {
+  bool up_write, up_noop, down_write, down_noop;
+};
+
+template <class K, class L, class T, class D>
+KSA_HD Decision decide_select(const K& k, const L& lat, D d, T* now, T* last_up, T* last_down, int32_t* replicas) {
+  T t = *now;
+  int32_t r = *replicas;
+  Decision o;
+  const bool up_hit = d >= k.up_msgs;                  // main.go:51
+  const bool up_blocked = *last_up + k.up_cool > t;    // main.go:52 (strict After)
+  const bool up_call = up_hit && !up_blocked;
+  o.up_noop = up_call && r >= k.max32;                 // scale.go:62
+  o.up_write = up_call && !o.up_noop;
+  int32_t up_next = add_i32(r, k.up32);
+  up_next = up_next > k.max32 ? k.max32 : up_next;
+  t += (up_call ? lat.get_ns : T(0)) + (o.up_write ? lat.update_ns : T(0));
+  r = o.up_write ? up_next : r;
+  *last_up = up_call ? t : *last_up;                   // main.go:62 (also after a no-op)
+  const bool down_hit = !(up_hit && up_blocked) && d <= k.down_msgs;  // main.go:65
+  const bool down_call = down_hit && !(*last_down + k.down_cool > t);
+  o.down_noop = down_call && r <= k.min32;             // scale.go:89
+  o.down_write = down_call && !o.down_noop;
+  int32_t down_next = sub_i32(r, k.down32);
+  down_next = down_next < k.min32 ? k.min32 : down_next;
+  t += (down_call ? lat.get_ns : T(0)) + (o.down_write ? lat.update_ns : T(0));
+  r = o.down_write ? down_next : r;
+  *last_down = down_call ? t : *last_down;             // main.go:76
+  *now = t;
+  *replicas = r;
+  return o;
+}
+
+// simulate() on the millisecond clock: t_ms / depth as narrow_policy_trace makes them.
+KSA_HD Result simulate_ms(const Params& p, const MsLatency& lat, const int32_t* t_ms, const int32_t* depth, int32_t n,
+                          int32_t init_replicas, int64_t horizon_ns) {
+  Result res;
+  Accum acc;
+  acc.run_r = init_replicas;
+  MsCursor cursor = ms_cursor_init(t_ms, depth, n);
+  const int32_t horizon_ms = static_cast<int32_t>(horizon_ns / 1000000);
+  const MsRules k = make_ms_rules(p, horizon_ns, ms_bound(horizon_ms, lat));
+  int32_t now = 0;
+  int32_t last_up = 0, last_down = 0;  // main.go:37-38
+  int32_t replicas = init_replicas;
+  int32_t prev_t = 0;
+  int32_t prev_d = ms_depth_at(t_ms, depth, n, &cursor, 0);
+  int32_t first_up_ms = -1;
+  res.max_replicas = replicas;
+  const bool advances = k.period > 0 || lat.sqs_ns > 0;
+  while (advances && res.polls < kMaxPolls) {
+    const int32_t t_poll = now + k.period;  // main.go:41 sleep, then poll
+    if (t_poll > horizon_ms) break;
+    now = t_poll;
+    accumulate_ms32(&res, &acc, t_poll - prev_t, replicas, prev_d);  // replicas as set by the previous poll
+    prev_t = now;
+    res.polls++;
+    const int32_t d = ms_depth_at(t_ms, depth, n, &cursor, now);  // sampled at call start
+    now += lat.sqs_ns;
+#if KSA_MS_SELECT
+    const Decision o = decide_select(k, lat, d, &now, &last_up, &last_down, &replicas);
+    res.ups += o.up_write;
+    res.noop_ups += o.up_noop;
+    res.downs += o.down_write;
+    res.noop_downs += o.down_noop;
+    first_up_ms = (o.up_write && first_up_ms < 0) ? t_poll : first_up_ms;
+#else
+    int32_t gets = 0, writes = 0;
+    KSA_DECIDE(k, lat, d, now, last_up, last_down, replicas, gets, writes,
+               { res.ups++; if (first_up_ms < 0) first_up_ms = t_poll; }, res.noop_ups++, res.downs++,
+               res.noop_downs++);
+    (void)gets;
+    (void)writes;
+#endif
+    if (replicas > res.max_replicas) res.max_replicas = replicas;
+    prev_d = d;
+  }
+  if (horizon_ms > prev_t) accumulate_ms32(&res, &acc, horizon_ms - prev_t, replicas, prev_d);
+  flush(&res, &acc);
+  res.first_up_ns = first_up_ms < 0 ? -1 : static_cast<int64_t>(first_up_ms) * 1000000;
+  res.final_replicas = replicas;
+  return res;
+}
+
+// Host check for simulate_ms (see above): whole-ms latencies, whole-ms periods wherever a
+// period can fire (0 < poll <= horizon), depths in [0, 2^31 - 2], and 2B + 1 < 2^31.
+inline bool ms_path_ok(const int64_t* t_ns, const int64_t* depth, int32_t n, int64_t horizon_ns, const int64_t* latency,
+                       const int64_t* params, int64_t configs) {
+  if (n < 1 || t_ns[0] != 0 || horizon_ns < 0) return false;
+  int64_t lat_ms = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (latency[k] < 0 || latency[k] > kMaxLatencyNs || latency[k] % 1000000 != 0) return false;
+    lat_ms += (k == 0 ? 1 : 2) * (latency[k] / 1000000);
+  }
+  const int64_t bound = horizon_ns / 1000000 + lat_ms;
+  if (2 * bound + 1 >= (int64_t(1) << 31)) return false;
+  for (int32_t i = 0; i < n; ++i)
+    if (depth[i] < 0 || depth[i] > INT32_MAX - 1) return false;
+  for (int64_t i = 0; i < configs; ++i) {
+    const int64_t poll = params[i];  // params [9][m]: poll first
+    if (poll > 0 && poll <= horizon_ns && poll % 1000000 != 0) return false;
+  }
+  return true;
+}
+
+// The trace as simulate_ms reads it: boundaries ceil(t / 1 ms) (kMsNever past 2^31 ms), depths.
+inline void narrow_policy_trace(const int64_t* t_ns, const int64_t* depth, int32_t n, int32_t* t32, int32_t* d32) {
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t t = ceil_div_1e6(t_ns[i]);
+    t32[i] = t < kMsNever ? static_cast<int32_t>(t) : kMsNever;
+    d32[i] = static_cast<int32_t>(depth[i]);
+  }
+}
+
 }  // namespace ksa_sim

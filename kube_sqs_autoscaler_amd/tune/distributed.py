@@ -128,12 +128,13 @@ def run_open_loop(g: Group, trace: sweep.Trace, params: np.ndarray, init_replica
     part = params[:, lo:hi]
     if hi > lo:
         res = sweep.run(trace, part, init_replicas, horizon_ns, latency_ns, g.device, gpu_index=g.local_rank)
-        out, kernel_ms = res.out, res.kernel_ms
+        out, kernel_ms, ns_clock = res.out, res.kernel_ms, not res.ms_clock
     else:  # more ranks than configurations
         out = {k: np.zeros(0, dtype=np.int64 if k in sweep.OUT64 else np.int32) for k in sweep.OUT64 + sweep.OUT32}
-        kernel_ms = 0.0
+        kernel_ms, ns_clock = 0.0, False
     full = g.all_gather_fields(out, counts)
-    return sweep.SweepResult(params, full, g.device, g.max(kernel_ms))
+    # ms_clock: every shard ran the millisecond clock
+    return sweep.SweepResult(params, full, g.device, g.max(kernel_ms), g.max(float(ns_clock)) == 0.0)
 
 
 def run_closed_loop(g: Group, trace: closedloop.ArrivalTrace, params: np.ndarray, model: closedloop.QueueModel,

@@ -155,14 +155,19 @@ def test_sweep_kernel_equals_cpu_and_oracle():
                       down_cool_ns=list(range(0, 600 * S, 60 * S)), up_msgs=[50, 100, 200, 400, 800],
                       down_msgs=[5, 50], up_pods=[1, 2], max_pods=[8, 16], min_pods=[1])
     assert grid.shape[1] == 2 * 15 * 10 * 5 * 2 * 2 * 2
-    for n in (1000, 6000):  # <= 2048 segments are staged in LDS, more are read from global memory
+    # traces staged in LDS up to 32 KiB: <= 2048 int64 segments on the nanosecond clock, <= 4096
+    # int32 ones on the millisecond clock; longer ones are read from global memory
+    for n in (1000, 3000, 6000):
         tr = _random_walk_trace(n, n)
         horizon = int(tr.t_ns[-1]) + 5 * S
         g = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="gpu")
-        c = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="cpu")
+        gn = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="gpu", clock="ns")
+        c = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="cpu", clock="ns")
         assert g.device == "gpu" and g.kernel_ms > 0
+        assert g.ms_clock and not gn.ms_clock and not c.ms_clock
         for k in g.out:
             assert np.array_equal(g.out[k], c.out[k]), k
+            assert np.array_equal(gn.out[k], c.out[k]), k
         assert int(g.out["ups"].sum()) > 0 and int(g.out["downs"].sum()) > 0
         for i in range(0, len(g), len(g) // 7):
             o = sweep.oracle_row(tr, g.config(i), 2, horizon, (2_000_000, 1_000_000, 1_000_000))
@@ -271,10 +276,12 @@ def test_sweep_kernel_random_lanes_equal_oracle():
         tr = random_walk_trace(n, seed)
         horizon = min(int(tr.t_ns[-1]) + 10 * S, 1800 * S)
         g = sweep.run(tr, params, 2, horizon, lat, device="gpu")
-        c = sweep.run(tr, params, 2, horizon, lat, device="cpu")
-        assert g.device == "gpu"
+        gn = sweep.run(tr, params, 2, horizon, lat, device="gpu", clock="ns")
+        c = sweep.run(tr, params, 2, horizon, lat, device="cpu", clock="ns")
+        assert g.device == "gpu" and g.ms_clock and not gn.ms_clock
         for k in g.out:
             assert np.array_equal(g.out[k], c.out[k]), k
+            assert np.array_equal(gn.out[k], c.out[k]), k
         for i in lanes_to_check(params.shape[1], 256, seed):
             o = sweep.oracle_row(tr, g.config(i), 2, horizon, lat)
             assert {k: g.row(i)[k] for k in o} == o, (i, g.config(i))

@@ -128,3 +128,82 @@ def test_extreme_cool_downs_and_periods_do_not_overflow(nat):
         got = {k: int(r.out[k][j]) for k in want}
         assert got == want, (r.config(j), got, want)
     assert np.all(r.out["polls"][grid[0] == big] == 0)
+
+
+# ---- millisecond clock (policy_sim.h simulate_ms) against the nanosecond one ----------------
+
+
+def _both_clocks(tr, grid, init, horizon, lat):
+    a = sweep.run(tr, grid, init, horizon, lat, device="cpu", clock="auto")
+    b = sweep.run(tr, grid, init, horizon, lat, device="cpu", clock="ns")
+    assert not b.ms_clock
+    for k in a.out:
+        assert np.array_equal(a.out[k], b.out[k]), k
+    return a
+
+
+@settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(
+    # trace boundaries anywhere (sub-ms too): the ms clock rounds them up
+    segs=st.lists(st.tuples(st.integers(1, 400 * 10**9), st.integers(0, 800)), min_size=0, max_size=12),
+    d0=st.integers(0, 800),
+    poll_ms=st.integers(1, 9000),
+    # cool-downs at any ns, negative ones too, and past every bound
+    cools=st.lists(st.one_of(st.integers(-(10**12), 10**12), st.sampled_from([0, 1, -1, 999_999, 1_000_001,
+                                                                              2**62, -(2**62)])), min_size=2, max_size=2),
+    up_msgs=st.one_of(st.integers(-5, 900), st.sampled_from([2**40, -(2**40)])),
+    down_msgs=st.one_of(st.integers(-5, 900), st.sampled_from([2**40, -(2**40)])),
+    up_pods=st.integers(-3, 6), down_pods=st.integers(-3, 6), max_pods=st.integers(-2, 14), min_pods=st.integers(-2, 14),
+    init=st.integers(0, 14), lat_ms=st.tuples(st.integers(0, 40), st.integers(0, 40), st.integers(0, 40)),
+    horizon_ns=st.integers(1, 900 * 10**9),
+)
+def test_ms_clock_equals_ns_clock_property(segs, d0, poll_ms, cools, up_msgs, down_msgs, up_pods, down_pods, max_pods,
+                                           min_pods, init, lat_ms, horizon_ns):
+    tr = sweep.Trace.from_segments([(0, d0)] + sorted(segs))
+    grid = sweep.grid(poll_ns=[poll_ms * 10**6, 2**63 - 1], up_cool_ns=[cools[0]], down_cool_ns=[cools[1]],
+                      up_msgs=[up_msgs], down_msgs=[down_msgs], up_pods=[up_pods], down_pods=[down_pods],
+                      max_pods=[max_pods], min_pods=[min_pods])
+    lat = tuple(x * 10**6 for x in lat_ms)
+    if lat[0] == 0 and poll_ms == 0:
+        return
+    r = _both_clocks(tr, grid, init, horizon_ns, lat)
+    assert r.ms_clock
+
+
+def test_ms_clock_is_chosen_only_when_exact():
+    tr = step_trace()
+    ms_lat = (2 * 10**6, 10**6, 10**6)
+    g = sweep.grid(poll_ns=[S, 5 * S], up_cool_ns=[0, 10 * S + 1])
+    assert _both_clocks(tr, g, 1, 900 * S, ms_lat).ms_clock
+    # a latency or a period that fires with a sub-ms part: the nanosecond clock, same results
+    assert not _both_clocks(tr, g, 1, 900 * S, (2_500_000, 10**6, 10**6)).ms_clock
+    assert not _both_clocks(tr, sweep.grid(poll_ns=[S + 1]), 1, 900 * S, ms_lat).ms_clock
+    # ... unless that period never fires (longer than the horizon)
+    assert _both_clocks(tr, sweep.grid(poll_ns=[S, 901 * S + 1]), 1, 900 * S, ms_lat).ms_clock
+    # depths outside [0, 2^31 - 2], or a horizon past 2^30 ms: the nanosecond clock
+    neg = sweep.Trace.from_segments([(0, 5), (60 * S, -1)])
+    assert not _both_clocks(neg, g, 1, 900 * S, ms_lat).ms_clock
+    big = sweep.Trace.from_segments([(0, 5), (60 * S, 2**31 - 1)])
+    assert not _both_clocks(big, g, 1, 900 * S, ms_lat).ms_clock
+    assert _both_clocks(sweep.Trace.from_segments([(0, 5), (60 * S, 2**31 - 2)]), g, 1, 900 * S, ms_lat).ms_clock
+    # the deepest queue over a long horizon: backlog runs far past 2^53 msg-ms, still exact
+    deep = sweep.Trace.from_segments([(0, 2**31 - 2), (3600 * S, 3), (7200 * S, 2**31 - 2)])
+    g2 = sweep.grid(poll_ns=[60 * S], up_cool_ns=[0], down_cool_ns=[0], up_msgs=[100], down_msgs=[10], max_pods=[3])
+    assert _both_clocks(deep, g2, 1, 10**8 * 10**6, ms_lat).ms_clock
+    long_h = 2**30 * 10**6
+    assert not sweep.run(tr, sweep.grid(poll_ns=[3600 * S]), 1, long_h, ms_lat, device="cpu").ms_clock
+    with pytest.raises(ValueError, match="clock"):
+        sweep.run(tr, g, 1, 900 * S, ms_lat, device="cpu", clock="fast")
+
+
+def test_ms_clock_boundaries_exactly_at_cool_down_expiry():
+    """Cool-downs that expire exactly on a poll, one ns before and one ns after (strict After,
+    main.go:52,66), and trace boundaries one ns either side of a poll: both clocks agree."""
+    polls = [k * S for k in range(1, 40)]
+    segs = [(0, 0)] + [(t + off, 500 if i % 2 == 0 else 0) for i, t in enumerate(polls[::3]) for off in (-1, 1)]
+    segs = sorted(set(segs))
+    tr = sweep.Trace(np.array([s[0] for s in segs]), np.array([s[1] for s in segs]))
+    g = sweep.grid(poll_ns=[S], up_cool_ns=[3 * S - 1, 3 * S, 3 * S + 1, 3 * S + 2 * 10**6],
+                   down_cool_ns=[2 * S - 1, 2 * S, 2 * S + 1], up_msgs=[100], down_msgs=[10])
+    for lat in ((0, 0, 0), (10**6, 10**6, 10**6), (0, 2 * 10**6, 0)):
+        assert _both_clocks(tr, g, 1, 60 * S, lat).ms_clock
