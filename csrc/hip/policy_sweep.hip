@@ -48,16 +48,14 @@ enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPo
 enum : int { kPodMs = 0, kBacklog, kFirstUp, kNumOut64 };
 enum : int { kUps = 0, kDowns, kNoopUps, kNoopDowns, kFinal, kMaxRep, kPolls, kNumOut32 };
 
-#ifndef KSA_SWEEP_FLAT
-#define KSA_SWEEP_FLAT 0
-#endif
 #ifndef KSA_SWEEP_WAVES_PER_EU
 #define KSA_SWEEP_WAVES_PER_EU 6
 #endif
 
-// The grid-stride loop over configurations. Called with the LDS copy or the global trace, in
-// separate branches, so each inlined copy addresses one memory (ds_read / global_load) instead of
-// flat loads that wait on both counters.
+// The grid-stride loop over configurations. The trace pointer is the LDS copy or the global
+// array, chosen per launch, so the loads are flat: specialising them into ds_read and
+// global_load copies of the loop (two inlined calls) measured slower on the global path (24.5 vs
+// 22.5 ms, profiles/r03u_sweep_ab.jsonl) and equal from LDS.
 template <bool kMs, class T>
 __device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, int64_t m, const ksa_sim::Latency& lat,
                                             const T* __restrict__ t, const T* __restrict__ d, int32_t n, int32_t init,
@@ -104,7 +102,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEE
   // allocation would cap occupancy even for traces that are read from global memory.
   constexpr int kMaxSeg = kLdsTraceBytes / (2 * static_cast<int>(sizeof(T)));
   extern __shared__ int64_t s_lds[];
-#if KSA_SWEEP_FLAT
   const bool in_lds = n <= kMaxSeg;
   T* s_t = reinterpret_cast<T*>(s_lds);
   T* s_d = s_t + (in_lds ? n : 0);
@@ -117,21 +114,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEE
   }
   sweep_lanes<kMs>(params, m, lat, in_lds ? static_cast<const T*>(s_t) : g_t, in_lds ? static_cast<const T*>(s_d) : g_d, n,
                    init, horizon, out64, out32);
-#else
-  if (n <= kMaxSeg) {
-    T* s_t = reinterpret_cast<T*>(s_lds);
-    T* s_d = s_t + n;
-    for (int i = threadIdx.x; i < n; i += kBlock) {
-      s_t[i] = g_t[i];
-      s_d[i] = g_d[i];
-    }
-    __syncthreads();
-    sweep_lanes<kMs>(params, m, lat, static_cast<const T*>(s_t), static_cast<const T*>(s_d), n, init, horizon, out64,
-                     out32);
-  } else {
-    sweep_lanes<kMs>(params, m, lat, g_t, g_d, n, init, horizon, out64, out32);
-  }
-#endif
 }
 
 bool ok(hipError_t e, const char* what) {

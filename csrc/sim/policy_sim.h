@@ -380,52 +380,6 @@ KSA_HD void accumulate_ms32(Result* r, Accum* a, int32_t dt_ms, int32_t replicas
   a->run += static_cast<int64_t>(depth) * dt_ms;
 }
 
-#ifndef KSA_MS_SELECT
-#define KSA_MS_SELECT 1
-#endif
-
-// KSA_DECIDE written with selects instead of branches: every lane evaluates both gates and both
-// actions and keeps what its own branch would have produced. In a 64-lane wave whose lanes take
-// different branches (different thresholds, cool-downs, bounds) the branchy form executes every
-// taken branch anyway, plus the exec-mask bookkeeping of each. Same semantics, term by term: the
-// scale-down check is skipped only when the scale-up gate passed but its cool-down had not
-// elapsed (main.go:52-53 `continue`); `now` advances by a GET per call and an update per write,
-// in order, so the scale-down cool-down compares against the time after the scale-up's calls.
-// K / L: rules and latencies in T's unit (MsRules + MsLatency with int32 ms, or Rules + Latency
-// with int64 ns); D: the depth's type.
-struct Decision {
-  bool up_write, up_noop, down_write, down_noop;
-};
-
-template <class K, class L, class T, class D>
-KSA_HD Decision decide_select(const K& k, const L& lat, D d, T* now, T* last_up, T* last_down, int32_t* replicas) {
-  T t = *now;
-  int32_t r = *replicas;
-  Decision o;
-  const bool up_hit = d >= k.up_msgs;                  // main.go:51
-  const bool up_blocked = *last_up + k.up_cool > t;    // main.go:52 (strict After)
-  const bool up_call = up_hit && !up_blocked;
-  o.up_noop = up_call && r >= k.max32;                 // scale.go:62
-  o.up_write = up_call && !o.up_noop;
-  int32_t up_next = add_i32(r, k.up32);
-  up_next = up_next > k.max32 ? k.max32 : up_next;
-  t += (up_call ? lat.get_ns : T(0)) + (o.up_write ? lat.update_ns : T(0));
-  r = o.up_write ? up_next : r;
-  *last_up = up_call ? t : *last_up;                   // main.go:62 (also after a no-op)
-  const bool down_hit = !(up_hit && up_blocked) && d <= k.down_msgs;  // main.go:65
-  const bool down_call = down_hit && !(*last_down + k.down_cool > t);
-  o.down_noop = down_call && r <= k.min32;             // scale.go:89
-  o.down_write = down_call && !o.down_noop;
-  int32_t down_next = sub_i32(r, k.down32);
-  down_next = down_next < k.min32 ? k.min32 : down_next;
-  t += (down_call ? lat.get_ns : T(0)) + (o.down_write ? lat.update_ns : T(0));
-  r = o.down_write ? down_next : r;
-  *last_down = down_call ? t : *last_down;             // main.go:76
-  *now = t;
-  *replicas = r;
-  return o;
-}
-
 // simulate() on the millisecond clock: t_ms / depth as narrow_policy_trace makes them.
 KSA_HD Result simulate_ms(const Params& p, const MsLatency& lat, const int32_t* t_ms, const int32_t* depth, int32_t n,
                           int32_t init_replicas, int64_t horizon_ns) {
@@ -452,21 +406,12 @@ KSA_HD Result simulate_ms(const Params& p, const MsLatency& lat, const int32_t* 
     res.polls++;
     const int32_t d = ms_depth_at(t_ms, depth, n, &cursor, now);  // sampled at call start
     now += lat.sqs_ns;
-#if KSA_MS_SELECT
-    const Decision o = decide_select(k, lat, d, &now, &last_up, &last_down, &replicas);
-    res.ups += o.up_write;
-    res.noop_ups += o.up_noop;
-    res.downs += o.down_write;
-    res.noop_downs += o.down_noop;
-    first_up_ms = (o.up_write && first_up_ms < 0) ? t_poll : first_up_ms;
-#else
     int32_t gets = 0, writes = 0;
     KSA_DECIDE(k, lat, d, now, last_up, last_down, replicas, gets, writes,
                { res.ups++; if (first_up_ms < 0) first_up_ms = t_poll; }, res.noop_ups++, res.downs++,
                res.noop_downs++);
     (void)gets;
     (void)writes;
-#endif
     if (replicas > res.max_replicas) res.max_replicas = replicas;
     prev_d = d;
   }

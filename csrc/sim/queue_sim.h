@@ -246,10 +246,6 @@ KSA_HD void advance(QueueState<A>* s, QueueResult* r, const QueueModel& m, const
   }
 }
 
-#ifndef KSA_QUEUE_SELECT
-#define KSA_QUEUE_SELECT 1
-#endif
-
 template <class A, class T>
 KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const QueueModel& m, const T* t_ms,
                                   const T* rate_milli, int32_t n, int32_t init_replicas, int64_t horizon_ns,
@@ -312,18 +308,7 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
     now += lat.sqs_ns;
     const int32_t before = replicas;
     int32_t gets = 0, writes = 0;
-#if KSA_QUEUE_SELECT
-    {
-      const Decision o = decide_select(k, lat, d, &now, &last_up, &last_down, &replicas);
-      res.ups += o.up_write;
-      res.downs += o.down_write;
-      // the calls made, for the poll-interval carry below
-      gets = (o.up_write || o.up_noop) + (o.down_write || o.down_noop);
-      writes = o.up_write + o.down_write;
-    }
-#else
     KSA_DECIDE(k, lat, d, now, last_up, last_down, replicas, gets, writes, res.ups++, (void)0, res.downs++, (void)0);
-#endif
     carry(sqs_ms + static_cast<Ms>(gets) * get_ms + static_cast<Ms>(writes) * upd_ms,
           sqs_sub + static_cast<uint32_t>(gets) * get_sub + static_cast<uint32_t>(writes) * upd_sub);
     const int32_t delta = sub_i32(replicas, before);
