@@ -918,7 +918,7 @@ PYBIND11_MODULE(_ksa_native, m) {
 
   m.def("queue_sweep_cpu",
         [](I64 t_ms, I64 rate_milli, int32_t init, int64_t horizon, I64 latency, I64 model, I64 params, int32_t seeds,
-           uint64_t seed0, int threads, bool saturating) {
+           uint64_t seed0, int threads, int arith) {
           if (t_ms.ndim() != 1 || rate_milli.ndim() != 1 || t_ms.shape(0) != rate_milli.shape(0) || t_ms.shape(0) < 1)
             throw py::value_error("t_ms / rate_milli must be 1-D arrays of equal non-zero length");
           if (t_ms.at(0) != 0) throw py::value_error("the arrival trace must start at t=0");
@@ -929,18 +929,18 @@ PYBIND11_MODULE(_ksa_native, m) {
           const int64_t lanes = params.shape(1) * seeds;
           I64 out64({int64_t(7), lanes});
           I32 out32({int64_t(5), lanes});
-          bool fast = false;
+          int used = 0;
           {
             py::gil_scoped_release rel;
-            fast = queue_sweep_cpu(t_ms.data(), rate_milli.data(), static_cast<int32_t>(t_ms.shape(0)), init, horizon,
+            used = queue_sweep_cpu(t_ms.data(), rate_milli.data(), static_cast<int32_t>(t_ms.shape(0)), init, horizon,
                                    latency.data(), model.data(), params.data(), params.shape(1), seeds, seed0,
-                                   out64.mutable_data(), out32.mutable_data(), threads, saturating ? 1 : 0);
+                                   out64.mutable_data(), out32.mutable_data(), threads, arith);
           }
-          return py::make_tuple(out64, out32, fast);
+          return py::make_tuple(out64, out32, (used & 1) != 0, (used & 2) != 0);
         },
         py::arg("t_ms"), py::arg("rate_milli"), py::arg("init_replicas"), py::arg("horizon_ns"), py::arg("latency"),
         py::arg("model"), py::arg("params"), py::arg("seeds"), py::arg("seed0") = 1, py::arg("threads") = 8,
-        py::arg("saturating") = false);
+        py::arg("arith") = 0);
 
   // ---- fakes ----
   py::class_<InjectedFault>(m, "InjectedFault")

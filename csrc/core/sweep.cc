@@ -69,16 +69,17 @@ bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
   return ms;
 }
 
-bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
+int queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
                      int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params, int64_t m,
                      int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, int threads, int arith) {
   const int64_t lanes = m * seeds;
-  if (lanes <= 0 || n < 1) return false;
+  if (lanes <= 0 || n < 1) return 0;
   for (int k = 0; k < 3; ++k)
-    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return false;  // closedloop.py validates first
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return 0;  // closedloop.py validates first
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
   const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
-  const bool fast = arith == 0 && ksa_sim::fast_path_ok(t_ms, rate_milli, n, qm, init_replicas, horizon_ns, params, m);
+  const bool fast = arith != 1 && ksa_sim::fast_path_ok(t_ms, rate_milli, n, qm, init_replicas, horizon_ns, params, m);
+  const bool ms_clock = fast && arith == 0 && ksa_sim::ms_clock_ok(horizon_ns, latency, params, m);
   std::vector<uint32_t> t32(fast ? n : 0), r32(fast ? n : 0);
   if (fast) ksa_sim::narrow_trace(t_ms, rate_milli, n, t32.data(), r32.data());
   auto work = [&](int64_t lo, int64_t hi) {
@@ -97,8 +98,9 @@ bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
       p.min_pods = params[8 * m + i];
       const uint64_t seed = seed0 + static_cast<uint64_t>(s);
       const ksa_sim::QueueResult r =
-          fast ? ksa_sim::simulate_queue<ksa_sim::FastArith>(p, lat, qm, t32.data(), r32.data(), n, init_replicas,
-                                                             horizon_ns, seed)
+          ms_clock ? ksa_sim::simulate_queue_ms(p, lat, qm, t32.data(), r32.data(), n, init_replicas, horizon_ns, seed)
+          : fast   ? ksa_sim::simulate_queue<ksa_sim::FastArith>(p, lat, qm, t32.data(), r32.data(), n, init_replicas,
+                                                               horizon_ns, seed)
                : ksa_sim::simulate_queue<ksa_sim::SatArith>(p, lat, qm, t_ms, rate_milli, n, init_replicas, horizon_ns,
                                                             seed);
       const int64_t o64[7] = {r.pod_ms, r.backlog_msg_ms, r.violation_ms, r.peak_backlog, r.arrived, r.served,
@@ -110,9 +112,10 @@ bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
   };
   int t = std::max(1, threads);
   if (t > lanes) t = static_cast<int>(lanes);
+  const int used = (fast ? 1 : 0) | (ms_clock ? 2 : 0);
   if (t == 1) {
     work(0, lanes);
-    return fast;
+    return used;
   }
   std::vector<std::thread> pool;
   const int64_t chunk = 256;
@@ -126,7 +129,7 @@ bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, 
       }
     });
   for (auto& th : pool) th.join();
-  return fast;
+  return used;
 }
 
 }  // namespace ksa

@@ -19,8 +19,10 @@ bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
 // Closed-loop sweep (csrc/sim/queue_sim.h), CPU path; layouts as ksa_queue_sweep_gpu
 // (csrc/hip/queue_sweep.hip): params [9][m], model {service_milli, startup_ns, slo_backlog,
 // init_backlog}, out64 [7][m*seeds], out32 [5][m*seeds], lane = config * seeds + seed. arith: 0
-// picks ksa_sim::FastArith when fast_path_ok holds, 1 forces SatArith. Returns true if FastArith ran.
-bool queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
+// picks ksa_sim::FastArith when fast_path_ok holds (with the millisecond decision clock,
+// simulate_queue_ms, when ms_clock_ok holds too), 1 forces SatArith, 2 allows FastArith without
+// the ms clock. Returns bit 0: FastArith ran, bit 1: the ms clock ran.
+int queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
                      int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params, int64_t m,
                      int32_t seeds, uint64_t seed0, int64_t* out64, int32_t* out32, int threads, int arith = 0);
 

@@ -43,7 +43,7 @@ thread_local std::string g_queue_error;
 
 // A: ksa_sim::FastArith (T = uint32_t, the host proved the sweep's bounds: fast_path_ok) or
 // ksa_sim::SatArith (T = int64_t).
-template <class A, class T>
+template <class A, class T, bool kMs>
 __global__ __launch_bounds__(kBlock)
 #if KSA_QUEUE_WAVES_PER_EU > 0
 __attribute__((amdgpu_waves_per_eu(KSA_QUEUE_WAVES_PER_EU)))
@@ -67,8 +67,11 @@ void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m, int32_t s
     p.down_pods = params[kDownPods * m + i];
     p.max_pods = params[kMaxPods * m + i];
     p.min_pods = params[kMinPods * m + i];
-    const ksa_sim::QueueResult r =
-        ksa_sim::simulate_queue<A>(p, lat, model, t_ms, rate_milli, n, init, horizon, seed0 + static_cast<uint64_t>(s));
+    ksa_sim::QueueResult r;
+    if constexpr (kMs)
+      r = ksa_sim::simulate_queue_ms(p, lat, model, t_ms, rate_milli, n, init, horizon, seed0 + static_cast<uint64_t>(s));
+    else
+      r = ksa_sim::simulate_queue<A>(p, lat, model, t_ms, rate_milli, n, init, horizon, seed0 + static_cast<uint64_t>(s));
     out64[kPodMs * lanes + l] = r.pod_ms;
     out64[kBacklogMsgMs * lanes + l] = r.backlog_msg_ms;
     out64[kViolationMs * lanes + l] = r.violation_ms;
@@ -92,18 +95,18 @@ bool ok(hipError_t e, const char* what) {
 
 // Launches one arithmetic's kernel on the arena's stream; the grid is one resident wave of
 // workgroups.
-template <class A, class T>
+template <class A, class T, bool kMs = false>
 bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, int32_t seeds, uint64_t seed0,
             const ksa_sim::Latency& lat, const ksa_sim::QueueModel& qm, const T* d_t, const T* d_r, int32_t n,
             int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
   const int64_t lanes = m * seeds;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_sweep_kernel<A, T>, kBlock, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_sweep_kernel<A, T, kMs>, kBlock, 0) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
   const int64_t want = (lanes + kBlock - 1) / kBlock;
   const int grid = static_cast<int>(std::min<int64_t>(want, static_cast<int64_t>(ar.cus) * per_cu));
-  hipLaunchKernelGGL((queue_sweep_kernel<A, T>), dim3(grid), dim3(kBlock), 0, ar.stream, d_p, m, seeds, seed0, lat, qm,
+  hipLaunchKernelGGL((queue_sweep_kernel<A, T, kMs>), dim3(grid), dim3(kBlock), 0, ar.stream, d_p, m, seeds, seed0, lat, qm,
                      d_t, d_r, n, init, horizon_ns, d_o64, d_o32);
   return ok(hipGetLastError(), "queue_sweep_kernel launch");
 }
@@ -118,7 +121,9 @@ const char* ksa_queue_sweep_last_error() { return g_queue_error.c_str(); }
 // startup_ns, slo_backlog, init_backlog}; latency {sqs, get, update} ns; params [9][m];
 // out64 [7][m*seeds] (pod_ms, backlog_msg_ms, violation_ms, peak_backlog, arrived, served,
 // final_backlog); out32 [5][m*seeds] (ups, downs, final, max_replicas, polls). arith: 0 picks
-// FastArith when ksa_sim::fast_path_ok holds, 1 forces SatArith; *fast_used reports the choice.
+// FastArith when ksa_sim::fast_path_ok holds, with the decisions on the millisecond clock when
+// ksa_sim::ms_clock_ok holds too; 1 forces SatArith; 2 allows FastArith but not the ms clock.
+// *fast_used reports the choice: bit 0 FastArith, bit 1 the millisecond clock.
 // 0 on success.
 int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,
                         int64_t horizon_ns, const int64_t* latency, const int64_t* model, const int64_t* params,
@@ -140,8 +145,9 @@ int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli,
   const int64_t lanes = m * seeds;
   if (lanes <= 0) return 0;
   const ksa_sim::QueueModel qm{model[0], model[1], model[2], model[3]};
-  const bool fast = arith == 0 && ksa_sim::fast_path_ok(t_ms, rate_milli, n, qm, init_replicas, horizon_ns, params, m);
-  if (fast_used) *fast_used = fast ? 1 : 0;
+  const bool fast = arith != 1 && ksa_sim::fast_path_ok(t_ms, rate_milli, n, qm, init_replicas, horizon_ns, params, m);
+  const bool ms_clock = fast && arith == 0 && ksa_sim::ms_clock_ok(horizon_ns, latency, params, m);
+  if (fast_used) *fast_used = (fast ? 1 : 0) | (ms_clock ? 2 : 0);
   // the trace in the chosen arithmetic's element type
   std::vector<uint32_t> t32, r32;
   const size_t elem = fast ? sizeof(uint32_t) : sizeof(int64_t);
@@ -176,8 +182,12 @@ int ksa_queue_sweep_gpu(int dev, const int64_t* t_ms, const int64_t* rate_milli,
   int32_t* o32 = static_cast<int32_t*>(d_o32);
   if (!ok(hipEventRecord(ar->e0, st), "hipEventRecord")) return -1;
   const bool launched =
-      fast ? launch<ksa_sim::FastArith>(*ar, p, m, seeds, seed0, lat, qm, static_cast<const uint32_t*>(d_t),
-                                        static_cast<const uint32_t*>(d_r), n, init_replicas, horizon_ns, o64, o32)
+      ms_clock ? launch<ksa_sim::FastArith, uint32_t, true>(*ar, p, m, seeds, seed0, lat, qm,
+                                                            static_cast<const uint32_t*>(d_t),
+                                                            static_cast<const uint32_t*>(d_r), n, init_replicas,
+                                                            horizon_ns, o64, o32)
+      : fast ? launch<ksa_sim::FastArith>(*ar, p, m, seeds, seed0, lat, qm, static_cast<const uint32_t*>(d_t),
+                                          static_cast<const uint32_t*>(d_r), n, init_replicas, horizon_ns, o64, o32)
            : launch<ksa_sim::SatArith>(*ar, p, m, seeds, seed0, lat, qm, static_cast<const int64_t*>(d_t),
                                        static_cast<const int64_t*>(d_r), n, init_replicas, horizon_ns, o64, o32);
   if (!launched) return -1;

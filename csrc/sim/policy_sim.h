@@ -299,10 +299,15 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
 // for the same sweeps, and tests pin it equal to simulate() on randomised inputs.
 constexpr int32_t kMsNever = INT32_MAX;
 
-struct MsRules {
-  int32_t up_msgs, down_msgs, up_cool, down_cool, period;
+// Th: the thresholds' type -- int32 for a replayed trace (depths bounded by the host), int64 for
+// the closed-loop queue (queue_sim.h), whose backlog has no such bound.
+template <class Th>
+struct MsRulesT {
+  Th up_msgs, down_msgs;
+  int32_t up_cool, down_cool, period;
   int32_t max32, min32, up32, down32;
 };
+using MsRules = MsRulesT<int32_t>;
 
 // Latencies in milliseconds (the field names are KSA_DECIDE's).
 struct MsLatency {
@@ -328,11 +333,17 @@ KSA_HD int32_t ms_bound(int32_t horizon_ms, const MsLatency& lat) {
   return horizon_ms + lat.sqs_ns + 2 * (lat.get_ns + lat.update_ns);
 }
 
-KSA_HD MsRules make_ms_rules(const Params& p, int64_t horizon_ns, int32_t bound) {
-  MsRules k;
+template <class Th = int32_t>
+KSA_HD MsRulesT<Th> make_ms_rules(const Params& p, int64_t horizon_ns, int32_t bound) {
+  MsRulesT<Th> k;
   const int64_t b1 = static_cast<int64_t>(bound) + 1;
-  k.up_msgs = clamp_i32(p.up_msgs, 0, INT32_MAX);     // d >= up_msgs, d in [0, 2^31 - 2]
-  k.down_msgs = clamp_i32(p.down_msgs, -1, INT32_MAX);  // d <= down_msgs
+  if constexpr (sizeof(Th) == 4) {
+    k.up_msgs = clamp_i32(p.up_msgs, 0, INT32_MAX);       // d >= up_msgs, d in [0, 2^31 - 2]
+    k.down_msgs = clamp_i32(p.down_msgs, -1, INT32_MAX);  // d <= down_msgs
+  } else {
+    k.up_msgs = p.up_msgs;
+    k.down_msgs = p.down_msgs;
+  }
   k.up_cool = clamp_i32(ceil_div_1e6(p.up_cool_ns), -b1, b1);
   k.down_cool = clamp_i32(ceil_div_1e6(p.down_cool_ns), -b1, b1);
   // a period past the horizon never fires (its first poll is past it); others are whole ms
@@ -424,9 +435,9 @@ KSA_HD Result simulate_ms(const Params& p, const MsLatency& lat, const int32_t* 
 
 // Host check for simulate_ms (see above): whole-ms latencies, whole-ms periods wherever a
 // period can fire (0 < poll <= horizon), depths in [0, 2^31 - 2], and 2B + 1 < 2^31.
-inline bool ms_path_ok(const int64_t* t_ns, const int64_t* depth, int32_t n, int64_t horizon_ns, const int64_t* latency,
-                       const int64_t* params, int64_t configs) {
-  if (n < 1 || t_ns[0] != 0 || horizon_ns < 0) return false;
+// The clock part of it, shared with the closed-loop simulator (queue_sim.h).
+inline bool ms_clock_ok(int64_t horizon_ns, const int64_t* latency, const int64_t* params, int64_t configs) {
+  if (horizon_ns < 0) return false;
   int64_t lat_ms = 0;
   for (int k = 0; k < 3; ++k) {
     if (latency[k] < 0 || latency[k] > kMaxLatencyNs || latency[k] % 1000000 != 0) return false;
@@ -434,13 +445,19 @@ inline bool ms_path_ok(const int64_t* t_ns, const int64_t* depth, int32_t n, int
   }
   const int64_t bound = horizon_ns / 1000000 + lat_ms;
   if (2 * bound + 1 >= (int64_t(1) << 31)) return false;
-  for (int32_t i = 0; i < n; ++i)
-    if (depth[i] < 0 || depth[i] > INT32_MAX - 1) return false;
   for (int64_t i = 0; i < configs; ++i) {
     const int64_t poll = params[i];  // params [9][m]: poll first
     if (poll > 0 && poll <= horizon_ns && poll % 1000000 != 0) return false;
   }
   return true;
+}
+
+inline bool ms_path_ok(const int64_t* t_ns, const int64_t* depth, int32_t n, int64_t horizon_ns, const int64_t* latency,
+                       const int64_t* params, int64_t configs) {
+  if (n < 1 || t_ns[0] != 0) return false;
+  for (int32_t i = 0; i < n; ++i)
+    if (depth[i] < 0 || depth[i] > INT32_MAX - 1) return false;
+  return ms_clock_ok(horizon_ns, latency, params, configs);
 }
 
 // The trace as simulate_ms reads it: boundaries ceil(t / 1 ms) (kMsNever past 2^31 ms), depths.

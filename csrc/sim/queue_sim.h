@@ -335,6 +335,79 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
   return res;
 }
 
+// simulate_queue<FastArith> with the decisions on policy_sim.h's 32-bit millisecond clock: for
+// sweeps whose periods and latencies are whole milliseconds (ms_clock_ok) every decision time is
+// one, so `now`, the cool-down timers and the poll times are int32 milliseconds -- no 64-bit time
+// compares and adds, and no carry of the poll's millisecond out of a nanosecond clock. The
+// thresholds stay 64-bit (the backlog they compare with is not bounded by 2^31); a new pod's
+// ready time is now + floor(startup / 1 ms), which is (now + startup) / 1 ms for a whole-ms now.
+// Same values as simulate_queue (tests pin the two equal).
+template <class T>
+KSA_HD QueueResult simulate_queue_ms(const Params& p, const Latency& lat_ns, const QueueModel& m, const T* t_ms,
+                                     const T* rate_milli, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+                                     uint64_t seed) {
+  using A = FastArith;
+  using Ms = A::Ms;
+  QueueResult res;
+  const MsLatency lat = ms_latency(lat_ns);
+  const int32_t horizon_ms = static_cast<int32_t>(horizon_ns / 1000000);
+  const MsRulesT<int64_t> k = make_ms_rules<int64_t>(p, horizon_ns, ms_bound(horizon_ms, lat));
+  QueueState<A> s;
+  const int64_t init_backlog = m.init_backlog > 0 ? m.init_backlog : 0;
+  s.q_micro = init_backlog * 1000000;
+  s.q_msgs = init_backlog;
+  s.ready = init_replicas;
+  s.pending = 0;
+  s.pending_at_ms = 0;
+  s.draws = 0;
+  s.memo_mean = -1;
+  s.memo_sd = 0;
+  const uint64_t base = seed * kSeedMul;
+  RateCursor<A, T> cur = rate_cursor_init<A>(t_ms, rate_milli, n);
+  const int64_t startup_ms = udiv_1e6(m.startup_ns);  // >= 0 under fast_path_ok
+  int32_t now = 0, last_up = 0, last_down = 0;  // main.go:37-38
+  int32_t replicas = init_replicas;
+  res.max_replicas = replicas;
+  int32_t prev = 0;
+  const bool advances = k.period > 0 || lat.sqs_ns > 0;
+  while (advances && res.polls < kMaxPolls) {
+    const int32_t t_poll = now + k.period;  // main.go:41 sleep, then poll
+    if (t_poll > horizon_ms) break;
+    advance(&s, &res, m, t_ms, rate_milli, n, &cur, base, static_cast<Ms>(prev), static_cast<Ms>(t_poll), replicas);
+    prev = t_poll;
+    now = t_poll;
+    res.polls++;
+    const int64_t d = s.q_msgs;  // depth the SQS call reports
+    now += lat.sqs_ns;
+    const int32_t before = replicas;
+    int32_t gets = 0, writes = 0;
+    KSA_DECIDE(k, lat, d, now, last_up, last_down, replicas, gets, writes, res.ups++, (void)0, res.downs++, (void)0);
+    (void)gets;
+    (void)writes;
+    const int32_t delta = sub_i32(replicas, before);
+    if (delta > 0) {  // new pods: billed now, draining after the start-up delay
+      s.pending += delta;
+      const int64_t at = static_cast<int64_t>(now) + startup_ms;
+      s.pending_at_ms = at < static_cast<int64_t>(A::kNeverMs) ? static_cast<Ms>(at) : A::kNeverMs;
+    } else if (delta < 0) {  // the Deployment controller removes not-yet-ready pods first
+      int32_t drop = -delta;
+      const int32_t from_pending = drop < s.pending ? drop : s.pending;
+      s.pending -= from_pending;
+      drop -= from_pending;
+      s.ready = s.ready > drop ? s.ready - drop : 0;
+    }
+    if (replicas > res.max_replicas) res.max_replicas = replicas;
+    if (s.q_msgs > res.peak_backlog) res.peak_backlog = s.q_msgs;
+  }
+  if (horizon_ms > prev)
+    advance(&s, &res, m, t_ms, rate_milli, n, &cur, base, static_cast<Ms>(prev), static_cast<Ms>(horizon_ms), replicas);
+  res.final_replicas = replicas;
+  res.final_backlog = s.q_msgs;
+  res.arrived /= 1000000;
+  res.served /= 1000000;
+  return res;
+}
+
 // Host check for FastArith: true when, for every configuration and seed, no accumulator,
 // backlog or product can reach kSat and no replica count can wrap, so FastArith and SatArith
 // compute the same values. Conservative bounds, in double with a factor-2 margin (2^61):

@@ -109,6 +109,7 @@ class ClosedLoopResult:
     horizon_ns: int
     kernel_ms: float = 0.0
     fast_arith: bool = False  # the native path ran queue_sim.h's FastArith (bounds proven)
+    ms_clock: bool = False  # ... with its decisions on the millisecond clock (simulate_queue_ms)
 
     def __len__(self) -> int:
         return self.params.shape[1]
@@ -159,10 +160,14 @@ def run(trace: ArrivalTrace, params: np.ndarray, model: QueueModel, init_replica
         arith: str = "auto") -> ClosedLoopResult:
     """Runs the sweep. ``arith``: ``"auto"`` runs queue_sim.h's FastArith (plain integer ops,
     32-bit times) when ``fast_path_ok`` proves that no quantity can saturate -- identical results --
-    and the saturating arithmetic otherwise; ``"saturating"`` always runs the latter."""
-    if arith not in ("auto", "saturating"):
-        raise ValueError(f"arith must be auto or saturating, not {arith!r}")
-    saturating = arith == "saturating"
+    with the decisions on 32-bit millisecond clocks when every period and latency is a whole
+    millisecond (``ms_clock_ok``), and the saturating arithmetic otherwise; ``"saturating"``
+    always runs the latter; ``"fast-ns"`` allows FastArith but keeps the nanosecond decision
+    clock (A/B and tests)."""
+    codes = {"auto": 0, "saturating": 1, "fast-ns": 2}
+    if arith not in codes:
+        raise ValueError(f"arith must be auto, saturating or fast-ns, not {arith!r}")
+    code = codes[arith]
     params = np.ascontiguousarray(params, dtype=np.int64)
     if params.ndim != 2 or params.shape[0] != len(PARAM_FIELDS):
         raise ValueError("params must have shape (9, m); build it with sweep.grid()")
@@ -193,23 +198,23 @@ def run(trace: ArrivalTrace, params: np.ndarray, model: QueueModel, init_replica
         rc = lib.ksa_queue_sweep_gpu(gpu_index, trace.t_ms.ctypes.data, trace.rate_milli.ctypes.data, len(trace.t_ms),
                                      init_replicas, horizon_ns, lat.ctypes.data, packed.ctypes.data, params.ctypes.data,
                                      m, seeds, seed0, out64.ctypes.data, out32.ctypes.data, ctypes.byref(ms),
-                                     1 if saturating else 0, ctypes.byref(used))
+                                     code, ctypes.byref(used))
         if rc != 0:
             raise RuntimeError("GPU closed-loop sweep failed: " + (lib.ksa_queue_sweep_last_error() or b"").decode())
         kernel_ms = ms.value
-        fast = bool(used.value)
+        fast, ms_clock = bool(used.value & 1), bool(used.value & 2)
     elif device == "cpu":
         from ..ops import native
 
-        out64, out32, fast = native().queue_sweep_cpu(trace.t_ms, trace.rate_milli, init_replicas, horizon_ns, lat,
-                                                      packed, params, seeds, seed0, threads or (os.cpu_count() or 8),
-                                                      saturating)
+        out64, out32, fast, ms_clock = native().queue_sweep_cpu(trace.t_ms, trace.rate_milli, init_replicas, horizon_ns,
+                                                                lat, packed, params, seeds, seed0,
+                                                                threads or (os.cpu_count() or 8), code)
         kernel_ms = 0.0
     else:
         raise ValueError(f"device must be auto, gpu or cpu, not {device!r}")
     out = {k: out64[i].reshape(m, seeds) for i, k in enumerate(OUT64)}
     out.update({k: out32[i].reshape(m, seeds) for i, k in enumerate(OUT32)})
-    return ClosedLoopResult(params, seeds, out, device, horizon_ns, kernel_ms, fast)
+    return ClosedLoopResult(params, seeds, out, device, horizon_ns, kernel_ms, fast, ms_clock)
 
 
 # ---------------------------------------------------------------------------------------------

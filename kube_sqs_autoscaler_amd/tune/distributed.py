@@ -147,10 +147,12 @@ def run_closed_loop(g: Group, trace: closedloop.ArrivalTrace, params: np.ndarray
     if hi > lo:
         res = closedloop.run(trace, params[:, lo:hi], model, init_replicas, horizon_ns, latency_ns, seeds, seed0,
                              g.device, gpu_index=g.local_rank)
-        out, kernel_ms = res.out, res.kernel_ms
+        out, kernel_ms, flags = res.out, res.kernel_ms, (res.fast_arith, res.ms_clock)
     else:
         out = {k: np.zeros((0, seeds), dtype=np.int64 if k in closedloop.OUT64 else np.int32)
                for k in closedloop.OUT64 + closedloop.OUT32}
-        kernel_ms = 0.0
+        kernel_ms, flags = 0.0, (True, True)
     full = g.all_gather_fields(out, counts)
-    return closedloop.ClosedLoopResult(params, seeds, full, g.device, horizon_ns, g.max(kernel_ms))
+    # fast_arith / ms_clock: every shard ran it
+    fast, ms_clock = (g.max(float(not f)) == 0.0 for f in flags)
+    return closedloop.ClosedLoopResult(params, seeds, full, g.device, horizon_ns, g.max(kernel_ms), fast, ms_clock)

@@ -1,8 +1,9 @@
 """Closed-loop what-if sweep throughput: configurations x seeds over a synthetic 24 h arrival
 pattern, gfx950 kernel vs the CPU path (same header, bit-identical). One JSON line per device.
 
-``--arith saturating`` forces queue_sim.h's saturating arithmetic on the GPU (default: auto, which
-runs FastArith when its bounds hold -- they do here). The CPU slice always runs the saturating
+``--arith saturating`` forces queue_sim.h's saturating arithmetic on the GPU, ``--arith fast-ns``
+FastArith with the nanosecond decision clock (default: auto, which runs FastArith when its bounds
+hold, on the millisecond decision clock when periods and latencies are whole ms -- both hold here). The CPU slice always runs the saturating
 arithmetic, so the equality line checks the GPU's arithmetic against it."""
 import argparse
 import json
@@ -18,7 +19,8 @@ from kube_sqs_autoscaler_amd.tune import closedloop as cl  # noqa: E402
 from kube_sqs_autoscaler_amd.tune import sweep  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--arith", choices=("auto", "saturating"), default="auto")
+ap.add_argument("--arith", choices=("auto", "saturating", "fast-ns"), default="auto",
+                help="GPU arithmetic: auto (FastArith on the ms decision clock here), fast-ns, saturating")
 args = ap.parse_args()
 S = 1_000_000_000
 minutes = np.arange(1440)
@@ -44,7 +46,7 @@ for device in ("gpu", "cpu"):
     summ = r.summary()
     feasible = summ["violation_s_p95"] <= 600
     best = int(np.argmin(np.where(feasible, summ["pod_hours_mean"], np.inf))) if feasible.any() else None
-    print(json.dumps({"device": device, "arith": "fast" if r.fast_arith else "saturating", "configs": sub.shape[1], "seeds": seeds, "lane_polls": polls,
+    print(json.dumps({"device": device, "arith": ("fast" if r.fast_arith else "saturating") + ("+ms" if r.ms_clock else ""), "configs": sub.shape[1], "seeds": seeds, "lane_polls": polls,
                       "wall_s": round(wall, 4), "kernel_ms": round(r.kernel_ms, 3),
                       "lane_polls_per_s": round(polls / wall, 1),
                       "feasible": int(feasible.sum()),

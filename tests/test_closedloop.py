@@ -190,6 +190,7 @@ def test_fast_arithmetic_selection_is_exact(nat, tweak, fast):
     auto = cl.run(tr, grid, model, 1, 2400 * S, LAT, seeds=4, seed0=2, device="cpu")
     sat = cl.run(tr, grid, model, 1, 2400 * S, LAT, seeds=4, seed0=2, device="cpu", arith="saturating")
     assert auto.fast_arith is fast and not sat.fast_arith
+    assert auto.ms_clock is fast and not sat.ms_clock  # whole-ms periods and latencies
     for k in auto.out:
         assert np.array_equal(auto.out[k], sat.out[k]), k
     for i in range(len(auto)):
@@ -237,3 +238,40 @@ def test_fast_arithmetic_matches_saturating_on_random_extremes(nat):
             assert np.array_equal(auto.out[k], sat.out[k]), (k, horizon_s, rates, model, auto.fast_arith)
         picked[auto.fast_arith] += 1
     assert picked[True] and picked[False]
+
+
+def test_ms_decision_clock_equals_ns_clock_on_random_inputs(nat):
+    """simulate_queue_ms (decisions on 32-bit millisecond clocks) against FastArith on the
+    nanosecond clock and against the saturating arithmetic: cool-downs and start-up delays at any
+    nanosecond (the ms clock ceils the former and floors the latter), several poll periods, rate
+    traces with sub-second boundaries, and periods that never fire."""
+    rng = np.random.default_rng(1017)
+    for _ in range(30):
+        horizon_s = int(rng.choice([300, 3600, 86400]))
+        starts = sorted({0.0, *[float(x) for x in rng.uniform(0.001, horizon_s, int(rng.integers(0, 6)))]})
+        tr = cl.ArrivalTrace.from_segments([(t, float(rng.choice([0.0, 0.3, 4.0, 60.0, 900.0]))) for t in starts])
+        cools = [0, int(rng.integers(0, 10**12)), int(rng.integers(-10**10, 10**10)), 7 * S + 1, -1, 2**62]
+        grid = sweep.grid(poll_ns=[int(rng.integers(1, 20_000)) * 10**6, int(rng.integers(1, 9)) * S, 2**62],
+                          up_cool_ns=cools[:3], down_cool_ns=cools[3:], up_msgs=[int(rng.integers(-5, 300))],
+                          down_msgs=[int(rng.integers(-5, 50))], up_pods=[int(rng.integers(0, 4))],
+                          down_pods=[int(rng.integers(0, 4))], max_pods=[int(rng.integers(0, 30))],
+                          min_pods=[int(rng.integers(0, 4))])
+        model = cl.QueueModel(service_rate=float(rng.choice([0.0, 0.7, 5.0, 80.0])),
+                              startup_ns=int(rng.integers(0, 200 * S)), slo_backlog=int(rng.integers(0, 500)),
+                              init_backlog=int(rng.integers(0, 5000)))
+        lat = tuple(int(x) * 10**6 for x in rng.integers(0, 30, 3))
+        if lat[0] == 0:
+            lat = (10**6,) + lat[1:]
+        args = (tr, grid, model, int(rng.integers(0, 5)), horizon_s * S, lat)
+        ms = cl.run(*args, seeds=3, seed0=4, device="cpu")
+        ns = cl.run(*args, seeds=3, seed0=4, device="cpu", arith="fast-ns")
+        sat = cl.run(*args, seeds=3, seed0=4, device="cpu", arith="saturating")
+        assert ms.fast_arith and ms.ms_clock and ns.fast_arith and not ns.ms_clock
+        for k in ms.out:
+            assert np.array_equal(ms.out[k], ns.out[k]), (k, lat, model)
+            assert np.array_equal(ms.out[k], sat.out[k]), (k, lat, model)
+    # a sub-millisecond latency: the nanosecond clock
+    tr = burst_trace()
+    r = cl.run(tr, sweep.grid(poll_ns=[5 * S]), cl.QueueModel(5.0, 0, 100), 1, 600 * S, (1_500_000, 10**6, 10**6),
+               seeds=1, device="cpu")
+    assert r.fast_arith and not r.ms_clock

@@ -189,13 +189,17 @@ def test_closed_loop_kernel_equals_cpu_and_python_model():
     model = cl.QueueModel(service_rate=5.0, startup_ns=60 * S, slo_backlog=200, init_backlog=10)
     lat = (2_000_000, 1_000_000, 1_000_000)
     g = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="gpu")
+    gn = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="gpu", arith="fast-ns")
     gs = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="gpu", arith="saturating")
     c = cl.run(tr, grid, model, 1, 2400 * S, lat, seeds=64, device="cpu", arith="saturating")
     assert g.device == "gpu" and g.kernel_ms > 0
-    # the bounds hold, so the GPU ran FastArith -- and matches the saturating arithmetic exactly
-    assert g.fast_arith and not gs.fast_arith and not c.fast_arith
+    # the bounds hold, so the GPU ran FastArith (on the millisecond decision clock: whole-ms
+    # periods and latencies) -- and matches the saturating arithmetic exactly
+    assert g.fast_arith and g.ms_clock and gn.fast_arith and not gn.ms_clock
+    assert not gs.fast_arith and not c.fast_arith
     for k in g.out:
         assert np.array_equal(g.out[k], c.out[k]), k
+        assert np.array_equal(gn.out[k], c.out[k]), k
         assert np.array_equal(gs.out[k], c.out[k]), k
     for i in range(0, len(g), 37):
         want = cl.reference_lane(tr, g.config(i), model, 1, 2400 * S, lat, 1 + 5)
