@@ -153,7 +153,7 @@ def _open_loop(ap: argparse.ArgumentParser, a, group) -> int:
     summary = {"configs": len(res), "feasible": int(ok.sum()), "device": res.device, "wall_s": round(wall, 4),
                "ranks": group.world if group is not None else 1,
                "kernel_ms": round(res.kernel_ms, 3), "simulated_polls": int(res.out["polls"].sum()),
-               "horizon_ns": horizon, "reference_defaults": baseline}
+               "clock": "ms" if res.ms_clock else "ns", "horizon_ns": horizon, "reference_defaults": baseline}
     if a.json:
         print(json.dumps(summary))
         for i in order:
@@ -215,7 +215,9 @@ def _closed_loop(ap: argparse.ArgumentParser, a, group) -> int:
     info = {"configs": len(res), "feasible": int(ok.sum()), "seeds": a.seeds, "device": res.device,
             "ranks": group.world if group is not None else 1,
             "wall_s": round(wall, 4), "kernel_ms": round(res.kernel_ms, 3),
-            "simulated_polls": int(res.out["polls"].sum()), "horizon_ns": horizon, "reference_defaults": base}
+            "simulated_polls": int(res.out["polls"].sum()),
+            "arith": ("fast" if res.fast_arith else "saturating") + ("+ms" if res.ms_clock else ""),
+            "horizon_ns": horizon, "reference_defaults": base}
     if a.json:
         print(json.dumps(info))
         for i in order:
