@@ -187,12 +187,14 @@ def cadenced(a) -> int:
             time.sleep(min(a.window, max(0.0, end - time.monotonic())))
             if child.poll() is not None:
                 break
+            # resources first: the scrape's own handler thread and socket may still be alive
+            # right after it returns, and would count as a thread and an fd of the process
+            res = proc_stats(child.pid)
             try:
                 m = scrape(port)
             except OSError as e:
                 m = {"scrape_error": str(e)}
-            row = {"window": k, "t_s": round(time.monotonic() - t_start, 1), **proc_stats(child.pid), **m,
-                   "injected": dict(injected)}
+            row = {"window": k, "t_s": round(time.monotonic() - t_start, 1), **res, **m, "injected": dict(injected)}
             rows.append(row)
             print(json.dumps(row), flush=True)
             k += 1
