@@ -41,10 +41,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kLdsTraceBytes = 32 * 1024;  // trace staged in LDS up to this size (-> 5 WG/CU)
-// Larger 32-bit traces (a day at 5 s: 17 280 segments, 135 KiB) are staged whole by one
-// 1024-thread workgroup per CU (a workgroup may declare all 160 KiB of a CU's LDS).
-constexpr int kBlockBig = 1024;
-constexpr int kLdsBigBytes = 160 * 1024;
 
 thread_local std::string g_sweep_error;
 
@@ -60,13 +56,13 @@ enum : int { kUps = 0, kDowns, kNoopUps, kNoopDowns, kFinal, kMaxRep, kPolls, kN
 // array, chosen per launch, so the loads are flat: specialising them into ds_read and
 // global_load copies of the loop (two inlined calls) measured slower on the global path (24.5 vs
 // 22.5 ms, profiles/r03u_sweep_ab.jsonl) and equal from LDS.
-template <bool kMs, int kB, class T>
+template <bool kMs, class T>
 __device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, int64_t m, const ksa_sim::Latency& lat,
                                             const T* __restrict__ t, const T* __restrict__ d, int32_t n, int32_t init,
                                             int64_t horizon, int64_t* __restrict__ out64, int32_t* __restrict__ out32) {
   const ksa_sim::MsLatency lat_ms = ksa_sim::ms_latency(lat);
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kB;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x; i < m; i += stride) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += stride) {
     ksa_sim::Params p;
     p.poll_ns = params[kPoll * m + i];
     p.up_cool_ns = params[kUpCool * m + i];
@@ -96,27 +92,28 @@ __device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, 
 }
 
 // kMs: ksa_sim::simulate_ms over a 32-bit trace (T = int32_t; the host checked ms_path_ok), else
-// ksa_sim::simulate over the int64 trace. kB: the workgroup size (kBlock, or kBlockBig for a
-// trace staged whole in up to 160 KiB of LDS). stage: the host's choice to stage the trace.
-template <bool kMs, class T, int kB>
-__global__ __launch_bounds__(kB) __attribute__((amdgpu_waves_per_eu(kB == kBlock ? KSA_SWEEP_WAVES_PER_EU : 4))) void
-sweep_kernel(const int64_t* __restrict__ params, int64_t m, ksa_sim::Latency lat, const T* __restrict__ g_t,
-             const T* __restrict__ g_d, int32_t n, int32_t init, int64_t horizon, int64_t* __restrict__ out64,
-             int32_t* __restrict__ out32, bool stage) {
+// ksa_sim::simulate over the int64 trace.
+template <bool kMs, class T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEEP_WAVES_PER_EU))) void sweep_kernel(
+    const int64_t* __restrict__ params, int64_t m, ksa_sim::Latency lat, const T* __restrict__ g_t,
+    const T* __restrict__ g_d, int32_t n, int32_t init, int64_t horizon, int64_t* __restrict__ out64,
+    int32_t* __restrict__ out32) {
   // Dynamic LDS: 2 x sizeof(T) per segment when the trace is staged, none otherwise -- a static
   // allocation would cap occupancy even for traces that are read from global memory.
+  constexpr int kMaxSeg = kLdsTraceBytes / (2 * static_cast<int>(sizeof(T)));
   extern __shared__ int64_t s_lds[];
+  const bool in_lds = n <= kMaxSeg;
   T* s_t = reinterpret_cast<T*>(s_lds);
-  T* s_d = s_t + (stage ? n : 0);
-  if (stage) {
-    for (int i = threadIdx.x; i < n; i += kB) {
+  T* s_d = s_t + (in_lds ? n : 0);
+  if (in_lds) {
+    for (int i = threadIdx.x; i < n; i += kBlock) {
       s_t[i] = g_t[i];
       s_d[i] = g_d[i];
     }
     __syncthreads();
   }
-  sweep_lanes<kMs, kB>(params, m, lat, stage ? static_cast<const T*>(s_t) : g_t, stage ? static_cast<const T*>(s_d) : g_d,
-                       n, init, horizon, out64, out32);
+  sweep_lanes<kMs>(params, m, lat, in_lds ? static_cast<const T*>(s_t) : g_t, in_lds ? static_cast<const T*>(s_d) : g_d, n,
+                   init, horizon, out64, out32);
 }
 
 bool ok(hipError_t e, const char* what) {
@@ -126,40 +123,23 @@ bool ok(hipError_t e, const char* what) {
 }
 
 // Launches one path's kernel on the arena's stream. The grid is one resident wave of workgroups
-// (KSA_SWEEP_GRID: "tiles" = one workgroup per block of configurations, or N x resident).
-template <bool kMs, class T, int kB>
-bool launch_block(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const ksa_sim::Latency& lat,
-                  const T* d_t, const T* d_d, int32_t n, int32_t init, int64_t horizon_ns, int64_t* d_o64,
-                  int32_t* d_o32, size_t lds) {
-  auto* fn = sweep_kernel<kMs, T, kB>;
-  if (lds > 64 * 1024 &&
-      !ok(hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds)),
-          "hipFuncSetAttribute"))
-    return false;
-  const int64_t want = (m + kB - 1) / kB;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kB, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-  int64_t cap = static_cast<int64_t>(ar.cus) * per_cu;
-  if (const char* g = std::getenv("KSA_SWEEP_GRID")) cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
-  const int grid = static_cast<int>(want < cap ? want : cap);
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kB), lds, ar.stream, d_p, m, lat, d_t, d_d, n, init, horizon_ns, d_o64, d_o32,
-                     lds > 0);
-  return ok(hipGetLastError(), "sweep_kernel launch");
-}
-
+// (KSA_SWEEP_GRID: "tiles" = one workgroup per 256 configurations, or N x resident).
 template <bool kMs, class T>
 bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const ksa_sim::Latency& lat, const T* d_t,
             const T* d_d, int32_t n, int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
+  const int64_t want = (m + kBlock - 1) / kBlock;
   const size_t trace_bytes = 2 * static_cast<size_t>(n) * sizeof(T);
-  if (trace_bytes <= static_cast<size_t>(kLdsTraceBytes))
-    return launch_block<kMs, T, kBlock>(ar, d_p, m, lat, d_t, d_d, n, init, horizon_ns, d_o64, d_o32, trace_bytes);
-  if constexpr (kMs) {
-    const char* big = std::getenv("KSA_SWEEP_BIG_LDS");  // "0": read such traces from global memory (A/B)
-    if (trace_bytes <= static_cast<size_t>(kLdsBigBytes) && !(big && std::strcmp(big, "0") == 0))
-      return launch_block<kMs, T, kBlockBig>(ar, d_p, m, lat, d_t, d_d, n, init, horizon_ns, d_o64, d_o32, trace_bytes);
-  }
-  return launch_block<kMs, T, kBlock>(ar, d_p, m, lat, d_t, d_d, n, init, horizon_ns, d_o64, d_o32, 0);
+  const size_t lds = trace_bytes <= static_cast<size_t>(kLdsTraceBytes) ? trace_bytes : 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<kMs, T>, kBlock, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  int64_t cap = static_cast<int64_t>(ar.cus) * per_cu;
+  if (const char* g = std::getenv("KSA_SWEEP_GRID")) cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
+  const int grid = static_cast<int>(want < cap ? want : cap);
+  hipLaunchKernelGGL((sweep_kernel<kMs, T>), dim3(grid), dim3(kBlock), lds, ar.stream, d_p, m, lat, d_t, d_d, n, init,
+                     horizon_ns, d_o64, d_o32);
+  return ok(hipGetLastError(), "sweep_kernel launch");
 }
 
 }  // namespace
