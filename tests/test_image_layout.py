@@ -114,3 +114,20 @@ def test_slim_image_layout_scales_with_only_its_runtime_packages(nat, image_root
             p.kill()
         sqs.stop()
         kube.stop()
+
+
+def test_package_uses_only_pyyaml_api_present_in_ubuntu_2204():
+    """The image ships Ubuntu 22.04's python3-yaml 5.4.1, not this container's PyYAML 6: the
+    package may only use what 5.4.1 has too -- safe_load / safe_dump and the error base class
+    (no yaml.load without a Loader, which 6 made mandatory; nothing added in 6)."""
+    import re
+
+    allowed = {"safe_load", "safe_dump", "YAMLError"}
+    used = set()
+    pkg = os.path.join(ROOT, "kube_sqs_autoscaler_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith(".py"):
+                with open(os.path.join(dirpath, fn)) as f:
+                    used |= set(re.findall(r"\byaml\.(\w+)", f.read()))
+    assert used and used <= allowed, used - allowed
