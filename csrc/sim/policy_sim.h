@@ -382,6 +382,7 @@ KSA_HD int32_t ms_depth_at(const int32_t* t_ms, const int32_t* depth, int32_t n,
   }
   return k->cur_d;
 }
+
 KSA_HD void accumulate_ms32(Result* r, Accum* a, int32_t dt_ms, int32_t replicas, int32_t depth) {
   r->pod_ms += static_cast<int64_t>(replicas) * dt_ms;
   if (replicas != a->run_r) {
