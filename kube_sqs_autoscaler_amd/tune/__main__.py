@@ -85,7 +85,9 @@ def main(argv=None) -> int:
     ap.add_argument("--queue", default=None, help="queue URL or ns/deployment to select from a multi-queue span log")
     ap.add_argument("--horizon", default="", help="simulated time (Go duration); default: trace length + 1 poll period")
     ap.add_argument("--init-replicas", type=int, default=1)
-    ap.add_argument("--latency", default="1ms,1ms,1ms", help="SQS, GET, write latency (Go durations)")
+    ap.add_argument("--latency", default="1ms,1ms,1ms",
+                    help="SQS, GET, write latency (Go durations); whole milliseconds, with whole-millisecond poll "
+                         "periods, let the simulators run on 32-bit millisecond clocks (faster, same results)")
     ap.add_argument("--grid", action="append", default=[], help="flag=values (repeatable)")
     ap.add_argument("--objective", default=None,
                     help="open loop: pod_ms|backlog|ups|downs (default pod_ms); closed loop: a summary column "
