@@ -1334,7 +1334,10 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
 Nanos HttpClient::spin_window() const {
   if (spin_ns_ <= 0) return 0;
   if (ewma_ns_ < 0) return spin_ns_;  // no sample yet: try
-  return ewma_ns_ <= 4 * spin_ns_ ? spin_ns_ : 0;
+  if (ewma_ns_ <= 4 * spin_ns_) return spin_ns_;
+  // a slower peer: spin through its expected response time when the budget allows
+  const Nanos through = 2 * ewma_ns_, budget = spin_budget_ns_.load(std::memory_order_relaxed);
+  return through <= budget ? through : 0;
 }
 
 Nanos HttpClient::rtt_ewma() const {

@@ -159,6 +159,11 @@ class alignas(kCacheLine) HttpClient {
   // up to `ns` before blocking in poll(2) (saves the scheduler wake-up on fast local peers); for
   // slower peers (real AWS / apiserver RTTs of milliseconds) it never spins. 0 disables.
   void set_busy_poll(Nanos ns) { spin_ns_ = ns; }
+  // With busy-poll on, a read may also spin through a slower peer's expected response time
+  // (twice the EWMA) when that fits in `ns` per request -- the Runner sets 1 % of the poll period
+  // on a worker's own thread, so a cadenced poll is not woken from an idle sleep on its answer,
+  // at a CPU cost bounded by 1 % of one core per request. 0 (default): never beyond the window.
+  void set_spin_budget(Nanos ns) { spin_budget_ns_ = ns; }
   Nanos rtt_ewma() const;
   // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller), the
   // three kinds Go's transport speaks:
@@ -200,6 +205,7 @@ class alignas(kCacheLine) HttpClient {
   HttpClientStats stats_;
   SSL_SESSION* session_ = nullptr;  // last resumable TLS session
   Nanos spin_ns_ = 0;
+  std::atomic<Nanos> spin_budget_ns_{0};
   Nanos ewma_ns_ = -1;   // response-time EWMA (-1: no sample yet)
   int64_t sent_at_ = 0;  // mono time the current request finished writing
   Nanos spin_window() const;

@@ -72,6 +72,8 @@ class DeploymentApi {
   virtual void warm() {}
   // The last request's time breakdown as a JSON object ("" when not timed).
   virtual std::string timing_json() const { return ""; }
+  // HttpClient::set_spin_budget of the client's connection. Default: nothing.
+  virtual void set_spin_budget(Nanos ns) { (void)ns; }
 };
 
 class TokenProvider {
@@ -181,6 +183,9 @@ class alignas(kCacheLine) KubeRestDeployments final : public DeploymentApi {
   void warm() override;
   void set_timing(bool on) {
     if (http_) http_->set_timing(on);
+  }
+  void set_spin_budget(Nanos ns) override {
+    if (http_) http_->set_spin_budget(ns);
   }
   std::string timing_json() const override {
     return http_ && http_->timing() ? http_timing_json(http_->last_timing()) : "";

@@ -396,6 +396,9 @@ void Runner::write_trace(const IterationRecord& r) {
 }
 
 void Runner::run(StopFlag* stop, int64_t max_iterations, Nanos start_delay) {
+  // This thread is the worker's own: its clients may spin through an answer within a share of
+  // the poll period (LoopConfig::spin_budget_per_mille; a back-to-back loop keeps the window).
+  set_spin_budget(std::max<Nanos>(cfg_.poll_period, 0) / 1000 * std::max(cfg_.spin_budget_per_mille, 0));
   if (start_delay > 0 && !clock_->sleep(start_delay, stop)) return;
   if (cfg_.connect_at_start) {
     sqs_->warm(clock_->unix_nanos());
@@ -631,6 +634,7 @@ void Scheduler::start(int64_t max_iterations) {
   const size_t n = runners_.size();
   for (size_t i = 0; i < n; ++i) {
     const Nanos period = std::max<Nanos>(runners_[i]->config().poll_period, 0);
+    runners_[i]->set_spin_budget(0);  // shared threads: a spin would hold up the other queues
     if (stagger_ && n > 1 && period > 0) {
       heap_.push_back(Item{t0 + static_cast<Nanos>(static_cast<double>(period) * i / n), i, true});
     } else {

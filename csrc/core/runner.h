@@ -63,6 +63,10 @@ struct LoopConfig {
   // instead of one shared arena. The CLI needs none: its first poll, or its first warm-up, dials
   // on the worker thread.
   bool connect_at_start = false;
+  // On a worker's own thread, its clients may busy-poll through an answer slower than the
+  // --busy-poll window while twice the response-time EWMA fits in this share of the poll period
+  // (per mille; HttpClient::set_spin_budget): 10 = 1 %. 0 disables. Pooled threads never do.
+  int32_t spin_budget_per_mille = 10;
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };
@@ -213,6 +217,11 @@ class alignas(kCacheLine) Runner {
   void cancel() {
     sqs_->cancel();
     scaler_->cancel();
+  }
+  // Both clients' HttpClient::set_spin_budget.
+  void set_spin_budget(Nanos ns) {
+    sqs_->api()->set_spin_budget(ns);
+    scaler_->api()->set_spin_budget(ns);
   }
   // Closes the clients' keep-alive connections (on the calling thread's file table).
   void release_connections() {

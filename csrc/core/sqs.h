@@ -53,6 +53,8 @@ class SqsApi {
   virtual bool runs_on_wire_work() const { return false; }
   // The last call's time breakdown as a JSON object ("" when not timed): set_timing below.
   virtual std::string timing_json() const { return ""; }
+  // HttpClient::set_spin_budget of the client's connection. Default: nothing.
+  virtual void set_spin_budget(Nanos ns) { (void)ns; }
   // Pre-poll warm-up (Runner prewarm), just before a call due at unix time `at_unix_ns`: do
   // now what the call would otherwise do first -- credentials, the request and its signature
   // for that second, the connection check or dial. Sends nothing. Default: nothing.
@@ -105,6 +107,9 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }
   bool runs_on_wire_work() const override { return true; }
   void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) override;
+  void set_spin_budget(Nanos ns) override {
+    if (http_) http_->set_spin_budget(ns);
+  }
   // Diagnostics: time each call -- credentials + signing, the HTTP phases (HttpTiming), the
   // response parse -- for timing_json().
   void set_timing(bool on) {

@@ -2,10 +2,12 @@
 
 The cadence rows of ``bench.py`` compare whole configurations in separate runs, so run-to-run
 noise (loopback send cost, scheduler placement) lands between them. Here the arms share one run:
-queue q gets arm q % 4 of ``--poll-prewarm`` {0, 1 ms} x ``--busy-poll`` {25 us, 300 us}, all
-queues against the same endpoint process, starts staggered over the period. One JSON line per
-arm and endpoint kind (fakes that sleep / never sleep): poll->patch p50/p90 and the per-call
-phase medians (``HttpTiming``, see ``bench/latency.py``).
+queue q gets arm q % 4, all
+queues against the same endpoint process, starts staggered over the period. The arms (ARMS):
+the CLI defaults (``--poll-prewarm=200us``, ``--busy-poll=25us``, a spin budget of 1 % of the
+period), the same without the spin budget, no warm-up, and a fixed 300 us busy-poll window. One
+JSON line per arm and endpoint kind (fakes that sleep / never sleep): poll->patch p50/p90 and the
+per-call phase medians (``HttpTiming``, see ``bench/latency.py``; ``--untimed`` drops them).
 
     python scripts/cadence_arms.py --period-ms 1000 --polls 27 --queues 16
 """
@@ -21,14 +23,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, _detail_medians  # noqa: E402
 
 MS = 1_000_000
-ARMS = [(0, 25_000), (1_000_000, 25_000), (0, 300_000), (1_000_000, 300_000)]  # (prewarm ns, busy-poll ns)
+# (prewarm ns, busy-poll ns, spin budget per mille of the period): the CLI defaults, the same
+# without the spin budget (round 3's first defaults), no warm-up, and a 300 us fixed window
+ARMS = [(200_000, 25_000, 10), (200_000, 25_000, 0), (0, 25_000, 0), (200_000, 300_000, 0)]
 
 
-def run(period_ms: int, polls: int, queues: int, skip: int = 2) -> None:
+def run(period_ms: int, polls: int, queues: int, skip: int = 2, timed: bool = True) -> None:
     for hot in (False, True):
         env = BenchEnv(queues, "scale", pipeline=True, busy_poll_ns=[a[1] for a in ARMS], servers="process",
                        poll_period_ns=period_ms * MS, stagger=True, hot_endpoints=hot,
-                       prewarm_ns=[a[0] for a in ARMS], timing=True)
+                       prewarm_ns=[a[0] for a in ARMS], spin_budget_per_mille=[a[2] for a in ARMS], timing=timed)
         files = [tempfile.TemporaryFile() for _ in env.runners]
         try:
             for r, f in zip(env.runners, files):
@@ -43,13 +47,13 @@ def run(period_ms: int, polls: int, queues: int, skip: int = 2) -> None:
             for f in files:
                 f.close()
             env.close()
-        for i, (prewarm, busy) in enumerate(ARMS):
+        for i, (prewarm, busy, budget) in enumerate(ARMS):
             spans = [s for s in per_arm[i] if s["patch_latency_ns"] >= 0]
             lat = sorted(s["patch_latency_ns"] for s in spans)
             if not lat:
                 continue
-            print(json.dumps({"period_ms": period_ms, "hot_endpoints": hot, "prewarm_us": prewarm / 1e3,
-                              "busy_poll_us": busy / 1e3, "samples": len(lat),
+            print(json.dumps({"period_ms": period_ms, "hot_endpoints": hot, "timed": timed, "prewarm_us": prewarm / 1e3,
+                              "busy_poll_us": busy / 1e3, "spin_budget_per_mille": budget, "samples": len(lat),
                               "p50_us": round(lat[len(lat) // 2] / 1e3, 1),
                               "p90_us": round(lat[int(len(lat) * 0.9)] / 1e3, 1),
                               "depth_us": round(statistics.median(s["depth_ns"] for s in spans) / 1e3, 1),
@@ -62,10 +66,11 @@ def main() -> int:
     ap.add_argument("--period-ms", type=int, default=1000)
     ap.add_argument("--polls", type=int, default=27, help="polls per queue (the first two are dropped)")
     ap.add_argument("--queues", type=int, default=16, help="a multiple of 4: each arm gets queues / 4")
+    ap.add_argument("--untimed", action="store_true", help="no per-call timing (the p50s without its syscalls)")
     a = ap.parse_args()
     if a.queues % len(ARMS):
         ap.error("--queues must be a multiple of 4")
-    run(a.period_ms, a.polls, a.queues)
+    run(a.period_ms, a.polls, a.queues, timed=not a.untimed)
     return 0
 
 

@@ -60,3 +60,31 @@ def test_bench_workers_dial_their_own_connections(nat):
             assert st["polls"] == 3 and st["speculative_reads"] == 3 and st["speculative_reads_used"] == 3
     finally:
         env.close()
+
+
+@pytest.mark.parametrize("period_ms,spins", [(200, True), (0, False)])
+def test_cadenced_worker_spins_through_a_slow_answer_within_its_budget(nat, period_ms, spins):
+    """HttpClient::set_spin_budget: a worker on its own thread may busy-poll through an answer
+    that takes longer than the --busy-poll window when twice the response-time EWMA fits in 1 %
+    of the poll period (200 ms -> 2 ms; the fakes answer after ~0.4 ms), so the poll is not woken
+    from an idle sleep by its answer. Back to back (no period, no budget) a peer that slow is
+    waited for in poll(2), as before."""
+    import json
+    import tempfile
+
+    env = BenchEnv(1, busy_poll_ns=25_000, poll_period_ns=period_ms * 1_000_000, timing=True,
+                   sqs_latency_ns=400_000, kube_latency_ns=400_000)
+    f = tempfile.TemporaryFile()
+    try:
+        env.runners[0].set_trace_fd(f.fileno())
+        env.run(8)
+        env.runners[0].set_trace_fd(-1)
+        f.seek(0)
+        spans = [json.loads(line) for line in f.read().decode().splitlines()][3:]  # EWMA settled
+    finally:
+        f.close()
+        env.close()
+    sqs = [s["detail"]["sqs"] for s in spans if s.get("detail") and s["detail"].get("sqs")]
+    assert len(sqs) >= 4
+    spun = sum(1 for c in sqs if c["spun"])
+    assert (spun == len(sqs)) if spins else (spun == 0), sqs
