@@ -719,7 +719,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("prefetch_always", &LoopConfig::prefetch_always)
       .def_readwrite("prewarm_ns", &LoopConfig::prewarm)
       .def_readwrite("connect_at_start", &LoopConfig::connect_at_start)
-      .def_readwrite("spin_budget_per_mille", &LoopConfig::spin_budget_per_mille);
+      .def_readwrite("spin_budget_ppm", &LoopConfig::spin_budget_ppm);
 
   py::class_<Runner, std::shared_ptr<Runner>>(m, "Runner")
       .def(py::init<LoopConfig, std::shared_ptr<SqsClient>, std::shared_ptr<PodAutoScaler>, std::shared_ptr<Clock>,

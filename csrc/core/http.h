@@ -160,9 +160,9 @@ class alignas(kCacheLine) HttpClient {
   // slower peers (real AWS / apiserver RTTs of milliseconds) it never spins. 0 disables.
   void set_busy_poll(Nanos ns) { spin_ns_ = ns; }
   // With busy-poll on, a read may also spin through a slower peer's expected response time
-  // (twice the EWMA) when that fits in `ns` per request -- the Runner sets 1 % of the poll period
-  // on a worker's own thread, so a cadenced poll is not woken from an idle sleep on its answer,
-  // at a CPU cost bounded by 1 % of one core per request. 0 (default): never beyond the window.
+  // (twice the EWMA) when that fits in `ns` per request -- the Runner sets its share of the poll
+  // period on a worker's own thread (LoopConfig::spin_budget_ppm), so a cadenced poll is not woken
+  // from an idle sleep on its answer, at a bounded CPU cost. 0 (default): never beyond the window.
   void set_spin_budget(Nanos ns) { spin_budget_ns_ = ns; }
   Nanos rtt_ewma() const;
   // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller), the

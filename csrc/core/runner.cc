@@ -397,8 +397,8 @@ void Runner::write_trace(const IterationRecord& r) {
 
 void Runner::run(StopFlag* stop, int64_t max_iterations, Nanos start_delay) {
   // This thread is the worker's own: its clients may spin through an answer within a share of
-  // the poll period (LoopConfig::spin_budget_per_mille; a back-to-back loop keeps the window).
-  set_spin_budget(std::max<Nanos>(cfg_.poll_period, 0) / 1000 * std::max(cfg_.spin_budget_per_mille, 0));
+  // the poll period (LoopConfig::spin_budget_ppm; a back-to-back loop keeps the window).
+  set_spin_budget(std::max<Nanos>(cfg_.poll_period, 0) / 1000000 * std::clamp<int64_t>(cfg_.spin_budget_ppm, 0, 1000000));
   if (start_delay > 0 && !clock_->sleep(start_delay, stop)) return;
   if (cfg_.connect_at_start) {
     sqs_->warm(clock_->unix_nanos());

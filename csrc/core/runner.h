@@ -65,8 +65,10 @@ struct LoopConfig {
   bool connect_at_start = false;
   // On a worker's own thread, its clients may busy-poll through an answer slower than the
   // --busy-poll window while twice the response-time EWMA fits in this share of the poll period
-  // (per mille; HttpClient::set_spin_budget): 10 = 1 %. 0 disables. Pooled threads never do.
-  int32_t spin_budget_per_mille = 10;
+  // (parts per million; HttpClient::set_spin_budget). The CLI gives a process's queues 1 % in
+  // total (10000 / queues each), so their spinning stays within a few % of one core whatever
+  // the queue count. 0 disables. Pooled threads never spin beyond the window.
+  int64_t spin_budget_ppm = 10000;
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };

@@ -25,6 +25,8 @@ from .sqs.session import custom_ca_bundle
 from .utils import proxy
 from .utils.goflag import SECOND
 
+SPIN_BUDGET_PPM = 10_000  # LoopConfig.spin_budget_ppm of a process's queues together: 1 %
+
 _SCALE_MODES = {"deployment": "Deployment", "scale": "Scale", "patch": "Patch"}
 
 
@@ -209,8 +211,10 @@ def new_sqs_client(target: TargetConfig, api):
     return native().SqsClient(api, target.queue_url, list(target.attribute_names))
 
 
-def loop_config(target: TargetConfig, pipeline_reads: bool = False, prewarm_ns: int = 0):
+def loop_config(target: TargetConfig, pipeline_reads: bool = False, prewarm_ns: int = 0, queues: int = 1):
     c = native().LoopConfig()
+    # the process's queues share a 1 % busy-poll budget of their poll period (runner.h)
+    c.spin_budget_ppm = SPIN_BUDGET_PPM // max(queues, 1)
     c.prefetch = pipeline_reads
     c.prewarm_ns = prewarm_ns
     c.poll_period_ns = target.poll_period_ns
@@ -244,7 +248,8 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
                           credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
-    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns), sqs, scaler, clock, log)
+    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns, len(cfg.targets)), sqs, scaler,
+                        clock, log)
     return Worker(target, runner, sqs_api, kube_api, log)
 
 

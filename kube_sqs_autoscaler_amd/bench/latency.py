@@ -27,7 +27,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
-from ..autoscaler import new_deployment_api, new_pod_autoscaler, new_sqs_api, new_sqs_client
+from ..autoscaler import SPIN_BUDGET_PPM, new_deployment_api, new_pod_autoscaler, new_sqs_api, new_sqs_client
 from ..config import TargetConfig
 from ..kube.config import RestConfig
 from ..ops import native
@@ -202,8 +202,8 @@ class BenchEnv:
     queues at one cadence do not poll in one burst. ``hot_endpoints``: every fake server is one
     busy-polling thread (HttpServer::set_hot), awake whenever a request arrives, as a loaded
     production endpoint is (supported with ``shared`` and ``process``). ``prewarm_ns``: the
-    loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_per_mille``: the share of the
-    poll period a worker may busy-poll through a slow answer (LoopConfig; the CLI's 10 = 1 %);
+    loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
+    period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
     these and ``busy_poll_ns`` may be lists, one value per queue, cycled (paired comparisons
     within one run). ``timing``: the clients time every request's
     phases (HttpTiming), traced polls carry the breakdown (``detail``), and the fakes record each
@@ -213,7 +213,7 @@ class BenchEnv:
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", log_level: str = "info", sqs_protocol: str = "query",
                  poll_period_ns: int = 0, stagger: bool = False, hot_endpoints: bool = False, prewarm_ns: int = 0,
-                 timing: bool = False, spin_budget_per_mille=10):
+                 timing: bool = False, spin_budget_ppm=None):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -285,7 +285,9 @@ class BenchEnv:
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline
             cfg.prewarm_ns = pw_q
-            cfg.spin_budget_per_mille = per_queue(spin_budget_per_mille, q)
+            # the CLI's share (autoscaler.loop_config) unless given
+            cfg.spin_budget_ppm = (SPIN_BUDGET_PPM // queues if spin_budget_ppm is None
+                                   else per_queue(spin_budget_ppm, q))
             # connect both clients when the worker starts, on its own thread (as --poll-prewarm
             # does before a poll): the on-wire GET never dials, and a dial from this thread would
             # put every worker's connection state in this thread's allocator arena, side by side

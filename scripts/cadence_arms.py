@@ -20,19 +20,23 @@ import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from kube_sqs_autoscaler_amd.autoscaler import SPIN_BUDGET_PPM  # noqa: E402
 from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, _detail_medians  # noqa: E402
 
 MS = 1_000_000
-# (prewarm ns, busy-poll ns, spin budget per mille of the period): the CLI defaults, the same
-# without the spin budget (round 3's first defaults), no warm-up, and a 300 us fixed window
-ARMS = [(200_000, 25_000, 10), (200_000, 25_000, 0), (0, 25_000, 0), (200_000, 300_000, 0)]
+# (prewarm ns, busy-poll ns, spin budget): the CLI defaults (None: the process's 1 % of the period
+# shared by its queues, autoscaler.loop_config), the same without the spin budget (round 3's first
+# defaults), no warm-up, and a 300 us fixed window
+ARMS = [(200_000, 25_000, None), (200_000, 25_000, 0), (0, 25_000, 0), (200_000, 300_000, 0)]
 
 
 def run(period_ms: int, polls: int, queues: int, skip: int = 2, timed: bool = True) -> None:
     for hot in (False, True):
         env = BenchEnv(queues, "scale", pipeline=True, busy_poll_ns=[a[1] for a in ARMS], servers="process",
                        poll_period_ns=period_ms * MS, stagger=True, hot_endpoints=hot,
-                       prewarm_ns=[a[0] for a in ARMS], spin_budget_per_mille=[a[2] for a in ARMS], timing=timed)
+                       prewarm_ns=[a[0] for a in ARMS],
+                       spin_budget_ppm=[SPIN_BUDGET_PPM // queues if a[2] is None else a[2] for a in ARMS],
+                       timing=timed)
         files = [tempfile.TemporaryFile() for _ in env.runners]
         try:
             for r, f in zip(env.runners, files):
@@ -53,7 +57,8 @@ def run(period_ms: int, polls: int, queues: int, skip: int = 2, timed: bool = Tr
             if not lat:
                 continue
             print(json.dumps({"period_ms": period_ms, "hot_endpoints": hot, "timed": timed, "prewarm_us": prewarm / 1e3,
-                              "busy_poll_us": busy / 1e3, "spin_budget_per_mille": budget, "samples": len(lat),
+                              "busy_poll_us": busy / 1e3, "spin_budget": "1%/queues" if budget is None else budget,
+                              "samples": len(lat),
                               "p50_us": round(lat[len(lat) // 2] / 1e3, 1),
                               "p90_us": round(lat[int(len(lat) * 0.9)] / 1e3, 1),
                               "depth_us": round(statistics.median(s["depth_ns"] for s in spans) / 1e3, 1),

@@ -88,3 +88,16 @@ def test_cadenced_worker_spins_through_a_slow_answer_within_its_budget(nat, peri
     assert len(sqs) >= 4
     spun = sum(1 for c in sqs if c["spun"])
     assert (spun == len(sqs)) if spins else (spun == 0), sqs
+
+
+def test_cli_queues_share_one_spin_budget(nat):
+    """autoscaler.loop_config: a process's queues share a 1 % busy-poll budget of their poll
+    period (runner.h LoopConfig.spin_budget_ppm), so a large fleet's spinning stays bounded."""
+    from kube_sqs_autoscaler_amd.autoscaler import SPIN_BUDGET_PPM, loop_config
+    from kube_sqs_autoscaler_amd.config import TargetConfig
+
+    t = TargetConfig(queue_url="https://sqs.us-east-1.amazonaws.com/1/q", deployment="d")
+    assert SPIN_BUDGET_PPM == 10_000
+    assert loop_config(t).spin_budget_ppm == 10_000
+    assert loop_config(t, queues=16).spin_budget_ppm == 625
+    assert loop_config(t, queues=64).spin_budget_ppm == 156

@@ -79,13 +79,20 @@ def test_prefetch_gate_costs_the_reference_api_reads(case):
 @given(scenarios())
 def test_pipelined_reads_keep_reference_decisions(case):
     """With API latency far below the poll period (ms vs s), overlapping the GET with the SQS
-    call changes no decision: same depth, actions and replicas at every poll."""
+    call changes no decision: same depth, actions and replicas at every poll -- up to the poll
+    where the two schedules first read different depths. A pipelined poll ends earlier, so later
+    polls start a little earlier than the sequential ones (by the overlapped GETs' latency, summed
+    over the polls so far); once that drift carries one schedule's poll across a trace boundary
+    the other does not cross yet, they sample different queues, as two reference processes
+    started a few ms apart would."""
     sc, _ = case
     if sc.params.poll_ns < 500 * MILLISECOND:
         return
     a = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency)
     b = oracle.simulate(sc.params, sc.trace, sc.names, sc.polls, sc.init_replicas, sc.latency, prefetch=True)
-    assert [e.key() for e in a] == [e.key() for e in b]
+    same = next((i for i, (x, y) in enumerate(zip(a, b)) if x.depth != y.depth), min(len(a), len(b)))
+    assert [e.key() for e in a[:same]] == [e.key() for e in b[:same]]
+    assert len(a) == len(b)
 
 
 @settings(max_examples=120, deadline=None, suppress_health_check=[HealthCheck.too_slow])
