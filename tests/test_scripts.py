@@ -1,0 +1,46 @@
+"""The evidence scripts under scripts/ stay runnable: each one on tiny settings (CPU here; the
+GPU sweep benches fall back to the CPU path when no GPU is visible)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240, env=None):
+    r = subprocess.run([sys.executable, *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, r.stderr[-2000:]
+    return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+
+
+def test_cadence_5s_script(nat):
+    rows = _run(["scripts/cadence_5s.py", "--period-ms", "60", "--queues", "2", "--polls", "4"])
+    assert [r["row"] for r in rows] == ["default", "reference_equivalent", "default_tls", "reference_equivalent_tls"]
+    assert all(r["samples"] >= 2 and r["errors"] == 0 and r["signature_failures"] == 0 for r in rows)
+
+
+def test_cadence_arms_script(nat):
+    rows = _run(["scripts/cadence_arms.py", "--period-ms", "60", "--polls", "4", "--queues", "4", "--untimed"])
+    assert len(rows) == 8  # 4 arms x (fakes that sleep, fakes that never sleep)
+    assert {r["spin_budget"] for r in rows} == {"1%/queues", 0}
+
+
+@pytest.mark.slow
+def test_soak_script_short(nat):
+    rows = _run(["scripts/soak.py", "--minutes", "0.3", "--window", "6", "--queues", "2", "--fault-every", "2"],
+                timeout=200)
+    summary = rows[-1]
+    assert summary["summary"] and summary["replay"]["mismatches"] == 0 and summary["exit_code"] == 0
+
+
+@pytest.mark.slow
+def test_sweep_bench_scripts_cpu(nat):
+    env = {"HIP_VISIBLE_DEVICES": "", "KSA_BENCH_SEGMENT_S": "300"}
+    rows = _run(["scripts/sweep_bench.py"], env=env)
+    assert any(r.get("device") == "cpu" and r["simulated_polls"] > 0 for r in rows)
+    rows = _run(["scripts/queue_sweep_bench.py"], env=env)
+    assert any(r.get("device") == "cpu" and r["lane_polls"] > 0 for r in rows)
