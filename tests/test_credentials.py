@@ -1,6 +1,5 @@
 """AWS credential chain (aws-sdk-go v1 session defaults the reference relies on, sqs/sqs.go:36)."""
 import json
-import os
 
 import pytest
 
