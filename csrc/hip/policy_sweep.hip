@@ -97,12 +97,10 @@ template <bool kMs, class T>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEEP_WAVES_PER_EU))) void sweep_kernel(
     const int64_t* __restrict__ params, int64_t m, ksa_sim::Latency lat, const T* __restrict__ g_t,
     const T* __restrict__ g_d, int32_t n, int32_t init, int64_t horizon, int64_t* __restrict__ out64,
-    int32_t* __restrict__ out32) {
-  // Dynamic LDS: 2 x sizeof(T) per segment when the trace is staged, none otherwise -- a static
-  // allocation would cap occupancy even for traces that are read from global memory.
-  constexpr int kMaxSeg = kLdsTraceBytes / (2 * static_cast<int>(sizeof(T)));
+    int32_t* __restrict__ out32, bool in_lds) {
+  // Dynamic LDS: 2 x sizeof(T) per segment when the host stages the trace (in_lds), none
+  // otherwise -- a static allocation would cap occupancy even for traces read from global memory.
   extern __shared__ int64_t s_lds[];
-  const bool in_lds = n <= kMaxSeg;
   T* s_t = reinterpret_cast<T*>(s_lds);
   T* s_d = s_t + (in_lds ? n : 0);
   if (in_lds) {
@@ -129,7 +127,10 @@ bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const
             const T* d_d, int32_t n, int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
   const int64_t want = (m + kBlock - 1) / kBlock;
   const size_t trace_bytes = 2 * static_cast<size_t>(n) * sizeof(T);
-  const size_t lds = trace_bytes <= static_cast<size_t>(kLdsTraceBytes) ? trace_bytes : 0;
+  size_t cap_bytes = kLdsTraceBytes;
+  if (const char* c = std::getenv("KSA_SWEEP_LDS_BYTES"))  // tuning knob: the staging cap (A/B)
+    cap_bytes = std::min<size_t>(static_cast<size_t>(std::max(0, std::atoi(c))), 64 * 1024);
+  const size_t lds = trace_bytes <= cap_bytes ? trace_bytes : 0;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<kMs, T>, kBlock, lds) != hipSuccess ||
       per_cu < 1)
@@ -138,7 +139,7 @@ bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const
   if (const char* g = std::getenv("KSA_SWEEP_GRID")) cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
   const int grid = static_cast<int>(want < cap ? want : cap);
   hipLaunchKernelGGL((sweep_kernel<kMs, T>), dim3(grid), dim3(kBlock), lds, ar.stream, d_p, m, lat, d_t, d_d, n, init,
-                     horizon_ns, d_o64, d_o32);
+                     horizon_ns, d_o64, d_o32, lds > 0);
   return ok(hipGetLastError(), "sweep_kernel launch");
 }
 
