@@ -31,9 +31,17 @@ constexpr int kBlock = 256;
 // Round 2 (register rate cursor + sqrt memo, 24000 x 32 lanes x 24 h): 5 waves 125.6 ms vs 4 waves
 // 131.3 ms. Round 3 (one-hash sampler, SatArith): 5 waves 109.1 ms (84 B scratch) vs 4 waves
 // 111.2 ms (122 VGPRs, none); FastArith fits 96 VGPRs at 5 waves with no scratch (68.2 ms,
-// profiles/r03h_queue).
+// profiles/r03h_queue). The millisecond-clock kernel (77 VGPRs, 6 waves at a floor of 5): a floor
+// of 7 (72 VGPRs, 12 B scratch outside the poll loop) 55.7 ms vs 61.4-62.6 ms, a floor of 8
+// (64 VGPRs, 60 B scratch) 60.1 ms (profiles/r03ai_queue_ab.jsonl).
 #ifndef KSA_QUEUE_WAVES_PER_EU
 #define KSA_QUEUE_WAVES_PER_EU 5
+#endif
+#ifndef KSA_QUEUE_FAST_WAVES_PER_EU
+#define KSA_QUEUE_FAST_WAVES_PER_EU KSA_QUEUE_WAVES_PER_EU
+#endif
+#ifndef KSA_QUEUE_MS_WAVES_PER_EU
+#define KSA_QUEUE_MS_WAVES_PER_EU 7
 #endif
 enum : int { kPoll = 0, kUpCool, kDownCool, kUpMsgs, kDownMsgs, kUpPods, kDownPods, kMaxPods, kMinPods, kNumParams };
 enum : int { kPodMs = 0, kBacklogMsgMs, kViolationMs, kPeakBacklog, kArrived, kServed, kFinalBacklog, kNumOut64 };
@@ -45,8 +53,9 @@ thread_local std::string g_queue_error;
 // ksa_sim::SatArith (T = int64_t).
 template <class A, class T, bool kMs>
 __global__ __launch_bounds__(kBlock)
-#if KSA_QUEUE_WAVES_PER_EU > 0
-__attribute__((amdgpu_waves_per_eu(KSA_QUEUE_WAVES_PER_EU)))
+#if KSA_QUEUE_WAVES_PER_EU > 0 && KSA_QUEUE_FAST_WAVES_PER_EU > 0 && KSA_QUEUE_MS_WAVES_PER_EU > 0
+__attribute__((amdgpu_waves_per_eu(kMs ? KSA_QUEUE_MS_WAVES_PER_EU
+                                       : A::kExact ? KSA_QUEUE_FAST_WAVES_PER_EU : KSA_QUEUE_WAVES_PER_EU)))
 #endif
 void queue_sweep_kernel(const int64_t* __restrict__ params, int64_t m, int32_t seeds, uint64_t seed0,
                         ksa_sim::Latency lat, ksa_sim::QueueModel model, const T* __restrict__ t_ms,

@@ -124,6 +124,7 @@ KSA_HD int64_t sample_arrivals(int64_t mean, uint64_t base, uint64_t k, int64_t*
 struct SatArith {
   using Ms = int64_t;
   static constexpr Ms kNeverMs = kNever;
+  static constexpr bool kExact = false;  // products may saturate: no reassociation
   KSA_HD static int64_t add(int64_t a, int64_t b) { return sat_add(a, b); }
   KSA_HD static int64_t mul(int64_t a, int64_t b) { return sat_mul(a, b); }
   KSA_HD static int64_t count_ms(int32_t c, Ms dt) { return sat_mul(c, dt); }
@@ -136,6 +137,7 @@ struct SatArith {
 struct FastArith {
   using Ms = uint32_t;
   static constexpr Ms kNeverMs = 0xFFFFFFFFu;
+  static constexpr bool kExact = true;  // no product reaches 2^63 (fast_path_ok): sums reassociate
   KSA_HD static int64_t add(int64_t a, int64_t b) { return a + b; }
   KSA_HD static int64_t mul(int64_t a, int64_t b) { return a * b; }
   // counts (replicas, pods) are in [0, 2^31) under fast_path_ok: one 32 x 32 -> 64 multiply
@@ -145,6 +147,14 @@ struct FastArith {
   KSA_HD static int64_t pods_rate_ms(int32_t pods, int64_t rate_milli, Ms dt) {
     const uint64_t per_pod = static_cast<uint64_t>(static_cast<uint32_t>(rate_milli)) * dt;
     return static_cast<int64_t>(static_cast<uint64_t>(static_cast<uint32_t>(pods)) * per_pod);
+  }
+  // rate x (ready x dt + pending x late) == pods_rate_ms(ready, rate, dt) +
+  // pods_rate_ms(pending, rate, late): ready + pending <= the replica bound R of fast_path_ok and
+  // late <= dt, so every partial sum and product is below rate x R x H < 2^61
+  KSA_HD static int64_t capacity(int32_t ready, Ms dt, int32_t pending, Ms late, int64_t rate_milli) {
+    const uint64_t pod_ms = static_cast<uint64_t>(static_cast<uint32_t>(ready)) * dt +
+                            static_cast<uint64_t>(static_cast<uint32_t>(pending)) * late;
+    return static_cast<int64_t>(pod_ms * static_cast<uint64_t>(static_cast<uint32_t>(rate_milli)));
   }
 };
 
@@ -231,10 +241,20 @@ KSA_HD void advance(QueueState<A>* s, QueueResult* r, const QueueModel& m, const
   s->q_micro = A::add(s->q_micro, a);
   r->arrived = A::add(r->arrived, a);
   // capacity: ready pods for the whole interval, pending ones from their ready time
-  int64_t cap = A::pods_rate_ms(s->ready, m.service_milli, dt);
-  if (s->pending > 0 && s->pending_at_ms < t1_ms) {
+  int64_t cap;
+  if constexpr (A::kExact) {
+    // one pod-milliseconds sum times the rate, the pending pods' time chosen by selects: the
+    // branch form made the gfx950 compiler copy the service step (its division by 10^6
+    // included) into both arms, and a wave whose lanes disagree on `pending` ran both
     const Ms from = s->pending_at_ms > t0_ms ? s->pending_at_ms : t0_ms;
-    cap = A::add(cap, A::pods_rate_ms(s->pending, m.service_milli, t1_ms - from));
+    const Ms late = s->pending > 0 && s->pending_at_ms < t1_ms ? t1_ms - from : 0;
+    cap = A::capacity(s->ready, dt, s->pending, late, m.service_milli);
+  } else {
+    cap = A::pods_rate_ms(s->ready, m.service_milli, dt);
+    if (s->pending > 0 && s->pending_at_ms < t1_ms) {
+      const Ms from = s->pending_at_ms > t0_ms ? s->pending_at_ms : t0_ms;
+      cap = A::add(cap, A::pods_rate_ms(s->pending, m.service_milli, t1_ms - from));
+    }
   }
   const int64_t served = s->q_micro < cap ? s->q_micro : cap;
   s->q_micro -= served;
