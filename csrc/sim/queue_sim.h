@@ -47,14 +47,29 @@ KSA_HD uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// floor(sqrt(x)), exact on CPU and GPU: a double-precision estimate (within a unit or two
-// whatever the rounding of the conversion and the sqrt) corrected with integer arithmetic. (An
-// integer Newton iteration is exact too, but each step is a 64-bit division -- a long software
-// sequence on the GPU.)
+// floor(sqrt(x)), exact on CPU and GPU: a floating-point estimate (within a few units whatever
+// the rounding of the conversion and the sqrt) corrected with integer arithmetic. (An integer
+// Newton iteration is exact too, but each step is a 64-bit division -- a long software sequence on
+// the GPU.) Below 2^48 -- every mean arrival count but absurd ones -- the estimate is single
+// precision: the two 32-bit halves converted and fused (|relative error| < 2^-23), one
+// v_sqrt_f32 (1 ulp) on gfx950, so r < 2^24 is off by at most 3 before the correction; the
+// double-precision sqrt it replaces is an rsq-and-Newton sequence of ~20 half-rate instructions
+// plus 64-bit conversions each way.
 KSA_HD uint64_t isqrt64(uint64_t x) {
   constexpr uint64_t kMax = 0xFFFFFFFFULL;  // floor(sqrt(2^64 - 1))
-  uint64_t r = static_cast<uint64_t>(__builtin_sqrt(static_cast<double>(x)));
-  if (r > kMax) r = kMax;
+  uint64_t r;
+  if (x < (uint64_t(1) << 48)) {
+    const float xf = __builtin_fmaf(static_cast<float>(static_cast<uint32_t>(x >> 32)), 4294967296.0f,
+                                    static_cast<float>(static_cast<uint32_t>(x)));
+#if defined(__HIP_DEVICE_COMPILE__)
+    r = static_cast<uint32_t>(__builtin_amdgcn_sqrtf(xf));
+#else
+    r = static_cast<uint32_t>(__builtin_sqrtf(xf));
+#endif
+  } else {
+    r = static_cast<uint64_t>(__builtin_sqrt(static_cast<double>(x)));
+    if (r > kMax) r = kMax;
+  }
   while (r * r > x) --r;
   while (r < kMax && (r + 1) * (r + 1) <= x) ++r;
   return r;
