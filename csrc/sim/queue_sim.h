@@ -106,12 +106,13 @@ KSA_HD int64_t sat_add(int64_t a, int64_t b) {
 // fields already give a normal approximation far finer than the Poisson noise it stands for.
 // sqrt(mean) is kept for the last mean (*memo_mean, *memo_sd): polls of one interval length inside
 // one rate segment -- most of them -- ask for the same mean, and the isqrt is the longest sequence
-// of the poll on the GPU. `base` is seed * kSeedMul, taken once per lane.
+// of the poll on the GPU. `key` is seed * kSeedMul + the draw's index: QueueState::key, one
+// 64-bit counter per lane (a separate base and index held two).
 constexpr int64_t kSqrt3Q16 = 113512;  // round(sqrt(3) * 2^16)
 constexpr uint64_t kSeedMul = 0xD1B54A32D192ED03ULL;
-KSA_HD int64_t sample_arrivals(int64_t mean, uint64_t base, uint64_t k, int64_t* memo_mean, int64_t* memo_sd) {
+KSA_HD int64_t sample_arrivals(int64_t mean, uint64_t key, int64_t* memo_mean, int64_t* memo_sd) {
   if (mean <= 0) return 0;
-  const uint64_t w = mix64(base + k);
+  const uint64_t w = mix64(key);
   // the four 16-bit fields, summed in two 32-bit lanes (2 x 65535 fits), then folded
   constexpr uint64_t kM = 0x0000FFFF0000FFFFULL;
   const uint64_t lanes = (w & kM) + ((w >> 16) & kM);
@@ -233,7 +234,7 @@ struct QueueState {
   int64_t q_msgs;        // q_micro / 1e6, kept current (the depth SQS reports)
   int32_t ready, pending;
   typename A::Ms pending_at_ms;  // when the pending pods start draining
-  uint64_t draws;
+  uint64_t key;  // the next draw's counter: seed * kSeedMul + draws so far
   int64_t memo_mean, memo_sd;  // sample_arrivals' last mean and its sd (memo_mean -1: none yet)
 };
 
@@ -242,7 +243,7 @@ struct QueueState {
 // backlog and replicas at the start of the interval (left Riemann sum, as policy_sim.h).
 template <class A, class T>
 KSA_HD void advance(QueueState<A>* s, QueueResult* r, const QueueModel& m, const T* t_ms, const T* rate_milli,
-                    int32_t n, RateCursor<A, T>* cur, uint64_t base, typename A::Ms t0_ms, typename A::Ms t1_ms,
+                    int32_t n, RateCursor<A, T>* cur, typename A::Ms t0_ms, typename A::Ms t1_ms,
                     int32_t replicas) {
   using Ms = typename A::Ms;
   if (t1_ms <= t0_ms) return;
@@ -252,7 +253,7 @@ KSA_HD void advance(QueueState<A>* s, QueueResult* r, const QueueModel& m, const
   r->backlog_msg_ms = A::add(r->backlog_msg_ms, A::mul(q0, dt));
   if (q0 > m.slo_backlog) r->violation_ms += dt;
   const int64_t mean = expected_arrivals(t_ms, rate_milli, n, cur, t0_ms, t1_ms);
-  const int64_t a = sample_arrivals(mean, base, s->draws++, &s->memo_mean, &s->memo_sd);
+  const int64_t a = sample_arrivals(mean, s->key++, &s->memo_mean, &s->memo_sd);
   s->q_micro = A::add(s->q_micro, a);
   r->arrived = A::add(r->arrived, a);
   // capacity: ready pods for the whole interval, pending ones from their ready time
@@ -297,10 +298,9 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
   s.ready = init_replicas;
   s.pending = 0;
   s.pending_at_ms = 0;
-  s.draws = 0;
+  s.key = seed * kSeedMul;
   s.memo_mean = -1;
   s.memo_sd = 0;
-  const uint64_t base = seed * kSeedMul;
   RateCursor<A, T> cur = rate_cursor_init<A>(t_ms, rate_milli, n);
   int64_t now = 0, last_up = 0, last_down = 0;  // main.go:37-38
   int32_t replicas = init_replicas;
@@ -334,7 +334,7 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
     if (t_poll > horizon_ns) break;
     carry(period_ms, period_sub);
     const Ms t_poll_ms = now_ms;
-    advance(&s, &res, m, t_ms, rate_milli, n, &cur, base, prev_ms, t_poll_ms, replicas);
+    advance(&s, &res, m, t_ms, rate_milli, n, &cur, prev_ms, t_poll_ms, replicas);
     prev_ms = t_poll_ms;
     now = t_poll;
     res.polls++;
@@ -362,7 +362,7 @@ KSA_HD QueueResult simulate_queue(const Params& p, const Latency& lat, const Que
     if (replicas > res.max_replicas) res.max_replicas = replicas;
     if (s.q_msgs > res.peak_backlog) res.peak_backlog = s.q_msgs;
   }
-  if (horizon_ms > prev_ms) advance(&s, &res, m, t_ms, rate_milli, n, &cur, base, prev_ms, horizon_ms, replicas);
+  if (horizon_ms > prev_ms) advance(&s, &res, m, t_ms, rate_milli, n, &cur, prev_ms, horizon_ms, replicas);
   res.final_replicas = replicas;
   res.final_backlog = s.q_msgs;
   res.arrived /= 1000000;
@@ -394,10 +394,9 @@ KSA_HD QueueResult simulate_queue_ms(const Params& p, const Latency& lat_ns, con
   s.ready = init_replicas;
   s.pending = 0;
   s.pending_at_ms = 0;
-  s.draws = 0;
+  s.key = seed * kSeedMul;
   s.memo_mean = -1;
   s.memo_sd = 0;
-  const uint64_t base = seed * kSeedMul;
   RateCursor<A, T> cur = rate_cursor_init<A>(t_ms, rate_milli, n);
   const int64_t startup_ms = udiv_1e6(m.startup_ns);  // >= 0 under fast_path_ok
   int32_t now = 0, last_up = 0, last_down = 0;  // main.go:37-38
@@ -408,7 +407,7 @@ KSA_HD QueueResult simulate_queue_ms(const Params& p, const Latency& lat_ns, con
   while (advances && res.polls < kMaxPolls) {
     const int32_t t_poll = now + k.period;  // main.go:41 sleep, then poll
     if (t_poll > horizon_ms) break;
-    advance(&s, &res, m, t_ms, rate_milli, n, &cur, base, static_cast<Ms>(prev), static_cast<Ms>(t_poll), replicas);
+    advance(&s, &res, m, t_ms, rate_milli, n, &cur, static_cast<Ms>(prev), static_cast<Ms>(t_poll), replicas);
     prev = t_poll;
     now = t_poll;
     res.polls++;
@@ -435,7 +434,7 @@ KSA_HD QueueResult simulate_queue_ms(const Params& p, const Latency& lat_ns, con
     if (s.q_msgs > res.peak_backlog) res.peak_backlog = s.q_msgs;
   }
   if (horizon_ms > prev)
-    advance(&s, &res, m, t_ms, rate_milli, n, &cur, base, static_cast<Ms>(prev), static_cast<Ms>(horizon_ms), replicas);
+    advance(&s, &res, m, t_ms, rate_milli, n, &cur, static_cast<Ms>(prev), static_cast<Ms>(horizon_ms), replicas);
   res.final_replicas = replicas;
   res.final_backlog = s.q_msgs;
   res.arrived /= 1000000;
