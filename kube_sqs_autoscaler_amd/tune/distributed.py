@@ -4,12 +4,18 @@ Extension (an operator tool, like the rest of :mod:`kube_sqs_autoscaler_amd.tune
 ``torchrun`` (``python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m
 kube_sqs_autoscaler_amd.tune --distributed ...``). Every rank:
 
-1. takes a contiguous slice of the configuration grid (near-equal sizes, so the ranks finish
-   together: every configuration of a grid simulates the same horizon);
+1. takes a cost-balanced share of the configuration grid (:func:`shard_plan`). A lane's work is
+   the number of polls it simulates, horizon / (poll period + SQS latency), so on a grid with
+   poll periods 1 s..10 s the 1 s configurations cost ten times the 10 s ones: equal-count
+   slices of the poll-sorted grid would leave the rank holding the shortest periods running
+   long after the others. Configurations are dealt out in cost order so every rank's summed
+   :func:`sweep.estimated_polls` is within a few % of the mean, and each rank's share stays
+   poll-sorted (neighbouring lanes of a wave share loop trip counts);
 2. runs it on its own GPU (``LOCAL_RANK``) with the same kernel a single-GPU sweep uses, or on
    CPU threads;
-3. all-gathers the per-configuration outputs over ``torch.distributed``. The backend is
-   ``nccl`` (RCCL over xGMI on an MI355X node) when the GPUs run the sweep, ``gloo`` on CPU.
+3. all-gathers the per-configuration outputs over ``torch.distributed`` and scatters them back
+   into grid order. The backend is ``nccl`` (RCCL over xGMI on an MI355X node) when the GPUs
+   run the sweep, ``gloo`` on CPU.
 
 The outputs are a few dozen bytes per configuration: every field is packed into one int64
 row per configuration, so a sweep makes one all-gather (plus one all-reduce of the kernel
@@ -26,11 +32,29 @@ import numpy as np
 from . import closedloop, sweep
 
 
-def shard_bounds(m: int, rank: int, world: int) -> Tuple[int, int]:
-    """Contiguous slice [lo, hi) of m configurations for `rank`; sizes differ by at most one."""
-    base, extra = divmod(m, world)
-    lo = rank * base + min(rank, extra)
-    return lo, lo + base + (1 if rank < extra else 0)
+def config_costs(params: np.ndarray, horizon_ns: int, latency_ns: Tuple[int, int, int]) -> np.ndarray:
+    """Per-configuration simulated polls (the unit :func:`sweep.estimated_polls` sums): the work
+    of one lane is proportional to it, whatever its other parameters."""
+    step = np.maximum(np.maximum(params[0], 0) + latency_ns[0], 1)
+    return np.minimum(horizon_ns // step, 1 << 26).astype(np.int64)
+
+
+def shard_plan(costs: np.ndarray, world: int) -> List[np.ndarray]:
+    """Splits configurations 0..m-1 over `world` ranks so the per-rank cost sums are balanced.
+
+    Configurations are sorted by decreasing cost (ties in grid order) and dealt out in a snake
+    order, 0, 1, ..., w-1, w-1, ..., 1, 0, 0, 1, ...: within every round of `world` the rank that
+    took the most expensive configuration takes the cheapest of the next round. Every rank gets
+    the same number of configurations (+-1), and its cost sum is within about one configuration's
+    cost of the mean. Each rank's index array comes out in decreasing-cost (= increasing poll)
+    order, so lanes next to each other in a wave run similar trip counts. The plan depends only
+    on the costs, so every rank computes the same one."""
+    m = len(costs)
+    order = np.lexsort((np.arange(m), -np.asarray(costs, dtype=np.int64)))
+    pos = np.arange(m)
+    rnd, k = np.divmod(pos, world)
+    ranks = np.where(rnd % 2 == 0, k, world - 1 - k)
+    return [order[ranks == r] for r in range(world)]
 
 
 class Group:
@@ -115,24 +139,37 @@ class Group:
         return float(t.item())
 
 
-def _shards(g: Group, m: int) -> Tuple[Tuple[int, int], List[int]]:
-    bounds = [shard_bounds(m, r, g.world) for r in range(g.world)]
-    return bounds[g.rank], [hi - lo for lo, hi in bounds]
+def _shards(g: Group, params: np.ndarray, horizon_ns: int,
+            latency_ns: Tuple[int, int, int]) -> Tuple[np.ndarray, List[int], np.ndarray]:
+    """This rank's configuration indices, every rank's count, and the rank-major concatenation
+    of all ranks' indices (row i of the all-gathered output belongs to configuration
+    ``gathered_order[i]``)."""
+    plan = shard_plan(config_costs(params, horizon_ns, latency_ns), g.world)
+    return plan[g.rank], [len(p) for p in plan], np.concatenate(plan) if plan else np.zeros(0, np.int64)
+
+
+def _to_grid_order(full: Dict[str, np.ndarray], gathered_order: np.ndarray) -> Dict[str, np.ndarray]:
+    res = {}
+    for k, v in full.items():
+        out = np.empty_like(v)
+        out[gathered_order] = v
+        res[k] = out
+    return res
 
 
 def run_open_loop(g: Group, trace: sweep.Trace, params: np.ndarray, init_replicas: int, horizon_ns: int,
                   latency_ns: Tuple[int, int, int]) -> sweep.SweepResult:
     """:func:`sweep.run` over the whole grid, sharded over the group's ranks."""
     params = np.ascontiguousarray(params, dtype=np.int64)
-    (lo, hi), counts = _shards(g, params.shape[1])
-    part = params[:, lo:hi]
-    if hi > lo:
-        res = sweep.run(trace, part, init_replicas, horizon_ns, latency_ns, g.device, gpu_index=g.local_rank)
+    mine, counts, order = _shards(g, params, horizon_ns, latency_ns)
+    if len(mine):
+        res = sweep.run(trace, np.ascontiguousarray(params[:, mine]), init_replicas, horizon_ns, latency_ns, g.device,
+                        gpu_index=g.local_rank)
         out, kernel_ms, ns_clock = res.out, res.kernel_ms, not res.ms_clock
     else:  # more ranks than configurations
         out = {k: np.zeros(0, dtype=np.int64 if k in sweep.OUT64 else np.int32) for k in sweep.OUT64 + sweep.OUT32}
         kernel_ms, ns_clock = 0.0, False
-    full = g.all_gather_fields(out, counts)
+    full = _to_grid_order(g.all_gather_fields(out, counts), order)
     # ms_clock: every shard ran the millisecond clock
     return sweep.SweepResult(params, full, g.device, g.max(kernel_ms), g.max(float(ns_clock)) == 0.0)
 
@@ -143,16 +180,16 @@ def run_closed_loop(g: Group, trace: closedloop.ArrivalTrace, params: np.ndarray
     """:func:`closedloop.run` over the whole grid, sharded over the group's ranks. Seeds are
     common to all configurations, so every shard draws the same arrival sequences."""
     params = np.ascontiguousarray(params, dtype=np.int64)
-    (lo, hi), counts = _shards(g, params.shape[1])
-    if hi > lo:
-        res = closedloop.run(trace, params[:, lo:hi], model, init_replicas, horizon_ns, latency_ns, seeds, seed0,
-                             g.device, gpu_index=g.local_rank)
+    mine, counts, order = _shards(g, params, horizon_ns, latency_ns)
+    if len(mine):
+        res = closedloop.run(trace, np.ascontiguousarray(params[:, mine]), model, init_replicas, horizon_ns, latency_ns,
+                             seeds, seed0, g.device, gpu_index=g.local_rank)
         out, kernel_ms, flags = res.out, res.kernel_ms, (res.fast_arith, res.ms_clock)
     else:
         out = {k: np.zeros((0, seeds), dtype=np.int64 if k in closedloop.OUT64 else np.int32)
                for k in closedloop.OUT64 + closedloop.OUT32}
         kernel_ms, flags = 0.0, (True, True)
-    full = g.all_gather_fields(out, counts)
+    full = _to_grid_order(g.all_gather_fields(out, counts), order)
     # fast_arith / ms_clock: every shard ran it
     fast, ms_clock = (g.max(float(not f)) == 0.0 for f in flags)
     return closedloop.ClosedLoopResult(params, seeds, full, g.device, horizon_ns, g.max(kernel_ms), fast, ms_clock)

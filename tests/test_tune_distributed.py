@@ -9,18 +9,43 @@ import sys
 
 import pytest
 
-from kube_sqs_autoscaler_amd.tune.distributed import shard_bounds
+import numpy as np
+
+from kube_sqs_autoscaler_amd.tune import sweep
+from kube_sqs_autoscaler_amd.tune.distributed import config_costs, shard_plan
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+S = 1_000_000_000
 
 
 @pytest.mark.parametrize("m,world", [(10, 3), (3, 8), (0, 2), (1000, 8), (7, 1)])
-def test_shard_bounds_partition(m, world):
-    bounds = [shard_bounds(m, r, world) for r in range(world)]
-    assert bounds[0][0] == 0 and bounds[-1][1] == m
-    assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
-    sizes = [hi - lo for lo, hi in bounds]
+def test_shard_plan_partitions_the_grid(m, world):
+    costs = np.random.default_rng(m).integers(1, 100, size=m)
+    plan = shard_plan(costs, world)
+    assert len(plan) == world
+    assert sorted(np.concatenate(plan).tolist()) == list(range(m))
+    sizes = [len(p) for p in plan]
     assert max(sizes) - min(sizes) <= 1
+    for p in plan:  # each share in decreasing-cost order, ties in grid order
+        assert all((costs[a], -a) >= (costs[b], -b) for a, b in zip(p, p[1:]))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_shard_plan_balances_cost_over_poll_periods(world):
+    """A lane's work is horizon / poll period: on a 1 s..10 s grid (poll outermost) equal-count
+    contiguous slices put ~10x the polls on rank 0 as on the last rank; the plan keeps the
+    per-rank cost sums within 10 % of each other."""
+    params = sweep.grid(poll_ns=[k * S for k in range(1, 11)], up_cool_ns=[0, 30 * S, 60 * S, 120 * S],
+                        up_msgs=[50, 100, 200], max_pods=[4, 8])
+    horizon, lat = 3600 * S, (1_000_000, 1_000_000, 1_000_000)
+    costs = config_costs(params, horizon, lat)
+    assert costs.sum() == sweep.estimated_polls(params, horizon, lat)
+    loads = [int(costs[p].sum()) for p in shard_plan(costs, world)]
+    assert max(loads) / min(loads) <= 1.1, loads
+    # what equal-count contiguous slices (the round-3 split) would have given
+    bounds = np.linspace(0, len(costs), world + 1).astype(int)
+    naive = [int(costs[a:b].sum()) for a, b in zip(bounds, bounds[1:])]
+    assert max(naive) / min(naive) > 2
 
 
 def _free_port():
@@ -46,24 +71,27 @@ def _run(args, world=None):
 def test_open_loop_three_ranks_equal_single_process(tmp_path):
     csv = tmp_path / "depth.csv"
     csv.write_text("seconds,depth\n" + "".join(f"{i * 5},{(i * 37) % 400}\n" for i in range(300)))
-    args = ["--trace", str(csv), "--device", "cpu", "--json", "--top", "0", "--grid", "scale-up-cool-down=0s:2m:20s",
-            "--grid", "scale-up-messages=50,100,200,400", "--grid", "max-pods=4,8,16"]  # 7 x 4 x 3 = 84 configs
+    # poll periods vary, so the cost-balanced plan interleaves the grid over the ranks and the
+    # gathered rows must be scattered back into grid order
+    args = ["--trace", str(csv), "--device", "cpu", "--json", "--top", "0", "--grid", "poll-period=1s,5s,10s",
+            "--grid", "scale-up-cool-down=0s:2m:20s", "--grid", "scale-up-messages=50,100,200,400",
+            "--grid", "max-pods=4,8,16"]  # 3 x 7 x 4 x 3 = 252 configs
     info1, rows1 = _run(args)
     info3, rows3 = _run(args, world=3)
     assert info3["ranks"] == 3 and info1["ranks"] == 1
-    assert info1["configs"] == info3["configs"] == 84
-    assert rows1 == rows3 and len(rows1) == 84
+    assert info1["configs"] == info3["configs"] == 252
+    assert rows1 == rows3 and len(rows1) == 252
 
 
 def test_closed_loop_two_ranks_equal_single_process(tmp_path):
     csv = tmp_path / "rate.csv"
     csv.write_text("seconds,msgs_per_second\n0,2\n600,30\n1200,2\n")
     args = ["--arrivals", str(csv), "--horizon", "40m", "--service-rate", "5", "--seeds", "6", "--device", "cpu",
-            "--json", "--top", "0", "--grid", "scale-up-cool-down=0s:4m:1m", "--grid", "max-pods=2,8,9"]
+            "--json", "--top", "0", "--grid", "scale-up-cool-down=0s:4m:1m", "--grid", "max-pods=2,8,9", "--grid", "poll-period=2s,7s"]
     info1, rows1 = _run(args)
     info2, rows2 = _run(args, world=2)
-    assert info2["ranks"] == 2 and info1["configs"] == info2["configs"] == 15
-    assert rows1 == rows2 and len(rows1) == 15
+    assert info2["ranks"] == 2 and info1["configs"] == info2["configs"] == 30
+    assert rows1 == rows2 and len(rows1) == 30
 
 
 def test_group_refuses_to_start_after_the_kernels_library(monkeypatch):
