@@ -21,6 +21,11 @@ median): p50 at 1/2/4/8 tracked queues with the default thread-per-queue fleet a
 sequential and reference-equivalent paths, TLS, a regional-RTT model, per-phase medians,
 wire-path decision parity and apiserver requests per poll on the Appendix C traces.
 
+Launch: ``python bench.py --gpus N`` with N > 1 outside a launcher starts the N ranks itself
+(child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set,
+before the parent touches torch or the GPU) and exits with the first failing rank's status;
+under ``torchrun`` the launcher's WORLD_SIZE must equal ``--gpus`` (exit 2 otherwise).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--queues Q] [--mode scale]
 """
 from __future__ import annotations
@@ -128,7 +133,61 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     }
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int, argv: list, script: str = __file__) -> int:
+    """Runs this script as ranks 0..n-1 of one job, one child process per rank (one GPU each).
+    Called before anything in this process imports torch or touches a GPU, and it never execs:
+    the parent only waits. Rank 0 inherits stdout, so its JSON line is the job's; the other
+    ranks' stdout goes to stderr. When a rank fails the others are stopped (they would block in
+    the next collective) and the first failure's exit status is returned."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(script), *argv], env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    _progress(f"rank {procs.index(p)} exited with status {code}; stopping the other ranks")
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            if live:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
@@ -155,7 +214,21 @@ def main(argv=None) -> int:
                     help="seconds after start past which the remaining secondary sections and cadence rows are skipped "
                          "(recorded under extra.skipped_sections); the headline line is always printed")
     args = ap.parse_args(argv)
+    if args.gpus < 1 or args.queues < 1:
+        ap.error("--gpus and --queues must be at least 1")
+    if "WORLD_SIZE" in os.environ:  # under torchrun (or a rank of _launch_ranks)
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} "
+                  "ranks", file=sys.stderr)
+            return 2
+    elif args.gpus > 1:
+        return _launch_ranks(args.gpus, argv)
     t_start = time.monotonic()
+    # stdout carries the one result line: what libraries print on fd 1 (gloo's "[Gloo] Rank 0 is
+    # connected ..." during rendezvous, RCCL/HIP notices) goes to stderr instead
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -352,7 +425,7 @@ def main(argv=None) -> int:
             },
             "extra": extra,
         }
-        print(json.dumps(out), flush=True)
+        os.write(result_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -15,6 +15,14 @@ def _json_line(stdout):
     return json.loads(lines[0])
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _check(out, n, steps, warmup):
     assert out["metric"].startswith("poll") and out["unit"] == "ms" and out["higher_is_better"] is False
     assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
@@ -36,12 +44,52 @@ def test_bench_two_ranks_gloo():
     env = dict(os.environ)
     env["CUDA_VISIBLE_DEVICES"] = ""  # CPU ranks: gloo backend
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29611", "bench.py", "--gpus", "2", "--steps", "150",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--steps", "150",
                         "--warmup", "10"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     out = _json_line(r.stdout)
     _check(out, 2, 150, 10)
     assert out["extra"]["tracked_queues"] == 2
+
+
+def test_bench_launches_its_own_ranks_without_a_launcher():
+    """`python bench.py --gpus 3` (what the driver runs on one node, no torchrun) starts three
+    ranks itself over gloo here (RCCL on GPUs), and rank 0's line covers all three."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--steps", "50", "--warmup", "5", "--no-sweep"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(r.stdout.splitlines()) == 1, r.stdout  # gloo's rendezvous chatter goes to stderr
+    out = _json_line(r.stdout)
+    _check(out, 3, 50, 5)
+    assert out["extra"]["tracked_queues"] == 3 and out["config"]["global_batch"] == 3
+
+
+def test_bench_refuses_a_launcher_world_that_differs_from_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "5"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""
+
+
+def test_rank_launcher_stops_the_job_when_one_rank_fails(tmp_path):
+    """A failing rank ends the job with its status; a rank still waiting (in a collective, here
+    a sleep) is stopped rather than left to hang the launch."""
+    import time
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1':\n    sys.exit(3)\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "time.sleep(120)\n")
+    t0 = time.monotonic()
+    assert bench._launch_ranks(3, [], script=str(script)) == 3
+    assert time.monotonic() - t0 < 30
 
 
 def test_bench_prints_its_line_when_secondary_sections_run_out_of_time():
