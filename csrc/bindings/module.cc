@@ -6,7 +6,9 @@
 // (/root/reference/sqs/sqs.go:14-18) and typedappv1.DeploymentInterface
 // (/root/reference/scale/scale.go:22) -- are exposed as subclassable base classes
 // (SqsApi, DeploymentApi), so Python fakes plug into the native loop exactly like the
-// reference's Go mocks plug into Run().
+// reference's Go mocks plug into Run(). The native fakes (localhost endpoints, in-memory
+// MockSqsApi / FakeDeployments) are a separate module, _ksa_fakes (fakes_module.cc), that tests,
+// benchmarks and the parity harness load; this one is what the image ships.
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -15,7 +17,6 @@
 
 #include "../core/clock.h"
 #include "../core/exec_auth.h"
-#include "../core/fakes.h"
 #include "../core/goutil.h"
 #include "../core/http.h"
 #include "../core/json.h"
@@ -186,7 +187,7 @@ Headers headers_from(const py::object& o) {
 }  // namespace
 
 PYBIND11_MODULE(_ksa_native, m) {
-  m.doc() = "Native runtime of the MI355X SQS autoscaler (control loop, SigV4, HTTP, fakes).";
+  m.doc() = "Native runtime of the MI355X SQS autoscaler (control loop, SigV4, HTTP/TLS, SQS + kube clients).";
   g_native_error = py::reinterpret_borrow<py::object>(
       PyErr_NewException("kube_sqs_autoscaler_amd.ops._ksa_native.NativeError", PyExc_RuntimeError, nullptr));
   m.attr("NativeError") = g_native_error;
@@ -409,13 +410,6 @@ PYBIND11_MODULE(_ksa_native, m) {
     Url u = unwrap(parse_url(s));
     return py::make_tuple(u.scheme, u.host, u.port, u.path);
   });
-  m.def("generate_self_signed", [](const std::string& host) {
-    std::string c, k;
-    Status s = generate_self_signed(host, &c, &k);
-    if (!s.ok()) raise_status(s);
-    return py::make_tuple(c, k);
-  });
-
   // ---- SQS ----
   m.def("default_attribute_names", &default_attribute_names);
   py::enum_<SqsProtocol>(m, "SqsProtocol").value("Query", SqsProtocol::Query).value("Json", SqsProtocol::Json);
@@ -460,15 +454,6 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["http"] = http_stats_dict(s.http);
         return d;
       });
-  py::class_<MockSqsApi, SqsApi, py::smart_holder>(m, "MockSqsApi")
-      .def(py::init<AttrMap>(), py::arg("attributes") = AttrMap{})
-      .def("set_attributes", &MockSqsApi::set_attributes)
-      .def("set_latency", &MockSqsApi::set_latency)
-      .def("fail_next", &MockSqsApi::fail_next)
-      .def("calls", &MockSqsApi::calls);
-  py::class_<TraceSqsApi, SqsApi, py::smart_holder>(m, "TraceSqsApi")
-      .def(py::init<std::shared_ptr<Clock>, std::vector<std::pair<Nanos, AttrMap>>, Nanos>(),
-           py::arg("clock"), py::arg("segments"), py::arg("per_call_latency_ns") = 0);
   py::class_<SqsClient, std::shared_ptr<SqsClient>>(m, "SqsClient")
       .def(py::init<std::shared_ptr<SqsApi>, std::string, std::vector<std::string>>(), py::arg("api"),
            py::arg("queue_url"), py::arg("attribute_names"))
@@ -645,20 +630,6 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["http"] = http_stats_dict(s.http);
         return d;
       });
-  py::class_<FakeDeployments, DeploymentApi, py::smart_holder>(m, "FakeDeployments")
-      .def(py::init<std::string>(), py::arg("namespace") = "namespace")
-      .def("add", &FakeDeployments::add)
-      .def("add_without_replicas", &FakeDeployments::add_without_replicas)
-      .def("replicas", &FakeDeployments::replicas)
-      .def("set_replicas", &FakeDeployments::set_replicas)
-      .def("set_latency", &FakeDeployments::set_latency)
-      .def("fail_next_get", &FakeDeployments::fail_next_get)
-      .def("fail_next_update", &FakeDeployments::fail_next_update)
-      .def("conflict_next", &FakeDeployments::conflict_next)
-      .def("enable_pipelining", &FakeDeployments::enable_pipelining)
-      .def("gets", &FakeDeployments::gets)
-      .def("updates", &FakeDeployments::updates);
-
   py::class_<ScaleSpan>(m, "ScaleSpan")
       .def_readonly("get_ns", &ScaleSpan::get_ns)
       .def_readonly("update_ns", &ScaleSpan::update_ns)
@@ -942,101 +913,6 @@ PYBIND11_MODULE(_ksa_native, m) {
         py::arg("t_ms"), py::arg("rate_milli"), py::arg("init_replicas"), py::arg("horizon_ns"), py::arg("latency"),
         py::arg("model"), py::arg("params"), py::arg("seeds"), py::arg("seed0") = 1, py::arg("threads") = 8,
         py::arg("arith") = 0);
-
-  // ---- fakes ----
-  py::class_<InjectedFault>(m, "InjectedFault")
-      .def(py::init([](int status, std::string body, std::string ct, bool drop, std::string retry_after,
-                       std::string method) {
-             InjectedFault f;
-             f.status = status;
-             f.body = std::move(body);
-             f.content_type = std::move(ct);
-             f.drop_connection = drop;
-             f.retry_after = std::move(retry_after);
-             f.method = std::move(method);
-             return f;
-           }),
-           py::arg("status") = 500, py::arg("body") = "", py::arg("content_type") = "text/plain",
-           py::arg("drop_connection") = false, py::arg("retry_after") = "", py::arg("method") = "");
-
-  py::class_<FakeSqsServer, std::shared_ptr<FakeSqsServer>>(m, "FakeSqsServer")
-      .def(py::init<>())
-      .def("require_signature", &FakeSqsServer::require_signature)
-      .def("start",
-           [](FakeSqsServer& s, const std::string& host, int port, bool tls) {
-             Status st = s.start(host, port, tls);
-             if (!st.ok()) raise_status(st);
-           },
-           py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("tls") = false)
-      .def("stop", &FakeSqsServer::stop, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("port", &FakeSqsServer::port)
-      .def_property_readonly("url", &FakeSqsServer::url)
-      .def_property_readonly("cert_pem", &FakeSqsServer::cert_pem)
-      .def("set_attributes", &FakeSqsServer::set_attributes)
-      .def("set_default_attributes", &FakeSqsServer::set_default_attributes)
-      .def("set_attribute_cycle", &FakeSqsServer::set_attribute_cycle)
-      .def("inject", &FakeSqsServer::inject)
-      .def("set_latency", &FakeSqsServer::set_latency)
-      .def("set_cpus", &FakeSqsServer::set_cpus)
-      .def("set_hot", &FakeSqsServer::set_hot)
-      .def("set_timing", &FakeSqsServer::set_timing)
-      .def("drop_connections", &FakeSqsServer::drop_connections)
-      .def("requests", &FakeSqsServer::requests)
-      .def("signature_failures", &FakeSqsServer::signature_failures)
-      .def("connections", &FakeSqsServer::connections)
-      .def("timings", [](const FakeSqsServer& s) {
-        std::vector<std::pair<int64_t, int64_t>> out;
-        for (auto& t : s.timings()) out.emplace_back(t.wake_ns, t.service_ns);
-        return out;
-      })
-      .def("clear_timings", &FakeSqsServer::clear_timings)
-      .def("last_body", &FakeSqsServer::last_body)
-      .def("last_headers", &FakeSqsServer::last_headers);
-
-  py::class_<FakeKubeServer, std::shared_ptr<FakeKubeServer>>(m, "FakeKubeServer")
-      .def(py::init<>())
-      .def("require_token", &FakeKubeServer::require_token)
-      .def("start",
-           [](FakeKubeServer& s, const std::string& host, int port, bool tls) {
-             Status st = s.start(host, port, tls);
-             if (!st.ok()) raise_status(st);
-           },
-           py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("tls") = false)
-      .def("stop", &FakeKubeServer::stop, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("port", &FakeKubeServer::port)
-      .def_property_readonly("url", &FakeKubeServer::url)
-      .def_property_readonly("cert_pem", &FakeKubeServer::cert_pem)
-      .def("add_deployment", &FakeKubeServer::add_deployment)
-      .def("replicas", &FakeKubeServer::replicas)
-      .def("set_replicas", &FakeKubeServer::set_replicas)
-      .def("deployment_json", &FakeKubeServer::deployment_json)
-      .def("lease_json", &FakeKubeServer::lease_json)
-      .def("add_node", &FakeKubeServer::add_node, py::arg("name"), py::arg("labels"), py::arg("resource"),
-           py::arg("gpus"), py::arg("unschedulable") = false)
-      .def("inject", &FakeKubeServer::inject)
-      .def("conflict_next", &FakeKubeServer::conflict_next)
-      .def("set_rbac", &FakeKubeServer::set_rbac)
-      .def("forbidden", &FakeKubeServer::forbidden)
-      .def("set_latency", &FakeKubeServer::set_latency)
-      .def("set_cpus", &FakeKubeServer::set_cpus)
-      .def("set_hot", &FakeKubeServer::set_hot)
-      .def("set_timing", &FakeKubeServer::set_timing)
-      .def("drop_connections", &FakeKubeServer::drop_connections)
-      .def("requests", &FakeKubeServer::requests)
-      .def("gets", &FakeKubeServer::gets)
-      .def("writes", &FakeKubeServer::writes)
-      .def("conflicts", &FakeKubeServer::conflicts)
-      .def("auth_failures", &FakeKubeServer::auth_failures)
-      .def("connections", &FakeKubeServer::connections)
-      .def("timings", [](const FakeKubeServer& s) {
-        std::vector<std::pair<int64_t, int64_t>> out;
-        for (auto& t : s.timings()) out.emplace_back(t.wake_ns, t.service_ns);
-        return out;
-      })
-      .def("clear_timings", &FakeKubeServer::clear_timings)
-      .def("last_method", &FakeKubeServer::last_method)
-      .def("last_body", &FakeKubeServer::last_body)
-      .def("last_path", &FakeKubeServer::last_path);
 
   m.attr("SECOND") = kSecond;
   m.attr("MILLISECOND") = kMillisecond;

@@ -1,4 +1,4 @@
-#include "http.h"
+#include "http_wire.h"
 
 #include "affinity.h"
 #include "goutil.h"
@@ -33,373 +33,9 @@
 
 namespace ksa {
 
-namespace {
-// OpenSSL writes through a socket BIO (plain write(2)), so a peer that closes mid-stream would
-// raise SIGPIPE and kill a process that has not ignored it (Python does; a C++ embedder may not).
-// Like Go's runtime, ignore SIGPIPE process-wide -- only if nobody installed a handler -- and
-// let the write fail with EPIPE instead. Plain sockets additionally use MSG_NOSIGNAL.
-void ignore_sigpipe_once() {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    struct sigaction cur;
-    if (sigaction(SIGPIPE, nullptr, &cur) == 0 && cur.sa_handler == SIG_DFL) signal(SIGPIPE, SIG_IGN);
-  });
-}
-}  // namespace
-
+using namespace wire;
 
 namespace {
-
-std::string lower(std::string s) {
-  for (auto& c : s) c = ascii_lower(c);
-  return s;
-}
-
-bool iequals(const std::string& a, const std::string& b) {
-  if (a.size() != b.size()) return false;
-  for (size_t i = 0; i < a.size(); ++i)
-    if (ascii_lower(a[i]) != ascii_lower(b[i])) return false;
-  return true;
-}
-
-std::string trim(const std::string& s) {
-  size_t b = 0, e = s.size();
-  while (b < e && (s[b] == ' ' || s[b] == '\t')) ++b;
-  while (e > b && (s[e - 1] == ' ' || s[e - 1] == '\t' || s[e - 1] == '\r')) --e;
-  return s.substr(b, e - b);
-}
-
-std::string header_of(const Headers& hs, const std::string& name) {
-  for (auto& [k, v] : hs)
-    if (iequals(k, name)) return v;
-  return "";
-}
-
-bool has_header(const Headers& hs, const std::string& name) {
-  for (auto& kv : hs)
-    if (iequals(kv.first, name)) return true;
-  return false;
-}
-
-// Case-insensitive "does `hay` contain `needle`" (needle given in lower case), no copies.
-bool icontains(const std::string& hay, const char* needle) {
-  const size_t n = std::strlen(needle);
-  if (n > hay.size()) return false;
-  for (size_t i = 0; i + n <= hay.size(); ++i) {
-    size_t k = 0;
-    while (k < n && ascii_lower(hay[i + k]) == needle[k]) ++k;
-    if (k == n) return true;
-  }
-  return false;
-}
-
-const std::string* header_ptr(const Headers& hs, const char* name, size_t len) {
-  for (auto& [k, v] : hs) {
-    if (k.size() != len) continue;
-    size_t i = 0;
-    while (i < len && ascii_lower(k[i]) == ascii_lower(name[i])) ++i;
-    if (i == len) return &v;
-  }
-  return nullptr;
-}
-
-std::string ssl_error_string() {
-  unsigned long e = ERR_get_error();
-  if (!e) return "unknown TLS error";
-  char buf[256];
-  ERR_error_string_n(e, buf, sizeof buf);
-  ERR_clear_error();
-  return buf;
-}
-
-// Waits for `events` on fd until the absolute deadline (0 = forever). A readable `cancel_fd`
-// (HttpClient::cancel) ends the wait with "request canceled".
-Status wait_fd(int fd, short events, int64_t deadline_ns, int cancel_fd = -1) {
-  while (true) {
-    int timeout_ms = -1;
-    if (deadline_ns) {
-      int64_t left = deadline_ns - mono_ns();
-      if (left <= 0) return Status::Err("i/o timeout");
-      timeout_ms = static_cast<int>((left + 999999) / 1000000);
-    }
-    struct pollfd p[2] = {{fd, events, 0}, {cancel_fd, POLLIN, 0}};
-    int r = ::poll(p, cancel_fd >= 0 ? 2 : 1, timeout_ms);
-    if (r > 0 && cancel_fd >= 0 && (p[1].revents & POLLIN)) return Status::Err("request canceled");
-    if (r > 0) return Status::OK();
-    if (r == 0) {
-      if (deadline_ns && mono_ns() >= deadline_ns) return Status::Err("i/o timeout");
-      continue;
-    }
-    if (errno == EINTR) continue;
-    return Status::Err(std::string("poll: ") + std::strerror(errno));
-  }
-}
-
-// A non-blocking socket, optionally wrapped in TLS, with deadline-bounded I/O. Cache-line
-// aligned, as Conn: the streams of different workers' clients never share a line, whichever
-// thread dialled them.
-class alignas(kCacheLine) Stream {
- public:
-  Stream(int fd, SSL* ssl) : fd_(fd), ssl_(ssl) {}
-  ~Stream() {
-    if (ssl_) {
-      SSL_shutdown(ssl_);
-      SSL_free(ssl_);
-    }
-    if (outer_) {
-      SSL_shutdown(outer_);
-      SSL_free(outer_);
-    }
-    if (fd_ >= 0) ::close(fd_);
-  }
-  int fd() const { return fd_; }
-
-  // Drives an SSL_* call that may want read/write readiness.
-  template <class F>
-  Status ssl_op(F op, int64_t deadline_ns, int* out, const char* what) {
-    int64_t spin_end = 0;
-    bool spin_over = false;
-    // SSL_get_error reads the thread's error queue, so it must start empty. A WANT_READ /
-    // WANT_WRITE result queues nothing: the busy-poll retries skip the clear (OpenSSL 3 resets
-    // all 16 queue slots per call, the largest cost of a TLS spin iteration in the r02q
-    // profile) unless something is queued after all.
-    ERR_clear_error();
-    for (int i = 0;; ++i) {
-      if (i > 0 && ERR_peek_error() != 0) ERR_clear_error();
-      int r = op();
-      if (r > 0) {
-        *out = r;
-        return Status::OK();
-      }
-      int e = SSL_get_error(ssl_, r);
-      if (e == SSL_ERROR_WANT_READ) {
-        // Busy-poll applies to TLS too: retry the operation itself (a non-blocking read of the
-        // socket underneath) for up to spin_ns_, so the call that sees the record's bytes also
-        // decrypts them; then sleep in poll(2).
-        if (spin_ns_ > 0 && !spin_over) {
-          if (spin_end == 0) spin_end = mono_ns() + spin_ns_;
-          if ((i & 7) != 7 || mono_ns() < spin_end) {
-#if defined(__x86_64__)
-            __builtin_ia32_pause();
-#endif
-            continue;
-          }
-          spin_over = true;
-        }
-        Status s = wait_fd(fd_, POLLIN, deadline_ns, cancel_fd_);
-        if (!s.ok()) return s;
-      } else if (e == SSL_ERROR_WANT_WRITE) {
-        Status s = wait_fd(fd_, POLLOUT, deadline_ns, cancel_fd_);
-        if (!s.ok()) return s;
-      } else if (e == SSL_ERROR_ZERO_RETURN) {
-        *out = 0;
-        return Status::OK();
-      } else if (e == SSL_ERROR_SYSCALL && ERR_peek_error() == 0) {
-        *out = 0;  // unexpected EOF: treat as connection closed
-        return Status::OK();
-      } else {
-        return Status::Err(std::string(what) + ": " + ssl_error_string());
-      }
-    }
-  }
-
-  Status handshake(bool server, int64_t deadline_ns) {
-    int out = 0;
-    if (server) return ssl_op([&] { return SSL_accept(ssl_); }, deadline_ns, &out, "tls accept");
-    Status s = ssl_op([&] { return SSL_connect(ssl_); }, deadline_ns, &out, "tls handshake");
-    if (s.ok() && out == 0) return Status::Err("tls handshake: connection closed");
-    return s;
-  }
-
-  // Appends what is available (at least one byte) to buf. *eof on orderly close.
-  Status read_some(std::string* buf, int64_t deadline_ns, bool* eof) {
-    char tmp[16384];
-    *eof = false;
-    if (ssl_) {
-      int n = 0;
-      Status s = ssl_op([&] { return SSL_read(ssl_, tmp, sizeof tmp); }, deadline_ns, &n, "tls read");
-      if (!s.ok()) return s;
-      if (n == 0) *eof = true;
-      else buf->append(tmp, static_cast<size_t>(n));
-      if (n > 0 && first_.armed) {
-        first_.armed = false;
-        first_.seen = mono_ns();
-      }
-      return Status::OK();
-    }
-    while (true) {
-      ssize_t n = recv_some(tmp, sizeof tmp);
-      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK) && spin_ns_ > 0) {
-        n = spin_recv(tmp, sizeof tmp);
-        if (n > 0 && first_.armed) first_.spun = true;
-      }
-      if (n > 0) {
-        if (first_.armed) {
-          first_.armed = false;
-          first_.seen = mono_ns();
-          first_.rx_real = pending_rx_real_;
-        }
-        buf->append(tmp, static_cast<size_t>(n));
-        return Status::OK();
-      }
-      if (n == 0) {
-        *eof = true;
-        return Status::OK();
-      }
-      if (errno == EINTR) continue;
-      if (errno == EAGAIN || errno == EWOULDBLOCK) {
-        Status s = wait_fd(fd_, POLLIN, deadline_ns, cancel_fd_);
-        if (!s.ok()) return s;
-        continue;
-      }
-      if (errno == ECONNRESET) {
-        *eof = true;
-        return Status::Err("connection reset by peer");
-      }
-      return Status::Err(std::string("read: ") + std::strerror(errno));
-    }
-  }
-
-  Status write_all(const std::string& data, int64_t deadline_ns, size_t* written = nullptr) {
-    size_t off = 0;
-    struct Report {
-      size_t* w;
-      size_t& off;
-      ~Report() {
-        if (w) *w = off;
-      }
-    } report{written, off};
-    while (off < data.size()) {
-      if (ssl_) {
-        int n = 0;
-        Status s = ssl_op(
-            [&] { return SSL_write(ssl_, data.data() + off, static_cast<int>(data.size() - off)); },
-            deadline_ns, &n, "tls write");
-        if (!s.ok()) return s;
-        if (n == 0) return Status::Err("write: connection closed");
-        off += static_cast<size_t>(n);
-        continue;
-      }
-      ssize_t n = ::send(fd_, data.data() + off, data.size() - off, MSG_NOSIGNAL);
-      if (n > 0) {
-        off += static_cast<size_t>(n);
-        continue;
-      }
-      if (n < 0 && errno == EINTR) continue;
-      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        Status s = wait_fd(fd_, POLLOUT, deadline_ns, cancel_fd_);
-        if (!s.ok()) return s;
-        continue;
-      }
-      return Status::Err(std::string("write: ") + std::strerror(errno));
-    }
-    return Status::OK();
-  }
-
-  // An idle keep-alive connection about to be reused: has the peer closed it (FIN, RST, a TLS
-  // close_notify) or sent something unsolicited? Go's transport learns this from the idle
-  // connection's read loop and dials a new one instead of writing into a dead socket; here the
-  // socket is peeked without blocking. TLS records that carry no application data (session
-  // tickets) are consumed by the peek and leave the connection usable.
-  bool peer_closed() {
-    if (ssl_) {
-      char c;
-      ERR_clear_error();
-      const int n = SSL_peek(ssl_, &c, 1);
-      if (n > 0) return true;  // unsolicited response bytes: the connection is out of sync
-      const int e = SSL_get_error(ssl_, n);
-      return !(e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE);
-    }
-    char c;
-    while (true) {
-      const ssize_t n = ::recv(fd_, &c, 1, MSG_PEEK | MSG_DONTWAIT);
-      if (n >= 0) return true;  // 0: orderly close; > 0: unsolicited bytes
-      if (errno == EINTR) continue;
-      return !(errno == EAGAIN || errno == EWOULDBLOCK);
-    }
-  }
-
-  void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
-  void set_cancel_fd(int fd) { cancel_fd_ = fd; }
-  // First-bytes timing of the next response (HttpClient::set_timing): arm before reading it;
-  // the first read that gets data stamps when this thread saw it and, on a plain socket with
-  // receive timestamps on, the kernel's receive time (CLOCK_REALTIME) of those bytes.
-  struct FirstBytes {
-    bool armed = false;
-    bool spun = false;
-    int64_t seen = 0;
-    int64_t rx_real = 0;
-  };
-  void enable_rx_timestamps() {
-    int on = 1;
-    ts_ = setsockopt(fd_, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
-  }
-  void arm_first_bytes() { first_ = FirstBytes{true, false, 0, 0}; }
-  const FirstBytes& first_bytes() const { return first_; }
-  SSL* ssl() const { return ssl_; }
-  void attach_ssl(SSL* ssl) { ssl_ = ssl; }  // TLS inside an established CONNECT tunnel
-  // TLS inside TLS (an https origin behind an https proxy): `inner` becomes the session the
-  // stream reads and writes; its BIO (tunnel_bio) carries its records through the current one.
-  void push_ssl(SSL* inner) {
-    outer_ = ssl_;
-    ssl_ = inner;
-  }
-
- private:
-  // Busy-poll on a plain socket: keep reading (non-blocking) for up to spin_ns_ before sleeping
-  // in poll(2). A response that lands within the window is picked up without a scheduler
-  // wake-up (several microseconds on every round trip), and by the same system call that sees
-  // it; past the window the thread blocks as usual, so idle waits cost no CPU.
-  // Returns recv's result; -1 with errno EAGAIN when the window passed without data.
-  ssize_t spin_recv(char* out, size_t cap) {
-    const int64_t end = mono_ns() + spin_ns_;
-    for (int i = 0;; ++i) {
-      const ssize_t n = recv_some(out, cap);
-      if (n >= 0) return n;
-      if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) return n;
-      if ((i & 15) == 15 && mono_ns() >= end) {
-        errno = EAGAIN;
-        return -1;
-      }
-#if defined(__x86_64__)
-      __builtin_ia32_pause();
-#endif
-    }
-  }
-
-  // recv(2), or recvmsg(2) with the receive timestamp while first-bytes timing is armed.
-  ssize_t recv_some(char* out, size_t cap) {
-    if (!(ts_ && first_.armed)) return ::recv(fd_, out, cap, 0);
-    struct iovec iov = {out, cap};
-    alignas(struct cmsghdr) char ctrl[CMSG_SPACE(sizeof(struct timespec))];
-    struct msghdr msg = {};
-    msg.msg_iov = &iov;
-    msg.msg_iovlen = 1;
-    msg.msg_control = ctrl;
-    msg.msg_controllen = sizeof ctrl;
-    const ssize_t n = ::recvmsg(fd_, &msg, 0);
-    if (n > 0) {
-      pending_rx_real_ = 0;
-      for (struct cmsghdr* cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
-        if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_TIMESTAMPNS) {
-          struct timespec ts;
-          std::memcpy(&ts, CMSG_DATA(cm), sizeof ts);
-          pending_rx_real_ = static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
-        }
-      }
-    }
-    return n;
-  }
-
-  int fd_;
-  SSL* ssl_;
-  SSL* outer_ = nullptr;  // the proxy's TLS session when ssl_ runs inside it
-  int64_t spin_ns_ = 0;
-  int cancel_fd_ = -1;
-  bool ts_ = false;
-  FirstBytes first_;
-  int64_t pending_rx_real_ = 0;
-};
 
 // BIO carrying one TLS session's records inside another (the https-proxy tunnel). Non-blocking
 // like the socket under it: when the outer session needs socket readiness the BIO reports a
@@ -451,212 +87,6 @@ BIO* tunnel_bio(SSL* outer) {
   return b;
 }
 
-// Largest message body either side accepts. Scale objects and Deployments are a few KiB and a
-// NodeList of a large cluster a few tens of MiB; a peer announcing more (or a chunked /
-// read-to-EOF body that keeps growing) is cut off instead of exhausting the 200 MiB pod.
-constexpr size_t kMaxBody = 128u << 20;
-
-// Incremental HTTP/1.1 message framing over a Stream with a carry-over buffer.
-class Reader {
- public:
-  Reader(Stream* s, std::string* buf) : s_(s), buf_(buf) {}
-
-  // Reads through the blank line; returns the head (without the terminator).
-  Status read_head(std::string* head, int64_t deadline_ns, bool* got_any) {
-    *got_any = !buf_->empty();
-    while (true) {
-      size_t p = buf_->find("\r\n\r\n");
-      if (p != std::string::npos) {
-        head->assign(*buf_, 0, p);
-        buf_->erase(0, p + 4);
-        return Status::OK();
-      }
-      if (buf_->size() > 1 << 20) return Status::Err("header too large");
-      bool eof = false;
-      Status s = s_->read_some(buf_, deadline_ns, &eof);
-      if (!s.ok()) return s;
-      if (eof) return Status::Err(buf_->empty() ? "EOF" : "unexpected EOF");
-      *got_any = true;
-    }
-  }
-
-  Status read_exact(size_t n, std::string* out, int64_t deadline_ns) {
-    if (n > kMaxBody || out->size() + n > kMaxBody) return Status::Err("message body too large");
-    while (buf_->size() < n) {
-      bool eof = false;
-      Status s = s_->read_some(buf_, deadline_ns, &eof);
-      if (!s.ok()) return s;
-      if (eof) return Status::Err("unexpected EOF");
-    }
-    out->append(*buf_, 0, n);
-    buf_->erase(0, n);
-    return Status::OK();
-  }
-
-  Status read_line(std::string* line, int64_t deadline_ns) {
-    while (true) {
-      size_t p = buf_->find("\r\n");
-      if (p != std::string::npos) {
-        line->assign(*buf_, 0, p);
-        buf_->erase(0, p + 2);
-        return Status::OK();
-      }
-      if (buf_->size() > 1 << 20) return Status::Err("line too long");
-      bool eof = false;
-      Status s = s_->read_some(buf_, deadline_ns, &eof);
-      if (!s.ok()) return s;
-      if (eof) return Status::Err("unexpected EOF");
-    }
-  }
-
-  Status read_chunked(std::string* out, int64_t deadline_ns) {
-    while (true) {
-      std::string line;
-      Status s = read_line(&line, deadline_ns);
-      if (!s.ok()) return s;
-      size_t semi = line.find(';');
-      std::string hex = trim(semi == std::string::npos ? line : line.substr(0, semi));
-      if (hex.empty()) return Status::Err("malformed chunk size");
-      char* end = nullptr;
-      errno = 0;
-      unsigned long long n = std::strtoull(hex.c_str(), &end, 16);
-      if (*end != '\0' || errno == ERANGE) return Status::Err("malformed chunk size");
-      if (n > kMaxBody || out->size() + n > kMaxBody) return Status::Err("message body too large");
-      if (n == 0) {
-        // trailers until blank line
-        while (true) {
-          std::string t;
-          s = read_line(&t, deadline_ns);
-          if (!s.ok()) return s;
-          if (t.empty()) return Status::OK();
-        }
-      }
-      s = read_exact(static_cast<size_t>(n), out, deadline_ns);
-      if (!s.ok()) return s;
-      std::string crlf;
-      s = read_line(&crlf, deadline_ns);
-      if (!s.ok()) return s;
-    }
-  }
-
-  Status read_to_eof(std::string* out, int64_t deadline_ns) {
-    out->append(*buf_);
-    buf_->clear();
-    while (true) {
-      bool eof = false;
-      std::string tmp;
-      Status s = s_->read_some(&tmp, deadline_ns, &eof);
-      if (!s.ok()) return s;
-      if (eof) return Status::OK();
-      if (out->size() + tmp.size() > kMaxBody) return Status::Err("message body too large");
-      out->append(tmp);
-    }
-  }
-
- private:
-  Stream* s_;
-  std::string* buf_;
-};
-
-// Header lines as Go's textproto.Reader.ReadMIMEHeader reads them (net/http, client and server):
-// "Name: value", a line starting with a space or tab continues the previous value (obs-fold),
-// and a line without a colon -- or a continuation with nothing to continue -- is a protocol error
-// ("malformed MIME header line"); *bad gets the line. Spans are trimmed in place: one string per
-// name and per value, nothing else allocated.
-bool parse_header_lines(const std::string& head, size_t from, Headers* out, std::string* bad) {
-  auto trimmed = [&](size_t b, size_t e) {
-    while (b < e && (head[b] == ' ' || head[b] == '\t')) ++b;
-    while (e > b && (head[e - 1] == ' ' || head[e - 1] == '\t' || head[e - 1] == '\r')) --e;
-    return std::string(head, b, e - b);
-  };
-  size_t pos = from;
-  const size_t first = out->size();
-  while (pos < head.size()) {
-    size_t e = head.find("\r\n", pos);
-    if (e == std::string::npos) e = head.size();
-    if (e > pos && (head[pos] == ' ' || head[pos] == '\t')) {
-      if (out->size() == first) {  // "malformed MIME header initial line"
-        *bad = head.substr(pos, e - pos);
-        return false;
-      }
-      std::string more = trimmed(pos, e);
-      if (!more.empty()) {
-        std::string& v = out->back().second;
-        if (!v.empty()) v.push_back(' ');
-        v += more;
-      }
-    } else if (e > pos) {
-      const char* colon = static_cast<const char*>(std::memchr(head.data() + pos, ':', e - pos));
-      if (!colon) {
-        *bad = head.substr(pos, e - pos);
-        return false;
-      }
-      const size_t c = static_cast<size_t>(colon - head.data());
-      out->emplace_back(trimmed(pos, c), trimmed(c + 1, e));
-    }
-    pos = e + 2;
-  }
-  return true;
-}
-
-bool wants_close(const Headers& hs, bool http10) {
-  const std::string* c = header_ptr(hs, "Connection", 10);
-  if (c && icontains(*c, "close")) return true;
-  if (http10 && !(c && icontains(*c, "keep-alive"))) return true;
-  return false;
-}
-
-bool is_chunked(const Headers& hs) {
-  const std::string* t = header_ptr(hs, "Transfer-Encoding", 17);
-  return t && icontains(*t, "chunked");
-}
-
-struct SslInit {
-  SslInit() { OPENSSL_init_ssl(0, nullptr); }
-};
-void ensure_ssl() { static SslInit once; }
-
-Status load_ca_pem(SSL_CTX* ctx, const std::string& pem) {
-  BIO* bio = BIO_new_mem_buf(pem.data(), static_cast<int>(pem.size()));
-  X509_STORE* store = SSL_CTX_get_cert_store(ctx);
-  int added = 0;
-  while (X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr)) {
-    X509_STORE_add_cert(store, x);
-    X509_free(x);
-    ++added;
-  }
-  ERR_clear_error();
-  BIO_free(bio);
-  if (!added) return Status::Err("no certificates found in CA data");
-  return Status::OK();
-}
-
-Status use_cert_key(SSL_CTX* ctx, const std::string& cert_pem, const std::string& key_pem) {
-  BIO* cb = BIO_new_mem_buf(cert_pem.data(), static_cast<int>(cert_pem.size()));
-  X509* cert = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr);
-  if (!cert) {
-    BIO_free(cb);
-    return Status::Err("invalid certificate PEM: " + ssl_error_string());
-  }
-  int ok = SSL_CTX_use_certificate(ctx, cert);
-  X509_free(cert);
-  // Remaining certificates form the chain.
-  while (X509* extra = PEM_read_bio_X509(cb, nullptr, nullptr, nullptr)) {
-    SSL_CTX_add_extra_chain_cert(ctx, extra);  // takes ownership
-  }
-  ERR_clear_error();
-  BIO_free(cb);
-  if (ok != 1) return Status::Err("SSL_CTX_use_certificate: " + ssl_error_string());
-  BIO* kb = BIO_new_mem_buf(key_pem.data(), static_cast<int>(key_pem.size()));
-  EVP_PKEY* key = PEM_read_bio_PrivateKey(kb, nullptr, nullptr, nullptr);
-  BIO_free(kb);
-  if (!key) return Status::Err("invalid private key PEM: " + ssl_error_string());
-  ok = SSL_CTX_use_PrivateKey(ctx, key);
-  EVP_PKEY_free(key);
-  if (ok != 1) return Status::Err("SSL_CTX_use_PrivateKey: " + ssl_error_string());
-  return Status::OK();
-}
-
 std::string percent_decode(const std::string& in) {
   std::string out;
   for (size_t i = 0; i < in.size(); ++i) {
@@ -679,10 +109,6 @@ std::string base64(const std::string& in) {
   return out;
 }
 
-bool is_ip_literal(const std::string& h) {
-  unsigned char buf[16];
-  return inet_pton(AF_INET, h.c_str(), buf) == 1 || inet_pton(AF_INET6, h.c_str(), buf) == 1;
-}
 
 // getaddrinfo(3) has no timeout, so a stuck resolver would hold a worker far past
 // --api-timeout (Go's dialer bounds the lookup by the request's context). Names are resolved on
@@ -1537,544 +963,4 @@ bool HttpClient::in_flight() const {
   std::lock_guard<std::mutex> lk(mu_);
   return in_flight_;
 }
-
-// ---------------------------------------------------------------------------------------
-// Server
-
-HttpServer::HttpServer(Handler h) : handler_(std::move(h)) {}
-
-HttpServer::~HttpServer() {
-  stop();
-  if (ctx_) SSL_CTX_free(ctx_);
-}
-
-Status HttpServer::enable_tls(const std::string& cert_pem, const std::string& key_pem) {
-  ensure_ssl();
-  ignore_sigpipe_once();
-  ctx_ = SSL_CTX_new(TLS_server_method());
-  if (!ctx_) return Status::Err("SSL_CTX_new: " + ssl_error_string());
-  return use_cert_key(ctx_, cert_pem, key_pem);
-}
-
-Status HttpServer::listen(const std::string& host, int port) {
-  struct addrinfo hints;
-  std::memset(&hints, 0, sizeof hints);
-  hints.ai_family = AF_UNSPEC;
-  hints.ai_socktype = SOCK_STREAM;
-  hints.ai_flags = AI_PASSIVE;
-  struct addrinfo* res = nullptr;
-  std::string p = std::to_string(port);
-  if (getaddrinfo(host.c_str(), p.c_str(), &hints, &res) != 0) return Status::Err("bad listen address " + host);
-  int fd = ::socket(res->ai_family, res->ai_socktype | SOCK_CLOEXEC, res->ai_protocol);
-  if (fd < 0) {
-    freeaddrinfo(res);
-    return Status::Err(std::string("socket: ") + std::strerror(errno));
-  }
-  int one = 1;
-  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-  // with timing on from the start, accepted sockets inherit receive stamps from the listener:
-  // a client's first request can arrive before its connection thread runs
-  if (timing_.load(std::memory_order_relaxed)) setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
-  if (::bind(fd, res->ai_addr, res->ai_addrlen) != 0 || ::listen(fd, 128) != 0) {
-    std::string e = std::strerror(errno);
-    ::close(fd);
-    freeaddrinfo(res);
-    return Status::Err("listen " + host + ":" + p + ": " + e);
-  }
-  freeaddrinfo(res);
-  struct sockaddr_storage ss;
-  socklen_t len = sizeof ss;
-  getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len);
-  port_ = ss.ss_family == AF_INET6 ? ntohs(reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port)
-                                   : ntohs(reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
-  listen_fd_ = fd;
-  acceptor_ = std::thread([this] {
-    pthread_setname_np(pthread_self(), hot_ ? "ksa-serve-hot" : "ksa-accept");
-    pin_current_thread(cpus_);
-    if (hot_) hot_loop();
-    else accept_loop();
-  });
-  return Status::OK();
-}
-
-void HttpServer::accept_loop() {
-  while (!stopping_.load()) {
-    int fd = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
-    if (fd < 0) {
-      if (errno == EINTR || errno == ECONNABORTED) continue;
-      break;  // listener shut down
-    }
-    if (stopping_.load()) {
-      ::close(fd);
-      break;
-    }
-    int one = 1;
-    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-    accepted_++;
-    std::vector<std::thread> finished;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      for (auto it = workers_.begin(); it != workers_.end();) {
-        if (it->done->load(std::memory_order_acquire)) {
-          finished.push_back(std::move(it->thread));
-          it = workers_.erase(it);
-        } else {
-          ++it;
-        }
-      }
-      open_fds_.push_back(fd);
-      auto done = std::make_shared<std::atomic<bool>>(false);
-      workers_.push_back(Worker{std::thread([this, fd, done] {
-                                  pthread_setname_np(pthread_self(), "ksa-serve");
-                                  pin_current_thread(cpus_);
-                                  serve(fd);
-                                  done->store(true, std::memory_order_release);
-                                }),
-                                done});
-    }
-    for (auto& t : finished) t.join();  // already returned (or about to): no blocking
-  }
-}
-
-namespace {
-int64_t realtime_ns() {
-  struct timespec ts;
-  clock_gettime(CLOCK_REALTIME, &ts);
-  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
-}
-
-// Blocks until `fd` is readable; returns the kernel receive time (CLOCK_REALTIME ns) of the
-// first queued byte, 0 when the socket reports none (closed, or timestamps unavailable).
-int64_t wait_rx_timestamp(int fd) {
-  struct pollfd p = {fd, POLLIN, 0};
-  while (::poll(&p, 1, -1) < 0 && errno == EINTR) {
-  }
-  char c;
-  struct iovec iov = {&c, 1};
-  alignas(struct cmsghdr) char ctrl[CMSG_SPACE(sizeof(struct timespec))];
-  struct msghdr msg = {};
-  msg.msg_iov = &iov;
-  msg.msg_iovlen = 1;
-  msg.msg_control = ctrl;
-  msg.msg_controllen = sizeof ctrl;
-  if (::recvmsg(fd, &msg, MSG_PEEK | MSG_DONTWAIT) <= 0) return 0;
-  for (struct cmsghdr* cm = CMSG_FIRSTHDR(&msg); cm; cm = CMSG_NXTHDR(&msg, cm)) {
-    if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_TIMESTAMPNS) {
-      struct timespec ts;
-      std::memcpy(&ts, CMSG_DATA(cm), sizeof ts);
-      return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
-    }
-  }
-  return 0;
-}
-}  // namespace
-
-void HttpServer::record_timing(ServeTiming t) {
-  std::lock_guard<std::mutex> lk(timing_mu_);
-  constexpr size_t kKeep = 1 << 16;
-  if (timings_.size() < kKeep) {
-    timings_.push_back(t);
-  } else {
-    timings_[timing_pos_] = t;
-    timing_pos_ = (timing_pos_ + 1) % kKeep;
-  }
-}
-
-std::vector<HttpServer::ServeTiming> HttpServer::timings() const {
-  std::lock_guard<std::mutex> lk(timing_mu_);
-  return timings_;
-}
-
-void HttpServer::clear_timings() {
-  std::lock_guard<std::mutex> lk(timing_mu_);
-  timings_.clear();
-  timing_pos_ = 0;
-}
-
-void HttpServer::serve(int fd) {
-  SSL* ssl = nullptr;
-  if (ctx_) {
-    ssl = SSL_new(ctx_);
-    SSL_set_fd(ssl, fd);
-  }
-  int fl = fcntl(fd, F_GETFL, 0);
-  fcntl(fd, F_SETFL, fl | O_NONBLOCK);
-  {
-    Stream stream(fd, ssl);
-    bool ok = true;
-    if (ssl) ok = stream.handshake(true, mono_ns() + 10 * kSecond).ok();
-    std::string rbuf;
-    Reader rd(&stream, &rbuf);
-    // receive stamps from the first request on when timing is already on (a socket stamps only
-    // the segments queued after the option is set); else from the first request after it is
-    bool stamps = false, stamps_tried = false;
-    auto arm_stamps = [&] {
-      int on = 1;
-      stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
-      stamps_tried = true;
-    };
-    if (timing_.load(std::memory_order_relaxed)) arm_stamps();
-    while (ok && !stopping_.load()) {
-      // With timing on: the next request's arrival, its kernel receive time and when this
-      // thread got to it.
-      int64_t rx = 0, t_read = 0;
-      if (timing_.load(std::memory_order_relaxed)) {
-        if (!stamps_tried) arm_stamps();
-        if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd);
-        t_read = realtime_ns();
-      }
-      std::string head;
-      bool got_any = false;
-      if (!rd.read_head(&head, 0, &got_any).ok()) break;
-      HttpRequest req;
-      size_t eol = head.find("\r\n");
-      std::string line = head.substr(0, eol);
-      size_t a = line.find(' '), b = line.rfind(' ');
-      if (a == std::string::npos || b == a) break;
-      req.method = line.substr(0, a);
-      req.target = line.substr(a + 1, b - a - 1);
-      // absolute-form (what clients send to a proxy; servers must accept it): keep path+query
-      if (req.target.compare(0, 7, "http://") == 0 || req.target.compare(0, 8, "https://") == 0) {
-        const size_t slash = req.target.find_first_of("/?", req.target.find("://") + 3);
-        req.target = slash == std::string::npos ? "/" : req.target.substr(slash);
-        if (req.target[0] == '?') req.target = "/" + req.target;
-      }
-      const bool http10 = line.compare(b + 1, 8, "HTTP/1.0") == 0;
-      std::string bad;
-      if (eol != std::string::npos && !parse_header_lines(head, eol + 2, &req.headers, &bad)) {
-        // net/http's server answers a malformed header with 400 and closes the connection
-        const std::string msg = "400 Bad Request: malformed MIME header line: " + bad;
-        stream.write_all("HTTP/1.1 400 Bad Request\r\nContent-Type: text/plain; charset=utf-8\r\n"
-                         "Connection: close\r\nContent-Length: " + std::to_string(msg.size()) + "\r\n\r\n" + msg,
-                         mono_ns() + kSecond);
-        break;
-      }
-      Status s;
-      if (is_chunked(req.headers)) {
-        s = rd.read_chunked(&req.body, 0);
-      } else if (!req.header("Content-Length").empty()) {
-        long long n = std::atoll(req.header("Content-Length").c_str());
-        if (n < 0 || n > (64LL << 20)) break;
-        s = rd.read_exact(static_cast<size_t>(n), &req.body, 0);
-      }
-      if (!s.ok()) break;
-      HttpResponse resp;
-      resp.status = 200;
-      handler_(req, &resp);
-      bool close_after = wants_close(req.headers, http10) || resp.status < 0;
-      if (resp.status < 0) break;  // handler asked to drop the connection without replying
-      std::string wire = "HTTP/1.1 " + std::to_string(resp.status) + " " +
-                         (resp.reason.empty() ? http_reason(resp.status) : resp.reason) + "\r\n";
-      for (auto& [k, v] : resp.headers) wire += k + ": " + v + "\r\n";
-      if (!has_header(resp.headers, "Content-Length")) {
-        wire += "Content-Length: ";
-        wire += std::to_string(resp.body.size());
-        wire += "\r\n";
-      }
-      if (close_after) wire += "Connection: close\r\n";
-      wire += "\r\n";
-      wire += resp.body;
-      if (!stream.write_all(wire, mono_ns() + 10 * kSecond).ok()) break;
-      served_++;
-      if (rx > 0) record_timing(ServeTiming{std::max<int64_t>(t_read - rx, 0), realtime_ns() - t_read});
-      if (close_after) break;
-    }
-    std::lock_guard<std::mutex> lk(mu_);
-    open_fds_.erase(std::remove(open_fds_.begin(), open_fds_.end(), fd), open_fds_.end());
-  }  // Stream dtor closes fd (after removal from open_fds_, so no fd-reuse race)
-}
-
-namespace {
-
-// One complete request at the front of `buf`: parses it into *req and returns the bytes it
-// took; 0 while incomplete; -1 for a request this server cannot take (malformed, chunked).
-long take_request(const std::string& buf, HttpRequest* req, bool* http10) {
-  const size_t end = buf.find("\r\n\r\n");
-  if (end == std::string::npos) return buf.size() > (64u << 10) ? -1 : 0;
-  const size_t eol = buf.find("\r\n");
-  const std::string line = buf.substr(0, eol);
-  const size_t a = line.find(' '), b = line.rfind(' ');
-  if (a == std::string::npos || b == a) return -1;
-  req->method = line.substr(0, a);
-  req->target = line.substr(a + 1, b - a - 1);
-  *http10 = line.compare(b + 1, 8, "HTTP/1.0") == 0;
-  req->headers.clear();
-  std::string bad;
-  const std::string head = buf.substr(0, end + 4);
-  if (!parse_header_lines(head, eol + 2, &req->headers, &bad)) return -1;
-  if (is_chunked(req->headers)) return -1;
-  size_t n = 0;
-  if (!req->header("Content-Length").empty()) {
-    const long long cl = std::atoll(req->header("Content-Length").c_str());
-    if (cl < 0 || cl > (64LL << 20)) return -1;
-    n = static_cast<size_t>(cl);
-  }
-  if (buf.size() < end + 4 + n) return 0;
-  req->body.assign(buf, end + 4, n);
-  return static_cast<long>(end + 4 + n);
-}
-
-std::string response_wire(const HttpResponse& resp, bool close_after) {
-  std::string wire = "HTTP/1.1 " + std::to_string(resp.status) + " " +
-                     (resp.reason.empty() ? http_reason(resp.status) : resp.reason) + "\r\n";
-  for (auto& [k, v] : resp.headers) wire += k + ": " + v + "\r\n";
-  if (!has_header(resp.headers, "Content-Length")) {
-    wire += "Content-Length: ";
-    wire += std::to_string(resp.body.size());
-    wire += "\r\n";
-  }
-  if (close_after) wire += "Connection: close\r\n";
-  wire += "\r\n";
-  wire += resp.body;
-  return wire;
-}
-
-}  // namespace
-
-void HttpServer::hot_loop() {
-  struct Conn {
-    int fd = -1;
-    SSL* ssl = nullptr;
-    bool handshaken = false;
-    bool stamps = false, stamps_tried = false;
-    std::string rbuf;
-  };
-  const int ep = epoll_create1(EPOLL_CLOEXEC);
-  if (ep < 0) return;
-  fcntl(listen_fd_, F_SETFL, fcntl(listen_fd_, F_GETFL, 0) | O_NONBLOCK);
-  struct epoll_event lev = {};
-  lev.events = EPOLLIN;
-  lev.data.fd = listen_fd_;
-  epoll_ctl(ep, EPOLL_CTL_ADD, listen_fd_, &lev);
-  std::map<int, Conn> conns;
-  auto drop = [&](int fd) {
-    auto it = conns.find(fd);
-    if (it == conns.end()) return;
-    epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
-    if (it->second.ssl) SSL_free(it->second.ssl);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      open_fds_.erase(std::remove(open_fds_.begin(), open_fds_.end(), fd), open_fds_.end());
-    }
-    ::close(fd);
-    conns.erase(it);
-  };
-  struct epoll_event evs[64];
-  while (!stopping_.load(std::memory_order_relaxed)) {
-    const int n = epoll_wait(ep, evs, 64, 0);  // busy-polled: this thread never sleeps
-    for (int i = 0; i < n; ++i) {
-      const int fd = evs[i].data.fd;
-      if (fd == listen_fd_) {
-        for (;;) {
-          const int c = ::accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
-          if (c < 0) break;
-          int one = 1;
-          setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-          accepted_++;
-          Conn cn;
-          cn.fd = c;
-          if (timing_.load(std::memory_order_relaxed)) {
-            cn.stamps = setsockopt(c, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one) == 0;
-            cn.stamps_tried = true;
-          }
-          if (ctx_) {
-            cn.ssl = SSL_new(ctx_);
-            SSL_set_fd(cn.ssl, c);
-          } else {
-            cn.handshaken = true;
-          }
-          conns[c] = std::move(cn);
-          {
-            std::lock_guard<std::mutex> lk(mu_);
-            open_fds_.push_back(c);
-          }
-          struct epoll_event ev = {};
-          ev.events = EPOLLIN | EPOLLRDHUP;
-          ev.data.fd = c;
-          epoll_ctl(ep, EPOLL_CTL_ADD, c, &ev);
-        }
-        continue;
-      }
-      auto it = conns.find(fd);
-      if (it == conns.end()) continue;
-      Conn& cn = it->second;
-      if (!cn.handshaken) {
-        const int r = SSL_accept(cn.ssl);
-        if (r == 1) {
-          cn.handshaken = true;
-        } else {
-          const int e = SSL_get_error(cn.ssl, r);
-          if (e != SSL_ERROR_WANT_READ && e != SSL_ERROR_WANT_WRITE) drop(fd);
-          continue;
-        }
-      }
-      // with timing on: the kernel's receive time of the oldest unread byte, when nothing is
-      // buffered yet
-      int64_t rx = 0, t_read = 0;
-      if (timing_.load(std::memory_order_relaxed)) {
-        if (!cn.stamps_tried) {
-          int on = 1;
-          cn.stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
-          cn.stamps_tried = true;
-        }
-        if (cn.stamps && cn.rbuf.empty() && !(cn.ssl && SSL_pending(cn.ssl) > 0)) rx = wait_rx_timestamp(fd);
-        t_read = realtime_ns();
-      }
-      bool closed = false;
-      char tmp[16384];
-      for (;;) {
-        int got;
-        if (cn.ssl) {
-          got = SSL_read(cn.ssl, tmp, sizeof tmp);
-          if (got <= 0) {
-            const int e = SSL_get_error(cn.ssl, got);
-            if (e != SSL_ERROR_WANT_READ && e != SSL_ERROR_WANT_WRITE) closed = true;
-            break;
-          }
-        } else {
-          got = static_cast<int>(::recv(fd, tmp, sizeof tmp, 0));
-          if (got == 0) closed = true;
-          if (got <= 0) break;
-        }
-        cn.rbuf.append(tmp, static_cast<size_t>(got));
-      }
-      bool close_after = false;
-      for (;;) {
-        HttpRequest req;
-        bool http10 = false;
-        const long used = take_request(cn.rbuf, &req, &http10);
-        if (used == 0) break;
-        if (used < 0) {
-          close_after = true;
-          break;
-        }
-        cn.rbuf.erase(0, static_cast<size_t>(used));
-        HttpResponse resp;
-        resp.status = 200;
-        handler_(req, &resp);
-        if (resp.status < 0) {
-          close_after = true;
-          break;
-        }
-        close_after = wants_close(req.headers, http10);
-        const std::string wire = response_wire(resp, close_after);
-        size_t off = 0;
-        while (off < wire.size()) {  // small responses: spin until written
-          int w;
-          if (cn.ssl) {
-            w = SSL_write(cn.ssl, wire.data() + off, static_cast<int>(wire.size() - off));
-            if (w <= 0) {
-              const int e = SSL_get_error(cn.ssl, w);
-              if (e == SSL_ERROR_WANT_WRITE || e == SSL_ERROR_WANT_READ) continue;
-              close_after = true;
-              break;
-            }
-          } else {
-            w = static_cast<int>(::send(fd, wire.data() + off, wire.size() - off, MSG_NOSIGNAL));
-            if (w < 0) {
-              if (errno == EAGAIN || errno == EINTR) continue;
-              close_after = true;
-              break;
-            }
-          }
-          off += static_cast<size_t>(w);
-        }
-        served_++;
-        if (rx > 0) record_timing(ServeTiming{std::max<int64_t>(t_read - rx, 0), realtime_ns() - t_read});
-        rx = 0;
-        if (close_after) break;
-      }
-      if (closed || close_after) drop(fd);
-    }
-  }
-  while (!conns.empty()) drop(conns.begin()->first);
-  ::close(ep);
-}
-
-void HttpServer::drop_connections() {
-  std::lock_guard<std::mutex> lk(mu_);
-  for (int fd : open_fds_) ::shutdown(fd, SHUT_RDWR);
-}
-
-void HttpServer::stop() {
-  if (stopping_.exchange(true)) return;
-  if (listen_fd_ >= 0) {
-    ::shutdown(listen_fd_, SHUT_RDWR);
-  }
-  if (acceptor_.joinable()) acceptor_.join();
-  if (listen_fd_ >= 0) {
-    ::close(listen_fd_);
-    listen_fd_ = -1;
-  }
-  std::vector<Worker> ws;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (int fd : open_fds_) ::shutdown(fd, SHUT_RDWR);
-    ws.swap(workers_);
-  }
-  for (auto& w : ws)
-    if (w.thread.joinable()) w.thread.join();
-}
-
-// ---------------------------------------------------------------------------------------
-// Self-signed certificates for TLS fakes
-
-Status generate_self_signed(const std::string& host, std::string* cert_pem, std::string* key_pem) {
-  ensure_ssl();
-  EVP_PKEY* pkey = EVP_EC_gen("P-256");
-  if (!pkey) return Status::Err("EVP_EC_gen: " + ssl_error_string());
-  X509* x = X509_new();
-  X509_set_version(x, 2);
-  ASN1_INTEGER_set(X509_get_serialNumber(x), 1);
-  X509_gmtime_adj(X509_getm_notBefore(x), -3600);
-  X509_gmtime_adj(X509_getm_notAfter(x), 3600L * 24 * 365);
-  X509_set_pubkey(x, pkey);
-  X509_NAME* name = X509_get_subject_name(x);
-  X509_NAME_add_entry_by_txt(name, "CN", MBSTRING_ASC,
-                             reinterpret_cast<const unsigned char*>(host.c_str()), -1, -1, 0);
-  // A distinct subject per certificate: two self-signed certificates for the same host (a proxy
-  // and an apiserver, both trusted in one CA bundle) must not shadow each other in the store's
-  // lookup by subject name.
-  unsigned char rnd[8];
-  RAND_bytes(rnd, sizeof rnd);
-  char org[32];
-  std::snprintf(org, sizeof org, "ksa-%02x%02x%02x%02x%02x%02x%02x%02x", rnd[0], rnd[1], rnd[2], rnd[3], rnd[4],
-                rnd[5], rnd[6], rnd[7]);
-  X509_NAME_add_entry_by_txt(name, "O", MBSTRING_ASC, reinterpret_cast<const unsigned char*>(org), -1, -1, 0);
-  X509_set_issuer_name(x, name);
-  std::string san = (is_ip_literal(host) ? "IP:" : "DNS:") + host;
-  X509V3_CTX v3;
-  X509V3_set_ctx_nodb(&v3);
-  X509V3_set_ctx(&v3, x, x, nullptr, nullptr, 0);
-  X509_EXTENSION* ext = X509V3_EXT_conf_nid(nullptr, &v3, NID_subject_alt_name, san.c_str());
-  if (ext) {
-    X509_add_ext(x, ext, -1);
-    X509_EXTENSION_free(ext);
-  }
-  X509_EXTENSION* bc = X509V3_EXT_conf_nid(nullptr, &v3, NID_basic_constraints, "critical,CA:TRUE");
-  if (bc) {
-    X509_add_ext(x, bc, -1);
-    X509_EXTENSION_free(bc);
-  }
-  if (!X509_sign(x, pkey, EVP_sha256())) {
-    X509_free(x);
-    EVP_PKEY_free(pkey);
-    return Status::Err("X509_sign: " + ssl_error_string());
-  }
-  BIO* cb = BIO_new(BIO_s_mem());
-  PEM_write_bio_X509(cb, x);
-  BIO* kb = BIO_new(BIO_s_mem());
-  PEM_write_bio_PrivateKey(kb, pkey, nullptr, nullptr, 0, nullptr, nullptr);
-  char* data = nullptr;
-  long n = BIO_get_mem_data(cb, &data);
-  cert_pem->assign(data, static_cast<size_t>(n));
-  n = BIO_get_mem_data(kb, &data);
-  key_pem->assign(data, static_cast<size_t>(n));
-  BIO_free(cb);
-  BIO_free(kb);
-  X509_free(x);
-  EVP_PKEY_free(pkey);
-  return Status::OK();
-}
-
 }  // namespace ksa

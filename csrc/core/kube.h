@@ -14,8 +14,8 @@
 //                            sends a JSON merge patch with a resourceVersion precondition.
 //                            When RBAC refuses /scale (a Role written for the reference) the
 //                            client falls back to ScaleMode::Deployment once and for all.
-//   * FakeDeployments     -- in-memory object tracker (the fake clientset the reference tests
-//                            use, scale_test.go:85-115) with latency and fault injection.
+//   (FakeDeployments, the in-memory object tracker the reference tests use via client-go's fake
+//   clientset, scale_test.go:85-115, is in csrc/fakes/mem_fakes.h: test builds only.)
 //   * PodAutoScaler       -- ScaleUp/ScaleDown with the reference's int32 clamp arithmetic and
 //                            log messages; a no-op at a bound returns OK (scale.go:62-65,89-92).
 #pragma once
@@ -244,54 +244,6 @@ Result<std::string> set_spec_replicas(const std::string& raw, int32_t replicas);
 // back to outside the plain case, and the reference the differential tests hold them to.
 Result<ScaleObject> parse_scale_object_dom(const std::string& json, bool absent_is_zero);
 Result<std::string> set_spec_replicas_dom(const std::string& raw, int32_t replicas);
-
-// In-memory object tracker (client-go fake clientset equivalent).
-class FakeDeployments final : public DeploymentApi {
- public:
-  explicit FakeDeployments(std::string namespace_ = "namespace");
-  void add(const std::string& name, int32_t replicas);
-  void add_without_replicas(const std::string& name);
-  Result<ScaleObject> get(const std::string& name) override;
-  Status update(const std::string& name, const ScaleObject& fetched, int32_t replicas) override;
-  // Pipelined read in virtual time: the snapshot is taken when the GET starts, and
-  // finish_get() only advances a VirtualClock to start + latency (the GET ran concurrently with
-  // whatever the caller did in between). Disabled unless enable_pipelining(true).
-  bool begin_get(const std::string& name, bool may_dial = true) override;
-  Result<ScaleObject> finish_get() override;
-  void enable_pipelining(bool on);
-
-  int32_t replicas(const std::string& name) const;  // -1 if absent
-  void set_replicas(const std::string& name, int32_t r);  // out-of-band edit (kubectl scale)
-  void set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call);
-  void fail_next_get(int n, std::string message);
-  void fail_next_update(int n, std::string message);
-  // Simulates a concurrent writer: bump resourceVersion right after each of the next n GETs,
-  // so the following update conflicts (409).
-  void conflict_next(int n);
-  uint64_t gets() const;
-  uint64_t updates() const;
-
- private:
-  struct Obj {
-    bool has_replicas = true;
-    int32_t replicas = 0;
-    uint64_t rv = 1;
-  };
-  mutable std::mutex mu_;
-  std::string ns_;
-  std::map<std::string, Obj> objs_;
-  std::shared_ptr<VirtualClock> clock_;
-  Nanos latency_ = 0;
-  int fail_get_ = 0, fail_update_ = 0, conflict_ = 0;
-  std::string fail_get_msg_, fail_update_msg_;
-  uint64_t gets_ = 0, updates_ = 0;
-  uint64_t rv_counter_ = 1000;
-  bool pipelining_ = false;
-  bool pending_ = false;
-  Nanos pending_done_at_ = 0;
-  Result<ScaleObject> pending_result_;
-  Result<ScaleObject> get_locked(const std::string& name);
-};
 
 // Per-call timing of one ScaleUp/ScaleDown (for poll->patch latency spans).
 struct ScaleSpan {

@@ -339,65 +339,6 @@ Result<AttrMap> HttpSqsApi::get_queue_attributes(const std::string& queue_url,
 }
 
 // ---------------------------------------------------------------------------------------
-// Fakes
-
-MockSqsApi::MockSqsApi(AttrMap initial) : attrs_(std::move(initial)) {}
-
-Result<AttrMap> MockSqsApi::get_queue_attributes(const std::string&,
-                                                 const std::vector<std::string>&) {
-  std::lock_guard<std::mutex> lk(mu_);
-  calls_++;
-  if (clock_) clock_->advance(latency_);
-  if (fail_n_ > 0) {
-    fail_n_--;
-    return Result<AttrMap>::Err(Status::Err(fail_msg_));
-  }
-  return Result<AttrMap>::Ok(attrs_);
-}
-
-void MockSqsApi::set_attributes(AttrMap attrs) {
-  std::lock_guard<std::mutex> lk(mu_);
-  attrs_ = std::move(attrs);
-}
-
-void MockSqsApi::set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call) {
-  std::lock_guard<std::mutex> lk(mu_);
-  clock_ = std::move(clock);
-  latency_ = per_call;
-}
-
-void MockSqsApi::fail_next(int n, std::string message) {
-  std::lock_guard<std::mutex> lk(mu_);
-  fail_n_ = n;
-  fail_msg_ = std::move(message);
-}
-
-uint64_t MockSqsApi::calls() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return calls_;
-}
-
-TraceSqsApi::TraceSqsApi(std::shared_ptr<Clock> clock,
-                         std::vector<std::pair<Nanos, AttrMap>> segments, Nanos per_call_latency)
-    : clock_(std::move(clock)), segments_(std::move(segments)), latency_(per_call_latency) {
-  std::stable_sort(segments_.begin(), segments_.end(),
-                   [](const auto& a, const auto& b) { return a.first < b.first; });
-}
-
-Result<AttrMap> TraceSqsApi::get_queue_attributes(const std::string&,
-                                                  const std::vector<std::string>&) {
-  // Sampled at call start, then the call "takes" latency_.
-  Nanos t = clock_->now();
-  AttrMap cur;
-  for (auto& seg : segments_) {
-    if (seg.first <= t) cur = seg.second;
-    else break;
-  }
-  if (latency_ > 0) clock_->sleep(latency_, nullptr);
-  return Result<AttrMap>::Ok(std::move(cur));
-}
-
-// ---------------------------------------------------------------------------------------
 // SqsClient
 
 SqsClient::SqsClient(std::shared_ptr<SqsApi> api, std::string queue_url,

@@ -3,7 +3,8 @@
 // Mirrors the reference's two-level design (/root/reference/sqs/sqs.go):
 //   * SqsApi       -- the injectable service seam (the reference's `SQS` interface,
 //                     sqs.go:14-18); HttpSqsApi is the real client (Query or JSON protocol,
-//                     SigV4-signed, SDK-style retries), MockSqsApi/TraceSqsApi are fakes.
+//                     SigV4-signed, SDK-style retries); the fakes MockSqsApi/TraceSqsApi
+//                     live in csrc/fakes/mem_fakes.h (test builds only).
 //   * SqsClient    -- NumMessages(): request the configured attribute names and sum their
 //                     strconv.Atoi values (sqs.go:45-67), with the reference's error texts.
 // Deliberate deviation: a requested attribute that is absent from the
@@ -157,46 +158,6 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   SqsApiStats stats_;
   uint64_t rng_ = 0x9E3779B97F4A7C15ULL;
   StopFlag cancel_;  // cancel(): interrupts retry back-off sleeps
-};
-
-// In-memory fake, the MockSQS of /root/reference/sqs/sqs_test.go:27-59: returns the stored
-// attribute map; set_attributes() is the SetQueueAttributes test hook. Optionally advances
-// a VirtualClock per call (API latency model) and injects failures.
-class MockSqsApi final : public SqsApi {
- public:
-  explicit MockSqsApi(AttrMap initial = {});
-  Result<AttrMap> get_queue_attributes(const std::string& queue_url,
-                                       const std::vector<std::string>& names) override;
-  void set_attributes(AttrMap attrs);
-  void set_latency(std::shared_ptr<VirtualClock> clock, Nanos per_call);
-  // The next `n` calls fail with `message`.
-  void fail_next(int n, std::string message);
-  uint64_t calls() const;
-
- private:
-  mutable std::mutex mu_;
-  AttrMap attrs_;
-  std::shared_ptr<VirtualClock> clock_;
-  Nanos latency_ = 0;
-  int fail_n_ = 0;
-  std::string fail_msg_;
-  uint64_t calls_ = 0;
-};
-
-// Time-driven fake: the attribute map is a piecewise-constant function of the clock
-// (segments sorted by start time). The decision-parity harness drives the reference's
-// synthetic traces through this.
-class TraceSqsApi final : public SqsApi {
- public:
-  TraceSqsApi(std::shared_ptr<Clock> clock, std::vector<std::pair<Nanos, AttrMap>> segments,
-              Nanos per_call_latency);
-  Result<AttrMap> get_queue_attributes(const std::string& queue_url,
-                                       const std::vector<std::string>& names) override;
-
- private:
-  std::shared_ptr<Clock> clock_;
-  std::vector<std::pair<Nanos, AttrMap>> segments_;
-  Nanos latency_;
 };
 
 class alignas(kCacheLine) SqsClient {

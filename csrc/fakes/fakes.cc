@@ -3,9 +3,9 @@
 #include <algorithm>
 #include <thread>
 
-#include "json.h"
-#include "sigv4.h"
-#include "xml.h"
+#include "../core/json.h"
+#include "../core/sigv4.h"
+#include "../core/xml.h"
 
 namespace ksa {
 

@@ -19,8 +19,8 @@
 #include <string>
 #include <vector>
 
-#include "http.h"
-#include "sqs.h"
+#include "http_server.h"
+#include "../core/sqs.h"
 
 namespace ksa {
 

@@ -30,6 +30,7 @@
 
 #include "../core/goutil.h"
 #include "../core/http.h"
+#include "../fakes/http_server.h"
 #include "../core/json.h"
 #include "../core/kube.h"
 #include "../core/sigv4.h"

@@ -28,7 +28,9 @@
 
 #include "../core/clock.h"
 #include "../core/exec_auth.h"
-#include "../core/fakes.h"
+#include "../fakes/fakes.h"
+#include "../fakes/http_server.h"
+#include "../fakes/mem_fakes.h"
 #include "../core/goutil.h"
 #include "../core/http.h"
 #include "../core/json.h"

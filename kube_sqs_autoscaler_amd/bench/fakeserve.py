@@ -15,7 +15,6 @@ import json
 import os
 import sys
 
-from ..ops import native
 from .latency import deployment_name, start_fake_endpoints
 
 
@@ -31,9 +30,8 @@ def main(argv=None) -> int:
     ap.add_argument("--hot", action="store_true", help="busy-polling servers that never sleep (HttpServer::set_hot)")
     ap.add_argument("--timing", action="store_true", help="record per-request timings (HttpServer::set_timing)")
     a = ap.parse_args(argv)
-    nat = native()
     cpus = json.loads(a.cpus) if a.cpus else None
-    sqs, kube = start_fake_endpoints(nat, a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus,
+    sqs, kube = start_fake_endpoints(a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus,
                                      a.queue_offset, hot=a.hot, timing=a.timing)
     try:
         info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],

@@ -30,7 +30,7 @@ from typing import Dict, List, Optional
 from ..autoscaler import SPIN_BUDGET_PPM, new_deployment_api, new_pod_autoscaler, new_sqs_api, new_sqs_client
 from ..config import TargetConfig
 from ..kube.config import RestConfig
-from ..ops import native
+from ..ops import fakes, native
 from ..sqs.credentials import static_provider
 
 AKID = "AKIDBENCHEXAMPLE"
@@ -83,7 +83,7 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
        "ApproximateNumberOfMessagesNotVisible": "0"}
 
 
-def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
+def start_fake_endpoints(queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
                          kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None, offset: int = 0,
                          hot: bool = False, timing: bool = False):
     """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues numbered from
@@ -92,11 +92,12 @@ def start_fake_endpoints(nat, queues: int, n_servers: int, tls: bool = False, sq
     ``hot``: each server is one busy-polling thread that never sleeps (HttpServer::set_hot).
     ``timing``: the servers record each request's wake-up delay and service time
     (HttpServer::set_timing; off by default, it adds two syscalls per request)."""
+    fk = fakes()
     sqs_servers, kube_servers = [], []
     for i in range(n_servers):
-        sqs = nat.FakeSqsServer()
+        sqs = fk.FakeSqsServer()
         sqs.require_signature(AKID, SECRET, REGION)
-        kube = nat.FakeKubeServer()
+        kube = fk.FakeKubeServer()
         kube.require_token(TOKEN)
         if cpus is not None:
             sqs.set_cpus(cpus[i])
@@ -234,7 +235,7 @@ class BenchEnv:
             self.sqs_servers = [r.sqs[0] for r in self.remotes]
             self.kube_servers = [r.kube[0] for r in self.remotes]
         elif servers in ("shared", "per-queue"):
-            self.sqs_servers, self.kube_servers = start_fake_endpoints(nat, queues, n_servers, tls, sqs_latency_ns,
+            self.sqs_servers, self.kube_servers = start_fake_endpoints(queues, n_servers, tls, sqs_latency_ns,
                                                                        kube_latency_ns, hot=hot_endpoints,
                                                                        timing=timing)
         else:

@@ -11,7 +11,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
-from ..ops import native
+from ..ops import fakes, native
 from .oracle import Event, Faults, Latency, depth_of, simulate
 from .traces import Scenario
 
@@ -116,8 +116,8 @@ def run_native(
         log.set_sink(log_sink)
 
     if faults is None:
-        sqs_api = nat.TraceSqsApi(clock, [(t, dict(a)) for t, a in scenario.trace], lat.sqs_ns)
-        kube = nat.FakeDeployments("default")
+        sqs_api = fakes().TraceSqsApi(clock, [(t, dict(a)) for t, a in scenario.trace], lat.sqs_ns)
+        kube = fakes().FakeDeployments("default")
         kube.add("target", scenario.init_replicas)
         kube.set_latency(clock, lat.get_ns)
         kube.enable_pipelining(prefetch)
@@ -245,9 +245,9 @@ def run_wire(scenario: Scenario, mode: str = "scale", prefetch: bool = True, ser
     akid, secret, region, token = "AKIDPARITY", "parity/secret", "us-east-1", "parity-token"
     own = servers is None
     if own:
-        sqs_srv = nat.FakeSqsServer()
+        sqs_srv = fakes().FakeSqsServer()
         sqs_srv.start("127.0.0.1", 0, False)
-        kube_srv = nat.FakeKubeServer()
+        kube_srv = fakes().FakeKubeServer()
         kube_srv.start("127.0.0.1", 0, False)
     else:
         sqs_srv, kube_srv = servers
@@ -327,7 +327,7 @@ def wire_summary(configs=WIRE_CONFIGS) -> dict:
     from . import traces
 
     nat = native()
-    sqs_srv, kube_srv = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs_srv, kube_srv = fakes().FakeSqsServer(), fakes().FakeKubeServer()
     sqs_srv.start("127.0.0.1", 0, False)
     kube_srv.start("127.0.0.1", 0, False)
     out = {}

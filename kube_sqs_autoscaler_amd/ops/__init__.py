@@ -4,7 +4,11 @@ Two in-tree artifacts back the framework (built by :mod:`kube_sqs_autoscaler_amd
 
 * ``_ksa_native`` -- the C++ runtime: control loop (the reference's ``Run``,
   /root/reference/main.go:35-80), SQS client (/root/reference/sqs/sqs.go), Deployment actuator
-  (/root/reference/scale/scale.go), SigV4, HTTP/TLS transport and the localhost fakes.
+  (/root/reference/scale/scale.go), SigV4, HTTP/TLS transport. The image ships this one.
+* ``_ksa_fakes`` -- the native test doubles: localhost fake SQS / kube-apiserver endpoints and
+  the in-memory fakes of the two API seams (the reference keeps its mocks in ``_test.go`` files,
+  /root/reference/main_test.go:241-304, /root/reference/sqs/sqs_test.go:27-59). Tests, the
+  benchmark and the parity harness load it with :func:`fakes`.
 * ``libksa_gpu.so`` -- the gfx950 HIP node probe (see :mod:`.gpu`).
 
 ``native()`` builds the extension on first use when it is missing or stale (a few seconds of
@@ -19,6 +23,7 @@ from types import ModuleType
 
 _lock = threading.Lock()
 _mod: ModuleType | None = None
+_fakes: ModuleType | None = None
 
 
 class NativeUnavailable(RuntimeError):
@@ -56,3 +61,27 @@ def native() -> ModuleType:
 
 def native_path() -> str:
     return native().__file__
+
+
+def fakes() -> ModuleType:
+    """Returns the ``_ksa_fakes`` module (test doubles), building it in-tree if needed. It
+    registers subclasses of ``_ksa_native``'s seams, so the runtime is loaded first."""
+    global _fakes
+    if _fakes is not None:
+        return _fakes
+    native()
+    with _lock:
+        if _fakes is not None:
+            return _fakes
+        if os.environ.get("KSA_NO_AUTOBUILD") != "1" and _sources_present():
+            from . import build
+
+            try:
+                build.build_fakes(verbose=False)
+            except Exception as e:  # pragma: no cover - toolchain failure
+                raise NativeUnavailable(f"failed to build the native fakes: {e}") from e
+        try:
+            _fakes = importlib.import_module("kube_sqs_autoscaler_amd.ops._ksa_fakes")
+        except ImportError as e:
+            raise NativeUnavailable(f"cannot import the native fakes (test builds only): {e}") from e
+        return _fakes

@@ -3,8 +3,12 @@
 Artifacts (git-ignored, but they travel to the GPU box with the gpurun snapshot):
 
 * ``kube_sqs_autoscaler_amd/ops/_ksa_native<EXT_SUFFIX>`` -- pybind11 module linking the C++
-  core in ``csrc/core`` (control loop, SigV4, HTTP/TLS transport, SQS + Kubernetes clients,
-  fake endpoints) against OpenSSL.
+  core in ``csrc/core`` (control loop, SigV4, HTTP/TLS client, SQS + Kubernetes clients)
+  against OpenSSL. This is the production runtime the image ships.
+* ``kube_sqs_autoscaler_amd/ops/_ksa_fakes<EXT_SUFFIX>`` -- the test doubles in ``csrc/fakes``
+  (localhost fake SQS / kube-apiserver, their HTTP server, in-memory API fakes), linked against
+  the core as a static archive (only what they use). Tests, the benchmark and the parity
+  harness load it; the slim image does not contain it.
 * ``kube_sqs_autoscaler_amd/ops/libksa_gpu.so`` -- ``hipcc --offload-arch=gfx950`` build of
   ``csrc/hip/gpu_probe.hip`` (GPU inventory + HBM health check), loaded with ctypes.
 * ``build/native_tests[_asan|_tsan]`` -- host-only C++ test binaries (sanitizer builds).
@@ -33,6 +37,7 @@ OPS = Path(__file__).resolve().parent
 BUILD = ROOT / "build"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 NATIVE_SO = OPS / f"_ksa_native{EXT_SUFFIX}"
+FAKES_SO = OPS / f"_ksa_fakes{EXT_SUFFIX}"
 GPU_SO = OPS / "libksa_gpu.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
@@ -46,6 +51,10 @@ LIBS = ["-lssl", "-lcrypto", "-pthread"]
 
 def _core_sources() -> list[Path]:
     return sorted((CSRC / "core").glob("*.cc"))
+
+
+def _fakes_sources() -> list[Path]:
+    return sorted((CSRC / "fakes").glob("*.cc"))
 
 
 def _newest_header() -> float:
@@ -83,25 +92,48 @@ def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: 
     return objs
 
 
-def build_native(jobs: int = 8, verbose: bool = True) -> Path:
-    """Builds the pybind11 extension in place; returns its path."""
+RELEASE_FLAGS = ["-fvisibility=hidden"]
+
+
+def _binding_object(name: str) -> Path:
     import pybind11
 
-    py_inc = sysconfig.get_paths()["include"]
-    extra = ["-fvisibility=hidden"]
-    core = _compile_objects("release", extra, _core_sources(), jobs)
-    mod_src = CSRC / "bindings" / "module.cc"
-    mod_obj = BUILD / "obj-release" / "module.o"
-    if _stale(mod_obj, [mod_src], _newest_header()):
-        _run([CXX, *CXXFLAGS, *extra, f"-I{pybind11.get_include()}", f"-I{py_inc}", "-c", str(mod_src), "-o", str(mod_obj)])
-    deps = core + [mod_obj]
-    if _stale(NATIVE_SO, deps, 0.0):
-        tmp = NATIVE_SO.with_suffix(".tmp.so")
-        _run([CXX, "-shared", "-o", str(tmp), *map(str, deps), *LIBS])
-        os.replace(tmp, NATIVE_SO)
+    src = CSRC / "bindings" / f"{name}.cc"
+    obj = BUILD / "obj-release" / f"{name}.o"
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    if _stale(obj, [src], _newest_header()):
+        _run([CXX, *CXXFLAGS, *RELEASE_FLAGS, f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+              "-c", str(src), "-o", str(obj)])
+    return obj
+
+
+def _link(out: Path, inputs: list[Path], verbose: bool) -> None:
+    if _stale(out, inputs, 0.0):
+        tmp = out.with_suffix(".tmp.so")
+        _run([CXX, "-shared", "-o", str(tmp), *map(str, inputs), *LIBS])
+        os.replace(tmp, out)
         if verbose:
-            print(f"[build] linked {NATIVE_SO.relative_to(ROOT)}")
+            print(f"[build] linked {out.relative_to(ROOT)}")
+
+
+def build_native(jobs: int = 8, verbose: bool = True) -> Path:
+    """Builds the production pybind11 extension in place; returns its path."""
+    core = _compile_objects("release", RELEASE_FLAGS, _core_sources(), jobs)
+    _link(NATIVE_SO, core + [_binding_object("module")], verbose)
     return NATIVE_SO
+
+
+def build_fakes(jobs: int = 8, verbose: bool = True) -> Path:
+    """Builds the test-doubles extension (``_ksa_fakes``) in place; returns its path. The core
+    goes in as a static archive, so the module carries only the core objects the fakes use."""
+    core = _compile_objects("release", RELEASE_FLAGS, _core_sources(), jobs)
+    archive = BUILD / "obj-release" / "libksa_core.a"
+    if _stale(archive, core, 0.0):
+        archive.unlink(missing_ok=True)
+        _run(["ar", "rcs", str(archive), *map(str, core)])
+    fakes = _compile_objects("release", RELEASE_FLAGS, _fakes_sources(), jobs)
+    _link(FAKES_SO, fakes + [_binding_object("fakes_module"), archive], verbose)
+    return FAKES_SO
 
 
 def build_gpu_probe(verbose: bool = True) -> Path | None:
@@ -130,7 +162,7 @@ def build_native_tests(sanitizer: str | None = None, jobs: int = 8) -> Path:
         "tsan": ["-g", "-O1", "-fsanitize=thread"],
     }[sanitizer]
     variant = sanitizer or "test"
-    srcs = _core_sources() + [CSRC / "tests" / "native_tests.cc"]
+    srcs = _core_sources() + _fakes_sources() + [CSRC / "tests" / "native_tests.cc"]
     objs = _compile_objects(variant, flags, srcs, jobs)
     out = BUILD / ("native_tests" + (f"_{sanitizer}" if sanitizer else ""))
     if _stale(out, objs, 0.0):
@@ -148,8 +180,10 @@ def build_fuzzer(jobs: int = 8) -> Path:
     """libFuzzer harness over the wire parsers (needs a clang with libFuzzer: ROCm's has it)."""
     if not Path(CLANGXX).exists() and shutil.which(CLANGXX) is None:
         raise RuntimeError(f"{CLANGXX} not found; cannot build the fuzzer")
-    # the fakes and the loop are not wire parsers (and fakes.cc trips a clang ODR false positive)
-    srcs = [p for p in _core_sources() if p.stem not in ("fakes", "runner", "sweep")] + [CSRC / "tests" / "fuzz_wire.cc"]
+    # the loop and the fake endpoints are not wire parsers (and fakes.cc trips a clang ODR false
+    # positive); the fakes' HTTP server is a target (request framing)
+    srcs = [p for p in _core_sources() if p.stem not in ("runner", "sweep")] + [CSRC / "fakes" / "http_server.cc",
+                                                                                CSRC / "tests" / "fuzz_wire.cc"]
     objs = _compile_objects("fuzz", FUZZ_FLAGS + ["-fsanitize=fuzzer-no-link"], srcs, jobs, cxx=CLANGXX)
     out = BUILD / "fuzz_wire"
     if _stale(out, objs, 0.0):
@@ -158,7 +192,7 @@ def build_fuzzer(jobs: int = 8) -> Path:
 
 
 def build_all(hip: bool = True, jobs: int = 8) -> dict:
-    out = {"native": str(build_native(jobs=jobs))}
+    out = {"native": str(build_native(jobs=jobs)), "fakes": str(build_fakes(jobs=jobs))}
     if hip:
         out["gpu_probe"] = str(build_gpu_probe())
     return out

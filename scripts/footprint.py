@@ -2,9 +2,9 @@
 steady CPU of the CLI tracking 1 and 64 queues at 1 s polls against localhost fakes."""
 import os, subprocess, sys, time, yaml
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from kube_sqs_autoscaler_amd.ops import native
+from kube_sqs_autoscaler_amd.ops import fakes, native
 nat = native()
-sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+sqs, kube = fakes().FakeSqsServer(), fakes().FakeKubeServer()
 sqs.start(); kube.start()
 kc = "/tmp/fp_kc.yaml"
 open(kc, "w").write(yaml.safe_dump({"current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],

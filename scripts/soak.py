@@ -84,7 +84,7 @@ def cadenced(a) -> int:
 
     from kube_sqs_autoscaler_amd.models.oracle import Params
     from kube_sqs_autoscaler_amd.models.replay import group_spans, replay_queue
-    from kube_sqs_autoscaler_amd.ops import native
+    from kube_sqs_autoscaler_amd.ops import fakes, native
     from kube_sqs_autoscaler_amd.utils.goflag import parse_duration
 
     nat = native()
@@ -92,10 +92,11 @@ def cadenced(a) -> int:
     up_cool, down_cool = parse_duration(a.up_cool_down), parse_duration(a.down_cool_down)
     tmp = tempfile.mkdtemp(prefix="ksa-soak-")
     tokens = ["soak-token-1", "soak-token-2"]
-    sqs = nat.FakeSqsServer()
+    fk = fakes()
+    sqs = fk.FakeSqsServer()
     sqs.require_signature(AKID, SECRET, REGION)
     sqs.start("127.0.0.1", 0, True)
-    kube = nat.FakeKubeServer()
+    kube = fk.FakeKubeServer()
     kube.require_token(tokens[0])
     kube.start("127.0.0.1", 0, True)
     token_file = os.path.join(tmp, "token")
@@ -157,11 +158,11 @@ def cadenced(a) -> int:
                 kind = step % 6
                 step += 1
                 if kind == 0:
-                    kube.inject(2, nat.InjectedFault(503, '{"kind":"Status","code":503,"message":"overloaded"}',
+                    kube.inject(2, fk.InjectedFault(503, '{"kind":"Status","code":503,"message":"overloaded"}',
                                                      "application/json", retry_after="1"))
                     injected["kube_503_retry_after"] += 2
                 elif kind == 1:
-                    kube.inject(1, nat.InjectedFault(500, '{"kind":"Status","code":500,"message":"etcd"}',
+                    kube.inject(1, fk.InjectedFault(500, '{"kind":"Status","code":500,"message":"etcd"}',
                                                      "application/json"))
                     injected["kube_500"] += 1
                 elif kind == 2:
@@ -171,7 +172,7 @@ def cadenced(a) -> int:
                     kube.drop_connections()
                     injected["kube_drop"] += 1
                 elif kind == 4:
-                    sqs.inject(2, nat.InjectedFault(503, THROTTLE, "text/xml", retry_after="1"))
+                    sqs.inject(2, fk.InjectedFault(503, THROTTLE, "text/xml", retry_after="1"))
                     injected["sqs_throttle"] += 2
                 else:
                     sqs.drop_connections()

@@ -13,8 +13,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-second test")
 
 
+class _RuntimeAndFakes:
+    """One handle on the production runtime (_ksa_native) and the native test doubles
+    (_ksa_fakes, a separate module the image does not ship): names resolve in the runtime first."""
+
+    def __init__(self, runtime, doubles):
+        self._runtime, self._doubles = runtime, doubles
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._runtime, name)
+        except AttributeError:
+            return getattr(self._doubles, name)
+
+
 @pytest.fixture(scope="session")
 def nat():
-    from kube_sqs_autoscaler_amd.ops import native
+    from kube_sqs_autoscaler_amd.ops import fakes, native
 
-    return native()
+    return _RuntimeAndFakes(native(), fakes())

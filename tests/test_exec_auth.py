@@ -23,13 +23,6 @@ V1A1 = "client.authentication.k8s.io/v1alpha1"
 S = 1_000_000_000
 
 
-@pytest.fixture
-def nat():
-    from kube_sqs_autoscaler_amd.ops import native
-
-    return native()
-
-
 def plugin(tmp_path, body, name="plugin.py"):
     """An executable Python credential plugin; it appends one line per run to runs.log."""
     p = tmp_path / name

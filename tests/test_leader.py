@@ -110,7 +110,7 @@ def test_renew_loop_reports_loss(kube):
     a = LeaderElector(LeaseLock(RestConfig(host=kube.url, bearer_token=TOKEN), "ml", "ksa"), "a", 0.6, 0.3, 0.05)
     assert a.try_acquire_or_renew()
     a._leader = True
-    kube.inject(1000, __import__("kube_sqs_autoscaler_amd.ops", fromlist=["native"]).native().InjectedFault(500, "down"))
+    kube.inject(1000, __import__("kube_sqs_autoscaler_amd.ops", fromlist=["fakes"]).fakes().InjectedFault(500, "down"))
     lost = threading.Event()
     stop = threading.Event()
     t = threading.Thread(target=a.renew_loop, args=(stop, lost.set))
