@@ -5,8 +5,9 @@ IMAGE ?= kube-sqs-autoscaler-amd
 VERSION ?= v0.1.0
 PY ?= python3
 
-test:            ## CPU test suite (no GPU needed)
-	$(PY) -m pytest tests -q -m "not gpu"
+test:            ## CPU test suite (no GPU needed): parallel, then the timing-sensitive tests serially
+	$(PY) -m pytest tests -q -m "not gpu" -n auto
+	$(PY) -m pytest tests -q -m "serial and not gpu"
 
 test-gpu:        ## GPU tests on an MI355X box
 	$(PY) -m pytest tests -q -m gpu

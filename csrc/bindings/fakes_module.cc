@@ -110,6 +110,7 @@ PYBIND11_MODULE(_ksa_fakes, m) {
       .def("requests", &FakeSqsServer::requests)
       .def("signature_failures", &FakeSqsServer::signature_failures)
       .def("connections", &FakeSqsServer::connections)
+      .def("connection_threads", &FakeSqsServer::connection_threads)
       .def("timings", [](const FakeSqsServer& s) {
         std::vector<std::pair<int64_t, int64_t>> out;
         for (auto& t : s.timings()) out.emplace_back(t.wake_ns, t.service_ns);

@@ -406,6 +406,8 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("rtt_ewma", &HttpClient::rtt_ewma)
       .def("close", &HttpClient::close)
       .def("stats", [](HttpClient& c) { return http_stats_dict(c.stats()); });
+  m.def("http_spin_window", &HttpClient::spin_window_for, py::arg("busy_poll_ns"), py::arg("ewma_ns"),
+        py::arg("budget_ns"));
   m.def("parse_url", [](const std::string& s) {
     Url u = unwrap(parse_url(s));
     return py::make_tuple(u.scheme, u.host, u.port, u.path);

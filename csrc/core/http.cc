@@ -757,13 +757,17 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   return Status::OK();
 }
 
-Nanos HttpClient::spin_window() const {
-  if (spin_ns_ <= 0) return 0;
-  if (ewma_ns_ < 0) return spin_ns_;  // no sample yet: try
-  if (ewma_ns_ <= 4 * spin_ns_) return spin_ns_;
+Nanos HttpClient::spin_window_for(Nanos busy_poll, Nanos ewma, Nanos budget) {
+  if (busy_poll <= 0) return 0;
+  if (ewma < 0) return busy_poll;  // no sample yet: try
+  if (ewma <= 4 * busy_poll) return busy_poll;
   // a slower peer: spin through its expected response time when the budget allows
-  const Nanos through = 2 * ewma_ns_, budget = spin_budget_ns_.load(std::memory_order_relaxed);
+  const Nanos through = 2 * ewma;
   return through <= budget ? through : 0;
+}
+
+Nanos HttpClient::spin_window() const {
+  return spin_window_for(spin_ns_, ewma_ns_, spin_budget_ns_.load(std::memory_order_relaxed));
 }
 
 Nanos HttpClient::rtt_ewma() const {

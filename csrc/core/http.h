@@ -166,6 +166,9 @@ class alignas(kCacheLine) HttpClient {
   // from an idle sleep on its answer, at a bounded CPU cost. 0 (default): never beyond the window.
   void set_spin_budget(Nanos ns) { spin_budget_ns_ = ns; }
   Nanos rtt_ewma() const;
+  // The read spin of the next response: `busy_poll` (the window) while the EWMA is unknown or
+  // within 4x the window; else twice the EWMA when that fits in `budget`; else 0 (block at once).
+  static Nanos spin_window_for(Nanos busy_poll, Nanos ewma, Nanos budget);
   // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller), the
   // three kinds Go's transport speaks:
   //   "http://[user:pass@]host:port"   an https origin is reached through a CONNECT tunnel (TLS

@@ -65,9 +65,10 @@ struct LoopConfig {
   bool connect_at_start = false;
   // On a worker's own thread, its clients may busy-poll through an answer slower than the
   // --busy-poll window while twice the response-time EWMA fits in this share of the poll period
-  // (parts per million; HttpClient::set_spin_budget). The CLI gives a process's queues 1 % in
-  // total (10000 / queues each), so their spinning stays within a few % of one core whatever
-  // the queue count. 0 disables. Pooled threads never spin beyond the window.
+  // (parts per million; Runner::set_spin_budget splits it over the poll's SQS call, GET and
+  // write, so it bounds the poll's spinning as a whole). The CLI gives a process's queues 1 % in
+  // total (10000 / queues each), so their spinning stays within 1 % of one core whatever the
+  // queue count. 0 disables. Pooled threads never spin beyond the window.
   int64_t spin_budget_ppm = 10000;
 };
 
@@ -220,10 +221,13 @@ class alignas(kCacheLine) Runner {
     sqs_->cancel();
     scaler_->cancel();
   }
-  // Both clients' HttpClient::set_spin_budget.
+  // Splits one poll's spin budget over the requests a poll makes (HttpClient::set_spin_budget
+  // applies per request): half to the SQS call, a quarter to each of the apiserver's GET and
+  // write, so a scaling poll spins at most `ns` in total. (An SDK retry of the SQS call spins
+  // within its own half again; retries are the error path.)
   void set_spin_budget(Nanos ns) {
-    sqs_->api()->set_spin_budget(ns);
-    scaler_->api()->set_spin_budget(ns);
+    sqs_->api()->set_spin_budget(ns / 2);
+    scaler_->api()->set_spin_budget(ns / 4);
   }
   // Closes the clients' keep-alive connections (on the calling thread's file table).
   void release_connections() {

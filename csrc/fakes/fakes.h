@@ -67,6 +67,7 @@ class FakeSqsServer {
   uint64_t requests() const { return requests_.load(); }
   uint64_t signature_failures() const { return sig_failures_.load(); }
   uint64_t connections() const;
+  size_t connection_threads() const { return server_ ? server_->connection_threads() : 0; }
   // HttpServer::timings(): per request, the server's wake-up delay and service time.
   std::vector<HttpServer::ServeTiming> timings() const { return server_ ? server_->timings() : std::vector<HttpServer::ServeTiming>{}; }
   void clear_timings() { if (server_) server_->clear_timings(); }

@@ -29,6 +29,11 @@ class HttpServer {
   void stop();
   uint64_t requests_served() const { return served_.load(); }
   uint64_t connections_accepted() const { return accepted_.load(); }
+  // Connection threads not yet joined (running, or finished and reaped on the next accept).
+  size_t connection_threads() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return workers_.size();
+  }
   // Close every open client connection after its in-flight response (idle-close test).
   void drop_connections();
   // CPUs for the acceptor and connection threads (call before listen(); empty: unpinned).
@@ -66,7 +71,7 @@ class HttpServer {
   int port_ = 0;
   std::atomic<bool> stopping_{false};
   std::thread acceptor_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::vector<int> open_fds_;
   // Connection threads; finished ones are joined on the next accept, so a long-lived fake
   // serving many short connections does not accumulate dead threads (and their stacks).

@@ -10,4 +10,7 @@ python3 -m kube_sqs_autoscaler_amd.ops.build --sanitizers
 TSAN_OPTIONS="halt_on_error=1" ./build/native_tests_tsan
 python3 -m kube_sqs_autoscaler_amd.ops.build --no-hip --fuzz
 mkdir -p build/fuzz_corpus && ./build/fuzz_wire -max_total_time=60 -timeout=10 build/fuzz_corpus csrc/tests/fuzz_corpus
-python3 -m pytest tests -q -m "not gpu"
+# parallel over the runner's CPUs (pytest-xdist); the timing-sensitive `serial` tests skip
+# themselves under xdist workers and run afterwards on their own
+python3 -m pytest tests -q -m "not gpu" -n auto
+python3 -m pytest tests -q -m "serial and not gpu"

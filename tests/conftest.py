@@ -11,6 +11,17 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: multi-second test")
+    config.addinivalue_line("markers", "serial: timing-sensitive; skipped under pytest-xdist workers "
+                                       "(CI runs them in a serial pass: scripts/ci.sh)")
+
+
+def pytest_collection_modifyitems(config, items):
+    if not os.environ.get("PYTEST_XDIST_WORKER"):
+        return
+    skip = pytest.mark.skip(reason="serial test: measures timing, so it runs only outside xdist (scripts/ci.sh)")
+    for item in items:
+        if "serial" in item.keywords:
+            item.add_marker(skip)
 
 
 class _RuntimeAndFakes:

@@ -62,14 +62,35 @@ def test_bench_workers_dial_their_own_connections(nat):
         env.close()
 
 
-@pytest.mark.parametrize("period_ms,spins", [(200, True), (0, False)])
+US = 1_000
+
+
+@pytest.mark.parametrize("busy_poll,ewma,budget,window", [
+    (0, 50 * US, 10_000 * US, 0),              # --busy-poll=0s: never spin
+    (25 * US, -1, 0, 25 * US),                 # no response-time sample yet: try the window
+    (25 * US, 100 * US, 0, 25 * US),           # a fast peer (EWMA <= 4x window): the window
+    (25 * US, 101 * US, 0, 0),                 # slower, no budget (pooled thread / back to back)
+    (25 * US, 400 * US, 800 * US, 800 * US),   # slower, 2x EWMA fits the budget: spin through it
+    (25 * US, 400 * US, 799 * US, 0),          # ... and does not: block in poll(2) at once
+])
+def test_spin_window_decision(nat, busy_poll, ewma, budget, window):
+    """HttpClient::spin_window_for, the spin/no-spin decision of every response read, on injected
+    EWMA and budget values (deterministic; the end-to-end share check below is load-dependent)."""
+    assert nat.http_spin_window(busy_poll, ewma, budget) == window
+
+
+@pytest.mark.slow
+@pytest.mark.serial
+@pytest.mark.parametrize("period_ms,spins", [(1000, True), (0, False)])
 def test_cadenced_worker_spins_through_a_slow_answer_within_its_budget(nat, period_ms, spins):
-    """HttpClient::set_spin_budget: a worker on its own thread may busy-poll through an answer
-    that takes longer than the --busy-poll window when twice the response-time EWMA fits in 1 %
-    of the poll period (200 ms -> 2 ms; the fakes answer after ~0.4 ms), so the poll is not woken
-    from an idle sleep by its answer. The spin lasts 2 x EWMA (~1 ms): an answer a busy host
-    delays past that is waited for in poll(2), so most polls, not all, spin. Back to back (no
-    period, no budget) a peer that slow is always waited for in poll(2), as before."""
+    """End to end: a worker on its own thread may busy-poll through an answer that takes longer
+    than the --busy-poll window when twice the response-time EWMA fits in the SQS call's half of
+    1 % of the poll period (1 s -> 5 ms; the fakes answer after 0.4 ms plus their timer slack),
+    so the poll is not woken from an idle sleep by its answer. The spin lasts 2 x EWMA: an answer
+    a busy host delays past that is waited for in poll(2), so how many polls spin depends on the
+    load -- this runs serially (conftest: ``serial`` tests are skipped under xdist workers) and
+    asks only that spinning happens. Back to back (no period, no budget) a peer that slow is
+    always waited for in poll(2)."""
     import json
     import tempfile
 
@@ -88,7 +109,7 @@ def test_cadenced_worker_spins_through_a_slow_answer_within_its_budget(nat, peri
     sqs = [s["detail"]["sqs"] for s in spans if s.get("detail") and s["detail"].get("sqs")]
     assert len(sqs) >= 4
     spun = sum(1 for c in sqs if c["spun"])
-    assert (2 * spun > len(sqs)) if spins else (spun == 0), sqs
+    assert (spun >= 1) if spins else (spun == 0), sqs
 
 
 def test_cli_queues_share_one_spin_budget(nat):

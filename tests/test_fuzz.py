@@ -52,19 +52,29 @@ def test_http_server_reaps_connection_threads(nat):
     """Found by the fuzzer: the server kept one dead thread per closed connection."""
     import socket
 
+    import time
+
     srv = nat.FakeSqsServer()
     srv.start()
     try:
-        def vm_kib():  # an exited but unjoined thread still holds its 8 MiB stack mapping
-            with open("/proc/self/status") as f:
-                return next(int(l.split()[1]) for l in f if l.startswith("VmSize:"))
+        def live_threads():
+            return len(os.listdir("/proc/self/task"))
 
-        base = vm_kib()
+        base = live_threads()
         for _ in range(200):
             with socket.create_connection(("127.0.0.1", srv.port)) as s:
                 s.sendall(b"GET / HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
                 while s.recv(4096):
                     pass
-        assert vm_kib() - base < 200 * 1024  # 200 leaked stacks would be ~1.6 GiB
+        # An exited but unjoined thread is gone from /proc/self/task yet keeps its stack mapping,
+        # so the leak is counted where it lives: the server's list of unjoined connection threads
+        # (finished ones are joined on the next accept; the last connection's may still be there).
+        # Address-space size (VmSize) is no signal: glibc's per-thread malloc arenas reserve 64 MiB
+        # each under contention and never give the reservation back.
+        assert srv.connection_threads() <= 2
+        deadline = time.monotonic() + 5
+        while live_threads() > base + 1 and time.monotonic() < deadline:  # the last one exiting
+            time.sleep(0.01)
+        assert live_threads() <= base + 1
     finally:
         srv.stop()
