@@ -916,6 +916,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         py::arg("model"), py::arg("params"), py::arg("seeds"), py::arg("seed0") = 1, py::arg("threads") = 8,
         py::arg("arith") = 0);
 
+  m.attr("HTTP_TIMING") = kHttpTiming;  // false in the image build (-DKSA_HTTP_TIMING=0)
   m.attr("SECOND") = kSecond;
   m.attr("MILLISECOND") = kMillisecond;
   m.attr("MICROSECOND") = kMicrosecond;

@@ -645,7 +645,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   conn_ = std::make_unique<Conn>();
   conn_->stream = std::move(stream);
   conn_->rbuf = std::move(rbuf);
-  if (timing_) conn_->stream->enable_rx_timestamps();
+  if (timing()) conn_->stream->enable_rx_timestamps();
   stats_.connects++;
   return Status::OK();
 }
@@ -710,7 +710,7 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   }
   const bool reused = conn_->uses > 0;
   conn_->uses++;
-  if (timing_) timing_cur_.write_begin = mono_ns();
+  if (timing()) timing_cur_.write_begin = mono_ns();
 
   std::string& wire = wire_;  // kept across requests: no allocation per request
   if (wire.capacity() > 64 * 1024) std::string().swap(wire);
@@ -753,7 +753,7 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   }
   stats_.bytes_out += wire.size();
   sent_at_ = mono_ns();
-  if (timing_) timing_cur_.written = sent_at_;
+  if (timing()) timing_cur_.written = sent_at_;
   return Status::OK();
 }
 
@@ -782,7 +782,7 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
   const bool reused = conn_->uses > 1;
   Status s;
   conn_->stream->set_spin_ns(spin_window());
-  if (timing_) conn_->stream->arm_first_bytes();
+  if (timing()) conn_->stream->arm_first_bytes();
   Reader rd(conn_->stream.get(), &conn_->rbuf);
   std::string& head = head_;  // kept across responses: no allocation per response
   if (head.capacity() > 64 * 1024) std::string().swap(head);
@@ -845,7 +845,7 @@ Status HttpClient::read_response(const HttpRequest& req, HttpResponse* resp, int
     const Nanos rtt = now - sent_at_;
     ewma_ns_ = ewma_ns_ < 0 ? rtt : (ewma_ns_ * 7 + rtt) / 8;
     conn_->last_response_ns = now;
-    if (timing_) {
+    if (timing()) {
       const auto& fb = conn_->stream->first_bytes();
       timing_cur_.seen = fb.seen;
       timing_cur_.spun = fb.spun;
@@ -920,7 +920,7 @@ Status HttpClient::round_trip(const HttpRequest& req, HttpResponse* resp, Nanos 
   if (timeout == 0) return Status::Err("i/o timeout");  // no time left at all
   const int64_t deadline = t > 0 ? mono_ns() + t : 0;
   stats_.requests++;
-  if (timing_) timing_cur_ = HttpTiming{mono_ns()};
+  if (timing()) timing_cur_ = HttpTiming{mono_ns()};
   bool retryable = false;
   Status s = attempt(req, resp, deadline, &retryable);
   if (!s.ok() && retryable && !cancelled()) {
@@ -936,7 +936,7 @@ Status HttpClient::send(const HttpRequest& req) {
   if (cancelled()) return Status::Err("request canceled");
   const int64_t deadline = timeout_ > 0 ? mono_ns() + timeout_ : 0;
   stats_.requests++;
-  if (timing_) timing_cur_ = HttpTiming{mono_ns()};
+  if (timing()) timing_cur_ = HttpTiming{mono_ns()};
   bool retryable = false;
   Status s = write_request(req, deadline, &retryable);
   if (!s.ok() && retryable && !cancelled()) {

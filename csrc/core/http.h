@@ -78,6 +78,14 @@ struct HttpClientStats {
   std::string tls_cipher;   // its cipher suite, e.g. "TLS_AES_128_GCM_SHA256"
 };
 
+// Per-request timing (HttpClient::set_timing: HttpTiming, SO_TIMESTAMPNS receive stamps) is a
+// diagnostic for the benchmark's attribution rows. The image build compiles it out
+// (-DKSA_HTTP_TIMING=0, `ops.build --image`): set_timing() is then a no-op and timing() false.
+#ifndef KSA_HTTP_TIMING
+#define KSA_HTTP_TIMING 1
+#endif
+inline constexpr bool kHttpTiming = KSA_HTTP_TIMING != 0;
+
 // Where one request's time went (HttpClient::set_timing), CLOCK_MONOTONIC ns; 0 = not known.
 // rx is the kernel's receive time of the response's first bytes (SO_TIMESTAMPNS; plain sockets
 // only), so seen - rx is how long those bytes waited for this thread: its wake-up.
@@ -146,8 +154,8 @@ class alignas(kCacheLine) HttpClient {
   void set_caller_retries(bool on) { caller_retries_ = on; }
   // Per-request timing breakdown (diagnostics: a benchmark's attribution rows); adds a
   // timestamp read per phase and a recvmsg for the first response bytes. Off by default.
-  void set_timing(bool on) { timing_ = on; }
-  bool timing() const { return timing_; }
+  void set_timing(bool on) { timing_ = kHttpTiming && on; }
+  bool timing() const { return kHttpTiming && timing_; }
   HttpTiming last_timing() const;
   // Aborts any request in progress ("request canceled") and every later one: graceful shutdown
   // must not wait for a slow or hung peer (the in-flight call's timeout can be 30 s). Sticky.

@@ -359,7 +359,7 @@ class alignas(kCacheLine) Stream {
 
   // recv(2), or recvmsg(2) with the receive timestamp while first-bytes timing is armed.
   ssize_t recv_some(char* out, size_t cap) {
-    if (!(ts_ && first_.armed)) return ::recv(fd_, out, cap, 0);
+    if (!(kHttpTiming && ts_ && first_.armed)) return ::recv(fd_, out, cap, 0);
     struct iovec iov = {out, cap};
     alignas(struct cmsghdr) char ctrl[CMSG_SPACE(sizeof(struct timespec))];
     struct msghdr msg = {};

@@ -191,7 +191,7 @@ IterationRecord Runner::poll_body() {
   auto finish = [&]() -> IterationRecord& {
     scaler_->discard_prefetch();  // unused (no action this poll): drain it
     rec.total_ns = clock_->now() - t0;
-    if (trace_fd_ >= 0) {  // per-call breakdowns of timed clients (bench attribution rows)
+    if (kHttpTiming && trace_fd_ >= 0) {  // per-call breakdowns of timed clients (bench attribution rows)
       const std::string sq = sqs_->api()->timing_json();
       const std::string wr = rec.patch_latency_ns >= 0 ? scaler_->api()->timing_json() : std::string();
       if (!sq.empty() || !wr.empty())

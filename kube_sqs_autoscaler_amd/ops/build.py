@@ -18,7 +18,11 @@ Artifacts (git-ignored, but they travel to the GPU box with the gpurun snapshot)
 Objects are compiled in parallel and reused when neither the source nor any header under
 ``csrc/`` changed, so an incremental rebuild after touching one file takes seconds.
 
-Usage: ``python -m kube_sqs_autoscaler_amd.ops.build [--no-hip] [--sanitizers] [--fuzz]``
+``--image`` builds what the container image ships instead: ``_ksa_native`` alone, with the
+per-request HTTP timing diagnostics compiled out (``-DKSA_HTTP_TIMING=0``), and removes
+``_ksa_fakes`` from the package (Dockerfile).
+
+Usage: ``python -m kube_sqs_autoscaler_amd.ops.build [--no-hip] [--sanitizers] [--fuzz] [--image]``
 """
 from __future__ import annotations
 
@@ -29,6 +33,7 @@ import shutil
 import subprocess
 import sys
 import sysconfig
+import threading
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[2]
@@ -69,6 +74,11 @@ def _stale(target: Path, deps: list[Path], header_mtime: float) -> bool:
     return any(d.stat().st_mtime > t for d in deps) or header_mtime > t
 
 
+def _private(path: Path) -> Path:
+    """A per-process, per-thread temporary name next to `path` (then os.replace'd onto it)."""
+    return path.with_name(f"{path.name}.{os.getpid()}.{threading.get_ident()}.tmp")
+
+
 def _run(cmd: list[str]) -> None:
     proc = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
     if proc.returncode != 0:
@@ -84,10 +94,17 @@ def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: 
         obj = objdir / (src.stem + ".o")
         objs.append(obj)
         if _stale(obj, [src], hm):
-            todo.append([cxx or CXX, *CXXFLAGS, *extra, "-c", str(src), "-o", str(obj)])
+            todo.append((obj, [cxx or CXX, *CXXFLAGS, *extra, "-c", str(src), "-o"]))
     if todo:
+        def compile_one(obj: Path, cmd: list[str]) -> None:
+            # to a private name, then renamed: concurrent builds (test workers) never see a
+            # half-written object
+            tmp = _private(obj)
+            _run(cmd + [str(tmp)])
+            os.replace(tmp, obj)
+
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            for f in [ex.submit(_run, c) for c in todo]:
+            for f in [ex.submit(compile_one, o, c) for o, c in todo]:
                 f.result()
     return objs
 
@@ -95,21 +112,26 @@ def _compile_objects(variant: str, extra: list[str], sources: list[Path], jobs: 
 RELEASE_FLAGS = ["-fvisibility=hidden"]
 
 
-def _binding_object(name: str) -> Path:
+IMAGE_FLAGS = RELEASE_FLAGS + ["-DKSA_HTTP_TIMING=0"]
+
+
+def _binding_object(name: str, variant: str = "release", flags: list[str] = RELEASE_FLAGS) -> Path:
     import pybind11
 
     src = CSRC / "bindings" / f"{name}.cc"
-    obj = BUILD / "obj-release" / f"{name}.o"
+    obj = BUILD / f"obj-{variant}" / f"{name}.o"
     obj.parent.mkdir(parents=True, exist_ok=True)
     if _stale(obj, [src], _newest_header()):
-        _run([CXX, *CXXFLAGS, *RELEASE_FLAGS, f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
-              "-c", str(src), "-o", str(obj)])
+        tmp = _private(obj)
+        _run([CXX, *CXXFLAGS, *flags, f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+              "-c", str(src), "-o", str(tmp)])
+        os.replace(tmp, obj)
     return obj
 
 
 def _link(out: Path, inputs: list[Path], verbose: bool) -> None:
     if _stale(out, inputs, 0.0):
-        tmp = out.with_suffix(".tmp.so")
+        tmp = _private(out)
         _run([CXX, "-shared", "-o", str(tmp), *map(str, inputs), *LIBS])
         os.replace(tmp, out)
         if verbose:
@@ -123,14 +145,31 @@ def build_native(jobs: int = 8, verbose: bool = True) -> Path:
     return NATIVE_SO
 
 
+def build_image_runtime(jobs: int = 8, verbose: bool = True, out: Path = NATIVE_SO) -> Path:
+    """The image's runtime: ``_ksa_native`` with the HTTP timing diagnostics compiled out, and no
+    ``_ksa_fakes`` next to it. By default replaces the in-tree module and removes the in-tree
+    ``_ksa_fakes`` (run it last, in the image builder); ``out`` elsewhere leaves both alone."""
+    core = _compile_objects("image", IMAGE_FLAGS, _core_sources(), jobs)
+    inputs = core + [_binding_object("module", "image", IMAGE_FLAGS)]
+    tmp = _private(out)
+    _run([CXX, "-shared", "-o", str(tmp), *map(str, inputs), *LIBS])
+    os.replace(tmp, out)
+    if out == NATIVE_SO:
+        FAKES_SO.unlink(missing_ok=True)
+    if verbose:
+        print(f"[build] linked {out} (image: -DKSA_HTTP_TIMING=0, no _ksa_fakes)")
+    return out
+
+
 def build_fakes(jobs: int = 8, verbose: bool = True) -> Path:
     """Builds the test-doubles extension (``_ksa_fakes``) in place; returns its path. The core
     goes in as a static archive, so the module carries only the core objects the fakes use."""
     core = _compile_objects("release", RELEASE_FLAGS, _core_sources(), jobs)
     archive = BUILD / "obj-release" / "libksa_core.a"
     if _stale(archive, core, 0.0):
-        archive.unlink(missing_ok=True)
-        _run(["ar", "rcs", str(archive), *map(str, core)])
+        tmp = _private(archive)
+        _run(["ar", "rcs", str(tmp), *map(str, core)])
+        os.replace(tmp, archive)
     fakes = _compile_objects("release", RELEASE_FLAGS, _fakes_sources(), jobs)
     _link(FAKES_SO, fakes + [_binding_object("fakes_module"), archive], verbose)
     return FAKES_SO
@@ -203,8 +242,16 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--no-hip", action="store_true", help="skip the gfx950 probe")
     ap.add_argument("--sanitizers", action="store_true", help="also build ASan/UBSan and TSan test binaries")
     ap.add_argument("--fuzz", action="store_true", help="also build the libFuzzer wire-parser harness")
+    ap.add_argument("--image", action="store_true",
+                    help="build the image's runtime only: _ksa_native without HTTP timing, _ksa_fakes removed")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     args = ap.parse_args(argv)
+    if args.image:
+        out = {"native": str(build_image_runtime(jobs=args.jobs))}
+        if not args.no_hip:
+            out["gpu_probe"] = str(build_gpu_probe())
+        print(out)
+        return 0
     print(build_all(hip=not args.no_hip, jobs=args.jobs))
     if args.sanitizers:
         for s in (None, "asan", "tsan"):

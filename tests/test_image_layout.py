@@ -21,11 +21,24 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 AKID, SECRET, REGION, TOKEN = "AKIDIMAGE", "image/secret", "us-east-1", "image-token"
 
 
+@pytest.fixture(scope="module")
+def image_native(tmp_path_factory):
+    """_ksa_native as the image builders make it (`ops.build --image`: -DKSA_HTTP_TIMING=0),
+    built outside the tree (objects cached under build/obj-image)."""
+    from kube_sqs_autoscaler_amd.ops import build
+
+    out = tmp_path_factory.mktemp("image-native") / build.NATIVE_SO.name
+    return build.build_image_runtime(verbose=False, out=out)
+
+
 @pytest.fixture
-def image_root(nat, tmp_path):
+def image_root(nat, image_native, tmp_path):
+    """The slim image's /app: the package without the GPU probe, the test doubles
+    (_ksa_fakes) or the in-tree dev build of the runtime, plus the image build of _ksa_native."""
     app = tmp_path / "app"
     shutil.copytree(os.path.join(ROOT, "kube_sqs_autoscaler_amd"), app / "kube_sqs_autoscaler_amd",
-                    ignore=shutil.ignore_patterns("__pycache__", "libksa_gpu.so", "*.bin"))
+                    ignore=shutil.ignore_patterns("__pycache__", "libksa_gpu.so", "*.bin", "_ksa_fakes*", "_ksa_native*"))
+    shutil.copy(image_native, app / "kube_sqs_autoscaler_amd" / "ops" / image_native.name)
     deps = tmp_path / "dist-packages"
     deps.mkdir()
     d = os.path.dirname(yaml.__file__)
@@ -33,6 +46,28 @@ def image_root(nat, tmp_path):
     launcher = tmp_path / "kube-sqs-autoscaler"
     shutil.copy(os.path.join(ROOT, "deploy", "bin", "kube-sqs-autoscaler"), launcher)
     return tmp_path, launcher, f"{app}:{deps}"
+
+
+def test_image_runtime_carries_no_test_doubles_or_timing(image_native, image_root):
+    """What the image ships: no _ksa_fakes in the package; its _ksa_native links none of the
+    fakes (servers, in-memory API fakes) and has the HTTP timing diagnostics compiled out. The
+    in-tree dev build has no fakes either (they live in _ksa_fakes)."""
+    tmp, _, pythonpath = image_root
+    files = [f for _, _, fs in os.walk(tmp / "app") for f in fs]
+    assert not any(f.startswith("_ksa_fakes") for f in files)
+    syms = subprocess.run(["nm", "-C", str(image_native)], capture_output=True, text=True, check=True).stdout
+    for banned in ("FakeSqsServer", "FakeKubeServer", "FakeDeployments", "MockSqsApi", "TraceSqsApi",
+                   "HttpServer", "generate_self_signed", "enable_rx_timestamps"):
+        assert banned not in syms, banned
+    code = ("from kube_sqs_autoscaler_amd.ops import native; n = native(); assert n.__file__.startswith(%r); "
+            "print(n.HTTP_TIMING, sorted(a for a in dir(n) if a.startswith(('Fake', 'Mock', 'Trace', 'Injected'))))" % str(tmp))
+    r = subprocess.run([sys.executable, "-S", "-c", code], env={"PYTHONPATH": pythonpath, "KSA_NO_AUTOBUILD": "1"},
+                       capture_output=True, text=True, timeout=60, cwd=str(tmp))  # cwd: not the tree's copy
+    assert r.returncode == 0 and r.stdout.split() == ["False", "[]"], r.stdout + r.stderr
+    from kube_sqs_autoscaler_amd.ops import native
+
+    assert native().HTTP_TIMING is True
+    assert not [a for a in dir(native()) if a.startswith(("Fake", "Mock", "Trace", "Injected"))]
 
 
 def test_slim_image_layout_scales_with_only_its_runtime_packages(nat, image_root):
@@ -109,6 +144,7 @@ def test_slim_image_layout_scales_with_only_its_runtime_packages(nat, image_root
             outside.append(name)
         assert not outside, outside
         assert "prometheus_client" not in loaded and "torch" not in loaded
+        assert "kube_sqs_autoscaler_amd.ops._ksa_fakes" not in loaded
     finally:
         if p.poll() is None:
             p.kill()

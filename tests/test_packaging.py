@@ -37,19 +37,55 @@ def _docker_stages():
     return stages
 
 
+def _code(stage):
+    return [l for l in stage["body"] if l.strip() and not l.lstrip().startswith("#")]
+
+
 def test_default_image_is_slim_and_no_runtime_stage_is_a_dev_image():
-    """`docker build .` builds the last stage: the slim control-loop image. Only the builder
-    uses the ROCm dev image; the GPU image adds the HIP runtime package alone."""
+    """`docker build .` builds the last stage: the slim control-loop image. Only the GPU image's
+    builder uses the ROCm dev image; the GPU image adds the HIP runtime package alone."""
     stages = _docker_stages()
     assert stages[-1]["name"] == "slim"
-    runtime = [s for s in stages if s["name"] != "builder"]
+    runtime = [s for s in stages if not s["name"].endswith("builder")]
     assert all("dev" not in s["base"] for s in runtime)
-    assert not any("pip" in l for s in runtime for l in s["body"] if not l.lstrip().startswith("#"))
+    assert not any("pip" in l for s in runtime for l in _code(s))
     gpu = next(s for s in stages if s["name"] == "gpu")
     assert any("hip-runtime-amd" in l for l in gpu["body"])
-    base = next(s for s in stages if s["name"] == "base")
+    base = next(s for s in stages if s["name"] == "runtime")
     assert any("/kube-sqs-autoscaler /kube-sqs-autoscaler" in l for l in base["body"])  # the reference's command path
-    assert all(s["base"] == "base" for s in stages if s["name"] in ("gpu", "slim"))
+    assert all(s["base"] == "runtime" for s in stages if s["name"] in ("gpu", "slim"))
+
+
+def test_slim_stage_chain_never_references_rocm():
+    """The slim image and every stage it is built from or copies from (its builder included)
+    use no ROCm image or package: a CPU-only control loop needs no multi-GB toolchain."""
+    import re
+
+    stages = {s["name"]: s for s in _docker_stages()}
+    chain, todo = set(), ["slim"]
+    while todo:
+        name = todo.pop()
+        if name in chain or name not in stages:
+            continue
+        chain.add(name)
+        st = stages[name]
+        todo.append(st["base"])
+        todo += re.findall(r"--from=(\S+)", "".join(_code(st)))
+    assert chain == {"slim", "runtime", "slim-builder"}, chain
+    for name in chain:
+        st = stages[name]
+        assert "rocm" not in st["base"].lower(), name
+        assert not any(re.search(r"rocm|hipcc|hip-runtime|offload-arch", l, re.I) for l in _code(st)), name
+    # both builders ship the image runtime: timing compiled out, test doubles removed
+    for name in ("slim-builder", "gpu-builder"):
+        assert any("ops.build" in l and "--image" in l for l in _code(stages[name])), name
+
+
+def test_docker_context_excludes_host_built_libraries():
+    """COPY . /work must not carry a host-built .so (libksa_gpu.so, _ksa_fakes) into an image:
+    the builders compile everything from source."""
+    lines = [l.strip() for l in open(os.path.join(ROOT, ".dockerignore")) if l.strip() and not l.startswith("#")]
+    assert "**/*.so" in lines and "build" in lines
 
 
 def test_ci_workflow_runs_the_ci_gate():
