@@ -81,55 +81,75 @@ def _progress(msg: str) -> None:
 
 def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: float = float("inf")) -> dict:
     """Poll->patch latency at production poll periods (250 ms and 1 s; the reference's default
-    is 5 s, /root/reference/main.go:83): ``--cadence-queues`` queues, one thread each, staggered
-    over the period, against one endpoint process serving them all (bench/latency.py
-    ``measure_cadenced``). Default path (with the CLI's --poll-prewarm) and reference-equivalent
-    path, plain and TLS, with per-phase medians. The ``_hot_endpoints`` rows at 1 s serve the same
-    polls from endpoints that never sleep (a loaded production endpoint): the difference is what
-    the fakes' own idle wake-ups add. These rows run uninstrumented; the two ``_timed`` rows at 1 s
-    repeat the default path with every call broken down (HttpTiming on the client, per-request
-    wake-up and service times on the fakes) for the attribution -- the instrumentation adds a few
-    syscalls per request, so their p50 is not the row's number. Each row keeps >= 400 samples.
+    is 5 s, /root/reference/main.go:83), one thread per queue, staggered over the period, against
+    the ``split`` fake endpoints: one fake SQS process and one fake apiserver process serving
+    every queue, as production has two services (bench/latency.py ``measure_cadenced``). Default
+    path (with the CLI's --poll-prewarm) vs reference-equivalent path (full-Deployment GET+PUT,
+    sequential, no warm-up), in this order, most important first:
+
+    1. BASELINE's queue axis at 250 ms: 1, 2, 4 and 8 tracked queues, at least
+       ``--cadence-queue-samples`` scaling polls per row (``cadenced_p50_ms_by_tracked_queues``);
+    2. ``--cadence-queues`` queues at 250 ms, plain and TLS;
+    3. the same at 1 s, plain, and with endpoints that never sleep (``_hot_endpoints``, a loaded
+       production endpoint: the difference is what the fakes' own idle wake-ups add); the two
+       ``_timed`` rows repeat the default path with every call broken down (HttpTiming on the
+       client, per-request wake-up and service times on the fakes) for the attribution -- the
+       instrumentation adds a few syscalls per request, so their p50 is not the row's number.
+
     Rows that would start past ``deadline`` (time.monotonic) are skipped and listed."""
+    import math
+
     from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced
     from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS
 
     ms = 1_000_000
-    p50, rows = {}, {}
-    # (row, mode, pipelined, busy-poll, pre-poll warm-up): the CLI default, and the reference's path
+    skip = 2  # measure_cadenced drops each queue's first polls (dial, first allocations)
+    # (name, mode, pipelined, busy-poll, pre-poll warm-up): the CLI default, and the reference's path
     paths = (("default", args.mode, pipeline, bp, DEFAULT_POLL_PREWARM_NS), ("reference_equivalent", "deployment", False, 0, 0))
+    # plan rows: (group, period label, period ns, key, queues, polls per queue, path, tls, hot, timing)
     plan = []
+    for q in (1, 2, 4, 8):
+        polls = math.ceil(args.cadence_queue_samples / q) + skip
+        for path in paths:
+            plan.append(("by_queues", "250ms", 250 * ms, f"{path[0]}/{q}", q, polls, path, False, False, False))
     for label, period in (("250ms", 250 * ms), ("1s", 1000 * ms)):
-        for name, mode, pl, b, pw in paths:
+        for path in paths:
             for tls, hot in ((False, False), (True, False), (False, True)):
-                if hot and label != "1s":
+                if (tls and label != "250ms") or (hot and label != "1s"):
                     continue
-                key = name + ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
-                plan.append((label, period, key, mode, pl, b, pw, tls, hot, False))
-    name, mode, pl, b, pw = paths[0]
+                key = path[0] + ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
+                plan.append(("fleet", label, period, key, args.cadence_queues, args.cadence_polls, path, tls, hot, False))
     for hot in (False, True):
-        plan.append(("1s", 1000 * ms, name + ("_hot_endpoints" if hot else "") + "_timed", mode, pl, b, pw, False, hot,
-                     True))
+        plan.append(("fleet", "1s", 1000 * ms, paths[0][0] + ("_hot_endpoints" if hot else "") + "_timed",
+                     args.cadence_queues, args.cadence_polls, paths[0], False, hot, True))
     skipped = []
-    for label, period, key, mode, pl, b, pw, tls, hot, timing in plan:
+    p50, rows, by_q, by_q_samples = {}, {}, {}, {}
+    for group, label, period, key, queues, polls, (name, mode, pl, b, pw), tls, hot, timing in plan:
         if time.monotonic() > deadline:
             skipped.append(f"{label}/{key}")
             continue
-        r = measure_cadenced(period, args.cadence_polls, args.cadence_queues, mode, pl, b, tls, hot_endpoints=hot,
-                             prewarm_ns=pw, timing=timing)
-        rows.setdefault(label, {})[key] = r
-        if not timing:
-            p50.setdefault(label, {})[key] = r["p50_ms"]
-        _progress(f"cadence {label} {key}: p50 {r['p50_ms']} ms over {r['samples']} samples")
+        r = measure_cadenced(period, polls, queues, mode, pl, b, tls, skip=skip, hot_endpoints=hot, prewarm_ns=pw,
+                             timing=timing)
+        if group == "by_queues":
+            by_q.setdefault(name, {})[str(queues)] = r["p50_ms"]
+            by_q_samples.setdefault(name, {})[str(queues)] = r["samples"]
+        else:
+            rows.setdefault(label, {})[key] = r
+            if not timing:
+                p50.setdefault(label, {})[key] = r["p50_ms"]
+        _progress(f"cadence {label} {key}{' (' + str(queues) + ' queues)' if group == 'fleet' else ''}: "
+                  f"p50 {r['p50_ms']} ms over {r['samples']} samples")
     if skipped:
         _progress(f"cadence rows skipped (past --extras-budget-s): {skipped}")
     return {
         **({"cadenced_rows_skipped": skipped} if skipped else {}),
-        "cadenced_p50_ms": p50,
-        "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
         "cadenced_rows": rows,
+        "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
+        "cadenced_by_tracked_queues_samples": by_q_samples,
         "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()
                                                if "default" in v},
+        "cadenced_p50_ms": p50,
+        "cadenced_p50_ms_by_tracked_queues": {"250ms": by_q} if by_q else {},
     }
 
 
@@ -208,9 +228,11 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence-queues", type=int, default=16,
                     help="queues (one thread each, staggered) per production-cadence row")
     ap.add_argument("--cadence-polls", type=int, default=27,
-                    help="polls per queue per production-cadence row (the first 2 of each queue are dropped)")
+                    help="polls per queue per production-cadence fleet row (the first 2 of each queue are dropped)")
+    ap.add_argument("--cadence-queue-samples", type=int, default=200,
+                    help="scaling polls per row of the 250 ms 1/2/4/8-tracked-queue rows")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
-    ap.add_argument("--extras-budget-s", type=float, default=400.0,
+    ap.add_argument("--extras-budget-s", type=float, default=420.0,
                     help="seconds after start past which the remaining secondary sections and cadence rows are skipped "
                          "(recorded under extra.skipped_sections); the headline line is always printed")
     args = ap.parse_args(argv)
@@ -401,6 +423,11 @@ def main(argv=None) -> int:
             guarded("cadence_rows", lambda: extra.update(
                 _cadence_rows(args, pipeline, bp, p50, deadline=t_start + args.extras_budget_s)))
         guarded("decision_parity", parity, budgeted=False)  # seconds; part of the metric's name
+        # The driver keeps the tail of stdout: the per-row detail goes first, the summary rows last.
+        summary = ("wan_model_sqs2ms_kube1ms_p50_ms", "tls_p50_ms", "reference_equivalent_p50_ms",
+                   "sequential_scale_p50_ms", "p50_ms_by_tracked_queues_worker_processes", "p50_ms_by_tracked_queues",
+                   "cadenced_vs_hot_loop_default_plain", "cadenced_p50_ms", "cadenced_p50_ms_by_tracked_queues")
+        extra = {**{k: v for k, v in extra.items() if k not in summary}, **{k: extra[k] for k in summary if k in extra}}
         out = {
             "metric": METRIC,
             "value": round(p50, 4),

@@ -27,12 +27,14 @@ def main(argv=None) -> int:
     ap.add_argument("--kube-latency-ns", type=int, default=0)
     ap.add_argument("--cpus", default="", help="JSON list: the CPU list of each pair's threads")
     ap.add_argument("--queue-offset", type=int, default=0, help="number of the first bench queue served")
+    ap.add_argument("--only", default="both", choices=["both", "sqs", "kube"],
+                    help="serve one kind alone (the bench's split endpoints: SQS and the apiserver in two processes)")
     ap.add_argument("--hot", action="store_true", help="busy-polling servers that never sleep (HttpServer::set_hot)")
     ap.add_argument("--timing", action="store_true", help="record per-request timings (HttpServer::set_timing)")
     a = ap.parse_args(argv)
     cpus = json.loads(a.cpus) if a.cpus else None
     sqs, kube = start_fake_endpoints(a.queues, a.pairs, bool(a.tls), a.sqs_latency_ns, a.kube_latency_ns, cpus,
-                                     a.queue_offset, hot=a.hot, timing=a.timing)
+                                     a.queue_offset, hot=a.hot, timing=a.timing, only=a.only)
     try:
         info = {"pid": os.getpid(), "sqs": [{"url": s.url, "cert_pem": s.cert_pem} for s in sqs],
                 "kube": [{"url": k.url, "cert_pem": k.cert_pem} for k in kube]}
@@ -46,7 +48,7 @@ def main(argv=None) -> int:
                     "kube_connections": sum(k.connections() for k in kube),
                     "signature_failures": sum(s.signature_failures() for s in sqs),
                     "replicas": [kube[q % len(kube)].replicas("bench", deployment_name(a.queue_offset + q))
-                                 for q in range(a.queues)],
+                                 for q in range(a.queues)] if kube else [],
                 }), flush=True)
             elif cmd == "timings":
                 out = {"sqs": [t for s in sqs for t in s.timings()], "kube": [t for k in kube for t in k.timings()]}

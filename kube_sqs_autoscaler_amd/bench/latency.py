@@ -85,37 +85,43 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
 
 def start_fake_endpoints(queues: int, n_servers: int, tls: bool = False, sqs_latency_ns: int = 0,
                          kube_latency_ns: int = 0, cpus: Optional[List[List[int]]] = None, offset: int = 0,
-                         hot: bool = False, timing: bool = False):
+                         hot: bool = False, timing: bool = False, only: str = "both"):
     """``n_servers`` fake SQS + apiserver pairs serving ``queues`` bench queues numbered from
     ``offset`` (queue offset+q on pair q % n_servers): the 200 <-> 0 attribute cycle per queue
     and one Deployment per queue. ``cpus[i]``: the CPUs pair i's threads run on (None: unpinned).
     ``hot``: each server is one busy-polling thread that never sleeps (HttpServer::set_hot).
     ``timing``: the servers record each request's wake-up delay and service time
-    (HttpServer::set_timing; off by default, it adds two syscalls per request)."""
+    (HttpServer::set_timing; off by default, it adds two syscalls per request). ``only``:
+    ``sqs`` or ``kube`` starts that kind alone (the other list comes back empty)."""
+    if only not in ("both", "sqs", "kube"):
+        raise ValueError(f"only must be both, sqs or kube, not {only!r}")
     fk = fakes()
     sqs_servers, kube_servers = [], []
     for i in range(n_servers):
-        sqs = fk.FakeSqsServer()
-        sqs.require_signature(AKID, SECRET, REGION)
-        kube = fk.FakeKubeServer()
-        kube.require_token(TOKEN)
-        if cpus is not None:
-            sqs.set_cpus(cpus[i])
-            kube.set_cpus(cpus[i])
-        sqs.set_hot(hot)
-        kube.set_hot(hot)
-        sqs.set_timing(timing)
-        kube.set_timing(timing)
-        sqs.start("127.0.0.1", 0, tls)
-        sqs.set_latency(sqs_latency_ns)
-        kube.start("127.0.0.1", 0, tls)
-        kube.set_latency(kube_latency_ns)
-        sqs_servers.append(sqs)
-        kube_servers.append(kube)
+        servers = []
+        if only in ("both", "sqs"):
+            sqs = fk.FakeSqsServer()
+            sqs.require_signature(AKID, SECRET, REGION)
+            servers.append((sqs, sqs_latency_ns))
+            sqs_servers.append(sqs)
+        if only in ("both", "kube"):
+            kube = fk.FakeKubeServer()
+            kube.require_token(TOKEN)
+            servers.append((kube, kube_latency_ns))
+            kube_servers.append(kube)
+        for srv, latency in servers:
+            if cpus is not None:
+                srv.set_cpus(cpus[i])
+            srv.set_hot(hot)
+            srv.set_timing(timing)
+            srv.start("127.0.0.1", 0, tls)
+            srv.set_latency(latency)
     for q in range(queues):
         si = q % n_servers
-        sqs_servers[si].set_attribute_cycle(queue_url(sqs_servers[si].url, offset + q), [HIGH, LOW])
-        kube_servers[si].add_deployment("bench", deployment_name(offset + q), 1)
+        if sqs_servers:
+            sqs_servers[si].set_attribute_cycle(queue_url(sqs_servers[si].url, offset + q), [HIGH, LOW])
+        if kube_servers:
+            kube_servers[si].add_deployment("bench", deployment_name(offset + q), 1)
     return sqs_servers, kube_servers
 
 
@@ -141,7 +147,7 @@ class RemoteEndpoints:
 
     def __init__(self, queues: int, n_servers: int, tls: bool, sqs_latency_ns: int, kube_latency_ns: int,
                  cpus: Optional[List[List[int]]] = None, offset: int = 0, hot: bool = False,
-                 timing: bool = False):
+                 timing: bool = False, only: str = "both"):
         import json
         import subprocess
         import sys
@@ -152,7 +158,7 @@ class RemoteEndpoints:
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "kube_sqs_autoscaler_amd.bench.fakeserve", "--queues", str(queues), "--pairs",
              str(n_servers), "--tls", str(int(tls)), "--sqs-latency-ns", str(sqs_latency_ns), "--kube-latency-ns",
-             str(kube_latency_ns), "--queue-offset", str(offset), *extra], cwd=root, stdin=subprocess.PIPE,
+             str(kube_latency_ns), "--queue-offset", str(offset), "--only", only, *extra], cwd=root, stdin=subprocess.PIPE,
             stdout=subprocess.PIPE, text=True)
         line = self.proc.stdout.readline()
         if not line:
@@ -193,10 +199,11 @@ class BenchEnv:
 
     ``servers``: ``shared`` -- one fake SQS + apiserver pair in this process for every queue;
     ``per-queue`` -- one pair per queue, in this process; ``process`` -- one pair serving every
-    queue, in an endpoint process of its own (production's shape: every queue talks to the same
-    SQS endpoint and apiserver, which are other machines' processes); ``processes`` -- one
-    endpoint process per queue (as separate ranks see it: no two queues' endpoint threads share
-    a process).
+    queue, in an endpoint process of its own; ``split`` -- production's shape: one fake SQS
+    serving every queue in an endpoint process of its own and one apiserver in another (SQS and
+    the apiserver are different machines' processes, so the pipelined GET and the SQS request of
+    a poll are not served by one process's threads); ``processes`` -- one endpoint process per
+    queue (as separate ranks see it: no two queues' endpoint threads share a process).
 
     ``poll_period_ns``: every queue's ``--poll-period`` (0: back to back, the hot loop);
     ``stagger``: queue i of N starts i/N of a poll period late (Supervisor.stagger), so N
@@ -228,6 +235,11 @@ class BenchEnv:
                                           timing=timing)
             self.remotes = [self.remote]
             self.sqs_servers, self.kube_servers = self.remote.sqs, self.remote.kube
+        elif servers == "split":
+            self.remotes = [RemoteEndpoints(queues, 1, tls, sqs_latency_ns, kube_latency_ns, hot=hot_endpoints,
+                                            timing=timing, only=kind) for kind in ("sqs", "kube")]
+            self.remote = self.remotes[0]
+            self.sqs_servers, self.kube_servers = self.remotes[0].sqs, self.remotes[1].kube
         elif servers == "processes":
             self.remotes = [RemoteEndpoints(1, 1, tls, sqs_latency_ns, kube_latency_ns, offset=q, timing=timing)
                             for q in range(queues)]
@@ -239,7 +251,7 @@ class BenchEnv:
                                                                        kube_latency_ns, hot=hot_endpoints,
                                                                        timing=timing)
         else:
-            raise ValueError(f"servers must be shared, per-queue, process or processes, not {servers!r}")
+            raise ValueError(f"servers must be shared, per-queue, process, split or processes, not {servers!r}")
         self.sqs, self.kube = self.sqs_servers[0], self.kube_servers[0]
         self.clock = nat.RealClock()
         # one logger writing to one file, like the reference's global logrus logger
@@ -502,7 +514,7 @@ def _pct_ns(v: List[int], p: float) -> int:
 
 
 def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: str = "scale", pipeline: bool = True,
-                     busy_poll_ns: int = 0, tls: bool = False, skip: int = 2, servers: str = "process",
+                     busy_poll_ns: int = 0, tls: bool = False, skip: int = 2, servers: str = "split",
                      hot_endpoints: bool = False, prewarm_ns: int = 0, timing: bool = False) -> Dict:
     """Poll -> patch latency at a production poll cadence, not back to back.
 
@@ -512,7 +524,8 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
     connection unused for longer than ``kFreshConnNs`` gets the idle-close check again. The
     hot-loop rows measure none of that. Here ``queues`` queues (the default fleet: a thread
     each, staggered over the period) each run ``polls`` polls at ``poll_period_ns`` against
-    one endpoint process that serves them all; every poll scales (the 200/0 trace, zero
+    the ``split`` endpoints (one fake SQS process and one apiserver process serving them all, as
+    production has two services); every poll scales (the 200/0 trace, zero
     cool-downs). The first ``skip`` polls of each queue (dial, TLS handshake, first
     allocations) are dropped. Phases come from the per-poll spans (``--trace-file`` format).
     """

@@ -30,7 +30,7 @@ def test_fake_server_timings_only_when_enabled(nat, timing):
     assert all(wake >= 0 and service > 0 for wake, service in served["sqs"] + served["kube"])
 
 
-@pytest.mark.parametrize("servers", ["shared", "process"])
+@pytest.mark.parametrize("servers", ["shared", "process", "split"])
 def test_cadenced_rows_attribute_only_the_timed_runs(nat, servers):
     plain = measure_cadenced(20_000_000, 6, queues=4, busy_poll_ns=25_000, servers=servers, prewarm_ns=200_000)
     timed = measure_cadenced(20_000_000, 6, queues=4, busy_poll_ns=25_000, servers=servers, prewarm_ns=200_000,

@@ -112,7 +112,41 @@ def test_cadence_rows_past_their_deadline_are_skipped_and_named():
     sys.path.insert(0, ROOT)
     import bench
 
-    args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=1)
+    args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=1, cadence_queue_samples=4)
     out = bench._cadence_rows(args, True, 0, 0.02, deadline=0.0)
-    assert len(out["cadenced_rows_skipped"]) == 12 and "250ms/default" in out["cadenced_rows_skipped"]
+    assert len(out["cadenced_rows_skipped"]) == 18 and "250ms/default" in out["cadenced_rows_skipped"]
+    assert "250ms/reference_equivalent/8" in out["cadenced_rows_skipped"]
     assert out["cadenced_p50_ms"] == {} and out["cadenced_vs_hot_loop_default_plain"] == {}
+    assert out["cadenced_p50_ms_by_tracked_queues"] == {}
+
+
+@pytest.mark.slow
+def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
+    """BASELINE's 1/2/4/8 tracked queues at a 250 ms cadence, default vs reference-equivalent
+    path, each row with at least --cadence-queue-samples scaling polls (small here)."""
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from kube_sqs_autoscaler_amd.bench import latency
+
+    calls = []
+    real = latency.measure_cadenced
+
+    def fast(period, polls, queues, *a, **kw):  # the queue-axis rows only, at a 20 ms cadence
+        calls.append((period, polls, queues, a[0]))
+        return real(20_000_000, polls, queues, *a, **kw)
+
+    monkeypatch.setattr(latency, "measure_cadenced", fast)
+    args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=2, cadence_queue_samples=8)
+    import time
+
+    out = bench._cadence_rows(args, True, 25_000, 0.02, deadline=time.monotonic() + 120)
+    by_q = out["cadenced_p50_ms_by_tracked_queues"]["250ms"]
+    assert set(by_q) == {"default", "reference_equivalent"}
+    for name in by_q:
+        assert set(by_q[name]) == {"1", "2", "4", "8"} and all(v > 0 for v in by_q[name].values())
+        assert all(n >= 8 for n in out["cadenced_by_tracked_queues_samples"][name].values())
+    assert calls[0] == (250_000_000, 10, 1, "scale") and calls[1][3] == "deployment"
+    assert "cadenced_rows_skipped" not in out and set(out["cadenced_p50_ms"]) == {"250ms", "1s"}
+    assert list(out)[-1] == "cadenced_p50_ms_by_tracked_queues"
