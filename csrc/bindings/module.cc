@@ -801,6 +801,11 @@ PYBIND11_MODULE(_ksa_native, m) {
     d["iterations"] = s->iterations.load(std::memory_order_relaxed);
     return d;
   });
+  m.def("read_shared_worker_error", [ws](uintptr_t addr) {
+    const std::string t = read_shared_error(ws(addr));
+    return py::reinterpret_steal<py::str>(PyUnicode_DecodeUTF8(t.data(), static_cast<Py_ssize_t>(t.size()), "replace"));
+  });
+  m.def("write_shared_worker_error", [ws](uintptr_t addr, const std::string& t) { write_shared_error(ws(addr), t); });
   m.def("shared_worker_latencies", [ws](uintptr_t addr) {
     SharedWorkerState* s = ws(addr);
     const uint64_t n = s->counters[SharedWorkerState::kLatencySamples].load(std::memory_order_acquire);

@@ -326,8 +326,43 @@ SharedWorkerState* init_shared_worker_state(void* at) {
   s->control.store(SharedWorkerState::kWait, std::memory_order_relaxed);
   for (auto& v : s->lat_hist) v.store(0, std::memory_order_relaxed);
   for (auto& v : s->lat_ring) v.store(0, std::memory_order_relaxed);
+  s->error_seq.store(0, std::memory_order_relaxed);
+  s->error_len.store(0, std::memory_order_relaxed);
+  for (auto& v : s->error_words) v.store(0, std::memory_order_relaxed);
   std::atomic_thread_fence(std::memory_order_release);
   return s;
+}
+
+void write_shared_error(SharedWorkerState* s, const std::string& text) {
+  size_t n = std::min(text.size(), SharedWorkerState::kErrorBytes - 1);
+  if (n < text.size())  // cut at a UTF-8 character boundary
+    while (n > 0 && (static_cast<unsigned char>(text[n]) & 0xC0) == 0x80) --n;
+  const uint64_t seq = s->error_seq.load(std::memory_order_relaxed);
+  s->error_seq.store(seq + 1, std::memory_order_relaxed);  // odd: being written
+  std::atomic_thread_fence(std::memory_order_release);
+  for (size_t w = 0; w * 8 < n; ++w) {
+    uint64_t word = 0;
+    std::memcpy(&word, text.data() + w * 8, std::min<size_t>(8, n - w * 8));
+    s->error_words[w].store(word, std::memory_order_relaxed);
+  }
+  s->error_len.store(static_cast<uint32_t>(n), std::memory_order_relaxed);
+  s->error_seq.store(seq + 2, std::memory_order_release);
+}
+
+std::string read_shared_error(const SharedWorkerState* s) {
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    const uint64_t before = s->error_seq.load(std::memory_order_acquire);
+    if (before & 1) continue;  // the worker is mid-write
+    const size_t n = std::min<size_t>(s->error_len.load(std::memory_order_relaxed), SharedWorkerState::kErrorBytes - 1);
+    std::string out(n, '\0');
+    for (size_t w = 0; w * 8 < n; ++w) {
+      const uint64_t word = s->error_words[w].load(std::memory_order_relaxed);
+      std::memcpy(&out[w * 8], &word, std::min<size_t>(8, n - w * 8));
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (s->error_seq.load(std::memory_order_relaxed) == before) return out;
+  }
+  return "";
 }
 
 void Runner::mirror(const IterationRecord& r) {
@@ -336,6 +371,8 @@ void Runner::mirror(const IterationRecord& r) {
     std::lock_guard<std::mutex> lk(mu_);
     st = stats_;
   }
+  const bool good = r.depth_ok && r.up != Action::Failed && r.down != Action::Failed;
+  if (!good) write_shared_error(shared_, r.error);  // before the failure count that makes /readyz look
   using W = SharedWorkerState;
   auto put = [&](int i, uint64_t v) { shared_->counters[i].store(v, std::memory_order_relaxed); };
   put(W::kPolls, st.polls);

@@ -165,10 +165,23 @@ struct SharedWorkerState {
   std::atomic<int32_t> control;                   // parent -> worker
   alignas(64) std::atomic<uint64_t> lat_hist[kLatBuckets];  // per bucket (RunnerStats::latency_buckets)
   alignas(64) std::atomic<int64_t> lat_ring[kRing];
+  // The worker's last poll error (Runner::last_error), truncated to kErrorBytes - 1 bytes, for
+  // the parent's /readyz reason. A seqlock: error_seq is odd while the worker rewrites the text;
+  // the text is stored as relaxed atomic words, so a racing read is torn, never undefined, and is
+  // retried when the sequence moved (write_shared_error / read_shared_error).
+  static constexpr size_t kErrorBytes = 512;
+  alignas(64) std::atomic<uint64_t> error_seq;
+  std::atomic<uint32_t> error_len;
+  std::atomic<uint64_t> error_words[kErrorBytes / 8];
 };
 static_assert(std::atomic<int64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
 // Zero-initialises a SharedWorkerState in place (memory from a fresh shared mapping).
 SharedWorkerState* init_shared_worker_state(void* at);
+// The error slot of a SharedWorkerState: the worker (single writer) stores its last poll error,
+// the supervising process reads it. read_shared_error returns "" when it could not get a
+// consistent copy within a few retries (the worker rewriting it continuously).
+void write_shared_error(SharedWorkerState* s, const std::string& text);
+std::string read_shared_error(const SharedWorkerState* s);
 
 // The OS thread a Runner's loop runs on, kept for the Runner's lifetime across Supervisor runs
 // (named ksa-worker). glibc gives every thread a malloc arena of its own and hands the arena of

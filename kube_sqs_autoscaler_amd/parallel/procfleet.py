@@ -81,7 +81,9 @@ class SlotRunner:
         return max(0, time.monotonic_ns() - st["last_good_ns"])
 
     def last_error(self) -> str:
-        return ""  # the text stays in the worker process (its log has it)
+        """The worker's last poll error, as the thread fleet's Runner.last_error() gives it
+        (carried through the shared slot, truncated to 511 bytes)."""
+        return native().read_shared_worker_error(self._addr)
 
 
 class ProcWorker:

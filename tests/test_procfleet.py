@@ -191,3 +191,80 @@ def test_a_dead_worker_process_brings_the_fleet_down(servers):
     n = sqs.requests()
     time.sleep(0.2)
     assert sqs.requests() == n  # the surviving workers were stopped too
+
+
+@pytest.mark.parametrize("fleet_kind", ["threads", "processes"])
+def test_readyz_reports_the_last_error_for_both_fleets(nat, servers, fleet_kind):
+    """--readiness-failure-window with persistent failures: /readyz's 503 reason carries the
+    worker's last poll error whether the queue runs on a thread (Runner.last_error) or in a
+    worker process (the error text crosses the shared slot's seqlock), and the text is the same."""
+    import urllib.error
+    import urllib.request
+
+    from kube_sqs_autoscaler_amd import autoscaler
+    from kube_sqs_autoscaler_amd.config import parse_args
+    from kube_sqs_autoscaler_amd.metrics import Health, MetricsServer
+    from kube_sqs_autoscaler_amd.parallel.fleet import Fleet
+    from kube_sqs_autoscaler_amd.utils.log import make_logger
+
+    sqs, kube, env = servers
+    specs = _specs(sqs, kube, ["500"])
+    sqs.inject(1_000_000, nat.InjectedFault(403, "<ErrorResponse><Error><Type>Sender</Type><Code>AccessDenied</Code>"
+                                                 "<Message>not authorized</Message></Error></ErrorResponse>", "text/xml"))
+    cfg = parse_args([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=5ms", *specs], env)
+    rest = autoscaler.load_rest_config(cfg, env)
+    log = make_logger("fatal", "text")
+    build = lambda t: autoscaler.new_runner(t, cfg, rest, log, nat.RealClock(), environ=env)  # noqa: E731
+    if fleet_kind == "processes":
+        fleet = ProcessFleet([lambda t=t: build(t) for t in cfg.targets], cfg.targets)
+    else:
+        fleet = Fleet([build(t) for t in cfg.targets])
+    health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets],
+                    failure_window_ns=100_000_000)
+    m = MetricsServer(fleet, "127.0.0.1:0", health)
+    m.start()
+
+    def readyz():
+        try:
+            r = urllib.request.urlopen(f"http://127.0.0.1:{m.port}/readyz")
+            return r.status, r.read().decode()
+        except urllib.error.HTTPError as e:
+            return e.code, e.read().decode()
+
+    try:
+        fleet.start()
+        deadline = time.time() + 20
+        while "every poll failed" not in readyz()[1]:
+            assert time.time() < deadline, readyz()
+            time.sleep(0.02)
+        code, why = readyz()
+        assert code == 503
+        assert "; last error: Failed to get messages in SQS: AccessDenied: not authorized" in why, why
+        err = fleet.workers[0].runner.last_error()
+        assert err.startswith("Failed to get messages in SQS: AccessDenied: not authorized") and err in why
+    finally:
+        fleet.stop()
+        fleet.join()
+        m.stop()
+        if fleet_kind == "processes":
+            fleet.close()
+
+
+def test_shared_error_slot_truncates_on_a_character_boundary(nat):
+    """The worker-process error slot keeps at most 511 bytes and never splits a UTF-8 character."""
+    import mmap
+
+    buf = mmap.mmap(-1, nat.shared_worker_state_size())
+    import ctypes
+
+    addr = ctypes.addressof(ctypes.c_char.from_buffer(buf))
+    nat.init_shared_worker_state(addr)
+    assert nat.read_shared_worker_error(addr) == ""
+    nat.write_shared_worker_error(addr, "short error")
+    assert nat.read_shared_worker_error(addr) == "short error"
+    text = "x" * 510 + "é" + "tail"  # the 2-byte character straddles byte 511
+    nat.write_shared_worker_error(addr, text)
+    assert nat.read_shared_worker_error(addr) == "x" * 510
+    nat.write_shared_worker_error(addr, "later")  # a shorter text replaces a longer one
+    assert nat.read_shared_worker_error(addr) == "later"
+    del addr
