@@ -397,6 +397,8 @@ PYBIND11_MODULE(_ksa_native, m) {
            py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""),
            py::arg("timeout_ns") = -1)
       .def("set_busy_poll", &HttpClient::set_busy_poll)
+      .def("warm", &HttpClient::warm, py::arg("dial_budget_ns") = HttpClient::kWarmDialBudget,
+           py::call_guard<py::gil_scoped_release>())
       .def("set_proxy",
            [](HttpClient& c, const std::string& url) {
              Status s = c.set_proxy(url);

@@ -647,6 +647,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   conn_->rbuf = std::move(rbuf);
   if (timing()) conn_->stream->enable_rx_timestamps();
   stats_.connects++;
+  warm_dial_failed_ = false;  // reachable again: warm-ups may dial
   return Status::OK();
 }
 
@@ -669,7 +670,7 @@ bool HttpClient::fresh_locked() const {
                    (conn_->last_checked_ns > 0 && now - conn_->last_checked_ns < kFreshConnNs));
 }
 
-bool HttpClient::warm() {
+bool HttpClient::warm(Nanos dial_budget) {
   std::lock_guard<std::mutex> lk(mu_);
   if (in_flight_ || cancelled()) return false;
   if (fresh_locked()) return true;
@@ -677,7 +678,14 @@ bool HttpClient::warm() {
     stats_.idle_closed++;
     conn_.reset();
   }
-  if (!conn_ && !connect_locked(timeout_ > 0 ? mono_ns() + timeout_ : 0).ok()) return false;
+  if (!conn_) {
+    if (warm_dial_failed_) return false;  // the endpoint is down: the request dials
+    const Nanos budget = timeout_ > 0 ? std::min(timeout_, dial_budget) : dial_budget;
+    if (!connect_locked(mono_ns() + std::max<Nanos>(budget, 0)).ok()) {
+      warm_dial_failed_ = true;
+      return false;
+    }
+  }
   conn_->last_checked_ns = mono_ns();
   return true;
 }

@@ -124,11 +124,16 @@ int64_t realtime_ns() {
   return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
 }
 
-// Blocks until `fd` is readable; returns the kernel receive time (CLOCK_REALTIME ns) of the
-// first queued byte, 0 when the socket reports none (closed, or timestamps unavailable).
-int64_t wait_rx_timestamp(int fd) {
-  struct pollfd p = {fd, POLLIN, 0};
-  while (::poll(&p, 1, -1) < 0 && errno == EINTR) {
+// The kernel receive time (CLOCK_REALTIME ns) of the first queued byte of `fd`, 0 when there is
+// none (closed, nothing queued, or timestamps unavailable). `block`: wait until `fd` is readable
+// first (a connection thread, which has nothing else to do); the hot loop peeks without waiting
+// -- an epoll event can carry no request (a TLS handshake record) and the single thread must
+// not stall on it.
+int64_t wait_rx_timestamp(int fd, bool block) {
+  if (block) {
+    struct pollfd p = {fd, POLLIN, 0};
+    while (::poll(&p, 1, -1) < 0 && errno == EINTR) {
+    }
   }
   char c;
   struct iovec iov = {&c, 1};
@@ -201,7 +206,7 @@ void HttpServer::serve(int fd) {
       int64_t rx = 0, t_read = 0;
       if (timing_.load(std::memory_order_relaxed)) {
         if (!stamps_tried) arm_stamps();
-        if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd);
+        if (stamps && rbuf.empty() && !(ssl && SSL_pending(ssl) > 0)) rx = wait_rx_timestamp(fd, true);
         t_read = realtime_ns();
       }
       std::string head;
@@ -398,7 +403,7 @@ void HttpServer::hot_loop() {
           cn.stamps = setsockopt(fd, SOL_SOCKET, SO_TIMESTAMPNS, &on, sizeof on) == 0;
           cn.stamps_tried = true;
         }
-        if (cn.stamps && cn.rbuf.empty() && !(cn.ssl && SSL_pending(cn.ssl) > 0)) rx = wait_rx_timestamp(fd);
+        if (cn.stamps && cn.rbuf.empty() && !(cn.ssl && SSL_pending(cn.ssl) > 0)) rx = wait_rx_timestamp(fd, false);
         t_read = realtime_ns();
       }
       bool closed = false;
@@ -481,6 +486,12 @@ void HttpServer::stop() {
   if (stopping_.exchange(true)) return;
   if (listen_fd_ >= 0) {
     ::shutdown(listen_fd_, SHUT_RDWR);
+  }
+  {
+    // before joining the acceptor: in hot mode it is the thread serving the connections, and
+    // a connection thread may be waiting on an idle client; shutting the sockets down wakes both
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int fd : open_fds_) ::shutdown(fd, SHUT_RDWR);
   }
   if (acceptor_.joinable()) acceptor_.join();
   if (listen_fd_ >= 0) {

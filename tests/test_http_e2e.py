@@ -664,3 +664,38 @@ def test_pipelined_get_never_dials_inside_the_sqs_call(nat, sqs_server):
         assert time.perf_counter() - t0 < 10
     finally:
         tarpit.close()
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_timed_tls_server_serves_and_stops_with_an_idle_client(nat, hot):
+    """A client that finished its TLS handshake and sent nothing yet (a connection dialled ahead
+    by --poll-prewarm) must neither hold up the hot server's single thread nor its stop(): the
+    hot loop only peeks for the receive stamp, and stop() shuts client sockets down before it
+    joins the serving thread."""
+    import socket
+    import ssl
+    import threading
+    import time
+
+    srv = nat.FakeKubeServer()
+    srv.set_hot(hot)
+    srv.set_timing(True)
+    srv.start("127.0.0.1", 0, True)
+    srv.add_deployment("ns", "d", 3)
+    ctx = ssl.create_default_context()
+    ctx.check_hostname = False
+    ctx.verify_mode = ssl.CERT_NONE
+    idle = ctx.wrap_socket(socket.create_connection(("127.0.0.1", srv.port)))  # handshake done, no request
+    try:
+        tls = nat.TlsOptions()
+        tls.ca_pem = srv.cert_pem
+        c = nat.HttpClient(srv.url, tls, 5 * nat.SECOND)
+        t0 = time.monotonic()
+        status, _, _ = c.request("GET", "/apis/apps/v1/namespaces/ns/deployments/d")
+        assert status in (200, 401) and time.monotonic() - t0 < 2.0
+        c.close()
+        done = threading.Event()
+        threading.Thread(target=lambda: (srv.stop(), done.set()), daemon=True).start()
+        assert done.wait(10), "stop() hung on an idle client"
+    finally:
+        idle.close()
