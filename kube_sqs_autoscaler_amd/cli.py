@@ -77,7 +77,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     # kubesqs.NewSqsClient -> sqs.New(session.Must(session.NewSession()), ...) (sqs/sqs.go:36):
     # the session's configuration is checked now; credentials are still fetched on first use.
     try:
-        validate_session(env)
+        for w in validate_session(env):
+            log.log("warning", f"AWS shared config: {w}")
     except SessionError as e:
         return _panic(str(e))
 

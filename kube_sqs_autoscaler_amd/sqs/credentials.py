@@ -28,7 +28,6 @@ when the cached keys are within 5 minutes of expiry or after an ``ExpiredToken``
 """
 from __future__ import annotations
 
-import configparser
 import json
 import os
 import re
@@ -41,6 +40,7 @@ from datetime import datetime, timezone
 from typing import Callable, Dict, List, Mapping, Optional, Tuple
 
 from ..ops import native
+from . import ini
 from ..utils import proxy
 
 ECS_HOST = "http://169.254.170.2"
@@ -132,12 +132,11 @@ class SharedFileProvider(_Provider):
     def _section(self) -> Optional[Mapping[str, str]]:
         if not os.path.exists(self.path):
             return None
-        cp = configparser.RawConfigParser()
         try:
-            cp.read(self.path)
-        except configparser.Error as e:
+            cp = ini.read(self.path)
+        except ini.IniError as e:
             raise CredentialsError(f"SharedCredsLoad: failed to load shared credentials file: {e}")
-        if not cp.has_section(self.profile):
+        if cp is None or not cp.has_section(self.profile):
             return None
         return dict(cp.items(self.profile))
 
@@ -401,19 +400,17 @@ def load_profiles(environ: Mapping[str, str]) -> Dict[str, Dict[str, str]]:
     out: Dict[str, Dict[str, str]] = {}
     if _truthy(environ.get("AWS_SDK_LOAD_CONFIG")):
         cfg_path = environ.get("AWS_CONFIG_FILE") or os.path.join(home, ".aws", "config")
-        cp = configparser.RawConfigParser()
         try:
-            cp.read(cfg_path)
-        except configparser.Error as e:
+            cp = ini.read(cfg_path) or ini.IniFile(cfg_path)
+        except ini.IniError as e:
             raise CredentialsError(f"SharedConfigLoadError: failed to load config file {cfg_path}: {e}")
         for sec in cp.sections():
             name = sec[len("profile "):].strip() if sec.startswith("profile ") else sec
             out.setdefault(name, {}).update(dict(cp.items(sec)))
     cred_path = environ.get("AWS_SHARED_CREDENTIALS_FILE") or os.path.join(home, ".aws", "credentials")
-    cp = configparser.RawConfigParser()
     try:
-        cp.read(cred_path)
-    except configparser.Error as e:
+        cp = ini.read(cred_path) or ini.IniFile(cred_path)
+    except ini.IniError as e:
         raise CredentialsError(f"SharedCredsLoad: failed to load shared credentials file: {e}")
     for sec in cp.sections():
         out.setdefault(sec, {}).update(dict(cp.items(sec)))

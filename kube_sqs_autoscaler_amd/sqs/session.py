@@ -24,15 +24,19 @@ instead of logging one error per poll. aws-sdk-go v1.35.35's checks (go.mod:6), 
    ``AWS_SDK_LOAD_CONFIG``) must hold at least one certificate.
 
 Error texts are the SDK's (``awserr``: ``Code: message`` plus ``\\ncaused by: <cause>``). The
-cause of a shared-file parse error is this parser's wording, not the SDK's ini parser's (parity
-unpinned: no Go toolchain to compare against); the code, message and file name are the SDK's.
+shared files are read by :mod:`.ini`, which fails only on a section header without its ``]``
+and skips (with a warning the CLI logs) lines it cannot use -- which malformed files the SDK's
+own ini parser rejects is parity unpinned, and crash-looping on a file the reference loads
+would be the worse error. The cause of a parse error is this parser's wording; the code,
+message and file name are the SDK's.
 """
 from __future__ import annotations
 
-import configparser
 import os
 import ssl
 from typing import Dict, List, Mapping, Optional, Tuple
+
+from . import ini
 
 
 class SessionError(Exception):
@@ -71,20 +75,12 @@ def _go_errno_text(e: OSError) -> str:
     return msg[:1].lower() + msg[1:]
 
 
-def _read_ini(path: str) -> Optional[configparser.RawConfigParser]:
+def _read_ini(path: str) -> Optional[ini.IniFile]:
     """A shared file, or None when it cannot be read (the SDK skips such files)."""
     try:
-        with open(path, "r", encoding="utf-8", errors="replace") as f:
-            text = f.read()
-    except OSError:
-        return None
-    cp = configparser.RawConfigParser(strict=False, interpolation=None)
-    try:
-        cp.read_string(text, source=path)
-    except configparser.Error as e:
-        cause = str(e).replace("\n", " ")
-        raise SessionError(f"SharedConfigLoadError: failed to load config file, {path}\ncaused by: {cause}")
-    return cp
+        return ini.read(path)
+    except ini.IniError as e:
+        raise SessionError(f"SharedConfigLoadError: failed to load config file, {path}\ncaused by: {e}")
 
 
 _REGIONAL = ("legacy", "regional")
@@ -135,7 +131,7 @@ def _pem_has_certificate(data: bytes) -> bool:
             continue
 
 
-def _profile(name: str, files: List[Tuple[str, configparser.RawConfigParser]], ex_opts: bool,
+def _profile(name: str, files: List[Tuple[str, ini.IniFile]], ex_opts: bool,
              seen: set) -> Optional[Dict[str, str]]:
     """``sharedConfig.setFromIniFiles``: the profile's options merged over the files (None if no
     file has it), with the assume-role checks. Raises SessionError."""
@@ -232,17 +228,20 @@ def custom_ca_bundle(environ: Mapping[str, str]) -> str:
     return (prof or {}).get("ca_bundle", "")
 
 
-def validate_session(environ: Mapping[str, str]) -> None:
-    """Raises :class:`SessionError` where ``session.NewSession()`` would fail."""
+def validate_session(environ: Mapping[str, str]) -> List[str]:
+    """Raises :class:`SessionError` where ``session.NewSession()`` would fail; returns the
+    shared files' skipped-line warnings (:mod:`.ini`) for the caller to log."""
     _check_env(environ)
     env_ca = environ.get("AWS_CA_BUNDLE", "")
     ca_data = _open_ca(env_ca) if env_ca else None
     ex_opts = load_config_enabled(environ)
     files = []
+    warnings: List[str] = []
     for path in shared_files(environ):
         cp = _read_ini(path)
         if cp is not None:
             files.append((path, cp))
+            warnings += cp.warnings
     prof: Optional[Dict] = None
     try:
         prof = _profile(session_profile(environ), files, ex_opts, set())
@@ -263,3 +262,4 @@ def validate_session(environ: Mapping[str, str]) -> None:
         ca_data = _open_ca(prof["ca_bundle"])
     if ca_data is not None and not _pem_has_certificate(ca_data):
         raise SessionError("LoadCustomCABundleError: failed to load custom CA bundle PEM file")
+    return warnings

@@ -70,17 +70,48 @@ def test_ca_bundle(home, tmp_path, nat):
 
 
 def test_unparsable_shared_files(home, tmp_path):
+    """Only a section header without its ']' fails the session (the SDK's lexer cannot get past
+    it either); the config file is only read with AWS_SDK_LOAD_CONFIG."""
     bad = tmp_path / "bad"
-    bad.write_text("aws_access_key_id = outside any section\n")
+    bad.write_text("[default\naws_access_key_id = AKID\n")
     with pytest.raises(SessionError) as e:
         validate_session({**home, "AWS_SHARED_CREDENTIALS_FILE": str(bad)})
     assert str(e.value).startswith(f"SharedConfigLoadError: failed to load config file, {bad}\ncaused by: ")
+    assert "section header without a closing ']'" in str(e.value)
     # the config file is only read with AWS_SDK_LOAD_CONFIG (Go ParseBool: "yes" is false)
     env = {**home, "AWS_CONFIG_FILE": str(bad)}
     validate_session(env)
     validate_session({**env, "AWS_SDK_LOAD_CONFIG": "yes"})
     with pytest.raises(SessionError, match="SharedConfigLoadError"):
         validate_session({**env, "AWS_SDK_LOAD_CONFIG": "1"})
+
+
+@pytest.mark.parametrize("text,warned", [
+    ("aws_access_key_id = outside any section\n[default]\naws_access_key_id = A\naws_secret_access_key = S\n",
+     "key outside any [section]"),
+    ("[default]\nnot an assignment\naws_access_key_id = A\naws_secret_access_key = S\n", "not a key = value line"),
+    ("# comment\n; comment\n\n[default]\naws_access_key_id = A ; inline text stays in the value\n"
+     "aws_secret_access_key: S\n[default]\ns3 =\n  max_concurrent_requests = 10\n", None),
+])
+def test_shared_files_the_sdk_may_accept_are_loaded_with_warnings(home, tmp_path, text, warned):
+    """Constructs the SDK's ini parser may well accept (parity unpinned: no SDK here) do not
+    crash-loop the pod: the unusable lines are skipped and reported as warnings, and the rest of
+    the file -- here the default profile's keys -- is used."""
+    from kube_sqs_autoscaler_amd.sqs import ini
+
+    f = tmp_path / "credentials"
+    f.write_text(text)
+    warnings = validate_session({**home, "AWS_SHARED_CREDENTIALS_FILE": str(f)})
+    if warned:
+        assert len(warnings) == 1 and warned in warnings[0] and str(f) in warnings[0]
+    else:
+        assert warnings == []
+    parsed = ini.read(str(f))
+    d = dict(parsed.items("default"))
+    assert d["aws_access_key_id"].startswith("A") and d["aws_secret_access_key"] == "S"
+    if warned is None:
+        assert d["aws_access_key_id"] == "A ; inline text stays in the value"
+        assert d["s3"] == "\nmax_concurrent_requests = 10"
 
 
 def test_profile_checks_with_load_config(home, tmp_path):
@@ -168,7 +199,7 @@ def _run(tmp_path, extra):
 
 def test_cli_panics_on_bad_session(tmp_path):
     bad = tmp_path / "credentials"
-    bad.write_text("not an ini file\n")
+    bad.write_text("[default\nnot an ini file\n")
     cases = [
         ({"AWS_SHARED_CREDENTIALS_FILE": str(bad)}, "panic: SharedConfigLoadError: failed to load config file, "),
         ({"AWS_CONFIG_FILE": str(bad), "AWS_SDK_LOAD_CONFIG": "1"}, "panic: SharedConfigLoadError: failed to load config file, "),
