@@ -1019,6 +1019,32 @@ TEST(exec_provider_shared_across_threads) {
 
 }  // namespace
 
+// The worker-process error slot (SharedWorkerState, seqlock over relaxed atomic words): a reader
+// racing the writer gets one of the texts written, whole, or "" -- never a mix (TSan-clean: every
+// shared access is atomic).
+TEST(shared_error_slot_seqlock) {
+  alignas(64) static unsigned char mem[sizeof(SharedWorkerState)];
+  SharedWorkerState* s = init_shared_worker_state(mem);
+  CHECK(read_shared_error(s).empty());
+  const std::string a(300, 'a'), b = "short b error", c(600, 'c');
+  std::atomic<bool> done{false};
+  std::thread writer([&] {
+    for (int i = 0; i < 20000; ++i) write_shared_error(s, i % 3 == 0 ? a : i % 3 == 1 ? b : c);
+    done = true;
+  });
+  const std::string c_cut(SharedWorkerState::kErrorBytes - 1, 'c');
+  long reads = 0, bad = 0;
+  while (!done.load()) {
+    const std::string t = read_shared_error(s);
+    ++reads;
+    if (!(t.empty() || t == a || t == b || t == c_cut)) ++bad;
+  }
+  writer.join();
+  CHECK(bad == 0);
+  CHECK(reads > 0);
+  CHECK(read_shared_error(s) == b || read_shared_error(s) == a || read_shared_error(s) == c_cut);
+}
+
 int main() {
   for (auto& t : registry()) {
     int before = g_failed;
