@@ -43,11 +43,11 @@ def test_cli_gpu_aware_max_local(tmp_path, capfd):
     import yaml
 
     from kube_sqs_autoscaler_amd.cli import main
-    from kube_sqs_autoscaler_amd.ops import gpu, native
+    from kube_sqs_autoscaler_amd.ops import fakes, gpu
 
-    nat = native()
+    fk = fakes()
     n_gpus = gpu.device_count()
-    sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs, kube = fk.FakeSqsServer(), fk.FakeKubeServer()
     sqs.start()
     kube.start()
     try:
@@ -83,11 +83,11 @@ def test_cli_gpu_aware_max_local_with_worker_processes(tmp_path):
 
     import yaml
 
-    from kube_sqs_autoscaler_amd.ops import gpu, native
+    from kube_sqs_autoscaler_amd.ops import fakes, gpu
 
-    nat = native()
+    fk = fakes()
     n_gpus = gpu.device_count()
-    sqs, kube = nat.FakeSqsServer(), nat.FakeKubeServer()
+    sqs, kube = fk.FakeSqsServer(), fk.FakeKubeServer()
     sqs.start()
     kube.start()
     p = None
