@@ -83,62 +83,62 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     """Poll->patch latency at production poll periods (250 ms and 1 s; the reference's default
     is 5 s, /root/reference/main.go:83), one thread per queue, staggered over the period, against
     the ``split`` fake endpoints: one fake SQS process and one fake apiserver process serving
-    every queue, as production has two services (bench/latency.py ``measure_cadenced``). Default
-    path (with the CLI's --poll-prewarm) vs reference-equivalent path (full-Deployment GET+PUT,
-    sequential, no warm-up), in this order, most important first:
+    every queue, as production has two services (bench/latency.py ``measure_cadenced_arms``).
+    Every row runs the default path (with the CLI's --poll-prewarm) and the reference-equivalent
+    path (full-Deployment GET+PUT, sequential, no warm-up) as paired arms of ONE run, their
+    queues interleaved: a box's idle-state and frequency behaviour drifts between runs and moved
+    single-path runs of one path by 2x (profiles/r04c_cadence_probe.jsonl), so paths compared in
+    separate runs could invert by chance. In this order, most important first:
 
-    1. BASELINE's queue axis at 250 ms: 1, 2, 4 and 8 tracked queues, at least
-       ``--cadence-queue-samples`` scaling polls per row (``cadenced_p50_ms_by_tracked_queues``);
-    2. ``--cadence-queues`` queues at 250 ms, plain and TLS;
-    3. the same at 1 s, plain, and with endpoints that never sleep (``_hot_endpoints``, a loaded
-       production endpoint: the difference is what the fakes' own idle wake-ups add); the two
-       ``_timed`` rows repeat the default path with every call broken down (HttpTiming on the
-       client, per-request wake-up and service times on the fakes) for the attribution -- the
-       instrumentation adds a few syscalls per request, so their p50 is not the row's number.
+    1. BASELINE's queue axis at 250 ms: 1, 2, 4 and 8 tracked queues per path, at least
+       ``--cadence-queue-samples`` scaling polls per path (``cadenced_p50_ms_by_tracked_queues``);
+    2. ``--cadence-queues`` queues per path at 250 ms, plain and TLS;
+    3. the same at 1 s, plain, TLS, and with endpoints that never sleep (``_hot_endpoints``, a
+       loaded production endpoint: the difference is what the fakes' own idle wake-ups add);
+       the ``_timed`` rows repeat the plain and hot rows with every call broken down (HttpTiming
+       on the client, per-request wake-up and service times on the fakes) for the attribution --
+       the instrumentation adds a few syscalls per request, so their p50 is not the row's number.
 
     Rows that would start past ``deadline`` (time.monotonic) are skipped and listed."""
     import math
 
-    from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced
+    from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced_arms
     from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS
 
     ms = 1_000_000
-    skip = 2  # measure_cadenced drops each queue's first polls (dial, first allocations)
-    # (name, mode, pipelined, busy-poll, pre-poll warm-up): the CLI default, and the reference's path
-    paths = (("default", args.mode, pipeline, bp, DEFAULT_POLL_PREWARM_NS), ("reference_equivalent", "deployment", False, 0, 0))
-    # plan rows: (group, period label, period ns, key, queues, polls per queue, path, tls, hot, timing)
+    skip = 2  # each queue's first polls (dial, first allocations) are dropped
+    arms = {"default": dict(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp, prewarm_ns=DEFAULT_POLL_PREWARM_NS),
+            "reference_equivalent": dict(mode="deployment", pipeline=False, busy_poll_ns=0, prewarm_ns=0)}
+    # plan rows: (group, period label, period ns, suffix, queues per arm, polls per queue, tls, hot, timing)
     plan = []
     for q in (1, 2, 4, 8):
-        polls = math.ceil(args.cadence_queue_samples / q) + skip
-        for path in paths:
-            plan.append(("by_queues", "250ms", 250 * ms, f"{path[0]}/{q}", q, polls, path, False, False, False))
-    for label, period in (("250ms", 250 * ms), ("1s", 1000 * ms)):
-        for path in paths:
-            for tls, hot in ((False, False), (True, False), (False, True)):
-                if (tls and label != "250ms") or (hot and label != "1s"):
-                    continue
-                key = path[0] + ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
-                plan.append(("fleet", label, period, key, args.cadence_queues, args.cadence_polls, path, tls, hot, False))
+        plan.append(("by_queues", "250ms", 250 * ms, f"/{q}", q, math.ceil(args.cadence_queue_samples / q) + skip,
+                     False, False, False))
+    for label, period, variants in (("250ms", 250 * ms, ((False, False), (True, False))),
+                                    ("1s", 1000 * ms, ((False, False), (True, False), (False, True)))):
+        for tls, hot in variants:
+            suffix = ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
+            plan.append(("fleet", label, period, suffix, args.cadence_queues, args.cadence_polls, tls, hot, False))
     for hot in (False, True):
-        plan.append(("fleet", "1s", 1000 * ms, paths[0][0] + ("_hot_endpoints" if hot else "") + "_timed",
-                     args.cadence_queues, args.cadence_polls, paths[0], False, hot, True))
+        plan.append(("fleet", "1s", 1000 * ms, ("_hot_endpoints" if hot else "") + "_timed", args.cadence_queues,
+                     args.cadence_polls, False, hot, True))
     skipped = []
     p50, rows, by_q, by_q_samples = {}, {}, {}, {}
-    for group, label, period, key, queues, polls, (name, mode, pl, b, pw), tls, hot, timing in plan:
+    for group, label, period, suffix, queues, polls, tls, hot, timing in plan:
         if time.monotonic() > deadline:
-            skipped.append(f"{label}/{key}")
+            skipped.append(f"{label}/{group}{suffix}")
             continue
-        r = measure_cadenced(period, polls, queues, mode, pl, b, tls, skip=skip, hot_endpoints=hot, prewarm_ns=pw,
-                             timing=timing)
-        if group == "by_queues":
-            by_q.setdefault(name, {})[str(queues)] = r["p50_ms"]
-            by_q_samples.setdefault(name, {})[str(queues)] = r["samples"]
-        else:
-            rows.setdefault(label, {})[key] = r
-            if not timing:
-                p50.setdefault(label, {})[key] = r["p50_ms"]
-        _progress(f"cadence {label} {key}{' (' + str(queues) + ' queues)' if group == 'fleet' else ''}: "
-                  f"p50 {r['p50_ms']} ms over {r['samples']} samples")
+        res = measure_cadenced_arms(period, polls, queues, arms, tls, skip=skip, hot_endpoints=hot, timing=timing)
+        for name, r in res.items():
+            if group == "by_queues":
+                by_q.setdefault(name, {})[str(queues)] = r["p50_ms"]
+                by_q_samples.setdefault(name, {})[str(queues)] = r["samples"]
+            else:
+                rows.setdefault(label, {})[name + suffix] = r
+                if not timing:
+                    p50.setdefault(label, {})[name + suffix] = r["p50_ms"]
+        _progress(f"cadence {label} {group}{suffix} ({queues} queues per path): " +
+                  ", ".join(f"{name} p50 {r['p50_ms']} ms over {r['samples']}" for name, r in res.items()))
     if skipped:
         _progress(f"cadence rows skipped (past --extras-budget-s): {skipped}")
     return {
@@ -232,7 +232,7 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence-queue-samples", type=int, default=200,
                     help="scaling polls per row of the 250 ms 1/2/4/8-tracked-queue rows")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
-    ap.add_argument("--extras-budget-s", type=float, default=420.0,
+    ap.add_argument("--extras-budget-s", type=float, default=400.0,
                     help="seconds after start past which the remaining secondary sections and cadence rows are skipped "
                          "(recorded under extra.skipped_sections); the headline line is always printed")
     args = ap.parse_args(argv)

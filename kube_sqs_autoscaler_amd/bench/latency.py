@@ -212,8 +212,8 @@ class BenchEnv:
     production endpoint is (supported with ``shared`` and ``process``). ``prewarm_ns``: the
     loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
     period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
-    these and ``busy_poll_ns`` may be lists, one value per queue, cycled (paired comparisons
-    within one run). ``timing``: the clients time every request's
+    these, ``busy_poll_ns``, ``mode`` and ``pipeline`` may be lists, one value per queue, cycled
+    (paired comparisons within one run: :func:`measure_cadenced_arms`). ``timing``: the clients time every request's
     phases (HttpTiming), traced polls carry the breakdown (``detail``), and the fakes record each
     request's wake-up delay and service time (HttpServer::set_timing)."""
 
@@ -273,6 +273,7 @@ class BenchEnv:
             si = q % n_servers
             sqs, kube = self.sqs_servers[si], self.kube_servers[si]
             bp_q, pw_q = per_queue(busy_poll_ns, q), per_queue(prewarm_ns, q)
+            mode_q, pipeline_q = per_queue(mode, q), per_queue(pipeline, q)
             rest = RestConfig(host=kube.url, bearer_token=TOKEN, insecure=tls)
             sqs_tls = None
             if tls:
@@ -283,7 +284,7 @@ class BenchEnv:
             t = TargetConfig(queue_url=queue_url(sqs.url, q), deployment=deployment_name(q), namespace="bench",
                              poll_period_ns=poll_period_ns, scale_up_cool_down_ns=0, scale_down_cool_down_ns=0,
                              scale_up_messages=100, scale_down_messages=10, max_pods=8, min_pods=1)
-            kube_api = new_deployment_api(rest, "bench", mode, 30 * nat.SECOND, self.clock, busy_poll_ns=bp_q)
+            kube_api = new_deployment_api(rest, "bench", mode_q, 30 * nat.SECOND, self.clock, busy_poll_ns=bp_q)
             scaler = new_pod_autoscaler(t, kube_api, self.log, self.clock)
             sqs_api = new_sqs_api(REGION, self.clock, endpoint=sqs.url, protocol=sqs_protocol, credentials=creds,
                                   tls=sqs_tls, busy_poll_ns=bp_q)
@@ -296,7 +297,7 @@ class BenchEnv:
             cfg.scale_down_cool_down_ns = 0
             cfg.scale_up_messages = 100
             cfg.scale_down_messages = 10
-            cfg.prefetch = pipeline
+            cfg.prefetch = pipeline_q
             cfg.prewarm_ns = pw_q
             # the CLI's share (autoscaler.loop_config) unless given
             cfg.spin_budget_ppm = (SPIN_BUDGET_PPM // queues if spin_budget_ppm is None
@@ -516,70 +517,93 @@ def _pct_ns(v: List[int], p: float) -> int:
 def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: str = "scale", pipeline: bool = True,
                      busy_poll_ns: int = 0, tls: bool = False, skip: int = 2, servers: str = "split",
                      hot_endpoints: bool = False, prewarm_ns: int = 0, timing: bool = False) -> Dict:
-    """Poll -> patch latency at a production poll cadence, not back to back.
+    """Poll -> patch latency at a production poll cadence, not back to back: one path
+    (:func:`measure_cadenced_arms` with a single arm; see there)."""
+    arm = dict(mode=mode, pipeline=pipeline, busy_poll_ns=busy_poll_ns, prewarm_ns=prewarm_ns)
+    return measure_cadenced_arms(poll_period_ns, polls, queues, {"only": arm}, tls, skip, servers, hot_endpoints,
+                                 timing)["only"]
+
+
+def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, arms: Dict[str, Dict],
+                          tls: bool = False, skip: int = 2, servers: str = "split", hot_endpoints: bool = False,
+                          timing: bool = False) -> Dict[str, Dict]:
+    """Poll -> patch latency at a production poll cadence for one or more paths side by side.
 
     The reference sleeps ``--poll-period`` (5 s by default) before every poll
     (/root/reference/main.go:41,83). Between polls the worker thread is asleep, its caches and
     branch predictors are cold, the CPU may sit in a deep idle state, and a keep-alive
     connection unused for longer than ``kFreshConnNs`` gets the idle-close check again. The
-    hot-loop rows measure none of that. Here ``queues`` queues (the default fleet: a thread
-    each, staggered over the period) each run ``polls`` polls at ``poll_period_ns`` against
-    the ``split`` endpoints (one fake SQS process and one apiserver process serving them all, as
-    production has two services); every poll scales (the 200/0 trace, zero
-    cool-downs). The first ``skip`` polls of each queue (dial, TLS handshake, first
-    allocations) are dropped. Phases come from the per-poll spans (``--trace-file`` format).
+    hot-loop rows measure none of that. Here every arm (``name -> dict(mode, pipeline,
+    busy_poll_ns, prewarm_ns)``) gets ``queues_per_arm`` queues; queue q runs arm q % len(arms),
+    so the arms' queues interleave in one fleet (a thread each, starts staggered over the
+    period) and run ``polls`` polls at ``poll_period_ns`` in the same run, against the same
+    ``split`` endpoints (one fake SQS process and one apiserver process serving every queue, as
+    production has two services). Comparing paths in one run, not in runs one after the other,
+    matters at a cadence: a box's idle-state and frequency behaviour drifts over tens of seconds
+    and moved single-path runs of the same path by 2x between consecutive runs
+    (profiles/r04c_cadence_probe.jsonl). Every poll scales (the 200/0 trace, zero cool-downs).
+    The first ``skip`` polls of each queue (dial, TLS handshake, first allocations) are dropped.
+    Phases come from the per-poll spans (``--trace-file`` format).
     """
     import json
     import statistics
     import tempfile
 
-    env = BenchEnv(queues, mode, tls=tls, pipeline=pipeline, busy_poll_ns=busy_poll_ns, servers=servers,
-                   poll_period_ns=poll_period_ns, stagger=True, hot_endpoints=hot_endpoints, prewarm_ns=prewarm_ns,
-                   timing=timing)
+    names = list(arms)
+    n = len(names)
+    col = lambda k: [arms[a][k] for a in names]  # noqa: E731 -- cycled per queue by BenchEnv
+    env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
+                   busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
+                   hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing)
     files = [tempfile.TemporaryFile() for _ in env.runners]
-    spans: List[dict] = []
+    spans: Dict[str, List[dict]] = {a: [] for a in names}
     try:
         for r, f in zip(env.runners, files):
             r.set_trace_fd(f.fileno())
         wall = env.run(polls)
-        for r, f in zip(env.runners, files):
+        for q, (r, f) in enumerate(zip(env.runners, files)):
             r.set_trace_fd(-1)
             f.seek(0)
-            spans += [json.loads(line) for line in f.read().decode().splitlines()][skip:]
+            spans[names[q % n]] += [json.loads(line) for line in f.read().decode().splitlines()][skip:]
         res = env.collect(polls, wall)
         served = env.server_timings()
     finally:
         for f in files:
             f.close()
         env.close()
-    lat = [s["patch_latency_ns"] for s in spans if s["patch_latency_ns"] >= 0]
-    scaled = [s for s in spans if s["patch_latency_ns"] >= 0]
-    med = (lambda k: round(statistics.median(s[k] for s in scaled) / 1e3, 2)) if scaled else (lambda k: None)
-    return {
-        "poll_period_ms": poll_period_ns / 1e6,
-        "queues": queues,
-        "mode": mode,
-        "pipeline_reads": pipeline,
-        "tls": tls,
-        "hot_endpoints": hot_endpoints,
-        "prewarm_us": prewarm_ns / 1e3,
-        "p50_ms": round(_pct_ns(lat, 50) / 1e6, 4) if lat else None,
-        "p90_ms": round(_pct_ns(lat, 90) / 1e6, 4) if lat else None,
-        "p99_ms": round(_pct_ns(lat, 99) / 1e6, 4) if lat else None,
-        "samples": len(lat),
-        "polls": len(spans),
-        "errors": sum(1 for s in spans if "error" in s),
-        "signature_failures": res.signature_failures,
-        "phase_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
-                            "patch_us": med("patch_latency_ns")},
-        "wall_s": round(wall, 2),
-        # With timing: the fake endpoints' side of each request (HttpServer::timings) -- how long
-        # the endpoint's thread took to wake up for it after the kernel received it, and to answer
-        # it -- and every client call's phases.
-        **({"endpoint_median_us": {k: {"wake": _median_us([w for w, _ in v]),
-                                       "service": _median_us([sv for _, sv in v])} for k, v in served.items()},
-            "call_phase_median_us": _detail_medians(scaled)} if timing else {}),
-    }
+    out = {}
+    for a in names:
+        lat = [s["patch_latency_ns"] for s in spans[a] if s["patch_latency_ns"] >= 0]
+        scaled = [s for s in spans[a] if s["patch_latency_ns"] >= 0]
+        med = (lambda k: round(statistics.median(s[k] for s in scaled) / 1e3, 2)) if scaled else (lambda k: None)
+        arm = arms[a]
+        out[a] = {
+            "poll_period_ms": poll_period_ns / 1e6,
+            "queues": queues_per_arm,
+            **({"paired_with": [b for b in names if b != a], "queues_in_run": queues_per_arm * n} if n > 1 else {}),
+            "mode": arm["mode"],
+            "pipeline_reads": arm["pipeline"],
+            "tls": tls,
+            "hot_endpoints": hot_endpoints,
+            "prewarm_us": arm["prewarm_ns"] / 1e3,
+            "p50_ms": round(_pct_ns(lat, 50) / 1e6, 4) if lat else None,
+            "p90_ms": round(_pct_ns(lat, 90) / 1e6, 4) if lat else None,
+            "p99_ms": round(_pct_ns(lat, 99) / 1e6, 4) if lat else None,
+            "samples": len(lat),
+            "polls": len(spans[a]),
+            "errors": sum(1 for s in spans[a] if "error" in s),
+            "signature_failures": res.signature_failures,
+            "phase_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
+                                "patch_us": med("patch_latency_ns")},
+            "wall_s": round(wall, 2),
+            # With timing: every client call's phases, and the fake endpoints' side of each
+            # request (HttpServer::timings, all arms together) -- how long the endpoint's thread
+            # took to wake up for it after the kernel received it, and to answer it.
+            **({"endpoint_median_us": {k: {"wake": _median_us([w for w, _ in v]),
+                                           "service": _median_us([sv for _, sv in v])} for k, v in served.items()},
+                "call_phase_median_us": _detail_medians(scaled)} if timing else {}),
+        }
+    return out
 
 
 def _detail_medians(spans: List[dict]) -> Dict:

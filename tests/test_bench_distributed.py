@@ -114,8 +114,8 @@ def test_cadence_rows_past_their_deadline_are_skipped_and_named():
 
     args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=1, cadence_queue_samples=4)
     out = bench._cadence_rows(args, True, 0, 0.02, deadline=0.0)
-    assert len(out["cadenced_rows_skipped"]) == 18 and "250ms/default" in out["cadenced_rows_skipped"]
-    assert "250ms/reference_equivalent/8" in out["cadenced_rows_skipped"]
+    assert len(out["cadenced_rows_skipped"]) == 11 and "250ms/fleet" in out["cadenced_rows_skipped"]
+    assert "250ms/by_queues/8" in out["cadenced_rows_skipped"] and "1s/fleet_hot_endpoints_timed" in out["cadenced_rows_skipped"]
     assert out["cadenced_p50_ms"] == {} and out["cadenced_vs_hot_loop_default_plain"] == {}
     assert out["cadenced_p50_ms_by_tracked_queues"] == {}
 
@@ -131,13 +131,13 @@ def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
     from kube_sqs_autoscaler_amd.bench import latency
 
     calls = []
-    real = latency.measure_cadenced
+    real = latency.measure_cadenced_arms
 
-    def fast(period, polls, queues, *a, **kw):  # the queue-axis rows only, at a 20 ms cadence
-        calls.append((period, polls, queues, a[0]))
-        return real(20_000_000, polls, queues, *a, **kw)
+    def fast(period, polls, queues, arms, *a, **kw):  # every row at a 20 ms cadence
+        calls.append((period, polls, queues, sorted(arms)))
+        return real(20_000_000, polls, queues, arms, *a, **kw)
 
-    monkeypatch.setattr(latency, "measure_cadenced", fast)
+    monkeypatch.setattr(latency, "measure_cadenced_arms", fast)
     args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=2, cadence_queue_samples=8)
     import time
 
@@ -147,6 +147,11 @@ def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
     for name in by_q:
         assert set(by_q[name]) == {"1", "2", "4", "8"} and all(v > 0 for v in by_q[name].values())
         assert all(n >= 8 for n in out["cadenced_by_tracked_queues_samples"][name].values())
-    assert calls[0] == (250_000_000, 10, 1, "scale") and calls[1][3] == "deployment"
+    assert calls[0] == (250_000_000, 10, 1, ["default", "reference_equivalent"])  # both paths in one run
+    assert [c[2] for c in calls[:4]] == [1, 2, 4, 8]
     assert "cadenced_rows_skipped" not in out and set(out["cadenced_p50_ms"]) == {"250ms", "1s"}
+    assert set(out["cadenced_p50_ms"]["250ms"]) == {"default", "reference_equivalent", "default_tls",
+                                                   "reference_equivalent_tls"}
+    r = out["cadenced_rows"]["1s"]["default_timed"]
+    assert r["paired_with"] == ["reference_equivalent"] and r["queues_in_run"] == 4 and "call_phase_median_us" in r
     assert list(out)[-1] == "cadenced_p50_ms_by_tracked_queues"
