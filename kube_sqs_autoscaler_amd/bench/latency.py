@@ -552,9 +552,12 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     names = list(arms)
     n = len(names)
     col = lambda k: [arms[a][k] for a in names]  # noqa: E731 -- cycled per queue by BenchEnv
+    # each arm's queues get the spin budget the CLI gives a process tracking that many queues
+    # (1 % of the period shared by them), not a share diluted by the other arms' queues
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
-                   hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing)
+                   hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,
+                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm)
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: Dict[str, List[dict]] = {a: [] for a in names}
     try:
