@@ -49,7 +49,8 @@ def native() -> ModuleType:
             from . import build
 
             try:
-                build.build_native(verbose=False)
+                if not build.native_up_to_date():
+                    build.build_native(verbose=False)
             except Exception as e:  # pragma: no cover - toolchain failure
                 raise NativeUnavailable(f"failed to build the native runtime: {e}") from e
         try:
@@ -77,7 +78,8 @@ def fakes() -> ModuleType:
             from . import build
 
             try:
-                build.build_fakes(verbose=False)
+                if not build.fakes_up_to_date():
+                    build.build_fakes(verbose=False)
             except Exception as e:  # pragma: no cover - toolchain failure
                 raise NativeUnavailable(f"failed to build the native fakes: {e}") from e
         try:

@@ -138,6 +138,26 @@ def _link(out: Path, inputs: list[Path], verbose: bool) -> None:
             print(f"[build] linked {out.relative_to(ROOT)}")
 
 
+def _newest_source(dirs: list[Path], files: list[Path]) -> float:
+    paths = [p for d in dirs for p in d.rglob("*") if p.suffix in (".cc", ".h")] + files
+    return max((p.stat().st_mtime for p in paths), default=0.0)
+
+
+def native_up_to_date() -> bool:
+    """The in-tree ``_ksa_native`` is newer than every source it is built from. Decided on the
+    module and the sources alone, not the object files: ``build/`` does not travel with the tree
+    (a GPU box gets the built module and no objects), and a process there must not recompile a
+    module that is current -- least of all several ranks at once."""
+    return NATIVE_SO.exists() and NATIVE_SO.stat().st_mtime >= _newest_source(
+        [CSRC / "core", CSRC / "sim"], [CSRC / "bindings" / "module.cc"])
+
+
+def fakes_up_to_date() -> bool:
+    """:func:`native_up_to_date` for ``_ksa_fakes`` (the fakes and the core they link)."""
+    return FAKES_SO.exists() and FAKES_SO.stat().st_mtime >= _newest_source(
+        [CSRC / "core", CSRC / "sim", CSRC / "fakes"], [CSRC / "bindings" / "fakes_module.cc"])
+
+
 def build_native(jobs: int = 8, verbose: bool = True) -> Path:
     """Builds the production pybind11 extension in place; returns its path."""
     core = _compile_objects("release", RELEASE_FLAGS, _core_sources(), jobs)

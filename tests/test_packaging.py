@@ -95,3 +95,25 @@ def test_ci_workflow_runs_the_ci_gate():
     steps = [st.get("run", "") for st in wf["jobs"]["cpu"]["steps"]]
     assert any("make ci" in r for r in steps)
     assert "make ci" in open(os.path.join(ROOT, "Makefile")).read() or "scripts/ci.sh" in open(os.path.join(ROOT, "Makefile")).read()
+
+
+def test_module_up_to_date_check_needs_no_object_files(tmp_path, monkeypatch):
+    """native()/fakes() rebuild only when the module is older than a source: a GPU box gets the
+    built modules without build/ (gpurun ignores it), and several bench ranks starting at once
+    must not all recompile a current module."""
+    import time
+
+    from kube_sqs_autoscaler_amd.ops import build
+
+    so = tmp_path / "mod.so"
+    so.write_bytes(b"")
+    monkeypatch.setattr(build, "NATIVE_SO", so)
+    monkeypatch.setattr(build, "FAKES_SO", so)
+    monkeypatch.setattr(build, "BUILD", tmp_path / "no-build-dir")
+    os.utime(so, (0, 0))
+    assert not build.native_up_to_date() and not build.fakes_up_to_date()
+    future = time.time() + 3600
+    os.utime(so, (future, future))
+    assert build.native_up_to_date() and build.fakes_up_to_date()
+    so.unlink()
+    assert not build.native_up_to_date()
