@@ -245,7 +245,7 @@ def test_sharded_sweep_cli_on_gpu(tmp_path):
     csv.write_text("0,1\n300,25\n900,1\n")
     args = ["--arrivals", str(csv), "--horizon", "30m", "--service-rate", "5", "--seeds", "8", "--json", "--top", "0",
             "--slo-backlog", "100", "--grid", "scale-up-cool-down=0s,1m", "--grid", "max-pods=4,8,16", "--latency",
-            "1ms,1ms,1ms"]
+            "1ms,1ms,1ms", "--grid", "poll-period=2s,5s"]  # mixed periods: the cost-sorted shard is scattered back
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
                         "--master-addr=127.0.0.1", "--master-port=29517", "-m", "kube_sqs_autoscaler_amd.tune",
@@ -253,9 +253,9 @@ def test_sharded_sweep_cli_on_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     info, rows = lines[0], lines[1:]
-    assert info["device"] == "gpu" and info["ranks"] == 1 and len(rows) == 6
+    assert info["device"] == "gpu" and info["ranks"] == 1 and len(rows) == 12
     tr = cl.ArrivalTrace.from_csv(str(csv))
-    grid = sweep.grid(up_cool_ns=[0, 60 * S], max_pods=[4, 8, 16])
+    grid = sweep.grid(poll_ns=[2 * S, 5 * S], up_cool_ns=[0, 60 * S], max_pods=[4, 8, 16])
     c = cl.run(tr, grid, cl.QueueModel(5.0, 60 * S, 100), 1, 1800 * S, (1_000_000,) * 3, seeds=8, device="cpu")
     want = sorted((c.row(i) for i in range(len(c))), key=lambda x: x["pod_hours_mean"])
     assert sorted(rows, key=lambda x: x["pod_hours_mean"]) == want
