@@ -166,11 +166,18 @@ def _launch_ranks(n: int, argv: list, script: str = __file__) -> int:
     Called before anything in this process imports torch or touches a GPU, and it never execs:
     the parent only waits. Rank 0 inherits stdout, so its JSON line is the job's; the other
     ranks' stdout goes to stderr. When a rank fails the others are stopped (they would block in
-    the next collective) and the first failure's exit status is returned."""
+    the next collective) and the first failure's exit status is returned; a SIGTERM / SIGINT to
+    the launcher stops every rank before it exits."""
     import signal
     import subprocess
 
     port = _free_port()
+
+    def stop(signum, frame):  # the launcher's own SIGTERM / SIGINT: the finally below stops the ranks
+        raise SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, stop)
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),

@@ -155,3 +155,37 @@ def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
     r = out["cadenced_rows"]["1s"]["default_timed"]
     assert r["paired_with"] == ["reference_equivalent"] and r["queues_in_run"] == 4 and "call_phase_median_us" in r
     assert list(out)[-1] == "cadenced_p50_ms_by_tracked_queues"
+
+
+def test_rank_launcher_stops_its_ranks_when_it_is_terminated(tmp_path):
+    """A SIGTERM to `bench.py --gpus N` (a driver time limit) must not leave its ranks running."""
+    import signal
+    import time
+
+    script = tmp_path / "rank.py"
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    script.write_text("import os, time\n"
+                      f"open(os.path.join({str(pids)!r}, os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                      "time.sleep(120)\n")
+    launcher = tmp_path / "launch.py"
+    launcher.write_text(f"import sys; sys.path.insert(0, {ROOT!r}); import bench\n"
+                        f"sys.exit(bench._launch_ranks(2, [], script={str(script)!r}))\n")
+    p = subprocess.Popen([sys.executable, str(launcher)])
+    deadline = time.monotonic() + 30
+    while len(list(pids.iterdir())) < 2 and time.monotonic() < deadline:
+        time.sleep(0.05)
+    ranks = [int(f.read_text()) for f in pids.iterdir()]
+    assert len(ranks) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    for pid in ranks:
+        deadline = time.monotonic() + 10
+        while time.monotonic() < deadline:
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.05)
+        else:
+            raise AssertionError(f"rank pid {pid} still running")
