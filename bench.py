@@ -266,11 +266,15 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # one rank per GPU over RCCL; more ranks than GPUs (a rehearsal of an N-GPU run on a smaller
+    # box) cannot share a device under RCCL, so such a job pools its samples over gloo instead
+    backend = "nccl" if use_cuda and torch.cuda.device_count() >= local_world else "gloo"
     if use_cuda:
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
-    device = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
+    device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        if use_cuda:  # RCCL; eager init bound to this rank's GPU
+        if backend == "nccl":  # RCCL; eager init bound to this rank's GPU
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
@@ -341,6 +345,7 @@ def main(argv=None) -> int:
             "pipeline_reads": pipeline,
             "busy_poll_us": args.busy_poll_us,
             "fake_endpoints": servers,
+            "collective_backend": backend if world > 1 else None,
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},

@@ -65,6 +65,7 @@ def test_bench_launches_its_own_ranks_without_a_launcher():
     out = _json_line(r.stdout)
     _check(out, 3, 50, 5)
     assert out["extra"]["tracked_queues"] == 3 and out["config"]["global_batch"] == 3
+    assert out["extra"]["collective_backend"] == "gloo"  # no GPUs here (RCCL on a GPU node)
 
 
 def test_bench_refuses_a_launcher_world_that_differs_from_gpus():
