@@ -41,7 +41,7 @@ def main() -> None:
                       up_cool_ns=list(range(0, 600 * S, (6 if big else 20) * S)),
                       down_cool_ns=list(range(0, 1200 * S, (30 if big else 60) * S)),
                       up_msgs=[50, 100, 150, 200, 300, 400, 600, 800, 1200, 1600] if big else [50, 100, 200, 400, 800],
-                      max_pods=[4, 8, 16, 32, 64] if big else [8, 16, 32], min_pods=[1, 2] if big else [1])
+                      max_pods=[4, 8, 16, 32, 64] if big else [8, 16, 32], min_pods=[1, 2, 3, 4] if big else [1])
     horizon, lat = (6 if big else 24) * 3600 * S, (2_000_000, 1_000_000, 1_000_000)
     m = grid.shape[1]
     costs = config_costs(grid, horizon, lat)
