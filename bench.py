@@ -5,13 +5,13 @@ BASELINE.json names the metric "poll->scale-patch p50 latency (ms); decision par
 synthetic trace", reported at 1/2/4/8 concurrently tracked queues. The reference publishes no
 number (BASELINE.json ``published: {}``), so ``vs_baseline`` is null.
 
-One rank per GPU (``torch.distributed``; backend ``nccl`` = RCCL on ROCm when a GPU is present,
-``gloo`` otherwise). Each rank is one autoscaler process tracking ``--queues`` queues (default
-1) against its own localhost fake SQS + fake kube-apiserver, so the job tracks
+One rank per GPU (``torch.distributed``; backend ``nccl`` = RCCL on ROCm when every rank has a
+GPU of its own, ``gloo`` otherwise). Each rank is one autoscaler process tracking ``--queues``
+queues (default 1) against its own localhost fake SQS + fake kube-apiserver, so the job tracks
 ``N x queues`` queues in total (weak scaling). The ranks share nothing while timed -- each is an
 independent control-plane process, as N reference deployments would be; the collective
-(``all_gather``) only pools the latency samples for the job-wide p50 afterwards. A "step" is one control-loop iteration on every
-tracked queue: SigV4-signed SQS GetQueueAttributes -> Deployment GET -> replica write (the trace
+(``all_gather``) only pools the latency samples for the job-wide p50 afterwards. A "step" is
+one control-loop iteration on every tracked queue: SigV4-signed SQS GetQueueAttributes -> Deployment GET -> replica write (the trace
 alternates 200/0 messages, so every iteration scales). K timed steps are bracketed by a barrier
 + ``torch.cuda.synchronize()``; ``value`` is the p50 over every sample of every rank.
 
@@ -19,7 +19,9 @@ Secondary rows (single rank; fixed ``--secondary-samples`` per queue, three inte
 median): p50 at 1/2/4/8 tracked queues with the default thread-per-queue fleet and with
 ``--worker-processes`` (each queue against its own fake endpoint process), the strictly
 sequential and reference-equivalent paths, TLS, a regional-RTT model, per-phase medians,
-wire-path decision parity and apiserver requests per poll on the Appendix C traces.
+wire-path decision parity and apiserver requests per poll on the Appendix C traces; and the
+production-cadence rows (250 ms and 1 s poll periods, 1/2/4/8 and 16 queues, the default and
+reference-equivalent paths as paired arms of each run: ``_cadence_rows``).
 
 Launch: ``python bench.py --gpus N`` with N > 1 outside a launcher starts the N ranks itself
 (child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set,
