@@ -235,12 +235,14 @@ class alignas(kCacheLine) Runner {
     scaler_->cancel();
   }
   // Splits one poll's spin budget over the requests a poll makes (HttpClient::set_spin_budget
-  // applies per request): half to the SQS call, a quarter to each of the apiserver's GET and
-  // write, so a scaling poll spins at most `ns` in total. (An SDK retry of the SQS call spins
-  // within its own half again; retries are the error path.)
+  // applies per request): three quarters to the SQS call, an eighth to each of the apiserver's
+  // GET and write, so a scaling poll spins at most `ns` in total. The SQS answer is the one slow
+  // enough to need the budget (at a cadence its EWMA is past 4x the busy-poll window); the
+  // apiserver's answers mostly come within the window, which needs none. (An SDK retry of the
+  // SQS call spins within its own share again; retries are the error path.)
   void set_spin_budget(Nanos ns) {
-    sqs_->api()->set_spin_budget(ns / 2);
-    scaler_->api()->set_spin_budget(ns / 4);
+    sqs_->api()->set_spin_budget(ns / 4 * 3);
+    scaler_->api()->set_spin_budget(ns / 8);
   }
   // Closes the clients' keep-alive connections (on the calling thread's file table).
   void release_connections() {

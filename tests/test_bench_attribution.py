@@ -84,8 +84,8 @@ def test_spin_window_decision(nat, busy_poll, ewma, budget, window):
 @pytest.mark.parametrize("period_ms,spins", [(1000, True), (0, False)])
 def test_cadenced_worker_spins_through_a_slow_answer_within_its_budget(nat, period_ms, spins):
     """End to end: a worker on its own thread may busy-poll through an answer that takes longer
-    than the --busy-poll window when twice the response-time EWMA fits in the SQS call's half of
-    1 % of the poll period (1 s -> 5 ms; the fakes answer after 0.4 ms plus their timer slack),
+    than the --busy-poll window when twice the response-time EWMA fits in the SQS call's three
+    quarters of 1 % of the poll period (1 s -> 7.5 ms; the fakes answer after 0.4 ms plus their timer slack),
     so the poll is not woken from an idle sleep by its answer. The spin lasts 2 x EWMA: an answer
     a busy host delays past that is waited for in poll(2), so how many polls spin depends on the
     load -- this runs serially (conftest: ``serial`` tests are skipped under xdist workers) and
