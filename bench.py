@@ -274,6 +274,8 @@ def main(argv=None) -> int:
     backend = "nccl" if use_cuda and torch.cuda.device_count() >= local_world else "gloo"
     if use_cuda:
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+    if world > 1 and backend == "gloo" and use_cuda and rank == 0:
+        _progress(f"{local_world} ranks on {torch.cuda.device_count()} GPU(s): ranks share GPUs, samples pool over gloo")
     device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     if world > 1:
         if backend == "nccl":  # RCCL; eager init bound to this rank's GPU
@@ -348,6 +350,7 @@ def main(argv=None) -> int:
             "busy_poll_us": args.busy_poll_us,
             "fake_endpoints": servers,
             "collective_backend": backend if world > 1 else None,
+            "gpus_visible": torch.cuda.device_count() if use_cuda else 0,
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
             "connections": {"sqs": res.sqs_connections, "kube": res.kube_connections},
