@@ -94,6 +94,9 @@ def test_ci_workflow_runs_the_ci_gate():
     wf = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "ci.yml")))
     steps = [st.get("run", "") for st in wf["jobs"]["cpu"]["steps"]]
     assert any("make ci" in r for r in steps)
+    image = [st.get("run", "") for st in wf["jobs"]["image"]["steps"]]
+    assert any("docker build --target slim" in r for r in image)
+    assert any("_ksa_fakes" in r for r in image)
     assert "make ci" in open(os.path.join(ROOT, "Makefile")).read() or "scripts/ci.sh" in open(os.path.join(ROOT, "Makefile")).read()
 
 
