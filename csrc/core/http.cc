@@ -549,6 +549,7 @@ Status HttpClient::dial(const Url& to, int64_t deadline_ns, int* fd_out) {
 
 Status HttpClient::connect_locked(int64_t deadline_ns) {
   if (!ctx_status_.ok()) return ctx_status_;
+  const int64_t t_dial = mono_ns();
   int fd = -1;
   Status d = dial(has_proxy_ ? proxy_ : origin_, deadline_ns, &fd);
   if (!d.ok()) return has_proxy_ ? Status::Err("proxyconnect tcp: " + d.message()) : d;
@@ -648,6 +649,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   if (timing()) conn_->stream->enable_rx_timestamps();
   stats_.connects++;
   warm_dial_failed_ = false;  // reachable again: warm-ups may dial
+  last_dial_ns_ = mono_ns() - t_dial;
   return Status::OK();
 }
 
@@ -680,7 +682,10 @@ bool HttpClient::warm(Nanos dial_budget) {
   }
   if (!conn_) {
     if (warm_dial_failed_) return false;  // the endpoint is down: the request dials
-    const Nanos budget = timeout_ > 0 ? std::min(timeout_, dial_budget) : dial_budget;
+    // an endpoint whose dials are known to take longer (a distant apiserver, a proxy) gets
+    // twice its last dial time, so a slow but healthy endpoint is still warmed
+    const Nanos want = std::max(dial_budget, 2 * last_dial_ns_);
+    const Nanos budget = timeout_ > 0 ? std::min(timeout_, want) : want;
     if (!connect_locked(mono_ns() + std::max<Nanos>(budget, 0)).ok()) {
       warm_dial_failed_ = true;
       return false;

@@ -141,9 +141,9 @@ class alignas(kCacheLine) HttpClient {
   // idle-close peek the next request would make -- and dials (with TLS) when there is none or
   // the peer closed it, so the request itself finds a live, freshly checked connection. Dial
   // errors are left for the request to report. Returns whether a connection is ready.
-  // The dial runs under `dial_budget` (capped by the client's timeout), not the full request
-  // timeout: an endpoint that drops packets must not hold up the poll it prepares (the SQS read
-  // comes after the warm-up). After a warm-up dial fails, later warm-ups do not dial again until
+  // The dial runs under `dial_budget` -- or twice the last successful dial's time when that is
+  // longer, capped by the client's timeout -- not the full request timeout: an endpoint that
+  // drops packets must not hold up the poll it prepares (the SQS read comes after the warm-up). After a warm-up dial fails, later warm-ups do not dial again until
   // a request has connected: while an endpoint is down the poll behaves like the reference's
   // sleep-then-poll, each request dialing under its own timeout.
   static constexpr Nanos kWarmDialBudget = 100 * kMillisecond;
@@ -238,6 +238,7 @@ class alignas(kCacheLine) HttpClient {
   bool in_flight_ = false;
   bool caller_retries_ = false;
   bool warm_dial_failed_ = false;  // warm(): the last warm-up dial failed, none since connected
+  Nanos last_dial_ns_ = 0;          // how long the last successful dial (TCP + proxy + TLS) took
   bool timing_ = false;
   HttpTiming timing_cur_, timing_last_;
   bool fresh_locked() const;

@@ -1,7 +1,8 @@
 """--poll-prewarm against an endpoint that does not answer: the warm-up dial runs under a short
-budget (HttpClient::kWarmDialBudget, 100 ms) instead of --api-timeout, and is not repeated while
-the endpoint stays down, so the SQS depth read -- which comes after the warm-up -- keeps the
-reference's cadence (sleep-then-poll, /root/reference/main.go:41-43)."""
+budget (HttpClient::kWarmDialBudget, 100 ms, or twice the last successful dial) instead of
+--api-timeout, and is not repeated while the endpoint stays down, so the SQS depth read -- which
+comes after the warm-up -- keeps the reference's cadence (sleep-then-poll,
+/root/reference/main.go:41-43)."""
 import json
 import socket
 import threading
@@ -131,3 +132,77 @@ def test_poll_cadence_holds_while_the_apiserver_drops_packets(nat, silent, tmp_p
     gaps = [(b["ts"] - b["total_ns"] - a["ts"]) / MS for a, b in zip(spans, spans[1:])]
     assert all(g < 50 + 150 for g in gaps), gaps  # never a 300 ms warm-up dial in front of a poll
     assert sorted(gaps)[len(gaps) // 2] < 50 + 30, gaps
+
+
+class SlowTlsEndpoint:
+    """A healthy TLS endpoint whose handshake starts `delay` s after the TCP accept (a distant
+    apiserver or a proxy): answers every request with 200 and closes the connection."""
+
+    def __init__(self, nat, tmp_path, delay):
+        import ssl
+
+        cert, key = nat.generate_self_signed("127.0.0.1")
+        (tmp_path / "c.pem").write_text(cert)
+        (tmp_path / "k.pem").write_text(key)
+        self.ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        self.ctx.load_cert_chain(str(tmp_path / "c.pem"), str(tmp_path / "k.pem"))
+        self.delay = delay
+        self.sock = socket.socket()
+        self.sock.bind(("127.0.0.1", 0))
+        self.sock.listen(16)
+        self.sock.settimeout(0.05)
+        self.port = self.sock.getsockname()[1]
+        self._stop = False
+        self.thread = threading.Thread(target=self._serve, daemon=True)
+        self.thread.start()
+
+    def _serve(self):
+        while not self._stop:
+            try:
+                c, _ = self.sock.accept()
+            except OSError:
+                continue
+            threading.Thread(target=self._one, args=(c,), daemon=True).start()
+
+    def _one(self, c):
+        try:
+            time.sleep(self.delay)
+            c.settimeout(5)
+            s = self.ctx.wrap_socket(c, server_side=True)
+            buf = b""
+            while b"\r\n\r\n" not in buf:
+                d = s.recv(4096)
+                if not d:
+                    return
+                buf += d
+            s.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\nConnection: close\r\n\r\nok")
+            s.close()
+        except OSError:
+            c.close()
+
+    def close(self):
+        self._stop = True
+        self.thread.join()
+        self.sock.close()
+
+
+def test_warm_dial_budget_follows_a_slow_healthy_endpoint(nat, tmp_path):
+    """A healthy endpoint whose dial takes longer than the 100 ms budget: the first warm-up gives
+    up (and the request dials itself); after that the warm-up budget is twice the last dial time,
+    so the endpoint is warmed again instead of failing every other poll."""
+    ep = SlowTlsEndpoint(nat, tmp_path, 0.15)
+    try:
+        tls = nat.TlsOptions()
+        tls.insecure_skip_verify = True
+        c = nat.HttpClient(f"https://127.0.0.1:{ep.port}", tls, 5 * nat.SECOND)
+        assert c.warm() is False  # 100 ms < the 150 ms handshake delay
+        status, _, body = c.request("GET", "/")
+        assert status == 200 and body == b"ok"  # the request's own dial (~150 ms) succeeds
+        # the server closed the connection ("Connection: close"): the next warm-up redials, now
+        # under 2 x ~150 ms
+        t0 = time.monotonic()
+        assert c.warm() is True
+        assert 0.14 <= time.monotonic() - t0 < 1.0
+        assert c.stats()["connects"] == 2
+    finally:
+        ep.close()
