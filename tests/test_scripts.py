@@ -44,3 +44,11 @@ def test_sweep_bench_scripts_cpu(nat):
     assert any(r.get("device") == "cpu" and r["simulated_polls"] > 0 for r in rows)
     rows = _run(["scripts/queue_sweep_bench.py"], env=env)
     assert any(r.get("device") == "cpu" and r["lane_polls"] > 0 for r in rows)
+
+
+@pytest.mark.slow
+def test_shard_balance_script_cpu(nat):
+    rows = _run(["scripts/shard_balance.py", "--device", "cpu", "--world", "2"])
+    summary = {r["split"]: r for r in rows if "world" in r}
+    assert summary["cost_balanced"]["max_over_min_polls"] <= 1.01
+    assert summary["contiguous"]["max_over_min_polls"] > 2
