@@ -148,6 +148,10 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
         "cadenced_rows": rows,
         "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
         "cadenced_by_tracked_queues_samples": by_q_samples,
+        "cadenced_by_tracked_queues_setup": ("q tracked queues per path, one thread each; the default and the "
+                                             "reference-equivalent path's queues interleaved in one run (2q "
+                                             "threads, starts staggered over the period) against one fake SQS "
+                                             "process and one fake apiserver process"),
         "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()
                                                if "default" in v},
         "cadenced_p50_ms": p50,
