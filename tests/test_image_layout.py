@@ -64,6 +64,12 @@ def test_image_runtime_carries_no_test_doubles_or_timing(image_native, image_roo
     r = subprocess.run([sys.executable, "-S", "-c", code], env={"PYTHONPATH": pythonpath, "KSA_NO_AUTOBUILD": "1"},
                        capture_output=True, text=True, timeout=60, cwd=str(tmp))  # cwd: not the tree's copy
     assert r.returncode == 0 and r.stdout.split() == ["False", "[]"], r.stdout + r.stderr
+    code = ("from kube_sqs_autoscaler_amd.ops import NativeUnavailable, fakes\n"
+            "try:\n    fakes()\nexcept NativeUnavailable as e:\n    print('refused:', e)\n")
+    r = subprocess.run([sys.executable, "-S", "-c", code], env={"PYTHONPATH": pythonpath, "KSA_NO_AUTOBUILD": "1"},
+                       capture_output=True, text=True, timeout=60, cwd=str(tmp))
+    assert r.returncode == 0 and r.stdout.startswith("refused: cannot import the native fakes (test builds only)"), \
+        r.stdout + r.stderr
     from kube_sqs_autoscaler_amd.ops import native
 
     assert native().HTTP_TIMING is True
