@@ -252,3 +252,36 @@ def test_cli_valid_session_starts(tmp_path, nat):
     finally:
         sqs.stop()
         kube.stop()
+
+
+def test_shared_file_reader_fails_only_on_an_unclosed_section_header():
+    """Property: whatever the lines, the reader raises only when a line starts a section header
+    it never closes; every other input parses (unusable lines become warnings)."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from kube_sqs_autoscaler_amd.sqs import ini
+
+    no_breaks = st.characters(blacklist_categories=("Cs",),
+                              blacklist_characters="\r\n\x0b\x0c\x1c\x1d\x1e\x85\u2028\u2029")
+    line = st.one_of(st.text(alphabet=no_breaks, max_size=30),
+                     st.sampled_from(["[default]", "[profile x]", "key = value", "  continued", "# c", "; c", "=v",
+                                      ":v", "[", "[open"]))
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.lists(line, max_size=12))
+    def check(lines):
+        text = "\n".join(lines)
+        unclosed = any(l.strip().startswith("[") and "]" not in l.strip() for l in lines)
+        try:
+            f = ini.parse(text, "f")
+        except ini.IniError:
+            assert unclosed, lines
+            return
+        assert not unclosed or all(  # an unclosed header inside a continuation is just text
+            l[:1] in (" ", "\t") for l in lines if l.strip().startswith("[") and "]" not in l.strip()), lines
+        for sec in f.sections():
+            for k, _ in f.items(sec):
+                assert k == k.lower()
+
+    check()
