@@ -104,3 +104,22 @@ def test_group_refuses_to_start_after_the_kernels_library(monkeypatch):
     monkeypatch.delitem(sys.modules, "torch", raising=False)
     with pytest.raises(RuntimeError, match="before the first GPU sweep"):
         distributed.Group("cpu")
+
+
+def test_shard_plan_imbalance_is_at_most_one_configuration():
+    """Property: the snake deal keeps any two ranks' cost sums within the costliest single
+    configuration, for any costs and rank count."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.lists(st.integers(1, 10**6), max_size=80), st.integers(1, 9))
+    def check(costs, world):
+        c = np.array(costs, dtype=np.int64)
+        plan = shard_plan(c, world)
+        assert sorted(np.concatenate(plan).tolist()) == list(range(len(c)))
+        if len(c):
+            loads = [int(c[p].sum()) for p in plan]
+            assert max(loads) - min(loads) <= int(c.max())
+
+    check()
