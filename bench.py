@@ -154,9 +154,26 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
                                              "process and one fake apiserver process"),
         "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()
                                                if "default" in v},
+        "cadenced_reference_over_default": _ratios(p50, by_q),
         "cadenced_p50_ms": p50,
         "cadenced_p50_ms_by_tracked_queues": {"250ms": by_q} if by_q else {},
     }
+
+
+def _ratios(p50: dict, by_q: dict) -> dict:
+    """Per paired cell, reference-equivalent p50 / default p50 (> 1: the default path is faster)."""
+    out = {}
+    for label, row in p50.items():
+        for key, v in row.items():
+            if key.startswith("default"):
+                ref = row.get("reference_equivalent" + key[len("default"):])
+                if ref and v:
+                    out.setdefault(label, {})[key[len("default"):].lstrip("_") or "plain"] = round(ref / v, 2)
+    d, r = by_q.get("default", {}), by_q.get("reference_equivalent", {})
+    for q in d:
+        if r.get(q) and d[q]:
+            out.setdefault("250ms_by_tracked_queues", {})[q] = round(r[q] / d[q], 2)
+    return out
 
 
 def _free_port() -> int:
@@ -447,7 +464,8 @@ def main(argv=None) -> int:
         # The driver keeps the tail of stdout: the per-row detail goes first, the summary rows last.
         summary = ("wan_model_sqs2ms_kube1ms_p50_ms", "tls_p50_ms", "reference_equivalent_p50_ms",
                    "sequential_scale_p50_ms", "p50_ms_by_tracked_queues_worker_processes", "p50_ms_by_tracked_queues",
-                   "cadenced_vs_hot_loop_default_plain", "cadenced_p50_ms", "cadenced_p50_ms_by_tracked_queues")
+                   "cadenced_vs_hot_loop_default_plain", "cadenced_reference_over_default", "cadenced_p50_ms",
+                   "cadenced_p50_ms_by_tracked_queues")
         extra = {**{k: v for k, v in extra.items() if k not in summary}, **{k: extra[k] for k in summary if k in extra}}
         out = {
             "metric": METRIC,

@@ -156,6 +156,9 @@ def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
     r = out["cadenced_rows"]["1s"]["default_timed"]
     assert r["paired_with"] == ["reference_equivalent"] and r["queues_in_run"] == 4 and "call_phase_median_us" in r
     assert list(out)[-1] == "cadenced_p50_ms_by_tracked_queues"
+    ratios = out["cadenced_reference_over_default"]
+    assert set(ratios["250ms"]) == {"plain", "tls"} and set(ratios["1s"]) == {"plain", "tls", "hot_endpoints"}
+    assert set(ratios["250ms_by_tracked_queues"]) == {"1", "2", "4", "8"}
 
 
 def test_rank_launcher_stops_its_ranks_when_it_is_terminated(tmp_path):
