@@ -143,9 +143,10 @@ class alignas(kCacheLine) HttpClient {
   // errors are left for the request to report. Returns whether a connection is ready.
   // The dial runs under `dial_budget` -- or twice the last successful dial's time when that is
   // longer, capped by the client's timeout -- not the full request timeout: an endpoint that
-  // drops packets must not hold up the poll it prepares (the SQS read comes after the warm-up). After a warm-up dial fails, later warm-ups do not dial again until
-  // a request has connected: while an endpoint is down the poll behaves like the reference's
-  // sleep-then-poll, each request dialing under its own timeout.
+  // drops packets must not hold up the poll it prepares (the SQS read comes after the
+  // warm-up). After a warm-up dial fails, later warm-ups do not dial again until a request has
+  // connected: while an endpoint is down the poll behaves like the reference's sleep-then-poll,
+  // each request dialing under its own timeout.
   static constexpr Nanos kWarmDialBudget = 100 * kMillisecond;
   bool warm(Nanos dial_budget = kWarmDialBudget);
   // Whether a request could go out now without dialing: a connection exists and is either

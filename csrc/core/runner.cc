@@ -372,7 +372,7 @@ void Runner::mirror(const IterationRecord& r) {
     st = stats_;
   }
   const bool good = r.depth_ok && r.up != Action::Failed && r.down != Action::Failed;
-  if (!good) write_shared_error(shared_, r.error);  // before the failure count that makes /readyz look
+  if (!good) write_shared_error(shared_, r.error);  // before the failure counters /readyz reads
   using W = SharedWorkerState;
   auto put = [&](int i, uint64_t v) { shared_->counters[i].store(v, std::memory_order_relaxed); };
   put(W::kPolls, st.polls);
