@@ -209,7 +209,7 @@ class BenchEnv:
     ``stagger``: queue i of N starts i/N of a poll period late (Supervisor.stagger), so N
     queues at one cadence do not poll in one burst. ``hot_endpoints``: every fake server is one
     busy-polling thread (HttpServer::set_hot), awake whenever a request arrives, as a loaded
-    production endpoint is (supported with ``shared`` and ``process``). ``prewarm_ns``: the
+    production endpoint is (supported with ``shared``, ``process`` and ``split``). ``prewarm_ns``: the
     loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
     period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
     these, ``busy_poll_ns``, ``mode`` and ``pipeline`` may be lists, one value per queue, cycled
