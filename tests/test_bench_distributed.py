@@ -193,3 +193,23 @@ def test_rank_launcher_stops_its_ranks_when_it_is_terminated(tmp_path):
             time.sleep(0.05)
         else:
             raise AssertionError(f"rank pid {pid} still running")
+
+
+def test_rank_pinning_slices_the_cpus(monkeypatch):
+    """--pin-ranks: rank r of a node's N ranks gets slice r of N contiguous slices of the CPUs it
+    may use; auto leaves ranks unpinned with fewer than 4 CPUs each, and one rank always."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    got = {}
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)))
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.setdefault("cpus", list(cpus)))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    assert bench._pin_rank("auto") == list(range(24, 32)) == got["cpus"]
+    assert bench._pin_rank("off") is None
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
+    assert bench._pin_rank("auto") is None  # 2 CPUs per rank: left unpinned
+    assert bench._pin_rank("on") == [6, 7]
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert bench._pin_rank("auto") is None
