@@ -5,8 +5,9 @@
 // whose thread migrates across CCDs, or whose peers run on another CCD, pays cross-die cache
 // transfers on every request. Pinning each worker (and, in the benchmark, its fake endpoints)
 // to one L3 domain keeps that traffic inside one CCD -- the CPU-side analogue of keeping a
-// GPU kernel's tiles in one XCD's L2. The CPU lists come from the caller
-// (kube_sqs_autoscaler_amd/utils/topology.py reads the L3 domains from sysfs).
+// GPU kernel's tiles in one XCD's L2. The CPU lists come from the caller (Runner::set_cpus,
+// the worker-process fleet's per-worker lists, the fakes' set_cpus); the CLI pins nothing by
+// default, and bench.py confines a multi-rank job's ranks to CPU slices at the process level.
 #pragma once
 
 #include <vector>
