@@ -163,6 +163,8 @@ py::dict http_stats_dict(const HttpClientStats& s) {
   d["tls_resumptions"] = s.tls_resumptions;
   d["reconnect_retries"] = s.reconnect_retries;
   d["idle_closed"] = s.idle_closed;
+  d["presends"] = s.presends;
+  d["presend_discards"] = s.presend_discards;
   d["bytes_out"] = s.bytes_out;
   d["bytes_in"] = s.bytes_in;
   d["tls_version"] = s.tls_version;
@@ -399,6 +401,17 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("set_busy_poll", &HttpClient::set_busy_poll)
       .def("warm", &HttpClient::warm, py::arg("dial_budget_ns") = HttpClient::kWarmDialBudget,
            py::call_guard<py::gil_scoped_release>())
+      .def("stage",
+           [](HttpClient& c, const std::string& method, const std::string& target, py::object headers,
+              py::bytes body) {
+             HttpRequest req;
+             req.method = method;
+             req.target = target;
+             req.headers = headers_from(headers);
+             req.body = std::string(body);
+             return c.stage(req);
+           },
+           py::arg("method"), py::arg("target"), py::arg("headers") = py::none(), py::arg("body") = py::bytes(""))
       .def("set_proxy",
            [](HttpClient& c, const std::string& url) {
              Status s = c.set_proxy(url);
@@ -693,6 +706,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("prefetch", &LoopConfig::prefetch)
       .def_readwrite("prefetch_always", &LoopConfig::prefetch_always)
       .def_readwrite("prewarm_ns", &LoopConfig::prewarm)
+      .def_readwrite("presend", &LoopConfig::presend)
       .def_readwrite("connect_at_start", &LoopConfig::connect_at_start)
       .def_readwrite("spin_budget_ppm", &LoopConfig::spin_budget_ppm);
 

@@ -648,6 +648,7 @@ Status HttpClient::connect_locked(int64_t deadline_ns) {
   conn_->rbuf = std::move(rbuf);
   if (timing()) conn_->stream->enable_rx_timestamps();
   stats_.connects++;
+  conn_gen_++;
   warm_dial_failed_ = false;  // reachable again: warm-ups may dial
   last_dial_ns_ = mono_ns() - t_dial;
   return Status::OK();
@@ -708,24 +709,8 @@ bool HttpClient::ready_without_dial() {
   return true;
 }
 
-Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable) {
-  *retryable = false;
-  // The idle-close peek may be skipped on a connection used or checked this recently -- unless
-  // the request must not be replayed and nobody above retries it (a Deployment write).
-  if (conn_ && conn_->uses > 0 && !(fresh_locked() && (caller_retries_ || replayable(req))) &&
-      conn_->stream->peer_closed()) {
-    stats_.idle_closed++;
-    conn_.reset();  // closed while idle: dial a fresh one (the request was never sent)
-  }
-  if (!conn_) {
-    Status s = connect_locked(deadline_ns);
-    if (!s.ok()) return s;
-  }
-  const bool reused = conn_->uses > 0;
-  conn_->uses++;
-  if (timing()) timing_cur_.write_begin = mono_ns();
-
-  std::string& wire = wire_;  // kept across requests: no allocation per request
+void HttpClient::serialize_locked(const HttpRequest& req, std::string* out) const {
+  std::string& wire = *out;
   if (wire.capacity() > 64 * 1024) std::string().swap(wire);
   wire.clear();
   wire.reserve(256 + req.body.size());
@@ -755,8 +740,69 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
   wire += "\r\n";
   wire += req.body;
 
+}
+
+bool HttpClient::stage(const HttpRequest& req) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (in_flight_ || cancelled() || !conn_ || !staged_.empty()) return false;
+  serialize_locked(req, &staged_);
+  constexpr size_t kHoldBack = 64;  // written at the due time: releases the rest
+  if (staged_.size() <= 2 * kHoldBack) {
+    staged_.clear();
+    return false;
+  }
+  staged_sent_ = staged_.size() - kHoldBack;
+  staged_gen_ = conn_gen_;
+  if (!conn_->stream->write_corked(staged_.data(), staged_sent_)) {
+    staged_.clear();
+    conn_.reset();  // part of it may be queued: the connection cannot carry another request
+    return false;
+  }
+  return true;
+}
+
+Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bool* retryable) {
+  *retryable = false;
+  // The idle-close peek may be skipped on a connection used or checked this recently -- unless
+  // the request must not be replayed and nobody above retries it (a Deployment write).
+  if (conn_ && conn_->uses > 0 && !(fresh_locked() && (caller_retries_ || replayable(req))) &&
+      conn_->stream->peer_closed()) {
+    stats_.idle_closed++;
+    conn_.reset();  // closed while idle: dial a fresh one (the request was never sent)
+  }
+  if (!conn_) {
+    Status s = connect_locked(deadline_ns);
+    if (!s.ok()) return s;
+  }
+  const bool reused = conn_->uses > 0;
+  conn_->uses++;
+  if (timing()) timing_cur_.write_begin = mono_ns();
+
+  std::string& wire = wire_;  // kept across requests: no allocation per request
+  serialize_locked(req, &wire);
+  // A staged prefix of this request (stage()) is queued, corked, on this connection: write the
+  // rest, which releases it. One staged for a different request, or on a connection since
+  // replaced, is dropped with its connection.
+  size_t skip = 0;
+  if (!staged_.empty()) {
+    if (staged_gen_ == conn_gen_ && wire == staged_) {
+      skip = staged_sent_;
+      stats_.presends++;
+    } else if (staged_gen_ == conn_gen_) {
+      stats_.presend_discards++;
+      staged_.clear();
+      conn_.reset();
+      Status c = connect_locked(deadline_ns);
+      if (!c.ok()) return c;
+      conn_->uses++;
+    } else {
+      stats_.presend_discards++;
+    }
+    staged_.clear();
+  }
   size_t written = 0;
-  Status s = conn_->stream->write_all(wire, deadline_ns, &written);
+  Status s = conn_->stream->write_all(wire, deadline_ns, &written, skip);
+  if (skip) conn_->stream->uncork();
   if (!s.ok()) {
     // Go's transport retries a request that never reached the wire (nothingWrittenError), and
     // a partly written one only if it is replayable.

@@ -72,6 +72,8 @@ struct HttpClientStats {
   uint64_t tls_resumptions = 0;  // reconnects that resumed the previous TLS session
   uint64_t reconnect_retries = 0;
   uint64_t idle_closed = 0;  // reused connections found closed by the peer before a write
+  uint64_t presends = 0;     // requests whose staged (pre-sent) prefix was completed
+  uint64_t presend_discards = 0;  // staged requests that did not match the next request
   uint64_t bytes_out = 0;
   uint64_t bytes_in = 0;
   std::string tls_version;  // of the last TLS connection ("" before one), e.g. "TLSv1.3"
@@ -149,6 +151,15 @@ class alignas(kCacheLine) HttpClient {
   // each request dialing under its own timeout.
   static constexpr Nanos kWarmDialBudget = 100 * kMillisecond;
   bool warm(Nanos dial_budget = kWarmDialBudget);
+  // Pre-send (Runner prewarm, after warm()): hands all but the last few bytes of `req` -- the
+  // request the next round_trip() will make -- to the kernel now, corked: nothing goes on the
+  // wire until that round_trip() writes the rest (or the kernel's 200 ms cork limit passes --
+  // far beyond the warm-up window), so the peer sees the request when it would have, but the
+  // kernel's send path has run and the request's final write runs warm.
+  // When the next request turns out different, or the connection was replaced meanwhile, the
+  // staged connection is closed (its queued bytes cannot be taken back) and the request dials
+  // a fresh one. Needs a live connection; returns whether the request was staged.
+  bool stage(const HttpRequest& req);
   // Whether a request could go out now without dialing: a connection exists and is either
   // fresh (a response or a check within kFreshConnNs) or passes the idle-close peek. The
   // pipelined GET, sent from inside the SQS call, goes out only then (a dial there would run
@@ -239,6 +250,11 @@ class alignas(kCacheLine) HttpClient {
   bool in_flight_ = false;
   bool caller_retries_ = false;
   bool warm_dial_failed_ = false;  // warm(): the last warm-up dial failed, none since connected
+  uint64_t conn_gen_ = 0;          // connections made so far (identifies conn_ across resets)
+  std::string staged_;             // stage(): the staged request's wire bytes ("" = none)
+  size_t staged_sent_ = 0;         // how many of them are queued in the kernel, corked
+  uint64_t staged_gen_ = 0;        // the connection they are queued on
+  void serialize_locked(const HttpRequest& req, std::string* wire) const;
   Nanos last_dial_ns_ = 0;          // how long the last successful dial (TCP + proxy + TLS) took
   bool timing_ = false;
   HttpTiming timing_cur_, timing_last_;

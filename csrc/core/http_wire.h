@@ -16,6 +16,8 @@
 #include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <poll.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <sys/socket.h>
 #include <unistd.h>
 #include <csignal>
@@ -250,8 +252,9 @@ class alignas(kCacheLine) Stream {
     }
   }
 
-  Status write_all(const std::string& data, int64_t deadline_ns, size_t* written = nullptr) {
-    size_t off = 0;
+  // Writes data[from..]; *written: the bytes of data written in all (from included).
+  Status write_all(const std::string& data, int64_t deadline_ns, size_t* written = nullptr, size_t from = 0) {
+    size_t off = from;
     struct Report {
       size_t* w;
       size_t& off;
@@ -307,6 +310,36 @@ class alignas(kCacheLine) Stream {
       if (errno == EINTR) continue;
       return !(errno == EAGAIN || errno == EWOULDBLOCK);
     }
+  }
+
+  // Corked write (HttpClient::stage): `len` bytes handed to the kernel now but held back from
+  // the wire until the next uncorked write -- a plain socket with MSG_MORE, TLS under TCP_CORK
+  // (uncork() after the final record). The kernel's send path runs for them here, so the final
+  // write later runs warm. Never blocks: a socket that cannot take the bytes at once fails it.
+  bool write_corked(const char* data, size_t len) {
+    if (ssl_) {
+      int on = 1;
+      if (setsockopt(fd_, IPPROTO_TCP, TCP_CORK, &on, sizeof on) != 0) return false;
+      corked_ = true;
+      ERR_clear_error();
+      const int n = SSL_write(ssl_, data, static_cast<int>(len));
+      return n == static_cast<int>(len);
+    }
+    size_t off = 0;
+    while (off < len) {
+      const ssize_t n = ::send(fd_, data + off, len - off, MSG_NOSIGNAL | MSG_MORE | MSG_DONTWAIT);
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) return false;
+      off += static_cast<size_t>(n);
+    }
+    return true;
+  }
+  // Releases TCP_CORK (TLS after write_corked): what is queued goes on the wire now.
+  void uncork() {
+    if (!corked_) return;
+    int off = 0;
+    setsockopt(fd_, IPPROTO_TCP, TCP_CORK, &off, sizeof off);
+    corked_ = false;
   }
 
   void set_spin_ns(int64_t ns) { spin_ns_ = ns; }
@@ -386,6 +419,7 @@ class alignas(kCacheLine) Stream {
   SSL* outer_ = nullptr;  // the proxy's TLS session when ssl_ runs inside it
   int64_t spin_ns_ = 0;
   int cancel_fd_ = -1;
+  bool corked_ = false;
   bool ts_ = false;
   FirstBytes first_;
   int64_t pending_rx_real_ = 0;

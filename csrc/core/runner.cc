@@ -88,7 +88,7 @@ IterationRecord Runner::step(StopFlag* stop) {
     const Nanos due = clock_->now() + period;
     slept = clock_->sleep(period - w, stop);
     if (slept) {
-      warm(due);
+      warm(due, true);
       slept = clock_->spin_until(due, stop);
     }
   } else {
@@ -105,8 +105,8 @@ IterationRecord Runner::step(StopFlag* stop) {
   return poll_once();
 }
 
-void Runner::warm(Nanos due) {
-  sqs_->warm(clock_->unix_nanos() + (due - clock_->now()));
+void Runner::warm(Nanos due, bool presend) {
+  sqs_->warm(clock_->unix_nanos() + (due - clock_->now()), presend && cfg_.presend);
   // the Deployment read and write only follow on polls the gates may let through (or every
   // poll, with a GET sent on every poll)
   if ((cfg_.prefetch && cfg_.prefetch_always) || action_likely(due)) scaler_->warm();

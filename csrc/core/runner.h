@@ -57,6 +57,14 @@ struct LoopConfig {
   // up to `prewarm` of CPU per poll. 0 disables. With a poll period under 2x `prewarm` the
   // preparation runs at the due time instead, without the early wake-up.
   Nanos prewarm = 0;
+  // With the early wake-up, also pre-send the SQS request (HttpClient::stage): all but its last
+  // bytes are handed to the kernel corked, so the kernel's send path has run before the due
+  // time and the poll's own write runs warm; nothing reaches the wire before the due time
+  // (unless the poll starts over 200 ms late, the kernel's cork limit: then the peer holds a
+  // partial request until the rest comes), and
+  // the request is byte for byte the one the poll sends (when it is not -- its signing second
+  // rolled over -- the staged connection is dropped and the poll dials a fresh one).
+  bool presend = true;
   // Dial both clients at Run() entry, on the worker's own thread, before the timers are armed
   // (decisions unchanged). A harness that would otherwise connect them from its main thread
   // (the bench) gets each connection's TLS state and buffers from the worker's allocator arena
@@ -228,7 +236,7 @@ class alignas(kCacheLine) Runner {
   IterationRecord poll_once();
   // The pre-poll warm-up (LoopConfig::prewarm) for a poll due at `due`, without waiting: the
   // Scheduler runs it as its own event `prewarm` before the poll's.
-  void prepare(Nanos due) { warm(due); }
+  void prepare(Nanos due) { warm(due, true); }
   // Shutdown: aborts this worker's API call in progress and its back-off/throttle waits.
   void cancel() {
     sqs_->cancel();
@@ -289,7 +297,7 @@ class alignas(kCacheLine) Runner {
 
  private:
   IterationRecord poll_body();
-  void warm(Nanos due);
+  void warm(Nanos due, bool presend = false);
   void record(const IterationRecord& r);
   void mirror(const IterationRecord& r);
   CpuList cpus_;

@@ -175,16 +175,28 @@ void HttpSqsApi::sign_locked(const std::string& queue_url, const std::vector<std
   }
 }
 
-void HttpSqsApi::warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) {
+void HttpSqsApi::warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns,
+                      bool presend) {
   if (!endpoint_status_.ok() || cancel_.stopped()) return;
   // Credentials first: a refresh (IMDS, STS, a credential process) happens here, not inside
   // the poll. Then the request signed for the second the poll is due in, and the connection.
   auto cr = creds_.get(at_unix_ns);
-  if (cr.ok()) {
+  if (!cr.ok()) {
+    http_->warm();
+    return;
+  }
+  HttpRequest req;
+  {
     std::lock_guard<std::mutex> lk(prep_mu_);
     sign_locked(queue_url, names, cr.value, at_unix_ns);
+    if (presend) {  // the request call_once() will make, byte for byte, when the second holds
+      req.method = "POST";
+      req.target = url_.path.empty() ? "/" : url_.path;
+      req.body = prepared_body_;
+      req.headers = signed_headers_;
+    }
   }
-  http_->warm();
+  if (http_->warm() && presend) http_->stage(req);
 }
 
 Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,

@@ -58,11 +58,15 @@ class SqsApi {
   virtual void set_spin_budget(Nanos ns) { (void)ns; }
   // Pre-poll warm-up (Runner prewarm), just before a call due at unix time `at_unix_ns`: do
   // now what the call would otherwise do first -- credentials, the request and its signature
-  // for that second, the connection check or dial. Sends nothing. Default: nothing.
-  virtual void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) {
+  // for that second, the connection check or dial -- and, with `presend`, hand all but the
+  // request's last bytes to the kernel corked (HttpClient::stage): nothing reaches the wire
+  // before the call. Default: nothing.
+  virtual void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns,
+                    bool presend = false) {
     (void)queue_url;
     (void)names;
     (void)at_unix_ns;
+    (void)presend;
   }
 };
 
@@ -107,7 +111,8 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   std::string endpoint() const { return endpoint_; }
   Nanos waiting_until() const override { return wait_until_.load(std::memory_order_acquire); }
   bool runs_on_wire_work() const override { return true; }
-  void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns) override;
+  void warm(const std::string& queue_url, const std::vector<std::string>& names, int64_t at_unix_ns,
+            bool presend = false) override;
   void set_spin_budget(Nanos ns) override {
     if (http_) http_->set_spin_budget(ns);
   }
@@ -170,7 +175,7 @@ class alignas(kCacheLine) SqsClient {
   const std::vector<std::string>& attribute_names() const { return names_; }
   std::shared_ptr<SqsApi> api() const { return api_; }
   void cancel() { api_->cancel(); }
-  void warm(int64_t at_unix_ns) { api_->warm(queue_url_, names_, at_unix_ns); }
+  void warm(int64_t at_unix_ns, bool presend = false) { api_->warm(queue_url_, names_, at_unix_ns, presend); }
 
  private:
   std::shared_ptr<SqsApi> api_;

@@ -212,6 +212,7 @@ class BenchEnv:
     production endpoint is (supported with ``shared``, ``process`` and ``split``). ``prewarm_ns``: the
     loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
     period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
+    ``presend``: stage each poll's SQS request during the warm-up (LoopConfig.presend);
     these, ``busy_poll_ns``, ``mode`` and ``pipeline`` may be lists, one value per queue, cycled
     (paired comparisons within one run: :func:`measure_cadenced_arms`). ``timing``: the clients time every request's
     phases (HttpTiming), traced polls carry the breakdown (``detail``), and the fakes record each
@@ -221,7 +222,7 @@ class BenchEnv:
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", log_level: str = "info", sqs_protocol: str = "query",
                  poll_period_ns: int = 0, stagger: bool = False, hot_endpoints: bool = False, prewarm_ns: int = 0,
-                 timing: bool = False, spin_budget_ppm=None):
+                 timing: bool = False, spin_budget_ppm=None, presend=True):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -299,6 +300,7 @@ class BenchEnv:
             cfg.scale_down_messages = 10
             cfg.prefetch = pipeline_q
             cfg.prewarm_ns = pw_q
+            cfg.presend = per_queue(presend, q)
             # the CLI's share (autoscaler.loop_config) unless given
             cfg.spin_budget_ppm = (SPIN_BUDGET_PPM // queues if spin_budget_ppm is None
                                    else per_queue(spin_budget_ppm, q))
@@ -534,7 +536,7 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     branch predictors are cold, the CPU may sit in a deep idle state, and a keep-alive
     connection unused for longer than ``kFreshConnNs`` gets the idle-close check again. The
     hot-loop rows measure none of that. Here every arm (``name -> dict(mode, pipeline,
-    busy_poll_ns, prewarm_ns)``) gets ``queues_per_arm`` queues; queue q runs arm q % len(arms),
+    busy_poll_ns, prewarm_ns[, presend])``) gets ``queues_per_arm`` queues; queue q runs arm q % len(arms),
     so the arms' queues interleave in one fleet (a thread each, starts staggered over the
     period) and run ``polls`` polls at ``poll_period_ns`` in the same run, against the same
     ``split`` endpoints (one fake SQS process and one apiserver process serving every queue, as
@@ -551,13 +553,13 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
 
     names = list(arms)
     n = len(names)
-    col = lambda k: [arms[a][k] for a in names]  # noqa: E731 -- cycled per queue by BenchEnv
+    col = lambda k, default=None: [arms[a].get(k, default) for a in names]  # noqa: E731 -- cycled per queue
     # each arm's queues get the spin budget the CLI gives a process tracking that many queues
     # (1 % of the period shared by them), not a share diluted by the other arms' queues
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
                    hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,
-                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm)
+                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm, presend=col("presend", True))
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: Dict[str, List[dict]] = {a: [] for a in names}
     try:
