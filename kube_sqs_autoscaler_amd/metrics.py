@@ -58,6 +58,22 @@ _API_COUNTERS = [
 ]
 _NS_COUNTERS = {"throttle_ns"}  # exported in seconds
 
+# Per-worker transport counters of each client's keep-alive connection (HttpClientStats, the
+# "http" sub-dict of the client stats), labelled client="sqs" | "apiserver": (metric, help, key)
+_HTTP_COUNTERS = [
+    ("http_requests", "HTTP requests written (retries included)", "requests"),
+    ("http_connects", "Connections dialled (TCP, plus the TLS handshake over HTTPS)", "connects"),
+    ("http_tls_resumptions", "TLS handshakes that resumed a session instead of a full handshake", "tls_resumptions"),
+    ("http_reconnect_retries", "Requests re-sent on a fresh connection after a reused one failed before any "
+                               "response byte", "reconnect_retries"),
+    ("http_idle_closed", "Keep-alive connections found closed by the peer before a request", "idle_closed"),
+    ("http_presends", "Polls whose SQS request was staged during the warm-up and released at the due time",
+     "presends"),
+    ("http_presend_discards", "Staged requests dropped (the poll's request differed, or the connection was "
+                              "replaced) together with their connection", "presend_discards"),
+]
+_CLIENT_LABEL = {"sqs_api": "sqs", "kube_api": "apiserver"}
+
 
 def _client_stats(client) -> dict:
     try:
@@ -107,6 +123,7 @@ class FleetCollector:
         stats = self.fleet.stats()
         fams = {k: _Family(f"ksa_{k}_total", "counter", h) for k, h in _COUNTERS}
         api = {k: _Family(f"ksa_{k}_total", "counter", h) for k, h, _, _ in _API_COUNTERS}
+        http = {k: _Family(f"ksa_{k}_total", "counter", h) for k, h, _ in _HTTP_COUNTERS}
         depth = _Family("ksa_queue_depth", "gauge", "Last observed queue depth (sum of attributes)")
         reps = _Family("ksa_replicas", "gauge", "Last observed Deployment replicas")
         failing = _Family("ksa_consecutive_failed_polls", "gauge",
@@ -126,6 +143,11 @@ class FleetCollector:
                 if key in clients[attr]:
                     v = clients[attr][key]
                     api[k].add("", lv, v / 1e9 if key in _NS_COUNTERS else v)
+            for attr, name in _CLIENT_LABEL.items():
+                transport = clients[attr].get("http") or {}
+                for k, _, key in _HTTP_COUNTERS:
+                    if key in transport:
+                        http[k].add("", lv + [("client", name)], transport[key])
             depth.add("", lv, s["last_depth"])
             reps.add("", lv, s["last_replicas"])
             failing.add("", lv, s.get("consecutive_failed_polls", 0))
@@ -139,7 +161,8 @@ class FleetCollector:
                 hist.add("_bucket", lv + [("le", _num(le))], cum)
             hist.add("_count", lv, cum)
             hist.add("_sum", lv, s["latency_sum_ns"] / 1e9)
-        return [*fams.values(), *(f for f in api.values() if f.samples), depth, reps, failing, failing_s, lat, hist]
+        return [*fams.values(), *(f for f in (*api.values(), *http.values()) if f.samples), depth, reps, failing,
+                failing_s, lat, hist]
 
     def exposition(self) -> bytes:
         out: List[str] = []

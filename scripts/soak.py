@@ -67,10 +67,14 @@ def scrape(port: int) -> dict:
             continue
         name = line.split("{", 1)[0]
         if name.endswith("_total"):
-            tot[name[4:-6]] = tot.get(name[4:-6], 0) + float(line.rsplit(" ", 1)[1])
+            key = name[4:-6]
+            if 'client="' in line:  # transport counters: one per client (sqs / apiserver)
+                key += "_" + line.split('client="', 1)[1].split('"', 1)[0]
+            tot[key] = tot.get(key, 0) + float(line.rsplit(" ", 1)[1])
     return {k: int(v) for k, v in tot.items() if k in (
         "polls", "scale_ups", "scale_downs", "depth_errors", "failed_ups", "failed_downs", "sqs_retries",
-        "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors")}
+        "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors") or (
+        k.startswith("http_") and k.split("_")[1] in ("connects", "presends", "presend", "reconnect", "idle"))}
 
 
 def free_port() -> int:

@@ -77,6 +77,16 @@ def test_metrics_endpoints(nat):
             assert metric["ksa_apiserver_gets_total"] == 10 and metric["ksa_apiserver_conflicts_total"] == 0
             assert metric["ksa_apiserver_throttled_total"] == 0 and metric["ksa_apiserver_throttle_seconds_total"] == 0
             assert metric["ksa_sqs_throttle_retries_total"] == 0 and metric["ksa_speculative_reads_skipped_total"] == 0
+            # transport counters, per client: one keep-alive connection each; the apiserver
+            # connection carries the 10 GETs and the 10 writes
+            http = {(line.split("{")[0], line.split('client="')[1].split('"')[0]): float(line.rsplit(" ", 1)[1])
+                    for line in body.splitlines() if line.startswith("ksa_http_") and 'deployment="bench/gpu-worker-0"' in line}
+            assert http[("ksa_http_requests_total", "sqs")] == 10
+            assert http[("ksa_http_requests_total", "apiserver")] == 20
+            assert http[("ksa_http_connects_total", "sqs")] == 1 == http[("ksa_http_connects_total", "apiserver")]
+            # back to back (no poll period): no warm-up, so nothing is staged
+            assert http[("ksa_http_presends_total", "sqs")] == 0 == http[("ksa_http_presend_discards_total", "sqs")]
+            assert "# TYPE ksa_http_idle_closed_total counter" in body
             # latency histogram: cumulative buckets ending at +Inf == count, same sum as the summary
             buckets = [(line.split('le="')[1].split('"')[0], float(line.rsplit(" ", 1)[1]))
                        for line in body.splitlines()

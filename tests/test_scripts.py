@@ -35,6 +35,10 @@ def test_soak_script_short(nat):
                 timeout=200)
     summary = rows[-1]
     assert summary["summary"] and summary["replay"]["mismatches"] == 0 and summary["exit_code"] == 0
+    # the per-client transport counters of /metrics reach the window rows: the CLI's default
+    # warm-up stages the polls' SQS requests (1 s period)
+    windows = [r for r in rows if "window" in r and "scrape_error" not in r]
+    assert windows and windows[-1]["http_connects_sqs"] >= 2 and windows[-1]["http_presends_sqs"] > 0
 
 
 @pytest.mark.slow
