@@ -169,17 +169,20 @@ def test_rank_launcher_stops_its_ranks_when_it_is_terminated(tmp_path):
     script = tmp_path / "rank.py"
     pids = tmp_path / "pids"
     pids.mkdir()
+    # written under a temporary name and renamed, so the test never reads a half-written file
     script.write_text("import os, time\n"
-                      f"open(os.path.join({str(pids)!r}, os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                      f"f = os.path.join({str(pids)!r}, os.environ['RANK'])\n"
+                      "open(f + '.tmp', 'w').write(str(os.getpid()))\n"
+                      "os.replace(f + '.tmp', f)\n"
                       "time.sleep(120)\n")
     launcher = tmp_path / "launch.py"
     launcher.write_text(f"import sys; sys.path.insert(0, {ROOT!r}); import bench\n"
                         f"sys.exit(bench._launch_ranks(2, [], script={str(script)!r}))\n")
     p = subprocess.Popen([sys.executable, str(launcher)])
     deadline = time.monotonic() + 30
-    while len(list(pids.iterdir())) < 2 and time.monotonic() < deadline:
+    while len(list(pids.glob("[0-9]"))) < 2 and time.monotonic() < deadline:
         time.sleep(0.05)
-    ranks = [int(f.read_text()) for f in pids.iterdir()]
+    ranks = [int(f.read_text()) for f in pids.glob("[0-9]")]
     assert len(ranks) == 2
     p.send_signal(signal.SIGTERM)
     assert p.wait(timeout=30) == 128 + signal.SIGTERM
