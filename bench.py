@@ -198,6 +198,34 @@ def _pin_rank(mode: str):
     return mine
 
 
+def _pool(samples_ns, wall_s: float, device, collective: bool):
+    """The job-wide view after the timed region: every rank's latency samples (sorted) and the
+    slowest rank's wall time. Over the process group when ``collective`` (tensors on ``device``:
+    this rank's GPU under RCCL, the CPU under gloo); ranks may hold different sample counts (a
+    poll whose write failed records none), and all_gather needs equal shapes, so each pads to
+    the largest count with -1 and the padding is dropped."""
+    import torch
+    import torch.distributed as dist
+
+    samples = torch.tensor(sorted(samples_ns), dtype=torch.int64, device=device)
+    wall_t = torch.tensor([wall_s], dtype=torch.float64, device=device)
+    if collective:
+        world = dist.get_world_size()
+        count = torch.tensor([samples.numel()], dtype=torch.int64, device=device)
+        counts = [torch.empty_like(count) for _ in range(world)]
+        dist.all_gather(counts, count)
+        longest = max(int(c.item()) for c in counts)
+        if longest:  # (every rank empty: nothing to gather)
+            padded = torch.full((longest,), -1, dtype=torch.int64, device=device)
+            padded[: samples.numel()] = samples
+            gathered = [torch.empty_like(padded) for _ in range(world)]
+            dist.all_gather(gathered, padded)
+            samples = torch.cat(gathered)
+            samples = samples[samples >= 0]
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    return sorted(samples.cpu().tolist()), float(wall_t.item())
+
+
 def _free_port() -> int:
     import socket
 
@@ -359,24 +387,7 @@ def main(argv=None) -> int:
     finally:
         env.close()
 
-    samples = torch.tensor(sorted(res.samples), dtype=torch.int64, device=device)
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
-    if world > 1:
-        # Ranks can hold different sample counts (a poll whose write failed records none):
-        # all_gather needs equal shapes, so pad to the largest count with -1 and drop the padding.
-        count = torch.tensor([samples.numel()], dtype=torch.int64, device=device)
-        counts = [torch.empty_like(count) for _ in range(world)]
-        dist.all_gather(counts, count)
-        longest = max(int(c.item()) for c in counts)
-        padded = torch.full((longest,), -1, dtype=torch.int64, device=device)
-        padded[: samples.numel()] = samples
-        gathered = [torch.empty_like(padded) for _ in range(world)]
-        dist.all_gather(gathered, padded)
-        samples = torch.cat(gathered)
-        samples = samples[samples >= 0]
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    all_ns = sorted(samples.cpu().tolist())
-    wall_max = float(wall_t.item())
+    all_ns, wall_max = _pool(res.samples, wall, device, collective=world > 1)
 
     def pct(v, p):
         import math

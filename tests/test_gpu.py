@@ -261,6 +261,33 @@ def test_sharded_sweep_cli_on_gpu(tmp_path):
     assert sorted(rows, key=lambda x: x["pod_hours_mean"]) == want
 
 
+def test_bench_pools_samples_over_rccl():
+    """bench.py's job-wide pooling (``_pool``: padded all_gather of the samples, MAX all_reduce of
+    the wall time) on this GPU's tensors over an RCCL process group. One GPU allows one rank, so
+    the group has one; the collectives, dtypes (int64, float64) and the padding path are the ones
+    an N-GPU job runs. In a fresh process, as above."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import json, os, sys, torch, torch.distributed as dist\n"
+        f"sys.path.insert(0, {root!r}); import bench\n"
+        "torch.cuda.set_device(0); dev = torch.device('cuda', 0)\n"
+        "dist.init_process_group('nccl', device_id=dev)\n"
+        "ns, wall = bench._pool([30, 10, 20], 1.5, dev, collective=True)\n"
+        "empty, _ = bench._pool([], 0.25, dev, collective=True)\n"
+        "print(json.dumps({'backend': dist.get_backend(), 'ns': ns, 'wall': wall, 'empty': empty}))\n"
+        "dist.destroy_process_group()\n")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29519", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert out == {"backend": "nccl", "ns": [10, 20, 30], "wall": 1.5, "empty": []}
+
+
 def test_sweep_kernel_random_lanes_equal_oracle():
     """the gfx950 open-loop kernel against the independent Python oracle on 256 lanes
     per dispatch (adversarial + random configurations), with the trace in LDS and in global
