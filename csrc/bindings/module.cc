@@ -890,7 +890,8 @@ PYBIND11_MODULE(_ksa_native, m) {
   using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
   using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
   m.def("sweep_cpu",
-        [](I64 trace_t, I64 trace_d, int32_t init, int64_t horizon, I64 latency, I64 params, int threads, bool ns_clock) {
+        [](I64 trace_t, I64 trace_d, int32_t init, int64_t horizon, I64 latency, I64 params, int threads, bool ns_clock,
+           int skip) {
           if (trace_t.ndim() != 1 || trace_d.ndim() != 1 || trace_t.shape(0) != trace_d.shape(0) || trace_t.shape(0) < 1)
             throw py::value_error("trace_t / trace_d must be 1-D arrays of equal non-zero length");
           if (trace_t.at(0) != 0) throw py::value_error("the trace must start at t=0");
@@ -899,17 +900,18 @@ PYBIND11_MODULE(_ksa_native, m) {
           const int64_t m = params.shape(1);
           I64 out64({int64_t(3), m});
           I32 out32({int64_t(7), m});
-          bool ms = false;
+          if (skip < 0 || skip > 2) throw py::value_error("skip must be 0 (auto), 1 (always) or 2 (never)");
+          int used = 0;
           {
             py::gil_scoped_release rel;
-            ms = sweep_cpu(trace_t.data(), trace_d.data(), static_cast<int32_t>(trace_t.shape(0)), init, horizon,
-                           latency.data(), params.data(), m, out64.mutable_data(), out32.mutable_data(), threads,
-                           ns_clock ? 1 : 0);
+            used = sweep_cpu(trace_t.data(), trace_d.data(), static_cast<int32_t>(trace_t.shape(0)), init, horizon,
+                             latency.data(), params.data(), m, out64.mutable_data(), out32.mutable_data(), threads,
+                             (ns_clock ? 1 : 0) | (skip << 2));
           }
-          return py::make_tuple(out64, out32, ms);
+          return py::make_tuple(out64, out32, (used & 1) != 0, (used & 2) != 0);
         },
         py::arg("trace_t"), py::arg("trace_d"), py::arg("init_replicas"), py::arg("horizon_ns"), py::arg("latency"),
-        py::arg("params"), py::arg("threads") = 8, py::arg("ns_clock") = false);
+        py::arg("params"), py::arg("threads") = 8, py::arg("ns_clock") = false, py::arg("skip") = 0);
 
   m.def("queue_sweep_cpu",
         [](I64 t_ms, I64 rate_milli, int32_t init, int64_t horizon, I64 latency, I64 model, I64 params, int32_t seeds,

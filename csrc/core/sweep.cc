@@ -9,14 +9,17 @@
 
 namespace ksa {
 
-bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
-               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads,
-               int arith) {
-  if (m <= 0 || n < 1) return false;
+int sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+              const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads,
+              int arith) {
+  if (m <= 0 || n < 1) return 0;
   for (int k = 0; k < 3; ++k)
-    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return false;  // sweep.py validates first
+    if (latency[k] < 0 || latency[k] > ksa_sim::kMaxLatencyNs) return 0;  // sweep.py validates first
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
-  const bool ms = arith == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
+  const bool ms = (arith & 3) == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
+  const int skip_mode = (arith >> 2) & 3;
+  const bool skip = skip_mode == 1 || (skip_mode == 0 && ksa_sim::skip_pays(trace_t, n, horizon_ns, latency, params, m, ms ? 4 : 8));
+  const int used = (ms ? 1 : 0) | (skip ? 2 : 0);
   std::vector<int32_t> t32(ms ? n : 0), d32(ms ? n : 0);
   if (ms) ksa_sim::narrow_policy_trace(trace_t, trace_d, n, t32.data(), d32.data());
   const ksa_sim::MsLatency lat_ms = ksa_sim::ms_latency(lat);
@@ -33,8 +36,10 @@ bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
       p.max_pods = params[7 * m + i];
       p.min_pods = params[8 * m + i];
       const ksa_sim::Result r =
-          ms ? ksa_sim::simulate_ms(p, lat_ms, t32.data(), d32.data(), n, init_replicas, horizon_ns)
-             : ksa_sim::simulate(p, lat, trace_t, trace_d, n, init_replicas, horizon_ns);
+          ms ? (skip ? ksa_sim::simulate_ms<true>(p, lat_ms, t32.data(), d32.data(), n, init_replicas, horizon_ns)
+                     : ksa_sim::simulate_ms<false>(p, lat_ms, t32.data(), d32.data(), n, init_replicas, horizon_ns))
+             : (skip ? ksa_sim::simulate<true>(p, lat, trace_t, trace_d, n, init_replicas, horizon_ns)
+                     : ksa_sim::simulate<false>(p, lat, trace_t, trace_d, n, init_replicas, horizon_ns));
       out64[0 * m + i] = r.pod_ms;
       out64[1 * m + i] = r.backlog;
       out64[2 * m + i] = r.first_up_ns;
@@ -51,7 +56,7 @@ bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
   if (t > m) t = static_cast<int>(m);
   if (t == 1) {
     work(0, m);
-    return ms;
+    return used;
   }
   // Interleaved chunks balance the (period-dependent) cost across threads.
   std::vector<std::thread> pool;
@@ -66,7 +71,7 @@ bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_
       }
     });
   for (auto& th : pool) th.join();
-  return ms;
+  return used;
 }
 
 int queue_sweep_cpu(const int64_t* t_ms, const int64_t* rate_milli, int32_t n, int32_t init_replicas,

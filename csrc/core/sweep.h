@@ -10,11 +10,13 @@
 namespace ksa {
 
 // Layouts as in ksa_sweep_gpu (csrc/hip/policy_sweep.hip): params [9][m], out64 [3][m],
-// out32 [7][m], latency {sqs, get, update} ns. arith: 0 runs ksa_sim::simulate_ms when
-// ms_path_ok holds, 1 forces simulate (nanosecond clock). Returns true if the ms clock ran.
-bool sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
-               const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads,
-               int arith = 0);
+// out32 [7][m], latency {sqs, get, update} ns. arith bits 0-1: 0 runs ksa_sim::simulate_ms when
+// ms_path_ok holds, 1 forces simulate (nanosecond clock); bits 2-3: the steady-stretch skip, 0 when
+// ksa_sim::skip_pays, 1 always, 2 never (same results). Returns bit 0: the ms clock ran, bit 1:
+// the skip ran.
+int sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas, int64_t horizon_ns,
+              const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64, int32_t* out32, int threads,
+              int arith = 0);
 
 // Closed-loop sweep (csrc/sim/queue_sim.h), CPU path; layouts as ksa_queue_sweep_gpu
 // (csrc/hip/queue_sweep.hip): params [9][m], model {service_milli, startup_ns, slo_backlog,

@@ -56,7 +56,7 @@ enum : int { kUps = 0, kDowns, kNoopUps, kNoopDowns, kFinal, kMaxRep, kPolls, kN
 // array, chosen per launch, so the loads are flat: specialising them into ds_read and
 // global_load copies of the loop (two inlined calls) measured slower on the global path (24.5 vs
 // 22.5 ms, profiles/r03u_sweep_ab.jsonl) and equal from LDS.
-template <bool kMs, class T>
+template <bool kMs, bool kSkip, class T>
 __device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, int64_t m, const ksa_sim::Latency& lat,
                                             const T* __restrict__ t, const T* __restrict__ d, int32_t n, int32_t init,
                                             int64_t horizon, int64_t* __restrict__ out64, int32_t* __restrict__ out32) {
@@ -75,9 +75,9 @@ __device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, 
     p.min_pods = params[kMinPods * m + i];
     ksa_sim::Result r;
     if constexpr (kMs)
-      r = ksa_sim::simulate_ms(p, lat_ms, t, d, n, init, horizon);
+      r = ksa_sim::simulate_ms<kSkip>(p, lat_ms, t, d, n, init, horizon);
     else
-      r = ksa_sim::simulate(p, lat, t, d, n, init, horizon);
+      r = ksa_sim::simulate<kSkip>(p, lat, t, d, n, init, horizon);
     out64[kPodMs * m + i] = r.pod_ms;
     out64[kBacklog * m + i] = r.backlog;
     out64[kFirstUp * m + i] = r.first_up_ns;
@@ -92,8 +92,9 @@ __device__ __forceinline__ void sweep_lanes(const int64_t* __restrict__ params, 
 }
 
 // kMs: ksa_sim::simulate_ms over a 32-bit trace (T = int32_t; the host checked ms_path_ok), else
-// ksa_sim::simulate over the int64 trace.
-template <bool kMs, class T>
+// ksa_sim::simulate over the int64 trace. kSkip: the steady-stretch skip (ksa_sim::skip_pays), a
+// separate instantiation because its code costs registers and time where no stretch forms.
+template <bool kMs, bool kSkip, class T>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEEP_WAVES_PER_EU))) void sweep_kernel(
     const int64_t* __restrict__ params, int64_t m, ksa_sim::Latency lat, const T* __restrict__ g_t,
     const T* __restrict__ g_d, int32_t n, int32_t init, int64_t horizon, int64_t* __restrict__ out64,
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KSA_SWEE
     }
     __syncthreads();
   }
-  sweep_lanes<kMs>(params, m, lat, in_lds ? static_cast<const T*>(s_t) : g_t, in_lds ? static_cast<const T*>(s_d) : g_d, n,
+  sweep_lanes<kMs, kSkip>(params, m, lat, in_lds ? static_cast<const T*>(s_t) : g_t, in_lds ? static_cast<const T*>(s_d) : g_d, n,
                    init, horizon, out64, out32);
 }
 
@@ -122,7 +123,7 @@ bool ok(hipError_t e, const char* what) {
 
 // Launches one path's kernel on the arena's stream. The grid is one resident wave of workgroups
 // (KSA_SWEEP_GRID: "tiles" = one workgroup per 256 configurations, or N x resident).
-template <bool kMs, class T>
+template <bool kMs, bool kSkip, class T>
 bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const ksa_sim::Latency& lat, const T* d_t,
             const T* d_d, int32_t n, int32_t init, int64_t horizon_ns, int64_t* d_o64, int32_t* d_o32) {
   const int64_t want = (m + kBlock - 1) / kBlock;
@@ -132,13 +133,13 @@ bool launch(const ksa_gpu::DeviceArena& ar, const int64_t* d_p, int64_t m, const
     cap_bytes = std::min<size_t>(static_cast<size_t>(std::max(0, std::atoi(c))), 64 * 1024);
   const size_t lds = trace_bytes <= cap_bytes ? trace_bytes : 0;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<kMs, T>, kBlock, lds) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sweep_kernel<kMs, kSkip, T>, kBlock, lds) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
   int64_t cap = static_cast<int64_t>(ar.cus) * per_cu;
   if (const char* g = std::getenv("KSA_SWEEP_GRID")) cap = std::strcmp(g, "tiles") == 0 ? want : cap * std::max(1, std::atoi(g));
   const int grid = static_cast<int>(want < cap ? want : cap);
-  hipLaunchKernelGGL((sweep_kernel<kMs, T>), dim3(grid), dim3(kBlock), lds, ar.stream, d_p, m, lat, d_t, d_d, n, init,
+  hipLaunchKernelGGL((sweep_kernel<kMs, kSkip, T>), dim3(grid), dim3(kBlock), lds, ar.stream, d_p, m, lat, d_t, d_d, n, init,
                      horizon_ns, d_o64, d_o32, lds > 0);
   return ok(hipGetLastError(), "sweep_kernel launch");
 }
@@ -151,9 +152,10 @@ const char* ksa_sweep_last_error() { return g_sweep_error.c_str(); }
 
 // params: [9][m] int64 (poll, up_cool, down_cool, up_msgs, down_msgs, up_pods, down_pods, max, min)
 // out64:  [3][m] int64 (pod_ms, backlog, first_up_ns); out32: [7][m] int32 (ups, downs, noop_ups,
-// noop_downs, final, max_replicas, polls). latency: {sqs, get, update} ns. arith: 0 runs the
-// millisecond clock when ksa_sim::ms_path_ok holds, 1 forces the nanosecond one; *ms_used reports
-// the choice. Returns 0 on success.
+// noop_downs, final, max_replicas, polls). latency: {sqs, get, update} ns. arith bits 0-1: 0 runs
+// the millisecond clock when ksa_sim::ms_path_ok holds, 1 forces the nanosecond one; bits 2-3: the
+// steady-stretch skip, 0 when ksa_sim::skip_pays, 1 always, 2 never (same results). *ms_used
+// reports the choices: bit 0 the ms clock, bit 1 the skip. Returns 0 on success.
 int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t init_replicas,
                   int64_t horizon_ns, const int64_t* latency, const int64_t* params, int64_t m, int64_t* out64,
                   int32_t* out32, double* kernel_ms, int32_t arith, int32_t* ms_used) {
@@ -168,8 +170,10 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
     }
   }
   if (m <= 0) return 0;
-  const bool ms = arith == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
-  if (ms_used) *ms_used = ms ? 1 : 0;
+  const bool ms = (arith & 3) == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
+  const int skip_mode = (arith >> 2) & 3;
+  const bool skip = skip_mode == 1 || (skip_mode == 0 && ksa_sim::skip_pays(trace_t, n, horizon_ns, latency, params, m, ms ? 4 : 8));
+  if (ms_used) *ms_used = (ms ? 1 : 0) | (skip ? 2 : 0);
   // the trace in the chosen path's element type
   std::vector<int32_t> t32, d32;
   const size_t elem = ms ? sizeof(int32_t) : sizeof(int64_t);
@@ -203,11 +207,15 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
   int64_t* o64 = static_cast<int64_t*>(d_o64);
   int32_t* o32 = static_cast<int32_t*>(d_o32);
   if (!ok(hipEventRecord(ar->e0, st), "hipEventRecord")) return -1;
+  const auto* g_t32 = static_cast<const int32_t*>(d_t);
+  const auto* g_d32 = static_cast<const int32_t*>(d_d);
+  const auto* g_t64 = static_cast<const int64_t*>(d_t);
+  const auto* g_d64 = static_cast<const int64_t*>(d_d);
   const bool launched =
-      ms ? launch<true>(*ar, p, m, lat, static_cast<const int32_t*>(d_t), static_cast<const int32_t*>(d_d), n,
-                        init_replicas, horizon_ns, o64, o32)
-         : launch<false>(*ar, p, m, lat, static_cast<const int64_t*>(d_t), static_cast<const int64_t*>(d_d), n,
-                         init_replicas, horizon_ns, o64, o32);
+      ms ? (skip ? launch<true, true>(*ar, p, m, lat, g_t32, g_d32, n, init_replicas, horizon_ns, o64, o32)
+                 : launch<true, false>(*ar, p, m, lat, g_t32, g_d32, n, init_replicas, horizon_ns, o64, o32))
+         : (skip ? launch<false, true>(*ar, p, m, lat, g_t64, g_d64, n, init_replicas, horizon_ns, o64, o32)
+                 : launch<false, false>(*ar, p, m, lat, g_t64, g_d64, n, init_replicas, horizon_ns, o64, o32));
   if (!launched) return -1;
   if (!ok(hipEventRecord(ar->e1, st), "hipEventRecord")) return -1;
   if (!ok(hipMemcpyAsync(out64, o64, kNumOut64 * m * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync") ||

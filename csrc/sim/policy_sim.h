@@ -240,6 +240,30 @@ KSA_HD int64_t interval_ms(Intervals t, int32_t gets, int32_t writes) {
   return t.g0 + (gets == 0 ? 0 : (gets == 1 ? (writes == 0 ? t.g1u0 : t.g1u1) : g2));
 }
 
+// Steady stretches. A poll that called nothing leaves the timers and replicas as they were, so
+// the polls after it call nothing either for as long as they see the same depth (until the
+// trace's next boundary) and (a) that depth is strictly between the thresholds, or (b) it is at
+// or past a threshold whose cool-down has not run out: blocked at `now` = t + sqs, it stays
+// blocked while t + sqs < last + cool (the up check, blocked, also skips the down check, as the
+// reference's `continue` does). Each such poll only adds a left sum of the same dt, so the
+// simulators add a whole stretch at once, and a lane's loop runs once per decision or trace
+// boundary instead of once per poll. Returns the exclusive bound on the start time of a poll in
+// the stretch, capped at horizon + 1 (a poll starts at t <= horizon). T: int32 on the
+// millisecond clock, int64 on the nanosecond one; the hosts' bounds keep every sum in range.
+template <class K, class T>
+KSA_HD T steady_limit(const K& k, T d, T last_up, T last_down, T sqs, T next_t, T horizon) {
+  T lim = next_t < horizon + 1 ? next_t : horizon + 1;
+  if (d >= k.up_msgs) {
+    const T b = last_up + k.up_cool - sqs;
+    if (b < lim) lim = b;
+  } else if (d <= k.down_msgs) {
+    const T b = last_down + k.down_cool - sqs;
+    if (b < lim) lim = b;
+  }
+  return lim;
+}
+
+template <bool kSkip = true>
 KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns, const int64_t* depth, int32_t n,
                        int32_t init_replicas, int64_t horizon_ns) {
   Result res;
@@ -273,6 +297,20 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
     if (replicas > res.max_replicas) res.max_replicas = replicas;
     prev_d = d;
     dt_ms = interval_ms(iv, gets, writes);
+    if (kSkip && gets == 0) {  // a poll that called nothing: skip the stretch of polls just like it
+      const int64_t lim = steady_limit(k, d, last_up, last_down, lat.sqs_ns, cursor.next_t, horizon_ns);
+      const int64_t s = k.period + lat.sqs_ns;
+      const int64_t t1 = now + k.period;
+      if (t1 < lim) {
+        int64_t j = (lim - 1 - t1) / s + 1;
+        if (j > kMaxPolls - res.polls) j = kMaxPolls - res.polls;
+        res.pod_ms += static_cast<int64_t>(replicas) * dt_ms * j;  // j left sums of dt_ms, one run
+        acc.run += d * dt_ms * j;
+        res.polls += static_cast<int32_t>(j);
+        prev_t += j * s;
+        now = prev_t + lat.sqs_ns;
+      }
+    }
   }
   if (horizon_ns > prev_t) accumulate_ms(&res, &acc, (horizon_ns - prev_t) / 1000000, replicas, prev_d);
   flush(&res, &acc);
@@ -393,6 +431,7 @@ KSA_HD void accumulate_ms32(Result* r, Accum* a, int32_t dt_ms, int32_t replicas
 }
 
 // simulate() on the millisecond clock: t_ms / depth as narrow_policy_trace makes them.
+template <bool kSkip = true>
 KSA_HD Result simulate_ms(const Params& p, const MsLatency& lat, const int32_t* t_ms, const int32_t* depth, int32_t n,
                           int32_t init_replicas, int64_t horizon_ns) {
   Result res;
@@ -426,6 +465,21 @@ KSA_HD Result simulate_ms(const Params& p, const MsLatency& lat, const int32_t* 
     (void)writes;
     if (replicas > res.max_replicas) res.max_replicas = replicas;
     prev_d = d;
+    if (kSkip && gets == 0) {  // a poll that called nothing: skip the stretch of polls just like it
+      const int32_t lim = steady_limit(k, d, last_up, last_down, lat.sqs_ns, cursor.next_t, horizon_ms);
+      const int32_t s = k.period + lat.sqs_ns;
+      const int32_t t1 = now + k.period;
+      if (t1 < lim) {
+        int32_t j = (lim - 1 - t1) / s + 1;
+        if (j > kMaxPolls - res.polls) j = kMaxPolls - res.polls;
+        const int64_t span = static_cast<int64_t>(j) * s;
+        res.pod_ms += static_cast<int64_t>(replicas) * span;  // j left sums of dt = s, one run
+        acc.run += static_cast<int64_t>(d) * span;
+        res.polls += j;
+        prev_t = static_cast<int32_t>(prev_t + span);
+        now = prev_t + lat.sqs_ns;
+      }
+    }
   }
   if (horizon_ms > prev_t) accumulate_ms32(&res, &acc, horizon_ms - prev_t, replicas, prev_d);
   flush(&res, &acc);
@@ -459,6 +513,28 @@ inline bool ms_path_ok(const int64_t* t_ns, const int64_t* depth, int32_t n, int
   for (int32_t i = 0; i < n; ++i)
     if (depth[i] < 0 || depth[i] > INT32_MAX - 1) return false;
   return ms_clock_ok(horizon_ns, latency, params, configs);
+}
+
+// Whether the steady-stretch skip (simulate<true>) pays for a sweep: only when a trace segment
+// spans `polls` polls or more -- a coarse trace (a sample a minute) under a poll of a few seconds.
+// On a trace sampled at every poll (--trace-file spans, or 5 s samples under a 5 s poll) no
+// stretch forms, and the check alone made the gfx950 kernel 19 % slower (profiles/r04v). Measured
+// on gfx950 (profiles/r04w): the millisecond clock gains from 4 polls a segment (6: 1.67x, 12:
+// 2.24x); the nanosecond clock, whose skip divides in 64 bits, from about 8 (6: 0.94x, 12: 1.38x).
+// The results do not depend on the choice: a skipped stretch adds exactly what its polls would.
+inline bool skip_pays(const int64_t* t_ns, int32_t n, int64_t horizon_ns, const int64_t* latency, const int64_t* params,
+                      int64_t configs, int64_t polls) {
+  int64_t within = 0;  // segments starting inside the horizon
+  while (within < n && t_ns[within] <= horizon_ns) ++within;
+  if (within < 1) within = 1;
+  const int64_t seg = horizon_ns / within;
+  int64_t step = INT64_MAX;  // the shortest poll-to-poll interval of the grid
+  for (int64_t i = 0; i < configs; ++i) {
+    const int64_t poll = params[i] > 0 ? params[i] : 0;
+    const int64_t st = poll < kMaxLatencyNs ? poll + latency[0] : kMaxLatencyNs;
+    if (st > 0 && st < step) step = st;
+  }
+  return step != INT64_MAX && step <= seg / polls;
 }
 
 // The trace as simulate_ms reads it: boundaries ceil(t / 1 ms) (kMsNever past 2^31 ms), depths.

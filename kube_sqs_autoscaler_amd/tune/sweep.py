@@ -150,6 +150,7 @@ class SweepResult:
     device: str
     kernel_ms: float = 0.0
     ms_clock: bool = False  # the native path ran policy_sim.h's simulate_ms (whole-ms periods and latencies)
+    skip: bool = False  # ... with the steady-stretch skip (policy_sim.h steady_limit; same results)
 
     def __len__(self) -> int:
         return self.params.shape[1]
@@ -165,13 +166,18 @@ class SweepResult:
 
 def run(trace: Trace, params: np.ndarray, init_replicas: int = 1, horizon_ns: int = 3600 * 10**9,
         latency_ns: Tuple[int, int, int] = (1_000_000, 1_000_000, 1_000_000), device: str = "auto",
-        threads: int = 0, gpu_index: int = 0, clock: str = "auto") -> SweepResult:
+        threads: int = 0, gpu_index: int = 0, clock: str = "auto", skip: str = "auto") -> SweepResult:
     """Runs the sweep. ``clock``: ``"auto"`` simulates on 32-bit millisecond clocks when every
     period that can fire and every latency is a whole number of milliseconds (policy_sim.h
     ``ms_path_ok``; identical results), else on 64-bit nanosecond clocks; ``"ns"`` always uses
-    the latter."""
+    the latter. ``skip``: adding up a stretch of polls that call nothing at once (policy_sim.h
+    ``steady_limit``; identical results) -- ``"auto"`` when a trace segment spans several polls
+    (``skip_pays``), ``"on"`` / ``"off"`` to force it."""
     if clock not in ("auto", "ns"):
         raise ValueError(f"clock must be auto or ns, not {clock!r}")
+    skip_mode = {"auto": 0, "on": 1, "off": 2}.get(skip)
+    if skip_mode is None:
+        raise ValueError(f"skip must be auto, on or off, not {skip!r}")
     params = np.ascontiguousarray(params, dtype=np.int64)
     if params.ndim != 2 or params.shape[0] != len(PARAM_FIELDS):
         raise ValueError("params must have shape (9, m); build it with grid()")
@@ -197,22 +203,23 @@ def run(trace: Trace, params: np.ndarray, init_replicas: int = 1, horizon_ns: in
         used = ctypes.c_int32(0)
         rc = lib.ksa_sweep_gpu(gpu_index, trace.t_ns.ctypes.data, trace.depth.ctypes.data, len(trace.t_ns), init_replicas,
                                horizon_ns, lat.ctypes.data, params.ctypes.data, m, out64.ctypes.data, out32.ctypes.data,
-                               ctypes.byref(ms), 1 if clock == "ns" else 0, ctypes.byref(used))
+                               ctypes.byref(ms), (1 if clock == "ns" else 0) | (skip_mode << 2), ctypes.byref(used))
         if rc != 0:
             raise RuntimeError("GPU sweep failed: " + (lib.ksa_sweep_last_error() or b"").decode())
         kernel_ms = ms.value
-        ms_clock = bool(used.value)
+        ms_clock, skipped = bool(used.value & 1), bool(used.value & 2)
     elif device == "cpu":
         from ..ops import native
 
-        out64, out32, ms_clock = native().sweep_cpu(trace.t_ns, trace.depth, init_replicas, horizon_ns, lat, params,
-                                                    threads or (os.cpu_count() or 8), clock == "ns")
+        out64, out32, ms_clock, skipped = native().sweep_cpu(trace.t_ns, trace.depth, init_replicas, horizon_ns, lat,
+                                                             params, threads or (os.cpu_count() or 8), clock == "ns",
+                                                             skip_mode)
         kernel_ms = 0.0
     else:
         raise ValueError(f"device must be auto, gpu or cpu, not {device!r}")
     out = {k: out64[i] for i, k in enumerate(OUT64)}
     out.update({k: out32[i] for i, k in enumerate(OUT32)})
-    return SweepResult(params, out, device, kernel_ms, ms_clock)
+    return SweepResult(params, out, device, kernel_ms, ms_clock, skipped)
 
 
 def pareto_front(pod_ms: np.ndarray, backlog: np.ndarray) -> np.ndarray:

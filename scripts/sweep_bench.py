@@ -29,19 +29,28 @@ m = grid.shape[1]
 horizon = 24 * 3600 * S
 lat = (2_000_000, 1_000_000, 1_000_000)
 results = {}
-# (device, clock): the GPU on both clocks (the auto run takes the millisecond one: whole-ms periods
-# and latencies), the CPU on the nanosecond clock (the exactness baseline)
-for device, clock in (("gpu", "auto"), ("gpu", "ns"), ("cpu", "ns")):
+by_skip = {}
+# (device, clock, skip): the GPU on both clocks (the auto run takes the millisecond one: whole-ms
+# periods and latencies), the CPU on the nanosecond clock (the exactness baseline). The
+# steady-stretch skip as sweep.run picks it ("auto"), or -- KSA_BENCH_SKIP_AB=1 -- every run with
+# it forced on and off (same results).
+skips = ("on", "off") if os.environ.get("KSA_BENCH_SKIP_AB") == "1" else ("auto",)
+runs = [(dev, clk, sk) for dev, clk in (("gpu", "auto"), ("gpu", "ns"), ("cpu", "ns")) for sk in skips]
+for device, clock, skip in runs:
     if device == "gpu" and not sweep.gpu_available():
         continue
     sub = grid if device == "gpu" else grid[:, : m // 20]  # CPU on a 5 % slice, scaled
-    sweep.run(tr, sub[:, :1024], 1, horizon, lat, device, clock=clock)  # warm-up
+    # warm-up: the GPU's device buffers and code object; the CPU path's first large run (page
+    # faults on fresh output arrays, thread start-up) ran up to 2x slower, so it warms at full size
+    sweep.run(tr, sub[:, :1024] if device == "gpu" else sub, 1, horizon, lat, device, clock=clock, skip=skip)
     t0 = time.perf_counter()
-    r = sweep.run(tr, sub, 1, horizon, lat, device, threads=16, clock=clock)
+    r = sweep.run(tr, sub, 1, horizon, lat, device, threads=min(16, os.cpu_count() or 8), clock=clock, skip=skip)
     wall = time.perf_counter() - t0
     polls = int(r.out["polls"].sum())
-    results[device + "_" + clock] = r
-    print(json.dumps({"device": device, "clock": "ms" if r.ms_clock else "ns", "configs": sub.shape[1],
+    results.setdefault(device + "_" + clock, r)
+    by_skip[(device, clock, skip)] = r
+    print(json.dumps({"device": device, "clock": "ms" if r.ms_clock else "ns", "skip": r.skip, "segment_s": seg_s,
+                      "configs": sub.shape[1],
                       "simulated_polls": polls, "wall_s": round(wall, 4),
                       "kernel_ms": round(r.kernel_ms, 3), "polls_per_s": round(polls / wall, 1),
                       "best_pod_ms_within_backlog_p50": int(np.min(r.out["pod_ms"][r.out["backlog"] <= np.median(r.out["backlog"])]))}),
@@ -56,3 +65,7 @@ if "gpu_auto" in results:
     a, b = results["gpu_auto"], results["gpu_ns"]
     print(json.dumps({"gpu_ms_clock_equals_gpu_ns_clock": all(np.array_equal(a.out[key], b.out[key]) for key in a.out)}),
           flush=True)
+if len(skips) == 2:  # each run without the skip against the same run with it
+    same = all(np.array_equal(r.out[key], by_skip[(d, c, "off")].out[key])
+               for (d, c, sk), r in by_skip.items() if sk == "on" for key in r.out)
+    print(json.dumps({"skip_off_equals_skip_on": same}), flush=True)

@@ -160,14 +160,18 @@ def test_sweep_kernel_equals_cpu_and_oracle():
     for n in (1000, 3000, 6000):
         tr = _random_walk_trace(n, n)
         horizon = int(tr.t_ns[-1]) + 5 * S
-        g = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="gpu")
-        gn = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="gpu", clock="ns")
-        c = sweep.run(tr, grid, 2, horizon, (2_000_000, 1_000_000, 1_000_000), device="cpu", clock="ns")
-        assert g.device == "gpu" and g.kernel_ms > 0
-        assert g.ms_clock and not gn.ms_clock and not c.ms_clock
-        for k in g.out:
-            assert np.array_equal(g.out[k], c.out[k]), k
-            assert np.array_equal(gn.out[k], c.out[k]), k
+        lat = (2_000_000, 1_000_000, 1_000_000)
+        c = sweep.run(tr, grid, 2, horizon, lat, device="cpu", clock="ns", skip="off")
+        g = sweep.run(tr, grid, 2, horizon, lat, device="gpu")
+        assert g.device == "gpu" and g.kernel_ms > 0 and g.ms_clock and g.skip and not c.ms_clock
+        # every kernel instantiation: both clocks, with and without the steady-stretch skip
+        for clock in ("auto", "ns"):
+            for skip in ("on", "off"):
+                gk = g if (clock, skip) == ("auto", "on") else sweep.run(tr, grid, 2, horizon, lat, device="gpu",
+                                                                          clock=clock, skip=skip)
+                assert gk.ms_clock == (clock == "auto") and gk.skip == (skip == "on")
+                for k in g.out:
+                    assert np.array_equal(gk.out[k], c.out[k]), (k, clock, skip)
         assert int(g.out["ups"].sum()) > 0 and int(g.out["downs"].sum()) > 0
         for i in range(0, len(g), len(g) // 7):
             o = sweep.oracle_row(tr, g.config(i), 2, horizon, (2_000_000, 1_000_000, 1_000_000))

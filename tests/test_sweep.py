@@ -59,9 +59,11 @@ def test_cpu_equals_oracle_property(segs, d0, poll, up_cool, down_cool, up_msgs,
     cfg = dict(poll_ns=[poll], up_cool_ns=[up_cool], down_cool_ns=[down_cool], up_msgs=[up_msgs],
                down_msgs=[down_msgs], up_pods=[up_pods], down_pods=[down_pods], max_pods=[max_pods], min_pods=[min_pods])
     lat = (lat_ms * 10**6,) * 3
-    res = sweep.run(tr, sweep.grid(**cfg), init, horizon_s * S, lat, device="cpu")
-    o = sweep.oracle_row(tr, res.config(0), init, horizon_s * S, lat)
-    assert {k: res.row(0)[k] for k in o} == o
+    o = None
+    for skip in ("on", "off"):  # the steady-stretch skip adds a stretch at once: same results
+        res = sweep.run(tr, sweep.grid(**cfg), init, horizon_s * S, lat, device="cpu", skip=skip)
+        o = o or sweep.oracle_row(tr, res.config(0), init, horizon_s * S, lat)
+        assert {k: res.row(0)[k] for k in o} == o, skip
 
 
 def test_work_budget_guard():
@@ -134,11 +136,14 @@ def test_extreme_cool_downs_and_periods_do_not_overflow(nat):
 
 
 def _both_clocks(tr, grid, init, horizon, lat):
-    a = sweep.run(tr, grid, init, horizon, lat, device="cpu", clock="auto")
-    b = sweep.run(tr, grid, init, horizon, lat, device="cpu", clock="ns")
-    assert not b.ms_clock
-    for k in a.out:
-        assert np.array_equal(a.out[k], b.out[k]), k
+    """Both clocks, each with and without the steady-stretch skip: the same results."""
+    a = sweep.run(tr, grid, init, horizon, lat, device="cpu", clock="auto", skip="on")
+    assert a.skip
+    for clock, skip in (("ns", "on"), ("auto", "off"), ("ns", "off")):
+        b = sweep.run(tr, grid, init, horizon, lat, device="cpu", clock=clock, skip=skip)
+        assert b.ms_clock == (clock == "auto" and a.ms_clock) and b.skip == (skip == "on")
+        for k in a.out:
+            assert np.array_equal(a.out[k], b.out[k]), (k, clock, skip)
     return a
 
 
@@ -207,3 +212,27 @@ def test_ms_clock_boundaries_exactly_at_cool_down_expiry():
                    down_cool_ns=[2 * S - 1, 2 * S, 2 * S + 1], up_msgs=[100], down_msgs=[10])
     for lat in ((0, 0, 0), (10**6, 10**6, 10**6), (0, 2 * 10**6, 0)):
         assert _both_clocks(tr, g, 1, 60 * S, lat).ms_clock
+
+
+def test_steady_stretch_skip_is_chosen_for_coarse_traces():
+    """skip="auto" (policy_sim.h skip_pays): on when a trace segment spans four or more of the
+    grid's shortest poll intervals on the millisecond clock (eight on the nanosecond one), off for
+    a trace sampled at every poll (the GPU kernel is slower with the check where no stretch
+    forms). Either way the results are the same, and the skip leaves the simulated poll count as
+    it is."""
+    rng = np.random.default_rng(3)
+    coarse = sweep.Trace(np.arange(0, 3600 * S, 60 * S), rng.integers(0, 400, 60))
+    fine = sweep.Trace(np.arange(0, 3600 * S, 5 * S), rng.integers(0, 400, 720))
+    g = sweep.grid(poll_ns=[5 * S, 10 * S], up_cool_ns=[0, 60 * S, 300 * S], down_cool_ns=[0, 120 * S],
+                   up_msgs=[100, 300], down_msgs=[10, 50])
+    lat = (2 * 10**6, 10**6, 10**6)
+    assert sweep.run(coarse, g, 1, 3600 * S, lat, device="cpu").skip  # 12 polls a segment
+    assert not sweep.run(fine, g, 1, 3600 * S, lat, device="cpu").skip  # 1
+    half = sweep.Trace(np.arange(0, 3600 * S, 30 * S), rng.integers(0, 400, 120))  # 6
+    assert sweep.run(half, g, 1, 3600 * S, lat, device="cpu").skip
+    assert not sweep.run(half, g, 1, 3600 * S, lat, device="cpu", clock="ns").skip
+    for tr in (coarse, fine):
+        r = _both_clocks(tr, g, 1, 3600 * S, lat)
+        assert r.out["polls"].min() > 300  # every lane still counts every poll
+    with pytest.raises(ValueError, match="skip"):
+        sweep.run(coarse, g, 1, 3600 * S, lat, device="cpu", skip="maybe")
