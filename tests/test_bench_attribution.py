@@ -85,17 +85,19 @@ def test_spin_window_decision(nat, busy_poll, ewma, budget, window):
 def test_cadenced_worker_spins_through_a_slow_answer_within_its_budget(nat, period_ms, spins):
     """End to end: a worker on its own thread may busy-poll through an answer that takes longer
     than the --busy-poll window when twice the response-time EWMA fits in the SQS call's three
-    quarters of 1 % of the poll period (1 s -> 7.5 ms; the fakes answer after 0.4 ms plus their timer slack),
-    so the poll is not woken from an idle sleep by its answer. The spin lasts 2 x EWMA: an answer
-    a busy host delays past that is waited for in poll(2), so how many polls spin depends on the
-    load -- this runs serially (conftest: ``serial`` tests are skipped under xdist workers) and
-    asks only that spinning happens. Back to back (no period, no budget) a peer that slow is
-    always waited for in poll(2)."""
+    quarters of the spin budget, so the poll is not woken from an idle sleep by its answer. The
+    fakes answer after 0.4 ms plus their timer slack; on an idle VM that slack has reached 4 ms
+    (timers woken late out of deep idle), past the CLI's 1 % budget at 1 s (7.5 ms for 2 x EWMA),
+    so this gives the worker 10 % of the period (75 ms): the decision under test is the same.
+    The spin lasts 2 x EWMA: an answer a busy host delays past that is waited for in poll(2), so
+    how many polls spin depends on the load -- this runs serially (conftest: ``serial`` tests are
+    skipped under xdist workers) and asks only that spinning happens. Back to back (no period,
+    no budget) a peer that slow is always waited for in poll(2)."""
     import json
     import tempfile
 
     env = BenchEnv(1, busy_poll_ns=25_000, poll_period_ns=period_ms * 1_000_000, timing=True,
-                   sqs_latency_ns=400_000, kube_latency_ns=400_000)
+                   sqs_latency_ns=400_000, kube_latency_ns=400_000, spin_budget_ppm=100_000)
     f = tempfile.TemporaryFile()
     try:
         env.runners[0].set_trace_fd(f.fileno())
