@@ -18,7 +18,7 @@ int sweep_cpu(const int64_t* trace_t, const int64_t* trace_d, int32_t n, int32_t
   const ksa_sim::Latency lat{latency[0], latency[1], latency[2]};
   const bool ms = (arith & 3) == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
   const int skip_mode = (arith >> 2) & 3;
-  const bool skip = skip_mode == 1 || (skip_mode == 0 && ksa_sim::skip_pays(trace_t, n, horizon_ns, latency, params, m, ms ? 4 : 8));
+  const bool skip = skip_mode == 1 || (skip_mode == 0 && ksa_sim::skip_pays(trace_t, n, horizon_ns, latency, params, m, ms ? 4 : 5));
   const int used = (ms ? 1 : 0) | (skip ? 2 : 0);
   std::vector<int32_t> t32(ms ? n : 0), d32(ms ? n : 0);
   if (ms) ksa_sim::narrow_policy_trace(trace_t, trace_d, n, t32.data(), d32.data());

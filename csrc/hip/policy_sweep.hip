@@ -172,7 +172,7 @@ int ksa_sweep_gpu(int dev, const int64_t* trace_t, const int64_t* trace_d, int32
   if (m <= 0) return 0;
   const bool ms = (arith & 3) == 0 && ksa_sim::ms_path_ok(trace_t, trace_d, n, horizon_ns, latency, params, m);
   const int skip_mode = (arith >> 2) & 3;
-  const bool skip = skip_mode == 1 || (skip_mode == 0 && ksa_sim::skip_pays(trace_t, n, horizon_ns, latency, params, m, ms ? 4 : 8));
+  const bool skip = skip_mode == 1 || (skip_mode == 0 && ksa_sim::skip_pays(trace_t, n, horizon_ns, latency, params, m, ms ? 4 : 5));
   if (ms_used) *ms_used = (ms ? 1 : 0) | (skip ? 2 : 0);
   // the trace in the chosen path's element type
   std::vector<int32_t> t32, d32;

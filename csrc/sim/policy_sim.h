@@ -263,6 +263,22 @@ KSA_HD T steady_limit(const K& k, T d, T last_up, T last_down, T sqs, T next_t, 
   return lim;
 }
 
+// floor(x / s) capped at `cap`, for 0 <= x < 2^60, 1 <= s <= 2^62 and cap <= 2^26 (the skip's
+// poll count on the nanosecond clock): a double-precision estimate, then one exact integer step
+// either way, instead of the GPU's long 64-bit division sequence. Below the cap the quotient is
+// under 2^27, where the estimate's relative error (a few 2^-53) is far below one, so it is off by
+// at most one only when x / s is within that error of an integer; the products stay below 2^63.
+KSA_HD int64_t capped_quotient(int64_t x, int64_t s, int64_t cap) {
+  const double e = static_cast<double>(x) / static_cast<double>(s);
+  if (e >= static_cast<double>(cap) + 2.0) return cap;
+  int64_t q = static_cast<int64_t>(e);
+  if (q * s > x)
+    --q;
+  else if ((q + 1) * s <= x)
+    ++q;
+  return q < cap ? q : cap;
+}
+
 template <bool kSkip = true>
 KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns, const int64_t* depth, int32_t n,
                        int32_t init_replicas, int64_t horizon_ns) {
@@ -302,8 +318,7 @@ KSA_HD Result simulate(const Params& p, const Latency& lat, const int64_t* t_ns,
       const int64_t s = k.period + lat.sqs_ns;
       const int64_t t1 = now + k.period;
       if (t1 < lim) {
-        int64_t j = (lim - 1 - t1) / s + 1;
-        if (j > kMaxPolls - res.polls) j = kMaxPolls - res.polls;
+        const int64_t j = capped_quotient(lim - 1 - t1, s, kMaxPolls - res.polls - 1) + 1;
         res.pod_ms += static_cast<int64_t>(replicas) * dt_ms * j;  // j left sums of dt_ms, one run
         acc.run += d * dt_ms * j;
         res.polls += static_cast<int32_t>(j);
@@ -519,8 +534,9 @@ inline bool ms_path_ok(const int64_t* t_ns, const int64_t* depth, int32_t n, int
 // spans `polls` polls or more -- a coarse trace (a sample a minute) under a poll of a few seconds.
 // On a trace sampled at every poll (--trace-file spans, or 5 s samples under a 5 s poll) no
 // stretch forms, and the check alone made the gfx950 kernel 19 % slower (profiles/r04v). Measured
-// on gfx950 (profiles/r04w): the millisecond clock gains from 4 polls a segment (6: 1.67x, 12:
-// 2.24x); the nanosecond clock, whose skip divides in 64 bits, from about 8 (6: 0.94x, 12: 1.38x).
+// on gfx950 (profiles/r04aa): the millisecond clock gains from 3-4 polls a segment (3: 1.07x, 6:
+// 1.65x, 12: 2.21x); the nanosecond clock, whose skip count takes a capped_quotient, from 5-6
+// (3: 0.79x, 6: 1.19x, 12: 1.71x).
 // The results do not depend on the choice: a skipped stretch adds exactly what its polls would.
 inline bool skip_pays(const int64_t* t_ns, int32_t n, int64_t horizon_ns, const int64_t* latency, const int64_t* params,
                       int64_t configs, int64_t polls) {

@@ -216,7 +216,7 @@ def test_ms_clock_boundaries_exactly_at_cool_down_expiry():
 
 def test_steady_stretch_skip_is_chosen_for_coarse_traces():
     """skip="auto" (policy_sim.h skip_pays): on when a trace segment spans four or more of the
-    grid's shortest poll intervals on the millisecond clock (eight on the nanosecond one), off for
+    grid's shortest poll intervals on the millisecond clock (five on the nanosecond one), off for
     a trace sampled at every poll (the GPU kernel is slower with the check where no stretch
     forms). Either way the results are the same, and the skip leaves the simulated poll count as
     it is."""
@@ -228,7 +228,7 @@ def test_steady_stretch_skip_is_chosen_for_coarse_traces():
     lat = (2 * 10**6, 10**6, 10**6)
     assert sweep.run(coarse, g, 1, 3600 * S, lat, device="cpu").skip  # 12 polls a segment
     assert not sweep.run(fine, g, 1, 3600 * S, lat, device="cpu").skip  # 1
-    half = sweep.Trace(np.arange(0, 3600 * S, 30 * S), rng.integers(0, 400, 120))  # 6
+    half = sweep.Trace(np.arange(0, 3600 * S, 25 * S), rng.integers(0, 400, 144))  # 5 - latency
     assert sweep.run(half, g, 1, 3600 * S, lat, device="cpu").skip
     assert not sweep.run(half, g, 1, 3600 * S, lat, device="cpu", clock="ns").skip
     for tr in (coarse, fine):
