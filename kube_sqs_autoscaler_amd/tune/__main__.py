@@ -155,7 +155,8 @@ def _open_loop(ap: argparse.ArgumentParser, a, group) -> int:
     summary = {"configs": len(res), "feasible": int(ok.sum()), "device": res.device, "wall_s": round(wall, 4),
                "ranks": group.world if group is not None else 1,
                "kernel_ms": round(res.kernel_ms, 3), "simulated_polls": int(res.out["polls"].sum()),
-               "clock": "ms" if res.ms_clock else "ns", "horizon_ns": horizon, "reference_defaults": baseline}
+               "clock": "ms" if res.ms_clock else "ns", "steady_skip": res.skip, "horizon_ns": horizon,
+               "reference_defaults": baseline}
     if a.json:
         print(json.dumps(summary))
         for i in order:

@@ -165,13 +165,15 @@ def run_open_loop(g: Group, trace: sweep.Trace, params: np.ndarray, init_replica
     if len(mine):
         res = sweep.run(trace, np.ascontiguousarray(params[:, mine]), init_replicas, horizon_ns, latency_ns, g.device,
                         gpu_index=g.local_rank)
-        out, kernel_ms, ns_clock = res.out, res.kernel_ms, not res.ms_clock
+        out, kernel_ms, ns_clock, no_skip = res.out, res.kernel_ms, not res.ms_clock, not res.skip
     else:  # more ranks than configurations
         out = {k: np.zeros(0, dtype=np.int64 if k in sweep.OUT64 else np.int32) for k in sweep.OUT64 + sweep.OUT32}
-        kernel_ms, ns_clock = 0.0, False
+        kernel_ms, ns_clock, no_skip = 0.0, False, False
     full = _to_grid_order(g.all_gather_fields(out, counts), order)
-    # ms_clock: every shard ran the millisecond clock
-    return sweep.SweepResult(params, full, g.device, g.max(kernel_ms), g.max(float(ns_clock)) == 0.0)
+    # ms_clock / skip: every shard ran the millisecond clock / the steady-stretch skip (each shard
+    # picks the skip for its own configurations; the results do not depend on it)
+    return sweep.SweepResult(params, full, g.device, g.max(kernel_ms), g.max(float(ns_clock)) == 0.0,
+                             g.max(float(no_skip)) == 0.0)
 
 
 def run_closed_loop(g: Group, trace: closedloop.ArrivalTrace, params: np.ndarray, model: closedloop.QueueModel,

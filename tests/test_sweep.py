@@ -101,6 +101,7 @@ def test_tune_cli(tmp_path, capsys):
     assert rc == 0
     lines = [json.loads(l) for l in capsys.readouterr().out.splitlines()]
     assert lines[0]["configs"] == 7 * 3 * 2 and lines[0]["reference_defaults"]["ups"] > 0
+    assert lines[0]["steady_skip"] is True  # 5 segments over 900 s: 180 s each under the 5 s poll
     pods = [l["pod_ms"] for l in lines[1:]]
     assert len(pods) == 3 and pods == sorted(pods)
 
