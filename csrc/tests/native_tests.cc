@@ -40,6 +40,7 @@
 #include "../core/sigv4.h"
 #include "../core/sqs.h"
 #include "../core/xml.h"
+#include "../sim/policy_sim.h"
 
 using namespace ksa;
 
@@ -1022,6 +1023,37 @@ TEST(exec_provider_shared_across_threads) {
 // The worker-process error slot (SharedWorkerState, seqlock over relaxed atomic words): a reader
 // racing the writer gets one of the texts written, whole, or "" -- never a mix (TSan-clean: every
 // shared access is atomic).
+// policy_sim.h capped_quotient (the nanosecond clock's skip count): equal to exact integer
+// division capped at `cap` over its whole domain (0 <= x < 2^60, 1 <= s <= 2^62, cap <= 2^26),
+// at quotients exactly on, one below and one above an integer, and under UBSan for overflow.
+TEST(capped_quotient_exact) {
+  auto want = [](int64_t x, int64_t s, int64_t cap) { return std::min(x / s, cap); };
+  const int64_t caps[] = {-1, 0, 1, 7, (1 << 26) - 1, 1 << 26};
+  const int64_t ss[] = {1, 2, 3, 999'999, 1'000'000, 5'002'000'000LL, (1LL << 40) + 1, 1LL << 61, 1LL << 62};
+  uint64_t r = 0x9e3779b97f4a7c15ULL;
+  int checked = 0;
+  for (int64_t cap : caps)
+    for (int64_t s : ss) {
+      for (int64_t q : {int64_t(0), int64_t(1), cap - 1, cap, cap + 1, int64_t(1) << 25, (int64_t(1) << 26) + 5}) {
+        if (q < 0) continue;
+        for (int64_t d : {int64_t(-1), int64_t(0), int64_t(1), s - 1}) {  // x around q * s
+          if (q > 0 && s > ((int64_t(1) << 60) - 1) / q) continue;
+          const int64_t x = q * s + d;
+          if (x < 0 || x >= (int64_t(1) << 60)) continue;
+          CHECK(ksa_sim::capped_quotient(x, s, cap) == want(x, s, cap));
+          ++checked;
+        }
+      }
+      for (int k = 0; k < 2000; ++k) {  // random x over the domain
+        r = r * 6364136223846793005ULL + 1442695040888963407ULL;
+        const int64_t x = static_cast<int64_t>(r >> 4) >> (r % 40);
+        CHECK(ksa_sim::capped_quotient(x, s, cap) == want(x, s, cap));
+        ++checked;
+      }
+    }
+  CHECK(checked > 100000);
+}
+
 TEST(shared_error_slot_seqlock) {
   alignas(64) static unsigned char mem[sizeof(SharedWorkerState)];
   SharedWorkerState* s = init_shared_worker_state(mem);
