@@ -295,7 +295,8 @@ def test_bench_pools_samples_over_rccl():
 def test_sweep_kernel_random_lanes_equal_oracle():
     """the gfx950 open-loop kernel against the independent Python oracle on 256 lanes
     per dispatch (adversarial + random configurations), with the trace in LDS and in global
-    memory, plus GPU == CPU on every lane of the dispatch."""
+    memory, plus GPU == CPU on every lane of the dispatch, in every kernel instantiation (both
+    clocks, with and without the steady-stretch skip)."""
     import sys
     import os
 
@@ -310,13 +311,15 @@ def test_sweep_kernel_random_lanes_equal_oracle():
     for n, seed in ((400, 1), (2600, 2)):
         tr = random_walk_trace(n, seed)
         horizon = min(int(tr.t_ns[-1]) + 10 * S, 1800 * S)
-        g = sweep.run(tr, params, 2, horizon, lat, device="gpu")
-        gn = sweep.run(tr, params, 2, horizon, lat, device="gpu", clock="ns")
-        c = sweep.run(tr, params, 2, horizon, lat, device="cpu", clock="ns")
-        assert g.device == "gpu" and g.ms_clock and not gn.ms_clock
-        for k in g.out:
-            assert np.array_equal(g.out[k], c.out[k]), k
-            assert np.array_equal(gn.out[k], c.out[k]), k
+        c = sweep.run(tr, params, 2, horizon, lat, device="cpu", clock="ns", skip="off")
+        # both clocks, each with the steady-stretch skip forced on and off
+        runs = {(clock, skip): sweep.run(tr, params, 2, horizon, lat, device="gpu", clock=clock, skip=skip)
+                for clock in ("auto", "ns") for skip in ("on", "off")}
+        for (clock, skip), g in runs.items():
+            assert g.device == "gpu" and g.ms_clock == (clock == "auto") and g.skip == (skip == "on")
+            for k in g.out:
+                assert np.array_equal(g.out[k], c.out[k]), (k, clock, skip)
+        g = runs[("auto", "on")]
         for i in lanes_to_check(params.shape[1], 256, seed):
             o = sweep.oracle_row(tr, g.config(i), 2, horizon, lat)
             assert {k: g.row(i)[k] for k in o} == o, (i, g.config(i))
