@@ -251,8 +251,13 @@ def test_sharded_sweep_cli_on_gpu(tmp_path):
             "--slo-backlog", "100", "--grid", "scale-up-cool-down=0s,1m", "--grid", "max-pods=4,8,16", "--latency",
             "1ms,1ms,1ms", "--grid", "poll-period=2s,5s"]  # mixed periods: the cost-sorted shard is scattered back
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import socket
+
+    with socket.socket() as sk:  # a free port, not a fixed one another job on the box may hold
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-                        "--master-addr=127.0.0.1", "--master-port=29517", "-m", "kube_sqs_autoscaler_amd.tune",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "kube_sqs_autoscaler_amd.tune",
                         "--distributed", "--device", "gpu", *args], cwd=root, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -285,7 +290,12 @@ def test_bench_pools_samples_over_rccl():
         "empty, _ = bench._pool([], 0.25, dev, collective=True)\n"
         "print(json.dumps({'backend': dist.get_backend(), 'ns': ns, 'wall': wall, 'empty': empty}))\n"
         "dist.destroy_process_group()\n")
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29519", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import socket
+
+    with socket.socket() as sk:  # a free port, not a fixed one another job on the box may hold
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
