@@ -152,6 +152,7 @@ py::dict record_dict(const IterationRecord& r) {
   d["update_ns"] = r.update_ns;
   d["total_ns"] = r.total_ns;
   d["patch_latency_ns"] = r.patch_latency_ns;
+  d["cpu_ns"] = r.cpu_ns;
   d["error"] = r.error;
   return d;
 }
@@ -767,6 +768,7 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["last_replicas"] = s.last_replicas;
         d["latency_samples"] = s.latency_samples;
         d["latency_sum_ns"] = s.latency_sum_ns;
+        d["poll_cpu_ns"] = s.poll_cpu_ns;
         d["latency_buckets"] = std::vector<uint64_t>(s.latency_buckets, s.latency_buckets + kLatBuckets);
         d["consecutive_failed_polls"] = s.consecutive_failed_polls;
         return d;
@@ -798,7 +800,7 @@ PYBIND11_MODULE(_ksa_native, m) {
     static const char* names[] = {"polls", "depth_errors", "scale_ups", "scale_downs", "noop_ups", "noop_downs",
                                   "cooldown_skips_up", "cooldown_skips_down", "failed_ups", "failed_downs",
                                   "speculative_reads", "speculative_reads_used", "speculative_reads_gated",
-                                  "apiserver_reads", "latency_samples", "consecutive_failed_polls"};
+                                  "apiserver_reads", "latency_samples", "consecutive_failed_polls", "poll_cpu_ns"};
     static_assert(sizeof(names) / sizeof(names[0]) == SharedWorkerState::kNumCounters, "counter names");
     py::dict d;
     for (int i = 0; i < SharedWorkerState::kNumCounters; ++i)
@@ -939,7 +941,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         py::arg("model"), py::arg("params"), py::arg("seeds"), py::arg("seed0") = 1, py::arg("threads") = 8,
         py::arg("arith") = 0);
 
-  m.attr("HTTP_TIMING") = kHttpTiming;  // false in the image build (-DKSA_HTTP_TIMING=0)
+  m.attr("HTTP_TIMING") = kHttpTiming;
+  m.attr("HTTP_MAX_SPIN_THROUGH_NS") = HttpClient::kMaxSpinThrough;  // false in the image build (-DKSA_HTTP_TIMING=0)
   m.attr("SECOND") = kSecond;
   m.attr("MILLISECOND") = kMillisecond;
   m.attr("MICROSECOND") = kMicrosecond;

@@ -39,6 +39,13 @@ inline int64_t mono_ns() {
       .count();
 }
 
+// CPU time of the calling thread (CLOCK_THREAD_CPUTIME_ID), nanoseconds.
+inline int64_t thread_cpu_ns() {
+  struct timespec ts;
+  if (clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts) != 0) return 0;
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
 constexpr Nanos kMicrosecond = 1000;
 constexpr Nanos kMillisecond = 1000 * kMicrosecond;
 constexpr Nanos kSecond = 1000 * kMillisecond;

@@ -819,10 +819,13 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
 Nanos HttpClient::spin_window_for(Nanos busy_poll, Nanos ewma, Nanos budget) {
   if (busy_poll <= 0) return 0;
   if (ewma < 0) return busy_poll;  // no sample yet: try
-  if (ewma <= 4 * busy_poll) return busy_poll;
-  // a slower peer: spin through its expected response time when the budget allows
-  const Nanos through = 2 * ewma;
-  return through <= budget ? through : 0;
+  const Nanos window = ewma <= 4 * busy_poll ? busy_poll : 0;
+  // A peer answering within the absolute ceiling may be spun through (twice its EWMA, at most
+  // the ceiling) when the budget allows; a slower one -- any remote endpoint -- never beyond
+  // the window, whatever the budget: its answer is a network round trip away.
+  if (ewma > kMaxSpinThrough) return window;
+  const Nanos through = std::min(2 * ewma, kMaxSpinThrough);
+  return through > window && through <= budget ? through : window;
 }
 
 Nanos HttpClient::spin_window() const {

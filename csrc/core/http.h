@@ -184,16 +184,24 @@ class alignas(kCacheLine) HttpClient {
   void set_timeout(Nanos t) { timeout_ = t; }
   // Adaptive busy-poll: while the peer's response-time EWMA is within 4x `ns`, a read spins for
   // up to `ns` before blocking in poll(2) (saves the scheduler wake-up on fast local peers); for
-  // slower peers (real AWS / apiserver RTTs of milliseconds) it never spins. 0 disables.
+  // slower peers it does not spin, and a peer slower than kMaxSpinThrough (real AWS / apiserver
+  // RTTs of milliseconds) is never spun for, whatever the budget. 0 disables.
   void set_busy_poll(Nanos ns) { spin_ns_ = ns; }
-  // With busy-poll on, a read may also spin through a slower peer's expected response time
-  // (twice the EWMA) when that fits in `ns` per request -- the Runner sets its share of the poll
-  // period on a worker's own thread (LoopConfig::spin_budget_ppm), so a cadenced poll is not woken
-  // from an idle sleep on its answer, at a bounded CPU cost. 0 (default): never beyond the window.
+  // With busy-poll on, a read may also spin through a near peer's expected response time (twice
+  // the EWMA, at most kMaxSpinThrough) when that fits in `ns` per request -- the Runner sets its
+  // share of the poll period on a worker's own thread (LoopConfig::spin_budget_ppm, capped by the
+  // cgroup CPU quota), so a cadenced poll of a near endpoint is not woken from an idle sleep on
+  // its answer. 0 (default): never beyond the window.
   void set_spin_budget(Nanos ns) { spin_budget_ns_ = ns; }
   Nanos rtt_ewma() const;
+  // The absolute ceiling of one read's spin. A peer whose EWMA is above it is a network round
+  // trip away: spinning would burn CPU for the whole RTT (under a 100m CPU limit -- the
+  // reference's manifest, README.md:60-66 -- 10 ms per 100 ms CFS period, a few such spins
+  // exhaust the quota and the throttled thread then answers late).
+  static constexpr Nanos kMaxSpinThrough = 200 * kMicrosecond;
   // The read spin of the next response: `busy_poll` (the window) while the EWMA is unknown or
-  // within 4x the window; else twice the EWMA when that fits in `budget`; else 0 (block at once).
+  // within 4x the window, else 0; raised to twice the EWMA when the EWMA is within
+  // kMaxSpinThrough and that spin (capped at kMaxSpinThrough) fits in `budget`.
   static Nanos spin_window_for(Nanos busy_poll, Nanos ewma, Nanos budget);
   // Forward proxy (Go's http.ProxyFromEnvironment; the proxy is chosen by the caller), the
   // three kinds Go's transport speaks:

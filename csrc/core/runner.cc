@@ -81,6 +81,7 @@ bool Runner::action_likely(Nanos t0) const {
 }
 
 IterationRecord Runner::step(StopFlag* stop) {
+  cpu_from_ = thread_cpu_ns();
   // main.go:41 -- sleep BEFORE the poll.
   const Nanos period = cfg_.poll_period, w = cfg_.prewarm;
   bool slept;
@@ -114,6 +115,7 @@ void Runner::warm(Nanos due, bool presend) {
 }
 
 IterationRecord Runner::poll_once() {
+  if (cpu_from_ < 0) cpu_from_ = thread_cpu_ns();  // pooled: the poll alone
   LogBatch batch;  // the poll's log lines go out together once it is done (log.h)
   return poll_body();
 }
@@ -260,13 +262,18 @@ IterationRecord Runner::poll_body() {
   return finish();
 }
 
-void Runner::record(const IterationRecord& r) {
+void Runner::record(IterationRecord& r) {
+  if (cpu_from_ >= 0) {
+    r.cpu_ns = thread_cpu_ns() - cpu_from_;
+    cpu_from_ = -1;
+  }
   const Nanos now = clock_->now();
   progress_ns_.store(now, std::memory_order_release);
   const bool good = r.depth_ok && r.up != Action::Failed && r.down != Action::Failed;
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.polls++;
+    if (r.cpu_ns > 0) stats_.poll_cpu_ns += r.cpu_ns;
     if (good) {
       stats_.consecutive_failed_polls = 0;
       stats_.last_good_ns = now;
@@ -390,6 +397,7 @@ void Runner::mirror(const IterationRecord& r) {
   put(W::kSpeculativeReadsGated, st.speculative_reads_gated);
   put(W::kApiserverReads, st.apiserver_reads);
   put(W::kConsecutiveFailedPolls, st.consecutive_failed_polls);
+  put(W::kPollCpuNs, static_cast<uint64_t>(st.poll_cpu_ns));
   shared_->last_good_ns.store(st.last_good_ns, std::memory_order_relaxed);
   shared_->last_depth.store(st.last_depth, std::memory_order_relaxed);
   shared_->last_replicas.store(st.last_replicas, std::memory_order_relaxed);
@@ -417,7 +425,8 @@ std::string iteration_json(const IterationRecord& r, int64_t unix_ns, const std:
                   ",\"gets\":" + std::to_string(r.gets) +
                   ",\"depth_ns\":" + std::to_string(r.depth_ns) + ",\"get_ns\":" + std::to_string(r.get_ns) +
                   ",\"update_ns\":" + std::to_string(r.update_ns) + ",\"total_ns\":" + std::to_string(r.total_ns) +
-                  ",\"patch_latency_ns\":" + std::to_string(r.patch_latency_ns);
+                  ",\"patch_latency_ns\":" + std::to_string(r.patch_latency_ns) +
+                  ",\"cpu_ns\":" + std::to_string(r.cpu_ns);
   if (!r.error.empty()) j += ",\"error\":" + json_quote(r.error);
   if (!r.detail.empty()) j += ",\"detail\":" + r.detail;
   j += "}";
@@ -432,10 +441,21 @@ void Runner::write_trace(const IterationRecord& r) {
   (void)n;
 }
 
+Nanos Runner::spin_budget_for(const LoopConfig& cfg, const CpuQuota& quota) {
+  const int64_t ppm = std::clamp<int64_t>(cfg.spin_budget_ppm, 0, 1000000);
+  Nanos b = std::max<Nanos>(cfg.poll_period, 0) / 1000000 * ppm;
+  // Under a CFS limit a poll spins at most a tenth of the quota of one CFS period (this queue's
+  // share of it: the CLI's 1 % split over the queues): 1 ms per poll under a 100m limit.
+  if (quota.limited()) b = std::min<Nanos>(b, quota.quota_ns / 10 * std::min<int64_t>(ppm, 10000) / 10000);
+  return b;
+}
+
 void Runner::run(StopFlag* stop, int64_t max_iterations, Nanos start_delay) {
-  // This thread is the worker's own: its clients may spin through an answer within a share of
-  // the poll period (LoopConfig::spin_budget_ppm; a back-to-back loop keeps the window).
-  set_spin_budget(std::max<Nanos>(cfg_.poll_period, 0) / 1000000 * std::clamp<int64_t>(cfg_.spin_budget_ppm, 0, 1000000));
+  // This thread is the worker's own: its clients may spin through a near endpoint's answer
+  // within a share of the poll period (LoopConfig::spin_budget_ppm; a back-to-back loop keeps
+  // the window), capped by the process's CPU limit.
+  static const CpuQuota quota = read_cpu_quota();  // once per process
+  set_spin_budget(spin_budget_for(cfg_, quota));
   if (start_delay > 0 && !clock_->sleep(start_delay, stop)) return;
   if (cfg_.connect_at_start) {
     sqs_->warm(clock_->unix_nanos());

@@ -76,7 +76,9 @@ struct LoopConfig {
   // (parts per million; Runner::set_spin_budget splits it over the poll's SQS call, GET and
   // write, so it bounds the poll's spinning as a whole). The CLI gives a process's queues 1 % in
   // total (10000 / queues each), so their spinning stays within 1 % of one core whatever the
-  // queue count. 0 disables. Pooled threads never spin beyond the window.
+  // queue count; under a cgroup CPU limit, within a tenth of the quota (Runner::spin_budget_for).
+  // Only answers within HttpClient::kMaxSpinThrough are ever spun through: a remote endpoint
+  // costs no spinning. 0 disables. Pooled threads never spin beyond the window.
   int64_t spin_budget_ppm = 10000;
 };
 
@@ -102,6 +104,10 @@ struct IterationRecord {
   Nanos update_ns = 0;         // Deployment PUT/PATCH(es)
   Nanos total_ns = 0;          // end of sleep -> end of iteration
   Nanos patch_latency_ns = -1; // end of sleep -> end of last successful write (-1: no write)
+  // CPU time of the worker thread for this poll: from the start of the iteration (its sleep, then
+  // the warm-up and its spin, then the poll) to the end of the poll -- everything but a sleep
+  // costs CPU here, spinning included. Pooled threads (Scheduler) count the poll alone. -1: none.
+  Nanos cpu_ns = -1;
   std::string error;
   std::string detail;  // traced polls with timed clients: {"sqs":{...},"write":{...}} (HttpTiming)
 };
@@ -139,6 +145,7 @@ struct RunnerStats {
   int32_t last_replicas = -1;
   uint64_t latency_samples = 0;
   int64_t latency_sum_ns = 0;                 // over every sample (the ring keeps the latest)
+  int64_t poll_cpu_ns = 0;                    // sum of IterationRecord::cpu_ns over every poll
   // Readiness: polls in a row that failed to read the depth or to write the Deployment, and
   // when the last poll that did neither ended (clock time; Run() entry before any poll).
   uint64_t consecutive_failed_polls = 0;
@@ -156,7 +163,7 @@ struct SharedWorkerState {
   enum Counter : int {
     kPolls, kDepthErrors, kScaleUps, kScaleDowns, kNoopUps, kNoopDowns, kCooldownSkipsUp,
     kCooldownSkipsDown, kFailedUps, kFailedDowns, kSpeculativeReads, kSpeculativeReadsUsed,
-    kSpeculativeReadsGated, kApiserverReads, kLatencySamples, kConsecutiveFailedPolls, kNumCounters
+    kSpeculativeReadsGated, kApiserverReads, kLatencySamples, kConsecutiveFailedPolls, kPollCpuNs, kNumCounters
   };
   enum Control : int32_t { kWait = 0, kGo = 1, kStop = 2 };
   enum Status : int32_t { kStarting = 0, kReady = 1, kRunning = 2, kExited = 3, kFailed = 4 };
@@ -252,6 +259,9 @@ class alignas(kCacheLine) Runner {
     sqs_->api()->set_spin_budget(ns / 4 * 3);
     scaler_->api()->set_spin_budget(ns / 8);
   }
+  // The spin budget run() gives a poll: LoopConfig::spin_budget_ppm of the poll period, and
+  // under a cgroup CPU limit at most a tenth of one CFS period's quota (times this queue's share).
+  static Nanos spin_budget_for(const LoopConfig& cfg, const CpuQuota& quota);
   // Closes the clients' keep-alive connections (on the calling thread's file table).
   void release_connections() {
     sqs_->api()->close_connections();
@@ -298,7 +308,8 @@ class alignas(kCacheLine) Runner {
  private:
   IterationRecord poll_body();
   void warm(Nanos due, bool presend = false);
-  void record(const IterationRecord& r);
+  void record(IterationRecord& r);
+  int64_t cpu_from_ = -1;  // thread CPU time at the start of the iteration in progress
   void mirror(const IterationRecord& r);
   CpuList cpus_;
   SharedWorkerState* shared_ = nullptr;

@@ -130,6 +130,8 @@ class FleetCollector:
                           "Polls in a row that failed to read the queue depth or to write the Deployment")
         failing_s = _Family("ksa_failing_seconds", "gauge",
                             "How long every poll has been failing (0 after a successful poll)")
+        cpu = _Family("ksa_poll_cpu_seconds_total", "counter",
+                      "CPU time of the worker thread in its polls (warm-up and busy-poll spinning included)")
         lat = _Family("ksa_poll_to_patch_seconds", "summary", "Poll start -> replica write acknowledged")
         hist = _Family("ksa_poll_to_patch_latency_seconds", "histogram",
                        "Poll start -> replica write acknowledged, per scaling poll")
@@ -152,6 +154,7 @@ class FleetCollector:
             reps.add("", lv, s["last_replicas"])
             failing.add("", lv, s.get("consecutive_failed_polls", 0))
             failing_s.add("", lv, w.runner.failing_ns() / 1e9)
+            cpu.add("", lv, s.get("poll_cpu_ns", 0) / 1e9)
             # every sample since start (the latency ring only keeps the latest)
             lat.add("_count", lv, s["latency_samples"])
             lat.add("_sum", lv, s["latency_sum_ns"] / 1e9)
@@ -162,7 +165,7 @@ class FleetCollector:
             hist.add("_count", lv, cum)
             hist.add("_sum", lv, s["latency_sum_ns"] / 1e9)
         return [*fams.values(), *(f for f in (*api.values(), *http.values()) if f.samples), depth, reps, failing,
-                failing_s, lat, hist]
+                failing_s, cpu, lat, hist]
 
     def exposition(self) -> bytes:
         out: List[str] = []
