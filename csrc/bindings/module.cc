@@ -251,6 +251,15 @@ PYBIND11_MODULE(_ksa_native, m) {
       });
   py::class_<StaticCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "StaticCredentialsProvider")
       .def(py::init<Credentials>());
+  py::class_<SharedCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "SharedCredentialsProvider")
+      .def(py::init([](std::shared_ptr<CredentialsProvider> inner, std::shared_ptr<Clock> clock, int64_t window_ns) {
+             return std::make_shared<SharedCredentialsProvider>(
+                 std::move(inner), [clock] { return clock->unix_nanos(); }, window_ns);
+           }),
+           py::arg("inner"), py::arg("clock"), py::arg("expiry_window_ns") = 5LL * 60 * kSecond)
+      // the lock may be held by a fetch waiting for the GIL (a Python inner provider)
+      .def("fetches", &SharedCredentialsProvider::fetches, py::call_guard<py::gil_scoped_release>())
+      .def("stale", &SharedCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>());
 
   py::class_<SigV4Signer, std::shared_ptr<SigV4Signer>>(m, "SigV4Signer")
       .def(py::init<std::string, std::string>(), py::arg("region"), py::arg("service"))
@@ -422,6 +431,19 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def("rtt_ewma", &HttpClient::rtt_ewma)
       .def("close", &HttpClient::close)
       .def("stats", [](HttpClient& c) { return http_stats_dict(c.stats()); });
+  auto quota_tuple = [](const CpuQuota& q) { return py::make_tuple(q.quota_ns, q.period_ns); };
+  m.def("parse_cpu_max", [quota_tuple](const std::string& t) { return quota_tuple(parse_cpu_max(t)); });
+  m.def("parse_cfs_quota", [quota_tuple](const std::string& q, const std::string& p) {
+    return quota_tuple(parse_cfs_quota(q, p));
+  });
+  m.def("read_cpu_quota", [quota_tuple](const std::string& root) { return quota_tuple(read_cpu_quota(root)); },
+        py::arg("root") = "/sys/fs/cgroup");
+  m.def("runner_spin_budget", [](const LoopConfig& cfg, int64_t quota_ns, int64_t period_ns) {
+    CpuQuota q;
+    q.quota_ns = quota_ns;
+    q.period_ns = period_ns;
+    return Runner::spin_budget_for(cfg, q);
+  }, py::arg("config"), py::arg("quota_ns") = 0, py::arg("period_ns") = 0);
   m.def("http_spin_window", &HttpClient::spin_window_for, py::arg("busy_poll_ns"), py::arg("ewma_ns"),
         py::arg("budget_ns"));
   m.def("parse_url", [](const std::string& s) {

@@ -192,7 +192,27 @@ Result<Credentials> CachedCredentials::get(int64_t unix_now_ns) {
 
 void CachedCredentials::invalidate() {
   std::lock_guard<std::mutex> lk(mu_);
+  if (have_) provider_->stale(cached_);
   have_ = false;
+}
+
+Result<Credentials> SharedCredentialsProvider::retrieve() {
+  std::lock_guard<std::mutex> lk(mu_);  // concurrent askers wait for the one fetch
+  if (have_ && (cached_.expires_unix_ns == 0 || now_() + window_ < cached_.expires_unix_ns))
+    return Result<Credentials>::Ok(cached_);
+  fetches_++;
+  auto r = inner_->retrieve();
+  have_ = r.ok() && r.value.valid();
+  if (have_) cached_ = r.value;
+  return r;
+}
+
+void SharedCredentialsProvider::stale(const Credentials& c) {
+  std::lock_guard<std::mutex> lk(mu_);
+  // the first client to see this set rejected drops it; the others then get its replacement
+  if (have_ && c.access_key_id == cached_.access_key_id && c.session_token == cached_.session_token &&
+      c.expires_unix_ns == cached_.expires_unix_ns)
+    have_ = false;
 }
 
 namespace {

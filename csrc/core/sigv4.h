@@ -9,6 +9,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -69,6 +70,8 @@ class CredentialsProvider {
  public:
   virtual ~CredentialsProvider() = default;
   virtual Result<Credentials> retrieve() = 0;
+  // A client found `c` rejected (ExpiredToken): a provider that caches drops it. Default: none.
+  virtual void stale(const Credentials& c) { (void)c; }
 };
 
 class StaticCredentialsProvider final : public CredentialsProvider {
@@ -95,6 +98,33 @@ class alignas(kCacheLine) CachedCredentials {
   std::mutex mu_;
   bool have_ = false;
   Credentials cached_;
+};
+
+// One credential source for every SQS client of a process with the same chain configuration
+// (region). Each client's CachedCredentials asks it when its own copy nears expiry; it calls
+// `inner` only when its copy does too (or a client reported it stale), under its lock, so N
+// tracked queues make one STS / ECS / IMDS fetch per expiry instead of N -- the reference builds
+// one session per process (/root/reference/sqs/sqs.go:36). `unix_now` is the clock (wall time).
+class SharedCredentialsProvider final : public CredentialsProvider {
+ public:
+  SharedCredentialsProvider(std::shared_ptr<CredentialsProvider> inner, std::function<int64_t()> unix_now,
+                            int64_t expiry_window_ns)
+      : inner_(std::move(inner)), now_(std::move(unix_now)), window_(expiry_window_ns) {}
+  Result<Credentials> retrieve() override;
+  void stale(const Credentials& c) override;
+  uint64_t fetches() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return fetches_;
+  }
+
+ private:
+  std::shared_ptr<CredentialsProvider> inner_;
+  std::function<int64_t()> now_;
+  int64_t window_;
+  mutable std::mutex mu_;
+  bool have_ = false;
+  Credentials cached_;
+  uint64_t fetches_ = 0;
 };
 
 struct SignDebug {

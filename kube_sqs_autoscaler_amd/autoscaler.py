@@ -207,6 +207,19 @@ def new_sqs_api(region: str, clock, endpoint: str = "", protocol: str = "query",
     return nat.HttpSqsApi(o, creds, clock)
 
 
+def shared_sqs_credentials(cache: dict, region: str, clock, environ: Optional[Mapping[str, str]] = None):
+    """The process's credential source for SQS clients of ``region`` (the STS region of a web
+    identity / assume-role chain follows it): one ``SharedCredentialsProvider`` per distinct
+    chain configuration, kept in ``cache``, so N tracked queues make one credential fetch per
+    expiry instead of N -- as the reference's one session per process (sqs/sqs.go:36). Each
+    client still keeps its own copy and refreshes it in its pre-poll warm-up, off the poll."""
+    p = cache.get(region)
+    if p is None:
+        p = cache[region] = native().SharedCredentialsProvider(make_chain_provider(environ=environ, region=region),
+                                                               clock)
+    return p
+
+
 def new_sqs_client(target: TargetConfig, api):
     return native().SqsClient(api, target.queue_url, list(target.attribute_names))
 
@@ -235,7 +248,10 @@ class Worker:
 
 
 def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger, clock,
-               credentials=None, environ: Optional[Mapping[str, str]] = None, tag_queue: bool = False) -> Worker:
+               credentials=None, environ: Optional[Mapping[str, str]] = None, tag_queue: bool = False,
+               credentials_cache: Optional[dict] = None) -> Worker:
+    """``credentials_cache``: share one credential source per region between the process's
+    workers (:func:`shared_sqs_credentials`); None with no ``credentials``: a chain of its own."""
     nat = native()
     log = base_logger
     if tag_queue:
@@ -245,7 +261,10 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
                                   burst=cfg.kube_api_burst, logger=log)
     scaler = new_pod_autoscaler(target, kube_api, log, clock)
     scaler.dry_run = cfg.dry_run
-    sqs_api = new_sqs_api(target.region or cfg.aws_region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
+    region = target.region or cfg.aws_region
+    if credentials is None and credentials_cache is not None:
+        credentials = shared_sqs_credentials(credentials_cache, region, clock, environ)
+    sqs_api = new_sqs_api(region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
                           credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
     runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns, len(cfg.targets)), sqs, scaler,

@@ -92,13 +92,16 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     if cfg.trace_file:
         trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
 
+    # one AWS credential source per region for the process's queues (each worker process of
+    # --worker-processes builds its own after the fork, as separate reference processes would)
+    creds: dict = {}
     if cfg.worker_processes:
         # fork the workers first: before this process starts threads or touches the GPU
         from .parallel.procfleet import ProcessFleet
 
         def build(t):
             def make():
-                w = autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi)
+                w = autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi, credentials_cache=creds)
                 if trace_fd >= 0:
                     w.runner.set_trace_fd(trace_fd)
                 return w
@@ -107,7 +110,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         fleet = ProcessFleet([build(t) for t in cfg.targets], cfg.targets)
         workers = fleet.workers
     else:
-        workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi) for t in cfg.targets]
+        workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi, credentials_cache=creds)
+                   for t in cfg.targets]
         if trace_fd >= 0:
             for w in workers:
                 w.runner.set_trace_fd(trace_fd)

@@ -1,0 +1,109 @@
+"""One AWS credential source per process and chain configuration (sigv4.h SharedCredentialsProvider).
+
+The reference builds one session per process (/root/reference/sqs/sqs.go:36), so one credential
+fetch per expiry. Round 4 gave every tracked queue a chain of its own: N queues made N STS / ECS /
+IMDS fetches at every expiry, each a Python urllib call on a worker thread.
+"""
+import json
+import threading
+from datetime import datetime, timedelta, timezone
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import pytest
+import yaml
+
+SEC = 1_000_000_000
+AKID, SECRET, REGION, TOKEN = "ASIASHARED", "shared/secret", "us-east-1", "kube-token"
+
+
+def test_shared_provider_fetches_once_per_expiry(nat):
+    clock = nat.VirtualClock()
+    calls = []
+
+    class Inner(nat.CredentialsProvider):
+        def retrieve(self):
+            calls.append(clock.unix_nanos())
+            return nat.Credentials("AKID", "secret", f"tok-{len(calls)}", clock.unix_nanos() + 600 * SEC, "Test")
+
+    shared = nat.SharedCredentialsProvider(Inner(), clock)  # 5-minute expiry window
+    got = [shared.retrieve() for _ in range(8)]
+    assert len(calls) == 1 and {c.session_token for c in got} == {"tok-1"}
+    clock.advance(299 * SEC)  # 301 s left: still outside the window
+    assert shared.retrieve().session_token == "tok-1" and len(calls) == 1
+    clock.advance(2 * SEC)  # 299 s left: inside it -> one fetch for every asker
+    assert {shared.retrieve().session_token for _ in range(8)} == {"tok-2"} and len(calls) == 2
+    # ExpiredToken seen by one client: the set is dropped once; a report about an older set is ignored
+    old = got[0]
+    shared.stale(old)
+    assert shared.retrieve().session_token == "tok-2" and len(calls) == 2
+    shared.stale(shared.retrieve())
+    assert shared.retrieve().session_token == "tok-3" and len(calls) == 3
+    assert shared.fetches() == 3
+
+
+class _Ecs(BaseHTTPRequestHandler):
+    """A container-credentials endpoint (AWS_CONTAINER_CREDENTIALS_FULL_URI): the first set
+    expires 5 min + 1.5 s from now (so it enters every client's 5-minute refresh window 1.5 s
+    into the run), later ones in an hour."""
+
+    fetches = 0
+    lock = threading.Lock()
+
+    def do_GET(self):  # noqa: N802
+        with _Ecs.lock:
+            _Ecs.fetches += 1
+            n = _Ecs.fetches
+        left = timedelta(minutes=5, seconds=1.5) if n == 1 else timedelta(hours=1)
+        body = json.dumps({"AccessKeyId": AKID, "SecretAccessKey": SECRET, "Token": f"session-{n}",
+                           "Expiration": (datetime.now(timezone.utc) + left).strftime("%Y-%m-%dT%H:%M:%S.%fZ")}).encode()
+        self.send_response(200)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def log_message(self, *a):
+        pass
+
+
+@pytest.mark.slow
+def test_eight_queues_one_fetch_per_expiry(nat, tmp_path):
+    from kube_sqs_autoscaler_amd.cli import main
+
+    _Ecs.fetches = 0
+    ecs = ThreadingHTTPServer(("127.0.0.1", 0), _Ecs)
+    threading.Thread(target=ecs.serve_forever, daemon=True).start()
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, REGION)
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    try:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"HOME": str(tmp_path), "KUBE_CONFIG_PATH": str(kc), "AWS_EC2_METADATA_DISABLED": "true",
+               "AWS_CONTAINER_CREDENTIALS_FULL_URI": f"http://127.0.0.1:{ecs.server_address[1]}/creds"}
+        specs = []
+        for i in range(8):
+            url = f"{sqs.url}/123/q{i}"
+            sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500" if i % 2 == 0 else "0"})
+            kube.add_deployment("gpu", f"w{i}", 4)
+            specs += ["--queue", f"url={url},deployment=w{i},namespace=gpu,attribute-names=ApproximateNumberOfMessages"]
+        rc = main([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=100ms",
+                   "--scale-up-cool-down=0s", "--scale-down-cool-down=0s", "--log-level=error", *specs],
+                  environ=env, max_iterations=25)  # 2.5 s: across the first set's refresh point
+        assert rc == 0
+        assert _Ecs.fetches == 2  # the first set, then its one refresh -- not 8 of each
+        assert sqs.signature_failures() == 0
+        # decisions are the reference's: each queue scaled to its bound
+        assert [kube.replicas("gpu", f"w{i}") for i in range(8)] == [8, 1] * 4
+        tokens = [v for k, v in sqs.last_headers() if k.lower() == "x-amz-security-token"]
+        assert tokens == ["session-2"]  # the last poll signed with the refreshed set
+    finally:
+        ecs.shutdown()
+        sqs.stop()
+        kube.stop()

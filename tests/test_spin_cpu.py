@@ -71,3 +71,44 @@ def test_busy_poll_costs_no_cpu_against_a_remote_endpoint(nat, endpoints, tmp_pa
     # (xdist) costs a few hundred us in either arm.
     assert statistics.median(default) <= 1.1 * statistics.median(off) + 20_000, (default, off)
     assert statistics.median(default) < latency_ms * 1_000_000 / 10, default
+
+
+@pytest.mark.parametrize("text,want", [
+    ("max 100000\n", (0, 0)),
+    ("10000 100000\n", (10_000_000, 100_000_000)),  # limits.cpu: 100m
+    ("250000 100000", (250_000_000, 100_000_000)),
+    ("garbage", (0, 0)),
+    ("-1 100000", (0, 0)),
+])
+def test_parse_cgroup_v2_cpu_max(nat, text, want):
+    assert nat.parse_cpu_max(text) == want
+
+
+def test_parse_cgroup_v1_cfs_quota(nat):
+    assert nat.parse_cfs_quota("-1\n", "100000\n") == (0, 0)
+    assert nat.parse_cfs_quota("10000\n", "100000\n") == (10_000_000, 100_000_000)
+
+
+def test_read_cpu_quota_from_a_cgroup_tree(nat, tmp_path):
+    (tmp_path / "cpu.max").write_text("20000 100000\n")
+    assert nat.read_cpu_quota(str(tmp_path)) == (20_000_000, 100_000_000)
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("50000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert nat.read_cpu_quota(str(v1)) == (50_000_000, 100_000_000)
+    assert nat.read_cpu_quota(str(tmp_path / "none")) == (0, 0)
+
+
+def test_spin_budget_capped_by_the_cpu_quota(nat):
+    """Runner::spin_budget_for: 1 % of the poll period (the CLI's share for one queue), and under
+    a CFS limit at most a tenth of one period's quota times the queue's share."""
+    cfg = nat.LoopConfig()
+    cfg.poll_period_ns = 5 * nat.SECOND
+    cfg.spin_budget_ppm = 10_000
+    assert nat.runner_spin_budget(cfg) == 50_000_000  # 1 % of 5 s, no limit
+    assert nat.runner_spin_budget(cfg, 10_000_000, 100_000_000) == 1_000_000  # 100m: 1 ms
+    cfg.spin_budget_ppm = 625  # one of 16 queues
+    assert nat.runner_spin_budget(cfg, 10_000_000, 100_000_000) == 62_500
+    cfg.poll_period_ns = 0
+    assert nat.runner_spin_budget(cfg, 10_000_000, 100_000_000) == 0
