@@ -774,7 +774,7 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
     Status s = connect_locked(deadline_ns);
     if (!s.ok()) return s;
   }
-  const bool reused = conn_->uses > 0;
+  bool reused = conn_->uses > 0;
   conn_->uses++;
   if (timing()) timing_cur_.write_begin = mono_ns();
 
@@ -795,6 +795,7 @@ Status HttpClient::write_request(const HttpRequest& req, int64_t deadline_ns, bo
       Status c = connect_locked(deadline_ns);
       if (!c.ok()) return c;
       conn_->uses++;
+      reused = false;  // a failed write on the fresh connection is not a stale-connection retry
     } else {
       stats_.presend_discards++;
     }

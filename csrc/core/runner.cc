@@ -107,7 +107,7 @@ IterationRecord Runner::step(StopFlag* stop) {
 }
 
 void Runner::warm(Nanos due, bool presend) {
-  sqs_->warm(clock_->unix_nanos() + (due - clock_->now()), presend && cfg_.presend);
+  sqs_->warm(clock_->unix_nanos() + (due - clock_->now()), presend && cfg_.presend && cfg_.prewarm <= kMaxPresendLead);
   // the Deployment read and write only follow on polls the gates may let through (or every
   // poll, with a GET sent on every poll)
   if ((cfg_.prefetch && cfg_.prefetch_always) || action_likely(due)) scaler_->warm();

@@ -36,6 +36,10 @@
 
 namespace ksa {
 
+// --poll-presend stages only when the warm-up lead is this short: far inside the kernel's 200 ms
+// TCP_CORK limit.
+inline constexpr Nanos kMaxPresendLead = 50 * kMillisecond;
+
 struct LoopConfig {
   Nanos poll_period = 5 * kSecond;            // --poll-period           main.go:83
   Nanos scale_down_cool_down = 30 * kSecond;  // --scale-down-cool-down  main.go:84
@@ -57,14 +61,16 @@ struct LoopConfig {
   // up to `prewarm` of CPU per poll. 0 disables. With a poll period under 2x `prewarm` the
   // preparation runs at the due time instead, without the early wake-up.
   Nanos prewarm = 0;
-  // With the early wake-up, also pre-send the SQS request (HttpClient::stage): all but its last
-  // bytes are handed to the kernel corked, so the kernel's send path has run before the due
-  // time and the poll's own write runs warm; nothing reaches the wire before the due time
-  // (unless the poll starts over 200 ms late, the kernel's cork limit: then the peer holds a
-  // partial request until the rest comes), and
-  // the request is byte for byte the one the poll sends (when it is not -- its signing second
-  // rolled over -- the staged connection is dropped and the poll dials a fresh one).
-  bool presend = true;
+  // With the early wake-up, also pre-send the SQS request (HttpClient::stage; --poll-presend,
+  // off by default): all but its last bytes are handed to the kernel corked, so the kernel's send
+  // path has run before the due time and the poll's own write runs warm; nothing reaches the wire
+  // before the due time, and the request is byte for byte the one the poll sends (when it is not
+  // -- its signing second rolled over -- the staged connection is dropped and the poll dials a
+  // fresh one). Linux releases a cork after 200 ms, so only a lead under kMaxPresendLead stages
+  // (a poll that starts over 200 ms late lets the peer see a partial request until the rest
+  // comes). Off by default: paired A/Bs showed no end-to-end win beyond noise (p50 0.96x,
+  // profiles/r04r_presend_ab.jsonl) for a staging path and a redial on a discard.
+  bool presend = false;
   // Dial both clients at Run() entry, on the worker's own thread, before the timers are armed
   // (decisions unchanged). A harness that would otherwise connect them from its main thread
   // (the bench) gets each connection's TLS state and buffers from the worker's allocator arena

@@ -224,8 +224,10 @@ def new_sqs_client(target: TargetConfig, api):
     return native().SqsClient(api, target.queue_url, list(target.attribute_names))
 
 
-def loop_config(target: TargetConfig, pipeline_reads: bool = False, prewarm_ns: int = 0, queues: int = 1):
+def loop_config(target: TargetConfig, pipeline_reads: bool = False, prewarm_ns: int = 0, queues: int = 1,
+                presend: bool = False):
     c = native().LoopConfig()
+    c.presend = presend
     # the process's queues share a 1 % busy-poll budget of their poll period (runner.h)
     c.spin_budget_ppm = SPIN_BUDGET_PPM // max(queues, 1)
     c.prefetch = pipeline_reads
@@ -267,8 +269,8 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     sqs_api = new_sqs_api(region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
                           credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
-    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns, len(cfg.targets)), sqs, scaler,
-                        clock, log)
+    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns, len(cfg.targets), cfg.poll_presend),
+                        sqs, scaler, clock, log)
     return Worker(target, runner, sqs_api, kube_api, log)
 
 

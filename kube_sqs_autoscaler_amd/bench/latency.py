@@ -212,7 +212,8 @@ class BenchEnv:
     production endpoint is (supported with ``shared``, ``process`` and ``split``). ``prewarm_ns``: the
     loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
     period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
-    ``presend``: stage each poll's SQS request during the warm-up (LoopConfig.presend);
+    ``presend``: stage each poll's SQS request during the warm-up (LoopConfig.presend; the CLI's
+    --poll-presend, off by default);
     these, ``busy_poll_ns``, ``mode`` and ``pipeline`` may be lists, one value per queue, cycled
     (paired comparisons within one run: :func:`measure_cadenced_arms`). ``timing``: the clients time every request's
     phases (HttpTiming), traced polls carry the breakdown (``detail``), and the fakes record each
@@ -222,7 +223,7 @@ class BenchEnv:
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", log_level: str = "info", sqs_protocol: str = "query",
                  poll_period_ns: int = 0, stagger: bool = False, hot_endpoints: bool = False, prewarm_ns: int = 0,
-                 timing: bool = False, spin_budget_ppm=None, presend=True):
+                 timing: bool = False, spin_budget_ppm=None, presend=False):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -559,7 +560,7 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
                    hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,
-                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm, presend=col("presend", True))
+                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm, presend=col("presend", False))
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: Dict[str, List[dict]] = {a: [] for a in names}
     try:

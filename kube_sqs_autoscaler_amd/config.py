@@ -30,6 +30,8 @@ Extensions (all off or reference-equivalent by default):
   ``action_likely``), so an idle queue reads the apiserver no more often than the reference.
 * ``--worker-processes``: one worker process per tracked queue (parallel/procfleet.py) instead
   of one thread per queue.
+* ``--poll-presend`` (default off): stage the SQS request during the warm-up (runner.h
+  ``LoopConfig::presend``); off because paired A/Bs showed no end-to-end win beyond noise.
 * ``--poll-prewarm`` (default 200us): the pre-poll warm-up (runner.h ``LoopConfig::prewarm``):
   the signed SQS request, the bearer token and both connections are ready, and the core awake,
   when the poll is due. The pipelined GET never dials inside the SQS call, so this is also what
@@ -107,6 +109,7 @@ class Config:
     worker_processes: bool = False
     busy_poll_ns: int = 25_000
     poll_prewarm_ns: int = DEFAULT_POLL_PREWARM_NS
+    poll_presend: bool = False
     kube_api_qps: float = 5.0
     kube_api_burst: int = 10
     trace_file: str = ""
@@ -177,6 +180,7 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.int("kube-api-burst", 10, "Requests allowed in a burst above -kube-api-qps (client-go default)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this; a queue on its own thread may also spin through twice the peer's response time when that fits in its share of 1% of -poll-period, split over the poll's requests (0s disables both)")
     fs.duration("poll-prewarm", DEFAULT_POLL_PREWARM_NS, "Before each poll, wake this long early to sign the SQS request, read the token and check (or dial, within 100ms) both connections, then start the poll on time; decisions are unchanged (0s disables)")
+    fs.bool("poll-presend", False, "With -poll-prewarm under 50ms: also hand all but the last bytes of the SQS request to the kernel during the warm-up, corked, so the poll's own write runs warm (nothing reaches the wire early)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
     fs.string("trace-file", "", "Append one JSON span per poll (depth, decisions, per-call latencies) to this file; empty disables")
@@ -297,6 +301,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         worker_processes=fs["worker-processes"],
         busy_poll_ns=fs["busy-poll"],
         poll_prewarm_ns=fs["poll-prewarm"],
+        poll_presend=fs["poll-presend"],
         kube_api_qps=fs["kube-api-qps"],
         kube_api_burst=fs["kube-api-burst"],
         trace_file=fs["trace-file"],

@@ -134,6 +134,8 @@ def cadenced(a) -> int:
             f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", f"--trace-file={trace}",
             f"--metrics-addr=127.0.0.1:{port}", "--log-level=error", "--api-timeout=10s"]
     args += [f"--queue=url={u},deployment=workers-{q},namespace=soak" for q, u in enumerate(urls)]
+    if a.presend:
+        args.append("--poll-presend")
     env = dict(os.environ, AWS_ACCESS_KEY_ID=AKID, AWS_SECRET_ACCESS_KEY=SECRET, KUBE_CONFIG_PATH=kc,
                AWS_CA_BUNDLE=ca, HOME=tmp)
     err = open(os.path.join(tmp, "stderr.log"), "w")
@@ -293,6 +295,7 @@ def main() -> int:
     ap.add_argument("--boundary-us", type=int, default=250,
                     help="cool-down comparisons this close to the edge are not judged by the replay")
     ap.add_argument("--hot", action="store_true", help="back-to-back single-queue soak without faults")
+    ap.add_argument("--presend", action="store_true", help="run the CLI with --poll-presend (staged SQS requests)")
     a = ap.parse_args()
     return hot(a) if a.hot else cadenced(a)
 

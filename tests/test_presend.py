@@ -147,3 +147,30 @@ def test_cadenced_polls_presend_their_sqs_request(nat, presend):
             assert st["presends"] == 0
     finally:
         env.close()
+
+
+def test_poll_presend_flag_off_by_default_and_wired():
+    """--poll-presend (default off) is LoopConfig.presend; the CLI's loop config follows it."""
+    from kube_sqs_autoscaler_amd.autoscaler import loop_config
+    from kube_sqs_autoscaler_amd.config import parse_args
+
+    off = parse_args(["--sqs-queue-url=u"])
+    on = parse_args(["--sqs-queue-url=u", "--poll-presend"])
+    assert off.poll_presend is False and on.poll_presend is True
+    for cfg in (off, on):
+        lc = loop_config(cfg.targets[0], cfg.pipeline_reads, cfg.poll_prewarm_ns, 1, cfg.poll_presend)
+        assert lc.presend is cfg.poll_presend
+
+
+@pytest.mark.parametrize("prewarm_ms,staged", [(1, True), (60, False)])
+def test_presend_only_with_a_lead_far_inside_the_cork_limit(nat, prewarm_ms, staged):
+    """Linux releases TCP_CORK after 200 ms: a warm-up lead of kMaxPresendLead (50 ms) or more
+    never stages, so no partial request can reach the peer before the poll."""
+    env = BenchEnv(1, busy_poll_ns=25_000, poll_period_ns=3 * prewarm_ms * 1_000_000, prewarm_ns=prewarm_ms * 1_000_000,
+                   presend=True)
+    try:
+        env.run(5)
+        st = env.sqs_apis[0].stats()["http"]
+        assert (st["presends"] >= 2) if staged else (st["presends"] == 0 and st["presend_discards"] == 0)
+    finally:
+        env.close()

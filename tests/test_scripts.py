@@ -31,11 +31,11 @@ def test_cadence_arms_script(nat):
 
 @pytest.mark.slow
 def test_soak_script_short(nat):
-    rows = _run(["scripts/soak.py", "--minutes", "0.3", "--window", "6", "--queues", "2", "--fault-every", "2"],
-                timeout=200)
+    rows = _run(["scripts/soak.py", "--minutes", "0.3", "--window", "6", "--queues", "2", "--fault-every", "2",
+                 "--presend"], timeout=200)
     summary = rows[-1]
     assert summary["summary"] and summary["replay"]["mismatches"] == 0 and summary["exit_code"] == 0
-    # the per-client transport counters of /metrics reach the window rows: the CLI's default
+    # the per-client transport counters of /metrics reach the window rows: with --poll-presend the
     # warm-up stages the polls' SQS requests (1 s period)
     windows = [r for r in rows if "window" in r and "scrape_error" not in r]
     assert windows and windows[-1]["http_connects_sqs"] >= 2 and windows[-1]["http_presends_sqs"] > 0
