@@ -26,7 +26,9 @@ reference-equivalent paths as paired arms of each run: ``_cadence_rows``).
 Launch: ``python bench.py --gpus N`` with N > 1 outside a launcher starts the N ranks itself
 (child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set,
 before the parent touches torch or the GPU) and exits with the first failing rank's status;
-under ``torchrun`` the launcher's WORLD_SIZE must equal ``--gpus`` (exit 2 otherwise).
+under ``torchrun`` the launcher's WORLD_SIZE must equal ``--gpus`` (exit 2 otherwise). A node
+with fewer visible GPUs than ranks exits 2, unless ``--rehearse-shared-gpus``: then the ranks
+share GPUs over gloo and ``n_gpus`` is the number of GPUs actually used.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--queues Q] [--mode scale]
 """
@@ -86,20 +88,25 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     is 5 s, /root/reference/main.go:83), one thread per queue, staggered over the period, against
     the ``split`` fake endpoints: one fake SQS process and one fake apiserver process serving
     every queue, as production has two services (bench/latency.py ``measure_cadenced_arms``).
-    Every row runs the default path (with the CLI's --poll-prewarm) and the reference-equivalent
-    path (full-Deployment GET+PUT, sequential, no warm-up) as paired arms of ONE run, their
-    queues interleaved: a box's idle-state and frequency behaviour drifts between runs and moved
-    single-path runs of one path by 2x (profiles/r04c_cadence_probe.jsonl), so paths compared in
-    separate runs could invert by chance. In this order, most important first:
+    Every row runs the default path (the CLI's flags: --poll-prewarm, --busy-poll) and the
+    reference-equivalent path (full-Deployment GET+PUT, sequential, no warm-up, no busy-poll) as
+    paired arms of ONE run, their queues interleaved: a box's idle-state and frequency behaviour
+    drifts between runs and moved single-path runs of one path by 2x
+    (profiles/r04c_cadence_probe.jsonl), so paths compared in separate runs could invert by
+    chance. Every row also reports each arm's worker CPU per poll (``cpu_ms_per_poll``, the
+    spans' thread CPU time: warm-up, spinning and the poll). In this order, most important first:
 
     1. BASELINE's queue axis at 250 ms: 1, 2, 4 and 8 tracked queues per path, at least
        ``--cadence-queue-samples`` scaling polls per path (``cadenced_p50_ms_by_tracked_queues``);
-    2. ``--cadence-queues`` queues per path at 250 ms, plain and TLS;
-    3. the same at 1 s, plain, TLS, and with endpoints that never sleep (``_hot_endpoints``, a
-       loaded production endpoint: the difference is what the fakes' own idle wake-ups add);
-       the ``_timed`` rows repeat the plain and hot rows with every call broken down (HttpTiming
-       on the client, per-request wake-up and service times on the fakes) for the attribution --
-       the instrumentation adds a few syscalls per request, so their p50 is not the row's number.
+    2. the regional-RTT model at a cadence (``wan_cadenced_p50_ms``, ``cpu_ms_per_poll``): 1 s,
+       the fakes answering SQS after 2 ms and the apiserver after 1 ms -- the structural saving
+       (one apiserver round trip, overlapped) at the CPU each path spends;
+    3. the queue axis again against endpoints that never sleep (``_hot_endpoints``: a loaded
+       production endpoint), and timed at 1 and 8 queues (every call broken down on the client,
+       HttpTiming, and on the fakes, wake-up and service time per request) -- the attribution of
+       the axis's growth (``cadenced_by_tracked_queues_attribution``);
+    4. ``--cadence-queues`` queues per path at 250 ms, plain and TLS, and at 1 s, plain and with
+       hot endpoints; then 1 s timed.
 
     Rows that would start past ``deadline`` (time.monotonic) are skipped and listed."""
     import math
@@ -111,52 +118,79 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     skip = 2  # each queue's first polls (dial, first allocations) are dropped
     arms = {"default": dict(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp, prewarm_ns=DEFAULT_POLL_PREWARM_NS),
             "reference_equivalent": dict(mode="deployment", pipeline=False, busy_poll_ns=0, prewarm_ns=0)}
-    # plan rows: (group, period label, period ns, suffix, queues per arm, polls per queue, tls, hot, timing)
-    plan = []
-    for q in (1, 2, 4, 8):
-        plan.append(("by_queues", "250ms", 250 * ms, f"/{q}", q, math.ceil(args.cadence_queue_samples / q) + skip,
-                     False, False, False))
+    # plan rows: (group, period label, period ns, suffix, queues per arm, polls per queue, tls, hot, timing, wan)
+    by_q_polls = lambda q: math.ceil(args.cadence_queue_samples / q) + skip  # noqa: E731
+    plan = [("by_queues", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, False, False, False) for q in (1, 2, 4, 8)]
+    plan.append(("wan", "1s", 1000 * ms, "_wan_sqs2ms_kube1ms", args.cadence_queues, args.cadence_polls,
+                 False, False, False, True))
+    plan += [("by_queues_hot", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, True, False, False)
+             for q in (1, 2, 4, 8)]
+    plan += [("by_queues_timed", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, False, True, False) for q in (1, 8)]
     for label, period, variants in (("250ms", 250 * ms, ((False, False), (True, False))),
-                                    ("1s", 1000 * ms, ((False, False), (True, False), (False, True)))):
+                                    ("1s", 1000 * ms, ((False, False), (False, True)))):
         for tls, hot in variants:
             suffix = ("_tls" if tls else "") + ("_hot_endpoints" if hot else "")
-            plan.append(("fleet", label, period, suffix, args.cadence_queues, args.cadence_polls, tls, hot, False))
-    for hot in (False, True):
-        plan.append(("fleet", "1s", 1000 * ms, ("_hot_endpoints" if hot else "") + "_timed", args.cadence_queues,
-                     args.cadence_polls, False, hot, True))
+            plan.append(("fleet", label, period, suffix, args.cadence_queues, args.cadence_polls, tls, hot, False, False))
+    plan.append(("fleet", "1s", 1000 * ms, "_timed", args.cadence_queues, args.cadence_polls, False, False, True, False))
     skipped = []
-    p50, rows, by_q, by_q_samples = {}, {}, {}, {}
-    for group, label, period, suffix, queues, polls, tls, hot, timing in plan:
+    p50, rows, cpu = {}, {}, {}
+    by_q = {"250ms": {}, "250ms_hot_endpoints": {}}
+    by_q_samples, by_q_setup, attribution = {}, {}, {}
+    for group, label, period, suffix, queues, polls, tls, hot, timing, wan in plan:
         if time.monotonic() > deadline:
             skipped.append(f"{label}/{group}{suffix}")
             continue
-        res = measure_cadenced_arms(period, polls, queues, arms, tls, skip=skip, hot_endpoints=hot, timing=timing)
+        res = measure_cadenced_arms(period, polls, queues, arms, tls, skip=skip, hot_endpoints=hot, timing=timing,
+                                    sqs_latency_ns=2 * ms if wan else 0, kube_latency_ns=1 * ms if wan else 0)
         for name, r in res.items():
-            if group == "by_queues":
-                by_q.setdefault(name, {})[str(queues)] = r["p50_ms"]
-                by_q_samples.setdefault(name, {})[str(queues)] = r["samples"]
+            if group in ("by_queues", "by_queues_hot"):
+                key = "250ms" + ("_hot_endpoints" if hot else "")
+                by_q[key].setdefault(name, {})[str(queues)] = r["p50_ms"]
+                by_q_samples.setdefault(key, {}).setdefault(name, {})[str(queues)] = r["samples"]
+                cpu.setdefault(f"{key}_by_tracked_queues", {}).setdefault(name, {})[str(queues)] = r.get("cpu_ms_per_poll")
+                if name == "default":
+                    by_q_setup.setdefault(key, {})[str(queues)] = r["setup"]
+            elif group == "by_queues_timed":
+                attribution.setdefault(str(queues), {})[name] = {
+                    k: r.get(k) for k in ("p50_ms", "phase_median_us", "call_phase_median_us", "endpoint_median_us",
+                                          "setup")}
             else:
                 rows.setdefault(label, {})[name + suffix] = r
+                cpu.setdefault(label + suffix, {})[name] = r.get("cpu_ms_per_poll")
                 if not timing:
                     p50.setdefault(label, {})[name + suffix] = r["p50_ms"]
         _progress(f"cadence {label} {group}{suffix} ({queues} queues per path): " +
-                  ", ".join(f"{name} p50 {r['p50_ms']} ms over {r['samples']}" for name, r in res.items()))
+                  ", ".join(f"{name} p50 {r['p50_ms']} ms over {r['samples']}, cpu {r.get('cpu_ms_per_poll')} ms/poll"
+                            for name, r in res.items()))
     if skipped:
         _progress(f"cadence rows skipped (past --extras-budget-s): {skipped}")
+    wan_row = {k[len(""):]: v for k, v in p50.get("1s", {}).items() if k.endswith("_wan_sqs2ms_kube1ms")}
+    wan_p50 = {k.replace("_wan_sqs2ms_kube1ms", ""): v for k, v in wan_row.items()}
+    growth = {}
+    for key, row in by_q.items():
+        for name, v in row.items():
+            if v.get("1") and v.get("8"):
+                growth.setdefault(key, {})[name] = round(v["8"] / v["1"], 2)
     return {
         **({"cadenced_rows_skipped": skipped} if skipped else {}),
         "cadenced_rows": rows,
         "cadenced_samples": {k: {n: r["samples"] for n, r in v.items()} for k, v in rows.items()},
         "cadenced_by_tracked_queues_samples": by_q_samples,
-        "cadenced_by_tracked_queues_setup": ("q tracked queues per path, one thread each; the default and the "
-                                             "reference-equivalent path's queues interleaved in one run (2q "
-                                             "threads, starts staggered over the period) against one fake SQS "
-                                             "process and one fake apiserver process"),
+        "cadenced_by_tracked_queues_setup": by_q_setup,
+        "cadenced_by_tracked_queues_setup_note": (
+            "q tracked queues per path, one thread each; the default and the reference-equivalent path's queues "
+            "interleaved in one run (2q threads, starts staggered over the period) against one fake SQS process and "
+            "one fake apiserver process (thread per connection; _hot_endpoints: one busy-polling thread each)"),
+        "cadenced_by_tracked_queues_attribution": attribution,
         "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()
                                                if "default" in v},
         "cadenced_reference_over_default": _ratios(p50, by_q),
         "cadenced_p50_ms": p50,
-        "cadenced_p50_ms_by_tracked_queues": {"250ms": by_q} if by_q else {},
+        "cadenced_by_tracked_queues_8_over_1": growth,
+        "cadenced_p50_ms_by_tracked_queues": {k: v for k, v in by_q.items() if v},
+        "cpu_ms_per_poll_all_rows": cpu,
+        "wan_cadenced_p50_ms": wan_p50,
+        "cpu_ms_per_poll": cpu.get("1s_wan_sqs2ms_kube1ms", {}),
     }
 
 
@@ -169,10 +203,11 @@ def _ratios(p50: dict, by_q: dict) -> dict:
                 ref = row.get("reference_equivalent" + key[len("default"):])
                 if ref and v:
                     out.setdefault(label, {})[key[len("default"):].lstrip("_") or "plain"] = round(ref / v, 2)
-    d, r = by_q.get("default", {}), by_q.get("reference_equivalent", {})
-    for q in d:
-        if r.get(q) and d[q]:
-            out.setdefault("250ms_by_tracked_queues", {})[q] = round(r[q] / d[q], 2)
+    for setup, row in by_q.items():
+        d, r = row.get("default", {}), row.get("reference_equivalent", {})
+        for q in d:
+            if r.get(q) and d[q]:
+                out.setdefault(f"{setup}_by_tracked_queues", {})[q] = round(r[q] / d[q], 2)
     return out
 
 
@@ -309,12 +344,15 @@ def main(argv=None) -> int:
                     help="queues (one thread each, staggered) per production-cadence row")
     ap.add_argument("--cadence-polls", type=int, default=27,
                     help="polls per queue per production-cadence fleet row (the first 2 of each queue are dropped)")
-    ap.add_argument("--cadence-queue-samples", type=int, default=200,
+    ap.add_argument("--cadence-queue-samples", type=int, default=120,
                     help="scaling polls per row of the 250 ms 1/2/4/8-tracked-queue rows")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
     ap.add_argument("--pin-ranks", default="auto", choices=["auto", "on", "off"],
                     help="confine each rank of a multi-rank job to its own slice of this process's CPUs, as N "
                          "autoscaler pods with CPU limits are (auto: on when the job has more than one rank)")
+    ap.add_argument("--rehearse-shared-gpus", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share GPUs, samples pool over gloo): a rehearsal of an "
+                         "N-GPU run on a smaller box, reported with n_gpus = the GPUs actually used")
     ap.add_argument("--extras-budget-s", type=float, default=400.0,
                     help="seconds after start past which the remaining secondary sections and cadence rows are skipped "
                          "(recorded under extra.skipped_sections); the headline line is always printed")
@@ -344,9 +382,17 @@ def main(argv=None) -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available()
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    # one rank per GPU over RCCL; more ranks than GPUs (a rehearsal of an N-GPU run on a smaller
-    # box) cannot share a device under RCCL, so such a job pools its samples over gloo instead
-    backend = "nccl" if use_cuda and torch.cuda.device_count() >= local_world else "gloo"
+    gpus_visible = torch.cuda.device_count() if use_cuda else 0
+    # One rank per GPU over RCCL. More ranks than GPUs is only a rehearsal of an N-GPU run on a
+    # smaller box (--rehearse-shared-gpus): ranks share devices, which RCCL cannot, so such a job
+    # pools its samples over gloo and reports the GPUs it actually used, not N.
+    shared_gpus = world > 1 and gpus_visible < local_world
+    if shared_gpus and not args.rehearse_shared_gpus:
+        print(f"bench.py: {local_world} ranks on this node but {gpus_visible} GPU(s) visible; one rank per GPU is "
+              "required (--rehearse-shared-gpus runs them anyway, reporting the GPUs actually used)", file=sys.stderr)
+        return 2
+    n_gpus = min(gpus_visible, local_world) * (world // max(local_world, 1)) if shared_gpus else world
+    backend = "nccl" if use_cuda and not shared_gpus else "gloo"
     if use_cuda:
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
     if world > 1 and backend == "gloo" and use_cuda and rank == 0:
@@ -408,7 +454,9 @@ def main(argv=None) -> int:
             "busy_poll_us": args.busy_poll_us,
             "fake_endpoints": servers,
             "collective_backend": backend if world > 1 else None,
-            "gpus_visible": torch.cuda.device_count() if use_cuda else 0,
+            "gpus_visible": gpus_visible,
+            "ranks": world,
+            "rehearsal_shared_gpus": shared_gpus,
             "rank0_cpus": f"{pinned[0]}-{pinned[-1]}" if pinned else None,
             "iterations_per_s": round(args.queues * world * args.steps / wall_max, 1),
             "signature_failures": res.signature_failures,
@@ -503,13 +551,14 @@ def main(argv=None) -> int:
         summary = ("wan_model_sqs2ms_kube1ms_p50_ms", "tls_p50_ms", "reference_equivalent_p50_ms",
                    "sequential_scale_p50_ms", "p50_ms_by_tracked_queues_worker_processes", "p50_ms_by_tracked_queues",
                    "cadenced_vs_hot_loop_default_plain", "cadenced_reference_over_default", "cadenced_p50_ms",
-                   "cadenced_p50_ms_by_tracked_queues")
+                   "cadenced_by_tracked_queues_8_over_1", "cadenced_p50_ms_by_tracked_queues", "wan_cadenced_p50_ms",
+                   "cpu_ms_per_poll")
         extra = {**{k: v for k, v in extra.items() if k not in summary}, **{k: extra[k] for k in summary if k in extra}}
         out = {
             "metric": METRIC,
             "value": round(p50, 4),
             "unit": "ms",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(wall_max * 1000.0 / args.steps, 5),

@@ -3,8 +3,8 @@
 ``python -m kube_sqs_autoscaler_amd.bench.fakeserve --queues Q --pairs N`` starts N fake SQS +
 apiserver pairs serving Q bench queues (latency.start_fake_endpoints), prints one JSON line
 with their URLs and certificates, then answers commands on stdin, one per line:
-``stats`` -> a JSON line of request / connection / signature counters and the replicas of every
-bench Deployment; ``timings`` -> a JSON line with every served request's (wake-up delay, service
+``stats`` -> a JSON line of request / connection / signature counters, the replicas of every
+bench Deployment, and this process's thread count and CPU time (``threads``, ``cpu_ns``); ``timings`` -> a JSON line with every served request's (wake-up delay, service
 time) in ns, per endpoint kind (HttpServer::timings), and clears them; ``quit`` -> stop the
 servers and exit (EOF on stdin does the same).
 """
@@ -14,8 +14,9 @@ import argparse
 import json
 import os
 import sys
+import time
 
-from .latency import deployment_name, start_fake_endpoints
+from .latency import deployment_name, start_fake_endpoints, thread_count
 
 
 def main(argv=None) -> int:
@@ -49,6 +50,7 @@ def main(argv=None) -> int:
                     "signature_failures": sum(s.signature_failures() for s in sqs),
                     "replicas": [kube[q % len(kube)].replicas("bench", deployment_name(a.queue_offset + q))
                                  for q in range(a.queues)] if kube else [],
+                    "threads": thread_count(), "cpu_ns": time.process_time_ns(),
                 }), flush=True)
             elif cmd == "timings":
                 out = {"sqs": [t for s in sqs for t in s.timings()], "kube": [t for k in kube for t in k.timings()]}

@@ -125,6 +125,18 @@ def start_fake_endpoints(queues: int, n_servers: int, tls: bool = False, sqs_lat
     return sqs_servers, kube_servers
 
 
+def thread_count(pid: str = "self") -> int:
+    """Threads of a process (/proc/<pid>/status), 0 when unknown."""
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("Threads:"):
+                    return int(line.split()[1])
+    except OSError:
+        pass
+    return 0
+
+
 def queue_url(sqs_url: str, q: int) -> str:
     return f"{sqs_url}/000000000000/bench-queue-{q}"
 
@@ -529,7 +541,7 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
 
 def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, arms: Dict[str, Dict],
                           tls: bool = False, skip: int = 2, servers: str = "split", hot_endpoints: bool = False,
-                          timing: bool = False) -> Dict[str, Dict]:
+                          timing: bool = False, sqs_latency_ns: int = 0, kube_latency_ns: int = 0) -> Dict[str, Dict]:
     """Poll -> patch latency at a production poll cadence for one or more paths side by side.
 
     The reference sleeps ``--poll-period`` (5 s by default) before every poll
@@ -546,7 +558,11 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     and moved single-path runs of the same path by 2x between consecutive runs
     (profiles/r04c_cadence_probe.jsonl). Every poll scales (the 200/0 trace, zero cool-downs).
     The first ``skip`` polls of each queue (dial, TLS handshake, first allocations) are dropped.
-    Phases come from the per-poll spans (``--trace-file`` format).
+    Phases come from the per-poll spans (``--trace-file`` format), and so does each poll's CPU time
+    on the worker thread (``cpu_ns``: warm-up, its spin, busy-polling and the poll itself), reported
+    per arm as ``cpu_ms_per_poll``. ``sqs_latency_ns`` / ``kube_latency_ns``: the fakes answer that
+    much later (a regional round trip). ``setup`` records what the run had: the CPUs this process
+    may use, its threads, and with endpoint processes their threads and CPU per request served.
     """
     import json
     import statistics
@@ -560,13 +576,24 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
                    hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,
-                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm, presend=col("presend", False))
+                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm, presend=col("presend", False),
+                   sqs_latency_ns=sqs_latency_ns, kube_latency_ns=kube_latency_ns)
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: Dict[str, List[dict]] = {a: [] for a in names}
+    setup = {"cpus_available": len(os.sched_getaffinity(0))}
     try:
         for r, f in zip(env.runners, files):
             r.set_trace_fd(f.fileno())
+        before = [rem.stats() for rem in env.remotes]
         wall = env.run(polls)
+        after = [rem.stats() for rem in env.remotes]
+        setup["autoscaler_threads"] = thread_count()
+        if after:
+            setup["endpoint_threads"] = [s.get("threads", 0) for s in after]
+            setup["endpoint_cpu_us_per_request"] = [
+                round((a["cpu_ns"] - b["cpu_ns"]) / 1e3 / max(1, a["sqs_requests"] + a["kube_requests"]
+                                                              - b["sqs_requests"] - b["kube_requests"]), 2)
+                for a, b in zip(after, before)]
         for q, (r, f) in enumerate(zip(env.runners, files)):
             r.set_trace_fd(-1)
             f.seek(0)
@@ -602,6 +629,8 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
             "phase_median_us": {"depth_us": med("depth_ns"), "get_wait_us": med("get_ns"), "write_us": med("update_ns"),
                                 "patch_us": med("patch_latency_ns")},
             "wall_s": round(wall, 2),
+            **_cpu_per_poll(spans[a]),
+            "setup": setup,
             # With timing: every client call's phases, and the fake endpoints' side of each
             # request (HttpServer::timings, all arms together) -- how long the endpoint's thread
             # took to wake up for it after the kernel received it, and to answer it.
@@ -610,6 +639,17 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
                 "call_phase_median_us": _detail_medians(scaled)} if timing else {}),
         }
     return out
+
+
+def _cpu_per_poll(spans: List[dict]) -> Dict:
+    """The worker thread's CPU per poll (span ``cpu_ns``): mean and median, milliseconds."""
+    import statistics
+
+    cpu = [s["cpu_ns"] for s in spans if s.get("cpu_ns", -1) >= 0]
+    if not cpu:
+        return {}
+    return {"cpu_ms_per_poll": round(sum(cpu) / len(cpu) / 1e6, 4),
+            "cpu_ms_per_poll_p50": round(statistics.median(cpu) / 1e6, 4)}
 
 
 def _detail_medians(spans: List[dict]) -> Dict:

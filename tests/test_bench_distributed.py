@@ -23,9 +23,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _check(out, n, steps, warmup):
+def _check(out, n, steps, warmup, gpus=None):
+    """``n`` ranks; ``gpus``: the n_gpus reported (default n; a CPU rehearsal uses none)."""
     assert out["metric"].startswith("poll") and out["unit"] == "ms" and out["higher_is_better"] is False
-    assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
+    assert out["n_gpus"] == (n if gpus is None else gpus) and out["steps"] == steps and out["warmup"] == warmup
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["scaling"] == "weak"
     assert out["config"]["parallelism"] == f"dp{n}" and out["vs_baseline"] is None
     assert out["extra"]["decision_parity"]["fraction"] == 1.0
@@ -45,10 +46,11 @@ def test_bench_two_ranks_gloo():
     env["CUDA_VISIBLE_DEVICES"] = ""  # CPU ranks: gloo backend
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--steps", "150",
-                        "--warmup", "10"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+                        "--warmup", "10", "--rehearse-shared-gpus"], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     out = _json_line(r.stdout)
-    _check(out, 2, 150, 10)
+    _check(out, 2, 150, 10, gpus=0)
     assert out["extra"]["tracked_queues"] == 2
 
 
@@ -58,14 +60,26 @@ def test_bench_launches_its_own_ranks_without_a_launcher():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--steps", "50", "--warmup", "5", "--no-sweep"],
-                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--steps", "50", "--warmup", "5", "--no-sweep",
+                        "--rehearse-shared-gpus"], cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert len(r.stdout.splitlines()) == 1, r.stdout  # gloo's rendezvous chatter goes to stderr
     out = _json_line(r.stdout)
-    _check(out, 3, 50, 5)
+    _check(out, 3, 50, 5, gpus=0)  # a rehearsal: n_gpus is the GPUs used (none here), not 3
     assert out["extra"]["tracked_queues"] == 3 and out["config"]["global_batch"] == 3
+    assert out["extra"]["ranks"] == 3 and out["extra"]["rehearsal_shared_gpus"] is True
     assert out["extra"]["collective_backend"] == "gloo"  # no GPUs here (RCCL on a GPU node)
+
+
+def test_bench_refuses_more_ranks_than_gpus_without_the_rehearsal_flag():
+    """`--gpus 3` on a box without 3 GPUs exits 2: n_gpus must be GPUs, not ranks sharing one."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--steps", "5", "--warmup", "1", "--no-sweep"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2 and r.stdout == ""
+    assert "3 ranks on this node but 0 GPU(s) visible" in r.stderr
 
 
 def test_bench_refuses_a_launcher_world_that_differs_from_gpus():
@@ -106,7 +120,7 @@ def test_bench_prints_its_line_when_secondary_sections_run_out_of_time():
 
 
 def test_cadence_rows_past_their_deadline_are_skipped_and_named():
-    """The cadence section checks the budget before every row (12 rows of up to ~27 s each), so a
+    """The cadence section checks the budget before every row (16 rows of up to ~30 s each), so a
     slow box cannot run the whole section past --extras-budget-s."""
     import argparse
 
@@ -115,16 +129,21 @@ def test_cadence_rows_past_their_deadline_are_skipped_and_named():
 
     args = argparse.Namespace(mode="scale", cadence_polls=3, cadence_queues=1, cadence_queue_samples=4)
     out = bench._cadence_rows(args, True, 0, 0.02, deadline=0.0)
-    assert len(out["cadenced_rows_skipped"]) == 11 and "250ms/fleet" in out["cadenced_rows_skipped"]
-    assert "250ms/by_queues/8" in out["cadenced_rows_skipped"] and "1s/fleet_hot_endpoints_timed" in out["cadenced_rows_skipped"]
+    sk = out["cadenced_rows_skipped"]
+    assert len(sk) == 16 and "250ms/fleet" in sk and "1s/wan_wan_sqs2ms_kube1ms" in sk
+    assert "250ms/by_queues/8" in sk and "250ms/by_queues_hot/8" in sk and "250ms/by_queues_timed/1" in sk
+    assert "1s/fleet_timed" in sk
     assert out["cadenced_p50_ms"] == {} and out["cadenced_vs_hot_loop_default_plain"] == {}
-    assert out["cadenced_p50_ms_by_tracked_queues"] == {}
+    assert out["cadenced_p50_ms_by_tracked_queues"] == {} and out["wan_cadenced_p50_ms"] == {}
+    assert out["cpu_ms_per_poll"] == {}
 
 
 @pytest.mark.slow
 def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
     """BASELINE's 1/2/4/8 tracked queues at a 250 ms cadence, default vs reference-equivalent
-    path, each row with at least --cadence-queue-samples scaling polls (small here)."""
+    path, each row with at least --cadence-queue-samples scaling polls (small here), against
+    sleeping and hot endpoints, with the 1- and 8-queue attribution; the regional-RTT row at a
+    cadence with both arms' CPU per poll."""
     import argparse
 
     sys.path.insert(0, ROOT)
@@ -143,21 +162,34 @@ def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
     import time
 
     out = bench._cadence_rows(args, True, 25_000, 0.02, deadline=time.monotonic() + 120)
-    by_q = out["cadenced_p50_ms_by_tracked_queues"]["250ms"]
-    assert set(by_q) == {"default", "reference_equivalent"}
-    for name in by_q:
-        assert set(by_q[name]) == {"1", "2", "4", "8"} and all(v > 0 for v in by_q[name].values())
-        assert all(n >= 8 for n in out["cadenced_by_tracked_queues_samples"][name].values())
+    for setup in ("250ms", "250ms_hot_endpoints"):
+        by_q = out["cadenced_p50_ms_by_tracked_queues"][setup]
+        assert set(by_q) == {"default", "reference_equivalent"}
+        for name in by_q:
+            assert set(by_q[name]) == {"1", "2", "4", "8"} and all(v > 0 for v in by_q[name].values())
+            assert all(n >= 8 for n in out["cadenced_by_tracked_queues_samples"][setup][name].values())
+        assert set(out["cadenced_by_tracked_queues_8_over_1"][setup]) == {"default", "reference_equivalent"}
+        for q, st in out["cadenced_by_tracked_queues_setup"][setup].items():
+            assert st["cpus_available"] >= 1 and st["autoscaler_threads"] >= 2 * int(q)
+            assert len(st["endpoint_threads"]) == 2 and len(st["endpoint_cpu_us_per_request"]) == 2
     assert calls[0] == (250_000_000, 10, 1, ["default", "reference_equivalent"])  # both paths in one run
     assert [c[2] for c in calls[:4]] == [1, 2, 4, 8]
+    att = out["cadenced_by_tracked_queues_attribution"]
+    assert set(att) == {"1", "8"} and "endpoint_median_us" in att["8"]["default"]
+    assert "call_phase_median_us" in att["1"]["reference_equivalent"]
     assert "cadenced_rows_skipped" not in out and set(out["cadenced_p50_ms"]) == {"250ms", "1s"}
     assert set(out["cadenced_p50_ms"]["250ms"]) == {"default", "reference_equivalent", "default_tls",
                                                    "reference_equivalent_tls"}
     r = out["cadenced_rows"]["1s"]["default_timed"]
     assert r["paired_with"] == ["reference_equivalent"] and r["queues_in_run"] == 4 and "call_phase_median_us" in r
-    assert list(out)[-1] == "cadenced_p50_ms_by_tracked_queues"
+    assert set(out["wan_cadenced_p50_ms"]) == {"default", "reference_equivalent"}
+    assert all(v > 2.0 for v in out["wan_cadenced_p50_ms"].values())  # a 2 ms SQS answer at least
+    assert set(out["cpu_ms_per_poll"]) == {"default", "reference_equivalent"}
+    assert all(v > 0 for v in out["cpu_ms_per_poll"].values())
+    assert list(out)[-2:] == ["wan_cadenced_p50_ms", "cpu_ms_per_poll"]
     ratios = out["cadenced_reference_over_default"]
-    assert set(ratios["250ms"]) == {"plain", "tls"} and set(ratios["1s"]) == {"plain", "tls", "hot_endpoints"}
+    assert set(ratios["250ms"]) == {"plain", "tls"}
+    assert set(ratios["1s"]) == {"plain", "hot_endpoints", "wan_sqs2ms_kube1ms"}
     assert set(ratios["250ms_by_tracked_queues"]) == {"1", "2", "4", "8"}
 
 
