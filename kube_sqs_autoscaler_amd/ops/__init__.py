@@ -70,7 +70,11 @@ def fakes() -> ModuleType:
     global _fakes
     if _fakes is not None:
         return _fakes
-    native()
+    if not native().HTTP_TIMING and _sources_present():
+        # a dev tree running the image build (-DKSA_HTTP_TIMING=0): the attribution rows would
+        # come out empty (an image has no sources and no fakes: the import below says so)
+        raise NativeUnavailable("the loaded _ksa_native is the image build (no HTTP timing, no test doubles); "
+                                "rebuild the dev module: python -m kube_sqs_autoscaler_amd.ops.build")
     with _lock:
         if _fakes is not None:
             return _fakes

@@ -43,6 +43,11 @@ BUILD = ROOT / "build"
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 NATIVE_SO = OPS / f"_ksa_native{EXT_SUFFIX}"
 FAKES_SO = OPS / f"_ksa_fakes{EXT_SUFFIX}"
+# Written next to the in-tree _ksa_native by build_image_runtime (the timing-less image build);
+# removed by build_native. Its presence makes native_up_to_date() false, so a dev tree that ran
+# `build --image` gets the release module back on the next native() instead of running tests and
+# benchmarks without HTTP timing.
+IMAGE_STAMP = OPS / "_ksa_native.image-build"
 GPU_SO = OPS / "libksa_gpu.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
@@ -148,7 +153,7 @@ def native_up_to_date() -> bool:
     module and the sources alone, not the object files: ``build/`` does not travel with the tree
     (a GPU box gets the built module and no objects), and a process there must not recompile a
     module that is current -- least of all several ranks at once."""
-    return NATIVE_SO.exists() and NATIVE_SO.stat().st_mtime >= _newest_source(
+    return NATIVE_SO.exists() and not IMAGE_STAMP.exists() and NATIVE_SO.stat().st_mtime >= _newest_source(
         [CSRC / "core", CSRC / "sim"], [CSRC / "bindings" / "module.cc"])
 
 
@@ -162,6 +167,7 @@ def build_native(jobs: int = 8, verbose: bool = True) -> Path:
     """Builds the production pybind11 extension in place; returns its path."""
     core = _compile_objects("release", RELEASE_FLAGS, _core_sources(), jobs)
     _link(NATIVE_SO, core + [_binding_object("module")], verbose)
+    IMAGE_STAMP.unlink(missing_ok=True)
     return NATIVE_SO
 
 
@@ -176,6 +182,7 @@ def build_image_runtime(jobs: int = 8, verbose: bool = True, out: Path = NATIVE_
     os.replace(tmp, out)
     if out == NATIVE_SO:
         FAKES_SO.unlink(missing_ok=True)
+        IMAGE_STAMP.write_text("-DKSA_HTTP_TIMING=0\n")
     if verbose:
         print(f"[build] linked {out} (image: -DKSA_HTTP_TIMING=0, no _ksa_fakes)")
     return out

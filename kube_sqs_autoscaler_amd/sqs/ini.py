@@ -14,8 +14,10 @@ only on what the SDK's lexer cannot get past either -- a section header without 
 * lines that are neither a comment, a section header nor a ``key = value`` / ``key: value``
   assignment.
 
-Accepted, as before: ``#`` / ``;`` comment lines, blank lines, indented continuation lines
-(appended to the previous value with a newline, as in the SDK's nested ``s3 =`` blocks), repeated
+Accepted, as before: ``#`` / ``;`` comment lines, blank lines, continuation lines -- indented
+deeper than their key's line, as configparser reads them -- (appended to the previous value with
+a newline, as in the SDK's nested ``s3 =`` blocks; keys and headers indented alike are read as
+keys and headers), repeated
 sections (merged) and keys (the last wins). Keys are lower-cased; inline ``;``/``#`` text after a
 value is part of the value (neither parser strips it). Fixtures: tests/test_session.py.
 """
@@ -54,12 +56,17 @@ def parse(text: str, path: str = "") -> IniFile:
     where = path or "<string>"
     section: Optional[Dict[str, str]] = None
     last_key: Optional[str] = None
+    key_indent = 0  # leading whitespace of last_key's line
     for n, raw in enumerate(text.splitlines(), 1):
         line = raw.strip()
         if not line or line[0] in "#;":
             continue
-        if raw[:1] in (" ", "\t") and section is not None and last_key is not None:
-            section[last_key] += "\n" + line  # continuation of the previous value
+        indent = len(raw) - len(raw.lstrip())
+        if indent > key_indent and section is not None and last_key is not None:
+            # a continuation of the previous value: indented deeper than its key line (as
+            # configparser reads it), so a file whose keys are all indented alike is still read
+            # key by key
+            section[last_key] += "\n" + line
             continue
         if line.startswith("["):
             end = line.find("]")
@@ -81,7 +88,7 @@ def parse(text: str, path: str = "") -> IniFile:
         i = min(seps)
         key = line[:i].strip().lower()
         section[key] = line[i + 1:].strip()
-        last_key = key
+        last_key, key_indent = key, indent
     return out
 
 

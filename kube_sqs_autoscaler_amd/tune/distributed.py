@@ -35,8 +35,11 @@ from . import closedloop, sweep
 def config_costs(params: np.ndarray, horizon_ns: int, latency_ns: Tuple[int, int, int]) -> np.ndarray:
     """Per-configuration simulated polls (the unit :func:`sweep.estimated_polls` sums): the work
     of one lane is proportional to it, whatever its other parameters."""
-    step = np.maximum(np.maximum(params[0], 0) + latency_ns[0], 1)
-    return np.minimum(horizon_ns // step, 1 << 26).astype(np.int64)
+    # the poll period clipped to the horizon first: a huge period from a user grid must cost one
+    # poll, not wrap negative in int64 when the latency is added (and cost horizon polls)
+    period = np.clip(np.asarray(params[0], dtype=np.int64), 0, max(int(horizon_ns), 0))
+    step = np.maximum(period + min(max(int(latency_ns[0]), 0), max(int(horizon_ns), 0)), 1)
+    return np.maximum(np.minimum(horizon_ns // step, 1 << 26), 0).astype(np.int64)
 
 
 def shard_plan(costs: np.ndarray, world: int) -> List[np.ndarray]:

@@ -173,3 +173,18 @@ def test_package_uses_only_pyyaml_api_present_in_ubuntu_2204():
                 with open(os.path.join(dirpath, fn)) as f:
                     used |= set(re.findall(r"\byaml\.(\w+)", f.read()))
     assert used and used <= allowed, used - allowed
+
+
+def test_an_in_tree_image_build_is_replaced_by_the_release_module(monkeypatch, tmp_path):
+    """`ops.build --image` writes the timing-less module over the in-tree one. Its
+    stamp makes native_up_to_date() false, so the next native() rebuilds the release module; the
+    stamp goes with that rebuild."""
+    from kube_sqs_autoscaler_amd.ops import build
+
+    stamp = tmp_path / "stamp"
+    monkeypatch.setattr(build, "IMAGE_STAMP", stamp)
+    assert build.native_up_to_date()
+    stamp.write_text("-DKSA_HTTP_TIMING=0\n")
+    assert not build.native_up_to_date()
+    build.build_native(verbose=False)  # objects are current: a relink
+    assert not stamp.exists() and build.native_up_to_date()

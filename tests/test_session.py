@@ -285,3 +285,29 @@ def test_shared_file_reader_fails_only_on_an_unclosed_section_header():
                 assert k == k.lower()
 
     check()
+
+
+def test_indented_keys_and_headers_are_keys_and_headers():
+    """a line continues the previous value only when indented deeper than that key's
+    line (configparser's rule), so a file whose keys (or headers) are indented alike parses key by
+    key; the SDK's nested ``s3 =`` block still folds into its key."""
+    from kube_sqs_autoscaler_amd.sqs import ini
+
+    f = ini.parse("[default]\n  aws_access_key_id = A\n  aws_secret_access_key = B\n"
+                  "  [profile x]\n  region = eu-west-1\n  s3 =\n    max_concurrent_requests = 20\n"
+                  "    addressing_style = path\n  output = json\n", "f")
+    assert dict(f.items("default")) == {"aws_access_key_id": "A", "aws_secret_access_key": "B"}
+    assert dict(f.items("profile x")) == {"region": "eu-west-1", "output": "json",
+                                          "s3": "\nmax_concurrent_requests = 20\naddressing_style = path"}
+    # unindented keys: an indented line is a continuation, as before
+    g = ini.parse("[default]\nkey = a\n  b\nother = c\n", "g")
+    assert dict(g.items("default")) == {"key": "a\nb", "other": "c"}
+
+
+def test_indented_credentials_file_feeds_the_chain(tmp_path):
+    from kube_sqs_autoscaler_amd.sqs.credentials import SharedFileProvider
+
+    p = tmp_path / "credentials"
+    p.write_text("[default]\n  aws_access_key_id = AKIDINDENT\n  aws_secret_access_key = SECRETINDENT\n")
+    c = SharedFileProvider({"AWS_SHARED_CREDENTIALS_FILE": str(p), "HOME": str(tmp_path)}).fetch()
+    assert c.access_key_id == "AKIDINDENT" and c.secret_access_key == "SECRETINDENT"

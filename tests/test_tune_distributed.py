@@ -123,3 +123,13 @@ def test_shard_plan_imbalance_is_at_most_one_configuration():
             assert max(loads) - min(loads) <= int(c.max())
 
     check()
+
+
+def test_config_costs_do_not_wrap_on_huge_periods():
+    """a poll period near int64's max plus the latency wrapped negative, was clamped
+    to a step of 1 and costed at horizon polls; clipped to the horizon it costs what it is, at
+    most one poll."""
+    horizon = 24 * 3600 * 10**9
+    params = np.array([[5 * 10**9, np.iinfo(np.int64).max - 10, horizon * 2, 0]], dtype=np.int64)
+    costs = config_costs(params, horizon, (10**6, 10**6, 10**6))
+    assert costs.tolist() == [horizon // (5 * 10**9 + 10**6), 0, 0, min(horizon // 10**6, 1 << 26)]
