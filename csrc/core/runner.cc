@@ -90,7 +90,14 @@ IterationRecord Runner::step(StopFlag* stop) {
     slept = clock_->sleep(period - w, stop);
     if (slept) {
       warm(due, true);
-      slept = clock_->spin_until(due, stop);
+      // Spin to the due time only for a near SQS endpoint (an answer within
+      // HttpClient::kMaxSpinThrough, or none measured yet): its poll is short enough for an awake
+      // core with warm caches to show. Against a remote endpoint (milliseconds) that saving is
+      // noise while the spin would be most of the poll's CPU: the warm-up's work is done, and the
+      // thread sleeps out the rest of the lead.
+      const Nanos ewma = sqs_->api()->response_ewma();
+      slept = ewma <= HttpClient::kMaxSpinThrough ? clock_->spin_until(due, stop)
+                                                  : clock_->sleep(due - clock_->now(), stop);
     }
   } else {
     slept = clock_->sleep(period, stop);

@@ -55,11 +55,14 @@ struct LoopConfig {
   bool prefetch_always = false;
   // Pre-poll warm-up (--poll-prewarm): wake this long before a poll is due, do what the poll
   // would do first without sending anything -- credentials, the signed SQS request for that
-  // second, the bearer token, both connections checked (or dialled) -- then spin until the due
-  // time, so the poll starts on time on an awake core with its code and data in cache. The
-  // poll itself, and so every decision, is unchanged (sleep-then-poll, main.go:41); the cost is
-  // up to `prewarm` of CPU per poll. 0 disables. With a poll period under 2x `prewarm` the
-  // preparation runs at the due time instead, without the early wake-up.
+  // second, the bearer token, both connections checked (or dialled) -- then, for a near SQS
+  // endpoint (response EWMA within HttpClient::kMaxSpinThrough), spin until the due time, so the
+  // poll starts on time on an awake core with its code and data in cache; against a remote one
+  // sleep out the rest of the lead (the spin would cost more CPU than the poll and save noise).
+  // The poll itself, and so every decision, is unchanged (sleep-then-poll, main.go:41); the cost
+  // is up to `prewarm` of CPU per poll of a near endpoint, the warm-up's own work otherwise.
+  // 0 disables. With a poll period under 2x `prewarm` the preparation runs at the due time
+  // instead, without the early wake-up.
   Nanos prewarm = 0;
   // With the early wake-up, also pre-send the SQS request (HttpClient::stage; --poll-presend,
   // off by default): all but its last bytes are handed to the kernel corked, so the kernel's send

@@ -56,6 +56,8 @@ class SqsApi {
   virtual std::string timing_json() const { return ""; }
   // HttpClient::set_spin_budget of the client's connection. Default: nothing.
   virtual void set_spin_budget(Nanos ns) { (void)ns; }
+  // The endpoint's response-time EWMA (HttpClient::rtt_ewma); -1: unknown (no sample, or not HTTP).
+  virtual Nanos response_ewma() const { return -1; }
   // Pre-poll warm-up (Runner prewarm), just before a call due at unix time `at_unix_ns`: do
   // now what the call would otherwise do first -- credentials, the request and its signature
   // for that second, the connection check or dial -- and, with `presend`, hand all but the
@@ -116,6 +118,7 @@ class alignas(kCacheLine) HttpSqsApi final : public SqsApi {
   void set_spin_budget(Nanos ns) override {
     if (http_) http_->set_spin_budget(ns);
   }
+  Nanos response_ewma() const override { return http_ ? http_->rtt_ewma() : -1; }
   // Diagnostics: time each call -- credentials + signing, the HTTP phases (HttpTiming), the
   // response parse -- for timing_json().
   void set_timing(bool on) {
