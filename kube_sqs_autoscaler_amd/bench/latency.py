@@ -590,7 +590,8 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
         setup["autoscaler_threads"] = thread_count()
         if after:
             setup["endpoint_threads"] = [s.get("threads", 0) for s in after]
-            setup["endpoint_cpu_us_per_request"] = [
+            # (hot endpoints busy-poll: their CPU is the whole run's, not per request)
+            setup["endpoint_cpu_us_per_request"] = None if hot_endpoints else [
                 round((a["cpu_ns"] - b["cpu_ns"]) / 1e3 / max(1, a["sqs_requests"] + a["kube_requests"]
                                                               - b["sqs_requests"] - b["kube_requests"]), 2)
                 for a, b in zip(after, before)]
