@@ -580,7 +580,10 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
                    sqs_latency_ns=sqs_latency_ns, kube_latency_ns=kube_latency_ns)
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: Dict[str, List[dict]] = {a: [] for a in names}
-    setup = {"cpus_available": len(os.sched_getaffinity(0))}
+    quota, quota_period = env.nat.read_cpu_quota()
+    # the CPUs this process may run on, and the cgroup's CPU bandwidth (cores' worth; None: no limit)
+    setup = {"cpus_available": len(os.sched_getaffinity(0)),
+             "cpu_quota_cores": round(quota / quota_period, 2) if quota else None}
     try:
         for r, f in zip(env.runners, files):
             r.set_trace_fd(f.fileno())
