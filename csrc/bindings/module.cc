@@ -730,6 +730,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("prefetch_always", &LoopConfig::prefetch_always)
       .def_readwrite("prewarm_ns", &LoopConfig::prewarm)
       .def_readwrite("presend", &LoopConfig::presend)
+      .def_readwrite("prewarm_spin", &LoopConfig::prewarm_spin)
       .def_readwrite("connect_at_start", &LoopConfig::connect_at_start)
       .def_readwrite("spin_budget_ppm", &LoopConfig::spin_budget_ppm);
 

@@ -96,8 +96,8 @@ IterationRecord Runner::step(StopFlag* stop) {
       // noise while the spin would be most of the poll's CPU: the warm-up's work is done, and the
       // thread sleeps out the rest of the lead.
       const Nanos ewma = sqs_->api()->response_ewma();
-      slept = ewma <= HttpClient::kMaxSpinThrough ? clock_->spin_until(due, stop)
-                                                  : clock_->sleep(due - clock_->now(), stop);
+      slept = cfg_.prewarm_spin && ewma <= HttpClient::kMaxSpinThrough ? clock_->spin_until(due, stop)
+                                                                       : clock_->sleep(due - clock_->now(), stop);
     }
   } else {
     slept = clock_->sleep(period, stop);

@@ -64,6 +64,9 @@ struct LoopConfig {
   // 0 disables. With a poll period under 2x `prewarm` the preparation runs at the due time
   // instead, without the early wake-up.
   Nanos prewarm = 0;
+  // After the warm-up, spin to the due time when the SQS endpoint is near (above); false: always
+  // sleep out the rest of the lead (the A/B knob of scripts/spin_arms.py).
+  bool prewarm_spin = true;
   // With the early wake-up, also pre-send the SQS request (HttpClient::stage; --poll-presend,
   // off by default): all but its last bytes are handed to the kernel corked, so the kernel's send
   // path has run before the due time and the poll's own write runs warm; nothing reaches the wire

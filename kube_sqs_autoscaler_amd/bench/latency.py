@@ -225,7 +225,8 @@ class BenchEnv:
     loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
     period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
     ``presend``: stage each poll's SQS request during the warm-up (LoopConfig.presend; the CLI's
-    --poll-presend, off by default);
+    --poll-presend, off by default); ``prewarm_spin``: spin to the due time after the warm-up for
+    a near endpoint (LoopConfig.prewarm_spin);
     these, ``busy_poll_ns``, ``mode`` and ``pipeline`` may be lists, one value per queue, cycled
     (paired comparisons within one run: :func:`measure_cadenced_arms`). ``timing``: the clients time every request's
     phases (HttpTiming), traced polls carry the breakdown (``detail``), and the fakes record each
@@ -235,7 +236,7 @@ class BenchEnv:
                  kube_latency_ns: int = 0, log_fd: Optional[int] = None, pipeline: bool = True,
                  busy_poll_ns: int = 0, servers: str = "shared", log_level: str = "info", sqs_protocol: str = "query",
                  poll_period_ns: int = 0, stagger: bool = False, hot_endpoints: bool = False, prewarm_ns: int = 0,
-                 timing: bool = False, spin_budget_ppm=None, presend=False):
+                 timing: bool = False, spin_budget_ppm=None, presend=False, prewarm_spin=True):
         nat = native()
         self.nat = nat
         self.mode = mode
@@ -314,6 +315,7 @@ class BenchEnv:
             cfg.prefetch = pipeline_q
             cfg.prewarm_ns = pw_q
             cfg.presend = per_queue(presend, q)
+            cfg.prewarm_spin = per_queue(prewarm_spin, q)
             # the CLI's share (autoscaler.loop_config) unless given
             cfg.spin_budget_ppm = (SPIN_BUDGET_PPM // queues if spin_budget_ppm is None
                                    else per_queue(spin_budget_ppm, q))
@@ -549,7 +551,7 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     branch predictors are cold, the CPU may sit in a deep idle state, and a keep-alive
     connection unused for longer than ``kFreshConnNs`` gets the idle-close check again. The
     hot-loop rows measure none of that. Here every arm (``name -> dict(mode, pipeline,
-    busy_poll_ns, prewarm_ns[, presend])``) gets ``queues_per_arm`` queues; queue q runs arm q % len(arms),
+    busy_poll_ns, prewarm_ns[, presend, prewarm_spin, spin_budget_ppm])``) gets ``queues_per_arm`` queues; queue q runs arm q % len(arms),
     so the arms' queues interleave in one fleet (a thread each, starts staggered over the
     period) and run ``polls`` polls at ``poll_period_ns`` in the same run, against the same
     ``split`` endpoints (one fake SQS process and one apiserver process serving every queue, as
@@ -576,7 +578,8 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
                    hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,
-                   spin_budget_ppm=SPIN_BUDGET_PPM // queues_per_arm, presend=col("presend", False),
+                   spin_budget_ppm=col("spin_budget_ppm", SPIN_BUDGET_PPM // queues_per_arm),
+                   presend=col("presend", False), prewarm_spin=col("prewarm_spin", True),
                    sqs_latency_ns=sqs_latency_ns, kube_latency_ns=kube_latency_ns)
     files = [tempfile.TemporaryFile() for _ in env.runners]
     spans: Dict[str, List[dict]] = {a: [] for a in names}

@@ -1,0 +1,51 @@
+"""What the CLI's spinning buys at a production cadence, and what it costs in CPU.
+
+Three spins sit on the default poll path: the pre-poll warm-up's spin to the due time
+(LoopConfig.prewarm_spin, near endpoints only), the busy-poll window on every read
+(--busy-poll, 25 us) and the spin through a near endpoint's answer within the 1 % budget
+(LoopConfig.spin_budget_ppm). Each arm drops some of them; all arms share one run (queue q runs
+arm q % arms, starts staggered over the period, one fake SQS and one fake apiserver process), so
+the box's idle-state drift does not land between them. One JSON line per arm, period and endpoint
+kind: poll->patch p50/p90 and the worker's CPU per poll (the spans' thread CPU time).
+
+    python scripts/spin_arms.py --period-ms 1000 --polls 27 --queues 8
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced_arms  # noqa: E402
+from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS  # noqa: E402
+
+MS = 1_000_000
+BASE = dict(mode="scale", pipeline=True, busy_poll_ns=25_000, prewarm_ns=DEFAULT_POLL_PREWARM_NS)
+ARMS = {
+    "default": BASE,
+    "no_prewarm_spin": dict(BASE, prewarm_spin=False),
+    "no_spin_budget": dict(BASE, spin_budget_ppm=0),
+    "window_only": dict(BASE, prewarm_spin=False, spin_budget_ppm=0),
+    "no_spin": dict(BASE, prewarm_spin=False, spin_budget_ppm=0, busy_poll_ns=0),
+}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--period-ms", type=int, nargs="+", default=[250, 1000])
+    ap.add_argument("--polls", type=int, default=27, help="polls per queue (the first two are dropped)")
+    ap.add_argument("--queues", type=int, default=8, help="queues per arm")
+    a = ap.parse_args()
+    for period in a.period_ms:
+        for hot in (False, True):
+            res = measure_cadenced_arms(period * MS, a.polls, a.queues, ARMS, hot_endpoints=hot)
+            for name, r in res.items():
+                print(json.dumps({"arm": name, "period_ms": period, "hot_endpoints": hot, "queues": a.queues,
+                                  **{k: r.get(k) for k in ("p50_ms", "p90_ms", "samples", "cpu_ms_per_poll",
+                                                           "cpu_ms_per_poll_p50", "phase_median_us")}}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
