@@ -26,6 +26,7 @@
 #include <thread>
 #include <vector>
 
+#include "../core/affinity.h"
 #include "../core/clock.h"
 #include "../core/exec_auth.h"
 #include "../fakes/fakes.h"
@@ -1016,6 +1017,85 @@ TEST(exec_provider_shared_across_threads) {
   std::remove((std::string(dir) + "/runs").c_str());
   std::remove(script.c_str());
   rmdir(dir);
+}
+
+// One credential source shared by 16 clients' caches on 16 threads (the CLI's 16 tracked
+// queues): the inner provider runs once per expiry, whatever the concurrency, and a stale report
+// about an older set is ignored (TSan target: the caches and the shared copy under their locks).
+TEST(shared_credentials_one_fetch_per_expiry) {
+  struct Counting final : CredentialsProvider {
+    std::atomic<int> calls{0};
+    std::atomic<int64_t>* now;
+    Result<Credentials> retrieve() override {
+      const int n = ++calls;
+      Credentials c;
+      c.access_key_id = "AKID";
+      c.secret_access_key = "secret";
+      c.session_token = "tok-" + std::to_string(n);
+      c.expires_unix_ns = now->load() + 600 * kSecond;
+      return Result<Credentials>::Ok(c);
+    }
+  };
+  std::atomic<int64_t> now{1700000000LL * kSecond};
+  auto inner = std::make_shared<Counting>();
+  inner->now = &now;
+  auto shared = std::make_shared<SharedCredentialsProvider>(inner, [&now] { return now.load(); }, 300 * kSecond);
+  std::vector<std::unique_ptr<CachedCredentials>> caches;
+  for (int i = 0; i < 16; ++i) caches.push_back(std::make_unique<CachedCredentials>(shared, 300 * kSecond));
+  auto round = [&](const std::string& want) {
+    std::atomic<int> good{0};
+    std::vector<std::thread> ts;
+    for (int i = 0; i < 16; ++i)
+      ts.emplace_back([&, i] {
+        for (int k = 0; k < 50; ++k) {
+          auto r = caches[i]->get(now.load());
+          if (r.ok() && r.value.session_token == want) ++good;
+        }
+      });
+    for (auto& t : ts) t.join();
+    CHECK_EQ(good.load(), 16 * 50);
+  };
+  round("tok-1");
+  CHECK_EQ(inner->calls.load(), 1);
+  now += 301 * kSecond;  // 299 s left: every cache is in its refresh window
+  round("tok-2");
+  CHECK_EQ(inner->calls.load(), 2);
+  caches[3]->invalidate();  // ExpiredToken on one client: one re-fetch for all
+  auto r = caches[3]->get(now.load());
+  CHECK(r.ok() && r.value.session_token == "tok-3");
+  CHECK_EQ(inner->calls.load(), 3);
+  caches[5]->invalidate();  // a late report about tok-2 (already replaced): no fetch
+  r = caches[5]->get(now.load());
+  CHECK(r.ok() && r.value.session_token == "tok-3");
+  CHECK_EQ(inner->calls.load(), 3);
+  CHECK_EQ(shared->fetches(), uint64_t(3));
+}
+
+// HttpClient::spin_window_for: no answer slower than kMaxSpinThrough is ever spun for, and no
+// spin exceeds it, whatever the budget.
+TEST(spin_window_ceiling) {
+  const Nanos us = kMicrosecond;
+  CHECK_EQ(HttpClient::spin_window_for(25 * us, 15000 * us, 37500 * us), Nanos(0));
+  CHECK_EQ(HttpClient::spin_window_for(25 * us, 201 * us, kSecond), Nanos(0));
+  CHECK_EQ(HttpClient::spin_window_for(25 * us, 150 * us, kSecond), HttpClient::kMaxSpinThrough);
+  CHECK_EQ(HttpClient::spin_window_for(25 * us, 40 * us, 80 * us), 80 * us);
+  CHECK_EQ(HttpClient::spin_window_for(25 * us, 40 * us, 79 * us), 25 * us);
+  for (Nanos bp : {Nanos(0), 25 * us, 300 * us})
+    for (Nanos ewma = -1; ewma < 20 * kMillisecond; ewma += 7 * us)
+      CHECK(HttpClient::spin_window_for(bp, ewma, kSecond) <= std::max(bp, HttpClient::kMaxSpinThrough));
+}
+
+TEST(cgroup_cpu_quota_parsers) {
+  CHECK(!parse_cpu_max("max 100000").limited());
+  CpuQuota q = parse_cpu_max("10000 100000\n");
+  CHECK(q.limited() && q.quota_ns == 10 * kMillisecond && q.period_ns == 100 * kMillisecond);
+  CHECK(!parse_cpu_max("").limited() && !parse_cpu_max("x y").limited() && !parse_cpu_max("0 100000").limited());
+  CHECK(!parse_cfs_quota("-1\n", "100000\n").limited());
+  CHECK(parse_cfs_quota("50000\n", "100000\n").quota_ns == 50 * kMillisecond);
+  LoopConfig lc;
+  lc.poll_period = 5 * kSecond;
+  CHECK_EQ(Runner::spin_budget_for(lc, CpuQuota()), 50 * kMillisecond);
+  CHECK_EQ(Runner::spin_budget_for(lc, q), kMillisecond);
 }
 
 }  // namespace
