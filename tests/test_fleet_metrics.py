@@ -96,6 +96,9 @@ def test_metrics_endpoints(nat):
             assert all(a[1] <= b[1] for a, b in zip(buckets, buckets[1:]))
             assert metric["ksa_poll_to_patch_latency_seconds_count"] == 10
             assert metric["ksa_poll_to_patch_latency_seconds_sum"] == metric["ksa_poll_to_patch_seconds_sum"] > 0
+            # the worker thread's CPU over its 10 polls (runner.h IterationRecord::cpu_ns)
+            assert "# TYPE ksa_poll_cpu_seconds_total counter" in body
+            assert 0 < metric["ksa_poll_cpu_seconds_total"] < 10 * 0.05
             assert urllib.request.urlopen(base + "/readyz").read() == b"ok"
             assert urllib.request.urlopen(base + "/healthz").status == 200
         finally:

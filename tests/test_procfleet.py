@@ -81,6 +81,7 @@ def test_fleet_mirrors_stats_latencies_and_max_override(nat, servers):
         assert [s["polls"] for s in st] == [8, 8] and [s["scale_ups"] for s in st] == [8, 1]
         assert kube.replicas("gpu", "w0") == 12 and kube.replicas("gpu", "w1") == 5
         assert len(fleet.workers[0].runner.latencies()) == 8 and st[0]["latency_samples"] == 8
+        assert all(s["poll_cpu_ns"] > 0 for s in st)  # each worker process's poll CPU, through its slot
         assert all(v > 0 for v in fleet.workers[0].runner.latencies())
         assert st[0]["latency_sum_ns"] == sum(fleet.workers[0].runner.latencies())
     finally:
