@@ -796,6 +796,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         d["consecutive_failed_polls"] = s.consecutive_failed_polls;
         return d;
       })
+      .def("prewarm_spin_budget", &Runner::prewarm_spin_budget)
+      .def("set_spin_budget", &Runner::set_spin_budget)
       .def("idle_ns", &Runner::idle_ns)
       .def("failing_ns", &Runner::failing_ns)
       .def("last_error", &Runner::last_error)

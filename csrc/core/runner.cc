@@ -95,9 +95,12 @@ IterationRecord Runner::step(StopFlag* stop) {
       // core with warm caches to show. Against a remote endpoint (milliseconds) that saving is
       // noise while the spin would be most of the poll's CPU: the warm-up's work is done, and the
       // thread sleeps out the rest of the lead.
+      // The spin is the end of the lead, within the warm-up's share of the poll's spin budget.
       const Nanos ewma = sqs_->api()->response_ewma();
-      slept = cfg_.prewarm_spin && ewma <= HttpClient::kMaxSpinThrough ? clock_->spin_until(due, stop)
-                                                                       : clock_->sleep(due - clock_->now(), stop);
+      const Nanos rest = due - clock_->now();
+      Nanos spin = cfg_.prewarm_spin && ewma <= HttpClient::kMaxSpinThrough ? rest : 0;
+      if (prewarm_spin_budget_ >= 0) spin = std::min(spin, prewarm_spin_budget_);
+      slept = clock_->sleep(rest - spin, stop) && clock_->spin_until(due, stop);
     }
   } else {
     slept = clock_->sleep(period, stop);
@@ -458,9 +461,9 @@ Nanos Runner::spin_budget_for(const LoopConfig& cfg, const CpuQuota& quota) {
 }
 
 void Runner::run(StopFlag* stop, int64_t max_iterations, Nanos start_delay) {
-  // This thread is the worker's own: its clients may spin through a near endpoint's answer
-  // within a share of the poll period (LoopConfig::spin_budget_ppm; a back-to-back loop keeps
-  // the window), capped by the process's CPU limit.
+  // This thread is the worker's own: it may spin before the due time and through a near
+  // endpoint's answer within a share of the poll period (LoopConfig::spin_budget_ppm; a
+  // back-to-back loop keeps the window), capped by the process's CPU limit.
   static const CpuQuota quota = read_cpu_quota();  // once per process
   set_spin_budget(spin_budget_for(cfg_, quota));
   if (start_delay > 0 && !clock_->sleep(start_delay, stop)) return;

@@ -59,8 +59,9 @@ struct LoopConfig {
   // endpoint (response EWMA within HttpClient::kMaxSpinThrough), spin until the due time, so the
   // poll starts on time on an awake core with its code and data in cache; against a remote one
   // sleep out the rest of the lead (the spin would cost more CPU than the poll and save noise).
-  // The poll itself, and so every decision, is unchanged (sleep-then-poll, main.go:41); the cost
-  // is up to `prewarm` of CPU per poll of a near endpoint, the warm-up's own work otherwise.
+  // The spin is the last part of the lead, at most the warm-up's quarter of the poll's spin
+  // budget (Runner::set_spin_budget); the part before it is slept. The poll itself, and so every
+  // decision, is unchanged (sleep-then-poll, main.go:41).
   // 0 disables. With a poll period under 2x `prewarm` the preparation runs at the due time
   // instead, without the early wake-up.
   Nanos prewarm = 0;
@@ -261,16 +262,21 @@ class alignas(kCacheLine) Runner {
     sqs_->cancel();
     scaler_->cancel();
   }
-  // Splits one poll's spin budget over the requests a poll makes (HttpClient::set_spin_budget
-  // applies per request): three quarters to the SQS call, an eighth to each of the apiserver's
-  // GET and write, so a scaling poll spins at most `ns` in total. The SQS answer is the one slow
-  // enough to need the budget (at a cadence its EWMA is past 4x the busy-poll window); the
-  // apiserver's answers mostly come within the window, which needs none. (An SDK retry of the
-  // SQS call spins within its own share again; retries are the error path.)
+  // Splits one poll's spin budget over what a poll spins for: a quarter to the warm-up's spin
+  // to the due time, half to the SQS call's read, an eighth to each of the apiserver's GET and
+  // write (HttpClient::set_spin_budget applies per request), so a scaling poll spins at most
+  // `ns` in total. The SQS answer is the one slow enough to need a read budget (at a cadence its
+  // EWMA is past 4x the busy-poll window); the apiserver's answers mostly come within the window,
+  // which needs none. (An SDK retry of the SQS call spins within its own share again; retries
+  // are the error path.)
   void set_spin_budget(Nanos ns) {
-    sqs_->api()->set_spin_budget(ns / 4 * 3);
+    prewarm_spin_budget_ = ns / 4;
+    sqs_->api()->set_spin_budget(ns / 2);
     scaler_->api()->set_spin_budget(ns / 8);
   }
+  // The warm-up's share: the spin before the due time is at most this (the rest of the lead is
+  // slept). -1 (before set_spin_budget, e.g. a harness calling step() itself): the whole lead.
+  Nanos prewarm_spin_budget() const { return prewarm_spin_budget_; }
   // The spin budget run() gives a poll: LoopConfig::spin_budget_ppm of the poll period, and
   // under a cgroup CPU limit at most a tenth of one CFS period's quota (times this queue's share).
   static Nanos spin_budget_for(const LoopConfig& cfg, const CpuQuota& quota);
@@ -322,6 +328,7 @@ class alignas(kCacheLine) Runner {
   void warm(Nanos due, bool presend = false);
   void record(IterationRecord& r);
   int64_t cpu_from_ = -1;  // thread CPU time at the start of the iteration in progress
+  Nanos prewarm_spin_budget_ = -1;
   void mirror(const IterationRecord& r);
   CpuList cpus_;
   SharedWorkerState* shared_ = nullptr;

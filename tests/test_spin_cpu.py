@@ -113,3 +113,33 @@ def test_spin_budget_capped_by_the_cpu_quota(nat):
     assert nat.runner_spin_budget(cfg, 10_000_000, 100_000_000) == 62_500
     cfg.poll_period_ns = 0
     assert nat.runner_spin_budget(cfg, 10_000_000, 100_000_000) == 0
+
+
+def test_runner_splits_the_poll_spin_budget(nat):
+    """Runner::set_spin_budget: a quarter of the poll's budget to the warm-up's spin (the rest of
+    its lead is slept), half to the SQS read, an eighth to each apiserver request."""
+    from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
+
+    env = BenchEnv(1)
+    try:
+        r = env.runners[0]
+        assert r.prewarm_spin_budget() == -1  # never set: a harness's step() spins the whole lead
+        r.set_spin_budget(400_000)
+        assert r.prewarm_spin_budget() == 100_000
+    finally:
+        env.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ppm,spins", [(10_000, False), (1_000_000, True)])
+def test_warm_up_spin_stays_within_the_budget(nat, ppm, spins):
+    """A 2 ms warm-up lead at a 20 ms period: with the CLI's 1 % (200 us per poll, 50 us of it for
+    the warm-up) the worker sleeps most of the lead and spins its last 50 us; with the whole
+    period as budget it spins the whole lead, 2 ms of CPU per poll."""
+    from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced_arms
+
+    arm = dict(mode="scale", pipeline=True, busy_poll_ns=25_000, prewarm_ns=2_000_000, spin_budget_ppm=ppm)
+    r = measure_cadenced_arms(20_000_000, 12, 1, {"a": arm}, servers="shared")["a"]
+    assert r["samples"] >= 8
+    cpu = r["cpu_ms_per_poll_p50"]
+    assert (cpu > 1.5) if spins else (cpu < 1.0), r
