@@ -165,8 +165,8 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
                             for name, r in res.items()))
     if skipped:
         _progress(f"cadence rows skipped (past --extras-budget-s): {skipped}")
-    wan_row = {k[len(""):]: v for k, v in p50.get("1s", {}).items() if k.endswith("_wan_sqs2ms_kube1ms")}
-    wan_p50 = {k.replace("_wan_sqs2ms_kube1ms", ""): v for k, v in wan_row.items()}
+    wan_p50 = {k[:-len("_wan_sqs2ms_kube1ms")]: v for k, v in p50.get("1s", {}).items()
+               if k.endswith("_wan_sqs2ms_kube1ms")}
     growth = {}
     for key, row in by_q.items():
         for name, v in row.items():
