@@ -36,12 +36,17 @@ def main() -> int:
     ap.add_argument("--period-ms", type=int, nargs="+", default=[250, 1000])
     ap.add_argument("--polls", type=int, default=27, help="polls per queue (the first two are dropped)")
     ap.add_argument("--queues", type=int, default=8, help="queues per arm")
+    ap.add_argument("--sqs-latency-ms", type=float, default=0.0, help="the fake SQS answers this much later")
+    ap.add_argument("--kube-latency-ms", type=float, default=0.0, help="the fake apiserver answers this much later")
+    ap.add_argument("--sleeping-only", action="store_true", help="skip the endpoints that never sleep")
     a = ap.parse_args()
+    lat = dict(sqs_latency_ns=int(a.sqs_latency_ms * MS), kube_latency_ns=int(a.kube_latency_ms * MS))
     for period in a.period_ms:
-        for hot in (False, True):
-            res = measure_cadenced_arms(period * MS, a.polls, a.queues, ARMS, hot_endpoints=hot)
+        for hot in (False,) if a.sleeping_only else (False, True):
+            res = measure_cadenced_arms(period * MS, a.polls, a.queues, ARMS, hot_endpoints=hot, **lat)
             for name, r in res.items():
                 print(json.dumps({"arm": name, "period_ms": period, "hot_endpoints": hot, "queues": a.queues,
+                                  "sqs_latency_ms": a.sqs_latency_ms, "kube_latency_ms": a.kube_latency_ms,
                                   **{k: r.get(k) for k in ("p50_ms", "p90_ms", "samples", "cpu_ms_per_poll",
                                                            "cpu_ms_per_poll_p50", "phase_median_us")}}), flush=True)
     return 0
