@@ -7,7 +7,7 @@ trip at the 5 s default period was spun through (about 13 ms of CPU per poll), e
 quota. Here the CLI polls a fake SQS that answers after 3 ms or 15 ms, at --poll-period=1s, with
 the default --busy-poll and with --busy-poll=0s, and the worker thread's CPU time per poll (the
 trace file's ``cpu_ns``, CLOCK_THREAD_CPUTIME_ID from the start of the iteration to the end of
-the poll) must agree within 10 % (medians over 7 polls, both runs at once). At 3 ms round 4 spun through every answer (2 x EWMA = 6 ms fits
+the poll) must agree within 10 % (medians over 2 x 7 polls, the arms run at once, in both orders). At 3 ms round 4 spun through every answer (2 x EWMA = 6 ms fits
 the 7.5 ms SQS share of 1 % of 1 s). The queue depth sits in the dead band (no apiserver call),
 so only the remote SQS answer is measured.
 """
@@ -41,13 +41,13 @@ def endpoints(nat, tmp_path):
     kube.stop()
 
 
-def _poll_cpu(endpoints, tmp_path, busy_poll: str, delay_s: float = 0.0, out: dict = None):
+def _poll_cpu(endpoints, tmp_path, busy_poll: str, delay_s: float = 0.0, out: dict = None, run: int = 0):
     from kube_sqs_autoscaler_amd.cli import main
 
     sqs, kube, env = endpoints
     time.sleep(delay_s)
     url = f"{sqs.url}/123/jobs-{busy_poll}"
-    trace = tmp_path / f"trace_{busy_poll}.jsonl"
+    trace = tmp_path / f"trace_{busy_poll}_{run}.jsonl"
     rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=w", f"--aws-region={REGION}",
                f"--sqs-endpoint={sqs.url}", "--poll-period=1s", "--attribute-names=ApproximateNumberOfMessages",
                f"--busy-poll={busy_poll}", f"--trace-file={trace}", "--log-level=error"],
@@ -61,29 +61,35 @@ def _poll_cpu(endpoints, tmp_path, busy_poll: str, delay_s: float = 0.0, out: di
 @pytest.mark.slow
 @pytest.mark.parametrize("latency_ms", [3, 15])
 def test_busy_poll_costs_no_cpu_against_a_remote_endpoint(nat, endpoints, tmp_path, latency_ms):
-    """The two CLI runs are paired: they run at once, the second half a period behind the first,
-    so a box's idle-state and clock drift (which moves the CPU time of the same work by tens of
-    %) lands on both alike."""
+    """The CLI runs are paired: two at once, the second half a period behind the first, then
+    again with the order swapped, so a box's idle-state and clock drift (which moves the CPU time
+    of the same work by tens of %) and whatever the first-started run pays land on both arms
+    alike (on the MI355X box a fixed order put +45 us on whichever arm started first,
+    profiles/r05c/)."""
     sqs, kube, _ = endpoints
     sqs.set_latency(latency_ms * 1_000_000)
     for arm in ("25us", "0s"):
         sqs.set_attributes(f"{sqs.url}/123/jobs-{arm}", {"ApproximateNumberOfMessages": "50"})  # the dead band
     kube.add_deployment("default", "w", 2)
-    cpu: dict = {}
-    runs = [threading.Thread(target=_poll_cpu, args=(endpoints, tmp_path, arm, delay, cpu))
-            for arm, delay in (("25us", 0.0), ("0s", 0.5))]
-    for t in runs:
-        t.start()
-    for t in runs:
-        t.join()
+    cpu = {"25us": [], "0s": []}
+    for run, order in enumerate((("25us", "0s"), ("0s", "25us"))):
+        got: dict = {}
+        runs = [threading.Thread(target=_poll_cpu, args=(endpoints, tmp_path, arm, delay, got, run))
+                for arm, delay in zip(order, (0.0, 0.5))]
+        for t in runs:
+            t.start()
+        for t in runs:
+            t.join()
+        for arm in order:
+            cpu[arm] += got[arm]
     default, off = cpu["25us"], cpu["0s"]
     assert kube.requests() == 0  # the dead band: the apiserver is never called
     print(json.dumps({"latency_ms": latency_ms, "cpu_ns_per_poll": {"busy_poll_25us": default, "busy_poll_0s": off}}))
     assert all(c > 0 for c in default + off)
     # A spin through the answer would cost >= latency_ms of CPU per poll; the arms' medians must
-    # agree within 10 % (plus 30 us of clock noise). Medians: one poll preempted on a loaded host
+    # agree within 10 % (plus 20 us of clock noise). Medians: one poll preempted on a loaded host
     # (xdist) costs a few hundred us in either arm.
-    assert statistics.median(default) <= 1.1 * statistics.median(off) + 30_000, (default, off)
+    assert statistics.median(default) <= 1.1 * statistics.median(off) + 20_000, (default, off)
     assert statistics.median(default) < latency_ms * 1_000_000 / 10, default
 
 
