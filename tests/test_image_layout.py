@@ -188,3 +188,14 @@ def test_an_in_tree_image_build_is_replaced_by_the_release_module(monkeypatch, t
     assert not build.native_up_to_date()
     build.build_native(verbose=False)  # objects are current: a relink
     assert not stamp.exists() and build.native_up_to_date()
+
+
+def test_fakes_refuse_an_image_build_of_the_runtime_in_a_dev_tree(monkeypatch, nat):
+    """A dev tree whose loaded _ksa_native is the image build (no HTTP timing) gets a clear error
+    from fakes() instead of attribution rows that come out empty."""
+    import kube_sqs_autoscaler_amd.ops as ops
+
+    monkeypatch.setattr(ops, "_fakes", None)
+    monkeypatch.setattr(ops.native(), "HTTP_TIMING", False)
+    with pytest.raises(ops.NativeUnavailable, match="image build"):
+        ops.fakes()
