@@ -455,7 +455,7 @@ Nanos Runner::spin_budget_for(const LoopConfig& cfg, const CpuQuota& quota) {
   const int64_t ppm = std::clamp<int64_t>(cfg.spin_budget_ppm, 0, 1000000);
   Nanos b = std::max<Nanos>(cfg.poll_period, 0) / 1000000 * ppm;
   // Under a CFS limit a poll spins at most a tenth of the quota of one CFS period (this queue's
-  // share of it: the CLI's 1 % split over the queues): 1 ms per poll under a 100m limit.
+  // share of it, as a 1 % budget split over the queues): 1 ms per poll under a 100m limit.
   if (quota.limited()) b = std::min<Nanos>(b, quota.quota_ns / 10 * std::min<int64_t>(ppm, 10000) / 10000);
   return b;
 }

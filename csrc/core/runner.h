@@ -84,15 +84,18 @@ struct LoopConfig {
   // instead of one shared arena. The CLI needs none: its first poll, or its first warm-up, dials
   // on the worker thread.
   bool connect_at_start = false;
-  // On a worker's own thread, its clients may busy-poll through an answer slower than the
-  // --busy-poll window while twice the response-time EWMA fits in this share of the poll period
-  // (parts per million; Runner::set_spin_budget splits it over the poll's SQS call, GET and
-  // write, so it bounds the poll's spinning as a whole). The CLI gives a process's queues 1 % in
-  // total (10000 / queues each), so their spinning stays within 1 % of one core whatever the
-  // queue count; under a cgroup CPU limit, within a tenth of the quota (Runner::spin_budget_for).
-  // Only answers within HttpClient::kMaxSpinThrough are ever spun through: a remote endpoint
-  // costs no spinning. 0 disables. Pooled threads never spin beyond the window.
-  int64_t spin_budget_ppm = 10000;
+  // On a worker's own thread, the share of the poll period (parts per million) a poll may spend
+  // spinning beyond the --busy-poll window: to the due time after the warm-up, and through an
+  // answer slower than the window while twice the response-time EWMA fits (Runner::set_spin_budget
+  // splits it over the warm-up, the SQS call, the GET and the write, so it bounds the poll's
+  // spinning as a whole). The CLI's --busy-poll-budget gives a process's queues that percent in
+  // total (10000 ppm per percent, divided by the queue count), so their spinning stays within it
+  // whatever the queue count; under a cgroup CPU limit, within a tenth of the quota
+  // (Runner::spin_budget_for). Only answers within HttpClient::kMaxSpinThrough are ever spun
+  // through: a remote endpoint costs no spinning. 0 (the CLI's default since round 5: paired runs
+  // showed no latency gain beyond noise for about 1.5x the CPU per poll, profiles/r05c, r05d):
+  // the window only. Pooled threads never spin beyond the window.
+  int64_t spin_budget_ppm = 0;
 };
 
 enum class Action : int { None = 0, CoolDown = 1, Scaled = 2, NoopAtBound = 3, Failed = 4 };

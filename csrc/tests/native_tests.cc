@@ -1093,7 +1093,10 @@ TEST(cgroup_cpu_quota_parsers) {
   CHECK(!parse_cfs_quota("-1\n", "100000\n").limited());
   CHECK(parse_cfs_quota("50000\n", "100000\n").quota_ns == 50 * kMillisecond);
   LoopConfig lc;
+  CHECK_EQ(lc.spin_budget_ppm, int64_t(0));  // the CLI's default: the --busy-poll window only
   lc.poll_period = 5 * kSecond;
+  CHECK_EQ(Runner::spin_budget_for(lc, CpuQuota()), Nanos(0));
+  lc.spin_budget_ppm = 10000;  // --busy-poll-budget=1
   CHECK_EQ(Runner::spin_budget_for(lc, CpuQuota()), 50 * kMillisecond);
   CHECK_EQ(Runner::spin_budget_for(lc, q), kMillisecond);
 }

@@ -25,7 +25,13 @@ from .sqs.session import custom_ca_bundle
 from .utils import proxy
 from .utils.goflag import SECOND
 
-SPIN_BUDGET_PPM = 10_000  # LoopConfig.spin_budget_ppm of a process's queues together: 1 %
+ONE_PERCENT_PPM = 10_000  # LoopConfig.spin_budget_ppm for 1 % of the poll period
+DEFAULT_SPIN_BUDGET_PPM = 0  # --busy-poll-budget's default (0 %): the --busy-poll window only
+
+
+def spin_budget_ppm(budget_pct: float, queues: int = 1) -> int:
+    """LoopConfig.spin_budget_ppm of one of ``queues`` queues sharing ``--busy-poll-budget``."""
+    return int(round(budget_pct * ONE_PERCENT_PPM)) // max(queues, 1)
 
 _SCALE_MODES = {"deployment": "Deployment", "scale": "Scale", "patch": "Patch"}
 
@@ -225,11 +231,11 @@ def new_sqs_client(target: TargetConfig, api):
 
 
 def loop_config(target: TargetConfig, pipeline_reads: bool = False, prewarm_ns: int = 0, queues: int = 1,
-                presend: bool = False):
+                presend: bool = False, spin_budget_pct: float = 0.0):
     c = native().LoopConfig()
     c.presend = presend
-    # the process's queues share a 1 % busy-poll budget of their poll period (runner.h)
-    c.spin_budget_ppm = SPIN_BUDGET_PPM // max(queues, 1)
+    # the process's queues share --busy-poll-budget of their poll period (runner.h)
+    c.spin_budget_ppm = spin_budget_ppm(spin_budget_pct, queues)
     c.prefetch = pipeline_reads
     c.prewarm_ns = prewarm_ns
     c.poll_period_ns = target.poll_period_ns
@@ -269,8 +275,8 @@ def new_runner(target: TargetConfig, cfg: Config, rest: RestConfig, base_logger,
     sqs_api = new_sqs_api(region, clock, cfg.sqs_endpoint, cfg.sqs_protocol, cfg.api_timeout_ns,
                           credentials, environ, busy_poll_ns=cfg.busy_poll_ns)
     sqs = new_sqs_client(target, sqs_api)
-    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns, len(cfg.targets), cfg.poll_presend),
-                        sqs, scaler, clock, log)
+    runner = nat.Runner(loop_config(target, cfg.pipeline_reads, cfg.poll_prewarm_ns, len(cfg.targets), cfg.poll_presend,
+                                    cfg.busy_poll_budget_pct), sqs, scaler, clock, log)
     return Worker(target, runner, sqs_api, kube_api, log)
 
 

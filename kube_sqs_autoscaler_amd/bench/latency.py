@@ -27,7 +27,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
-from ..autoscaler import SPIN_BUDGET_PPM, new_deployment_api, new_pod_autoscaler, new_sqs_api, new_sqs_client
+from ..autoscaler import DEFAULT_SPIN_BUDGET_PPM, new_deployment_api, new_pod_autoscaler, new_sqs_api, new_sqs_client
 from ..config import TargetConfig
 from ..kube.config import RestConfig
 from ..ops import fakes, native
@@ -223,7 +223,8 @@ class BenchEnv:
     busy-polling thread (HttpServer::set_hot), awake whenever a request arrives, as a loaded
     production endpoint is (supported with ``shared``, ``process`` and ``split``). ``prewarm_ns``: the
     loop's pre-poll warm-up (``--poll-prewarm``); ``spin_budget_ppm``: the share of the poll
-    period a worker may busy-poll through a slow answer (LoopConfig; None: the CLI's 1 % / queues);
+    period a worker may spin beyond the --busy-poll window (LoopConfig; None: the CLI's default,
+    ``--busy-poll-budget=0``);
     ``presend``: stage each poll's SQS request during the warm-up (LoopConfig.presend; the CLI's
     --poll-presend, off by default); ``prewarm_spin``: spin to the due time after the warm-up for
     a near endpoint (LoopConfig.prewarm_spin);
@@ -317,7 +318,7 @@ class BenchEnv:
             cfg.presend = per_queue(presend, q)
             cfg.prewarm_spin = per_queue(prewarm_spin, q)
             # the CLI's share (autoscaler.loop_config) unless given
-            cfg.spin_budget_ppm = (SPIN_BUDGET_PPM // queues if spin_budget_ppm is None
+            cfg.spin_budget_ppm = (DEFAULT_SPIN_BUDGET_PPM // queues if spin_budget_ppm is None
                                    else per_queue(spin_budget_ppm, q))
             # connect both clients when the worker starts, on its own thread (as --poll-prewarm
             # does before a poll): the on-wire GET never dials, and a dial from this thread would
@@ -578,7 +579,7 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
                    hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,
-                   spin_budget_ppm=col("spin_budget_ppm", SPIN_BUDGET_PPM // queues_per_arm),
+                   spin_budget_ppm=col("spin_budget_ppm", DEFAULT_SPIN_BUDGET_PPM // queues_per_arm),
                    presend=col("presend", False), prewarm_spin=col("prewarm_spin", True),
                    sqs_latency_ns=sqs_latency_ns, kube_latency_ns=kube_latency_ns)
     files = [tempfile.TemporaryFile() for _ in env.runners]

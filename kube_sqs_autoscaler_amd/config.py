@@ -30,6 +30,9 @@ Extensions (all off or reference-equivalent by default):
   ``action_likely``), so an idle queue reads the apiserver no more often than the reference.
 * ``--worker-processes``: one worker process per tracked queue (parallel/procfleet.py) instead
   of one thread per queue.
+* ``--busy-poll-budget`` (default 0): the share of the poll period a queue may spend spinning
+  beyond the ``--busy-poll`` window (runner.h ``LoopConfig::spin_budget_ppm``); off because paired
+  runs showed no latency gain beyond noise for about 1.5x the CPU per poll (profiles/r05c, r05d).
 * ``--poll-presend`` (default off): stage the SQS request during the warm-up (runner.h
   ``LoopConfig::presend``); off because paired A/Bs showed no end-to-end win beyond noise.
 * ``--poll-prewarm`` (default 200us): the pre-poll warm-up (runner.h ``LoopConfig::prewarm``):
@@ -108,6 +111,7 @@ class Config:
     worker_threads: int = 0
     worker_processes: bool = False
     busy_poll_ns: int = 25_000
+    busy_poll_budget_pct: float = 0.0
     poll_prewarm_ns: int = DEFAULT_POLL_PREWARM_NS
     poll_presend: bool = False
     kube_api_qps: float = 5.0
@@ -178,7 +182,8 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.bool("pipeline-reads", True, "Send the Deployment GET together with the SQS poll so the two round trips overlap, on polls likely to scale (decisions unchanged; -pipeline-reads=false for strictly sequential calls)")
     fs.float64("kube-api-qps", 5.0, "Client-side limit on kube-apiserver requests per second for each tracked queue, as client-go's default rest client (0 disables)")
     fs.int("kube-api-burst", 10, "Requests allowed in a burst above -kube-api-qps (client-go default)")
-    fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this; a queue on its own thread may also spin through twice the peer's response time when that fits in its share of 1% of -poll-period, split over the poll's requests (0s disables both)")
+    fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
+    fs.float64("busy-poll-budget", 0.0, "Percent of -poll-period the process's queues may each spend spinning beyond -busy-poll, split over their queues: to the due time after -poll-prewarm and through a near endpoint's answer (never for an answer slower than 200us; at most a tenth of a cgroup CPU quota); 0 disables")
     fs.duration("poll-prewarm", DEFAULT_POLL_PREWARM_NS, "Before each poll, wake this long early to sign the SQS request, read the token and check (or dial, within 100ms) both connections, then start the poll on time (spinning to it only when SQS answers within 200us); decisions are unchanged (0s disables)")
     fs.bool("poll-presend", False, "With -poll-prewarm under 50ms: also hand all but the last bytes of the SQS request to the kernel during the warm-up, corked, so the poll's own write runs warm (nothing reaches the wire early)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
@@ -300,6 +305,7 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         worker_threads=fs["worker-threads"],
         worker_processes=fs["worker-processes"],
         busy_poll_ns=fs["busy-poll"],
+        busy_poll_budget_pct=fs["busy-poll-budget"],
         poll_prewarm_ns=fs["poll-prewarm"],
         poll_presend=fs["poll-presend"],
         kube_api_qps=fs["kube-api-qps"],
@@ -331,6 +337,8 @@ def config_from_flags(fs: FlagSet, environ: Optional[Dict[str, str]] = None) -> 
         raise FlagError(f'invalid value "{cfg.gpu_aware_max}" for flag -gpu-aware-max: must be empty, local or cluster')
     if cfg.worker_processes and cfg.worker_threads > 0:
         raise FlagError("-worker-processes and -worker-threads cannot be combined")
+    if not 0.0 <= cfg.busy_poll_budget_pct <= 100.0:
+        raise FlagError(f'invalid value "{cfg.busy_poll_budget_pct:g}" for flag -busy-poll-budget: must be between 0 and 100')
     if cfg.poll_prewarm_ns < 0:
         raise FlagError(f'invalid value "{cfg.poll_prewarm_ns}ns" for flag -poll-prewarm: must not be negative')
     if cfg.gpus_per_pod < 1:

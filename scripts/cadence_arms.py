@@ -4,8 +4,9 @@ The cadence rows of ``bench.py`` compare whole configurations in separate runs, 
 noise (loopback send cost, scheduler placement) lands between them. Here the arms share one run:
 queue q gets arm q % 4, all
 queues against the same endpoint process, starts staggered over the period. The arms (ARMS):
-the CLI defaults (``--poll-prewarm=200us``, ``--busy-poll=25us``, a spin budget of 1 % of the
-period), the same without the spin budget, no warm-up, and a fixed 300 us busy-poll window. One
+``--poll-prewarm=200us`` and ``--busy-poll=25us`` with ``--busy-poll-budget=1`` (round 4's
+defaults), the same without the spin budget (the CLI defaults since round 5), no warm-up, and a
+fixed 300 us busy-poll window. One
 JSON line per arm and endpoint kind (fakes that sleep / never sleep): poll->patch p50/p90 and the
 per-call phase medians (``HttpTiming``, see ``bench/latency.py``; ``--untimed`` drops them).
 
@@ -20,12 +21,12 @@ import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from kube_sqs_autoscaler_amd.autoscaler import SPIN_BUDGET_PPM  # noqa: E402
+from kube_sqs_autoscaler_amd.autoscaler import ONE_PERCENT_PPM  # noqa: E402
 from kube_sqs_autoscaler_amd.bench.latency import BenchEnv, _detail_medians  # noqa: E402
 
 MS = 1_000_000
-# (prewarm ns, busy-poll ns, spin budget): the CLI defaults (None: the process's 1 % of the period
-# shared by its queues, autoscaler.loop_config), the same without the spin budget (round 3's first
+# (prewarm ns, busy-poll ns, spin budget): --busy-poll-budget=1 (None: the process's 1 % of the
+# period shared by its queues, autoscaler.loop_config), the same without the spin budget (the CLI
 # defaults), no warm-up, and a 300 us fixed window
 ARMS = [(200_000, 25_000, None), (200_000, 25_000, 0), (0, 25_000, 0), (200_000, 300_000, 0)]
 
@@ -35,7 +36,7 @@ def run(period_ms: int, polls: int, queues: int, skip: int = 2, timed: bool = Tr
         env = BenchEnv(queues, "scale", pipeline=True, busy_poll_ns=[a[1] for a in ARMS], servers="process",
                        poll_period_ns=period_ms * MS, stagger=True, hot_endpoints=hot,
                        prewarm_ns=[a[0] for a in ARMS],
-                       spin_budget_ppm=[SPIN_BUDGET_PPM // queues if a[2] is None else a[2] for a in ARMS],
+                       spin_budget_ppm=[ONE_PERCENT_PPM // queues if a[2] is None else a[2] for a in ARMS],
                        timing=timed)
         files = [tempfile.TemporaryFile() for _ in env.runners]
         try:

@@ -1,12 +1,15 @@
-"""What the CLI's spinning buys at a production cadence, and what it costs in CPU.
+"""What the poll path's spinning buys at a production cadence, and what it costs in CPU.
 
-Three spins sit on the default poll path: the pre-poll warm-up's spin to the due time
-(LoopConfig.prewarm_spin, near endpoints only), the busy-poll window on every read
-(--busy-poll, 25 us) and the spin through a near endpoint's answer within the 1 % budget
-(LoopConfig.spin_budget_ppm). Each arm drops some of them; all arms share one run (queue q runs
-arm q % arms, starts staggered over the period, one fake SQS and one fake apiserver process), so
-the box's idle-state drift does not land between them. One JSON line per arm, period and endpoint
-kind: poll->patch p50/p90 and the worker's CPU per poll (the spans' thread CPU time).
+Three spins can sit on a poll: the busy-poll window on every read (--busy-poll, 25 us), and,
+within --busy-poll-budget (LoopConfig.spin_budget_ppm; 0 by default since round 5), the pre-poll
+warm-up's spin to the due time (LoopConfig.prewarm_spin, near endpoints only) and the spin through
+a near endpoint's answer. The arms: the CLI defaults (the window only), a 1 % budget (round 4's
+defaults), the same without the warm-up's spin, and no spinning at all. All arms share one run
+(queue q runs arm q % arms, starts staggered over the period, one fake SQS and one fake apiserver
+process), so the box's idle-state drift does not land between them. One JSON line per arm,
+period and endpoint kind: poll->patch p50/p90 and the worker's CPU per poll (the spans' thread
+CPU time). (Rounds 5's r05c/r05d runs named the arms from the 1 % budget's side: "default" was
+today's budget_1pct, "window_only" today's default.)
 
     python scripts/spin_arms.py --period-ms 1000 --polls 27 --queues 8
 """
@@ -17,6 +20,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from kube_sqs_autoscaler_amd.autoscaler import ONE_PERCENT_PPM  # noqa: E402
 from kube_sqs_autoscaler_amd.bench.latency import measure_cadenced_arms  # noqa: E402
 from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS  # noqa: E402
 
@@ -24,10 +28,9 @@ MS = 1_000_000
 BASE = dict(mode="scale", pipeline=True, busy_poll_ns=25_000, prewarm_ns=DEFAULT_POLL_PREWARM_NS)
 ARMS = {
     "default": BASE,
-    "no_prewarm_spin": dict(BASE, prewarm_spin=False),
-    "no_spin_budget": dict(BASE, spin_budget_ppm=0),
-    "window_only": dict(BASE, prewarm_spin=False, spin_budget_ppm=0),
-    "no_spin": dict(BASE, prewarm_spin=False, spin_budget_ppm=0, busy_poll_ns=0),
+    "budget_1pct": dict(BASE, spin_budget_ppm=ONE_PERCENT_PPM),
+    "budget_1pct_no_warmup_spin": dict(BASE, spin_budget_ppm=ONE_PERCENT_PPM, prewarm_spin=False),
+    "no_spin": dict(BASE, busy_poll_ns=0),
 }
 
 

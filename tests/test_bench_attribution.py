@@ -113,13 +113,17 @@ def test_worker_never_spins_through_a_slow_answer(nat, period_ms):
 
 
 def test_cli_queues_share_one_spin_budget(nat):
-    """autoscaler.loop_config: a process's queues share a 1 % busy-poll budget of their poll
-    period (runner.h LoopConfig.spin_budget_ppm), so a large fleet's spinning stays bounded."""
-    from kube_sqs_autoscaler_amd.autoscaler import SPIN_BUDGET_PPM, loop_config
-    from kube_sqs_autoscaler_amd.config import TargetConfig
+    """autoscaler.loop_config: a process's queues share --busy-poll-budget of their poll period
+    (runner.h LoopConfig.spin_budget_ppm), so a large fleet's spinning stays bounded; the default
+    is 0, the --busy-poll window only."""
+    from kube_sqs_autoscaler_amd.autoscaler import DEFAULT_SPIN_BUDGET_PPM, loop_config
+    from kube_sqs_autoscaler_amd.config import TargetConfig, parse_args
 
     t = TargetConfig(queue_url="https://sqs.us-east-1.amazonaws.com/1/q", deployment="d")
-    assert SPIN_BUDGET_PPM == 10_000
-    assert loop_config(t).spin_budget_ppm == 10_000
-    assert loop_config(t, queues=16).spin_budget_ppm == 625
-    assert loop_config(t, queues=64).spin_budget_ppm == 156
+    assert DEFAULT_SPIN_BUDGET_PPM == 0 and parse_args(["--sqs-queue-url=u"]).busy_poll_budget_pct == 0.0
+    assert loop_config(t).spin_budget_ppm == 0 and nat.LoopConfig().spin_budget_ppm == 0
+    assert parse_args(["--sqs-queue-url=u", "--busy-poll-budget=1"]).busy_poll_budget_pct == 1.0
+    assert loop_config(t, spin_budget_pct=1.0).spin_budget_ppm == 10_000
+    assert loop_config(t, queues=16, spin_budget_pct=1.0).spin_budget_ppm == 625
+    assert loop_config(t, queues=64, spin_budget_pct=1.0).spin_budget_ppm == 156
+    assert loop_config(t, spin_budget_pct=0.25).spin_budget_ppm == 2_500

@@ -5,7 +5,8 @@ README.md:60-66): a CFS quota of 10 ms per 100 ms. Round 4 let a worker spin thr
 endpoint's response-time EWMA whenever that fitted 1 % of the poll period, so a 15 ms SQS round
 trip at the 5 s default period was spun through (about 13 ms of CPU per poll), exhausting that
 quota. Here the CLI polls a fake SQS that answers after 3 ms or 15 ms, at --poll-period=1s, with
-the default --busy-poll and with --busy-poll=0s, and the worker thread's CPU time per poll (the
+the most spinning it can be given (--busy-poll=25us and --busy-poll-budget=1, round 4's defaults;
+since round 5 the budget defaults to 0) and with --busy-poll=0s, and the worker thread's CPU time per poll (the
 trace file's ``cpu_ns``, CLOCK_THREAD_CPUTIME_ID from the start of the iteration to the end of
 the poll) must agree within 10 % (medians over 2 x 7 polls, the arms run at once, in both orders). At 3 ms round 4 spun through every answer (2 x EWMA = 6 ms fits
 the 7.5 ms SQS share of 1 % of 1 s). The queue depth sits in the dead band (no apiserver call),
@@ -42,24 +43,28 @@ def endpoints(nat, tmp_path):
     kube.stop()
 
 
-def _poll_cpu(endpoints, tmp_path, busy_poll: str, delay_s: float = 0.0, out: dict = None, run: int = 0):
+ARMS = {"spin": ["--busy-poll=25us", "--busy-poll-budget=1"], "off": ["--busy-poll=0s"]}
+
+
+def _poll_cpu(endpoints, tmp_path, arm: str, delay_s: float = 0.0, out: dict = None, run: int = 0):
     from kube_sqs_autoscaler_amd.cli import main
 
     sqs, kube, env = endpoints
     time.sleep(delay_s)
-    url = f"{sqs.url}/123/jobs-{busy_poll}"
-    trace = tmp_path / f"trace_{busy_poll}_{run}.jsonl"
+    url = f"{sqs.url}/123/jobs-{arm}"
+    trace = tmp_path / f"trace_{arm}_{run}.jsonl"
     rc = main([f"--sqs-queue-url={url}", "--kubernetes-deployment=w", f"--aws-region={REGION}",
                f"--sqs-endpoint={sqs.url}", "--poll-period=1s", "--attribute-names=ApproximateNumberOfMessages",
-               f"--busy-poll={busy_poll}", f"--trace-file={trace}", "--log-level=error"],
+               *ARMS[arm], f"--trace-file={trace}", "--log-level=error"],
               environ=env, max_iterations=POLLS + 1)
     assert rc == 0
     spans = [json.loads(line) for line in trace.read_text().splitlines()]
     assert len(spans) == POLLS + 1 and all(s["depth"] == 50 and "error" not in s for s in spans)
-    out[busy_poll] = [s["cpu_ns"] for s in spans[1:]]  # the first poll dials
+    out[arm] = [s["cpu_ns"] for s in spans[1:]]  # the first poll dials
 
 
 @pytest.mark.slow
+@pytest.mark.serial  # CPU time per poll: a loaded host (xdist) preempts one arm's polls, not the other's
 @pytest.mark.parametrize("latency_ms", [3, 15])
 def test_busy_poll_costs_no_cpu_against_a_remote_endpoint(nat, endpoints, tmp_path, latency_ms):
     """The CLI runs are paired: two at once, the second half a period behind the first, then
@@ -69,11 +74,11 @@ def test_busy_poll_costs_no_cpu_against_a_remote_endpoint(nat, endpoints, tmp_pa
     profiles/r05c/)."""
     sqs, kube, _ = endpoints
     sqs.set_latency(latency_ms * 1_000_000)
-    for arm in ("25us", "0s"):
+    for arm in ARMS:
         sqs.set_attributes(f"{sqs.url}/123/jobs-{arm}", {"ApproximateNumberOfMessages": "50"})  # the dead band
     kube.add_deployment("default", "w", 2)
-    cpu = {"25us": [], "0s": []}
-    for run, order in enumerate((("25us", "0s"), ("0s", "25us"))):
+    cpu = {arm: [] for arm in ARMS}
+    for run, order in enumerate((("spin", "off"), ("off", "spin"))):
         got: dict = {}
         runs = [threading.Thread(target=_poll_cpu, args=(endpoints, tmp_path, arm, delay, got, run))
                 for arm, delay in zip(order, (0.0, 0.5))]
@@ -83,9 +88,10 @@ def test_busy_poll_costs_no_cpu_against_a_remote_endpoint(nat, endpoints, tmp_pa
             t.join()
         for arm in order:
             cpu[arm] += got[arm]
-    default, off = cpu["25us"], cpu["0s"]
+    default, off = cpu["spin"], cpu["off"]
     assert kube.requests() == 0  # the dead band: the apiserver is never called
-    print(json.dumps({"latency_ms": latency_ms, "cpu_ns_per_poll": {"busy_poll_25us": default, "busy_poll_0s": off}}))
+    print(json.dumps({"latency_ms": latency_ms, "cpu_ns_per_poll": {"busy_poll_25us_budget_1pct": default,
+                                                                     "busy_poll_0s": off}}))
     assert all(c > 0 for c in default + off)
     # A spin through the answer would cost >= latency_ms of CPU per poll; the arms' medians must
     # agree within 10 % (plus 20 us of clock noise). Medians: one poll preempted on a loaded host
@@ -122,7 +128,7 @@ def test_read_cpu_quota_from_a_cgroup_tree(nat, tmp_path):
 
 
 def test_spin_budget_capped_by_the_cpu_quota(nat):
-    """Runner::spin_budget_for: 1 % of the poll period (the CLI's share for one queue), and under
+    """Runner::spin_budget_for: 1 % of the poll period (--busy-poll-budget=1, one queue), and under
     a CFS limit at most a tenth of one period's quota times the queue's share."""
     cfg = nat.LoopConfig()
     cfg.poll_period_ns = 5 * nat.SECOND
@@ -151,9 +157,10 @@ def test_runner_splits_the_poll_spin_budget(nat):
 
 
 @pytest.mark.slow
+@pytest.mark.serial  # a preempted spin ends at its wall-clock deadline having used less CPU
 @pytest.mark.parametrize("ppm,spins", [(10_000, False), (1_000_000, True)])
 def test_warm_up_spin_stays_within_the_budget(nat, tmp_path, ppm, spins):
-    """A 2 ms warm-up lead at a 20 ms period: with the CLI's 1 % (200 us per poll, 50 us of it for
+    """A 2 ms warm-up lead at a 20 ms period: with a 1 % budget (200 us per poll, 50 us of it for
     the warm-up) the worker sleeps most of the lead and spins its last 50 us; with the whole
     period as budget it spins the whole lead, 2 ms of CPU per poll. The in-memory SQS double
     has no response-time EWMA, so it counts as near: the budget alone decides."""
