@@ -71,10 +71,13 @@ def scrape(port: int) -> dict:
             if 'client="' in line:  # transport counters: one per client (sqs / apiserver)
                 key += "_" + line.split('client="', 1)[1].split('"', 1)[0]
             tot[key] = tot.get(key, 0) + float(line.rsplit(" ", 1)[1])
-    return {k: int(v) for k, v in tot.items() if k in (
+    out = {k: int(v) for k, v in tot.items() if k in (
         "polls", "scale_ups", "scale_downs", "depth_errors", "failed_ups", "failed_downs", "sqs_retries",
         "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors") or (
         k.startswith("http_") and k.split("_")[1] in ("connects", "presends", "presend", "reconnect", "idle"))}
+    if "poll_cpu_seconds" in tot and out.get("polls"):  # the workers' CPU per poll so far (ksa_poll_cpu_seconds_total)
+        out["poll_cpu_ms_per_poll"] = round(tot["poll_cpu_seconds"] * 1000 / out["polls"], 4)
+    return out
 
 
 def free_port() -> int:

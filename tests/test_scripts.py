@@ -39,6 +39,7 @@ def test_soak_script_short(nat):
     # warm-up stages the polls' SQS requests (1 s period)
     windows = [r for r in rows if "window" in r and "scrape_error" not in r]
     assert windows and windows[-1]["http_connects_sqs"] >= 2 and windows[-1]["http_presends_sqs"] > 0
+    assert 0 < windows[-1]["poll_cpu_ms_per_poll"] < 50  # ksa_poll_cpu_seconds_total over the polls
 
 
 @pytest.mark.slow
