@@ -98,7 +98,8 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     spans' thread CPU time: warm-up, spinning and the poll). In this order, most important first:
 
     1. BASELINE's queue axis at 250 ms: 1, 2, 4 and 8 tracked queues per path, at least
-       ``--cadence-queue-samples`` scaling polls per path (``cadenced_p50_ms_by_tracked_queues``);
+       ``--cadence-queue-samples`` scaling polls per path, in ``--cadence-queue-rounds``
+       interleaved rounds pooled per cell (``cadenced_p50_ms_by_tracked_queues``);
     2. the regional-RTT model at a cadence (``wan_cadenced_p50_ms``, ``cpu_ms_per_poll``): 1 s,
        the fakes answering SQS after 2 ms and the apiserver after 1 ms -- the structural saving
        (one apiserver round trip, overlapped) at the CPU each path spends;
@@ -120,12 +121,18 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     arms = {"default": dict(mode=args.mode, pipeline=pipeline, busy_poll_ns=bp, prewarm_ns=DEFAULT_POLL_PREWARM_NS),
             "reference_equivalent": dict(mode="deployment", pipeline=False, busy_poll_ns=0, prewarm_ns=0)}
     # plan rows: (group, period label, period ns, suffix, queues per arm, polls per queue, tls, hot, timing, wan)
-    by_q_polls = lambda q: math.ceil(args.cadence_queue_samples / q) + skip  # noqa: E731
-    plan = [("by_queues", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, False, False, False) for q in (1, 2, 4, 8)]
+    # The queue axis runs in ROUNDS interleaved rounds of 1, 2, 4, 8 queues, each cell's samples
+    # pooled over its rounds: a box's idle state drifts over tens of seconds (one 1-queue cell
+    # read 0.20 ms and the next run's 0.09 ms, profiles/r05e, r05g), and cells measured in one
+    # stretch each put that drift between them.
+    rounds = max(1, int(getattr(args, "cadence_queue_rounds", 3)))
+    by_q_polls = lambda q: math.ceil(args.cadence_queue_samples / rounds / q) + skip  # noqa: E731
+    plan = [("by_queues", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, False, False, False)
+            for _ in range(rounds) for q in (1, 2, 4, 8)]
     plan.append(("wan", "1s", 1000 * ms, "_wan_sqs2ms_kube1ms", args.cadence_queues, args.cadence_polls,
                  False, False, False, True))
     plan += [("by_queues_hot", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, True, False, False)
-             for q in (1, 2, 4, 8)]
+             for _ in range(rounds) for q in (1, 2, 4, 8)]
     plan += [("by_queues_timed", "250ms", 250 * ms, f"/{q}", q, by_q_polls(q), False, False, True, False) for q in (1, 8)]
     for label, period, variants in (("250ms", 250 * ms, ((False, False), (True, False))),
                                     ("1s", 1000 * ms, ((False, False), (False, True)))):
@@ -137,18 +144,27 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     p50, rows, cpu = {}, {}, {}
     by_q = {"250ms": {}, "250ms_hot_endpoints": {}}
     by_q_samples, by_q_setup, attribution = {}, {}, {}
+    pooled = {}  # (setup key, arm, queues) -> ([latency ns], [cpu ns], [per-round p50 ms])
     for group, label, period, suffix, queues, polls, tls, hot, timing, wan in plan:
         if time.monotonic() > deadline:
-            skipped.append(f"{label}/{group}{suffix}")
+            if f"{label}/{group}{suffix}" not in skipped:
+                skipped.append(f"{label}/{group}{suffix}")
             continue
+        by_queue_row = group in ("by_queues", "by_queues_hot")
         res = measure_cadenced_arms(period, polls, queues, arms, tls, skip=skip, hot_endpoints=hot, timing=timing,
-                                    sqs_latency_ns=2 * ms if wan else 0, kube_latency_ns=1 * ms if wan else 0)
+                                    sqs_latency_ns=2 * ms if wan else 0, kube_latency_ns=1 * ms if wan else 0,
+                                    keep_samples=by_queue_row)
         for name, r in res.items():
-            if group in ("by_queues", "by_queues_hot"):
+            if by_queue_row:
                 key = "250ms" + ("_hot_endpoints" if hot else "")
-                by_q[key].setdefault(name, {})[str(queues)] = r["p50_ms"]
-                by_q_samples.setdefault(key, {}).setdefault(name, {})[str(queues)] = r["samples"]
-                cpu.setdefault(f"{key}_by_tracked_queues", {}).setdefault(name, {})[str(queues)] = r.get("cpu_ms_per_poll")
+                lat, cpus, rounds_p50 = pooled.setdefault((key, name, queues), ([], [], []))
+                lat += r.pop("latencies_ns")
+                cpus += r.pop("cpu_ns")
+                rounds_p50.append(r["p50_ms"])
+                by_q[key].setdefault(name, {})[str(queues)] = round(_pct(lat, 50) / 1e6, 4) if lat else None
+                by_q_samples.setdefault(key, {}).setdefault(name, {})[str(queues)] = len(lat)
+                cpu.setdefault(f"{key}_by_tracked_queues", {}).setdefault(name, {})[str(queues)] = (
+                    round(sum(cpus) / len(cpus) / 1e6, 4) if cpus else None)
                 if name == "default":
                     by_q_setup.setdefault(key, {})[str(queues)] = r["setup"]
             elif group == "by_queues_timed":
@@ -183,6 +199,8 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
             "interleaved in one run (2q threads, starts staggered over the period) against one fake SQS process and "
             "one fake apiserver process (thread per connection; _hot_endpoints: one busy-polling thread each)"),
         "cadenced_by_tracked_queues_attribution": attribution,
+        "cadenced_by_tracked_queues_rounds_p50_ms": {
+            f"{key}/{name}/{q}": v[2] for (key, name, q), v in pooled.items()},
         "cadenced_vs_hot_loop_default_plain": {k: round(v["default"] / hot_p50_ms, 2) for k, v in p50.items()
                                                if "default" in v},
         "cadenced_reference_over_default": _ratios(p50, by_q),
@@ -193,6 +211,14 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
         "wan_cadenced_p50_ms": wan_p50,
         "cpu_ms_per_poll": cpu.get("1s_wan_sqs2ms_kube1ms", {}),
     }
+
+
+def _pct(v, p: float) -> int:
+    """Nearest-rank percentile of ``v`` (ns)."""
+    import math
+
+    v = sorted(v)
+    return v[min(len(v), max(1, math.ceil(p / 100.0 * len(v)))) - 1]
 
 
 def _ratios(p50: dict, by_q: dict) -> dict:
@@ -346,7 +372,9 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence-polls", type=int, default=27,
                     help="polls per queue per production-cadence fleet row (the first 2 of each queue are dropped)")
     ap.add_argument("--cadence-queue-samples", type=int, default=120,
-                    help="scaling polls per row of the 250 ms 1/2/4/8-tracked-queue rows")
+                    help="scaling polls per cell of the 250 ms 1/2/4/8-tracked-queue rows (over all its rounds)")
+    ap.add_argument("--cadence-queue-rounds", type=int, default=3,
+                    help="interleaved rounds of the 1/2/4/8-queue rows; each cell pools its rounds' samples")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
     ap.add_argument("--pin-ranks", default="auto", choices=["auto", "on", "off"],
                     help="confine each rank of a multi-rank job to its own slice of this process's CPUs, as N "

@@ -544,7 +544,8 @@ def measure_cadenced(poll_period_ns: int, polls: int, queues: int = 16, mode: st
 
 def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, arms: Dict[str, Dict],
                           tls: bool = False, skip: int = 2, servers: str = "split", hot_endpoints: bool = False,
-                          timing: bool = False, sqs_latency_ns: int = 0, kube_latency_ns: int = 0) -> Dict[str, Dict]:
+                          timing: bool = False, sqs_latency_ns: int = 0, kube_latency_ns: int = 0,
+                          keep_samples: bool = False) -> Dict[str, Dict]:
     """Poll -> patch latency at a production poll cadence for one or more paths side by side.
 
     The reference sleeps ``--poll-period`` (5 s by default) before every poll
@@ -566,6 +567,8 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     per arm as ``cpu_ms_per_poll``. ``sqs_latency_ns`` / ``kube_latency_ns``: the fakes answer that
     much later (a regional round trip). ``setup`` records what the run had: the CPUs this process
     may use, its threads, and with endpoint processes their threads and CPU per request served.
+    ``keep_samples``: each arm also returns its raw ``latencies_ns`` and ``cpu_ns`` (one per kept
+    poll), so a caller can pool several runs.
     """
     import json
     import statistics
@@ -639,6 +642,8 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
             "wall_s": round(wall, 2),
             **_cpu_per_poll(spans[a]),
             "setup": setup,
+            **({"latencies_ns": lat, "cpu_ns": [s["cpu_ns"] for s in spans[a] if s.get("cpu_ns", -1) >= 0]}
+               if keep_samples else {}),
             # With timing: every client call's phases, and the fake endpoints' side of each
             # request (HttpServer::timings, all arms together) -- how long the endpoint's thread
             # took to wake up for it after the kernel received it, and to answer it.

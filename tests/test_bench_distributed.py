@@ -173,8 +173,11 @@ def test_cadence_rows_cover_the_queue_axis_default_and_reference(monkeypatch):
             assert st["cpus_available"] >= 1 and st["autoscaler_threads"] >= 2 * int(q)
             assert len(st["endpoint_threads"]) == 2
             assert (st["endpoint_cpu_us_per_request"] is None) if "hot" in setup else len(st["endpoint_cpu_us_per_request"]) == 2
-    assert calls[0] == (250_000_000, 10, 1, ["default", "reference_equivalent"])  # both paths in one run
-    assert [c[2] for c in calls[:4]] == [1, 2, 4, 8]
+    # both paths in one run; three interleaved rounds of 1/2/4/8 queues, pooled per cell
+    assert calls[0] == (250_000_000, 5, 1, ["default", "reference_equivalent"])
+    assert [c[2] for c in calls[:12]] == [1, 2, 4, 8] * 3
+    rounds = out["cadenced_by_tracked_queues_rounds_p50_ms"]
+    assert len(rounds["250ms/default/1"]) == 3 and len(rounds["250ms_hot_endpoints/reference_equivalent/8"]) == 3
     att = out["cadenced_by_tracked_queues_attribution"]
     assert set(att) == {"1", "8"} and "endpoint_median_us" in att["8"]["default"]
     assert "call_phase_median_us" in att["1"]["reference_equivalent"]
