@@ -191,3 +191,29 @@ def test_warm_up_spin_stays_within_the_budget(nat, tmp_path, ppm, spins):
     assert len(cpu) == 10
     median_ms = cpu[len(cpu) // 2] / 1e6
     assert (median_ms > 1.5) if spins else (median_ms < 1.0), cpu
+
+
+def test_spin_window_invariants(nat):
+    """Property (hypothesis) of HttpClient::spin_window_for over its whole input range: never more
+    than the window or the 200 us ceiling; nothing for a peer slower than the ceiling beyond the
+    window rule; beyond the window only within the budget; 0 with busy-poll off."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    ceiling = nat.HTTP_MAX_SPIN_THROUGH_NS
+    ns = st.integers(min_value=-1, max_value=10**10)
+
+    @settings(max_examples=500, deadline=None)
+    @given(st.integers(min_value=0, max_value=10**7), ns, st.integers(min_value=0, max_value=10**10))
+    def check(bp, ewma, budget):
+        w = nat.http_spin_window(bp, ewma, budget)
+        window = bp if (ewma < 0 or ewma <= 4 * bp) else 0
+        assert 0 <= w <= max(bp, ceiling)
+        if bp == 0:
+            assert w == 0
+        if ewma < 0 or ewma > ceiling:
+            assert w == window  # unknown or remote: the window rule alone, whatever the budget
+        if w > window:
+            assert w <= budget and w <= min(2 * ewma, ceiling)
+
+    check()
