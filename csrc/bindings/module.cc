@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include "../core/clock.h"
+#include "../core/cred_slot.h"
 #include "../core/exec_auth.h"
 #include "../core/goutil.h"
 #include "../core/http.h"
@@ -251,6 +252,31 @@ PYBIND11_MODULE(_ksa_native, m) {
       });
   py::class_<StaticCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "StaticCredentialsProvider")
       .def(py::init<Credentials>());
+  // ---- the process fleet's shared credential slot (cred_slot.h) ----
+  auto cs = [](uintptr_t addr) { return reinterpret_cast<SharedCredentialSlot*>(addr); };
+  m.def("credential_slot_size", [] { return sizeof(SharedCredentialSlot); });
+  m.def("init_credential_slot", [](uintptr_t addr) { init_credential_slot(reinterpret_cast<void*>(addr)); });
+  m.def("publish_credentials", [cs](uintptr_t addr, const Credentials& c) { publish_credentials(cs(addr), c); });
+  m.def("publish_credential_error", [cs](uintptr_t addr, const std::string& e) { publish_credential_error(cs(addr), e); });
+  m.def("read_credential_slot", [cs](uintptr_t addr) -> py::tuple {
+    Credentials c;
+    std::string error;
+    uint64_t gen = 0;
+    if (!read_credential_slot(cs(addr), &c, &error, &gen)) return py::make_tuple(py::none(), std::string(), 0);
+    return py::make_tuple(py::cast(c), error, gen);
+  });
+  m.def("request_credentials", [cs](uintptr_t addr, uint64_t gen) { request_credentials(cs(addr), gen); });
+  m.def("credential_slot_needs_fetch", [cs](uintptr_t addr, int64_t unix_now, int64_t window) {
+    return credential_slot_needs_fetch(cs(addr), unix_now, window);
+  });
+  py::class_<SlotCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "SlotCredentialsProvider")
+      .def(py::init([cs](uintptr_t addr, std::shared_ptr<Clock> clock, int64_t window_ns, int64_t wait_limit_ns) {
+             return std::make_shared<SlotCredentialsProvider>(cs(addr), [clock] { return clock->unix_nanos(); },
+                                                              window_ns, wait_limit_ns);
+           }),
+           py::arg("addr"), py::arg("clock"), py::arg("expiry_window_ns") = 5LL * 60 * kSecond,
+           py::arg("wait_limit_ns") = 15 * kSecond)
+      .def("stale", &SlotCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>());
   py::class_<SharedCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "SharedCredentialsProvider")
       .def(py::init([](std::shared_ptr<CredentialsProvider> inner, std::shared_ptr<Clock> clock, int64_t window_ns) {
              return std::make_shared<SharedCredentialsProvider>(

@@ -1,0 +1,166 @@
+#include "cred_slot.h"
+
+#include <time.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+namespace ksa {
+
+namespace {
+
+enum Part : int { kAkid = 0, kSecret = 1, kToken = 2, kName = 3, kError = 4, kParts = 5 };
+
+void nap(Nanos ns) {
+  struct timespec ts = {static_cast<time_t>(ns / kSecond), static_cast<long>(ns % kSecond)};
+  nanosleep(&ts, nullptr);
+}
+
+void publish_parts(SharedCredentialSlot* s, const std::string (&parts)[kParts], int64_t expires) {
+  size_t total = 0;
+  for (const auto& p : parts) total += p.size();
+  if (total > SharedCredentialSlot::kBytes) {
+    std::string err[kParts];
+    err[kError] = "credentials do not fit the worker processes' shared slot (" + std::to_string(total) + " bytes)";
+    publish_parts(s, err, 0);
+    return;
+  }
+  std::string all;
+  all.reserve(total);
+  for (const auto& p : parts) all += p;
+  const uint64_t seq = s->seq.load(std::memory_order_relaxed);
+  s->seq.store(seq + 1, std::memory_order_relaxed);  // odd: being written
+  std::atomic_thread_fence(std::memory_order_release);
+  for (size_t w = 0; w * 8 < all.size(); ++w) {
+    uint64_t word = 0;
+    std::memcpy(&word, all.data() + w * 8, std::min<size_t>(8, all.size() - w * 8));
+    s->words[w].store(word, std::memory_order_relaxed);
+  }
+  for (int i = 0; i < kParts; ++i) s->len[i].store(static_cast<uint32_t>(parts[i].size()), std::memory_order_relaxed);
+  s->expires_unix_ns.store(expires, std::memory_order_relaxed);
+  s->seq.store(seq + 2, std::memory_order_release);
+  s->generation.fetch_add(1, std::memory_order_acq_rel);
+}
+
+}  // namespace
+
+SharedCredentialSlot* init_credential_slot(void* at) {
+  auto* s = new (at) SharedCredentialSlot;
+  s->seq.store(0, std::memory_order_relaxed);
+  s->generation.store(0, std::memory_order_relaxed);
+  s->wanted.store(0, std::memory_order_relaxed);
+  s->expires_unix_ns.store(0, std::memory_order_relaxed);
+  for (auto& l : s->len) l.store(0, std::memory_order_relaxed);
+  for (auto& w : s->words) w.store(0, std::memory_order_relaxed);
+  std::atomic_thread_fence(std::memory_order_release);
+  return s;
+}
+
+void publish_credentials(SharedCredentialSlot* s, const Credentials& c) {
+  const std::string parts[kParts] = {c.access_key_id, c.secret_access_key, c.session_token, c.provider_name, ""};
+  publish_parts(s, parts, c.expires_unix_ns);
+}
+
+void publish_credential_error(SharedCredentialSlot* s, const std::string& error) {
+  std::string parts[kParts];
+  parts[kError] = error.empty() ? "credential fetch failed" : error;
+  publish_parts(s, parts, 0);
+}
+
+bool read_credential_slot(const SharedCredentialSlot* s, Credentials* c, std::string* error, uint64_t* generation) {
+  for (int attempt = 0; attempt < 4096; ++attempt) {
+    const uint64_t gen = s->generation.load(std::memory_order_acquire);
+    const uint64_t before = s->seq.load(std::memory_order_acquire);
+    if (gen == 0) return false;
+    if (before & 1) {
+      if (attempt > 64) nap(10 * kMicrosecond);
+      continue;
+    }
+    uint32_t len[kParts];
+    size_t total = 0;
+    for (int i = 0; i < kParts; ++i) {
+      len[i] = std::min<uint32_t>(s->len[i].load(std::memory_order_relaxed), SharedCredentialSlot::kBytes);
+      total += len[i];
+    }
+    if (total > SharedCredentialSlot::kBytes) continue;  // torn lengths: the check below retries
+    std::string all(total, '\0');
+    for (size_t w = 0; w * 8 < total; ++w) {
+      const uint64_t word = s->words[w].load(std::memory_order_relaxed);
+      std::memcpy(&all[w * 8], &word, std::min<size_t>(8, total - w * 8));
+    }
+    const int64_t expires = s->expires_unix_ns.load(std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (s->seq.load(std::memory_order_relaxed) != before || s->generation.load(std::memory_order_relaxed) != gen)
+      continue;
+    size_t off = 0;
+    std::string parts[kParts];
+    for (int i = 0; i < kParts; ++i) {
+      parts[i] = all.substr(off, len[i]);
+      off += len[i];
+    }
+    *c = Credentials();
+    c->access_key_id = parts[kAkid];
+    c->secret_access_key = parts[kSecret];
+    c->session_token = parts[kToken];
+    c->provider_name = parts[kName];
+    c->expires_unix_ns = expires;
+    *error = parts[kError];
+    *generation = gen;
+    return true;
+  }
+  return false;
+}
+
+void request_credentials(SharedCredentialSlot* s, uint64_t generation) {
+  uint64_t cur = s->wanted.load(std::memory_order_relaxed);
+  while (cur < generation &&
+         !s->wanted.compare_exchange_weak(cur, generation, std::memory_order_acq_rel, std::memory_order_relaxed)) {
+  }
+}
+
+bool credential_slot_needs_fetch(const SharedCredentialSlot* s, int64_t unix_now, int64_t window) {
+  const uint64_t gen = s->generation.load(std::memory_order_acquire);
+  if (gen == 0 || s->wanted.load(std::memory_order_acquire) >= gen) return true;
+  if (s->len[kError].load(std::memory_order_relaxed) > 0) return false;  // retried when a worker asks
+  const int64_t expires = s->expires_unix_ns.load(std::memory_order_relaxed);
+  return expires != 0 && unix_now + window >= expires;
+}
+
+Result<Credentials> SlotCredentialsProvider::retrieve() {
+  Credentials c;
+  std::string error;
+  uint64_t gen = 0;
+  const bool have = read_credential_slot(slot_, &c, &error, &gen);
+  if (have && error.empty() && c.valid() && (c.expires_unix_ns == 0 || now_() + window_ < c.expires_unix_ns))
+    return Result<Credentials>::Ok(c);
+  // Nothing yet, an error, or a set about to expire: ask the supervisor for the next one.
+  request_credentials(slot_, have ? gen : 0);
+  const int64_t deadline = mono_ns() + wait_limit_;
+  while (mono_ns() < deadline) {
+    nap(200 * kMicrosecond);
+    Credentials next;
+    std::string next_error;
+    uint64_t next_gen = 0;
+    if (read_credential_slot(slot_, &next, &next_error, &next_gen) && next_gen > gen) {
+      if (!next_error.empty()) return Result<Credentials>::Err(Status::Err(next_error));
+      return Result<Credentials>::Ok(next);
+    }
+  }
+  // No answer: a set that has not expired yet still signs.
+  if (have && error.empty() && c.valid() && (c.expires_unix_ns == 0 || now_() < c.expires_unix_ns))
+    return Result<Credentials>::Ok(c);
+  return Result<Credentials>::Err(Status::Err(
+      have && !error.empty() ? error : "NoCredentialProviders: the supervisor published no credentials in time"));
+}
+
+void SlotCredentialsProvider::stale(const Credentials& c) {
+  Credentials cur;
+  std::string error;
+  uint64_t gen = 0;
+  if (read_credential_slot(slot_, &cur, &error, &gen) && error.empty() && cur.access_key_id == c.access_key_id &&
+      cur.session_token == c.session_token && cur.expires_unix_ns == c.expires_unix_ns)
+    request_credentials(slot_, gen);
+}
+
+}  // namespace ksa

@@ -1,0 +1,67 @@
+// One AWS credential set shared by the worker processes of --worker-processes.
+//
+// The reference builds one session per process (/root/reference/sqs/sqs.go:36): one credential
+// fetch per expiry. A thread fleet shares one SharedCredentialsProvider (sigv4.h) per region; a
+// process fleet forks one worker per queue, and without this each worker would run the chain
+// itself -- N STS / ECS / IMDS calls per expiry. Instead the supervisor keeps the chain and
+// publishes its current set into a slot of anonymous shared memory (one per region); each worker
+// reads it through SlotCredentialsProvider and, when its copy nears expiry or the set was
+// rejected, asks the supervisor for a newer one and waits for it.
+//
+// Like SharedWorkerState (runner.h): lock-free atomics only (address-free on x86-64), each word
+// with one writer -- the supervisor for the set, its generation and its error; the workers for
+// the `wanted` generation (an atomic max). The set is written under a seqlock.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+
+#include "clock.h"
+#include "sigv4.h"
+
+namespace ksa {
+
+struct SharedCredentialSlot {
+  static constexpr size_t kBytes = 12 * 1024;  // key id + secret + session token + names
+  std::atomic<uint64_t> seq;         // odd while the supervisor writes the set
+  std::atomic<uint64_t> generation;  // sets (or errors) published so far; 0: none yet
+  std::atomic<uint64_t> wanted;      // the newest generation a worker asked to be replaced
+  std::atomic<int64_t> expires_unix_ns;
+  std::atomic<uint32_t> len[5];      // access key id, secret, token, provider name, error
+  std::atomic<uint64_t> words[kBytes / 8];
+};
+
+SharedCredentialSlot* init_credential_slot(void* at);
+// Supervisor side: publish a set (error empty) or the chain's error (every waiting worker's
+// fetch then fails with it); either bumps the generation.
+void publish_credentials(SharedCredentialSlot* s, const Credentials& c);
+void publish_credential_error(SharedCredentialSlot* s, const std::string& error);
+// A consistent read: false while nothing is published (or a writer kept the seqlock busy).
+bool read_credential_slot(const SharedCredentialSlot* s, Credentials* c, std::string* error, uint64_t* generation);
+// Worker side: ask for a set newer than `generation` (an atomic max).
+void request_credentials(SharedCredentialSlot* s, uint64_t generation);
+// Supervisor side: whether the slot needs a fetch -- nothing published, a worker asked to
+// replace the current generation, or the set expires within `window` of `unix_now`.
+bool credential_slot_needs_fetch(const SharedCredentialSlot* s, int64_t unix_now, int64_t window);
+
+// A worker's credential source: the slot's set while it is outside `window` of its expiry;
+// otherwise a request to the supervisor and a wait (up to `wait_limit`) for a newer generation.
+class SlotCredentialsProvider final : public CredentialsProvider {
+ public:
+  SlotCredentialsProvider(SharedCredentialSlot* slot, std::function<int64_t()> unix_now, int64_t window,
+                          Nanos wait_limit = 15 * kSecond)
+      : slot_(slot), now_(std::move(unix_now)), window_(window), wait_limit_(wait_limit) {}
+  Result<Credentials> retrieve() override;
+  void stale(const Credentials& c) override;
+
+ private:
+  SharedCredentialSlot* slot_;
+  std::function<int64_t()> now_;
+  int64_t window_;
+  Nanos wait_limit_;
+};
+
+}  // namespace ksa

@@ -28,6 +28,7 @@
 
 #include "../core/affinity.h"
 #include "../core/clock.h"
+#include "../core/cred_slot.h"
 #include "../core/exec_auth.h"
 #include "../fakes/fakes.h"
 #include "../fakes/http_server.h"
@@ -1069,6 +1070,71 @@ TEST(shared_credentials_one_fetch_per_expiry) {
   CHECK(r.ok() && r.value.session_token == "tok-3");
   CHECK_EQ(inner->calls.load(), 3);
   CHECK_EQ(shared->fetches(), uint64_t(3));
+}
+
+// The process fleet's credential slot (cred_slot.h): a supervisor thread publishing sets of
+// varying sizes while worker threads read them never yields a torn set (every field of a read
+// comes from one publication), and a waiting worker gets the next generation (TSan target: all
+// shared words are atomics, as across processes).
+TEST(credential_slot_seqlock) {
+  auto mem = std::make_unique<SharedCredentialSlot>();
+  SharedCredentialSlot* slot = init_credential_slot(mem.get());
+  Credentials c0;
+  std::string e0;
+  uint64_t g0 = 0;
+  CHECK(!read_credential_slot(slot, &c0, &e0, &g0));  // nothing published yet
+  std::atomic<bool> done{false};
+  std::atomic<int> torn{0}, reads{0};
+  std::thread writer([&] {
+    for (int i = 1; i <= 3000; ++i) {
+      Credentials c;
+      c.access_key_id = "AKID" + std::to_string(i);
+      c.secret_access_key = "secret-" + std::to_string(i);
+      c.session_token = std::string(static_cast<size_t>(i % 700), 't') + std::to_string(i);
+      c.expires_unix_ns = i;
+      publish_credentials(slot, c);
+    }
+    done = true;
+  });
+  std::vector<std::thread> readers;
+  for (int r = 0; r < 4; ++r)
+    readers.emplace_back([&] {
+      while (!done) {
+        Credentials c;
+        std::string e;
+        uint64_t g = 0;
+        if (!read_credential_slot(slot, &c, &e, &g)) continue;
+        ++reads;
+        const std::string n = std::to_string(c.expires_unix_ns);
+        if (c.access_key_id != "AKID" + n || c.secret_access_key != "secret-" + n ||
+            c.session_token.size() < n.size() || c.session_token.substr(c.session_token.size() - n.size()) != n)
+          ++torn;
+      }
+    });
+  writer.join();
+  for (auto& t : readers) t.join();
+  CHECK_EQ(torn.load(), 0);
+  CHECK(reads.load() > 0);
+  Credentials last;
+  std::string err;
+  uint64_t gen = 0;
+  CHECK(read_credential_slot(slot, &last, &err, &gen) && gen == 3000 && last.expires_unix_ns == 3000);
+  // a worker whose set is within its window asks, and waits for the supervisor's next one
+  SlotCredentialsProvider worker(slot, [] { return int64_t(2990); }, 100, 5 * kSecond);
+  CHECK(!credential_slot_needs_fetch(slot, 0, 0));
+  std::thread supervisor([&] {
+    while (!credential_slot_needs_fetch(slot, 0, 0)) std::this_thread::yield();
+    Credentials next;
+    next.access_key_id = "AKIDnext";
+    next.secret_access_key = "s";
+    next.expires_unix_ns = 1 << 30;
+    publish_credentials(slot, next);
+  });
+  auto r = worker.retrieve();
+  supervisor.join();
+  CHECK(r.ok() && r.value.access_key_id == "AKIDnext");
+  publish_credential_error(slot, "STS said no");
+  CHECK(read_credential_slot(slot, &last, &err, &gen) && err == "STS said no" && gen == 3002);
 }
 
 // HttpClient::spin_window_for: no answer slower than kMaxSpinThrough is ever spun for, and no

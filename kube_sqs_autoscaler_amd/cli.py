@@ -92,22 +92,28 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     if cfg.trace_file:
         trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
 
-    # one AWS credential source per region for the process's queues (each worker process of
-    # --worker-processes builds its own after the fork, as separate reference processes would)
+    # one AWS credential source per region for the process's queues; under --worker-processes the
+    # supervisor keeps it and the workers read it through shared memory (parallel/credbroker.py)
     creds: dict = {}
+    broker = None
     if cfg.worker_processes:
         # fork the workers first: before this process starts threads or touches the GPU
+        from .parallel.credbroker import CredentialBroker
         from .parallel.procfleet import ProcessFleet
+
+        broker = CredentialBroker({t.region or cfg.aws_region for t in cfg.targets}, env)
 
         def build(t):
             def make():
-                w = autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi, credentials_cache=creds)
+                w = autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi,
+                                          credentials=broker.provider_for(t.region or cfg.aws_region))
                 if trace_fd >= 0:
                     w.runner.set_trace_fd(trace_fd)
                 return w
             return make
 
         fleet = ProcessFleet([build(t) for t in cfg.targets], cfg.targets)
+        broker.start()  # after the fork: the supervisor's own thread
         workers = fleet.workers
     else:
         workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi, credentials_cache=creds)
@@ -223,6 +229,7 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
             metrics.stop()
         if cfg.worker_processes:
             fleet.close()
+            broker.close()
         if trace_fd >= 0:
             os.close(trace_fd)
     return 0

@@ -1,0 +1,107 @@
+"""The process fleet's one AWS credential source (csrc/core/cred_slot.h).
+
+``--worker-processes`` forks one worker per queue. The reference fetches credentials once per
+process and expiry (one session, /root/reference/sqs/sqs.go:36); a fleet of N worker processes
+running the chain each would make N STS / ECS / IMDS calls per expiry. :class:`CredentialBroker`
+keeps the chain in the supervisor instead: one ``SharedCredentialSlot`` per region in an
+anonymous shared mapping (created before the workers fork, so they inherit it), a supervisor
+thread that fills each slot ahead of its expiry or when a worker asks (a set about to expire, or
+one the service rejected), and in each worker a native ``SlotCredentialsProvider`` that reads the
+slot and waits for the next set when its own is no longer good.
+"""
+from __future__ import annotations
+
+import ctypes
+import mmap
+import threading
+from typing import Dict, Iterable, Mapping, Optional
+
+from ..ops import native
+from ..sqs.credentials import make_chain_provider
+
+# Workers refresh their copy 5 minutes before expiry (CachedCredentials); the broker fills the
+# slot a minute before that, so a worker finds the next set already there -- but not more often
+# than every MIN_REFRESH_NS on its own (a set that lives less than that lead is fetched when a
+# worker asks).
+WORKER_WINDOW_NS = 5 * 60 * 1_000_000_000
+BROKER_LEAD_NS = 60 * 1_000_000_000
+MIN_REFRESH_NS = 10 * 1_000_000_000
+
+
+class CredentialBroker:
+    def __init__(self, regions: Iterable[str], environ: Optional[Mapping[str, str]] = None, clock=None,
+                 poll_s: float = 0.05, providers: Optional[Dict[str, object]] = None):
+        """``providers``: the chain per region (default: the SDK chain for that region)."""
+        nat = native()
+        self.regions = sorted(set(regions))
+        self.environ = environ
+        self.clock = clock or nat.RealClock()
+        self.poll_s = poll_s
+        self._providers = dict(providers or {})
+        size = nat.credential_slot_size()
+        self._slot = (size + mmap.PAGESIZE - 1) // mmap.PAGESIZE * mmap.PAGESIZE
+        self._mm = mmap.mmap(-1, max(1, len(self.regions)) * self._slot, flags=mmap.MAP_SHARED | mmap.MAP_ANONYMOUS)
+        self._buf = ctypes.c_char.from_buffer(self._mm)
+        base = ctypes.addressof(self._buf)
+        self.addrs = {r: base + i * self._slot for i, r in enumerate(self.regions)}
+        for a in self.addrs.values():
+            nat.init_credential_slot(a)
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._last_fetch: Dict[str, int] = {}
+        self.fetches = 0
+
+    def provider_for(self, region: str, clock=None):
+        """A worker's credential source for ``region`` (call it in the worker, after the fork)."""
+        return native().SlotCredentialsProvider(self.addrs[region], clock or native().RealClock(), WORKER_WINDOW_NS)
+
+    def _chain(self, region: str):
+        p = self._providers.get(region)
+        if p is None:
+            p = self._providers[region] = make_chain_provider(environ=self.environ, region=region)
+        return p
+
+    def serve_once(self) -> int:
+        """Fills every slot that needs it; returns how many were fetched."""
+        nat = native()
+        n = 0
+        for region, addr in self.addrs.items():
+            now = self.clock.unix_nanos()
+            _, _, gen = nat.read_credential_slot(addr)
+            asked = gen == 0 or nat.credential_slot_needs_fetch(addr, now, 0)  # none yet, a worker asked, expired
+            due = (nat.credential_slot_needs_fetch(addr, now, WORKER_WINDOW_NS + BROKER_LEAD_NS)
+                   and now - self._last_fetch.get(region, 0) >= MIN_REFRESH_NS)
+            if not (asked or due):
+                continue
+            self._last_fetch[region] = now
+            n += 1
+            self.fetches += 1
+            try:
+                nat.publish_credentials(addr, self._chain(region).retrieve())
+            except Exception as e:  # noqa: BLE001 -- every worker waiting on the slot gets the error
+                nat.publish_credential_error(addr, str(e))
+        return n
+
+    def start(self) -> None:
+        """The supervisor's serving thread (start it after the workers have forked)."""
+        if self._thread is not None:
+            return
+
+        def loop():
+            while not self._stop.is_set():
+                self.serve_once()
+                self._stop.wait(self.poll_s)
+
+        self._thread = threading.Thread(target=loop, name="ksa-credentials", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    def close(self) -> None:
+        self.stop()
+        del self._buf
+        self._mm.close()

@@ -107,3 +107,85 @@ def test_eight_queues_one_fetch_per_expiry(nat, tmp_path):
         ecs.shutdown()
         sqs.stop()
         kube.stop()
+
+
+def test_credential_slot_between_processes(nat):
+    """cred_slot.h: the supervisor publishes a set, a worker reads it, asks for the next when its
+    copy nears expiry, and gets it once the supervisor publishes; an error reaches the waiter."""
+    from kube_sqs_autoscaler_amd.parallel.credbroker import CredentialBroker
+
+    clock = nat.VirtualClock()
+    calls = []
+
+    class Inner(nat.CredentialsProvider):
+        def retrieve(self):
+            calls.append(1)
+            if len(calls) == 3:
+                raise RuntimeError("STS said no")
+            return nat.Credentials("AKID", "secret", f"tok-{len(calls)}", clock.unix_nanos() + 3600 * SEC, "Test")
+
+    broker = CredentialBroker(["us-east-1"], clock=clock, providers={"us-east-1": Inner()})
+    try:
+        addr = broker.addrs["us-east-1"]
+        assert nat.read_credential_slot(addr)[2] == 0 and broker.serve_once() == 1 and len(calls) == 1
+        worker = nat.SlotCredentialsProvider(addr, clock, 300 * SEC, 2 * SEC)
+        assert worker.retrieve().session_token == "tok-1"
+        assert broker.serve_once() == 0  # nothing asked, nothing due
+        clock.advance(3300 * SEC)  # 300 s left: inside the worker's window (and the broker's lead)
+        t = threading.Thread(target=lambda: broker.serve_once())
+        t.start()
+        assert worker.retrieve().session_token == "tok-2"
+        t.join()
+        assert len(calls) == 2
+        worker.stale(worker.retrieve())  # the service rejected tok-2: the next fetch fails
+        assert broker.serve_once() == 1
+        with pytest.raises(nat.NativeError, match="STS said no"):
+            worker.retrieve()
+        assert broker.serve_once() == 1  # the failed worker asked again
+        assert worker.retrieve().session_token == "tok-4"
+    finally:
+        broker.close()
+
+
+@pytest.mark.slow
+def test_worker_processes_share_one_fetch_per_expiry(nat, tmp_path):
+    """--worker-processes: 4 worker processes, one ECS fetch per expiry between them (the
+    supervisor's broker), decisions unchanged."""
+    from kube_sqs_autoscaler_amd.cli import main
+
+    _Ecs.fetches = 0
+    ecs = ThreadingHTTPServer(("127.0.0.1", 0), _Ecs)
+    threading.Thread(target=ecs.serve_forever, daemon=True).start()
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, REGION)
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    try:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"HOME": str(tmp_path), "KUBE_CONFIG_PATH": str(kc), "AWS_EC2_METADATA_DISABLED": "true",
+               "AWS_CONTAINER_CREDENTIALS_FULL_URI": f"http://127.0.0.1:{ecs.server_address[1]}/creds"}
+        specs = []
+        for i in range(4):
+            url = f"{sqs.url}/123/q{i}"
+            sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500" if i % 2 == 0 else "0"})
+            kube.add_deployment("gpu", f"w{i}", 4)
+            specs += ["--queue", f"url={url},deployment=w{i},namespace=gpu,attribute-names=ApproximateNumberOfMessages"]
+        rc = main([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=100ms", "--worker-processes",
+                   "--scale-up-cool-down=0s", "--scale-down-cool-down=0s", "--log-level=error", *specs],
+                  environ=env, max_iterations=25)
+        assert rc == 0
+        assert _Ecs.fetches == 2  # the first set, then its one refresh -- not 4 of each
+        assert sqs.signature_failures() == 0
+        assert [kube.replicas("gpu", f"w{i}") for i in range(4)] == [8, 1] * 2
+        tokens = [v for k, v in sqs.last_headers() if k.lower() == "x-amz-security-token"]
+        assert tokens == ["session-2"]
+    finally:
+        ecs.shutdown()
+        sqs.stop()
+        kube.stop()
