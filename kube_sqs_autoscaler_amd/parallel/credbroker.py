@@ -30,8 +30,11 @@ MIN_REFRESH_NS = 10 * 1_000_000_000
 
 class CredentialBroker:
     def __init__(self, regions: Iterable[str], environ: Optional[Mapping[str, str]] = None, clock=None,
-                 poll_s: float = 0.05, providers: Optional[Dict[str, object]] = None):
-        """``providers``: the chain per region (default: the SDK chain for that region)."""
+                 poll_s: float = 0.2, providers: Optional[Dict[str, object]] = None):
+        """``providers``: the chain per region (default: the SDK chain for that region).
+        ``poll_s``: how often the supervisor's thread looks at the slots -- what a worker that asks
+        for a new set waits at most on top of the fetch (5 wake-ups a second: a fraction of a
+        millicore)."""
         nat = native()
         self.regions = sorted(set(regions))
         self.environ = environ
