@@ -183,8 +183,8 @@ def new_flag_set(program: str = "kube-sqs-autoscaler") -> FlagSet:
     fs.float64("kube-api-qps", 5.0, "Client-side limit on kube-apiserver requests per second for each tracked queue, as client-go's default rest client (0 disables)")
     fs.int("kube-api-burst", 10, "Requests allowed in a burst above -kube-api-qps (client-go default)")
     fs.duration("busy-poll", 25_000, "Spin up to this long for an API response before sleeping, only while the peer answers within 4x this (0s disables)")
-    fs.float64("busy-poll-budget", 0.0, "Percent of -poll-period the process's queues may each spend spinning beyond -busy-poll, split over their queues: to the due time after -poll-prewarm and through a near endpoint's answer (never for an answer slower than 200us; at most a tenth of a cgroup CPU quota); 0 disables")
-    fs.duration("poll-prewarm", DEFAULT_POLL_PREWARM_NS, "Before each poll, wake this long early to sign the SQS request, read the token and check (or dial, within 100ms) both connections, then start the poll on time (spinning to it only when SQS answers within 200us); decisions are unchanged (0s disables)")
+    fs.float64("busy-poll-budget", 0.0, "Percent of -poll-period the process's queues may spend spinning beyond -busy-poll, split over the queues: to the due time after -poll-prewarm and through a near endpoint's answer (never for an answer slower than 200us; at most a tenth of a cgroup CPU quota); 0 disables")
+    fs.duration("poll-prewarm", DEFAULT_POLL_PREWARM_NS, "Before each poll, wake this long early to sign the SQS request, read the token and check (or dial, within 100ms) both connections, then start the poll on time (with -busy-poll-budget, spinning the end of the lead when SQS answers within 200us); decisions are unchanged (0s disables)")
     fs.bool("poll-presend", False, "With -poll-prewarm under 50ms: also hand all but the last bytes of the SQS request to the kernel during the warm-up, corked, so the poll's own write runs warm (nothing reaches the wire early)")
     fs.string("log-level", "info", "Log level: panic, fatal, error, warning, info, debug or trace")
     fs.string("log-format", "text", "Log format: text (logrus TextFormatter) or json")
