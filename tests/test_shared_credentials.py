@@ -189,3 +189,35 @@ def test_worker_processes_share_one_fetch_per_expiry(nat, tmp_path):
         ecs.shutdown()
         sqs.stop()
         kube.stop()
+
+
+def test_credential_slot_limits_and_regions(nat):
+    """A set too large for the slot reaches the workers as an error, not a torn read; each region
+    has a slot of its own, fetched with its own chain."""
+    from kube_sqs_autoscaler_amd.parallel.credbroker import CredentialBroker
+
+    clock = nat.VirtualClock()
+    seen = []
+
+    def chain(region, token):
+        class Inner(nat.CredentialsProvider):
+            def retrieve(self):
+                seen.append(region)
+                return nat.Credentials("AKID-" + region, "secret", token, 0, "Test")
+        return Inner()
+
+    broker = CredentialBroker(["eu-west-1", "us-east-1", "us-east-1"], clock=clock,
+                              providers={"eu-west-1": chain("eu-west-1", "t" * 20_000),
+                                         "us-east-1": chain("us-east-1", "small")})
+    try:
+        assert broker.regions == ["eu-west-1", "us-east-1"]
+        assert broker.serve_once() == 2 and sorted(seen) == ["eu-west-1", "us-east-1"]
+        creds, err, gen = nat.read_credential_slot(broker.addrs["eu-west-1"])
+        assert gen == 1 and "do not fit" in err
+        with pytest.raises(nat.NativeError, match="do not fit"):
+            nat.SlotCredentialsProvider(broker.addrs["eu-west-1"], clock, 300 * SEC, 1 * SEC).retrieve()
+        us = nat.SlotCredentialsProvider(broker.addrs["us-east-1"], clock, 300 * SEC, 1 * SEC).retrieve()
+        assert us.access_key_id == "AKID-us-east-1" and us.session_token == "small"
+        assert broker.serve_once() == 1  # the failed eu-west-1 worker asked again; us-east-1 never expires
+    finally:
+        broker.close()
