@@ -578,7 +578,7 @@ def measure_cadenced_arms(poll_period_ns: int, polls: int, queues_per_arm: int, 
     n = len(names)
     col = lambda k, default=None: [arms[a].get(k, default) for a in names]  # noqa: E731 -- cycled per queue
     # each arm's queues get the spin budget the CLI gives a process tracking that many queues
-    # (1 % of the period shared by them), not a share diluted by the other arms' queues
+    # (--busy-poll-budget shared by them), not a share diluted by the other arms' queues
     env = BenchEnv(queues_per_arm * n, col("mode"), tls=tls, pipeline=col("pipeline"),
                    busy_poll_ns=col("busy_poll_ns"), servers=servers, poll_period_ns=poll_period_ns, stagger=True,
                    hot_endpoints=hot_endpoints, prewarm_ns=col("prewarm_ns"), timing=timing,

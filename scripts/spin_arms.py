@@ -8,8 +8,8 @@ defaults), the same without the warm-up's spin, and no spinning at all. All arms
 (queue q runs arm q % arms, starts staggered over the period, one fake SQS and one fake apiserver
 process), so the box's idle-state drift does not land between them. One JSON line per arm,
 period and endpoint kind: poll->patch p50/p90 and the worker's CPU per poll (the spans' thread
-CPU time). (Rounds 5's r05c/r05d runs named the arms from the 1 % budget's side: "default" was
-today's budget_1pct, "window_only" today's default.)
+CPU time). (Round 5's r05c/r05d runs named the arms from the 1 % budget's side: "default" was
+today's budget_1pct, "window_only" today's default; r05g's budget arms gave each queue 1 %.)
 
     python scripts/spin_arms.py --period-ms 1000 --polls 27 --queues 8
 """
@@ -26,12 +26,18 @@ from kube_sqs_autoscaler_amd.config import DEFAULT_POLL_PREWARM_NS  # noqa: E402
 
 MS = 1_000_000
 BASE = dict(mode="scale", pipeline=True, busy_poll_ns=25_000, prewarm_ns=DEFAULT_POLL_PREWARM_NS)
-ARMS = {
-    "default": BASE,
-    "budget_1pct": dict(BASE, spin_budget_ppm=ONE_PERCENT_PPM),
-    "budget_1pct_no_warmup_spin": dict(BASE, spin_budget_ppm=ONE_PERCENT_PPM, prewarm_spin=False),
-    "no_spin": dict(BASE, busy_poll_ns=0),
-}
+
+
+def arms(queues: int) -> dict:
+    """The arms, each queue with the budget --busy-poll-budget=1 gives a process of ``queues``
+    queues (1 % of the period shared by them)."""
+    ppm = ONE_PERCENT_PPM // max(queues, 1)
+    return {
+        "default": BASE,
+        "budget_1pct": dict(BASE, spin_budget_ppm=ppm),
+        "budget_1pct_no_warmup_spin": dict(BASE, spin_budget_ppm=ppm, prewarm_spin=False),
+        "no_spin": dict(BASE, busy_poll_ns=0),
+    }
 
 
 def main() -> int:
@@ -46,7 +52,7 @@ def main() -> int:
     lat = dict(sqs_latency_ns=int(a.sqs_latency_ms * MS), kube_latency_ns=int(a.kube_latency_ms * MS))
     for period in a.period_ms:
         for hot in (False,) if a.sleeping_only else (False, True):
-            res = measure_cadenced_arms(period * MS, a.polls, a.queues, ARMS, hot_endpoints=hot, **lat)
+            res = measure_cadenced_arms(period * MS, a.polls, a.queues, arms(a.queues), hot_endpoints=hot, **lat)
             for name, r in res.items():
                 print(json.dumps({"arm": name, "period_ms": period, "hot_endpoints": hot, "queues": a.queues,
                                   "sqs_latency_ms": a.sqs_latency_ms, "kube_latency_ms": a.kube_latency_ms,
