@@ -90,12 +90,11 @@ IterationRecord Runner::step(StopFlag* stop) {
     slept = clock_->sleep(period - w, stop);
     if (slept) {
       warm(due, true);
-      // Spin to the due time only for a near SQS endpoint (an answer within
-      // HttpClient::kMaxSpinThrough, or none measured yet): its poll is short enough for an awake
-      // core with warm caches to show. Against a remote endpoint (milliseconds) that saving is
-      // noise while the spin would be most of the poll's CPU: the warm-up's work is done, and the
-      // thread sleeps out the rest of the lead.
-      // The spin is the end of the lead, within the warm-up's share of the poll's spin budget.
+      // Then sleep out the lead -- or spin its end, within the warm-up's share of the poll's spin
+      // budget (0 unless --busy-poll-budget), for a near SQS endpoint (an answer within
+      // HttpClient::kMaxSpinThrough, or none measured yet), whose poll is short enough for an
+      // awake core with warm caches to show. Against a remote endpoint (milliseconds) that saving
+      // is noise while the spin would be most of the poll's CPU.
       const Nanos ewma = sqs_->api()->response_ewma();
       const Nanos rest = due - clock_->now();
       Nanos spin = cfg_.prewarm_spin && ewma <= HttpClient::kMaxSpinThrough ? rest : 0;
