@@ -4,7 +4,8 @@ Production question: how many queues can one autoscaler process track at a given
 without polls starting late? N queues, each with its own connections and Deployment, run
 through ``Scheduler(K)``. Every poll is a full signed SQS call + Deployment GET (+ write when the
 fake's 200/0 cycle says so). Reports achieved polls/s against the ideal N/period, the fraction
-of polls that started more than 1 ms after they were due, and the worst lateness.
+of polls that started more than 1 ms after they were due, the worst lateness, and the worker
+threads' CPU per poll and in cores.
 """
 from __future__ import annotations
 
@@ -43,9 +44,11 @@ def run_capacity(queues: int, period_s: float, threads: int, duration_s: float =
         time.sleep(2 * period_s)
         sched.reset_lateness()
         p0 = sum(r.stats()["polls"] for r in runners)
+        c0 = sum(r.stats()["poll_cpu_ns"] for r in runners)
         t0 = time.perf_counter()
         time.sleep(duration_s)
         polls = sum(r.stats()["polls"] for r in runners) - p0
+        cpu = sum(r.stats()["poll_cpu_ns"] for r in runners) - c0
         wall = time.perf_counter() - t0
         late, max_late = sched.late_polls(), sched.max_lateness_ns()
         sched.stop()
@@ -59,6 +62,9 @@ def run_capacity(queues: int, period_s: float, threads: int, duration_s: float =
             "ideal_polls_per_s": round(queues / period_s, 1),
             "late_poll_fraction": round(late / max(polls, 1), 4),
             "max_lateness_ms": round(max_late / 1e6, 3),
+            # the pooled threads' CPU in the polls themselves (the warm-up events are not counted)
+            "cpu_ms_per_poll": round(cpu / max(polls, 1) / 1e6, 4),
+            "cpu_cores": round(cpu / 1e9 / wall, 3),
             "signature_failures": env.sqs.signature_failures(),
         }
     finally:
