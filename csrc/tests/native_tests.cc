@@ -1093,18 +1093,21 @@ TEST(credential_slot_seqlock) {
       c.session_token = std::string(static_cast<size_t>(i % 700), 't') + std::to_string(i);
       c.expires_unix_ns = i;
       publish_credentials(slot, c);
+      while (i == 1 && reads.load() == 0) std::this_thread::yield();  // the readers overlap the rest
     }
     done = true;
   });
   std::vector<std::thread> readers;
   for (int r = 0; r < 4; ++r)
     readers.emplace_back([&] {
-      while (!done) {
+      int mine = 0;
+      while (!done || mine == 0) {
         Credentials c;
         std::string e;
         uint64_t g = 0;
         if (!read_credential_slot(slot, &c, &e, &g)) continue;
         ++reads;
+        ++mine;
         const std::string n = std::to_string(c.expires_unix_ns);
         if (c.access_key_id != "AKID" + n || c.secret_access_key != "secret-" + n ||
             c.session_token.size() < n.size() || c.session_token.substr(c.session_token.size() - n.size()) != n)
