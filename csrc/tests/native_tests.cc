@@ -1211,18 +1211,20 @@ TEST(shared_error_slot_seqlock) {
   SharedWorkerState* s = init_shared_worker_state(mem);
   CHECK(read_shared_error(s).empty());
   const std::string a(300, 'a'), b = "short b error", c(600, 'c');
-  std::atomic<bool> done{false};
+  std::atomic<bool> done{false}, reading{false};
   std::thread writer([&] {
+    while (!reading.load()) std::this_thread::yield();  // the reads overlap the writes
     for (int i = 0; i < 20000; ++i) write_shared_error(s, i % 3 == 0 ? a : i % 3 == 1 ? b : c);
     done = true;
   });
   const std::string c_cut(SharedWorkerState::kErrorBytes - 1, 'c');
   long reads = 0, bad = 0;
-  while (!done.load()) {
+  reading = true;
+  do {
     const std::string t = read_shared_error(s);
     ++reads;
     if (!(t.empty() || t == a || t == b || t == c_cut)) ++bad;
-  }
+  } while (!done.load());
   writer.join();
   CHECK(bad == 0);
   CHECK(reads > 0);
