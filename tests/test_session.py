@@ -304,6 +304,38 @@ def test_indented_keys_and_headers_are_keys_and_headers():
     assert dict(g.items("default")) == {"key": "a\nb", "other": "c"}
 
 
+def test_uniform_indent_reads_like_no_indent():
+    """Property: indenting every header and key line by the same amount changes nothing -- the
+    same sections, keys and values as the unindented file (continuations stay deeper)."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from kube_sqs_autoscaler_amd.sqs import ini
+
+    word = st.text(alphabet="abcdefghijklmnopqrstuvwxyz_0123456789", min_size=1, max_size=8)
+    entry = st.tuples(word, word, st.lists(word, max_size=2))  # key, value, continuation lines
+    sections = st.lists(st.tuples(word, st.lists(entry, max_size=4)), min_size=1, max_size=3)
+
+    def render(secs, pad: str) -> str:
+        out = []
+        for name, entries in secs:
+            out.append(f"{pad}[{name}]")
+            for key, value, more in entries:
+                out.append(f"{pad}{key} = {value}")
+                out.extend(f"{pad}    {m}" for m in more)
+        return "\n".join(out) + "\n"
+
+    @settings(max_examples=200, deadline=None)
+    @given(sections, st.sampled_from(["  ", "\t", "    "]))
+    def check(secs, pad):
+        flat, indented = ini.parse(render(secs, ""), "f"), ini.parse(render(secs, pad), "g")
+        assert flat.sections() == indented.sections()
+        for s in flat.sections():
+            assert flat.items(s) == indented.items(s)
+
+    check()
+
+
 def test_indented_credentials_file_feeds_the_chain(tmp_path):
     from kube_sqs_autoscaler_amd.sqs.credentials import SharedFileProvider
 
