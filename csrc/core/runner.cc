@@ -108,6 +108,7 @@ IterationRecord Runner::step(StopFlag* stop) {
     if (slept && w > 0) warm(clock_->now());
   }
   if (!slept) {
+    cpu_from_ = -1;  // no poll to charge it to
     IterationRecord rec;
     rec.stopped = true;
     return rec;
