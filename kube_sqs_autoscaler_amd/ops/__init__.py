@@ -60,10 +60,6 @@ def native() -> ModuleType:
         return _mod
 
 
-def native_path() -> str:
-    return native().__file__
-
-
 def fakes() -> ModuleType:
     """Returns the ``_ksa_fakes`` module (test doubles), building it in-tree if needed. It
     registers subclasses of ``_ksa_native``'s seams, so the runtime is loaded first."""
