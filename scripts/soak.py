@@ -21,6 +21,16 @@ summary line has the mismatch count (must be 0) and whether fds / threads / RSS 
 
     python scripts/soak.py --minutes 10 --queues 8 --poll-period 1s > gpurun_out/soak.jsonl
 
+``--worker-processes``: the CLI runs one worker process per queue (resources are then summed over
+the supervisor and its workers). ``--ecs-refresh SECONDS``: the AWS credentials come from a
+container-credentials endpoint (AWS_CONTAINER_CREDENTIALS_FULL_URI) whose every set expires
+6 minutes plus SECONDS after it is issued. Under ``--worker-processes`` the supervisor's
+credential broker (parallel/credbroker.py) fetches the next set SECONDS after the last (at most
+every 10 s) and the workers switch to the newest a minute after that (their 5-minute window);
+without it the one shared provider per region refreshes SECONDS plus a minute after issue. The
+summary counts the endpoint's fetches, which must stay at one per refresh for the whole fleet,
+not one per queue, and names the session token of the last poll.
+
 ``--hot``: the old back-to-back soak of one queue (no faults), p50/p99 per window.
 """
 import argparse
@@ -48,15 +58,67 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
        "ApproximateNumberOfMessagesNotVisible": "0"}
 
 
-def proc_stats(pid: int) -> dict:
-    out = {"fds": len(os.listdir(f"/proc/{pid}/fd"))}
-    with open(f"/proc/{pid}/status") as f:
-        for line in f:
-            if line.startswith("VmRSS:"):
-                out["rss_kb"] = int(line.split()[1])
-            elif line.startswith("Threads:"):
-                out["threads"] = int(line.split()[1])
+def proc_stats(pid: int, tree: bool = False) -> dict:
+    """fds, threads and RSS of ``pid`` -- summed over it and its descendants with ``tree``."""
+    pids = [pid]
+    if tree:
+        import psutil
+
+        pids += [c.pid for c in psutil.Process(pid).children(recursive=True)]
+    out = {"fds": 0, "rss_kb": 0, "threads": 0}
+    for p in pids:
+        try:
+            out["fds"] += len(os.listdir(f"/proc/{p}/fd"))
+            with open(f"/proc/{p}/status") as f:
+                for line in f:
+                    if line.startswith("VmRSS:"):
+                        out["rss_kb"] += int(line.split()[1])
+                    elif line.startswith("Threads:"):
+                        out["threads"] += int(line.split()[1])
+        except OSError:  # a worker that just exited
+            continue
+    if tree:
+        out["processes"] = len(pids)
     return out
+
+
+class EcsEndpoint:
+    """A container-credentials endpoint: every set is new (its own session token) and expires
+    ``refresh_s`` plus 6 minutes after it is issued -- the broker's 5-minute window plus 1-minute
+    lead (parallel/credbroker.py) put its refresh ``refresh_s`` after issue."""
+
+    def __init__(self, refresh_s: float):
+        from datetime import datetime, timedelta, timezone
+        from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+        ep = self
+        self.fetches = 0
+        self.lock = threading.Lock()
+
+        class Handler(BaseHTTPRequestHandler):
+            def do_GET(self):  # noqa: N802
+                with ep.lock:
+                    ep.fetches += 1
+                    n = ep.fetches
+                expires = datetime.now(timezone.utc) + timedelta(minutes=6, seconds=refresh_s)
+                body = json.dumps({"AccessKeyId": AKID, "SecretAccessKey": SECRET, "Token": f"soak-session-{n}",
+                                   "Expiration": expires.strftime("%Y-%m-%dT%H:%M:%S.%fZ")}).encode()
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def log_message(self, *a):
+                pass
+
+        self.server = ThreadingHTTPServer(("127.0.0.1", 0), Handler)
+        self.url = f"http://127.0.0.1:{self.server.server_address[1]}/creds"
+        threading.Thread(target=self.server.serve_forever, daemon=True).start()
+
+    def close(self) -> None:
+        self.server.shutdown()
+        self.server.server_close()
 
 
 def scrape(port: int) -> dict:
@@ -139,8 +201,17 @@ def cadenced(a) -> int:
     args += [f"--queue=url={u},deployment=workers-{q},namespace=soak" for q, u in enumerate(urls)]
     if a.presend:
         args.append("--poll-presend")
-    env = dict(os.environ, AWS_ACCESS_KEY_ID=AKID, AWS_SECRET_ACCESS_KEY=SECRET, KUBE_CONFIG_PATH=kc,
-               AWS_CA_BUNDLE=ca, HOME=tmp)
+    if a.worker_processes:
+        args.append("--worker-processes")
+    env = dict(os.environ, KUBE_CONFIG_PATH=kc, AWS_CA_BUNDLE=ca, HOME=tmp)
+    ecs = None
+    if a.ecs_refresh > 0:
+        ecs = EcsEndpoint(a.ecs_refresh)
+        for k in ("AWS_ACCESS_KEY_ID", "AWS_SECRET_ACCESS_KEY", "AWS_SESSION_TOKEN", "AWS_PROFILE"):
+            env.pop(k, None)
+        env.update(AWS_CONTAINER_CREDENTIALS_FULL_URI=ecs.url, AWS_EC2_METADATA_DISABLED="true")
+    else:
+        env.update(AWS_ACCESS_KEY_ID=AKID, AWS_SECRET_ACCESS_KEY=SECRET)
     err = open(os.path.join(tmp, "stderr.log"), "w")
     child = subprocess.Popen(args, cwd=ROOT, env=env, stderr=err, stdout=subprocess.DEVNULL)
     injected = {"kube_503_retry_after": 0, "kube_500": 0, "kube_409": 0, "kube_drop": 0, "sqs_throttle": 0,
@@ -199,12 +270,14 @@ def cadenced(a) -> int:
                 break
             # resources first: the scrape's own handler thread and socket may still be alive
             # right after it returns, and would count as a thread and an fd of the process
-            res = proc_stats(child.pid)
+            res = proc_stats(child.pid, tree=a.worker_processes)
             try:
                 m = scrape(port)
             except OSError as e:
                 m = {"scrape_error": str(e)}
             row = {"window": k, "t_s": round(time.monotonic() - t_start, 1), **res, **m, "injected": dict(injected)}
+            if ecs is not None:
+                row["credential_fetches"] = ecs.fetches
             rows.append(row)
             print(json.dumps(row), flush=True)
             k += 1
@@ -215,8 +288,12 @@ def cadenced(a) -> int:
             child.send_signal(signal.SIGTERM)
         rc = child.wait(timeout=60)
         err.close()
+        elapsed = time.monotonic() - t_start
+        tokens_seen = [v for k2, v in sqs.last_headers() if k2.lower() == "x-amz-security-token"]
         sqs.stop()
         kube.stop()
+        if ecs is not None:
+            ecs.close()
     with open(trace) as f:
         spans = [json.loads(line) for line in f if line.strip()]
     p = Params(poll_ns=period, up_cool_ns=up_cool, down_cool_ns=down_cool, up_msgs=100, down_msgs=10, max_pods=8,
@@ -249,8 +326,16 @@ def cadenced(a) -> int:
         "resources": flat,
         "poll_to_patch_us": {"samples": len(lat), "p50": pct_us(50), "p90": pct_us(90), "p99": pct_us(99)},
         "signature_failures": sqs.signature_failures(), "kube_auth_failures": kube.auth_failures(),
+        "worker_processes": a.worker_processes,
         "ok": rc == 0 and all(r.ok for r in replays) and all(v and v["flat"] for v in flat.values()),
     }
+    if ecs is not None:
+        # one fetch at start-up, then one per refresh for the whole fleet (the thread fleet's
+        # shared provider refreshes a minute later in each set's life than the broker does)
+        most = 2 + int(elapsed / a.ecs_refresh)
+        summary["credentials"] = {"refresh_s": a.ecs_refresh, "fetches": ecs.fetches, "at_most": most,
+                                  "last_poll_token": tokens_seen[-1] if tokens_seen else None}
+        summary["ok"] = summary["ok"] and ecs.fetches <= most
     if not summary["ok"]:
         summary["stderr_tail"] = stderr_tail
     print(json.dumps(summary), flush=True)
@@ -299,6 +384,9 @@ def main() -> int:
                     help="cool-down comparisons this close to the edge are not judged by the replay")
     ap.add_argument("--hot", action="store_true", help="back-to-back single-queue soak without faults")
     ap.add_argument("--presend", action="store_true", help="run the CLI with --poll-presend (staged SQS requests)")
+    ap.add_argument("--worker-processes", action="store_true", help="run the CLI with --worker-processes")
+    ap.add_argument("--ecs-refresh", type=float, default=0.0,
+                    help="seconds between credential refreshes from a container-credentials endpoint (0: static keys)")
     a = ap.parse_args()
     return hot(a) if a.hot else cadenced(a)
 

@@ -43,6 +43,23 @@ def test_soak_script_short(nat):
 
 
 @pytest.mark.slow
+def test_soak_script_worker_processes_rotating_credentials(nat):
+    """--worker-processes with a container-credentials endpoint whose sets the broker refreshes
+    5 s after issue (at most every 10 s, credbroker.MIN_REFRESH_NS): the supervisor's broker
+    fetches for the whole fleet (one fetch per refresh, not one per worker), decisions and
+    signatures are unaffected, the resources are the process tree's. (The workers adopt a newer
+    set a minute after the broker has it -- their 5-minute window vs its 6 -- which the 10-minute
+    box soak shows, profiles/r05p/.)"""
+    rows = _run(["scripts/soak.py", "--minutes", "0.3", "--window", "6", "--queues", "3", "--fault-every", "2",
+                 "--worker-processes", "--ecs-refresh", "5"], timeout=200)
+    summary = rows[-1]
+    assert summary["ok"] and summary["replay"]["mismatches"] == 0 and summary["signature_failures"] == 0
+    creds = summary["credentials"]
+    assert 2 <= creds["fetches"] <= creds["at_most"], creds
+    assert summary["last_metrics"]["processes"] == 4  # the supervisor and 3 workers
+
+
+@pytest.mark.slow
 def test_sweep_bench_scripts_cpu(nat):
     env = {"HIP_VISIBLE_DEVICES": "", "KSA_BENCH_SEGMENT_S": "300"}
     rows = _run(["scripts/sweep_bench.py"], env=env)
