@@ -92,6 +92,8 @@ def test_queue_spec_plus_reference_form():
 @pytest.mark.parametrize("argv", [
     ["--queue=deployment=x"], ["--queue=url=u,bogus=1"], ["--queue=url=u,max-pods=x"], ["--queue=url"],
     ["--scale-mode=watch"], ["--sqs-protocol=grpc"], ["--log-format=xml"], ["--gpu-aware-max=remote"],
+    ["--busy-poll-budget=-1"], ["--busy-poll-budget=101"], ["--busy-poll-budget=NaN"], ["--busy-poll-budget=x"],
+    ["--poll-prewarm=-1ms"],
 ])
 def test_invalid_extension_values(argv):
     with pytest.raises(FlagError):
