@@ -60,6 +60,14 @@ def test_soak_script_worker_processes_rotating_credentials(nat):
 
 
 @pytest.mark.slow
+def test_cpu_split_script(nat):
+    rows = _run(["scripts/cpu_split.py", "--queues", "2", "--period-ms", "50", "--short-s", "2.5", "--long-s", "4"],
+                timeout=200)
+    assert [r["arm"] for r in rows] == ["default", "default_busy_poll_0", "reference_equivalent"]
+    assert all(r["ok"] and r["polls"] > 0 and r["span_cpu_ms_per_poll"] > 0 for r in rows)
+
+
+@pytest.mark.slow
 def test_sweep_bench_scripts_cpu(nat):
     env = {"HIP_VISIBLE_DEVICES": "", "KSA_BENCH_SEGMENT_S": "300"}
     rows = _run(["scripts/sweep_bench.py"], env=env)
