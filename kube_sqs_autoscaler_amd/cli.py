@@ -150,7 +150,13 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
         health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets],
                         leader_elect=cfg.leader_elect, failure_window_ns=cfg.readiness_failure_window_ns)
-        metrics = MetricsServer(fleet, cfg.metrics_addr, health)
+        if broker is not None:
+            def credential_fetches():
+                return dict(broker.fetches_by_region)
+        else:
+            def credential_fetches():
+                return {region: p.fetches() for region, p in list(creds.items())}
+        metrics = MetricsServer(fleet, cfg.metrics_addr, health, credential_fetches)
         metrics.start()
         log.log("info", f"Serving metrics on {cfg.metrics_addr}")
 

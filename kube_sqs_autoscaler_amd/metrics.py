@@ -14,7 +14,7 @@ import math
 import socket
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from .ops import native
 from .parallel.fleet import Fleet
@@ -115,9 +115,13 @@ class _Family:
 
 
 class FleetCollector:
-    def __init__(self, fleet: Fleet, health: Optional["Health"] = None) -> None:
+    def __init__(self, fleet: Fleet, health: Optional["Health"] = None,
+                 credential_fetches: Optional[Callable[[], Dict[str, int]]] = None) -> None:
+        """``credential_fetches``: the process's AWS credential fetches so far, per region (the
+        thread fleet's shared providers, or the process fleet's broker)."""
         self.fleet = fleet
         self.health = health
+        self.credential_fetches = credential_fetches
 
     def families(self) -> List[_Family]:
         stats = self.fleet.stats()
@@ -164,8 +168,15 @@ class FleetCollector:
                 hist.add("_bucket", lv + [("le", _num(le))], cum)
             hist.add("_count", lv, cum)
             hist.add("_sum", lv, s["latency_sum_ns"] / 1e9)
-        return [*fams.values(), *(f for f in (*api.values(), *http.values()) if f.samples), depth, reps, failing,
-                failing_s, cpu, lat, hist]
+        out = [*fams.values(), *(f for f in (*api.values(), *http.values()) if f.samples), depth, reps, failing,
+               failing_s, cpu, lat, hist]
+        if self.credential_fetches is not None:
+            creds = _Family("ksa_aws_credential_fetches_total", "counter",
+                            "AWS credential fetches of the process (one source per region, shared by its queues)")
+            for region, n in sorted(self.credential_fetches().items()):
+                creds.add("", [("region", region)], n)
+            out.append(creds)
+        return out
 
     def exposition(self) -> bytes:
         out: List[str] = []
@@ -279,11 +290,12 @@ def _listen(host: str, port: int, handler) -> ThreadingHTTPServer:
 
 
 class MetricsServer:
-    def __init__(self, fleet: Fleet, addr: str, health: Optional[Health] = None) -> None:
+    def __init__(self, fleet: Fleet, addr: str, health: Optional[Health] = None,
+                 credential_fetches: Optional[Callable[[], Dict[str, int]]] = None) -> None:
         self.fleet = fleet
         self.health = health or Health(fleet)
         hl = self.health
-        self.collector = FleetCollector(fleet)
+        self.collector = FleetCollector(fleet, credential_fetches=credential_fetches)
         coll = self.collector
 
         class Handler(BaseHTTPRequestHandler):

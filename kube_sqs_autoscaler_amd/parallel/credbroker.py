@@ -53,6 +53,7 @@ class CredentialBroker:
         self._thread: Optional[threading.Thread] = None
         self._last_fetch: Dict[str, int] = {}
         self.fetches = 0
+        self.fetches_by_region: Dict[str, int] = {r: 0 for r in self.regions}
 
     def provider_for(self, region: str, clock=None):
         """A worker's credential source for ``region`` (call it in the worker, after the fork)."""
@@ -79,6 +80,7 @@ class CredentialBroker:
             self._last_fetch[region] = now
             n += 1
             self.fetches += 1
+            self.fetches_by_region[region] += 1
             try:
                 nat.publish_credentials(addr, self._chain(region).retrieve())
             except Exception as e:  # noqa: BLE001 -- every worker waiting on the slot gets the error

@@ -135,7 +135,8 @@ def scrape(port: int) -> dict:
             tot[key] = tot.get(key, 0) + float(line.rsplit(" ", 1)[1])
     out = {k: int(v) for k, v in tot.items() if k in (
         "polls", "scale_ups", "scale_downs", "depth_errors", "failed_ups", "failed_downs", "sqs_retries",
-        "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors") or (
+        "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors",
+        "aws_credential_fetches") or (
         k.startswith("http_") and k.split("_")[1] in ("connects", "presends", "presend", "reconnect", "idle"))}
     if "poll_cpu_seconds" in tot and out.get("polls"):  # the workers' CPU per poll so far (ksa_poll_cpu_seconds_total)
         out["poll_cpu_ms_per_poll"] = round(tot["poll_cpu_seconds"] * 1000 / out["polls"], 4)

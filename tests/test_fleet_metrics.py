@@ -107,6 +107,19 @@ def test_metrics_endpoints(nat):
         env.close()
 
 
+def test_credential_fetches_family(nat):
+    """ksa_aws_credential_fetches_total: one sample per region from the process's credential
+    sources (cli.py passes the shared providers' or the broker's counts)."""
+    from kube_sqs_autoscaler_amd.metrics import FleetCollector
+    from kube_sqs_autoscaler_amd.parallel.fleet import Fleet
+
+    body = FleetCollector(Fleet([]), credential_fetches=lambda: {"us-east-1": 2, "eu-west-1": 1}).exposition().decode()
+    assert "# TYPE ksa_aws_credential_fetches_total counter" in body
+    assert 'ksa_aws_credential_fetches_total{region="eu-west-1"} 1.0' in body
+    assert 'ksa_aws_credential_fetches_total{region="us-east-1"} 2.0' in body
+    assert "ksa_aws_credential_fetches_total" not in FleetCollector(Fleet([])).exposition().decode()
+
+
 def test_pooled_scheduler_many_queues_few_threads(nat):
     """64 queues on 4 native threads: every queue polls, decisions match a dedicated loop."""
     env = BenchEnv(64)

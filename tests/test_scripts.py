@@ -57,6 +57,8 @@ def test_soak_script_worker_processes_rotating_credentials(nat):
     creds = summary["credentials"]
     assert 2 <= creds["fetches"] <= creds["at_most"], creds
     assert summary["last_metrics"]["processes"] == 4  # the supervisor and 3 workers
+    # /metrics counts the broker's fetches (ksa_aws_credential_fetches_total)
+    assert 1 <= summary["last_metrics"]["aws_credential_fetches"] <= creds["fetches"]
 
 
 @pytest.mark.slow
