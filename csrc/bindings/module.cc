@@ -276,7 +276,8 @@ PYBIND11_MODULE(_ksa_native, m) {
            }),
            py::arg("addr"), py::arg("clock"), py::arg("expiry_window_ns") = 5LL * 60 * kSecond,
            py::arg("wait_limit_ns") = 15 * kSecond)
-      .def("stale", &SlotCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>());
+      .def("stale", &SlotCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>())
+      .def("cancel", &SlotCredentialsProvider::cancel);
   py::class_<SharedCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "SharedCredentialsProvider")
       .def(py::init([](std::shared_ptr<CredentialsProvider> inner, std::shared_ptr<Clock> clock, int64_t window_ns) {
              return std::make_shared<SharedCredentialsProvider>(

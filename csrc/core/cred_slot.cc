@@ -138,6 +138,7 @@ Result<Credentials> SlotCredentialsProvider::retrieve() {
   request_credentials(slot_, have ? gen : 0);
   const int64_t deadline = mono_ns() + wait_limit_;
   while (mono_ns() < deadline) {
+    if (cancelled_.load(std::memory_order_acquire)) return Result<Credentials>::Err(Status::Err("request canceled"));
     nap(200 * kMicrosecond);
     Credentials next;
     std::string next_error;

@@ -48,7 +48,8 @@ void request_credentials(SharedCredentialSlot* s, uint64_t generation);
 bool credential_slot_needs_fetch(const SharedCredentialSlot* s, int64_t unix_now, int64_t window);
 
 // A worker's credential source: the slot's set while it is outside `window` of its expiry;
-// otherwise a request to the supervisor and a wait (up to `wait_limit`) for a newer generation.
+// otherwise a request to the supervisor and a wait (up to `wait_limit`, or until cancel()) for a
+// newer generation.
 class SlotCredentialsProvider final : public CredentialsProvider {
  public:
   SlotCredentialsProvider(SharedCredentialSlot* slot, std::function<int64_t()> unix_now, int64_t window,
@@ -56,8 +57,11 @@ class SlotCredentialsProvider final : public CredentialsProvider {
       : slot_(slot), now_(std::move(unix_now)), window_(window), wait_limit_(wait_limit) {}
   Result<Credentials> retrieve() override;
   void stale(const Credentials& c) override;
+  // The worker stops: a retrieve() waiting for the supervisor returns "request canceled" at once.
+  void cancel() override { cancelled_.store(true, std::memory_order_release); }
 
  private:
+  std::atomic<bool> cancelled_{false};
   SharedCredentialSlot* slot_;
   std::function<int64_t()> now_;
   int64_t window_;

@@ -72,6 +72,10 @@ class CredentialsProvider {
   virtual Result<Credentials> retrieve() = 0;
   // A client found `c` rejected (ExpiredToken): a provider that caches drops it. Default: none.
   virtual void stale(const Credentials& c) { (void)c; }
+  // The client that owns this source stops for good (its API's cancel(), on Runner::stop): a
+  // provider that waits for credentials stops waiting. Lock-free: the wait may hold the caller's
+  // lock. Default: nothing to interrupt.
+  virtual void cancel() {}
 };
 
 class StaticCredentialsProvider final : public CredentialsProvider {
@@ -91,6 +95,7 @@ class alignas(kCacheLine) CachedCredentials {
       : provider_(std::move(p)), window_(expiry_window_ns) {}
   Result<Credentials> get(int64_t unix_now_ns);
   void invalidate();
+  void cancel() { provider_->cancel(); }  // lock-free: get() may be waiting in retrieve()
 
  private:
   std::shared_ptr<CredentialsProvider> provider_;

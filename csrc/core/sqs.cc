@@ -88,6 +88,7 @@ HttpSqsApi::HttpSqsApi(SqsHttpOptions opts, std::shared_ptr<CredentialsProvider>
 
 void HttpSqsApi::cancel() {
   cancel_.request_stop();
+  creds_.cancel();  // a worker process waiting for its supervisor's next credential set
   if (http_) http_->cancel();
 }
 

@@ -1142,6 +1142,27 @@ TEST(credential_slot_seqlock) {
 
 // HttpClient::spin_window_for: no answer slower than kMaxSpinThrough is ever spun for, and no
 // spin exceeds it, whatever the budget.
+// A worker waiting for its supervisor's first set (an empty slot) stops waiting when its API is
+// cancelled (Runner::stop -> HttpSqsApi::cancel -> CachedCredentials -> the provider), instead of
+// holding the worker's shutdown for the whole wait limit.
+TEST(credential_slot_wait_cancels) {
+  auto mem = std::make_unique<SharedCredentialSlot>();
+  SharedCredentialSlot* slot = init_credential_slot(mem.get());
+  auto provider = std::make_shared<SlotCredentialsProvider>(slot, [] { return int64_t(0); }, 0, 30 * kSecond);
+  CachedCredentials cache(provider, 0);
+  const int64_t t0 = mono_ns();
+  std::thread stopper([&] {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    cache.cancel();  // while get() waits in retrieve() under the cache's lock
+  });
+  auto r = cache.get(0);
+  stopper.join();
+  const int64_t waited = mono_ns() - t0;
+  CHECK(!r.ok() && r.status.message() == "request canceled");
+  CHECK(waited < 5 * kSecond);
+  CHECK(credential_slot_needs_fetch(slot, 0, 0));  // the request stays asked for
+}
+
 TEST(spin_window_ceiling) {
   const Nanos us = kMicrosecond;
   CHECK_EQ(HttpClient::spin_window_for(25 * us, 15000 * us, 37500 * us), Nanos(0));

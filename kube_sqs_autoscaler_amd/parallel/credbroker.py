@@ -100,13 +100,19 @@ class CredentialBroker:
         self._thread = threading.Thread(target=loop, name="ksa-credentials", daemon=True)
         self._thread.start()
 
-    def stop(self) -> None:
+    def stop(self, timeout: float = 1.0) -> bool:
+        """Stops the serving thread; False when it is still inside a fetch after ``timeout``
+        (a hung credential endpoint: the thread is a daemon and ends with the process)."""
         self._stop.set()
         if self._thread is not None:
-            self._thread.join(timeout=30)
+            self._thread.join(timeout=timeout)
+            if self._thread.is_alive():
+                return False
             self._thread = None
+        return True
 
     def close(self) -> None:
-        self.stop()
+        if not self.stop():
+            return  # the thread may still publish into the slots: leave them mapped
         del self._buf
         self._mm.close()

@@ -221,3 +221,67 @@ def test_credential_slot_limits_and_regions(nat):
         assert broker.serve_once() == 1  # the failed eu-west-1 worker asked again; us-east-1 never expires
     finally:
         broker.close()
+
+
+class _HungEcs(BaseHTTPRequestHandler):
+    """A container-credentials endpoint that never answers within the chain's 5 s timeout."""
+
+    def do_GET(self):  # noqa: N802
+        threading.Event().wait(8)
+
+    def log_message(self, *a):
+        pass
+
+
+@pytest.mark.slow
+def test_worker_processes_stop_while_waiting_for_credentials(nat, tmp_path):
+    """--worker-processes against a hung credential endpoint: the workers wait for the
+    supervisor's first set (cred_slot.h) and the supervisor's broker is inside a 5 s fetch when
+    SIGTERM comes. The waits are cancelled with the workers' API calls (Runner::stop ->
+    SlotCredentialsProvider::cancel) and the broker's thread is not waited for, so the process
+    exits at once instead of after the fetch."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    ecs = ThreadingHTTPServer(("127.0.0.1", 0), _HungEcs)
+    ecs.daemon_threads = True
+    threading.Thread(target=ecs.serve_forever, daemon=True).start()
+    sqs = nat.FakeSqsServer()
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    try:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {k: v for k, v in os.environ.items() if not k.startswith("AWS_")}
+        env.update(HOME=str(tmp_path), KUBE_CONFIG_PATH=str(kc), AWS_EC2_METADATA_DISABLED="true",
+                   AWS_CONTAINER_CREDENTIALS_FULL_URI=f"http://127.0.0.1:{ecs.server_address[1]}/creds")
+        specs = []
+        for i in range(2):
+            kube.add_deployment("gpu", f"w{i}", 2)
+            specs.append(f"--queue=url={sqs.url}/123/q{i},deployment=w{i},namespace=gpu")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        child = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", f"--aws-region={REGION}",
+                                  f"--sqs-endpoint={sqs.url}", "--poll-period=200ms", "--worker-processes",
+                                  "--log-level=error", *specs], cwd=root, env=env,
+                                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        time.sleep(3.0)  # started: the workers' first polls wait for the broker's (hung) fetch
+        assert child.poll() is None
+        t0 = time.monotonic()
+        child.send_signal(signal.SIGTERM)
+        _, err = child.communicate(timeout=30)
+        took = time.monotonic() - t0
+        assert child.returncode == 0, err[-2000:]
+        assert took < 1.8, took  # not the rest of the 5 s fetch
+        assert sqs.requests() == 0  # nothing was signed without credentials
+    finally:
+        ecs.shutdown()
+        sqs.stop()
+        kube.stop()
