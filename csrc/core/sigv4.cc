@@ -197,13 +197,30 @@ void CachedCredentials::invalidate() {
 }
 
 Result<Credentials> SharedCredentialsProvider::retrieve() {
-  std::lock_guard<std::mutex> lk(mu_);  // concurrent askers wait for the one fetch
+  std::unique_lock<std::mutex> lk(mu_);
   if (have_ && (cached_.expires_unix_ns == 0 || now_() + window_ < cached_.expires_unix_ns))
     return Result<Credentials>::Ok(cached_);
+  if (fetching_) {  // another client is fetching: its outcome is this caller's too
+    const uint64_t ticket = fetched_;
+    done_.wait(lk, [&] { return fetched_ != ticket; });
+    return last_;
+  }
+  fetching_ = true;
   fetches_++;
-  auto r = inner_->retrieve();
+  lk.unlock();
+  Result<Credentials> r;  // outside the lock: stale() and fetches() stay quick meanwhile
+  try {
+    r = inner_->retrieve();
+  } catch (const std::exception& e) {  // the waiters must be released whatever happens
+    r = Result<Credentials>::Err(Status::Err(e.what()));
+  }
+  lk.lock();
+  fetching_ = false;
   have_ = r.ok() && r.value.valid();
   if (have_) cached_ = r.value;
+  last_ = r;
+  fetched_++;
+  done_.notify_all();
   return r;
 }
 

@@ -8,6 +8,7 @@
 // steady-state signing costs two SHA-256 digests and one HMAC.
 #pragma once
 
+#include <condition_variable>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -107,9 +108,12 @@ class alignas(kCacheLine) CachedCredentials {
 
 // One credential source for every SQS client of a process with the same chain configuration
 // (region). Each client's CachedCredentials asks it when its own copy nears expiry; it calls
-// `inner` only when its copy does too (or a client reported it stale), under its lock, so N
-// tracked queues make one STS / ECS / IMDS fetch per expiry instead of N -- the reference builds
-// one session per process (/root/reference/sqs/sqs.go:36). `unix_now` is the clock (wall time).
+// `inner` only when its copy does too (or a client reported it stale), so N tracked queues make
+// one STS / ECS / IMDS fetch per expiry instead of N -- the reference builds one session per
+// process (/root/reference/sqs/sqs.go:36). Callers that arrive while a fetch is in flight wait
+// for that fetch and take its outcome, its error included: against a hung or failing endpoint
+// the N queues share one timeout rather than queueing N of them behind each other. `unix_now`
+// is the clock (wall time).
 class SharedCredentialsProvider final : public CredentialsProvider {
  public:
   SharedCredentialsProvider(std::shared_ptr<CredentialsProvider> inner, std::function<int64_t()> unix_now,
@@ -127,8 +131,12 @@ class SharedCredentialsProvider final : public CredentialsProvider {
   std::function<int64_t()> now_;
   int64_t window_;
   mutable std::mutex mu_;
+  std::condition_variable done_;  // a fetch finished (fetched_ moved on)
   bool have_ = false;
   Credentials cached_;
+  bool fetching_ = false;
+  uint64_t fetched_ = 0;      // fetches finished
+  Result<Credentials> last_;  // the outcome of the last one
   uint64_t fetches_ = 0;
 };
 

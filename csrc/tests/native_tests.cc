@@ -1072,6 +1072,41 @@ TEST(shared_credentials_one_fetch_per_expiry) {
   CHECK_EQ(shared->fetches(), uint64_t(3));
 }
 
+// Against a credential endpoint that fails slowly (a hung ECS / IMDS answering with a timeout),
+// the clients asking at once share the one fetch's error instead of queueing a fetch each: one
+// inner call, every caller's answer within about one fetch's time.
+TEST(shared_credentials_share_a_failing_fetch) {
+  struct SlowFailing final : CredentialsProvider {
+    std::atomic<int> calls{0};
+    Result<Credentials> retrieve() override {
+      calls++;
+      std::this_thread::sleep_for(std::chrono::milliseconds(150));
+      return Result<Credentials>::Err(Status::Err("EC2RoleRequestError: timed out"));
+    }
+  };
+  auto inner = std::make_shared<SlowFailing>();
+  auto shared = std::make_shared<SharedCredentialsProvider>(inner, [] { return int64_t(0); }, 0);
+  std::atomic<int> failed{0};
+  const int64_t t0 = mono_ns();
+  std::vector<std::thread> clients;
+  std::atomic<bool> go{false};
+  for (int i = 0; i < 8; ++i)
+    clients.emplace_back([&] {
+      while (!go) std::this_thread::yield();
+      auto r = shared->retrieve();
+      if (!r.ok() && r.status.message() == "EC2RoleRequestError: timed out") ++failed;
+    });
+  go = true;
+  for (auto& t : clients) t.join();
+  const int64_t took = mono_ns() - t0;
+  CHECK_EQ(failed.load(), 8);
+  CHECK(inner->calls.load() <= 2);  // one, or two for a caller that arrived after the first ended
+  CHECK(took < 600 * kMillisecond);  // not 8 x 150 ms
+  // the next poll's ask is a fresh fetch (nothing cached from an error)
+  (void)shared->retrieve();
+  CHECK(inner->calls.load() <= 3 && shared->fetches() == static_cast<uint64_t>(inner->calls.load()));
+}
+
 // The process fleet's credential slot (cred_slot.h): a supervisor thread publishing sets of
 // varying sizes while worker threads read them never yields a torn set (every field of a read
 // comes from one publication), and a waiting worker gets the next generation (TSan target: all

@@ -226,7 +226,10 @@ def test_credential_slot_limits_and_regions(nat):
 class _HungEcs(BaseHTTPRequestHandler):
     """A container-credentials endpoint that never answers within the chain's 5 s timeout."""
 
+    asked = threading.Event()
+
     def do_GET(self):  # noqa: N802
+        _HungEcs.asked.set()
         threading.Event().wait(8)
 
     def log_message(self, *a):
@@ -234,18 +237,23 @@ class _HungEcs(BaseHTTPRequestHandler):
 
 
 @pytest.mark.slow
-def test_worker_processes_stop_while_waiting_for_credentials(nat, tmp_path):
-    """--worker-processes against a hung credential endpoint: the workers wait for the
-    supervisor's first set (cred_slot.h) and the supervisor's broker is inside a 5 s fetch when
-    SIGTERM comes. The waits are cancelled with the workers' API calls (Runner::stop ->
+@pytest.mark.serial  # a stop's wall time: a loaded host (xdist) slows the processes' exit
+@pytest.mark.parametrize("mode,queues,limit_s", [("processes", 2, 1.8), ("threads", 3, 7.0)])
+def test_stop_while_waiting_for_credentials(nat, tmp_path, mode, queues, limit_s):
+    """SIGTERM while the queues wait for credentials from a hung endpoint (the chain's ECS
+    fetch times out after 5 s). ``--worker-processes``: the workers wait for the supervisor's
+    first set (cred_slot.h); the waits are cancelled with their API calls (Runner::stop ->
     SlotCredentialsProvider::cancel) and the broker's thread is not waited for, so the process
-    exits at once instead of after the fetch."""
+    exits at once. Threads: the queues share the one fetch in flight (SharedCredentialsProvider)
+    instead of queueing a 5 s fetch each, so the stop waits out that fetch's rest (under 5 s)
+    rather than 5 s per queue (3 queues: about 12 s before)."""
     import os
     import signal
     import subprocess
     import sys
     import time
 
+    _HungEcs.asked.clear()
     ecs = ThreadingHTTPServer(("127.0.0.1", 0), _HungEcs)
     ecs.daemon_threads = True
     threading.Thread(target=ecs.serve_forever, daemon=True).start()
@@ -264,22 +272,24 @@ def test_worker_processes_stop_while_waiting_for_credentials(nat, tmp_path):
         env.update(HOME=str(tmp_path), KUBE_CONFIG_PATH=str(kc), AWS_EC2_METADATA_DISABLED="true",
                    AWS_CONTAINER_CREDENTIALS_FULL_URI=f"http://127.0.0.1:{ecs.server_address[1]}/creds")
         specs = []
-        for i in range(2):
+        for i in range(queues):
             kube.add_deployment("gpu", f"w{i}", 2)
             specs.append(f"--queue=url={sqs.url}/123/q{i},deployment=w{i},namespace=gpu")
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        extra = ["--worker-processes"] if mode == "processes" else []
         child = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", f"--aws-region={REGION}",
-                                  f"--sqs-endpoint={sqs.url}", "--poll-period=200ms", "--worker-processes",
+                                  f"--sqs-endpoint={sqs.url}", "--poll-period=200ms", *extra,
                                   "--log-level=error", *specs], cwd=root, env=env,
                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
-        time.sleep(3.0)  # started: the workers' first polls wait for the broker's (hung) fetch
+        assert _HungEcs.asked.wait(60), "the credential endpoint was never asked"
+        time.sleep(0.5)  # every queue is waiting for that fetch now
         assert child.poll() is None
         t0 = time.monotonic()
         child.send_signal(signal.SIGTERM)
-        _, err = child.communicate(timeout=30)
+        _, err = child.communicate(timeout=60)
         took = time.monotonic() - t0
         assert child.returncode == 0, err[-2000:]
-        assert took < 1.8, took  # not the rest of the 5 s fetch
+        assert took < limit_s, took
         assert sqs.requests() == 0  # nothing was signed without credentials
     finally:
         ecs.shutdown()
