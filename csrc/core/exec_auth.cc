@@ -191,28 +191,46 @@ Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code)
 ExecTokenProvider::ExecTokenProvider(ExecConfig cfg, std::shared_ptr<Clock> clock)
     : cfg_(std::move(cfg)), clock_(std::move(clock)) {}
 
-Result<ExecCredential> ExecTokenProvider::current_locked() {
+Result<ExecCredential> ExecTokenProvider::current() {
+  std::unique_lock<std::mutex> lk(mu_);
   // client-go: reuse the cached credential unless it expired (strict After, a zero expiry
   // never expires) or a 401 on it asked for a refresh.
   if (have_ && pending_code_ == 0 && (!cached_.has_expiry || clock_->unix_nanos() <= cached_.expiry_unix_ns))
     return Result<ExecCredential>::Ok(cached_);
-  auto r = run_exec_plugin(cfg_, pending_code_);
+  if (running_) {  // another queue runs the plugin: its outcome is this caller's too
+    const uint64_t ticket = finished_;
+    ran_.wait(lk, [&] { return finished_ != ticket; });
+    return last_;
+  }
+  running_ = true;
+  const int code = pending_code_;
   ++runs_;
-  if (!r.ok()) return Result<ExecCredential>::Err(r.status.wrap("getting credentials"));
-  cached_ = r.value;
-  have_ = true;
-  pending_code_ = 0;
+  lk.unlock();
+  Result<ExecCredential> r;
+  try {
+    r = run_exec_plugin(cfg_, code);
+  } catch (const std::exception& e) {  // the waiters must be released whatever happens
+    r = Result<ExecCredential>::Err(Status::Err(e.what()));
+  }
+  lk.lock();
+  running_ = false;
+  if (!r.ok()) {
+    r = Result<ExecCredential>::Err(r.status.wrap("getting credentials"));
+  } else {
+    cached_ = r.value;
+    have_ = true;
+    pending_code_ = 0;  // a 401 reported during the run was about the token this one replaces
+  }
+  last_ = r;
+  ++finished_;
+  ran_.notify_all();
   return r;
 }
 
-Result<ExecCredential> ExecTokenProvider::credential() {
-  std::lock_guard<std::mutex> lk(mu_);
-  return current_locked();
-}
+Result<ExecCredential> ExecTokenProvider::credential() { return current(); }
 
 Result<std::string> ExecTokenProvider::token() {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto c = current_locked();
+  auto c = current();
   if (!c.ok()) return Result<std::string>::Err(c.status);
   return Result<std::string>::Ok(c.value.token);
 }

@@ -10,6 +10,7 @@
 #pragma once
 
 #include <cstdint>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -48,6 +49,8 @@ class ExecTokenProvider final : public TokenProvider {
  public:
   ExecTokenProvider(ExecConfig cfg, std::shared_ptr<Clock> clock);
   // Cached token, or a fresh run when there is none, it expired, or a 401 invalidated it.
+  // Callers that arrive during a run wait for it and share its outcome, its error included, so
+  // a hanging or failing plugin costs the queues of a process one run, not one each.
   Result<std::string> token() override;
   void invalidate(const std::string& used) override;
   // The whole current credential (client certificate included), refreshed like token().
@@ -55,14 +58,18 @@ class ExecTokenProvider final : public TokenProvider {
   uint64_t runs() const;
 
  private:
-  Result<ExecCredential> current_locked();
+  Result<ExecCredential> current();
 
   ExecConfig cfg_;
   std::shared_ptr<Clock> clock_;
   mutable std::mutex mu_;
+  std::condition_variable ran_;  // a run finished (finished_ moved on)
   bool have_ = false;
   int pending_code_ = 0;  // 401 seen on the cached token
   ExecCredential cached_;
+  bool running_ = false;
+  uint64_t finished_ = 0;
+  Result<ExecCredential> last_;  // the outcome of the last run
   uint64_t runs_ = 0;
 };
 

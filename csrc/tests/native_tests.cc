@@ -1015,6 +1015,32 @@ TEST(exec_provider_shared_across_threads) {
   p->invalidate("tok-42");
   CHECK(p->token().ok());
   CHECK_EQ(p->runs(), uint64_t(2));
+  // A plugin that fails slowly: the 8 threads asking at once share one run's error instead of
+  // running it one after another (8 x 300 ms).
+  const std::string failing = std::string(dir) + "/failing.sh";
+  {
+    std::FILE* f = std::fopen(failing.c_str(), "w");
+    std::fputs("#!/bin/sh\nsleep 0.3\necho 'no credentials' >&2\nexit 3\n", f);
+    std::fclose(f);
+  }
+  chmod(failing.c_str(), 0755);
+  cfg.command = failing;
+  auto q = std::make_shared<ExecTokenProvider>(cfg, std::make_shared<RealClock>());
+  std::atomic<int> failed{0};
+  std::atomic<bool> go{false};
+  ts.clear();
+  const int64_t t0 = mono_ns();
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([&] {
+      while (!go) std::this_thread::yield();
+      if (!q->token().ok()) ++failed;
+    });
+  go = true;
+  for (auto& t : ts) t.join();
+  CHECK_EQ(failed.load(), 8);
+  CHECK(q->runs() <= uint64_t(2));
+  CHECK(mono_ns() - t0 < 1500 * kMillisecond);
+  std::remove(failing.c_str());
   std::remove((std::string(dir) + "/runs").c_str());
   std::remove(script.c_str());
   rmdir(dir);
