@@ -112,9 +112,11 @@ std::string base64(const std::string& in) {
 
 // getaddrinfo(3) has no timeout, so a stuck resolver would hold a worker far past
 // --api-timeout (Go's dialer bounds the lookup by the request's context). Names are resolved on
-// a helper thread and the caller stops waiting at the deadline; a late answer is freed by the
-// helper. IP literals (and calls without a deadline) resolve inline.
-Status resolve(const std::string& host, const std::string& port, int64_t deadline_ns, struct addrinfo** out) {
+// a helper thread and the caller stops waiting at the deadline, or when `cancelled` is set (a
+// stop: checked every 10 ms); a late answer is freed by the helper. IP literals (and calls
+// without a deadline) resolve inline.
+Status resolve(const std::string& host, const std::string& port, int64_t deadline_ns, struct addrinfo** out,
+               const std::atomic<bool>* cancelled) {
   struct addrinfo hints;
   std::memset(&hints, 0, sizeof hints);
   hints.ai_family = AF_UNSPEC;
@@ -148,10 +150,17 @@ Status resolve(const std::string& host, const std::string& port, int64_t deadlin
     st->cv.notify_all();
   }).detach();
   std::unique_lock<std::mutex> lk(st->mu);
-  const int64_t left = deadline_ns - mono_ns();
-  if (left <= 0 || !cv_wait_for(st->cv, lk, left, [&] { return st->done; })) {
-    st->abandoned = true;
-    return Status::Err("dial tcp: lookup " + host + ": i/o timeout");
+  while (!st->done) {
+    const int64_t left = deadline_ns - mono_ns();
+    if (left <= 0) {
+      st->abandoned = true;
+      return Status::Err("dial tcp: lookup " + host + ": i/o timeout");
+    }
+    if (cancelled && cancelled->load(std::memory_order_acquire)) {
+      st->abandoned = true;
+      return Status::Err("request canceled");
+    }
+    cv_wait_for(st->cv, lk, std::min<int64_t>(left, 10 * kMillisecond), [&] { return st->done; });
   }
   if (st->rc != 0) return Status::Err("dial tcp: lookup " + host + ": " + gai_strerror(st->rc));
   *out = st->res;
@@ -514,7 +523,7 @@ Status HttpClient::set_proxy(const std::string& proxy_url) {
 
 Status HttpClient::dial(const Url& to, int64_t deadline_ns, int* fd_out) {
   struct addrinfo* res = nullptr;
-  Status rs = resolve(to.host, std::to_string(to.port), deadline_ns, &res);
+  Status rs = resolve(to.host, std::to_string(to.port), deadline_ns, &res, &cancelled_);
   if (!rs.ok()) return rs;
   Status last = Status::Err("dial tcp " + to.host_header() + ": no addresses");
   int fd = -1;

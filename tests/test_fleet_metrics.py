@@ -450,3 +450,69 @@ def test_metrics_listen_addresses():
             assert urllib.request.urlopen(f"http://{host}:{m.port}/healthz", timeout=5).status == 200
         finally:
             m.stop()
+
+
+@pytest.mark.slow
+@pytest.mark.serial  # binds the container's resolver port: nothing else may resolve names meanwhile
+def test_stop_cancels_a_hung_name_lookup(nat, tmp_path):
+    """A poll dialling while the DNS server is silent waits in getaddrinfo on a helper thread
+    (http.cc resolve(), bounded by --api-timeout); a stop ends that wait too, not only the
+    socket waits. Needs a resolver at 127.0.0.1 this process may impersonate (the dev container,
+    as root); skipped elsewhere."""
+    import os
+    import signal
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    import yaml
+
+    try:
+        with open("/etc/resolv.conf") as f:
+            servers = [line.split()[1] for line in f if line.startswith("nameserver")]
+    except OSError:
+        servers = []
+    if servers[:1] != ["127.0.0.1"]:
+        pytest.skip("the resolver is not 127.0.0.1")
+    dns = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        dns.bind(("127.0.0.1", 53))  # a DNS server that never answers
+    except OSError as e:
+        dns.close()
+        pytest.skip(f"cannot stand in for the resolver: {e}")
+    kube = nat.FakeKubeServer()
+    kube.start()
+    try:
+        kube.add_deployment("default", "w", 2)
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": "t"}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = dict(os.environ, AWS_ACCESS_KEY_ID="AKID", AWS_SECRET_ACCESS_KEY="secret", KUBE_CONFIG_PATH=str(kc),
+                   HOME=str(tmp_path))
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        child = subprocess.Popen([sys.executable, "-m", "kube_sqs_autoscaler_amd", "--aws-region=us-east-1",
+                                  "--sqs-endpoint=http://sqs.hung-dns.example.com", "--poll-period=100ms",
+                                  "--sqs-queue-url=http://sqs.hung-dns.example.com/1/q", "--kubernetes-deployment=w",
+                                  "--api-timeout=30s", "--log-level=error"], cwd=root, env=env,
+                                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        deadline = time.monotonic() + 60
+        dns.settimeout(1.0)
+        while time.monotonic() < deadline:  # wait for the poll's lookup to reach the "server"
+            try:
+                dns.recvfrom(512)
+                break
+            except socket.timeout:
+                assert child.poll() is None
+        time.sleep(0.5)  # past the warm-up's 100 ms dial: the poll's own lookup is waiting now
+        t0 = time.monotonic()
+        child.send_signal(signal.SIGTERM)
+        _, err = child.communicate(timeout=60)
+        took = time.monotonic() - t0
+        assert child.returncode == 0, err[-2000:]
+        assert took < 2.0, took  # not the rest of the 30 s lookup budget
+    finally:
+        dns.close()
+        kube.stop()
