@@ -59,16 +59,22 @@ LOW = {"ApproximateNumberOfMessages": "0", "ApproximateNumberOfMessagesDelayed":
 
 
 def proc_stats(pid: int, tree: bool = False) -> dict:
-    """fds, threads and RSS of ``pid`` -- summed over it and its descendants with ``tree``."""
+    """fds, threads and RSS of ``pid`` -- summed over it and its descendants with ``tree``, which
+    adds their PSS (proportional set size: shared pages split between the processes)."""
     pids = [pid]
     if tree:
         import psutil
 
         pids += [c.pid for c in psutil.Process(pid).children(recursive=True)]
     out = {"fds": 0, "rss_kb": 0, "threads": 0}
+    if tree:
+        out["pss_kb"] = 0  # summed RSS counts the pages the workers share with the supervisor once each
     for p in pids:
         try:
             out["fds"] += len(os.listdir(f"/proc/{p}/fd"))
+            if tree:
+                with open(f"/proc/{p}/smaps_rollup") as f:
+                    out["pss_kb"] += sum(int(line.split()[1]) for line in f if line.startswith("Pss:"))
             with open(f"/proc/{p}/status") as f:
                 for line in f:
                     if line.startswith("VmRSS:"):
