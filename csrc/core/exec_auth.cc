@@ -7,6 +7,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 #include <map>
@@ -111,7 +112,7 @@ Status validate_exec_config(const ExecConfig& cfg) {
   return Status::OK();
 }
 
-Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code) {
+Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code, const std::atomic<bool>* abort) {
   Status v = validate_exec_config(cfg);
   if (!v.ok()) return Result<ExecCredential>::Err(v);
   const bool interactive = isatty(STDIN_FILENO) == 1;
@@ -147,16 +148,20 @@ Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code)
   const int64_t deadline_ms = cfg.timeout > 0 ? cfg.timeout / kMillisecond : -1;
   RealClock rc_clock;
   const Nanos start = rc_clock.now();
-  bool timed_out = false;
+  bool timed_out = false, aborted = false;
   for (;;) {
-    int wait_ms = -1;
+    if (abort && abort->load(std::memory_order_acquire)) {
+      aborted = true;
+      break;
+    }
+    int wait_ms = abort ? 20 : -1;
     if (deadline_ms >= 0) {
       const int64_t left = deadline_ms - (rc_clock.now() - start) / kMillisecond;
       if (left <= 0) {
         timed_out = true;
         break;
       }
-      wait_ms = static_cast<int>(left);
+      wait_ms = wait_ms < 0 ? static_cast<int>(left) : static_cast<int>(std::min<int64_t>(left, wait_ms));
     }
     struct pollfd p = {fds[0], POLLIN, 0};
     int pr = poll(&p, 1, wait_ms);
@@ -171,10 +176,11 @@ Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code)
     out.append(buf, static_cast<size_t>(n));
   }
   close(fds[0]);
-  if (timed_out) kill(pid, SIGKILL);
+  if (timed_out || aborted) kill(pid, SIGKILL);
   int status = 0;
   while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
   }
+  if (aborted) return Result<ExecCredential>::Err(Status::Err("request canceled"));
   if (timed_out) {
     return Result<ExecCredential>::Err(Status::Err("exec: executable " + cfg.command + " timed out after " +
                                                    std::to_string(cfg.timeout / kMillisecond) + "ms"));
@@ -203,19 +209,20 @@ Result<ExecCredential> ExecTokenProvider::current() {
     return last_;
   }
   running_ = true;
+  abort_.store(false, std::memory_order_relaxed);
   const int code = pending_code_;
   ++runs_;
   lk.unlock();
   Result<ExecCredential> r;
   try {
-    r = run_exec_plugin(cfg_, code);
+    r = run_exec_plugin(cfg_, code, &abort_);
   } catch (const std::exception& e) {  // the waiters must be released whatever happens
     r = Result<ExecCredential>::Err(Status::Err(e.what()));
   }
   lk.lock();
   running_ = false;
   if (!r.ok()) {
-    r = Result<ExecCredential>::Err(r.status.wrap("getting credentials"));
+    if (r.status.message() != "request canceled") r = Result<ExecCredential>::Err(r.status.wrap("getting credentials"));
   } else {
     cached_ = r.value;
     have_ = true;
@@ -233,6 +240,11 @@ Result<std::string> ExecTokenProvider::token() {
   auto c = current();
   if (!c.ok()) return Result<std::string>::Err(c.status);
   return Result<std::string>::Ok(c.value.token);
+}
+
+void ExecTokenProvider::cancel() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (running_) abort_.store(true, std::memory_order_release);
 }
 
 void ExecTokenProvider::invalidate(const std::string& used) {

@@ -9,6 +9,7 @@
 // rebuilt on posix_spawn so the worker threads never call back into Python for a token.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <condition_variable>
 #include <mutex>
@@ -43,7 +44,10 @@ Status validate_exec_config(const ExecConfig& cfg);
 
 // Runs the plugin once and parses its ExecCredential. `response_code` != 0 is passed to
 // v1alpha1 plugins in KUBERNETES_EXEC_INFO (spec.response.code), as client-go does on 401.
-Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code = 0);
+// `abort` (optional): set by another thread, the plugin is killed and the run ends with
+// "request canceled" (checked every 20 ms).
+Result<ExecCredential> run_exec_plugin(const ExecConfig& cfg, int response_code = 0,
+                                       const std::atomic<bool>* abort = nullptr);
 
 class ExecTokenProvider final : public TokenProvider {
  public:
@@ -53,6 +57,9 @@ class ExecTokenProvider final : public TokenProvider {
   // a hanging or failing plugin costs the queues of a process one run, not one each.
   Result<std::string> token() override;
   void invalidate(const std::string& used) override;
+  // Kills the run in flight, if any (a stopping client): it and its waiters end with
+  // "request canceled"; the cached credential, if any, stays.
+  void cancel() override;
   // The whole current credential (client certificate included), refreshed like token().
   Result<ExecCredential> credential();
   uint64_t runs() const;
@@ -68,6 +75,7 @@ class ExecTokenProvider final : public TokenProvider {
   int pending_code_ = 0;  // 401 seen on the cached token
   ExecCredential cached_;
   bool running_ = false;
+  std::atomic<bool> abort_{false};  // cancel() of the run in flight
   uint64_t finished_ = 0;
   Result<ExecCredential> last_;  // the outcome of the last run
   uint64_t runs_ = 0;

@@ -226,6 +226,7 @@ KubeRestDeployments::KubeRestDeployments(KubeOptions opts)
 
 void KubeRestDeployments::cancel() {
   cancel_.request_stop();
+  if (opts_.token) opts_.token->cancel();  // an exec plugin run this client waits for
   if (http_) http_->cancel();
 }
 

@@ -84,6 +84,9 @@ class TokenProvider {
   // token, so the next token() fetches a fresh one (client-go's exec authenticator and token
   // file source both refresh on 401).
   virtual void invalidate(const std::string& used) { (void)used; }
+  // A client of this source stops (its API's cancel()): a fetch in flight is abandoned and its
+  // waiters get "request canceled". Later calls fetch as usual. Default: nothing to interrupt.
+  virtual void cancel() {}
 };
 
 class StaticTokenProvider final : public TokenProvider {

@@ -1040,6 +1040,33 @@ TEST(exec_provider_shared_across_threads) {
   CHECK_EQ(failed.load(), 8);
   CHECK(q->runs() <= uint64_t(2));
   CHECK(mono_ns() - t0 < 1500 * kMillisecond);
+  // A hanging plugin: a stopping client's cancel() kills the run, which ends with "request
+  // canceled" for it and its waiters, long before the plugin timeout.
+  const std::string hanging = std::string(dir) + "/hanging.sh";
+  {
+    std::FILE* f = std::fopen(hanging.c_str(), "w");
+    std::fputs("#!/bin/sh\nexec sleep 30\n", f);
+    std::fclose(f);
+  }
+  chmod(hanging.c_str(), 0755);
+  cfg.command = hanging;
+  cfg.timeout = 20 * kSecond;
+  auto h = std::make_shared<ExecTokenProvider>(cfg, std::make_shared<RealClock>());
+  std::atomic<int> canceled{0};
+  ts.clear();
+  const int64_t t1 = mono_ns();
+  for (int t = 0; t < 3; ++t)
+    ts.emplace_back([&] {
+      auto r = h->token();
+      if (!r.ok() && r.status.message() == "request canceled") ++canceled;
+    });
+  std::this_thread::sleep_for(std::chrono::milliseconds(200));
+  h->cancel();
+  for (auto& t : ts) t.join();
+  CHECK_EQ(canceled.load(), 3);
+  CHECK(mono_ns() - t1 < 3 * kSecond);
+  CHECK_EQ(h->runs(), uint64_t(1));
+  std::remove(hanging.c_str());
   std::remove(failing.c_str());
   std::remove((std::string(dir) + "/runs").c_str());
   std::remove(script.c_str());
