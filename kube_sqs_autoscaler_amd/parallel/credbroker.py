@@ -54,6 +54,7 @@ class CredentialBroker:
         self._last_fetch: Dict[str, int] = {}
         self.fetches = 0
         self.fetches_by_region: Dict[str, int] = {r: 0 for r in self.regions}
+        self.refresh_errors = 0  # failed refreshes ahead of time (the set in the slot kept)
 
     def provider_for(self, region: str, clock=None):
         """A worker's credential source for ``region`` (call it in the worker, after the fork)."""
@@ -83,8 +84,13 @@ class CredentialBroker:
             self.fetches_by_region[region] += 1
             try:
                 nat.publish_credentials(addr, self._chain(region).retrieve())
-            except Exception as e:  # noqa: BLE001 -- every worker waiting on the slot gets the error
-                nat.publish_credential_error(addr, str(e))
+            except Exception as e:  # noqa: BLE001
+                # Every worker waiting on the slot gets the error. A refresh ahead of time that
+                # fails leaves the current set in place (it still signs) and is tried again.
+                if asked:
+                    nat.publish_credential_error(addr, str(e))
+                else:
+                    self.refresh_errors += 1
         return n
 
     def start(self) -> None:

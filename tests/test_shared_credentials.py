@@ -191,6 +191,45 @@ def test_worker_processes_share_one_fetch_per_expiry(nat, tmp_path):
         kube.stop()
 
 
+def test_failed_refresh_ahead_of_time_keeps_the_set(nat):
+    """The broker refreshes a set a minute before the workers' window; when that fetch fails (an
+    ECS / IMDS hiccup) the set in the slot, still good, stays -- a worker reading the slot then
+    still gets it -- and the refresh is tried again later. An error reaches the slot only when a
+    worker waits for a new set (as the SDK fails a call whose refresh fails inside its window)."""
+    from kube_sqs_autoscaler_amd.parallel.credbroker import MIN_REFRESH_NS, CredentialBroker
+
+    clock = nat.VirtualClock()
+    calls = []
+
+    class Flaky(nat.CredentialsProvider):
+        def retrieve(self):
+            calls.append(1)
+            if len(calls) in (2, 4):
+                raise RuntimeError("EC2RoleRequestError: connection refused")
+            return nat.Credentials("AKID", "secret", f"tok-{len(calls)}", clock.unix_nanos() + 3600 * SEC, "Test")
+
+    broker = CredentialBroker(["us-east-1"], clock=clock, providers={"us-east-1": Flaky()})
+    try:
+        addr = broker.addrs["us-east-1"]
+        assert broker.serve_once() == 1 and nat.read_credential_slot(addr)[2] == 1
+        clock.advance(3600 * SEC - 330 * SEC)  # 5.5 min left: the broker's lead, not yet the workers' window
+        assert broker.serve_once() == 1 and broker.refresh_errors == 1  # fetch 2 fails
+        creds, err, gen = nat.read_credential_slot(addr)
+        assert (creds.session_token, err, gen) == ("tok-1", "", 1)  # kept
+        worker = nat.SlotCredentialsProvider(addr, clock, 300 * SEC, 2 * SEC)
+        assert worker.retrieve().session_token == "tok-1"
+        assert broker.serve_once() == 0  # not again before MIN_REFRESH_NS
+        clock.advance(MIN_REFRESH_NS)
+        assert broker.serve_once() == 1 and nat.read_credential_slot(addr)[0].session_token == "tok-3"
+        # a worker that waits for a new set gets the error of a failing fetch
+        worker.stale(worker.retrieve())
+        assert broker.serve_once() == 1  # fetch 4 fails, asked for
+        with pytest.raises(nat.NativeError, match="EC2RoleRequestError"):
+            worker.retrieve()
+    finally:
+        broker.close()
+
+
 def test_credential_slot_limits_and_regions(nat):
     """A set too large for the slot reaches the workers as an error, not a torn read; each region
     has a slot of its own, fetched with its own chain."""
