@@ -181,6 +181,7 @@ class ProcessFleet:
             self.workers.append(ProcWorker(t, SlotRunner(self.addrs[i], scaler), pid))
         self._started = False
         self._stopped = False
+        self._stop_at = 0.0
         self._reaped = {}
         self._lock = threading.Lock()
 
@@ -220,7 +221,14 @@ class ProcessFleet:
         for a in self.addrs:  # the workers start together
             nat.set_shared_worker_control(a, 1)
 
+    # A worker still alive this long after a stop is stuck in something a stop does not end; it
+    # is killed, so the pod's shutdown never rests on the kubelet's SIGKILL after the grace
+    # period (30 s by default).
+    KILL_AFTER_S = 10.0
+
     def stop(self) -> None:
+        if not self._stopped:
+            self._stop_at = time.monotonic()
         self._stopped = True
         nat = native()
         for a in self.addrs:
@@ -266,8 +274,14 @@ class ProcessFleet:
     def join(self) -> None:
         if not self._started:
             self.stop()
-        while not self.wait(1.0):
-            pass
+        while not self.wait(0.2):
+            if self._stopped and time.monotonic() - self._stop_at > self.KILL_AFTER_S:
+                for w in self.workers:
+                    if w.pid not in self._reaped:
+                        try:
+                            os.kill(w.pid, signal.SIGKILL)
+                        except ProcessLookupError:
+                            pass
 
     def failed(self) -> List[int]:
         """Indices of workers that exited with an error or were killed (an OOM kill, a crash).

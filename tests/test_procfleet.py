@@ -269,3 +269,25 @@ def test_shared_error_slot_truncates_on_a_character_boundary(nat):
     nat.write_shared_worker_error(addr, "later")  # a shorter text replaces a longer one
     assert nat.read_shared_worker_error(addr) == "later"
     del addr
+
+
+def test_stuck_worker_is_killed_after_the_stop_deadline(nat):
+    """A worker that a stop cannot end (here: stuck building its clients, deaf to SIGTERM) is
+    SIGKILLed KILL_AFTER_S after the stop, so the supervisor's exit never waits on it."""
+    from types import SimpleNamespace
+
+    def stuck():
+        while True:
+            time.sleep(0.05)
+
+    fleet = ProcessFleet([stuck], [SimpleNamespace(name="d", queue_url="q", min_pods=1, max_pods=8)])
+    fleet.KILL_AFTER_S = 0.5
+    try:
+        time.sleep(0.2)
+        t0 = time.monotonic()
+        fleet.stop()
+        fleet.join()
+        assert time.monotonic() - t0 < 5.0
+        assert fleet.exit_codes() == [-signal.SIGKILL]
+    finally:
+        fleet.close()
