@@ -29,7 +29,9 @@ credential broker (parallel/credbroker.py) fetches the next set SECONDS after th
 every 10 s) and the workers switch to the newest a minute after that (their 5-minute window);
 without it the one shared provider per region refreshes SECONDS plus a minute after issue. The
 summary counts the endpoint's fetches, which must stay at one per refresh for the whole fleet,
-not one per queue, and names the session token of the last poll.
+not one per queue, and names the session token of the last poll. ``--ecs-outage START:SECONDS``
+makes the endpoint answer 500 for a while (an agent restart): the sets already fetched keep
+signing, so no poll may fail for it.
 
 ``--hot``: the old back-to-back soak of one queue (no faults), p50/p99 per window.
 """
@@ -93,16 +95,29 @@ class EcsEndpoint:
     ``refresh_s`` plus 6 minutes after it is issued -- the broker's 5-minute window plus 1-minute
     lead (parallel/credbroker.py) put its refresh ``refresh_s`` after issue."""
 
-    def __init__(self, refresh_s: float):
+    def __init__(self, refresh_s: float, outage=None):
+        """``outage``: (start, end) in time.monotonic() seconds during which every fetch fails
+        with a 500 (an ECS agent / Pod Identity agent restart)."""
         from datetime import datetime, timedelta, timezone
         from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
         ep = self
         self.fetches = 0
+        self.failed = 0
+        self.outage = outage
         self.lock = threading.Lock()
 
         class Handler(BaseHTTPRequestHandler):
             def do_GET(self):  # noqa: N802
+                if ep.outage and ep.outage[0] <= time.monotonic() < ep.outage[1]:
+                    with ep.lock:
+                        ep.failed += 1
+                    body = b'{"code":"InternalError","message":"agent restarting"}'
+                    self.send_response(500)
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return
                 with ep.lock:
                     ep.fetches += 1
                     n = ep.fetches
@@ -213,7 +228,11 @@ def cadenced(a) -> int:
     env = dict(os.environ, KUBE_CONFIG_PATH=kc, AWS_CA_BUNDLE=ca, HOME=tmp)
     ecs = None
     if a.ecs_refresh > 0:
-        ecs = EcsEndpoint(a.ecs_refresh)
+        outage = None
+        if a.ecs_outage:
+            start, length = (float(x) for x in a.ecs_outage.split(":"))
+            outage = (time.monotonic() + start, time.monotonic() + start + length)
+        ecs = EcsEndpoint(a.ecs_refresh, outage)
         for k in ("AWS_ACCESS_KEY_ID", "AWS_SECRET_ACCESS_KEY", "AWS_SESSION_TOKEN", "AWS_PROFILE"):
             env.pop(k, None)
         env.update(AWS_CONTAINER_CREDENTIALS_FULL_URI=ecs.url, AWS_EC2_METADATA_DISABLED="true")
@@ -341,7 +360,8 @@ def cadenced(a) -> int:
         # shared provider refreshes a minute later in each set's life than the broker does)
         most = 2 + int(elapsed / a.ecs_refresh)
         summary["credentials"] = {"refresh_s": a.ecs_refresh, "fetches": ecs.fetches, "at_most": most,
-                                  "last_poll_token": tokens_seen[-1] if tokens_seen else None}
+                                  "last_poll_token": tokens_seen[-1] if tokens_seen else None,
+                                  "outage_s": a.ecs_outage or None, "failed_fetches": ecs.failed}
         summary["ok"] = summary["ok"] and ecs.fetches <= most
     if not summary["ok"]:
         summary["stderr_tail"] = stderr_tail
@@ -394,6 +414,8 @@ def main() -> int:
     ap.add_argument("--worker-processes", action="store_true", help="run the CLI with --worker-processes")
     ap.add_argument("--ecs-refresh", type=float, default=0.0,
                     help="seconds between credential refreshes from a container-credentials endpoint (0: static keys)")
+    ap.add_argument("--ecs-outage", default="",
+                    help="START:SECONDS -- the credential endpoint answers 500 for SECONDS from START s into the soak")
     a = ap.parse_args()
     return hot(a) if a.hot else cadenced(a)
 
