@@ -92,16 +92,17 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     if cfg.trace_file:
         trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
 
-    # one AWS credential source per region for the process's queues; under --worker-processes the
-    # supervisor keeps it and the workers read it through shared memory (parallel/credbroker.py)
-    creds: dict = {}
-    broker = None
+    # One AWS credential source per region for the process's queues: a broker thread runs the
+    # chain ahead of expiry and publishes each set into shared memory, where every queue reads it
+    # (parallel/credbroker.py) -- worker threads here, or worker processes, which inherit the
+    # mapping. No queue's poll or warm-up runs a fetch, a refresh that fails ahead of time keeps
+    # the set that still signs, and a stop never waits for a fetch.
+    from .parallel.credbroker import CredentialBroker
+
+    broker = CredentialBroker({t.region or cfg.aws_region for t in cfg.targets}, env)
     if cfg.worker_processes:
         # fork the workers first: before this process starts threads or touches the GPU
-        from .parallel.credbroker import CredentialBroker
         from .parallel.procfleet import ProcessFleet
-
-        broker = CredentialBroker({t.region or cfg.aws_region for t in cfg.targets}, env)
 
         def build(t):
             def make():
@@ -116,7 +117,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         broker.start()  # after the fork: the supervisor's own thread
         workers = fleet.workers
     else:
-        workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi, credentials_cache=creds)
+        workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi,
+                                         credentials=broker.provider_for(t.region or cfg.aws_region))
                    for t in cfg.targets]
         if trace_fd >= 0:
             for w in workers:
@@ -124,6 +126,7 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         from .parallel.fleet import Fleet
 
         fleet = Fleet(workers, cfg.worker_threads)
+        broker.start()
 
     capper = None
     if cfg.gpu_aware_max:
@@ -150,13 +153,7 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
         health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets],
                         leader_elect=cfg.leader_elect, failure_window_ns=cfg.readiness_failure_window_ns)
-        if broker is not None:
-            def credential_fetches():
-                return dict(broker.fetches_by_region)
-        else:
-            def credential_fetches():
-                return {region: p.fetches() for region, p in list(creds.items())}
-        metrics = MetricsServer(fleet, cfg.metrics_addr, health, credential_fetches)
+        metrics = MetricsServer(fleet, cfg.metrics_addr, health, lambda: dict(broker.fetches_by_region))
         metrics.start()
         log.log("info", f"Serving metrics on {cfg.metrics_addr}")
 
@@ -235,7 +232,10 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
             metrics.stop()
         if cfg.worker_processes:
             fleet.close()
-            broker.close()
+        if cfg.worker_processes or fleet.wait(0):
+            broker.close()  # no queue reads the slots any more
+        else:
+            broker.stop()  # threads still running (an exception left them): keep the slots mapped
         if trace_fd >= 0:
             os.close(trace_fd)
     return 0

@@ -1,13 +1,15 @@
-"""The process fleet's one AWS credential source (csrc/core/cred_slot.h).
+"""The CLI's one AWS credential source per region (csrc/core/cred_slot.h).
 
-``--worker-processes`` forks one worker per queue. The reference fetches credentials once per
-process and expiry (one session, /root/reference/sqs/sqs.go:36); a fleet of N worker processes
-running the chain each would make N STS / ECS / IMDS calls per expiry. :class:`CredentialBroker`
-keeps the chain in the supervisor instead: one ``SharedCredentialSlot`` per region in an
-anonymous shared mapping (created before the workers fork, so they inherit it), a supervisor
-thread that fills each slot ahead of its expiry or when a worker asks (a set about to expire, or
-one the service rejected), and in each worker a native ``SlotCredentialsProvider`` that reads the
-slot and waits for the next set when its own is no longer good.
+The reference fetches credentials once per process and expiry (one session,
+/root/reference/sqs/sqs.go:36); N queues each running the chain would make N STS / ECS / IMDS
+calls per expiry. :class:`CredentialBroker` keeps the chain in one thread of the CLI process:
+one ``SharedCredentialSlot`` per region in an anonymous shared mapping (created before
+``--worker-processes`` forks its workers, so they inherit it), a thread that fills each slot a
+minute ahead of the queues' refresh window or when a queue asks (a set about to expire, or one
+the service rejected), and in each queue -- worker thread or worker process -- a native
+``SlotCredentialsProvider`` that reads the slot and waits (cancellably) for the next set when
+its own is no longer good. No poll or warm-up runs a fetch, and a refresh that fails ahead of
+time keeps the set that still signs.
 """
 from __future__ import annotations
 

@@ -1,8 +1,11 @@
-"""One AWS credential source per process and chain configuration (sigv4.h SharedCredentialsProvider).
+"""One AWS credential source per process and region.
 
 The reference builds one session per process (/root/reference/sqs/sqs.go:36), so one credential
 fetch per expiry. Round 4 gave every tracked queue a chain of its own: N queues made N STS / ECS /
-IMDS fetches at every expiry, each a Python urllib call on a worker thread.
+IMDS fetches at every expiry, each a Python urllib call on a worker thread. The CLI's queues
+(threads or processes) now read one broker's sets from shared memory (parallel/credbroker.py,
+cred_slot.h); a library user sharing a ``credentials_cache`` between ``new_runner`` calls gets
+one ``SharedCredentialsProvider`` (sigv4.h) per region instead.
 """
 import json
 import threading
@@ -277,15 +280,15 @@ class _HungEcs(BaseHTTPRequestHandler):
 
 @pytest.mark.slow
 @pytest.mark.serial  # a stop's wall time: a loaded host (xdist) slows the processes' exit
-@pytest.mark.parametrize("mode,queues,limit_s", [("processes", 2, 1.8), ("threads", 3, 7.0)])
+@pytest.mark.parametrize("mode,queues,limit_s", [("processes", 2, 1.8), ("threads", 3, 1.8)])
 def test_stop_while_waiting_for_credentials(nat, tmp_path, mode, queues, limit_s):
     """SIGTERM while the queues wait for credentials from a hung endpoint (the chain's ECS
-    fetch times out after 5 s). ``--worker-processes``: the workers wait for the supervisor's
-    first set (cred_slot.h); the waits are cancelled with their API calls (Runner::stop ->
-    SlotCredentialsProvider::cancel) and the broker's thread is not waited for, so the process
-    exits at once. Threads: the queues share the one fetch in flight (SharedCredentialsProvider)
-    instead of queueing a 5 s fetch each, so the stop waits out that fetch's rest (under 5 s)
-    rather than 5 s per queue (3 queues: about 12 s before)."""
+    fetch times out after 5 s). The CLI's queues -- worker threads or worker processes -- wait
+    for the broker's first set (cred_slot.h); the waits are cancelled with their API calls
+    (Runner::stop -> SlotCredentialsProvider::cancel) and the broker's thread, inside the fetch,
+    is not waited for, so the process exits at once (round 5 before the broker served the thread
+    fleet: 7.4 s with 2 queues, each queueing a fetch of its own; then 2.4 s, the queues sharing
+    the one fetch in flight)."""
     import os
     import signal
     import subprocess
