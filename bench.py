@@ -213,6 +213,34 @@ def _cadence_rows(args, pipeline: bool, bp: int, hot_p50_ms: float, deadline: fl
     }
 
 
+def _cadence_cpus(mode: str):
+    """The CPUs the cadence rows run on (``--cadence-cpus``): ``auto`` confines this process --
+    the autoscaler's threads and the endpoint processes it starts, which inherit it -- to the
+    first ceil(quota) of the CPUs it may use when a cgroup CPU quota allows fewer cores than
+    that (at least 4), so the rows' threads stay on a compact set of cores the quota can feed
+    instead of spreading over the whole host (256 CPUs and a 16-core quota on the MI355X box:
+    profiles/r05x had the 8-queue cell 1.3-1.4x the 1-queue cell in every round against
+    never-sleeping endpoints). ``off``: no change; a number: that many CPUs. Returns the CPU
+    list, or None when unchanged."""
+    import math
+
+    if mode == "off":
+        return None
+    allowed = sorted(os.sched_getaffinity(0))
+    if mode == "auto":
+        from kube_sqs_autoscaler_amd.ops import native
+
+        quota, period = native().read_cpu_quota()
+        if not quota:
+            return None
+        n = max(4, math.ceil(quota / period))
+    else:
+        n = max(1, int(mode))
+    if n >= len(allowed):
+        return None
+    return allowed[:n]
+
+
 def _pct(v, p: float) -> int:
     """Nearest-rank percentile of ``v`` (ns)."""
     import math
@@ -376,6 +404,9 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence-queue-rounds", type=int, default=3,
                     help="interleaved rounds of the 1/2/4/8-queue rows; each cell pools its rounds' samples")
     ap.add_argument("--no-cadence", action="store_true", help="skip the production-cadence rows")
+    ap.add_argument("--cadence-cpus", default="auto",
+                    help="CPUs the production-cadence rows run on: auto (the first ceil(cgroup CPU quota) CPUs, at "
+                         "least 4, when the quota is below the CPUs allowed), off, or a count")
     ap.add_argument("--pin-ranks", default="auto", choices=["auto", "on", "off"],
                     help="confine each rank of a multi-rank job to its own slice of this process's CPUs, as N "
                          "autoscaler pods with CPU limits are (auto: on when the job has more than one rank)")
@@ -573,8 +604,19 @@ def main(argv=None) -> int:
         if world == 1 and not args.no_sweep:
             guarded("secondary_rows", secondary)
         if world == 1 and not args.no_sweep and not args.no_cadence:
-            guarded("cadence_rows", lambda: extra.update(
-                _cadence_rows(args, pipeline, bp, p50, deadline=t_start + args.extras_budget_s)))
+            def cadence():
+                cpus = _cadence_cpus(args.cadence_cpus)
+                before = os.sched_getaffinity(0)
+                if cpus:
+                    os.sched_setaffinity(0, cpus)
+                    extra["cadenced_rows_cpus"] = f"{cpus[0]}-{cpus[-1]}" if cpus == list(range(cpus[0], cpus[-1] + 1)) \
+                        else cpus
+                try:
+                    extra.update(_cadence_rows(args, pipeline, bp, p50, deadline=t_start + args.extras_budget_s))
+                finally:
+                    os.sched_setaffinity(0, before)
+
+            guarded("cadence_rows", cadence)
         guarded("decision_parity", parity, budgeted=False)  # seconds; part of the metric's name
         # The driver keeps the tail of stdout: the per-row detail goes first, the summary rows last.
         summary = ("wan_model_sqs2ms_kube1ms_p50_ms", "tls_p50_ms", "reference_equivalent_p50_ms",
