@@ -22,7 +22,9 @@ sequential and reference-equivalent paths, TLS, a regional-RTT model, per-phase 
 wire-path decision parity and apiserver requests per poll on the Appendix C traces; and the
 production-cadence rows (250 ms and 1 s poll periods, 1/2/4/8 and 16 queues, sleeping and
 busy-polling endpoints, the regional-RTT model at 1 s, the default and reference-equivalent paths
-as paired arms of each run, each with its worker CPU per poll: ``_cadence_rows``).
+as paired arms of each run, each with its worker CPU per poll: ``_cadence_rows``), run on the
+first ceil(cgroup CPU quota) CPUs when the quota allows fewer cores than the CPUs visible
+(``--cadence-cpus``, recorded as ``cadenced_rows_cpus``).
 
 Launch: ``python bench.py --gpus N`` with N > 1 outside a launcher starts the N ranks itself
 (child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set,
