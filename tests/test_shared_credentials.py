@@ -112,6 +112,58 @@ def test_eight_queues_one_fetch_per_expiry(nat, tmp_path):
         kube.stop()
 
 
+@pytest.mark.slow
+def test_library_workers_share_one_provider(nat, tmp_path):
+    """A library user building workers with ``new_runner(..., credentials_cache=cache)`` (not the
+    CLI, which uses the broker) gets one ``SharedCredentialsProvider`` per region: 8 queues, one
+    ECS fetch per expiry, decisions unchanged."""
+    from kube_sqs_autoscaler_amd import autoscaler
+    from kube_sqs_autoscaler_amd.config import parse_args
+    from kube_sqs_autoscaler_amd.parallel.fleet import Fleet
+    from kube_sqs_autoscaler_amd.utils.log import make_logger
+
+    _Ecs.fetches = 0
+    ecs = ThreadingHTTPServer(("127.0.0.1", 0), _Ecs)
+    threading.Thread(target=ecs.serve_forever, daemon=True).start()
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, REGION)
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    try:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"HOME": str(tmp_path), "KUBE_CONFIG_PATH": str(kc), "AWS_EC2_METADATA_DISABLED": "true",
+               "AWS_CONTAINER_CREDENTIALS_FULL_URI": f"http://127.0.0.1:{ecs.server_address[1]}/creds"}
+        specs = []
+        for i in range(8):
+            url = f"{sqs.url}/123/q{i}"
+            sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500" if i % 2 == 0 else "0"})
+            kube.add_deployment("gpu", f"w{i}", 4)
+            specs += ["--queue", f"url={url},deployment=w{i},namespace=gpu,attribute-names=ApproximateNumberOfMessages"]
+        cfg = parse_args([f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", "--poll-period=100ms",
+                          "--scale-up-cool-down=0s", "--scale-down-cool-down=0s", *specs], env)
+        rest = autoscaler.load_rest_config(cfg, env)
+        cache: dict = {}
+        workers = [autoscaler.new_runner(t, cfg, rest, make_logger("error", "text"), nat.RealClock(), environ=env,
+                                         credentials_cache=cache) for t in cfg.targets]
+        assert list(cache) == [REGION] and isinstance(cache[REGION], nat.SharedCredentialsProvider)
+        fleet = Fleet(workers)
+        fleet.start(25)  # 2.5 s: across the first set's refresh point (5 min + 1.5 s)
+        fleet.join()
+        assert _Ecs.fetches == 2 == cache[REGION].fetches()
+        assert sqs.signature_failures() == 0
+        assert [kube.replicas("gpu", f"w{i}") for i in range(8)] == [8, 1] * 4
+    finally:
+        ecs.shutdown()
+        sqs.stop()
+        kube.stop()
+
+
 def test_credential_slot_between_processes(nat):
     """cred_slot.h: the supervisor publishes a set, a worker reads it, asks for the next when its
     copy nears expiry, and gets it once the supervisor publishes; an error reaches the waiter."""
