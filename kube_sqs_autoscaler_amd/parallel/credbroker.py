@@ -5,7 +5,7 @@ The reference fetches credentials once per process and expiry (one session,
 calls per expiry. :class:`CredentialBroker` keeps the chain in one thread of the CLI process:
 one ``SharedCredentialSlot`` per region in an anonymous shared mapping (created before
 ``--worker-processes`` forks its workers, so they inherit it), a thread that fills each slot a
-minute ahead of the queues' refresh window or when a queue asks (a set about to expire, or one
+while ahead of the queues' refresh window (up to 15 minutes) or when a queue asks (a set about to expire, or one
 the service rejected), and in each queue -- worker thread or worker process -- a native
 ``SlotCredentialsProvider`` that reads the slot and waits (cancellably) for the next set when
 its own is no longer good. No poll or warm-up runs a fetch, and a refresh that fails ahead of
@@ -21,13 +21,24 @@ from typing import Dict, Iterable, Mapping, Optional
 from ..ops import native
 from ..sqs.credentials import make_chain_provider
 
-# Workers refresh their copy 5 minutes before expiry (CachedCredentials); the broker fills the
-# slot a minute before that, so a worker finds the next set already there -- but not more often
-# than every MIN_REFRESH_NS on its own (a set that lives less than that lead is fetched when a
-# worker asks).
+# Queues refresh their copy 5 minutes before expiry (CachedCredentials, the SDK's window). The
+# broker fills the slot ahead of that, so a queue finds the next set already there: halfway
+# between its fetch and the queues' window, at most MAX_LEAD_NS early (an hour-long set: 15
+# minutes ahead of the window, so a credential endpoint may be down that long without a poll
+# failing; a short set is not refetched over and over) -- and not more often than every
+# MIN_REFRESH_NS on its own (a refresh that failed is retried that often).
 WORKER_WINDOW_NS = 5 * 60 * 1_000_000_000
-BROKER_LEAD_NS = 60 * 1_000_000_000
+MAX_LEAD_NS = 15 * 60 * 1_000_000_000
 MIN_REFRESH_NS = 10 * 1_000_000_000
+
+
+def refresh_due_at(fetched_at_ns: int, expires_ns: int) -> Optional[int]:
+    """When the broker refreshes a set it fetched at ``fetched_at_ns`` (None: never, for a set
+    that does not expire)."""
+    if not expires_ns:
+        return None
+    lead = min(MAX_LEAD_NS, max(0, (expires_ns - fetched_at_ns - WORKER_WINDOW_NS) // 2))
+    return expires_ns - WORKER_WINDOW_NS - lead
 
 
 class CredentialBroker:
@@ -54,6 +65,7 @@ class CredentialBroker:
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self._last_fetch: Dict[str, int] = {}
+        self._due_at: Dict[str, Optional[int]] = {}  # when each region's set is refreshed ahead of time
         self.fetches = 0
         self.fetches_by_region: Dict[str, int] = {r: 0 for r in self.regions}
         self.refresh_errors = 0  # failed refreshes ahead of time (the set in the slot kept)
@@ -74,10 +86,9 @@ class CredentialBroker:
         n = 0
         for region, addr in self.addrs.items():
             now = self.clock.unix_nanos()
-            _, _, gen = nat.read_credential_slot(addr)
-            asked = gen == 0 or nat.credential_slot_needs_fetch(addr, now, 0)  # none yet, a worker asked, expired
-            due = (nat.credential_slot_needs_fetch(addr, now, WORKER_WINDOW_NS + BROKER_LEAD_NS)
-                   and now - self._last_fetch.get(region, 0) >= MIN_REFRESH_NS)
+            asked = nat.credential_slot_needs_fetch(addr, now, 0)  # none yet, a worker asked, expired
+            due_at = self._due_at.get(region)
+            due = due_at is not None and now >= due_at and now - self._last_fetch.get(region, 0) >= MIN_REFRESH_NS
             if not (asked or due):
                 continue
             self._last_fetch[region] = now
@@ -85,7 +96,9 @@ class CredentialBroker:
             self.fetches += 1
             self.fetches_by_region[region] += 1
             try:
-                nat.publish_credentials(addr, self._chain(region).retrieve())
+                creds = self._chain(region).retrieve()
+                nat.publish_credentials(addr, creds)
+                self._due_at[region] = refresh_due_at(now, creds.expires_unix_ns)
             except Exception as e:  # noqa: BLE001
                 # Every worker waiting on the slot gets the error. A refresh ahead of time that
                 # fails leaves the current set in place (it still signs) and is tried again.

@@ -24,12 +24,12 @@ summary line has the mismatch count (must be 0) and whether fds / threads / RSS 
 ``--worker-processes``: the CLI runs one worker process per queue (resources are then summed over
 the supervisor and its workers). ``--ecs-refresh SECONDS``: the AWS credentials come from a
 container-credentials endpoint (AWS_CONTAINER_CREDENTIALS_FULL_URI) whose every set expires
-6 minutes plus SECONDS after it is issued. Under ``--worker-processes`` the supervisor's
-credential broker (parallel/credbroker.py) fetches the next set SECONDS after the last (at most
-every 10 s) and the workers switch to the newest a minute after that (their 5-minute window);
-without it the one shared provider per region refreshes SECONDS plus a minute after issue. The
-summary counts the endpoint's fetches, which must stay at one per refresh for the whole fleet,
-not one per queue, and names the session token of the last poll. ``--ecs-outage START:SECONDS``
+5 minutes plus twice SECONDS after it is issued. The CLI's credential broker
+(parallel/credbroker.py) refreshes a set halfway between its fetch and the queues' 5-minute
+window -- SECONDS after the last fetch (at most every 10 s) -- and the queues switch to the
+newest SECONDS after that, when their own copy enters the window. The summary counts the
+endpoint's fetches, which must stay at one per refresh for the whole fleet, not one per queue,
+and names the session token of the last poll. ``--ecs-outage START:SECONDS``
 makes the endpoint answer 500 for a while (an agent restart): the sets already fetched keep
 signing, so no poll may fail for it.
 
@@ -91,9 +91,10 @@ def proc_stats(pid: int, tree: bool = False) -> dict:
 
 
 class EcsEndpoint:
-    """A container-credentials endpoint: every set is new (its own session token) and expires
-    ``refresh_s`` plus 6 minutes after it is issued -- the broker's 5-minute window plus 1-minute
-    lead (parallel/credbroker.py) put its refresh ``refresh_s`` after issue."""
+    """A container-credentials endpoint: every set is new (its own session token) and expires 5
+    minutes plus twice ``refresh_s`` after it is issued -- the broker (parallel/credbroker.py
+    ``refresh_due_at``) refreshes it ``refresh_s`` after issue, halfway to the queues' 5-minute
+    window."""
 
     def __init__(self, refresh_s: float, outage=None):
         """``outage``: (start, end) in time.monotonic() seconds during which every fetch fails
@@ -121,7 +122,7 @@ class EcsEndpoint:
                 with ep.lock:
                     ep.fetches += 1
                     n = ep.fetches
-                expires = datetime.now(timezone.utc) + timedelta(minutes=6, seconds=refresh_s)
+                expires = datetime.now(timezone.utc) + timedelta(minutes=5, seconds=2 * refresh_s)
                 body = json.dumps({"AccessKeyId": AKID, "SecretAccessKey": SECRET, "Token": f"soak-session-{n}",
                                    "Expiration": expires.strftime("%Y-%m-%dT%H:%M:%S.%fZ")}).encode()
                 self.send_response(200)
@@ -356,8 +357,7 @@ def cadenced(a) -> int:
         "ok": rc == 0 and all(r.ok for r in replays) and all(v and v["flat"] for v in flat.values()),
     }
     if ecs is not None:
-        # one fetch at start-up, then one per refresh for the whole fleet (the thread fleet's
-        # shared provider refreshes a minute later in each set's life than the broker does)
+        # one fetch at start-up, then one per refresh for the whole fleet
         most = 2 + int(elapsed / a.ecs_refresh)
         summary["credentials"] = {"refresh_s": a.ecs_refresh, "fetches": ecs.fetches, "at_most": most,
                                   "last_poll_token": tokens_seen[-1] if tokens_seen else None,

@@ -246,8 +246,22 @@ def test_worker_processes_share_one_fetch_per_expiry(nat, tmp_path):
         kube.stop()
 
 
+def test_refresh_lead():
+    """credbroker.refresh_due_at: halfway between the fetch and the queues' 5-minute window, at
+    most 15 minutes before the window -- an hour-long set is refreshed 20 minutes before it
+    expires (a credential endpoint may be down 15 minutes without a poll failing); a short set
+    halfway through; one that does not expire never."""
+    from kube_sqs_autoscaler_amd.parallel.credbroker import refresh_due_at
+
+    m = 60 * SEC
+    assert refresh_due_at(0, 60 * m) == 40 * m
+    assert refresh_due_at(0, 6 * m) == 30 * SEC
+    assert refresh_due_at(0, 4 * m) == -1 * m  # already inside the window: at once (MIN_REFRESH_NS apart)
+    assert refresh_due_at(0, 0) is None
+
+
 def test_failed_refresh_ahead_of_time_keeps_the_set(nat):
-    """The broker refreshes a set a minute before the workers' window; when that fetch fails (an
+    """The broker refreshes a set ahead of the workers' window; when that fetch fails (an
     ECS / IMDS hiccup) the set in the slot, still good, stays -- a worker reading the slot then
     still gets it -- and the refresh is tried again later. An error reaches the slot only when a
     worker waits for a new set (as the SDK fails a call whose refresh fails inside its window)."""
