@@ -23,11 +23,12 @@ from ..sqs.credentials import make_chain_provider
 
 # Queues refresh their copy 5 minutes before expiry (CachedCredentials, the SDK's window). The
 # broker fills the slot ahead of that, so a queue finds the next set already there: halfway
-# between its fetch and the queues' window, at most MAX_LEAD_NS early (an hour-long set: 15
-# minutes ahead of the window, so a credential endpoint may be down that long without a poll
-# failing; a short set is not refetched over and over) -- and not more often than every
-# MIN_REFRESH_NS on its own (a refresh that failed is retried that often).
+# between its fetch and the queues' window, but at least MIN_LEAD_NS and at most MAX_LEAD_NS
+# early (an hour-long set: 15 minutes ahead of the window, so a credential endpoint may be down
+# that long without a poll failing) -- and not more often than every MIN_REFRESH_NS on its own
+# (a refresh that failed is retried that often; so is a set too short for the minimum lead).
 WORKER_WINDOW_NS = 5 * 60 * 1_000_000_000
+MIN_LEAD_NS = 60 * 1_000_000_000
 MAX_LEAD_NS = 15 * 60 * 1_000_000_000
 MIN_REFRESH_NS = 10 * 1_000_000_000
 
@@ -37,7 +38,8 @@ def refresh_due_at(fetched_at_ns: int, expires_ns: int) -> Optional[int]:
     that does not expire)."""
     if not expires_ns:
         return None
-    lead = min(MAX_LEAD_NS, max(0, (expires_ns - fetched_at_ns - WORKER_WINDOW_NS) // 2))
+    before_window = max(0, expires_ns - fetched_at_ns - WORKER_WINDOW_NS)
+    lead = min(MAX_LEAD_NS, before_window, max(MIN_LEAD_NS, before_window // 2))
     return expires_ns - WORKER_WINDOW_NS - lead
 
 

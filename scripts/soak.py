@@ -23,11 +23,10 @@ summary line has the mismatch count (must be 0) and whether fds / threads / RSS 
 
 ``--worker-processes``: the CLI runs one worker process per queue (resources are then summed over
 the supervisor and its workers). ``--ecs-refresh SECONDS``: the AWS credentials come from a
-container-credentials endpoint (AWS_CONTAINER_CREDENTIALS_FULL_URI) whose every set expires
-5 minutes plus twice SECONDS after it is issued. The CLI's credential broker
-(parallel/credbroker.py) refreshes a set halfway between its fetch and the queues' 5-minute
-window -- SECONDS after the last fetch (at most every 10 s) -- and the queues switch to the
-newest SECONDS after that, when their own copy enters the window. The summary counts the
+container-credentials endpoint (AWS_CONTAINER_CREDENTIALS_FULL_URI) whose every set lives just
+long enough for the CLI's credential broker (parallel/credbroker.py) to refresh it SECONDS
+after the last fetch (at most every 10 s); the queues switch to the newest when their own copy
+enters its 5-minute window. The summary counts the
 endpoint's fetches, which must stay at one per refresh for the whole fleet, not one per queue,
 and names the session token of the last poll. ``--ecs-outage START:SECONDS``
 makes the endpoint answer 500 for a while (an agent restart): the sets already fetched keep
@@ -91,10 +90,11 @@ def proc_stats(pid: int, tree: bool = False) -> dict:
 
 
 class EcsEndpoint:
-    """A container-credentials endpoint: every set is new (its own session token) and expires 5
-    minutes plus twice ``refresh_s`` after it is issued -- the broker (parallel/credbroker.py
-    ``refresh_due_at``) refreshes it ``refresh_s`` after issue, halfway to the queues' 5-minute
-    window."""
+    """A container-credentials endpoint: every set is new (its own session token) and lives long
+    enough past the queues' 5-minute window for the broker (parallel/credbroker.py
+    ``refresh_due_at``) to refresh it ``refresh_s`` after issue: twice ``refresh_s`` past the
+    window (the lead is half of that), or a minute more than ``refresh_s`` when that half would be
+    under the broker's one-minute minimum lead."""
 
     def __init__(self, refresh_s: float, outage=None):
         """``outage``: (start, end) in time.monotonic() seconds during which every fetch fails
@@ -103,6 +103,9 @@ class EcsEndpoint:
         from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
         ep = self
+        # a set the broker refreshes refresh_s after issue (credbroker.refresh_due_at: half the
+        # time before the queues' window, but at least a minute early)
+        life_past_window = 2 * refresh_s if refresh_s >= 60 else refresh_s + 60
         self.fetches = 0
         self.failed = 0
         self.outage = outage
@@ -122,7 +125,7 @@ class EcsEndpoint:
                 with ep.lock:
                     ep.fetches += 1
                     n = ep.fetches
-                expires = datetime.now(timezone.utc) + timedelta(minutes=5, seconds=2 * refresh_s)
+                expires = datetime.now(timezone.utc) + timedelta(minutes=5, seconds=life_past_window)
                 body = json.dumps({"AccessKeyId": AKID, "SecretAccessKey": SECRET, "Token": f"soak-session-{n}",
                                    "Expiration": expires.strftime("%Y-%m-%dT%H:%M:%S.%fZ")}).encode()
                 self.send_response(200)

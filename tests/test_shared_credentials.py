@@ -248,15 +248,19 @@ def test_worker_processes_share_one_fetch_per_expiry(nat, tmp_path):
 
 def test_refresh_lead():
     """credbroker.refresh_due_at: halfway between the fetch and the queues' 5-minute window, at
-    most 15 minutes before the window -- an hour-long set is refreshed 20 minutes before it
-    expires (a credential endpoint may be down 15 minutes without a poll failing); a short set
-    halfway through; one that does not expire never."""
+    least 1 and at most 15 minutes before the window -- an hour-long set is refreshed 20 minutes
+    before it expires (a credential endpoint may be down 15 minutes without a poll failing), a
+    15-minute one 10 minutes before; a set shorter than that minimum at once (MIN_REFRESH_NS
+    apart); one that does not expire never."""
     from kube_sqs_autoscaler_amd.parallel.credbroker import refresh_due_at
 
     m = 60 * SEC
     assert refresh_due_at(0, 60 * m) == 40 * m
-    assert refresh_due_at(0, 6 * m) == 30 * SEC
-    assert refresh_due_at(0, 4 * m) == -1 * m  # already inside the window: at once (MIN_REFRESH_NS apart)
+    assert refresh_due_at(0, 15 * m) == 5 * m
+    assert refresh_due_at(0, 8 * m) == 90 * SEC  # halfway through the 3 minutes before the window
+    assert refresh_due_at(0, 6 * m + 30 * SEC) == 30 * SEC  # the 1-minute minimum lead, not 45 s
+    assert refresh_due_at(0, 6 * m) == 0  # at once
+    assert refresh_due_at(0, 4 * m) == -1 * m  # already inside the window: at once
     assert refresh_due_at(0, 0) is None
 
 
