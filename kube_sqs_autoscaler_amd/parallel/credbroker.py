@@ -47,8 +47,8 @@ class CredentialBroker:
     def __init__(self, regions: Iterable[str], environ: Optional[Mapping[str, str]] = None, clock=None,
                  poll_s: float = 0.2, providers: Optional[Dict[str, object]] = None):
         """``providers``: the chain per region (default: the SDK chain for that region).
-        ``poll_s``: how often the supervisor's thread looks at the slots -- what a worker that asks
-        for a new set waits at most on top of the fetch (5 wake-ups a second: a fraction of a
+        ``poll_s``: how often the serving thread looks at the slots -- what a queue that asks for a
+        new set waits at most on top of the fetch (5 wake-ups a second: a fraction of a
         millicore)."""
         nat = native()
         self.regions = sorted(set(regions))
@@ -73,7 +73,7 @@ class CredentialBroker:
         self.refresh_errors = 0  # failed refreshes ahead of time (the set in the slot kept)
 
     def provider_for(self, region: str, clock=None):
-        """A worker's credential source for ``region`` (call it in the worker, after the fork)."""
+        """A queue's credential source for ``region`` (a worker process calls it after the fork)."""
         return native().SlotCredentialsProvider(self.addrs[region], clock or native().RealClock(), WORKER_WINDOW_NS)
 
     def _chain(self, region: str):
@@ -111,7 +111,7 @@ class CredentialBroker:
         return n
 
     def start(self) -> None:
-        """The supervisor's serving thread (start it after the workers have forked)."""
+        """The serving thread (with ``--worker-processes``, start it after the workers have forked)."""
         if self._thread is not None:
             return
 
