@@ -114,7 +114,6 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
             return make
 
         fleet = ProcessFleet([build(t) for t in cfg.targets], cfg.targets)
-        broker.start()  # after the fork: the supervisor's own thread
         workers = fleet.workers
     else:
         workers = [autoscaler.new_runner(t, cfg, rest, log, clock, environ=env, tag_queue=multi,
@@ -126,7 +125,6 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
         from .parallel.fleet import Fleet
 
         fleet = Fleet(workers, cfg.worker_threads)
-        broker.start()
 
     capper = None
     if cfg.gpu_aware_max:
@@ -197,6 +195,7 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
                 health.set_role("leader")
 
         log.log("info", "Starting kube-sqs-autoscaler")  # main.go:114
+        broker.start()  # (after any worker process has forked) the queues' first sets
         fleet.start(max_iterations)
         worker_died = False
         while not fleet.wait(0.2):
