@@ -135,7 +135,8 @@ class CredentialBroker:
         return True
 
     def close(self) -> None:
-        if not self.stop():
+        # an idle serving thread ends at once; one inside a fetch is not waited for
+        if not self.stop(timeout=0.1):
             return  # the thread may still publish into the slots: leave them mapped
         del self._buf
         self._mm.close()
