@@ -10,11 +10,18 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(args, timeout=240, env=None):
+def _run(args, timeout=240, env=None, soak=False):
+    """The script's JSON lines. ``soak``: a short soak's exit status also reflects whether fds /
+    threads / RSS stayed flat over its two steady windows, which an 18 s run with a fault every
+    2 s can miss by a reconnect in flight at a sample; the caller checks the summary's decisions
+    itself (flatness is what the 10-minute box soaks show, profiles/r05p/ and later)."""
     r = subprocess.run([sys.executable, *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout,
                        env=dict(os.environ, **(env or {})))
-    assert r.returncode == 0, r.stderr[-2000:]
-    return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    rows = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    if soak and r.returncode == 1 and rows and rows[-1].get("summary"):
+        return rows
+    assert r.returncode == 0, (r.stderr[-2000:], r.stdout.strip().splitlines()[-1:])
+    return rows
 
 
 def test_cadence_5s_script(nat):
@@ -32,9 +39,9 @@ def test_cadence_arms_script(nat):
 @pytest.mark.slow
 def test_soak_script_short(nat):
     rows = _run(["scripts/soak.py", "--minutes", "0.3", "--window", "6", "--queues", "2", "--fault-every", "2",
-                 "--presend"], timeout=200)
+                 "--presend"], timeout=200, soak=True)
     summary = rows[-1]
-    assert summary["summary"] and summary["replay"]["mismatches"] == 0 and summary["exit_code"] == 0
+    assert summary["summary"] and summary["replay"]["mismatches"] == 0 and summary["exit_code"] == 0, summary
     # the per-client transport counters of /metrics reach the window rows: with --poll-presend the
     # warm-up stages the polls' SQS requests (1 s period)
     windows = [r for r in rows if "window" in r and "scrape_error" not in r]
@@ -51,9 +58,10 @@ def test_soak_script_worker_processes_rotating_credentials(nat):
     set once their own copy enters its 5-minute window, past this short run: the box soaks show
     it, profiles/r05p/.)"""
     rows = _run(["scripts/soak.py", "--minutes", "0.3", "--window", "6", "--queues", "3", "--fault-every", "2",
-                 "--worker-processes", "--ecs-refresh", "5"], timeout=200)
+                 "--worker-processes", "--ecs-refresh", "5"], timeout=200, soak=True)
     summary = rows[-1]
-    assert summary["ok"] and summary["replay"]["mismatches"] == 0 and summary["signature_failures"] == 0
+    assert summary["exit_code"] == 0 and summary["replay"]["mismatches"] == 0, summary
+    assert summary["signature_failures"] == 0
     creds = summary["credentials"]
     assert 2 <= creds["fetches"] <= creds["at_most"], creds
     assert summary["last_metrics"]["processes"] == 4  # the supervisor and 3 workers
