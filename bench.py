@@ -48,6 +48,74 @@ sys.path.insert(0, ROOT)
 
 METRIC = "poll→scale-patch p50 latency (ms); decision parity vs ref on synthetic trace"
 
+# The driver parses the LAST line of stdout out of an 8,000-character tail; round 5's 24.6 KB
+# line lost its head there and was recorded unparsed (BENCH_r05.json). The line therefore holds
+# the headline keys and the summary rows only, compact and at most LINE_LIMIT bytes; the full
+# result (per-round cells, phase breakdowns, setups) goes to the --detail-out file it names.
+LINE_LIMIT = 4096
+# extra keys carried on the line, most important first; past LINE_LIMIT the last go first
+LINE_EXTRA_KEYS = ("samples", "p90_ms", "p99_ms", "signature_failures", "tracked_queues", "ranks",
+                   "collective_backend", "rehearsal_shared_gpus", "decision_parity", "skipped_sections",
+                   "section_errors", "p50_ms_by_tracked_queues", "wan_cadenced_p50_ms", "cpu_ms_per_poll",
+                   "cadenced_reference_over_default", "cadenced_p50_ms_by_tracked_queues")
+
+
+def result_line(out: dict, detail: str | None) -> str:
+    """The one stdout line of ``out`` (the full result): every top-level key, ``parallelism``
+    lifted out of ``config``, and an ``extra`` of LINE_EXTRA_KEYS only -- the decision parity as
+    its fraction and poll count, section errors cut to 200 characters -- plus ``detail``, the file
+    holding everything. Rows are dropped from the end of LINE_EXTRA_KEYS (and named under
+    ``dropped_from_line``) until the line fits LINE_LIMIT bytes."""
+    full = out.get("extra", {})
+    extra = {k: full[k] for k in LINE_EXTRA_KEYS if k in full}
+    if isinstance(extra.get("decision_parity"), dict):
+        dp = extra["decision_parity"]
+        agree = total = 0
+        for row in (dp.get("configs") or {}).values():
+            a, b = str(row.get("agree", "0/0")).split("/")
+            agree, total = agree + int(a), total + int(b)
+        extra["decision_parity"] = {"fraction": dp.get("fraction"), "polls": f"{agree}/{total}"}
+    if "section_errors" in extra:
+        extra["section_errors"] = {k: str(v)[:200] for k, v in extra["section_errors"].items()}
+    extra["detail"] = detail
+    line = {k: v for k, v in out.items() if k != "extra"}
+    line["parallelism"] = out.get("config", {}).get("parallelism")
+    line["extra"] = extra
+
+    def dumps() -> str:
+        return json.dumps(line, separators=(",", ":"), ensure_ascii=False)
+
+    s = dumps()
+    for k in reversed(LINE_EXTRA_KEYS):
+        if len(s.encode()) <= LINE_LIMIT:
+            break
+        if k in extra:
+            del extra[k]
+            extra.setdefault("dropped_from_line", []).append(k)
+            s = dumps()
+    if len(s.encode()) > LINE_LIMIT:  # only the headline is left: cut the free-text fields
+        line["data"] = str(line.get("data", ""))[:200]
+        line["config"] = {**line.get("config", {}), "model": str(line.get("config", {}).get("model", ""))[:300]}
+        s = dumps()
+    return s
+
+
+def write_detail(out: dict, path: str) -> str | None:
+    """The full result as JSON at ``path`` (written to a temporary name, then renamed); the path
+    written, or None when it cannot be written (the line then says so)."""
+    try:
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            json.dump(out, f, indent=1)
+            f.write("\n")
+        os.replace(tmp, path)
+        return path
+    except OSError as e:
+        _progress(f"--detail-out {path}: {e}")
+        return None
+
 
 def _parity_summary() -> dict:
     """Decision parity of the timed configuration: the five Appendix C scenarios through the
@@ -418,6 +486,9 @@ def main(argv=None) -> int:
     ap.add_argument("--extras-budget-s", type=float, default=400.0,
                     help="seconds after start past which the remaining secondary sections and cadence rows are skipped "
                          "(recorded under extra.skipped_sections); the headline line is always printed")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="file for the full result (every row and breakdown); the stdout line carries the headline "
+                         "and summary rows only, at most 4096 bytes, and names this file ('' : none)")
     args = ap.parse_args(argv)
     if args.gpus < 1 or args.queues < 1:
         ap.error("--gpus and --queues must be at least 1")
@@ -620,13 +691,6 @@ def main(argv=None) -> int:
 
             guarded("cadence_rows", cadence)
         guarded("decision_parity", parity, budgeted=False)  # seconds; part of the metric's name
-        # The driver keeps the tail of stdout: the per-row detail goes first, the summary rows last.
-        summary = ("wan_model_sqs2ms_kube1ms_p50_ms", "tls_p50_ms", "reference_equivalent_p50_ms",
-                   "sequential_scale_p50_ms", "p50_ms_by_tracked_queues_worker_processes", "p50_ms_by_tracked_queues",
-                   "cadenced_vs_hot_loop_default_plain", "cadenced_reference_over_default", "cadenced_p50_ms",
-                   "cadenced_by_tracked_queues_8_over_1", "cadenced_p50_ms_by_tracked_queues", "wan_cadenced_p50_ms",
-                   "cpu_ms_per_poll")
-        extra = {**{k: v for k, v in extra.items() if k not in summary}, **{k: extra[k] for k in summary if k in extra}}
         out = {
             "metric": METRIC,
             "value": round(p50, 4),
@@ -651,7 +715,8 @@ def main(argv=None) -> int:
             },
             "extra": extra,
         }
-        os.write(result_fd, (json.dumps(out) + "\n").encode())
+        detail = write_detail(out, args.detail_out) if args.detail_out else None
+        os.write(result_fd, (result_line(out, detail) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
