@@ -256,7 +256,9 @@ PYBIND11_MODULE(_ksa_native, m) {
   auto cs = [](uintptr_t addr) { return reinterpret_cast<SharedCredentialSlot*>(addr); };
   m.def("credential_slot_size", [] { return sizeof(SharedCredentialSlot); });
   m.def("init_credential_slot", [](uintptr_t addr) { init_credential_slot(reinterpret_cast<void*>(addr)); });
-  m.def("publish_credentials", [cs](uintptr_t addr, const Credentials& c) { publish_credentials(cs(addr), c); });
+  m.def("publish_credentials", [cs](uintptr_t addr, const Credentials& c, const std::string& refresh_error) {
+    publish_credentials(cs(addr), c, refresh_error);
+  }, py::arg("addr"), py::arg("creds"), py::arg("refresh_error") = "");
   m.def("publish_credential_error", [cs](uintptr_t addr, const std::string& e) { publish_credential_error(cs(addr), e); });
   m.def("read_credential_slot", [cs](uintptr_t addr) -> py::tuple {
     Credentials c;
@@ -266,16 +268,38 @@ PYBIND11_MODULE(_ksa_native, m) {
     return py::make_tuple(py::cast(c), error, gen);
   });
   m.def("request_credentials", [cs](uintptr_t addr, uint64_t gen) { request_credentials(cs(addr), gen); });
+  m.def("reject_credentials", [cs](uintptr_t addr, uint64_t gen) { reject_credentials(cs(addr), gen); });
+  m.def("credential_slot_still_signs", [cs](uintptr_t addr, int64_t unix_now, int64_t skew) {
+    return credential_slot_still_signs(cs(addr), unix_now, skew);
+  });
+  // the slot's counters and the refresh error of a set kept after a failed refresh
+  m.def("credential_slot_info", [cs](uintptr_t addr) {
+    auto* s = cs(addr);
+    Credentials c;
+    std::string error, refresh_error;
+    uint64_t gen = 0;
+    read_credential_slot(s, &c, &error, &gen, &refresh_error);
+    py::dict d;
+    d["generation"] = gen;
+    d["wanted"] = s->wanted.load();
+    d["rejected"] = s->rejected.load();
+    d["stale_signs"] = s->stale_signs.load();
+    d["error"] = error;
+    d["refresh_error"] = refresh_error;
+    return d;
+  });
+  m.attr("CREDENTIAL_STALE_SKEW_NS") = kStaleSkew;
   m.def("credential_slot_needs_fetch", [cs](uintptr_t addr, int64_t unix_now, int64_t window) {
     return credential_slot_needs_fetch(cs(addr), unix_now, window);
   });
   py::class_<SlotCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "SlotCredentialsProvider")
-      .def(py::init([cs](uintptr_t addr, std::shared_ptr<Clock> clock, int64_t window_ns, int64_t wait_limit_ns) {
+      .def(py::init([cs](uintptr_t addr, std::shared_ptr<Clock> clock, int64_t window_ns, int64_t wait_limit_ns,
+                         int64_t skew_ns) {
              return std::make_shared<SlotCredentialsProvider>(cs(addr), [clock] { return clock->unix_nanos(); },
-                                                              window_ns, wait_limit_ns);
+                                                              window_ns, wait_limit_ns, skew_ns);
            }),
            py::arg("addr"), py::arg("clock"), py::arg("expiry_window_ns") = 5LL * 60 * kSecond,
-           py::arg("wait_limit_ns") = 15 * kSecond)
+           py::arg("wait_limit_ns") = 15 * kSecond, py::arg("skew_ns") = kStaleSkew)
       .def("stale", &SlotCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>())
       .def("cancel", &SlotCredentialsProvider::cancel);
   py::class_<SharedCredentialsProvider, CredentialsProvider, py::smart_holder>(m, "SharedCredentialsProvider")
@@ -286,7 +310,8 @@ PYBIND11_MODULE(_ksa_native, m) {
            py::arg("inner"), py::arg("clock"), py::arg("expiry_window_ns") = 5LL * 60 * kSecond)
       // the lock may be held by a fetch waiting for the GIL (a Python inner provider)
       .def("fetches", &SharedCredentialsProvider::fetches, py::call_guard<py::gil_scoped_release>())
-      .def("stale", &SharedCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>());
+      .def("stale", &SharedCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>())
+      .def("cancel", &SharedCredentialsProvider::cancel, py::call_guard<py::gil_scoped_release>());
 
   py::class_<SigV4Signer, std::shared_ptr<SigV4Signer>>(m, "SigV4Signer")
       .def(py::init<std::string, std::string>(), py::arg("region"), py::arg("service"))
@@ -993,8 +1018,8 @@ PYBIND11_MODULE(_ksa_native, m) {
         py::arg("model"), py::arg("params"), py::arg("seeds"), py::arg("seed0") = 1, py::arg("threads") = 8,
         py::arg("arith") = 0);
 
-  m.attr("HTTP_TIMING") = kHttpTiming;
-  m.attr("HTTP_MAX_SPIN_THROUGH_NS") = HttpClient::kMaxSpinThrough;  // false in the image build (-DKSA_HTTP_TIMING=0)
+  m.attr("HTTP_TIMING") = kHttpTiming;  // false in the image build (-DKSA_HTTP_TIMING=0)
+  m.attr("HTTP_MAX_SPIN_THROUGH_NS") = HttpClient::kMaxSpinThrough;
   m.attr("SECOND") = kSecond;
   m.attr("MILLISECOND") = kMillisecond;
   m.attr("MICROSECOND") = kMicrosecond;

@@ -10,7 +10,7 @@ namespace ksa {
 
 namespace {
 
-enum Part : int { kAkid = 0, kSecret = 1, kToken = 2, kName = 3, kError = 4, kParts = 5 };
+enum Part : int { kAkid = 0, kSecret = 1, kToken = 2, kName = 3, kError = 4, kRefreshError = 5, kParts = 6 };
 
 void nap(Nanos ns) {
   struct timespec ts = {static_cast<time_t>(ns / kSecond), static_cast<long>(ns % kSecond)};
@@ -50,6 +50,8 @@ SharedCredentialSlot* init_credential_slot(void* at) {
   s->seq.store(0, std::memory_order_relaxed);
   s->generation.store(0, std::memory_order_relaxed);
   s->wanted.store(0, std::memory_order_relaxed);
+  s->rejected.store(0, std::memory_order_relaxed);
+  s->stale_signs.store(0, std::memory_order_relaxed);
   s->expires_unix_ns.store(0, std::memory_order_relaxed);
   for (auto& l : s->len) l.store(0, std::memory_order_relaxed);
   for (auto& w : s->words) w.store(0, std::memory_order_relaxed);
@@ -57,8 +59,9 @@ SharedCredentialSlot* init_credential_slot(void* at) {
   return s;
 }
 
-void publish_credentials(SharedCredentialSlot* s, const Credentials& c) {
-  const std::string parts[kParts] = {c.access_key_id, c.secret_access_key, c.session_token, c.provider_name, ""};
+void publish_credentials(SharedCredentialSlot* s, const Credentials& c, const std::string& refresh_error) {
+  const std::string parts[kParts] = {c.access_key_id, c.secret_access_key, c.session_token, c.provider_name, "",
+                                     refresh_error};
   publish_parts(s, parts, c.expires_unix_ns);
 }
 
@@ -68,7 +71,8 @@ void publish_credential_error(SharedCredentialSlot* s, const std::string& error)
   publish_parts(s, parts, 0);
 }
 
-bool read_credential_slot(const SharedCredentialSlot* s, Credentials* c, std::string* error, uint64_t* generation) {
+bool read_credential_slot(const SharedCredentialSlot* s, Credentials* c, std::string* error, uint64_t* generation,
+                          std::string* refresh_error) {
   for (int attempt = 0; attempt < 4096; ++attempt) {
     const uint64_t gen = s->generation.load(std::memory_order_acquire);
     const uint64_t before = s->seq.load(std::memory_order_acquire);
@@ -106,6 +110,7 @@ bool read_credential_slot(const SharedCredentialSlot* s, Credentials* c, std::st
     c->provider_name = parts[kName];
     c->expires_unix_ns = expires;
     *error = parts[kError];
+    if (refresh_error) *refresh_error = parts[kRefreshError];
     *generation = gen;
     return true;
   }
@@ -119,6 +124,14 @@ void request_credentials(SharedCredentialSlot* s, uint64_t generation) {
   }
 }
 
+void reject_credentials(SharedCredentialSlot* s, uint64_t generation) {
+  uint64_t cur = s->rejected.load(std::memory_order_relaxed);
+  while (cur < generation &&
+         !s->rejected.compare_exchange_weak(cur, generation, std::memory_order_acq_rel, std::memory_order_relaxed)) {
+  }
+  request_credentials(s, generation);
+}
+
 bool credential_slot_needs_fetch(const SharedCredentialSlot* s, int64_t unix_now, int64_t window) {
   const uint64_t gen = s->generation.load(std::memory_order_acquire);
   if (gen == 0 || s->wanted.load(std::memory_order_acquire) >= gen) return true;
@@ -127,30 +140,59 @@ bool credential_slot_needs_fetch(const SharedCredentialSlot* s, int64_t unix_now
   return expires != 0 && unix_now + window >= expires;
 }
 
-Result<Credentials> SlotCredentialsProvider::retrieve() {
+bool credential_slot_still_signs(const SharedCredentialSlot* s, int64_t unix_now, int64_t skew) {
   Credentials c;
   std::string error;
   uint64_t gen = 0;
-  const bool have = read_credential_slot(slot_, &c, &error, &gen);
-  if (have && error.empty() && c.valid() && (c.expires_unix_ns == 0 || now_() + window_ < c.expires_unix_ns))
-    return Result<Credentials>::Ok(c);
-  // Nothing yet, an error, or a set about to expire: ask the supervisor for the next one.
+  if (!read_credential_slot(s, &c, &error, &gen) || !error.empty() || !c.valid()) return false;
+  if (s->rejected.load(std::memory_order_acquire) >= gen) return false;
+  return c.expires_unix_ns == 0 || unix_now + skew < c.expires_unix_ns;
+}
+
+Result<Credentials> SlotCredentialsProvider::ride(const Credentials& c) {
+  slot_->stale_signs.fetch_add(1, std::memory_order_relaxed);
+  return Result<Credentials>::Ok(c);
+}
+
+Result<Credentials> SlotCredentialsProvider::retrieve() {
+  Credentials c;
+  std::string error, refresh_error;
+  uint64_t gen = 0;
+  const bool have = read_credential_slot(slot_, &c, &error, &gen, &refresh_error);
+  // a set, not an error, that no worker saw the service reject (stale() marks the generation)
+  const bool good = have && error.empty() && c.valid() && slot_->rejected.load(std::memory_order_acquire) < gen;
+  int64_t now = now_();
+  if (good && (c.expires_unix_ns == 0 || now + window_ < c.expires_unix_ns)) return Result<Credentials>::Ok(c);
+  // Inside the window, but the supervisor's refresh failed and kept this set, which signs for a
+  // while yet: sign with it (the supervisor keeps retrying on its own) rather than wait and fail.
+  if (good && !refresh_error.empty() && now + skew_ < c.expires_unix_ns) return ride(c);
+  // Nothing yet, an error, a rejected set, or one about to expire: ask the supervisor for the next.
   request_credentials(slot_, have ? gen : 0);
   const int64_t deadline = mono_ns() + wait_limit_;
+  // The supervisor looks at the slots every 200 ms and a fetch takes milliseconds to seconds:
+  // the first looks come quickly, then the nap backs off to 5 ms (a handful of wake-ups a
+  // second per waiting queue while an endpoint hangs).
+  Nanos pause = 200 * kMicrosecond;
   while (mono_ns() < deadline) {
     if (cancelled_.load(std::memory_order_acquire)) return Result<Credentials>::Err(Status::Err("request canceled"));
-    nap(200 * kMicrosecond);
+    nap(pause);
+    pause = std::min<Nanos>(pause * 2, 5 * kMillisecond);
     Credentials next;
-    std::string next_error;
+    std::string next_error, next_refresh_error;
     uint64_t next_gen = 0;
-    if (read_credential_slot(slot_, &next, &next_error, &next_gen) && next_gen > gen) {
+    if (read_credential_slot(slot_, &next, &next_error, &next_gen, &next_refresh_error) && next_gen > gen) {
       if (!next_error.empty()) return Result<Credentials>::Err(Status::Err(next_error));
-      return Result<Credentials>::Ok(next);
+      if (next_refresh_error.empty()) return Result<Credentials>::Ok(next);
+      // the refresh this worker asked for failed and the set was kept: it signs until the skew
+      now = now_();
+      if (slot_->rejected.load(std::memory_order_acquire) < next_gen &&
+          (next.expires_unix_ns == 0 || now + skew_ < next.expires_unix_ns))
+        return ride(next);
+      return Result<Credentials>::Err(Status::Err(next_refresh_error));
     }
   }
   // No answer: a set that has not expired yet still signs.
-  if (have && error.empty() && c.valid() && (c.expires_unix_ns == 0 || now_() < c.expires_unix_ns))
-    return Result<Credentials>::Ok(c);
+  if (good && (c.expires_unix_ns == 0 || now_() < c.expires_unix_ns)) return Result<Credentials>::Ok(c);
   return Result<Credentials>::Err(Status::Err(
       have && !error.empty() ? error : "NoCredentialProviders: the supervisor published no credentials in time"));
 }
@@ -159,9 +201,11 @@ void SlotCredentialsProvider::stale(const Credentials& c) {
   Credentials cur;
   std::string error;
   uint64_t gen = 0;
+  // the set in the slot is the one the service rejected: no worker signs with it again, and the
+  // next retrieve() waits for its replacement (the SDK expires its cache before the retry)
   if (read_credential_slot(slot_, &cur, &error, &gen) && error.empty() && cur.access_key_id == c.access_key_id &&
       cur.session_token == c.session_token && cur.expires_unix_ns == c.expires_unix_ns)
-    request_credentials(slot_, gen);
+    reject_credentials(slot_, gen);
 }
 
 }  // namespace ksa

@@ -201,8 +201,9 @@ Result<Credentials> SharedCredentialsProvider::retrieve() {
   if (have_ && (cached_.expires_unix_ns == 0 || now_() + window_ < cached_.expires_unix_ns))
     return Result<Credentials>::Ok(cached_);
   if (fetching_) {  // another client is fetching: its outcome is this caller's too
-    const uint64_t ticket = fetched_;
-    done_.wait(lk, [&] { return fetched_ != ticket; });
+    const uint64_t ticket = fetched_, cancels = cancels_;
+    done_.wait(lk, [&] { return fetched_ != ticket || cancels_ != cancels; });
+    if (fetched_ == ticket) return Result<Credentials>::Err(Status::Err("request canceled"));
     return last_;
   }
   fetching_ = true;
@@ -222,6 +223,12 @@ Result<Credentials> SharedCredentialsProvider::retrieve() {
   fetched_++;
   done_.notify_all();
   return r;
+}
+
+void SharedCredentialsProvider::cancel() {
+  std::lock_guard<std::mutex> lk(mu_);  // never held across a fetch: quick
+  cancels_++;
+  done_.notify_all();
 }
 
 void SharedCredentialsProvider::stale(const Credentials& c) {

@@ -113,7 +113,9 @@ class alignas(kCacheLine) CachedCredentials {
 // process (/root/reference/sqs/sqs.go:36). Callers that arrive while a fetch is in flight wait
 // for that fetch and take its outcome, its error included: against a hung or failing endpoint
 // the N queues share one timeout rather than queueing N of them behind each other. `unix_now`
-// is the clock (wall time).
+// is the clock (wall time). cancel() (one client's Runner::stop) releases the callers waiting
+// for a fetch at that moment with "request canceled"; it does not stop the fetch, which the
+// other clients still wait for, and later calls wait as before -- the provider is shared.
 class SharedCredentialsProvider final : public CredentialsProvider {
  public:
   SharedCredentialsProvider(std::shared_ptr<CredentialsProvider> inner, std::function<int64_t()> unix_now,
@@ -121,6 +123,7 @@ class SharedCredentialsProvider final : public CredentialsProvider {
       : inner_(std::move(inner)), now_(std::move(unix_now)), window_(expiry_window_ns) {}
   Result<Credentials> retrieve() override;
   void stale(const Credentials& c) override;
+  void cancel() override;
   uint64_t fetches() const {
     std::lock_guard<std::mutex> lk(mu_);
     return fetches_;
@@ -136,6 +139,7 @@ class SharedCredentialsProvider final : public CredentialsProvider {
   Credentials cached_;
   bool fetching_ = false;
   uint64_t fetched_ = 0;      // fetches finished
+  uint64_t cancels_ = 0;      // cancel() calls: a waiter that saw another count returns
   Result<Credentials> last_;  // the outcome of the last one
   uint64_t fetches_ = 0;
 };

@@ -1251,6 +1251,106 @@ TEST(credential_slot_wait_cancels) {
   CHECK(credential_slot_needs_fetch(slot, 0, 0));  // the request stays asked for
 }
 
+// After the service rejects a set (stale()), no worker of the slot signs with it again -- not
+// even before the supervisor has looked at the slot -- and the next retrieve() waits for the
+// replacement (the SDK expires its cache before retrying).
+TEST(credential_slot_rejected_set_not_resigned) {
+  auto mem = std::make_unique<SharedCredentialSlot>();
+  SharedCredentialSlot* slot = init_credential_slot(mem.get());
+  Credentials first;
+  first.access_key_id = "AKIDold";
+  first.secret_access_key = "s";
+  first.expires_unix_ns = 3600 * kSecond;
+  publish_credentials(slot, first);
+  SlotCredentialsProvider a(slot, [] { return int64_t(0); }, 300 * kSecond, 5 * kSecond);
+  SlotCredentialsProvider b(slot, [] { return int64_t(0); }, 300 * kSecond, 200 * kMillisecond);
+  auto r = a.retrieve();
+  CHECK(r.ok() && r.value.access_key_id == "AKIDold");
+  a.stale(r.value);
+  CHECK(slot->rejected.load() == 1 && credential_slot_needs_fetch(slot, 0, 0));
+  CHECK(!credential_slot_still_signs(slot, 0, kStaleSkew));
+  auto rb = b.retrieve();  // nobody answers: an error, not the rejected set
+  CHECK(!rb.ok() && rb.status.message().find("NoCredentialProviders") == 0);
+  std::thread supervisor([&] {
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    Credentials next = first;
+    next.access_key_id = "AKIDnew";
+    publish_credentials(slot, next);
+  });
+  auto ra = a.retrieve();
+  supervisor.join();
+  CHECK(ra.ok() && ra.value.access_key_id == "AKIDnew");
+}
+
+// A refresh that failed while the set still signs: the supervisor republishes the set with the
+// error and the workers, inside their window, sign with it at once (counted) until the set is
+// within the skew of its expiry; then they ask, and the chain's error reaches them.
+TEST(credential_slot_rides_out_a_failed_refresh) {
+  auto mem = std::make_unique<SharedCredentialSlot>();
+  SharedCredentialSlot* slot = init_credential_slot(mem.get());
+  Credentials c;
+  c.access_key_id = "AKID";
+  c.secret_access_key = "s";
+  c.expires_unix_ns = 420 * kSecond;
+  publish_credentials(slot, c);
+  std::atomic<int64_t> now{130 * kSecond};  // inside the 5-minute window
+  SlotCredentialsProvider w(slot, [&] { return now.load(); }, 300 * kSecond, 2 * kSecond);
+  CHECK(credential_slot_still_signs(slot, now, kStaleSkew));
+  publish_credentials(slot, c, "EcsCredentialsError: 500");
+  const int64_t t0 = mono_ns();
+  for (int i = 0; i < 100; ++i) CHECK(w.retrieve().ok());
+  CHECK(mono_ns() - t0 < kSecond);  // no waits
+  CHECK_EQ(slot->stale_signs.load(), uint64_t(100));
+  CHECK(!credential_slot_needs_fetch(slot, now, 0));  // nobody had to ask
+  now = 361 * kSecond;  // 59 s left: inside the skew
+  CHECK(!credential_slot_still_signs(slot, now, kStaleSkew));
+  std::thread supervisor([&] {
+    while (!credential_slot_needs_fetch(slot, now, 0)) std::this_thread::yield();
+    publish_credential_error(slot, "EcsCredentialsError: 500");
+  });
+  auto r = w.retrieve();
+  supervisor.join();
+  CHECK(!r.ok() && r.status.message() == "EcsCredentialsError: 500");
+  CHECK_EQ(slot->stale_signs.load(), uint64_t(100));
+}
+
+// SharedCredentialsProvider::cancel releases the callers waiting for another client's fetch
+// (a stop no longer waits out the whole fetch timeout); the fetch itself, and the
+// callers that come later, are unaffected.
+TEST(shared_provider_cancel_releases_waiters) {
+  struct Slow final : CredentialsProvider {
+    std::atomic<bool> go{false};
+    std::atomic<bool> in{false};
+    Result<Credentials> retrieve() override {
+      in = true;
+      while (!go) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      Credentials c;
+      c.access_key_id = "AKID";
+      c.secret_access_key = "s";
+      return Result<Credentials>::Ok(c);
+    }
+  };
+  auto inner = std::make_shared<Slow>();
+  SharedCredentialsProvider shared(inner, [] { return int64_t(0); }, 0);
+  Result<Credentials> fetched, waited;
+  std::thread fetcher([&] { fetched = shared.retrieve(); });
+  while (!inner->in) std::this_thread::yield();
+  std::atomic<bool> returned{false};
+  std::thread waiter([&] {
+    waited = shared.retrieve();
+    returned = true;
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  CHECK(!returned.load());
+  shared.cancel();
+  waiter.join();
+  CHECK(!waited.ok() && waited.status.message() == "request canceled");
+  inner->go = true;
+  fetcher.join();
+  CHECK(fetched.ok() && fetched.value.access_key_id == "AKID");
+  CHECK(shared.retrieve().ok() && shared.fetches() == 1);
+}
+
 TEST(spin_window_ceiling) {
   const Nanos us = kMicrosecond;
   CHECK_EQ(HttpClient::spin_window_for(25 * us, 15000 * us, 37500 * us), Nanos(0));

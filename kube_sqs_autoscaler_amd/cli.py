@@ -95,11 +95,13 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     # One AWS credential source per region for the process's queues: a broker thread runs the
     # chain ahead of expiry and publishes each set into shared memory, where every queue reads it
     # (parallel/credbroker.py) -- worker threads here, or worker processes, which inherit the
-    # mapping. No queue's poll or warm-up runs a fetch, a refresh that fails ahead of time keeps
-    # the set that still signs, and a stop never waits for a fetch.
+    # mapping. No queue's poll or warm-up runs a fetch, one region's hung endpoint never delays
+    # another's (a thread per region), a refresh that fails keeps the set while it still signs,
+    # and a stop never waits for a fetch.
     from .parallel.credbroker import CredentialBroker
 
-    broker = CredentialBroker({t.region or cfg.aws_region for t in cfg.targets}, env)
+    broker = CredentialBroker({t.region or cfg.aws_region for t in cfg.targets}, env,
+                              log=lambda lvl, m: log.log(lvl, m))
     if cfg.worker_processes:
         # fork the workers first: before this process starts threads or touches the GPU
         from .parallel.procfleet import ProcessFleet
@@ -151,7 +153,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
 
         health = Health(fleet, [Health.budget_ns(t.poll_period_ns, cfg.api_timeout_ns) for t in cfg.targets],
                         leader_elect=cfg.leader_elect, failure_window_ns=cfg.readiness_failure_window_ns)
-        metrics = MetricsServer(fleet, cfg.metrics_addr, health, lambda: dict(broker.fetches_by_region))
+        metrics = MetricsServer(fleet, cfg.metrics_addr, health, lambda: dict(broker.fetches_by_region),
+                                broker.stale_signs_by_region)
         metrics.start()
         log.log("info", f"Serving metrics on {cfg.metrics_addr}")
 

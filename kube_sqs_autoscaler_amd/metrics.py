@@ -116,12 +116,15 @@ class _Family:
 
 class FleetCollector:
     def __init__(self, fleet: Fleet, health: Optional["Health"] = None,
-                 credential_fetches: Optional[Callable[[], Dict[str, int]]] = None) -> None:
+                 credential_fetches: Optional[Callable[[], Dict[str, int]]] = None,
+                 credential_stale_signs: Optional[Callable[[], Dict[str, int]]] = None) -> None:
         """``credential_fetches``: the process's AWS credential fetches so far, per region (the
-        thread fleet's shared providers, or the process fleet's broker)."""
+        thread fleet's shared providers, or the process fleet's broker). ``credential_stale_signs``:
+        per region, the signatures made with a set kept after its refresh failed (the broker)."""
         self.fleet = fleet
         self.health = health
         self.credential_fetches = credential_fetches
+        self.credential_stale_signs = credential_stale_signs
 
     def families(self) -> List[_Family]:
         stats = self.fleet.stats()
@@ -176,6 +179,13 @@ class FleetCollector:
             for region, n in sorted(self.credential_fetches().items()):
                 creds.add("", [("region", region)], n)
             out.append(creds)
+        if self.credential_stale_signs is not None:
+            stale = _Family("ksa_aws_credential_stale_signs_total", "counter",
+                            "Signatures made with an AWS credential set inside its 5-minute refresh window because "
+                            "its refresh failed (the set still valid for more than a minute)")
+            for region, n in sorted(self.credential_stale_signs().items()):
+                stale.add("", [("region", region)], n)
+            out.append(stale)
         return out
 
     def exposition(self) -> bytes:
@@ -291,11 +301,13 @@ def _listen(host: str, port: int, handler) -> ThreadingHTTPServer:
 
 class MetricsServer:
     def __init__(self, fleet: Fleet, addr: str, health: Optional[Health] = None,
-                 credential_fetches: Optional[Callable[[], Dict[str, int]]] = None) -> None:
+                 credential_fetches: Optional[Callable[[], Dict[str, int]]] = None,
+                 credential_stale_signs: Optional[Callable[[], Dict[str, int]]] = None) -> None:
         self.fleet = fleet
         self.health = health or Health(fleet)
         hl = self.health
-        self.collector = FleetCollector(fleet, credential_fetches=credential_fetches)
+        self.collector = FleetCollector(fleet, credential_fetches=credential_fetches,
+                                        credential_stale_signs=credential_stale_signs)
         coll = self.collector
 
         class Handler(BaseHTTPRequestHandler):

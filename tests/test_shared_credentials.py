@@ -266,9 +266,10 @@ def test_refresh_lead():
 
 def test_failed_refresh_ahead_of_time_keeps_the_set(nat):
     """The broker refreshes a set ahead of the workers' window; when that fetch fails (an
-    ECS / IMDS hiccup) the set in the slot, still good, stays -- a worker reading the slot then
-    still gets it -- and the refresh is tried again later. An error reaches the slot only when a
-    worker waits for a new set (as the SDK fails a call whose refresh fails inside its window)."""
+    ECS / IMDS hiccup) the set in the slot, still good, stays -- republished with the fetch's
+    error, so a worker reading the slot still gets it -- and the refresh is tried again later. An
+    error reaches the slot only when a worker waits for a new set and none still signs (here: the
+    service rejected it)."""
     from kube_sqs_autoscaler_amd.parallel.credbroker import MIN_REFRESH_NS, CredentialBroker
 
     clock = nat.VirtualClock()
@@ -281,24 +282,30 @@ def test_failed_refresh_ahead_of_time_keeps_the_set(nat):
                 raise RuntimeError("EC2RoleRequestError: connection refused")
             return nat.Credentials("AKID", "secret", f"tok-{len(calls)}", clock.unix_nanos() + 3600 * SEC, "Test")
 
-    broker = CredentialBroker(["us-east-1"], clock=clock, providers={"us-east-1": Flaky()})
+    warned = []
+    broker = CredentialBroker(["us-east-1"], clock=clock, providers={"us-east-1": Flaky()},
+                              log=lambda lvl, m: warned.append((lvl, m)))
     try:
         addr = broker.addrs["us-east-1"]
         assert broker.serve_once() == 1 and nat.read_credential_slot(addr)[2] == 1
         clock.advance(3600 * SEC - 330 * SEC)  # 5.5 min left: the broker's lead, not yet the workers' window
         assert broker.serve_once() == 1 and broker.refresh_errors == 1  # fetch 2 fails
         creds, err, gen = nat.read_credential_slot(addr)
-        assert (creds.session_token, err, gen) == ("tok-1", "", 1)  # kept
+        assert (creds.session_token, err, gen) == ("tok-1", "", 2)  # kept, marked with the refresh's error
+        assert "connection refused" in nat.credential_slot_info(addr)["refresh_error"]
+        assert len(warned) == 1 and warned[0][0] == "warning" and "keep signing" in warned[0][1]
         worker = nat.SlotCredentialsProvider(addr, clock, 300 * SEC, 2 * SEC)
         assert worker.retrieve().session_token == "tok-1"
         assert broker.serve_once() == 0  # not again before MIN_REFRESH_NS
         clock.advance(MIN_REFRESH_NS)
         assert broker.serve_once() == 1 and nat.read_credential_slot(addr)[0].session_token == "tok-3"
-        # a worker that waits for a new set gets the error of a failing fetch
+        assert nat.credential_slot_info(addr)["refresh_error"] == ""
+        # a worker that waits for a new set after a rejection gets the error of a failing fetch
         worker.stale(worker.retrieve())
-        assert broker.serve_once() == 1  # fetch 4 fails, asked for
+        assert broker.serve_once() == 1  # fetch 4 fails, asked for; the rejected set is not kept
         with pytest.raises(nat.NativeError, match="EC2RoleRequestError"):
             worker.retrieve()
+        assert len(warned) == 1
     finally:
         broker.close()
 
