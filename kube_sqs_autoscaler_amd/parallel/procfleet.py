@@ -2,7 +2,7 @@
 
 The reference is one process per queue (/root/reference/main.go:95-97, one URL and one
 Deployment). :class:`~.fleet.Fleet` runs N queues as N threads of one process, and since each
-runner keeps one thread for its life (``HomeThread``, csrc/core/runner.h; ``profiles/README.md``
+runner keeps one thread for its life (``HomeThread``, csrc/core/runner.h; ``docs/HISTORY.md``
 r02l) 8 thread queues poll as fast as 8 processes. ``--worker-processes`` keeps the
 reference's isolation inside this build's single pod: separate address spaces, file tables
 and allocators per queue, and per-process CPU and memory accounting. The supervisor forks one

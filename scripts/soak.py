@@ -30,7 +30,9 @@ enters its 5-minute window. The summary counts the
 endpoint's fetches, which must stay at one per refresh for the whole fleet, not one per queue,
 and names the session token of the last poll. ``--ecs-outage START:SECONDS``
 makes the endpoint answer 500 for a while (an agent restart): the sets already fetched keep
-signing, so no poll may fail for it.
+signing -- past the queues' 5-minute window when the outage outlasts the broker's refresh lead,
+until a minute before the set expires (``ksa_aws_credential_stale_signs_total``) -- so no poll may
+fail for it: with an outage, the summary is ok only when no poll failed to read the depth.
 
 ``--hot``: the old back-to-back soak of one queue (no faults), p50/p99 per window.
 """
@@ -161,7 +163,7 @@ def scrape(port: int) -> dict:
     out = {k: int(v) for k, v in tot.items() if k in (
         "polls", "scale_ups", "scale_downs", "depth_errors", "failed_ups", "failed_downs", "sqs_retries",
         "sqs_throttle_retries", "apiserver_retries", "apiserver_conflicts", "apiserver_errors",
-        "aws_credential_fetches") or (
+        "aws_credential_fetches", "aws_credential_stale_signs") or (
         k.startswith("http_") and k.split("_")[1] in ("connects", "presends", "presend", "reconnect", "idle"))}
     if "poll_cpu_seconds" in tot and out.get("polls"):  # the workers' CPU per poll so far (ksa_poll_cpu_seconds_total)
         out["poll_cpu_ms_per_poll"] = round(tot["poll_cpu_seconds"] * 1000 / out["polls"], 4)
@@ -223,7 +225,7 @@ def cadenced(a) -> int:
     args = [sys.executable, "-m", "kube_sqs_autoscaler_amd", f"--poll-period={a.poll_period}",
             f"--scale-up-cool-down={a.up_cool_down}", f"--scale-down-cool-down={a.down_cool_down}", "--max-pods=8",
             f"--aws-region={REGION}", f"--sqs-endpoint={sqs.url}", f"--trace-file={trace}",
-            f"--metrics-addr=127.0.0.1:{port}", "--log-level=error", "--api-timeout=10s"]
+            f"--metrics-addr=127.0.0.1:{port}", "--log-level=warning", "--api-timeout=10s"]
     args += [f"--queue=url={u},deployment=workers-{q},namespace=soak" for q, u in enumerate(urls)]
     if a.presend:
         args.append("--poll-presend")
@@ -341,7 +343,8 @@ def cadenced(a) -> int:
         vals = [r[key] for r in steady if key in r]
         flat[key] = {"min": min(vals), "max": max(vals), "flat": max(vals) - min(vals) <= tol} if vals else None
     with open(os.path.join(tmp, "stderr.log")) as f:
-        stderr_tail = f.read()[-2000:]
+        stderr_all = f.read()
+    stderr_tail = stderr_all[-2000:]
     summary = {
         "summary": True, "minutes": a.minutes, "queues": a.queues, "poll_period": a.poll_period,
         "cool_downs": [a.up_cool_down, a.down_cool_down], "exit_code": rc, "windows": len(rows),
@@ -364,8 +367,12 @@ def cadenced(a) -> int:
         most = 2 + int(elapsed / a.ecs_refresh)
         summary["credentials"] = {"refresh_s": a.ecs_refresh, "fetches": ecs.fetches, "at_most": most,
                                   "last_poll_token": tokens_seen[-1] if tokens_seen else None,
-                                  "outage_s": a.ecs_outage or None, "failed_fetches": ecs.failed}
+                                  "outage_s": a.ecs_outage or None, "failed_fetches": ecs.failed,
+                                  "stale_signs": rows[-1].get("aws_credential_stale_signs") if rows else None,
+                                  "refresh_failed_warnings": stderr_all.count("keep signing with the current set")}
         summary["ok"] = summary["ok"] and ecs.fetches <= most
+        if a.ecs_outage:  # the sets still sign through the outage: no poll may fail for it
+            summary["ok"] = summary["ok"] and summary["replay"]["depth_errors"] == 0
     if not summary["ok"]:
         summary["stderr_tail"] = stderr_tail
     print(json.dumps(summary), flush=True)

@@ -1,4 +1,6 @@
-"""Every ``file:line`` a document cites must exist (a stale ``kube.cc:467``).
+"""Every ``file:line`` a document cites must exist (a stale ``kube.cc:467``), and
+every file of evidence under ``profiles/`` must be cited (248 files, most cited by
+nothing but an index).
 
 The reference is read-only (/root/reference), so citations of it keep their line numbers: each
 cited line (or range end) must exist in the cited reference file. This repository's own files
@@ -15,7 +17,11 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 DOCS = [os.path.join(ROOT, "docs", f) for f in sorted(os.listdir(os.path.join(ROOT, "docs"))) if f.endswith(".md")]
-DOCS += [os.path.join(ROOT, "README.md"), os.path.join(ROOT, "profiles", "README.md")]
+DOCS += [os.path.join(ROOT, "README.md")]
+# the documents whose citations keep a profile (docs/HISTORY.md narrates past rounds and may name
+# files pruned since: they are in the git history)
+CURRENT = [os.path.join(ROOT, "README.md")] + [os.path.join(ROOT, "docs", f) for f in
+                                               ("DESIGN.md", "OPERATIONS.md", "PARITY_MATRIX.md")]
 UPSTREAM = {"client_config.go"}  # client-go v0.19: not vendored by the reference
 CITE = re.compile(r"((?:/root/reference/)?[A-Za-z0-9_./-]+\.(?:py|cc|h|hip|go|mod|sh|toml|ya?ml)):"
                   r"(\d+(?:-\d+)?(?:,\d+(?:-\d+)?)*)")
@@ -112,3 +118,49 @@ def test_cited_symbols_exist():
             if sym not in src and not re.search(r"\b" + re.escape(name) + r"\b", src):
                 bad.append(f"{os.path.relpath(doc, ROOT)}: `{m.group(1)}` `{sym}` not found")
     assert seen >= 8 and not bad, "\n".join(bad)
+
+
+def _tracked_profiles():
+    import subprocess
+
+    try:
+        out = subprocess.run(["git", "ls-files", "profiles"], cwd=ROOT, capture_output=True, text=True, check=True)
+    except (OSError, subprocess.CalledProcessError):
+        pytest.skip("not a git checkout")
+    return [p for p in out.stdout.splitlines() if p]
+
+
+def _current_text():
+    text = ""
+    for doc in CURRENT:
+        with open(doc) as f:
+            text += f.read() + "\n"
+    return text
+
+
+def _cites(text, entry):
+    """``entry``: a profile's path under profiles/ -- ``file``, ``dir/file``, or ``dir/`` on its own
+    (citing a directory cites every file in it; a file of it cites only itself)."""
+    return re.search(r"(?<![\w-])" + re.escape(entry) + r"(?![\w.-])", text)
+
+
+def test_every_profile_is_cited():
+    """A file under profiles/ that README.md, DESIGN, OPERATIONS or PARITY_MATRIX does not cite
+    (by its path, or its directory's) is not evidence of anything: prune it."""
+    text = _current_text()
+    bad = []
+    for path in _tracked_profiles():
+        rel = path[len("profiles/"):]
+        top = rel.split("/", 1)[0]
+        entries = [rel] + ([top + "/"] if "/" in rel else [])
+        if not any(_cites(text, e) for e in entries):
+            bad.append(path)
+    assert not bad, "uncited profiles (cite them or delete them):\n" + "\n".join(bad)
+
+
+def test_cited_profiles_exist():
+    """Every ``profiles/<entry>`` the current documents cite is in the tree."""
+    text = _current_text()
+    bad = sorted({m.group(1) for m in re.finditer(r"profiles/([A-Za-z0-9_.-]+/?(?:[A-Za-z0-9_.-]+)?)", text)
+                  if not os.path.exists(os.path.join(ROOT, "profiles", m.group(1).rstrip("/")))})
+    assert not bad, bad

@@ -1,6 +1,6 @@
 """Each Runner polls on one OS thread for its whole life (HomeThread, csrc/core/runner.h), across
 Supervisor runs: a replaced thread would hand its malloc arena to another queue's new thread
-and interleave two queues' hot buffers (profiles/README.md, r02l)."""
+and interleave two queues' hot buffers (docs/HISTORY.md, r02l)."""
 import os
 
 from kube_sqs_autoscaler_amd.bench.latency import BenchEnv
