@@ -289,6 +289,12 @@ PYBIND11_MODULE(_ksa_native, m) {
     return d;
   });
   m.attr("CREDENTIAL_STALE_SKEW_NS") = kStaleSkew;
+  m.def("credential_slot_asks", [cs](uintptr_t addr) { return credential_slot_asks(cs(addr)); });
+  // the broker's serving thread sleeps here between looks (GIL released): a worker's ask wakes it
+  m.def("credential_slot_wait_ask", [cs](uintptr_t addr, uint32_t seen, int64_t timeout_ns) {
+    return credential_slot_wait_ask(cs(addr), seen, timeout_ns);
+  }, py::call_guard<py::gil_scoped_release>());
+  m.def("credential_slot_poke", [cs](uintptr_t addr) { credential_slot_poke(cs(addr)); });
   m.def("credential_slot_needs_fetch", [cs](uintptr_t addr, int64_t unix_now, int64_t window) {
     return credential_slot_needs_fetch(cs(addr), unix_now, window);
   });

@@ -1,6 +1,11 @@
 #include "cred_slot.h"
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
+
+#include <climits>
 
 #include <algorithm>
 #include <cstring>
@@ -15,6 +20,22 @@ enum Part : int { kAkid = 0, kSecret = 1, kToken = 2, kName = 3, kError = 4, kRe
 void nap(Nanos ns) {
   struct timespec ts = {static_cast<time_t>(ns / kSecond), static_cast<long>(ns % kSecond)};
   nanosleep(&ts, nullptr);
+}
+
+// Process-shared futex on a 32-bit atomic of the slot (the mapping is MAP_SHARED, so no
+// FUTEX_PRIVATE_FLAG). std::atomic<uint32_t> is the plain word on Linux.
+static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
+
+constexpr Nanos kCancelCheck = 20 * kMillisecond;
+
+void futex_wait(std::atomic<uint32_t>* word, uint32_t seen, Nanos timeout) {
+  if (timeout <= 0) return;
+  struct timespec ts = {static_cast<time_t>(timeout / kSecond), static_cast<long>(timeout % kSecond)};
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(word), FUTEX_WAIT, seen, &ts, nullptr, 0);
+}
+
+void futex_wake_all(std::atomic<uint32_t>* word) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(word), FUTEX_WAKE, INT_MAX, nullptr, nullptr, 0);
 }
 
 void publish_parts(SharedCredentialSlot* s, const std::string (&parts)[kParts], int64_t expires) {
@@ -41,6 +62,8 @@ void publish_parts(SharedCredentialSlot* s, const std::string (&parts)[kParts], 
   s->expires_unix_ns.store(expires, std::memory_order_relaxed);
   s->seq.store(seq + 2, std::memory_order_release);
   s->generation.fetch_add(1, std::memory_order_acq_rel);
+  s->published.fetch_add(1, std::memory_order_release);
+  futex_wake_all(&s->published);
 }
 
 }  // namespace
@@ -52,6 +75,8 @@ SharedCredentialSlot* init_credential_slot(void* at) {
   s->wanted.store(0, std::memory_order_relaxed);
   s->rejected.store(0, std::memory_order_relaxed);
   s->stale_signs.store(0, std::memory_order_relaxed);
+  s->asks.store(0, std::memory_order_relaxed);
+  s->published.store(0, std::memory_order_relaxed);
   s->expires_unix_ns.store(0, std::memory_order_relaxed);
   for (auto& l : s->len) l.store(0, std::memory_order_relaxed);
   for (auto& w : s->words) w.store(0, std::memory_order_relaxed);
@@ -122,6 +147,22 @@ void request_credentials(SharedCredentialSlot* s, uint64_t generation) {
   while (cur < generation &&
          !s->wanted.compare_exchange_weak(cur, generation, std::memory_order_acq_rel, std::memory_order_relaxed)) {
   }
+  s->asks.fetch_add(1, std::memory_order_release);
+  futex_wake_all(&s->asks);
+}
+
+uint32_t credential_slot_asks(const SharedCredentialSlot* s) { return s->asks.load(std::memory_order_acquire); }
+
+uint32_t credential_slot_wait_ask(SharedCredentialSlot* s, uint32_t seen, Nanos timeout) {
+  if (s->asks.load(std::memory_order_acquire) == seen) futex_wait(&s->asks, seen, timeout);
+  return s->asks.load(std::memory_order_acquire);
+}
+
+void credential_slot_poke(SharedCredentialSlot* s) {
+  s->asks.fetch_add(1, std::memory_order_release);
+  s->published.fetch_add(1, std::memory_order_release);
+  futex_wake_all(&s->asks);
+  futex_wake_all(&s->published);
 }
 
 void reject_credentials(SharedCredentialSlot* s, uint64_t generation) {
@@ -169,14 +210,11 @@ Result<Credentials> SlotCredentialsProvider::retrieve() {
   // Nothing yet, an error, a rejected set, or one about to expire: ask the supervisor for the next.
   request_credentials(slot_, have ? gen : 0);
   const int64_t deadline = mono_ns() + wait_limit_;
-  // The supervisor looks at the slots every 200 ms and a fetch takes milliseconds to seconds:
-  // the first looks come quickly, then the nap backs off to 5 ms (a handful of wake-ups a
-  // second per waiting queue while an endpoint hangs).
-  Nanos pause = 200 * kMicrosecond;
-  while (mono_ns() < deadline) {
+  // Sleep on the slot's `published` word until the supervisor publishes (the ask above woke its
+  // serving thread); the wait times out every kCancelCheck to look at cancel() and the deadline.
+  for (;;) {
+    const uint32_t seen = slot_->published.load(std::memory_order_acquire);
     if (cancelled_.load(std::memory_order_acquire)) return Result<Credentials>::Err(Status::Err("request canceled"));
-    nap(pause);
-    pause = std::min<Nanos>(pause * 2, 5 * kMillisecond);
     Credentials next;
     std::string next_error, next_refresh_error;
     uint64_t next_gen = 0;
@@ -190,11 +228,20 @@ Result<Credentials> SlotCredentialsProvider::retrieve() {
         return ride(next);
       return Result<Credentials>::Err(Status::Err(next_refresh_error));
     }
+    const int64_t left = deadline - mono_ns();
+    if (left <= 0) break;
+    futex_wait(&slot_->published, seen, std::min<Nanos>(left, kCancelCheck));
   }
   // No answer: a set that has not expired yet still signs.
   if (good && (c.expires_unix_ns == 0 || now_() < c.expires_unix_ns)) return Result<Credentials>::Ok(c);
   return Result<Credentials>::Err(Status::Err(
       have && !error.empty() ? error : "NoCredentialProviders: the supervisor published no credentials in time"));
+}
+
+void SlotCredentialsProvider::cancel() {
+  // Only the flag: a late stop (a signal after the supervisor unmapped the slots) must not touch
+  // the slot. A waiting retrieve() looks at the flag at least every kCancelCheck.
+  cancelled_.store(true, std::memory_order_release);
 }
 
 void SlotCredentialsProvider::stale(const Credentials& c) {

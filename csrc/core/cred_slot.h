@@ -17,7 +17,10 @@
 //
 // Like SharedWorkerState (runner.h): lock-free atomics only (address-free on x86-64), each word
 // with one writer -- the supervisor for the set, its generation and its error; the workers for
-// the `wanted` generation (an atomic max). The set is written under a seqlock.
+// the `wanted` generation (an atomic max). The set is written under a seqlock. Nobody polls for
+// the other side: a worker's ask bumps `asks` and a publication bumps `published`, each followed
+// by a process-shared futex wake, so the supervisor's serving thread and the waiting workers
+// sleep until there is something to read (the waits also time out, to look at cancel and stop).
 #pragma once
 
 #include <atomic>
@@ -41,6 +44,8 @@ struct SharedCredentialSlot {
   std::atomic<uint64_t> wanted;      // the newest generation a worker asked to be replaced
   std::atomic<uint64_t> rejected;    // the newest generation a worker saw the service reject
   std::atomic<uint64_t> stale_signs; // retrieve()s answered with a set kept after a failed refresh
+  std::atomic<uint32_t> asks;       // futex word: bumped by every request_credentials()
+  std::atomic<uint32_t> published;  // futex word: bumped by every publication
   std::atomic<int64_t> expires_unix_ns;
   // access key id, secret, token, provider name, error, refresh error (the set kept after a
   // failed refresh: why it was not replaced)
@@ -65,6 +70,12 @@ void reject_credentials(SharedCredentialSlot* s, uint64_t generation);
 // Supervisor side: whether the slot needs a fetch -- nothing published, a worker asked to
 // replace the current generation, or the set expires within `window` of `unix_now`.
 bool credential_slot_needs_fetch(const SharedCredentialSlot* s, int64_t unix_now, int64_t window);
+// Supervisor side: sleep until a worker asks (`asks` moves past `seen`), `timeout` passes or
+// credential_slot_poke() is called; returns the current `asks`.
+uint32_t credential_slot_wait_ask(SharedCredentialSlot* s, uint32_t seen, Nanos timeout);
+uint32_t credential_slot_asks(const SharedCredentialSlot* s);
+// Wakes every thread waiting on the slot (supervisor and workers): the supervisor's stop.
+void credential_slot_poke(SharedCredentialSlot* s);
 // Whether the slot's set may still be signed with at `unix_now`: a set (not an error) that was
 // not rejected and does not expire within `skew`. The supervisor keeps such a set when its
 // refresh fails.
@@ -82,7 +93,7 @@ class SlotCredentialsProvider final : public CredentialsProvider {
   Result<Credentials> retrieve() override;
   void stale(const Credentials& c) override;
   // The worker stops: a retrieve() waiting for the supervisor returns "request canceled" at once.
-  void cancel() override { cancelled_.store(true, std::memory_order_release); }
+  void cancel() override;
 
  private:
   Result<Credentials> ride(const Credentials& c);

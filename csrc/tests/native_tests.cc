@@ -1314,6 +1314,43 @@ TEST(credential_slot_rides_out_a_failed_refresh) {
   CHECK_EQ(slot->stale_signs.load(), uint64_t(100));
 }
 
+// Nobody polls the slot: the supervisor's serving thread sleeps on `asks` and a worker's ask
+// wakes it at once; a waiting worker sleeps on `published` and a publication wakes it at once.
+TEST(credential_slot_futex_wakeups) {
+  auto mem = std::make_unique<SharedCredentialSlot>();
+  SharedCredentialSlot* slot = init_credential_slot(mem.get());
+  const uint32_t seen = credential_slot_asks(slot);
+  std::atomic<int64_t> woke_after{-1};
+  std::thread supervisor([&] {
+    const int64_t t0 = mono_ns();
+    const uint32_t now_asks = credential_slot_wait_ask(slot, seen, 10 * kSecond);
+    woke_after = mono_ns() - t0;
+    CHECK(now_asks != seen);
+    Credentials c;
+    c.access_key_id = "AKID";
+    c.secret_access_key = "s";
+    publish_credentials(slot, c);
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  SlotCredentialsProvider w(slot, [] { return int64_t(0); }, 0, 10 * kSecond);
+  const int64_t t0 = mono_ns();
+  auto r = w.retrieve();  // asks (waking the supervisor), then sleeps until the publication
+  const int64_t took = mono_ns() - t0;
+  supervisor.join();
+  CHECK(r.ok() && r.value.access_key_id == "AKID");
+  CHECK(woke_after.load() >= 0 && woke_after.load() < 5 * kSecond);
+  CHECK(took < kSecond);
+  // a poke (the supervisor's stop) ends the wait without an ask
+  std::thread stopper([&] {
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    credential_slot_poke(slot);
+  });
+  const int64_t t1 = mono_ns();
+  credential_slot_wait_ask(slot, credential_slot_asks(slot), 10 * kSecond);
+  stopper.join();
+  CHECK(mono_ns() - t1 < 5 * kSecond);
+}
+
 // SharedCredentialsProvider::cancel releases the callers waiting for another client's fetch
 // (a stop no longer waits out the whole fetch timeout); the fetch itself, and the
 // callers that come later, are unaffected.

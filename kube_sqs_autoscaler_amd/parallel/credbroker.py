@@ -65,9 +65,10 @@ class CredentialBroker:
                  poll_s: float = 0.2, providers: Optional[Dict[str, object]] = None,
                  log: Optional[Callable[[str, str], None]] = None):
         """``providers``: the chain per region (default: the SDK chain for that region).
-        ``poll_s``: how often each region's serving thread looks at its slot -- what a queue that
-        asks for a new set waits at most on top of the fetch (5 wake-ups a second per region: a
-        fraction of a millicore). ``log(level, message)``: where the warnings go."""
+        ``poll_s``: how often each region's serving thread looks at its slot for a refresh that
+        is due (5 wake-ups a second per region: a fraction of a millicore); a queue that asks for
+        a new set wakes it at once (a futex on the slot). ``log(level, message)``: where the
+        warnings go."""
         nat = native()
         self.regions = sorted(set(regions))
         self.environ = environ
@@ -170,14 +171,20 @@ class CredentialBroker:
         if self._threads:
             return
 
+        nat = native()
+        timeout_ns = int(self.poll_s * 1e9)
+
         def loop(region: str):
+            addr = self.addrs[region]
             while not self._stop.is_set():
+                seen = nat.credential_slot_asks(addr)  # an ask during the serve below: serve again
                 try:
                     self.serve_region(region)
                 except Exception as e:  # noqa: BLE001 -- a broken slot must not end the thread
                     if self.log is not None:
                         self.log("error", f"AWS credential broker ({region}): {type(e).__name__}: {e}")
-                self._stop.wait(self.poll_s)
+                if not self._stop.is_set():
+                    nat.credential_slot_wait_ask(addr, seen, timeout_ns)
 
         for region in self.regions:
             t = threading.Thread(target=loop, args=(region,), name=f"ksa-credentials-{region}", daemon=True)
@@ -190,6 +197,8 @@ class CredentialBroker:
         import time
 
         self._stop.set()
+        for addr in self.addrs.values():  # wake the threads sleeping between looks
+            native().credential_slot_poke(addr)
         deadline = time.monotonic() + timeout
         for t in self._threads.values():
             t.join(timeout=max(0.0, deadline - time.monotonic()))

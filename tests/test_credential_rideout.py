@@ -96,7 +96,7 @@ def test_a_set_past_its_skew_fails_with_the_chains_error(nat):
 
 def test_a_rejected_set_is_not_signed_with_before_its_replacement(nat):
     """after ExpiredToken (stale()), the next retrieve() must not hand back the
-    rejected set while the broker has not looked at the slot yet (it looks every 200 ms, an SQS
+    rejected set while the broker has not replaced it yet (round 5: it looked every 200 ms, an SQS
     retry comes after 30-120 ms): it waits for the replacement, and without one it fails rather
     than re-sign with the rejected key."""
     from kube_sqs_autoscaler_amd.parallel.credbroker import CredentialBroker
@@ -131,8 +131,8 @@ def test_a_rejected_set_is_not_signed_with_before_its_replacement(nat):
 
 def test_one_regions_hung_endpoint_does_not_delay_another(nat):
     """Region A's credential endpoint hangs (30 s); region B's queue holds a set about to expire
-    and asks for a new one: B's serving thread fetches it within a second, because A's fetch
-    blocks only A's thread."""
+    and asks for a new one: B's serving thread fetches it within a second (its ask wakes that
+    thread at once: typically a millisecond), because A's fetch blocks only A's thread."""
     from kube_sqs_autoscaler_amd.parallel.credbroker import CredentialBroker
 
     clock = nat.RealClock()
