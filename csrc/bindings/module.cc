@@ -235,6 +235,7 @@ PYBIND11_MODULE(_ksa_native, m) {
       .def_readwrite("session_token", &Credentials::session_token)
       .def_readwrite("expires_unix_ns", &Credentials::expires_unix_ns)
       .def_readwrite("provider_name", &Credentials::provider_name)
+      .def_readonly("kept_after_failed_refresh", &Credentials::kept_after_failed_refresh)
       .def("valid", &Credentials::valid)
       .def("__repr__", [](const Credentials& c) {
         return "Credentials(access_key_id=" + c.access_key_id + ", provider=" + c.provider_name + ")";

@@ -190,9 +190,14 @@ bool credential_slot_still_signs(const SharedCredentialSlot* s, int64_t unix_now
   return c.expires_unix_ns == 0 || unix_now + skew < c.expires_unix_ns;
 }
 
-Result<Credentials> SlotCredentialsProvider::ride(const Credentials& c) {
-  slot_->stale_signs.fetch_add(1, std::memory_order_relaxed);
+Result<Credentials> SlotCredentialsProvider::ride(Credentials c) {
+  c.kept_after_failed_refresh = true;  // the request it signs is counted (signed_with_kept)
   return Result<Credentials>::Ok(c);
+}
+
+void SlotCredentialsProvider::signed_with_kept(const Credentials& c) {
+  (void)c;
+  slot_->stale_signs.fetch_add(1, std::memory_order_relaxed);
 }
 
 Result<Credentials> SlotCredentialsProvider::retrieve() {

@@ -43,7 +43,7 @@ struct SharedCredentialSlot {
   std::atomic<uint64_t> generation;  // sets (or errors) published so far; 0: none yet
   std::atomic<uint64_t> wanted;      // the newest generation a worker asked to be replaced
   std::atomic<uint64_t> rejected;    // the newest generation a worker saw the service reject
-  std::atomic<uint64_t> stale_signs; // retrieve()s answered with a set kept after a failed refresh
+  std::atomic<uint64_t> stale_signs; // SQS requests signed with a set kept after a failed refresh
   std::atomic<uint32_t> asks;       // futex word: bumped by every request_credentials()
   std::atomic<uint32_t> published;  // futex word: bumped by every publication
   std::atomic<int64_t> expires_unix_ns;
@@ -94,9 +94,12 @@ class SlotCredentialsProvider final : public CredentialsProvider {
   void stale(const Credentials& c) override;
   // The worker stops: a retrieve() waiting for the supervisor returns "request canceled" at once.
   void cancel() override;
+  // Counts a request signed with a kept set into the slot (every worker of the slot, threads and
+  // processes alike, adds to one count).
+  void signed_with_kept(const Credentials& c) override;
 
  private:
-  Result<Credentials> ride(const Credentials& c);
+  Result<Credentials> ride(Credentials c);
   std::atomic<bool> cancelled_{false};
   SharedCredentialSlot* slot_;
   std::function<int64_t()> now_;

@@ -62,6 +62,9 @@ struct Credentials {
   std::string session_token;
   int64_t expires_unix_ns = 0;  // 0 = does not expire
   std::string provider_name;
+  // Set by a provider that handed out a set inside its refresh window because the refresh
+  // failed (cred_slot.h): a request signed with it is reported through signed_with_kept().
+  bool kept_after_failed_refresh = false;
   bool valid() const { return !access_key_id.empty() && !secret_access_key.empty(); }
 };
 
@@ -73,6 +76,9 @@ class CredentialsProvider {
   virtual Result<Credentials> retrieve() = 0;
   // A client found `c` rejected (ExpiredToken): a provider that caches drops it. Default: none.
   virtual void stale(const Credentials& c) { (void)c; }
+  // A request was signed with `c`, a set handed out with kept_after_failed_refresh: a provider
+  // that counts those does so here. Default: nothing.
+  virtual void signed_with_kept(const Credentials& c) { (void)c; }
   // The client that owns this source stops for good (its API's cancel(), on Runner::stop): a
   // provider that waits for credentials stops waiting. Lock-free: the wait may hold the caller's
   // lock. Default: nothing to interrupt.
@@ -97,6 +103,10 @@ class alignas(kCacheLine) CachedCredentials {
   Result<Credentials> get(int64_t unix_now_ns);
   void invalidate();
   void cancel() { provider_->cancel(); }  // lock-free: get() may be waiting in retrieve()
+  // The client signed a request with `c` (from get()): counted by the provider when it was kept.
+  void signed_with(const Credentials& c) {
+    if (c.kept_after_failed_refresh) provider_->signed_with_kept(c);
+  }
 
  private:
   std::shared_ptr<CredentialsProvider> provider_;

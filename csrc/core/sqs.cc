@@ -213,6 +213,7 @@ Result<AttrMap> HttpSqsApi::call_once(const std::string& queue_url,
   std::unique_lock<std::mutex> prep_lock(prep_mu_);
   sign_locked(queue_url, names, cr.value, clock_->unix_nanos());
   if (timed) sign_ns_.store(mono_ns() - t_sign, std::memory_order_relaxed);
+  creds_.signed_with(cr.value);  // a set kept after a failed refresh: the provider counts the request
   HttpRequest req;
   req.method = "POST";
   req.target = url_.path.empty() ? "/" : url_.path;

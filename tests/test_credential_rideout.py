@@ -51,18 +51,91 @@ def test_outage_longer_than_the_lead_fails_no_poll(nat):
     try:
         addr = broker.addrs["us-east-1"]
         worker = nat.SlotCredentialsProvider(addr, clock, 300 * SEC, 1 * SEC)
-        tokens = []
+        tokens, kept = [], []
         for s in range(0, 200):
             broker.serve_once()
-            tokens.append(worker.retrieve().session_token)  # raises on a failed poll
+            c = worker.retrieve()  # raises on a failed poll
+            tokens.append(c.session_token)
+            kept.append(c.kept_after_failed_refresh)
             clock.advance(1 * SEC)
         assert tokens[:150] == ["tok-1"] * 150 and set(tokens[150:]) == {"tok-11"}
         assert len(calls) == 11  # 1 fetch, 9 failed refreshes 10 s apart (60..140 s), 1 that worked
-        assert broker.stale_signs_by_region() == {"us-east-1": 30}  # 120..149 s, inside the window
+        assert [s for s, k in enumerate(kept) if k] == list(range(120, 150))  # inside the window
         assert len(warned) == 1 and "EcsCredentialsError" in warned[0]
         assert nat.credential_slot_info(addr)["wanted"] == 0  # no queue had to ask
     finally:
         broker.close()
+
+
+@pytest.mark.slow
+def test_fleet_polls_ride_out_a_failing_refresh(nat, tmp_path):
+    """End to end: a queue whose set is inside its 5-minute window from the start (200 s left)
+    while every refresh fails. Each poll's ask gets the kept set back at once; every poll reads
+    the depth and scales as the reference would (4 -> 8 at 500 messages, one pod per poll), and
+    every signed SQS request is counted in ksa_aws_credential_stale_signs_total."""
+    from kube_sqs_autoscaler_amd import autoscaler
+    from kube_sqs_autoscaler_amd.config import parse_args
+    from kube_sqs_autoscaler_amd.metrics import FleetCollector
+    from kube_sqs_autoscaler_amd.parallel.credbroker import CredentialBroker
+    from kube_sqs_autoscaler_amd.parallel.fleet import Fleet
+    from kube_sqs_autoscaler_amd.utils.log import make_logger
+
+    clock = nat.RealClock()
+    calls = []
+
+    class Failing(nat.CredentialsProvider):
+        def retrieve(self):
+            calls.append(1)
+            if len(calls) > 1:
+                raise RuntimeError("EcsCredentialsError: 500 agent restarting")
+            return nat.Credentials(AKID, SECRET, "only", clock.unix_nanos() + 200 * SEC, "EcsProvider")
+
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, "us-east-1")
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    warned = []
+    broker = CredentialBroker(["us-east-1"], clock=clock, providers={"us-east-1": Failing()},
+                              log=lambda lvl, m: warned.append(m))
+    fleet = None
+    try:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"HOME": str(tmp_path), "KUBE_CONFIG_PATH": str(kc)}
+        url = f"{sqs.url}/123/q"
+        sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500"})
+        kube.add_deployment("gpu", "w", 4)
+        cfg = parse_args(["--aws-region=us-east-1", f"--sqs-endpoint={sqs.url}", "--poll-period=50ms",
+                          "--scale-up-cool-down=0s", "--scale-down-cool-down=0s", "--max-pods=8",
+                          f"--queue=url={url},deployment=w,namespace=gpu,attribute-names=ApproximateNumberOfMessages"],
+                         env)
+        rest = autoscaler.load_rest_config(cfg, env)
+        workers = [autoscaler.new_runner(t, cfg, rest, make_logger("error", "text"), clock, environ=env,
+                                         credentials=broker.provider_for("us-east-1")) for t in cfg.targets]
+        broker.start()
+        fleet = Fleet(workers)
+        fleet.start(10)
+        fleet.join()
+        st = fleet.stats()[0]
+        assert st["polls"] == 10 and st["depth_errors"] == 0 and kube.replicas("gpu", "w") == 8
+        assert sqs.signature_failures() == 0 and sqs.requests() == 10
+        stale = broker.stale_signs_by_region()["us-east-1"]
+        assert stale == 10, stale  # every signed request, warm-ups not counted
+        text = FleetCollector(fleet, credential_stale_signs=broker.stale_signs_by_region).exposition().decode()
+        assert 'ksa_aws_credential_stale_signs_total{region="us-east-1"} 10' in text
+        assert len(warned) == 1 and "keep signing" in warned[0]
+    finally:
+        if fleet is not None:
+            fleet.stop()
+            fleet.join()
+        broker.close()
+        sqs.stop()
+        kube.stop()
 
 
 def test_a_set_past_its_skew_fails_with_the_chains_error(nat):

@@ -164,3 +164,16 @@ def test_cited_profiles_exist():
     bad = sorted({m.group(1) for m in re.finditer(r"profiles/([A-Za-z0-9_.-]+/?(?:[A-Za-z0-9_.-]+)?)", text)
                   if not os.path.exists(os.path.join(ROOT, "profiles", m.group(1).rstrip("/")))})
     assert not bad, bad
+
+
+def test_readme_is_the_operators_view():
+    """README.md stays what an operator switching from the reference needs (65 KB of
+    round diaries); the narration lives in docs/HISTORY.md."""
+    with open(os.path.join(ROOT, "README.md"), "rb") as f:
+        body = f.read()
+    assert len(body) < 20 * 1024, len(body)
+    text = body.decode()
+    for section in ("## Switching from the reference", "### Flags", "### Deliberate deviations", "## Performance",
+                    "## Known limits"):
+        assert section in text, section
+    assert "in brief" not in text
