@@ -317,6 +317,7 @@ PYBIND11_MODULE(_ksa_native, m) {
            py::arg("inner"), py::arg("clock"), py::arg("expiry_window_ns") = 5LL * 60 * kSecond)
       // the lock may be held by a fetch waiting for the GIL (a Python inner provider)
       .def("fetches", &SharedCredentialsProvider::fetches, py::call_guard<py::gil_scoped_release>())
+      .def("stale_signs", &SharedCredentialsProvider::stale_signs)
       .def("stale", &SharedCredentialsProvider::stale, py::call_guard<py::gil_scoped_release>())
       .def("cancel", &SharedCredentialsProvider::cancel, py::call_guard<py::gil_scoped_release>());
 

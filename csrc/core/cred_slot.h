@@ -34,9 +34,6 @@
 
 namespace ksa {
 
-// How long before Expiration a set whose refresh failed stops being signed with.
-constexpr int64_t kStaleSkew = 60 * kSecond;
-
 struct SharedCredentialSlot {
   static constexpr size_t kBytes = 12 * 1024;  // key id + secret + session token + names
   std::atomic<uint64_t> seq;         // odd while the supervisor writes the set

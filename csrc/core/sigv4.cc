@@ -198,8 +198,14 @@ void CachedCredentials::invalidate() {
 
 Result<Credentials> SharedCredentialsProvider::retrieve() {
   std::unique_lock<std::mutex> lk(mu_);
-  if (have_ && (cached_.expires_unix_ns == 0 || now_() + window_ < cached_.expires_unix_ns))
+  const int64_t now = now_();
+  if (have_ && (cached_.expires_unix_ns == 0 || now + window_ < cached_.expires_unix_ns))
     return Result<Credentials>::Ok(cached_);
+  if (have_ && kept_ && now < retry_at_ && now + kStaleSkew < cached_.expires_unix_ns) {
+    Credentials k = cached_;  // its refresh failed a moment ago: sign with it, retry later
+    k.kept_after_failed_refresh = true;
+    return Result<Credentials>::Ok(k);
+  }
   if (fetching_) {  // another client is fetching: its outcome is this caller's too
     const uint64_t ticket = fetched_, cancels = cancels_;
     done_.wait(lk, [&] { return fetched_ != ticket || cancels_ != cancels; });
@@ -217,8 +223,20 @@ Result<Credentials> SharedCredentialsProvider::retrieve() {
   }
   lk.lock();
   fetching_ = false;
-  have_ = r.ok() && r.value.valid();
-  if (have_) cached_ = r.value;
+  const int64_t after = now_();
+  if (r.ok() && r.value.valid()) {
+    have_ = true;
+    kept_ = false;
+    cached_ = r.value;
+  } else if (!r.ok() && have_ && cached_.expires_unix_ns != 0 && after + kStaleSkew < cached_.expires_unix_ns) {
+    kept_ = true;  // the set still signs: keep it rather than fail the call (README.md)
+    retry_at_ = after + kKeptRetry;
+    Credentials k = cached_;
+    k.kept_after_failed_refresh = true;
+    r = Result<Credentials>::Ok(k);
+  } else {
+    have_ = kept_ = false;
+  }
   last_ = r;
   fetched_++;
   done_.notify_all();
@@ -236,7 +254,7 @@ void SharedCredentialsProvider::stale(const Credentials& c) {
   // the first client to see this set rejected drops it; the others then get its replacement
   if (have_ && c.access_key_id == cached_.access_key_id && c.session_token == cached_.session_token &&
       c.expires_unix_ns == cached_.expires_unix_ns)
-    have_ = false;
+    have_ = kept_ = false;
 }
 
 namespace {

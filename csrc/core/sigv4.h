@@ -8,6 +8,7 @@
 // steady-state signing costs two SHA-256 digests and one HMAC.
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -68,6 +69,13 @@ struct Credentials {
   bool valid() const { return !access_key_id.empty() && !secret_access_key.empty(); }
 };
 
+// A set whose refresh failed is still signed with until this long before its Expiration
+// (cred_slot.h, SharedCredentialsProvider): a deliberate deviation from aws-sdk-go, which fails
+// the call once its 5-minute window is reached and the refresh fails (README.md).
+constexpr int64_t kStaleSkew = 60LL * 1000 * 1000 * 1000;
+// While such a set is kept, the refresh is tried again at most this often.
+constexpr int64_t kKeptRetry = 10LL * 1000 * 1000 * 1000;
+
 // Credential source (env, shared file, web identity, ECS, IMDS ... live in Python; see
 // kube_sqs_autoscaler_amd/sqs/credentials.py). Native code only needs retrieve().
 class CredentialsProvider {
@@ -126,6 +134,9 @@ class alignas(kCacheLine) CachedCredentials {
 // is the clock (wall time). cancel() (one client's Runner::stop) releases the callers waiting
 // for a fetch at that moment with "request canceled"; it does not stop the fetch, which the
 // other clients still wait for, and later calls wait as before -- the provider is shared.
+// A refresh that fails while the cached set has more than kStaleSkew left keeps that set: it is
+// handed out (kept_after_failed_refresh) and the refresh retried every kKeptRetry, as the CLI's
+// broker does (cred_slot.h).
 class SharedCredentialsProvider final : public CredentialsProvider {
  public:
   SharedCredentialsProvider(std::shared_ptr<CredentialsProvider> inner, std::function<int64_t()> unix_now,
@@ -134,10 +145,16 @@ class SharedCredentialsProvider final : public CredentialsProvider {
   Result<Credentials> retrieve() override;
   void stale(const Credentials& c) override;
   void cancel() override;
+  void signed_with_kept(const Credentials& c) override {
+    (void)c;
+    stale_signs_.fetch_add(1, std::memory_order_relaxed);
+  }
   uint64_t fetches() const {
     std::lock_guard<std::mutex> lk(mu_);
     return fetches_;
   }
+  // Requests signed with a set kept after its refresh failed.
+  uint64_t stale_signs() const { return stale_signs_.load(std::memory_order_relaxed); }
 
  private:
   std::shared_ptr<CredentialsProvider> inner_;
@@ -152,6 +169,9 @@ class SharedCredentialsProvider final : public CredentialsProvider {
   uint64_t cancels_ = 0;      // cancel() calls: a waiter that saw another count returns
   Result<Credentials> last_;  // the outcome of the last one
   uint64_t fetches_ = 0;
+  bool kept_ = false;         // cached_ is a set whose refresh failed
+  int64_t retry_at_ = 0;      // (unix ns) while kept_: no fetch before this
+  std::atomic<uint64_t> stale_signs_{0};
 };
 
 struct SignDebug {

@@ -1356,6 +1356,55 @@ TEST(credential_slot_futex_wakeups) {
   CHECK(mono_ns() - t1 < 5 * kSecond);
 }
 
+// A library user's SharedCredentialsProvider rides out a failing refresh like the broker: inside
+// the window the cached set is handed out (marked kept) while it has more than kStaleSkew left,
+// the refresh retried every kKeptRetry, and the inner error surfaces only past the skew; a set the
+// service rejected is never kept.
+TEST(shared_provider_rides_out_a_failed_refresh) {
+  struct Chain final : CredentialsProvider {
+    std::atomic<int> calls{0};
+    std::atomic<bool> fail{false};
+    std::atomic<int64_t>* now;
+    Result<Credentials> retrieve() override {
+      ++calls;
+      if (fail) return Result<Credentials>::Err(Status::Err("EcsCredentialsError: 500"));
+      Credentials c;
+      c.access_key_id = "AKID";
+      c.secret_access_key = "s";
+      c.session_token = "t" + std::to_string(calls.load());
+      c.expires_unix_ns = now->load() + 420 * kSecond;
+      return Result<Credentials>::Ok(c);
+    }
+  };
+  std::atomic<int64_t> now{0};
+  auto chain = std::make_shared<Chain>();
+  chain->now = &now;
+  SharedCredentialsProvider shared(chain, [&] { return now.load(); }, 300 * kSecond);
+  CHECK(shared.retrieve().value.session_token == "t1");
+  chain->fail = true;
+  now = 130 * kSecond;  // inside the window, refresh failing
+  auto r = shared.retrieve();
+  CHECK(r.ok() && r.value.session_token == "t1" && r.value.kept_after_failed_refresh);
+  CHECK_EQ(chain->calls.load(), 2);
+  for (int i = 0; i < 50; ++i) CHECK(shared.retrieve().ok());  // within kKeptRetry: no fetch
+  CHECK_EQ(chain->calls.load(), 2);
+  shared.signed_with_kept(r.value);
+  CHECK_EQ(shared.stale_signs(), uint64_t(1));
+  now = 141 * kSecond;  // kKeptRetry later: one more (failing) fetch, the set still kept
+  CHECK(shared.retrieve().value.kept_after_failed_refresh);
+  CHECK_EQ(chain->calls.load(), 3);
+  now = 361 * kSecond;  // within the skew of Expiration: the chain's error
+  auto e = shared.retrieve();
+  CHECK(!e.ok() && e.status.message() == "EcsCredentialsError: 500");
+  // recovery, then a rejection during an outage: the rejected set is not kept
+  chain->fail = false;
+  CHECK(shared.retrieve().ok());
+  const Credentials fresh = shared.retrieve().value;
+  chain->fail = true;
+  shared.stale(fresh);
+  CHECK(!shared.retrieve().ok());
+}
+
 // SharedCredentialsProvider::cancel releases the callers waiting for another client's fetch
 // (a stop no longer waits out the whole fetch timeout); the fetch itself, and the
 // callers that come later, are unaffected.
