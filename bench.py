@@ -33,7 +33,11 @@ under ``torchrun`` the launcher's WORLD_SIZE must equal ``--gpus`` (exit 2 other
 with fewer visible GPUs than ranks exits 2, unless ``--rehearse-shared-gpus``: then the ranks
 share GPUs over gloo and ``n_gpus`` is the number of GPUs actually used.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--queues Q] [--mode scale]
+Output: rank 0 prints ONE compact JSON line on stdout, at most 4,096 bytes (``result_line``): the
+headline keys and the summary rows. The full result -- every row, round and breakdown -- goes
+to ``--detail-out`` (default ``gpurun_out/bench_detail.json``), which the line names.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--queues Q] [--mode scale] [--detail-out F]
 """
 from __future__ import annotations
 
