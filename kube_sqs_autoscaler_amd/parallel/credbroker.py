@@ -26,6 +26,7 @@ from __future__ import annotations
 import ctypes
 import mmap
 import threading
+import time
 from datetime import datetime, timezone
 from typing import Callable, Dict, Iterable, Mapping, Optional
 
@@ -87,6 +88,7 @@ class CredentialBroker:
         for a in self.addrs.values():
             nat.init_credential_slot(a)
         self._stop = threading.Event()
+        self._closed = False  # the slots unmapped (close())
         self._threads: Dict[str, threading.Thread] = {}
         self._lock = threading.Lock()  # the counters below (one serving thread per region)
         self._last_fetch: Dict[str, int] = {}
@@ -194,11 +196,10 @@ class CredentialBroker:
     def stop(self, timeout: float = 1.0) -> bool:
         """Stops the serving threads; False when one is still inside a fetch after ``timeout``
         (a hung credential endpoint: the threads are daemons and end with the process)."""
-        import time
-
         self._stop.set()
-        for addr in self.addrs.values():  # wake the threads sleeping between looks
-            native().credential_slot_poke(addr)
+        if self._threads and not self._closed:  # wake the threads sleeping between looks
+            for addr in self.addrs.values():
+                native().credential_slot_poke(addr)
         deadline = time.monotonic() + timeout
         for t in self._threads.values():
             t.join(timeout=max(0.0, deadline - time.monotonic()))
@@ -209,7 +210,8 @@ class CredentialBroker:
 
     def close(self) -> None:
         # idle serving threads end at once; one inside a fetch is not waited for
-        if not self.stop(timeout=0.1):
-            return  # a thread may still publish into the slots: leave them mapped
+        if self._closed or not self.stop(timeout=0.1):
+            return  # (a thread may still publish into the slots: leave them mapped)
+        self._closed = True
         del self._buf
         self._mm.close()

@@ -319,3 +319,19 @@ def test_two_region_fleet_decides_while_one_region_hangs(nat, tmp_path):
         broker.close()
         sqs.stop()
         kube.stop()
+
+
+def test_broker_close_and_stop_are_idempotent(nat):
+    """close() unmaps the slots once; a later stop() or close() (a second signal, a finally
+    after an exception) must not touch them."""
+    from kube_sqs_autoscaler_amd.parallel.credbroker import CredentialBroker
+
+    class Chain(nat.CredentialsProvider):
+        def retrieve(self):
+            return nat.Credentials(AKID, SECRET, "t", 0, "Test")
+
+    broker = CredentialBroker(["us-east-1", "eu-west-1"], providers={"us-east-1": Chain(), "eu-west-1": Chain()})
+    broker.start()
+    broker.close()
+    assert broker.stop() is True
+    broker.close()
