@@ -159,9 +159,10 @@ def test_every_profile_is_cited():
 
 
 def test_cited_profiles_exist():
-    """Every ``profiles/<entry>`` the current documents cite is in the tree."""
+    """Every ``profiles/<entry>`` the current documents cite is in the tree (``<rev>:profiles/...``
+    names a file in the git history instead)."""
     text = _current_text()
-    bad = sorted({m.group(1) for m in re.finditer(r"profiles/([A-Za-z0-9_.-]+/?(?:[A-Za-z0-9_.-]+)?)", text)
+    bad = sorted({m.group(1) for m in re.finditer(r"(?<![:\w])profiles/([A-Za-z0-9_.-]+/?(?:[A-Za-z0-9_.-]+)?)", text)
                   if not os.path.exists(os.path.join(ROOT, "profiles", m.group(1).rstrip("/")))})
     assert not bad, bad
 
