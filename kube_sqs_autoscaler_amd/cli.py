@@ -92,8 +92,8 @@ def main(argv: Optional[List[str]] = None, environ: Optional[Mapping[str, str]] 
     if cfg.trace_file:
         trace_fd = os.open(cfg.trace_file, os.O_WRONLY | os.O_CREAT | os.O_APPEND | os.O_CLOEXEC, 0o644)
 
-    # One AWS credential source per region for the process's queues: a broker thread runs the
-    # chain ahead of expiry and publishes each set into shared memory, where every queue reads it
+    # One AWS credential source per region for the process's queues: a broker thread per region
+    # runs the chain ahead of expiry and publishes each set into shared memory, where every queue reads it
     # (parallel/credbroker.py) -- worker threads here, or worker processes, which inherit the
     # mapping. No queue's poll or warm-up runs a fetch, one region's hung endpoint never delays
     # another's (a thread per region), a refresh that fails keeps the set while it still signs,

@@ -120,7 +120,7 @@ class FleetCollector:
                  credential_stale_signs: Optional[Callable[[], Dict[str, int]]] = None) -> None:
         """``credential_fetches``: the process's AWS credential fetches so far, per region (the
         thread fleet's shared providers, or the process fleet's broker). ``credential_stale_signs``:
-        per region, the signatures made with a set kept after its refresh failed (the broker)."""
+        per region, the SQS requests signed with a set kept after its refresh failed (the broker)."""
         self.fleet = fleet
         self.health = health
         self.credential_fetches = credential_fetches
@@ -181,8 +181,8 @@ class FleetCollector:
             out.append(creds)
         if self.credential_stale_signs is not None:
             stale = _Family("ksa_aws_credential_stale_signs_total", "counter",
-                            "Signatures made with an AWS credential set inside its 5-minute refresh window because "
-                            "its refresh failed (the set still valid for more than a minute)")
+                            "SQS requests signed with an AWS credential set inside its 5-minute refresh window because "
+                            "its refresh failed (the set valid for more than a minute yet)")
             for region, n in sorted(self.credential_stale_signs().items()):
                 stale.add("", [("region", region)], n)
             out.append(stale)
