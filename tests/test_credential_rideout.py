@@ -9,8 +9,10 @@
 * Each region has its own serving thread: one region's hung endpoint does not delay another's
   fetch (/root/reference/sqs/sqs.go:35-43: the client per queue's region).
 """
+import json
 import threading
 import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 import pytest
 import yaml
@@ -335,3 +337,85 @@ def test_broker_close_and_stop_are_idempotent(nat):
     broker.close()
     assert broker.stop() is True
     broker.close()
+
+
+class _EcsThenDown(BaseHTTPRequestHandler):
+    """A container-credentials endpoint that hands out one set with 200 s left (inside every
+    queue's 5-minute window from the start) and then answers 500 (an agent restart)."""
+
+    fetches = 0
+    failed = 0
+    lock = threading.Lock()
+
+    def do_GET(self):  # noqa: N802
+        from datetime import datetime, timedelta, timezone
+
+        with _EcsThenDown.lock:
+            _EcsThenDown.fetches += 1
+            first = _EcsThenDown.fetches == 1
+            if not first:
+                _EcsThenDown.failed += 1
+        if first:
+            body = json.dumps({"AccessKeyId": AKID, "SecretAccessKey": SECRET, "Token": "only-set",
+                               "Expiration": (datetime.now(timezone.utc) + timedelta(seconds=200))
+                               .strftime("%Y-%m-%dT%H:%M:%SZ")}).encode()
+            self.send_response(200)
+        else:
+            body = b'{"code":"InternalError","message":"agent restarting"}'
+            self.send_response(500)
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def log_message(self, *a):
+        pass
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("processes", [False, True])
+def test_cli_rides_out_a_credential_outage(nat, tmp_path, processes, capfd):
+    """The CLI (threads, or --worker-processes sharing the slot across processes) with its only
+    credential set inside the window and the endpoint down: every poll reads the depth and the
+    Deployments scale to their max; the kept set signs every request and the log carries one
+    warning."""
+    from kube_sqs_autoscaler_amd.cli import main
+
+    _EcsThenDown.fetches = _EcsThenDown.failed = 0
+    ecs = ThreadingHTTPServer(("127.0.0.1", 0), _EcsThenDown)
+    threading.Thread(target=ecs.serve_forever, daemon=True).start()
+    sqs = nat.FakeSqsServer()
+    sqs.require_signature(AKID, SECRET, "us-east-1")
+    sqs.start()
+    kube = nat.FakeKubeServer()
+    kube.require_token(TOKEN)
+    kube.start()
+    try:
+        kc = tmp_path / "kubeconfig"
+        kc.write_text(yaml.safe_dump({
+            "current-context": "t", "clusters": [{"name": "c", "cluster": {"server": kube.url}}],
+            "users": [{"name": "u", "user": {"token": TOKEN}}],
+            "contexts": [{"name": "t", "context": {"cluster": "c", "user": "u"}}]}))
+        env = {"HOME": str(tmp_path), "KUBE_CONFIG_PATH": str(kc), "AWS_EC2_METADATA_DISABLED": "true",
+               "AWS_CONTAINER_CREDENTIALS_FULL_URI": f"http://127.0.0.1:{ecs.server_address[1]}/creds"}
+        specs = []
+        for i in range(3):
+            url = f"{sqs.url}/123/q{i}"
+            sqs.set_attributes(url, {"ApproximateNumberOfMessages": "500"})
+            kube.add_deployment("gpu", f"w{i}", 4)
+            specs += ["--queue", f"url={url},deployment=w{i},namespace=gpu,attribute-names=ApproximateNumberOfMessages"]
+        extra = ["--worker-processes"] if processes else []
+        rc = main(["--aws-region=us-east-1", f"--sqs-endpoint={sqs.url}", "--poll-period=100ms", *extra,
+                   "--scale-up-cool-down=0s", "--scale-down-cool-down=0s", "--max-pods=8", "--log-level=warning",
+                   *specs], environ=env, max_iterations=6)
+        err = capfd.readouterr().err
+        assert rc == 0, err[-2000:]
+        assert [kube.replicas("gpu", f"w{i}") for i in range(3)] == [8, 8, 8]
+        assert sqs.requests() == 18 and sqs.signature_failures() == 0  # every poll read the depth
+        assert "Failed to get SQS messages" not in err
+        assert err.count("keep signing with the current set") == 1
+        assert "AWS credential refresh for us-east-1 failed: NoCredentialProviders" in err
+        assert _EcsThenDown.failed >= 1
+    finally:
+        ecs.shutdown()
+        sqs.stop()
+        kube.stop()
