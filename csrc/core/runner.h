@@ -220,7 +220,7 @@ std::string read_shared_error(const SharedWorkerState* s);
 // warm-up run, any restart of a Supervisor -- queue i's new thread inherits the arena in which
 // queue j's old thread allocated j's lazily-built buffers, and i's per-poll temporaries land on
 // the cache lines of buffers j's thread writes every poll. Measured on the 8-queue thread fleet
-// (profiles/README.md, r02l): the same instructions per poll, +70 % user cycles and ~80 more
+// (docs/HISTORY.md, r02l): the same instructions per poll, +70 % user cycles and ~80 more
 // cache misses per poll, +30 % p50; with the threads kept, the fleet polls like one queue.
 class HomeThread {
  public:

@@ -35,7 +35,7 @@ def _full():
 
 
 def test_round5_result_fits_and_parses_from_the_tail():
-    """Round 5's own full result (24.6 KB, profiles/r05ag) becomes a line of at most 4,096 bytes
+    """Round 5's own full result (24.6 KB; profiles/r05ag/bench.json at ee40be9) becomes a line of at most 4,096 bytes
     that parses from the tail with every headline key and every summary row."""
     out = _full()
     assert len(json.dumps(out)) > 20_000
